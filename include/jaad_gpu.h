@@ -1,0 +1,203 @@
+/*
+ * jaad_gpu.h -- C-ABI drop-in boundary for the DSP half of JAAD's decoder.
+ *
+ * The reference decoder (pucgenie/JAADec, pure Java) runs, per frame,
+ *     Decoder.decode0                       A/Decoder.java:103-121
+ *       syntacticElements.decode(in)        parse + Huffman        (stays on the host)
+ *       syntacticElements.process()         DSP                    (REPLACED by this library)
+ *       buffer.accept(channels, len, rate)  SampleBuffer PCM pack  (REPLACED by this library)
+ * (A/ = aac/src/main/java/net/sourceforge/jaad/aac/).  The host parser emits, instead of
+ * dequantised floats, the quantised spectrum plus the side information listed below, for
+ * MANY frames of MANY streams at once; one call turns the batch into interleaved int16 PCM
+ * byte-identical in layout to SampleBuffer.accept (S/SampleBuffer.java:168-209).
+ *
+ * Plain C types only: the JNI glue passes direct-ByteBuffer addresses.
+ * Every entry point returns an int status (0 = ok, <0 = jaad_status); nothing throws.
+ */
+#ifndef JAAD_GPU_H
+#define JAAD_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define JAAD_ABI_VERSION 1u
+
+/* ---- status codes (JNI maps every nonzero code to AACException, A/AACException.java) ---- */
+typedef enum jaad_status {
+    JAAD_OK = 0,
+    JAAD_ERR_INVALID_ARG = -1,   /* NULL/short buffer, bad sizes                              */
+    JAAD_ERR_NO_DEVICE = -2,     /* no usable gfx950 device / HIP runtime                    */
+    JAAD_ERR_HIP = -3,           /* a HIP runtime call failed                                 */
+    JAAD_ERR_UNSUPPORTED = -4,   /* profile/config not decodable (A/Decoder.java:115-116)     */
+    JAAD_ERR_BITSTREAM = -5,     /* side info out of range, e.g. max_sfb > swb count          */
+    JAAD_ERR_NOMEM = -6,
+    JAAD_ERR_ABI = -7            /* jaad_stream_cfg.abi_version mismatch                      */
+} jaad_status;
+
+/* ---- ICSInfo.WindowSequence ordinals (A/syntax/ICSInfo.java:26-53) ---- */
+enum {
+    JAAD_ONLY_LONG_SEQUENCE = 0,
+    JAAD_LONG_START_SEQUENCE = 1,
+    JAAD_EIGHT_SHORT_SEQUENCE = 2,
+    JAAD_LONG_STOP_SEQUENCE = 3
+};
+
+/* ---- section codebooks with DSP meaning (A/huffman/HCB.java) ---- */
+enum {
+    JAAD_ZERO_HCB = 0,
+    JAAD_FIRST_PAIR_HCB = 5,
+    JAAD_ESCAPE_HCB = 11,
+    JAAD_NOISE_HCB = 13,
+    JAAD_INTENSITY_HCB2 = 14,
+    JAAD_INTENSITY_HCB = 15
+};
+
+/* ---- TNS handling ---- */
+enum {
+    JAAD_TNS_COMPAT = 0,  /* reference behaviour: TNS.process is a no-op (A/tools/TNS.java:63-68)  */
+    JAAD_TNS_SPEC = 1     /* ISO/IEC 14496-3 4.6.9 all-pole filtering (parity unpinned by the ref) */
+};
+
+/* ---- output format flags for jaad_decode_* ---- */
+enum {
+    JAAD_PCM_BIG_ENDIAN = 0u,     /* SampleBuffer default (S/SampleBuffer.java:28-30)            */
+    JAAD_PCM_LITTLE_ENDIAN = 1u,  /* SampleBuffer.setBigEndian(false)                             */
+    JAAD_PCM_FLOAT32 = 2u         /* native-endian f32 samples BEFORE Math.round (tolerance checks) */
+};
+
+/*
+ * Stream configuration: what DecoderConfig.decode (A/DecoderConfig.java:175-254) derives from
+ * the AudioSpecificConfig.  One context serves any number of streams sharing one config.
+ */
+typedef struct jaad_stream_cfg {
+    uint32_t abi_version;     /* = JAAD_ABI_VERSION                                             */
+    uint8_t profile;          /* audio object type of the core: 2 = AAC LC (only one supported)  */
+    uint8_t sf_index;         /* core SampleFrequency index 0..11 (A/SampleFrequency.java:15-26) */
+    uint8_t channel_config;   /* 1 = one SCE (mono), 2 = one CPE (stereo)                        */
+    uint8_t tns_mode;         /* JAAD_TNS_COMPAT | JAAD_TNS_SPEC                                  */
+    uint8_t sbr;              /* 0; explicit SBR (AOT 5/29) arrives in a later ABI revision       */
+    uint8_t ps;               /* 0; see above                                                     */
+    uint8_t reserved[2];
+} jaad_stream_cfg;
+
+/*
+ * Per channel-frame side information (16 bytes), one per ICStream per frame.
+ * Filled by the host from ICSInfo.decode (A/syntax/ICSInfo.java:86-119) and ICStream.decode.
+ */
+typedef struct jaad_ics_info {
+    uint8_t window_sequence;   /* JAAD_*_SEQUENCE                                                 */
+    uint8_t window_shape;      /* ICSInfo.windowShape[CURRENT]: 0 sine, 1 KBD                      */
+    uint8_t window_shape_prev; /* ICSInfo.windowShape[PREVIOUS]                                    */
+    uint8_t max_sfb;           /* <= swb count of the window type                                  */
+    uint8_t grouping;          /* EIGHT_SHORT only: bit i (i=0..6) set <=> window i+1 is in the same
+                                  group as window i, i.e. the i-th scale_factor_grouping bit read by
+                                  A/syntax/ICSInfo.java:97-104. 0 for long windows.               */
+    uint8_t flags;             /* JAAD_ICS_* below                                                 */
+    uint8_t reserved[2];
+    uint32_t pns_state;        /* value of the static ICStream.randomState (A/syntax/ICStream.java:26)
+                                  when this ICStream's decodeSpectralData started                 */
+    uint32_t reserved2;
+} jaad_ics_info;
+
+enum {
+    JAAD_ICS_HAS_PNS = 1u << 0,     /* some band uses NOISE_HCB                                  */
+    JAAD_ICS_HAS_IS = 1u << 1,      /* some band uses INTENSITY_HCB(2) (right channel of a CPE)  */
+    JAAD_ICS_TNS = 1u << 2,         /* tns_data_present (coefficients in jaad_batch.tns)         */
+    JAAD_ICS_MS_PRESENT = 1u << 3,  /* left channel of a CPE: common_window && ms_mask != ALL_0
+                                       (A/syntax/CPE.java:149-153, isMSMaskPresent)             */
+    JAAD_ICS_COMMON_WINDOW = 1u << 4
+};
+
+/*
+ * TNS side info per channel-frame (TNS.decode, A/tools/TNS.java:35-61).  Up to 8 filters in
+ * total (long: <=3 in window 0; short: <=1 per window).  coef[] holds the 4-bit indices read
+ * from the bitstream; the value is TNS_TABLES[2*compress+res][idx] (A/tools/TNSTables.java).
+ */
+typedef struct jaad_tns_filter {
+    uint8_t window;    /* 0..7                                   */
+    uint8_t length;    /* in scale factor bands                  */
+    uint8_t order;     /* 0..20 (>20 rejected as the ref does)    */
+    uint8_t flags;     /* bit0 direction, bit1 coef_res, bit2 coef_compress */
+    uint8_t coef[20];
+} jaad_tns_filter;
+
+typedef struct jaad_tns {
+    uint8_t n_filters; /* 0..8, filters ordered by (window, filt) as parsed */
+    uint8_t reserved[3];
+    jaad_tns_filter filt[8];
+} jaad_tns;
+
+/*
+ * A batch: n_frames frames (raw_data_blocks) of one channel configuration.  Frames are grouped
+ * in runs: run r holds consecutive-in-time frames [frame_begin[r], frame_begin[r+1]) of the
+ * stream whose persistent DSP state (IMDCT overlap, ...) lives in context slot stream_slot[r].
+ * A run continues its slot's stream exactly where the previous call left it.
+ *
+ * ch-frame index = frame * channels + ch  (channels = 1 for an SCE config, 2 for a CPE config).
+ * Arrays marked [dev] live in device memory for jaad_decode_batch_device and in host memory
+ * for jaad_decode_batch; the run arrays are always host memory.
+ */
+typedef struct jaad_batch {
+    uint32_t n_frames;
+    uint32_t n_runs;
+    const uint32_t* stream_slot;  /* [n_runs]   host                                             */
+    const uint32_t* frame_begin;  /* [n_runs+1] host, frame_begin[0] = 0, frame_begin[n_runs] = n_frames */
+    const int16_t* q;             /* [dev] [ch-frame][1024] quantised coefficients, ICStream iqData order
+                                     (window-major for EIGHT_SHORT, A/syntax/ICStream.java:229-274);
+                                     bins >= swb_offset[max_sfb] of each window must be 0          */
+    const uint8_t* sf;            /* [dev] [ch-frame][128]: per (group, sfb) band, idx = g*max_sfb+sfb:
+                                     scalefactor-table index minus 100, i.e. the gain is
+                                     SCALEFACTOR_TABLE[sf+100] (negated for NOISE_HCB);
+                                     spectral: global-gain sum; noise: clip(off1,-100,155)+100;
+                                     intensity: 100-clip(off2,-155,100) (A/syntax/ICStream.java:172-220) */
+    const uint8_t* cb;            /* [dev] [ch-frame][128] section codebook per band (sfbCB)       */
+    const jaad_ics_info* ics;     /* [dev] [ch-frame]                                              */
+    const uint64_t* ms_used;      /* [dev] [frame][2] bit idx = g*max_sfb+sfb (CPE only, else NULL) */
+    const jaad_tns* tns;          /* [dev] [ch-frame] or NULL when no ch-frame sets JAAD_ICS_TNS    */
+} jaad_batch;
+
+typedef struct jaad_ctx jaad_ctx;
+
+/* DecoderConfig.getSampleLength (A/DecoderConfig.java:83-86) and getChannelCount (:108-115).
+ * Note: a mono (SCE) stream is emitted as 2 identical channels, as SyntacticElements.process
+ * does (A/syntax/SyntacticElements.java:243-245).                                          */
+int jaad_cfg_sample_length(const jaad_stream_cfg* cfg);
+int jaad_cfg_channel_count(const jaad_stream_cfg* cfg);
+/* bytes of PCM one frame produces for the given output flags */
+size_t jaad_frame_pcm_bytes(const jaad_stream_cfg* cfg, uint32_t flags);
+
+/* Create a context bound to HIP device `device` with `n_slots` independent stream states
+ * (each as freshly created by Decoder.create: overlap zero, window shapes sine).            */
+int jaad_ctx_create(const jaad_stream_cfg* cfg, uint32_t n_slots, int device, jaad_ctx** out);
+void jaad_ctx_destroy(jaad_ctx* ctx);
+
+/* Synchronous host-buffer entry: copies the batch to the device, runs the DSP, copies
+ * n_frames * jaad_frame_pcm_bytes(flags) bytes of PCM back to pcm_out (frame-major).       */
+int jaad_decode_batch(jaad_ctx* ctx, const jaad_batch* batch, void* pcm_out, size_t pcm_bytes,
+                      uint32_t flags);
+
+/* Device-resident entry: all [dev] arrays and pcm_dev are device pointers; work is queued on
+ * `hip_stream` (a hipStream_t, NULL = the context's stream) and the call returns without
+ * waiting.  Calls on one context must not overlap.                                         */
+int jaad_decode_batch_device(jaad_ctx* ctx, const jaad_batch* batch, void* pcm_dev, size_t pcm_bytes,
+                             uint32_t flags, void* hip_stream);
+int jaad_wait(jaad_ctx* ctx);
+
+/* Per-slot persistent DSP state (seek/resume, A/syntax/ICStream.java:47,56 overlap, ...).   */
+size_t jaad_state_bytes(const jaad_ctx* ctx);
+int jaad_state_export(jaad_ctx* ctx, uint32_t slot, void* buf, size_t bytes);
+int jaad_state_import(jaad_ctx* ctx, uint32_t slot, const void* buf, size_t bytes);
+int jaad_state_reset(jaad_ctx* ctx, uint32_t slot);
+
+const char* jaad_strerror(int status);
+/* last HIP error string recorded by the context (diagnostics) */
+const char* jaad_last_error(const jaad_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* JAAD_GPU_H */

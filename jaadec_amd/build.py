@@ -1,0 +1,86 @@
+"""Build the native pieces in-tree.
+
+* ``jaadec_amd/libjaadgpu.so`` -- the product: C-ABI (include/jaad_gpu.h) + gfx950 HIP kernels.
+* ``jaadec_amd/libjaadsynth.so`` -- host-side synthetic batch generator (bench/test inputs).
+* ``oracle/liboracle.so`` -- TEST INFRASTRUCTURE: the C restatement of the reference DSP.
+
+Everything is compiled with ``-ffp-contract=off``: the reference (Java >= 17) evaluates binary32
+arithmetic strictly, without fused multiply-add, and both the oracle and the HIP kernels follow
+its evaluation order so their results are bit-identical.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+PKG = ROOT / "jaadec_amd"
+CSRC = PKG / "csrc"
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = "gfx950"
+
+LIB = PKG / "libjaadgpu.so"
+SYNTH_LIB = PKG / "libjaadsynth.so"
+ORACLE_LIB = ROOT / "oracle" / "liboracle.so"
+
+
+def _run(cmd: list[str]) -> None:
+    print("+", " ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+
+
+def _stale(out: Path, deps: list[Path]) -> bool:
+    if not out.exists():
+        return True
+    t = out.stat().st_mtime
+    return any(d.stat().st_mtime > t for d in deps)
+
+
+def _deps(*globs: str) -> list[Path]:
+    out: list[Path] = []
+    for g in globs:
+        out += sorted(ROOT.glob(g))
+    return out
+
+
+def build_gpu(force: bool = False) -> Path:
+    srcs = [CSRC / "jaad_lc.hip", CSRC / "jaad_capi.cpp"]
+    deps = srcs + _deps("jaadec_amd/csrc/*.h", "jaadec_amd/csrc/tables/*.inc", "include/*.h")
+    if force or _stale(LIB, deps):
+        tmp = LIB.with_suffix(".so.tmp")
+        _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+              "-ffp-contract=off", "-fno-gpu-rdc", "-Wall", "-Wno-unused-function",
+              "-I", str(ROOT / "include"), "-o", str(tmp)] + [str(s) for s in srcs])
+        tmp.replace(LIB)
+    return LIB
+
+
+def build_synth(force: bool = False) -> Path:
+    srcs = [CSRC / "jaad_synth.cpp"]
+    deps = srcs + _deps("include/*.h", "jaadec_amd/csrc/tables/*.inc")
+    if force or _stale(SYNTH_LIB, deps):
+        _run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-Wall",
+              "-I", str(ROOT / "include"), "-o", str(SYNTH_LIB)] + [str(s) for s in srcs])
+    return SYNTH_LIB
+
+
+def build_oracle(force: bool = False) -> Path:
+    srcs = [ROOT / "oracle" / "jaad_oracle.c"]
+    deps = srcs + _deps("oracle/*.h", "include/*.h", "jaadec_amd/csrc/tables/*.inc")
+    if force or _stale(ORACLE_LIB, deps):
+        _run(["gcc", "-O2", "-std=c11", "-fPIC", "-shared", "-ffp-contract=off", "-fno-fast-math",
+              "-Wall", "-o", str(ORACLE_LIB)] + [str(s) for s in srcs] + ["-lm", "-lpthread"])
+    return ORACLE_LIB
+
+
+def build_all(force: bool = False) -> None:
+    build_oracle(force)
+    build_synth(force)
+    build_gpu(force)
+
+
+if __name__ == "__main__":
+    build_all(force="--force" in sys.argv)

@@ -1,0 +1,453 @@
+// C-ABI implementation (include/jaad_gpu.h): contexts, per-stream state, work planning and the
+// host/device batch entry points.  Host code only; kernels live in jaad_lc.hip.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "jaad_lc.h"
+#include "tables/jaad_tables.inc"
+
+using namespace jaad;
+
+namespace {
+
+// SampleFrequency maxTNS_SFB {long, short} (A/SampleFrequency.java:15-26)
+const unsigned char kMaxTnsSfb[12][2] = {{31, 9}, {31, 9}, {34, 10}, {40, 14}, {42, 14}, {51, 14},
+                                         {46, 14}, {46, 14}, {42, 14}, {42, 14}, {42, 14}, {39, 14}};
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t n)
+    {
+        if (n <= cap) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        hipError_t e = hipMalloc(&p, n);
+        if (e == hipSuccess) cap = n;
+        return e;
+    }
+    void release()
+    {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+}  // namespace
+
+struct jaad_ctx {
+    jaad_stream_cfg cfg{};
+    int device = 0;
+    int nch = 2;
+    uint32_t n_slots = 0;
+    hipStream_t stream = nullptr;
+    float* d_state[2] = {nullptr, nullptr};  // [slot][2][1024], double-buffered (see plan())
+    int parity = 0;                          // d_state[parity] holds the current state
+    LdsTables* d_tables = nullptr;
+    float* d_iq = nullptr;
+    DevBuf d_chunks, d_batch, d_pcm;
+    std::vector<ChunkDesc> chunks;
+    std::vector<uint32_t> plan_slots, plan_begin;  // plan cache key
+    std::vector<uint8_t> slot_used;
+    bool plan_valid = false;
+    int n_cu = 256;
+    float* dbg = nullptr;
+    std::string err;
+};
+
+namespace jaad {
+
+void build_lds_tables(int sf_index, LdsTables* t)
+{
+    std::memset(t, 0, sizeof(*t));
+    std::memcpy(t->win_long[0], JAAD_SINE_1024, sizeof(t->win_long[0]));
+    std::memcpy(t->win_long[1], JAAD_KBD_1024, sizeof(t->win_long[1]));
+    std::memcpy(t->win_short[0], JAAD_SINE_128, sizeof(t->win_short[0]));
+    std::memcpy(t->win_short[1], JAAD_KBD_128, sizeof(t->win_short[1]));
+    std::memcpy(t->mdct_l, JAAD_MDCT_TABLE_2048, sizeof(t->mdct_l));
+    std::memcpy(t->mdct_s, JAAD_MDCT_TABLE_128, sizeof(t->mdct_s));
+    for (int k = 0; k < 256; k++) {
+        t->roots_l[k][0] = JAAD_FFT_TABLE_512[k][0];
+        t->roots_l[k][1] = JAAD_FFT_TABLE_512[k][1];
+    }
+    for (int k = 0; k < 32; k++) {
+        t->roots_s[k][0] = JAAD_FFT_TABLE_64[k][0];
+        t->roots_s[k][1] = JAAD_FFT_TABLE_64[k][1];
+    }
+    for (int i = 0; i < 256; i++) {
+        t->sf_gain[i] = JAAD_SCALEFACTOR_TABLE[100 + i];
+        if (i < 128) t->iq_head[i] = JAAD_IQ_TABLE[i];
+    }
+    std::memcpy(t->tns_coef[0], JAAD_TNS_COEF_0_3, sizeof(JAAD_TNS_COEF_0_3));
+    std::memcpy(t->tns_coef[1], JAAD_TNS_COEF_0_4, sizeof(JAAD_TNS_COEF_0_4));
+    std::memcpy(t->tns_coef[2], JAAD_TNS_COEF_1_3, sizeof(JAAD_TNS_COEF_1_3));
+    std::memcpy(t->tns_coef[3], JAAD_TNS_COEF_1_4, sizeof(JAAD_TNS_COEF_1_4));
+    const short* L = JAAD_SWB_OFFSET_LONG_WINDOW[sf_index];
+    const short* S = JAAD_SWB_OFFSET_SHORT_WINDOW[sf_index];
+    t->nswb_l = JAAD_SWB_LONG_WINDOW_COUNT[sf_index];
+    t->nswb_s = JAAD_SWB_SHORT_WINDOW_COUNT[sf_index];
+    for (int i = 0; i <= t->nswb_l; i++) t->swb_l[i] = L[i];
+    for (int i = 0; i <= t->nswb_s; i++) t->swb_s[i] = S[i];
+    std::memset(t->quad2band_l, 255, sizeof(t->quad2band_l));
+    std::memset(t->quad2band_s, 255, sizeof(t->quad2band_s));
+    for (int b = 0; b < t->nswb_l; b++)
+        for (int p = L[b]; p < L[b + 1]; p += 4) t->quad2band_l[p >> 2] = (uint8_t)b;
+    for (int b = 0; b < t->nswb_s; b++)
+        for (int p = S[b]; p < S[b + 1]; p += 4) t->quad2band_s[p >> 2] = (uint8_t)b;
+    t->tns_max_l = kMaxTnsSfb[sf_index][0];
+    t->tns_max_s = kMaxTnsSfb[sf_index][1];
+}
+
+}  // namespace jaad
+
+namespace {
+
+int fail(jaad_ctx* c, hipError_t e, const char* what)
+{
+    if (c) {
+        c->err = std::string(what) + ": " + hipGetErrorString(e);
+    }
+    return JAAD_ERR_HIP;
+}
+
+#define HIPCHK(call)                                 \
+    do {                                             \
+        hipError_t e_ = (call);                      \
+        if (e_ != hipSuccess) return fail(ctx, e_, #call); \
+    } while (0)
+
+int validate_cfg(const jaad_stream_cfg* cfg)
+{
+    if (!cfg) return JAAD_ERR_INVALID_ARG;
+    if (cfg->abi_version != JAAD_ABI_VERSION) return JAAD_ERR_ABI;
+    if (cfg->profile != 2) return JAAD_ERR_UNSUPPORTED;  // Profile.AAC_LC (A/Profile.java)
+    if (cfg->sf_index > 11) return JAAD_ERR_UNSUPPORTED;
+    if (cfg->channel_config != 1 && cfg->channel_config != 2) return JAAD_ERR_UNSUPPORTED;
+    if (cfg->tns_mode > JAAD_TNS_SPEC) return JAAD_ERR_INVALID_ARG;
+    if (cfg->sbr || cfg->ps) return JAAD_ERR_UNSUPPORTED;
+    return JAAD_OK;
+}
+
+// (Re)build the chunk table for the batch's runs; cached when the run layout repeats.
+int plan(jaad_ctx* ctx, const jaad_batch* b)
+{
+    if (!b->stream_slot || !b->frame_begin) return JAAD_ERR_INVALID_ARG;
+    if (b->frame_begin[0] != 0 || b->frame_begin[b->n_runs] != b->n_frames) return JAAD_ERR_INVALID_ARG;
+    bool same = ctx->plan_valid && ctx->plan_slots.size() == b->n_runs &&
+                std::memcmp(ctx->plan_slots.data(), b->stream_slot, b->n_runs * sizeof(uint32_t)) == 0 &&
+                std::memcmp(ctx->plan_begin.data(), b->frame_begin, (b->n_runs + 1) * sizeof(uint32_t)) == 0;
+    if (same) return JAAD_OK;
+    ctx->chunks.clear();
+    std::fill(ctx->slot_used.begin(), ctx->slot_used.end(), 0);
+    for (uint32_t r = 0; r < b->n_runs; r++) {
+        uint32_t f0 = b->frame_begin[r], f1 = b->frame_begin[r + 1];
+        uint32_t slot = b->stream_slot[r];
+        if (f1 < f0 || slot >= ctx->n_slots) return JAAD_ERR_INVALID_ARG;
+        if (ctx->slot_used[slot]) return JAAD_ERR_INVALID_ARG;  // one run per stream per call
+        ctx->slot_used[slot] = 1;
+        if (f1 == f0) {  // empty run: carry the state over unchanged
+            ChunkDesc cd{f0, kChunkLoadState | kChunkStoreState, slot, 0};
+            ctx->chunks.push_back(cd);
+            continue;
+        }
+        for (uint32_t f = f0; f < f1; f += kChunkFrames) {
+            uint32_t n = f1 - f < (uint32_t)kChunkFrames ? f1 - f : (uint32_t)kChunkFrames;
+            uint32_t info = n;
+            info |= (f == f0) ? kChunkLoadState : kChunkPrefix;
+            if (f + n == f1) info |= kChunkStoreState;
+            ctx->chunks.push_back(ChunkDesc{f, info, slot, 0});
+        }
+    }
+    HIPCHK(ctx->d_chunks.ensure(ctx->chunks.size() * sizeof(ChunkDesc) + 16));
+    HIPCHK(hipMemcpy(ctx->d_chunks.p, ctx->chunks.data(), ctx->chunks.size() * sizeof(ChunkDesc), hipMemcpyHostToDevice));
+    ctx->plan_slots.assign(b->stream_slot, b->stream_slot + b->n_runs);
+    ctx->plan_begin.assign(b->frame_begin, b->frame_begin + b->n_runs + 1);
+    ctx->plan_valid = true;
+    return JAAD_OK;
+}
+
+size_t pcm_bytes_per_frame(uint32_t flags) { return (size_t)1024 * 2 * ((flags & JAAD_PCM_FLOAT32) ? 4 : 2); }
+
+int launch(jaad_ctx* ctx, const jaad_batch* db, void* pcm, uint32_t flags, hipStream_t stream)
+{
+    int rc = plan(ctx, db);
+    if (rc) return rc;
+    KernelArgs a{};
+    a.q = db->q;
+    a.sf = db->sf;
+    a.cb = db->cb;
+    a.ics = db->ics;
+    a.ms_used = db->ms_used;
+    a.tns = db->tns;
+    a.iq_table = ctx->d_iq;
+    a.tables = ctx->d_tables;
+    a.chunks = static_cast<const ChunkDesc*>(ctx->d_chunks.p);
+    a.state_in = ctx->d_state[ctx->parity];
+    a.state_out = ctx->d_state[ctx->parity ^ 1];
+    a.pcm = pcm;
+    a.n_chunks = (uint32_t)ctx->chunks.size();
+    a.nch = (uint32_t)ctx->nch;
+    a.out_mode = flags;
+    a.tns_mode = ctx->cfg.tns_mode;
+    a.dbg = ctx->dbg;
+    if (a.n_chunks == 0) return JAAD_OK;
+    // slots this call does not touch keep their state: carry them into the other buffer
+    size_t slot_bytes = 2048 * sizeof(float);
+    for (uint32_t s = 0; s < ctx->n_slots;) {
+        if (ctx->slot_used[s]) {
+            s++;
+            continue;
+        }
+        uint32_t e = s;
+        while (e < ctx->n_slots && !ctx->slot_used[e]) e++;
+        HIPCHK(hipMemcpyAsync(a.state_out + (size_t)s * 2048, a.state_in + (size_t)s * 2048, (e - s) * slot_bytes,
+                              hipMemcpyDeviceToDevice, stream));
+        s = e;
+    }
+    const int per_wg = kWavesPerWG;
+    int grid = (int)((a.n_chunks + per_wg - 1) / per_wg);
+    const bool tns_spec = ctx->cfg.tns_mode == JAAD_TNS_SPEC && db->tns != nullptr;
+    HIPCHK(launch_lc(a, grid, stream, tns_spec));
+    ctx->parity ^= 1;
+    return JAAD_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int jaad_cfg_sample_length(const jaad_stream_cfg* cfg)
+{
+    (void)cfg;
+    return 1024;  // frameLengthFlag=0, no upsampling SBR (A/DecoderConfig.java:83-86)
+}
+
+int jaad_cfg_channel_count(const jaad_stream_cfg* cfg)
+{
+    (void)cfg;
+    return 2;  // mono is duplicated while sbrEnabled (A/DecoderConfig.java:108-115)
+}
+
+size_t jaad_frame_pcm_bytes(const jaad_stream_cfg* cfg, uint32_t flags)
+{
+    return (size_t)jaad_cfg_sample_length(cfg) * jaad_cfg_channel_count(cfg) * ((flags & JAAD_PCM_FLOAT32) ? 4 : 2);
+}
+
+const char* jaad_strerror(int status)
+{
+    switch (status) {
+    case JAAD_OK: return "ok";
+    case JAAD_ERR_INVALID_ARG: return "invalid argument";
+    case JAAD_ERR_NO_DEVICE: return "no usable gfx950 device";
+    case JAAD_ERR_HIP: return "HIP runtime error";
+    case JAAD_ERR_UNSUPPORTED: return "unsupported configuration";
+    case JAAD_ERR_BITSTREAM: return "bitstream side info out of range";
+    case JAAD_ERR_NOMEM: return "out of memory";
+    case JAAD_ERR_ABI: return "ABI version mismatch";
+    default: return "unknown status";
+    }
+}
+
+const char* jaad_last_error(const jaad_ctx* ctx) { return ctx ? ctx->err.c_str() : ""; }
+
+// internal (not in the public header): device buffer of 6144 floats receiving stage dumps
+int jaad__debug_attach(jaad_ctx* ctx, void* dev_buf)
+{
+    if (!ctx) return JAAD_ERR_INVALID_ARG;
+    ctx->dbg = static_cast<float*>(dev_buf);
+    return JAAD_OK;
+}
+
+int jaad_ctx_create(const jaad_stream_cfg* cfg, uint32_t n_slots, int device, jaad_ctx** out)
+{
+    if (!out) return JAAD_ERR_INVALID_ARG;
+    *out = nullptr;
+    int rc = validate_cfg(cfg);
+    if (rc) return rc;
+    if (n_slots == 0) return JAAD_ERR_INVALID_ARG;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device || device < 0) return JAAD_ERR_NO_DEVICE;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return JAAD_ERR_NO_DEVICE;
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return JAAD_ERR_NO_DEVICE;
+    jaad_ctx* ctx = new (std::nothrow) jaad_ctx();
+    if (!ctx) return JAAD_ERR_NOMEM;
+    ctx->cfg = *cfg;
+    ctx->device = device;
+    ctx->nch = cfg->channel_config == 2 ? 2 : 1;
+    ctx->n_slots = n_slots;
+    ctx->n_cu = prop.multiProcessorCount;
+    ctx->slot_used.assign(n_slots, 0);
+    auto bail = [&](hipError_t e, const char* what) {
+        std::fprintf(stderr, "jaad_ctx_create: %s: %s\n", what, hipGetErrorString(e));
+        jaad_ctx_destroy(ctx);
+        return JAAD_ERR_HIP;
+    };
+    hipError_t e;
+    if ((e = hipSetDevice(device)) != hipSuccess) return bail(e, "hipSetDevice");
+    if ((e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking)) != hipSuccess) return bail(e, "hipStreamCreate");
+    size_t sbytes = (size_t)n_slots * 2048 * sizeof(float);
+    for (int i = 0; i < 2; i++) {
+        if ((e = hipMalloc(&ctx->d_state[i], sbytes)) != hipSuccess) return bail(e, "hipMalloc state");
+        if ((e = hipMemset(ctx->d_state[i], 0, sbytes)) != hipSuccess) return bail(e, "hipMemset state");
+    }
+    LdsTables* h = new (std::nothrow) LdsTables;
+    if (!h) {
+        jaad_ctx_destroy(ctx);
+        return JAAD_ERR_NOMEM;
+    }
+    build_lds_tables(cfg->sf_index, h);
+    if ((e = hipMalloc(&ctx->d_tables, sizeof(LdsTables))) != hipSuccess) { delete h; return bail(e, "hipMalloc tables"); }
+    e = hipMemcpy(ctx->d_tables, h, sizeof(LdsTables), hipMemcpyHostToDevice);
+    delete h;
+    if (e != hipSuccess) return bail(e, "hipMemcpy tables");
+    if ((e = hipMalloc(&ctx->d_iq, sizeof(JAAD_IQ_TABLE))) != hipSuccess) return bail(e, "hipMalloc iq");
+    if ((e = hipMemcpy(ctx->d_iq, JAAD_IQ_TABLE, sizeof(JAAD_IQ_TABLE), hipMemcpyHostToDevice)) != hipSuccess)
+        return bail(e, "hipMemcpy iq");
+    *out = ctx;
+    return JAAD_OK;
+}
+
+void jaad_ctx_destroy(jaad_ctx* ctx)
+{
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    for (int i = 0; i < 2; i++)
+        if (ctx->d_state[i]) (void)hipFree(ctx->d_state[i]);
+    if (ctx->d_tables) (void)hipFree(ctx->d_tables);
+    if (ctx->d_iq) (void)hipFree(ctx->d_iq);
+    ctx->d_chunks.release();
+    ctx->d_batch.release();
+    ctx->d_pcm.release();
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+static int check_batch(const jaad_ctx* ctx, const jaad_batch* b, size_t pcm_bytes, uint32_t flags)
+{
+    if (!ctx || !b) return JAAD_ERR_INVALID_ARG;
+    if (b->n_frames && (!b->q || !b->sf || !b->cb || !b->ics)) return JAAD_ERR_INVALID_ARG;
+    if (ctx->nch == 2 && b->n_frames && !b->ms_used) return JAAD_ERR_INVALID_ARG;
+    if (pcm_bytes < pcm_bytes_per_frame(flags) * b->n_frames) return JAAD_ERR_INVALID_ARG;
+    if (flags & ~(uint32_t)(JAAD_PCM_LITTLE_ENDIAN | JAAD_PCM_FLOAT32)) return JAAD_ERR_INVALID_ARG;
+    return JAAD_OK;
+}
+
+// host-side range checks the Java parser would have raised as AACException
+static int validate_side_info(const jaad_ctx* ctx, const jaad_batch* b)
+{
+    const int nch = ctx->nch;
+    const int nl = JAAD_SWB_LONG_WINDOW_COUNT[ctx->cfg.sf_index], ns = JAAD_SWB_SHORT_WINDOW_COUNT[ctx->cfg.sf_index];
+    for (size_t i = 0; i < (size_t)b->n_frames * nch; i++) {
+        const jaad_ics_info& ic = b->ics[i];
+        if (ic.window_sequence > 3 || ic.window_shape > 1 || ic.window_shape_prev > 1) return JAAD_ERR_BITSTREAM;
+        int lim = ic.window_sequence == JAAD_EIGHT_SHORT_SEQUENCE ? ns : nl;
+        if (ic.max_sfb > lim) return JAAD_ERR_BITSTREAM;  // ICStream.java:137-138 / IndexOutOfBounds
+        const int16_t* q = b->q + i * 1024;
+        for (int k = 0; k < 1024; k++)
+            if (q[k] > 8190 || q[k] < -8190) return JAAD_ERR_BITSTREAM;  // IQ_TABLE has 8191 entries
+        if (b->tns && (ic.flags & JAAD_ICS_TNS)) {
+            const jaad_tns& t = b->tns[i];
+            if (t.n_filters > 8) return JAAD_ERR_BITSTREAM;
+            for (int f = 0; f < t.n_filters; f++)
+                if (t.filt[f].order > 20 || t.filt[f].window > 7) return JAAD_ERR_BITSTREAM;  // TNS.java:56-57
+        }
+    }
+    return JAAD_OK;
+}
+
+int jaad_decode_batch(jaad_ctx* ctx, const jaad_batch* b, void* pcm_out, size_t pcm_bytes, uint32_t flags)
+{
+    int rc = check_batch(ctx, b, pcm_bytes, flags);
+    if (rc) return rc;
+    if (!pcm_out && b->n_frames) return JAAD_ERR_INVALID_ARG;
+    if ((rc = validate_side_info(ctx, b))) return rc;
+    HIPCHK(hipSetDevice(ctx->device));
+    const size_t nf = b->n_frames, ncf = nf * ctx->nch;
+    // one staging allocation, 256-B aligned sub-buffers
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    size_t o_q = 0, o_sf = al(o_q + ncf * 2048), o_cb = al(o_sf + ncf * 128), o_ics = al(o_cb + ncf * 128);
+    size_t o_ms = al(o_ics + ncf * sizeof(jaad_ics_info)), o_tns = al(o_ms + nf * 16);
+    size_t total = al(o_tns + (b->tns ? ncf * sizeof(jaad_tns) : 0));
+    HIPCHK(ctx->d_batch.ensure(total + 256));
+    size_t pbytes = pcm_bytes_per_frame(flags) * nf;
+    HIPCHK(ctx->d_pcm.ensure(pbytes + 256));
+    char* base = static_cast<char*>(ctx->d_batch.p);
+    hipStream_t s = ctx->stream;
+    if (nf) {
+        HIPCHK(hipMemcpyAsync(base + o_q, b->q, ncf * 2048, hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(base + o_sf, b->sf, ncf * 128, hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(base + o_cb, b->cb, ncf * 128, hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(base + o_ics, b->ics, ncf * sizeof(jaad_ics_info), hipMemcpyHostToDevice, s));
+        if (b->ms_used) HIPCHK(hipMemcpyAsync(base + o_ms, b->ms_used, nf * 16, hipMemcpyHostToDevice, s));
+        if (b->tns) HIPCHK(hipMemcpyAsync(base + o_tns, b->tns, ncf * sizeof(jaad_tns), hipMemcpyHostToDevice, s));
+    }
+    jaad_batch db = *b;
+    db.q = reinterpret_cast<const int16_t*>(base + o_q);
+    db.sf = reinterpret_cast<const uint8_t*>(base + o_sf);
+    db.cb = reinterpret_cast<const uint8_t*>(base + o_cb);
+    db.ics = reinterpret_cast<const jaad_ics_info*>(base + o_ics);
+    db.ms_used = b->ms_used ? reinterpret_cast<const uint64_t*>(base + o_ms) : nullptr;
+    db.tns = b->tns ? reinterpret_cast<const jaad_tns*>(base + o_tns) : nullptr;
+    if ((rc = launch(ctx, &db, ctx->d_pcm.p, flags, s))) return rc;
+    if (nf) HIPCHK(hipMemcpyAsync(pcm_out, ctx->d_pcm.p, pbytes, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return JAAD_OK;
+}
+
+int jaad_decode_batch_device(jaad_ctx* ctx, const jaad_batch* b, void* pcm_dev, size_t pcm_bytes, uint32_t flags,
+                             void* hip_stream)
+{
+    int rc = check_batch(ctx, b, pcm_bytes, flags);
+    if (rc) return rc;
+    if (!pcm_dev && b->n_frames) return JAAD_ERR_INVALID_ARG;
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : ctx->stream;
+    return launch(ctx, b, pcm_dev, flags, s);
+}
+
+int jaad_wait(jaad_ctx* ctx)
+{
+    if (!ctx) return JAAD_ERR_INVALID_ARG;
+    HIPCHK(hipDeviceSynchronize());
+    return JAAD_OK;
+}
+
+size_t jaad_state_bytes(const jaad_ctx* ctx) { return ctx ? 2048 * sizeof(float) : 0; }
+
+int jaad_state_export(jaad_ctx* ctx, uint32_t slot, void* buf, size_t bytes)
+{
+    if (!ctx || !buf || slot >= ctx->n_slots || bytes < jaad_state_bytes(ctx)) return JAAD_ERR_INVALID_ARG;
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    HIPCHK(hipMemcpy(buf, ctx->d_state[ctx->parity] + (size_t)slot * 2048, 2048 * sizeof(float), hipMemcpyDeviceToHost));
+    return JAAD_OK;
+}
+
+int jaad_state_import(jaad_ctx* ctx, uint32_t slot, const void* buf, size_t bytes)
+{
+    if (!ctx || !buf || slot >= ctx->n_slots || bytes < jaad_state_bytes(ctx)) return JAAD_ERR_INVALID_ARG;
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    HIPCHK(hipMemcpy(ctx->d_state[ctx->parity] + (size_t)slot * 2048, buf, 2048 * sizeof(float), hipMemcpyHostToDevice));
+    return JAAD_OK;
+}
+
+int jaad_state_reset(jaad_ctx* ctx, uint32_t slot)
+{
+    if (!ctx || slot >= ctx->n_slots) return JAAD_ERR_INVALID_ARG;
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    HIPCHK(hipMemset(ctx->d_state[ctx->parity] + (size_t)slot * 2048, 0, 2048 * sizeof(float)));
+    return JAAD_OK;
+}
+
+}  // extern "C"

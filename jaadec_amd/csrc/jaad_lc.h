@@ -1,0 +1,78 @@
+// Internal (host <-> device) definitions of the AAC-LC DSP kernel.  Not part of the C-ABI.
+#pragma once
+#include <stdint.h>
+
+#include "../../include/jaad_gpu.h"
+
+namespace jaad {
+
+constexpr int kWavesPerWG = 4;
+constexpr int kWGThreads = 64 * kWavesPerWG;
+constexpr int kChunkFrames = 8;  // frames one wave decodes back to back (overlap carried in VGPRs)
+
+// One unit of work = up to kChunkFrames consecutive frames of one run.  A chunk that does not
+// start its run first re-decodes the frame before it to rebuild the IMDCT overlap (the overlap
+// written by FilterBank.process depends only on the frame that writes it:
+// A/filterbank/FilterBank.java:46-51,61-70,90-100,116-118 overwrite all 1024 samples).
+struct ChunkDesc {
+    uint32_t frame0;
+    uint32_t info;   // [15:0] frames, bit16 recompute previous frame, bit17 load slot state,
+                     // bit18 store slot state after the last frame
+    uint32_t slot;
+    uint32_t pad;
+};
+enum : uint32_t { kChunkPrefix = 1u << 16, kChunkLoadState = 1u << 17, kChunkStoreState = 1u << 18 };
+
+// Constant tables staged into LDS once per workgroup (reference tables carried as data,
+// csrc/tables/jaad_tables.inc).  Layout shared by host (builder) and device (prologue copy).
+struct alignas(16) LdsTables {
+    float win_long[2][1024];   // SINE_1024, KBD_1024 (A/filterbank/SineWindows.java, KBDWindows.java)
+    float win_short[2][128];   // SINE_128, KBD_128
+    float mdct_l[512][2];      // MDCT_TABLE_2048 (A/filterbank/MDCTTables.java:5)
+    float mdct_s[64][2];       // MDCT_TABLE_128  (:519)
+    float roots_l[256][2];     // FFT_TABLE_512[k][0..1], k < 256 (A/filterbank/FFTTables.java:5)
+    float roots_s[32][2];      // FFT_TABLE_64[k],       k < 32  (:519)
+    float sf_gain[256];        // SCALEFACTOR_TABLE[100+i] (A/syntax/ScaleFactorTable.java)
+    float iq_head[128];        // IQ_TABLE[i], i < 128 (A/syntax/IQTable.java)
+    float tns_coef[4][16];     // TNS_TABLES (A/tools/TNSTables.java), zero padded
+    uint8_t quad2band_l[256];  // long window: scalefactor band of bins 4i..4i+3 (255 = none)
+    uint8_t quad2band_s[32];   // short window
+    int16_t swb_l[64];         // SWB offsets long (ScaleFactorBands.java), count+1 entries
+    int16_t swb_s[16];         // SWB offsets short
+    int32_t nswb_l, nswb_s, tns_max_l, tns_max_s;
+};
+static_assert(sizeof(LdsTables) % 16 == 0, "LdsTables must be 16-byte granular");
+
+struct KernelArgs {
+    const int16_t* q;
+    const uint8_t* sf;
+    const uint8_t* cb;
+    const jaad_ics_info* ics;
+    const uint64_t* ms_used;
+    const jaad_tns* tns;
+    const float* iq_table;      // full IQ_TABLE[8191] (device)
+    const LdsTables* tables;    // device copy of the LDS image
+    const ChunkDesc* chunks;
+    float* state_in;            // [slot][2][1024] overlap, read by chunks with kChunkLoadState
+    float* state_out;           // written by chunks with kChunkStoreState
+    void* pcm;                  // frame-major output
+    uint32_t n_chunks;
+    uint32_t nch;               // 1 (SCE) or 2 (CPE)
+    uint32_t out_mode;          // JAAD_PCM_* flags
+    uint32_t tns_mode;          // JAAD_TNS_*
+    float* dbg;                 // internal: stage dump of chunk 0's first emitted frame (or null)
+};
+
+void build_lds_tables(int sf_index, LdsTables* t);
+
+}  // namespace jaad
+
+#ifdef __HIP_PLATFORM_AMD__
+#include <hip/hip_runtime_api.h>
+namespace jaad {
+hipError_t launch_lc(const KernelArgs& a, int grid, hipStream_t stream, bool tns_spec);
+}
+#endif
+namespace jaad {
+
+}  // namespace jaad

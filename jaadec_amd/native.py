@@ -1,0 +1,293 @@
+"""ctypes binding of the C-ABI (include/jaad_gpu.h, include/jaad_synth.h).
+
+The product path is ``libjaadgpu.so`` (HIP kernels for gfx950).  There is deliberately no CPU
+fallback: if the library cannot be loaded, or no gfx950 device is present when a context is
+created, the call raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from pathlib import Path
+
+import numpy as np
+
+PKG = Path(__file__).resolve().parent
+LIB_PATH = PKG / "libjaadgpu.so"
+SYNTH_PATH = PKG / "libjaadsynth.so"
+
+ABI_VERSION = 1
+
+# status codes (jaad_status)
+OK, ERR_INVALID_ARG, ERR_NO_DEVICE, ERR_HIP, ERR_UNSUPPORTED, ERR_BITSTREAM, ERR_NOMEM, ERR_ABI = 0, -1, -2, -3, -4, -5, -6, -7
+
+ONLY_LONG_SEQUENCE, LONG_START_SEQUENCE, EIGHT_SHORT_SEQUENCE, LONG_STOP_SEQUENCE = 0, 1, 2, 3
+ZERO_HCB, NOISE_HCB, INTENSITY_HCB2, INTENSITY_HCB = 0, 13, 14, 15
+TNS_COMPAT, TNS_SPEC = 0, 1
+PCM_BIG_ENDIAN, PCM_LITTLE_ENDIAN, PCM_FLOAT32 = 0, 1, 2
+ICS_HAS_PNS, ICS_HAS_IS, ICS_TNS, ICS_MS_PRESENT, ICS_COMMON_WINDOW = 1, 2, 4, 8, 16
+
+ICS_DTYPE = np.dtype([
+    ("window_sequence", "u1"), ("window_shape", "u1"), ("window_shape_prev", "u1"), ("max_sfb", "u1"),
+    ("grouping", "u1"), ("flags", "u1"), ("reserved", "u1", (2,)), ("pns_state", "<u4"), ("reserved2", "<u4"),
+])
+assert ICS_DTYPE.itemsize == 16
+TNS_FILTER_DTYPE = np.dtype([("window", "u1"), ("length", "u1"), ("order", "u1"), ("flags", "u1"), ("coef", "u1", (20,))])
+TNS_DTYPE = np.dtype([("n_filters", "u1"), ("reserved", "u1", (3,)), ("filt", TNS_FILTER_DTYPE, (8,))])
+assert TNS_DTYPE.itemsize == 196
+
+
+class StreamCfg(C.Structure):
+    _fields_ = [("abi_version", C.c_uint32), ("profile", C.c_uint8), ("sf_index", C.c_uint8),
+                ("channel_config", C.c_uint8), ("tns_mode", C.c_uint8), ("sbr", C.c_uint8), ("ps", C.c_uint8),
+                ("reserved", C.c_uint8 * 2)]
+
+
+class BatchStruct(C.Structure):
+    _fields_ = [("n_frames", C.c_uint32), ("n_runs", C.c_uint32), ("stream_slot", C.c_void_p),
+                ("frame_begin", C.c_void_p), ("q", C.c_void_p), ("sf", C.c_void_p), ("cb", C.c_void_p),
+                ("ics", C.c_void_p), ("ms_used", C.c_void_p), ("tns", C.c_void_p)]
+
+
+class SynthParams(C.Structure):
+    _fields_ = [("seed", C.c_uint64), ("n_streams", C.c_uint32), ("frames_per_stream", C.c_uint32),
+                ("sf_index", C.c_uint8), ("channel_config", C.c_uint8), ("window_switching", C.c_uint8),
+                ("tns_percent", C.c_uint8), ("pns_percent", C.c_uint8), ("is_percent", C.c_uint8),
+                ("ms_mode", C.c_uint8), ("global_gain", C.c_uint8), ("escape_permille", C.c_uint8),
+                ("common_window", C.c_uint8), ("reserved", C.c_uint8 * 2), ("pns_state0", C.c_uint32)]
+
+
+# every symbol include/jaad_gpu.h declares (checked by tests/test_abi.py)
+EXPORTS = ["jaad_cfg_sample_length", "jaad_cfg_channel_count", "jaad_frame_pcm_bytes", "jaad_ctx_create",
+           "jaad_ctx_destroy", "jaad_decode_batch", "jaad_decode_batch_device", "jaad_wait", "jaad_state_bytes",
+           "jaad_state_export", "jaad_state_import", "jaad_state_reset", "jaad_strerror", "jaad_last_error"]
+
+
+class JaadError(RuntimeError):
+    """Raised for a nonzero jaad_status (the JNI glue maps these to AACException)."""
+
+    def __init__(self, status: int, what: str = ""):
+        self.status = status
+        super().__init__(f"{what}: {status} ({strerror(status)})" if what else f"{status} ({strerror(status)})")
+
+
+_lib = None
+_synth = None
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise RuntimeError(f"{LIB_PATH} is missing: build it with `python -m jaadec_amd.build` "
+                               "(there is no CPU fallback for the HIP path)")
+        L = C.CDLL(str(LIB_PATH))
+        L.jaad_cfg_sample_length.argtypes = [C.POINTER(StreamCfg)]
+        L.jaad_cfg_channel_count.argtypes = [C.POINTER(StreamCfg)]
+        L.jaad_frame_pcm_bytes.argtypes = [C.POINTER(StreamCfg), C.c_uint32]
+        L.jaad_frame_pcm_bytes.restype = C.c_size_t
+        L.jaad_ctx_create.argtypes = [C.POINTER(StreamCfg), C.c_uint32, C.c_int, C.POINTER(C.c_void_p)]
+        L.jaad_ctx_destroy.argtypes = [C.c_void_p]
+        L.jaad_ctx_destroy.restype = None
+        L.jaad_decode_batch.argtypes = [C.c_void_p, C.POINTER(BatchStruct), C.c_void_p, C.c_size_t, C.c_uint32]
+        L.jaad_decode_batch_device.argtypes = [C.c_void_p, C.POINTER(BatchStruct), C.c_void_p, C.c_size_t,
+                                               C.c_uint32, C.c_void_p]
+        L.jaad_wait.argtypes = [C.c_void_p]
+        L.jaad_state_bytes.argtypes = [C.c_void_p]
+        L.jaad_state_bytes.restype = C.c_size_t
+        L.jaad_state_export.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_size_t]
+        L.jaad_state_import.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_size_t]
+        L.jaad_state_reset.argtypes = [C.c_void_p, C.c_uint32]
+        L.jaad_strerror.argtypes = [C.c_int]
+        L.jaad_strerror.restype = C.c_char_p
+        L.jaad_last_error.argtypes = [C.c_void_p]
+        L.jaad_last_error.restype = C.c_char_p
+        _lib = L
+    return _lib
+
+
+def synth_lib() -> C.CDLL:
+    global _synth
+    if _synth is None:
+        if not SYNTH_PATH.exists():
+            raise RuntimeError(f"{SYNTH_PATH} is missing: build with `python -m jaadec_amd.build`")
+        S = C.CDLL(str(SYNTH_PATH))
+        S.jaad_synth_default.argtypes = [C.c_int, C.POINTER(SynthParams)]
+        S.jaad_synth_default.restype = None
+        S.jaad_synth_generate.argtypes = [C.POINTER(SynthParams)] + [C.c_void_p] * 8 + [C.c_int]
+        _synth = S
+    return _synth
+
+
+def strerror(status: int) -> str:
+    try:
+        return lib().jaad_strerror(status).decode()
+    except Exception:  # pragma: no cover - library missing
+        return "?"
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data
+
+
+@dataclass
+class Batch:
+    """Host SoA batch in the jaad_gpu.h layout (numpy arrays)."""
+
+    q: np.ndarray            # int16 [ncf, 1024]
+    sf: np.ndarray           # uint8 [ncf, 128]
+    cb: np.ndarray           # uint8 [ncf, 128]
+    ics: np.ndarray          # ICS_DTYPE [ncf]
+    ms_used: np.ndarray | None  # uint64 [nf, 2]
+    tns: np.ndarray | None      # TNS_DTYPE [ncf]
+    stream_slot: np.ndarray  # uint32 [n_runs]
+    frame_begin: np.ndarray  # uint32 [n_runs+1]
+    nch: int
+
+    @property
+    def n_frames(self) -> int:
+        return int(self.frame_begin[-1])
+
+    def struct(self) -> BatchStruct:
+        for a in (self.q, self.sf, self.cb, self.ics, self.stream_slot, self.frame_begin):
+            assert a.flags["C_CONTIGUOUS"]
+        return BatchStruct(self.n_frames, len(self.stream_slot), _ptr(self.stream_slot), _ptr(self.frame_begin),
+                           _ptr(self.q), _ptr(self.sf), _ptr(self.cb), _ptr(self.ics), _ptr(self.ms_used),
+                           _ptr(self.tns))
+
+    def select_runs(self, runs) -> "Batch":
+        """Sub-batch made of the given runs (frames renumbered, slots kept)."""
+        runs = list(runs)
+        fb = self.frame_begin
+        frames = np.concatenate([np.arange(fb[r], fb[r + 1]) for r in runs]) if runs else np.zeros(0, np.int64)
+        cfr = (frames[:, None] * self.nch + np.arange(self.nch)[None, :]).reshape(-1)
+        lens = np.array([fb[r + 1] - fb[r] for r in runs], np.uint32)
+        begin = np.zeros(len(runs) + 1, np.uint32)
+        begin[1:] = np.cumsum(lens)
+        return Batch(np.ascontiguousarray(self.q[cfr]), np.ascontiguousarray(self.sf[cfr]),
+                     np.ascontiguousarray(self.cb[cfr]), np.ascontiguousarray(self.ics[cfr]),
+                     None if self.ms_used is None else np.ascontiguousarray(self.ms_used[frames]),
+                     None if self.tns is None else np.ascontiguousarray(self.tns[cfr]),
+                     np.ascontiguousarray(self.stream_slot[runs]).astype(np.uint32), begin, self.nch)
+
+    def split_frames(self, cut: int) -> tuple["Batch", "Batch"]:
+        """Split every run at its frame `cut` (for multi-call continuation tests)."""
+        fb = self.frame_begin
+        a_frames, b_frames, la, lb = [], [], [], []
+        for r in range(len(self.stream_slot)):
+            f0, f1 = int(fb[r]), int(fb[r + 1])
+            m = min(f0 + cut, f1)
+            a_frames.append(np.arange(f0, m))
+            b_frames.append(np.arange(m, f1))
+            la.append(m - f0)
+            lb.append(f1 - m)
+
+        def mk(fr, lens):
+            frames = np.concatenate(fr)
+            cfr = (frames[:, None] * self.nch + np.arange(self.nch)[None, :]).reshape(-1)
+            begin = np.zeros(len(lens) + 1, np.uint32)
+            begin[1:] = np.cumsum(lens)
+            return Batch(np.ascontiguousarray(self.q[cfr]), np.ascontiguousarray(self.sf[cfr]),
+                         np.ascontiguousarray(self.cb[cfr]), np.ascontiguousarray(self.ics[cfr]),
+                         None if self.ms_used is None else np.ascontiguousarray(self.ms_used[frames]),
+                         None if self.tns is None else np.ascontiguousarray(self.tns[cfr]),
+                         self.stream_slot.copy(), begin, self.nch)
+
+        return mk(a_frames, la), mk(b_frames, lb)
+
+
+def synth_params(config_id: int = 2, **over) -> SynthParams:
+    p = SynthParams()
+    synth_lib().jaad_synth_default(config_id, C.byref(p))
+    for k, v in over.items():
+        setattr(p, k, v)
+    return p
+
+
+def synth_batch(p: SynthParams, with_tns: bool | None = None, threads: int = 0) -> Batch:
+    nch = 2 if p.channel_config == 2 else 1
+    nf = p.n_streams * p.frames_per_stream
+    ncf = nf * nch
+    q = np.empty((ncf, 1024), np.int16)
+    sf = np.empty((ncf, 128), np.uint8)
+    cb = np.empty((ncf, 128), np.uint8)
+    ics = np.empty(ncf, ICS_DTYPE)
+    ms = np.zeros((nf, 2), np.uint64) if nch == 2 else None
+    if with_tns is None:
+        with_tns = p.tns_percent > 0
+    tns = np.zeros(ncf, TNS_DTYPE) if with_tns else None
+    slot = np.empty(p.n_streams, np.uint32)
+    begin = np.empty(p.n_streams + 1, np.uint32)
+    rc = synth_lib().jaad_synth_generate(C.byref(p), _ptr(q), _ptr(sf), _ptr(cb), _ptr(ics), _ptr(ms), _ptr(tns),
+                                         _ptr(slot), _ptr(begin), threads)
+    if rc:
+        raise JaadError(rc, "jaad_synth_generate")
+    return Batch(q, sf, cb, ics, ms, tns, slot, begin, nch)
+
+
+def make_cfg(sf_index: int = 3, channel_config: int = 2, tns_mode: int = TNS_COMPAT) -> StreamCfg:
+    return StreamCfg(ABI_VERSION, 2, sf_index, channel_config, tns_mode, 0, 0)
+
+
+def pcm_frame_bytes(flags: int) -> int:
+    return 1024 * 2 * (4 if flags & PCM_FLOAT32 else 2)
+
+
+class Context:
+    """Owns a jaad_ctx: n_slots independent stream states on one gfx950 device."""
+
+    def __init__(self, cfg: StreamCfg, n_slots: int, device: int = 0):
+        self.cfg = cfg
+        self.n_slots = n_slots
+        h = C.c_void_p()
+        rc = lib().jaad_ctx_create(C.byref(cfg), n_slots, device, C.byref(h))
+        if rc:
+            raise JaadError(rc, "jaad_ctx_create")
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().jaad_ctx_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def _check(self, rc: int, what: str):
+        if rc:
+            detail = lib().jaad_last_error(self.h).decode()
+            raise JaadError(rc, f"{what} {detail}".strip())
+
+    def decode(self, batch: Batch, flags: int = PCM_BIG_ENDIAN) -> np.ndarray:
+        """Host-buffer batch decode -> PCM bytes (uint8 [n_frames, frame_bytes])."""
+        nb = pcm_frame_bytes(flags)
+        out = np.empty((batch.n_frames, nb), np.uint8)
+        bs = batch.struct()
+        self._check(lib().jaad_decode_batch(self.h, C.byref(bs), _ptr(out), out.nbytes, flags), "jaad_decode_batch")
+        return out
+
+    def decode_device(self, dev: dict, batch: Batch, pcm_dev_ptr: int, pcm_bytes: int, flags: int = 0,
+                      stream_ptr: int | None = None) -> None:
+        """Device-resident decode: dev maps array names to device pointers (ints)."""
+        bs = BatchStruct(batch.n_frames, len(batch.stream_slot), _ptr(batch.stream_slot), _ptr(batch.frame_begin),
+                         dev["q"], dev["sf"], dev["cb"], dev["ics"], dev.get("ms_used"), dev.get("tns"))
+        self._check(lib().jaad_decode_batch_device(self.h, C.byref(bs), pcm_dev_ptr, pcm_bytes, flags, stream_ptr),
+                    "jaad_decode_batch_device")
+
+    def state_export(self, slot: int) -> np.ndarray:
+        n = lib().jaad_state_bytes(self.h)
+        buf = np.empty(n, np.uint8)
+        self._check(lib().jaad_state_export(self.h, slot, _ptr(buf), n), "jaad_state_export")
+        return buf
+
+    def state_import(self, slot: int, buf: np.ndarray) -> None:
+        buf = np.ascontiguousarray(buf, np.uint8)
+        self._check(lib().jaad_state_import(self.h, slot, _ptr(buf), buf.nbytes), "jaad_state_import")
+
+    def state_reset(self, slot: int) -> None:
+        self._check(lib().jaad_state_reset(self.h, slot), "jaad_state_reset")

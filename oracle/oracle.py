@@ -1,0 +1,92 @@
+"""TEST INFRASTRUCTURE ONLY -- Python binding of the C restatement (oracle/jaad_oracle.c).
+
+Imported only by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg, always as the
+checker / reported baseline, never as the measured or shipped path.  Parity status: see
+oracle/jaad_oracle.h ("parity unpinned" by reference outputs; pinned by closed forms + fixtures).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+LIB_PATH = HERE / "liboracle.so"
+_lib = None
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise RuntimeError(f"{LIB_PATH} missing: run `python -m jaadec_amd.build`")
+        L = C.CDLL(str(LIB_PATH))
+        L.orc_fft.argtypes = [C.c_void_p, C.c_int, C.c_int]
+        L.orc_fft.restype = None
+        L.orc_imdct.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
+        L.orc_imdct.restype = None
+        L.orc_filterbank.argtypes = [C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.orc_filterbank.restype = None
+        L.orc_dequant.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.orc_tns_spec.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
+        L.orc_tns_spec.restype = None
+        L.orc_pcm_pack.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_uint32, C.c_void_p]
+        L.orc_decode_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_uint32]
+        L.orc_decode_batch_mt.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_uint32,
+                                          C.c_int]
+        _lib = L
+    return _lib
+
+
+def fft(x: np.ndarray, forward: bool = False) -> np.ndarray:
+    a = np.ascontiguousarray(np.stack([x.real, x.imag], -1).astype(np.float32))
+    lib().orc_fft(a.ctypes.data, len(x), int(forward))
+    return a[:, 0].astype(np.float64) + 1j * a[:, 1].astype(np.float64)
+
+
+def imdct(spec: np.ndarray) -> np.ndarray:
+    spec = np.ascontiguousarray(spec, np.float32)
+    out = np.empty(2 * len(spec), np.float32)
+    lib().orc_imdct(spec.ctypes.data, out.ctypes.data, 2 * len(spec))
+    return out
+
+
+def filterbank(seq: int, shape: int, shape_prev: int, spec: np.ndarray, overlap: np.ndarray) -> np.ndarray:
+    spec = np.ascontiguousarray(spec, np.float32)
+    out = np.empty(1024, np.float32)
+    assert overlap.dtype == np.float32 and overlap.flags["C_CONTIGUOUS"]
+    lib().orc_filterbank(seq, shape, shape_prev, spec.ctypes.data, out.ctypes.data, overlap.ctypes.data)
+    return out
+
+
+def pcm_pack(chans: list, flags: int = 0) -> bytes:
+    arrs = [np.ascontiguousarray(c, np.float32) for c in chans]
+    ptrs = (C.c_void_p * len(arrs))(*[a.ctypes.data for a in arrs])
+    n = len(arrs[0])
+    out = np.empty(n * len(arrs) * (4 if flags & 2 else 2), np.uint8)
+    lib().orc_pcm_pack(ptrs, len(arrs), n, flags, out.ctypes.data)
+    return out.tobytes()
+
+
+class Streams:
+    """Per-slot restated decoder state (orc_stream = ICStream.overlap per channel)."""
+
+    def __init__(self, n_slots: int):
+        self.state = np.zeros((n_slots, 2, 1024), np.float32)
+
+
+def decode_batch(cfg, batch, streams: Streams, flags: int = 0, threads: int = 1) -> np.ndarray:
+    """Decode a jaadec_amd.native.Batch on the CPU restatement; returns uint8 [n_frames, bytes]."""
+    nb = 1024 * 2 * (4 if flags & 2 else 2)
+    out = np.empty((batch.n_frames, nb), np.uint8)
+    bs = batch.struct()
+    if threads == 1:
+        rc = lib().orc_decode_batch(C.addressof(cfg), streams.state.ctypes.data, C.addressof(bs), out.ctypes.data,
+                                    out.nbytes, flags)
+    else:
+        rc = lib().orc_decode_batch_mt(C.addressof(cfg), streams.state.ctypes.data, C.addressof(bs),
+                                       out.ctypes.data, out.nbytes, flags, threads)
+    if rc:
+        raise RuntimeError(f"oracle decode failed: {rc}")
+    return out
