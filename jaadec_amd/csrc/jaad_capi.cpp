@@ -58,6 +58,7 @@ struct jaad_ctx {
     std::vector<uint8_t> slot_used;
     bool plan_valid = false;
     int n_cu = 256;
+    uint32_t chunk_frames = kDefaultChunkFrames;
     float* dbg = nullptr;
     std::string err;
 };
@@ -67,16 +68,34 @@ namespace jaad {
 void build_lds_tables(int sf_index, LdsTables* t)
 {
     std::memset(t, 0, sizeof(*t));
-    std::memcpy(t->win_long[0], JAAD_SINE_1024, sizeof(t->win_long[0]));
-    std::memcpy(t->win_long[1], JAAD_KBD_1024, sizeof(t->win_long[1]));
+    const float* LW[2] = {JAAD_SINE_1024, JAAD_KBD_1024};
+    for (int sh = 0; sh < 2; sh++)
+        for (int o = 0; o < 16; o++)
+            for (int u = 0; u < 64; u++) t->win_slot[sh][o][u] = LW[sh][long_pos_host(u, o)];
     std::memcpy(t->win_short[0], JAAD_SINE_128, sizeof(t->win_short[0]));
     std::memcpy(t->win_short[1], JAAD_KBD_128, sizeof(t->win_short[1]));
     std::memcpy(t->mdct_l, JAAD_MDCT_TABLE_2048, sizeof(t->mdct_l));
-    std::memcpy(t->mdct_s, JAAD_MDCT_TABLE_128, sizeof(t->mdct_s));
-    for (int k = 0; k < 256; k++) {
-        t->roots_l[k][0] = JAAD_FFT_TABLE_512[k][0];
-        t->roots_l[k][1] = JAAD_FFT_TABLE_512[k][1];
+    // 512-point IFFT twiddles roots[k*m] (FFT.java:116-120, inverse column 1) pre-arranged per
+    // register pass: pass 1 (i = 4, m = 64); pass 2 lane b = u&7: slot 0 -> stage 8 (m = 32, k = b),
+    // slots 1,2 -> stage 16 (m = 16, k = b + 8e), slots 3..6 -> stage 32 (m = 8, k = b + 8s);
+    // pass 3 lane u: slot 0 -> stage 64 (m = 4, k = u), 1,2 -> stage 128 (m = 2, k = u + 64e),
+    // 3..6 -> stage 256 (m = 1, k = u + 64s)
+    auto root = [](int idx, float* d) {
+        d[0] = JAAD_FFT_TABLE_512[idx][0];
+        d[1] = JAAD_FFT_TABLE_512[idx][1];
+    };
+    for (int k = 0; k < 4; k++) root(k * 64, t->tw1[k]);
+    for (int b = 0; b < 8; b++) {
+        root(32 * b, t->tw2[0][b]);
+        for (int e = 0; e < 2; e++) root(16 * (b + 8 * e), t->tw2[1 + e][b]);
+        for (int s = 0; s < 4; s++) root(8 * (b + 8 * s), t->tw2[3 + s][b]);
     }
+    for (int u = 0; u < 64; u++) {
+        root(4 * u, t->tw3[0][u]);
+        for (int e = 0; e < 2; e++) root(2 * (u + 64 * e), t->tw3[1 + e][u]);
+        for (int s = 0; s < 4; s++) root(u + 64 * s, t->tw3[3 + s][u]);
+    }
+    std::memcpy(t->mdct_s, JAAD_MDCT_TABLE_128, sizeof(t->mdct_s));
     for (int k = 0; k < 32; k++) {
         t->roots_s[k][0] = JAAD_FFT_TABLE_64[k][0];
         t->roots_s[k][1] = JAAD_FFT_TABLE_64[k][1];
@@ -157,8 +176,8 @@ int plan(jaad_ctx* ctx, const jaad_batch* b)
             ctx->chunks.push_back(cd);
             continue;
         }
-        for (uint32_t f = f0; f < f1; f += kChunkFrames) {
-            uint32_t n = f1 - f < (uint32_t)kChunkFrames ? f1 - f : (uint32_t)kChunkFrames;
+        for (uint32_t f = f0; f < f1; f += ctx->chunk_frames) {
+            uint32_t n = f1 - f < ctx->chunk_frames ? f1 - f : ctx->chunk_frames;
             uint32_t info = n;
             info |= (f == f0) ? kChunkLoadState : kChunkPrefix;
             if (f + n == f1) info |= kChunkStoreState;
@@ -211,7 +230,7 @@ int launch(jaad_ctx* ctx, const jaad_batch* db, void* pcm, uint32_t flags, hipSt
                               hipMemcpyDeviceToDevice, stream));
         s = e;
     }
-    const int per_wg = kWavesPerWG;
+    const int per_wg = ctx->nch == 2 ? kWavesPerWG / 2 : kWavesPerWG;
     int grid = (int)((a.n_chunks + per_wg - 1) / per_wg);
     const bool tns_spec = ctx->cfg.tns_mode == JAAD_TNS_SPEC && db->tns != nullptr;
     HIPCHK(launch_lc(a, grid, stream, tns_spec));

@@ -8,11 +8,11 @@ namespace jaad {
 
 constexpr int kWavesPerWG = 4;
 constexpr int kWGThreads = 64 * kWavesPerWG;
-constexpr int kChunkFrames = 8;  // frames one wave decodes back to back (overlap carried in VGPRs)
+constexpr int kDefaultChunkFrames = 8;  // frames one wave (pair) decodes back to back
 
-// One unit of work = up to kChunkFrames consecutive frames of one run.  A chunk that does not
-// start its run first re-decodes the frame before it to rebuild the IMDCT overlap (the overlap
-// written by FilterBank.process depends only on the frame that writes it:
+// One unit of work = up to N consecutive frames of one run.  A chunk that does not start its
+// run first re-decodes the frame before it to rebuild the IMDCT overlap (the overlap written by
+// FilterBank.process depends only on the frame that writes it:
 // A/filterbank/FilterBank.java:46-51,61-70,90-100,116-118 overwrite all 1024 samples).
 struct ChunkDesc {
     uint32_t frame0;
@@ -24,21 +24,24 @@ struct ChunkDesc {
 enum : uint32_t { kChunkPrefix = 1u << 16, kChunkLoadState = 1u << 17, kChunkStoreState = 1u << 18 };
 
 // Constant tables staged into LDS once per workgroup (reference tables carried as data,
-// csrc/tables/jaad_tables.inc).  Layout shared by host (builder) and device (prologue copy).
+// csrc/tables/jaad_tables.inc), pre-permuted so that every lane-parallel read is
+// bank-conflict free.  Built by the host (build_lds_tables), copied verbatim by the prologue.
 struct alignas(16) LdsTables {
-    float win_long[2][1024];   // SINE_1024, KBD_1024 (A/filterbank/SineWindows.java, KBDWindows.java)
-    float win_short[2][128];   // SINE_128, KBD_128
-    float mdct_l[512][2];      // MDCT_TABLE_2048 (A/filterbank/MDCTTables.java:5)
-    float mdct_s[64][2];       // MDCT_TABLE_128  (:519)
-    float roots_l[256][2];     // FFT_TABLE_512[k][0..1], k < 256 (A/filterbank/FFTTables.java:5)
-    float roots_s[32][2];      // FFT_TABLE_64[k],       k < 32  (:519)
-    float sf_gain[256];        // SCALEFACTOR_TABLE[100+i] (A/syntax/ScaleFactorTable.java)
-    float iq_head[128];        // IQ_TABLE[i], i < 128 (A/syntax/IQTable.java)
-    float tns_coef[4][16];     // TNS_TABLES (A/tools/TNSTables.java), zero padded
-    uint8_t quad2band_l[256];  // long window: scalefactor band of bins 4i..4i+3 (255 = none)
-    uint8_t quad2band_s[32];   // short window
-    int16_t swb_l[64];         // SWB offsets long (ScaleFactorBands.java), count+1 entries
-    int16_t swb_s[16];         // SWB offsets short
+    float win_slot[2][16][64];  // long window [shape][slot o][lane u] = W[long_pos(u,o)] (SINE/KBD_1024)
+    float mdct_l[512][2];       // MDCT_TABLE_2048 (A/filterbank/MDCTTables.java:5), k order
+    float tw3[7][64][2];        // 512-pt IFFT pass-3 twiddles [j][lane]  (FFT_TABLE_512, FFTTables.java:5)
+    float tw2[7][8][2];         // 512-pt IFFT pass-2 twiddles [j][lane&7]
+    float tw1[4][2];            // 512-pt IFFT pass-1 (i = 4) twiddles
+    float win_short[2][128];    // SINE_128, KBD_128
+    float mdct_s[64][2];        // MDCT_TABLE_128 (:519)
+    float roots_s[32][2];       // FFT_TABLE_64[k], k < 32 (:519)
+    float sf_gain[256];         // SCALEFACTOR_TABLE[100+i] (A/syntax/ScaleFactorTable.java)
+    float iq_head[128];         // IQ_TABLE[i], i < 128 (A/syntax/IQTable.java)
+    float tns_coef[4][16];      // TNS_TABLES (A/tools/TNSTables.java), zero padded
+    uint8_t quad2band_l[256];   // long window: scalefactor band of bins 4i..4i+3 (255 = none)
+    uint8_t quad2band_s[32];    // short window
+    int16_t swb_l[64];          // SWB offsets long (ScaleFactorBands.java), count+1 entries
+    int16_t swb_s[16];          // SWB offsets short
     int32_t nswb_l, nswb_s, tns_max_l, tns_max_s;
 };
 static_assert(sizeof(LdsTables) % 16 == 0, "LdsTables must be 16-byte granular");
@@ -63,6 +66,14 @@ struct KernelArgs {
     float* dbg;                 // internal: stage dump of chunk 0's first emitted frame (or null)
 };
 
+// position (0..1023) of lane u's IMDCT output slot o = 2s+h (see jaad_lc.hip, long_pos)
+inline int long_pos_host(int u, int o)
+{
+    int s = o >> 1, h = o & 1, k = u + 64 * s;
+    if (s < 4) return h ? 512 + 2 * k : 511 - 2 * k;
+    return h ? 1535 - 2 * k : 2 * k - 512;
+}
+
 void build_lds_tables(int sf_index, LdsTables* t);
 
 }  // namespace jaad
@@ -73,6 +84,3 @@ namespace jaad {
 hipError_t launch_lc(const KernelArgs& a, int grid, hipStream_t stream, bool tns_spec);
 }
 #endif
-namespace jaad {
-
-}  // namespace jaad

@@ -8,34 +8,34 @@
 //   SampleBuffer.accept PCM packing           S/SampleBuffer.java:168-209
 // in ONE pass over HBM: quantised int16 spectra in, interleaved PCM out.
 //
-// Work decomposition: one wave64 decodes a chunk of up to kChunkFrames consecutive frames of one
-// stream; the 1024-sample IMDCT overlap of every channel stays in VGPRs between frames (lane u
-// owns output positions {2u+128j} U {1023-2u-128j}); a chunk that does not start its stream
-// re-decodes the previous frame to rebuild the overlap.  Each frame's 512-point complex IFFT is
-// held as 8 complex values per lane and done in three register passes (bit-reversed radix-4 +
-// one radix-2 stage, then 3+3 radix-2 stages) with two LDS transposes.  The butterflies,
-// twiddles (the reference's float32 recurrence tables) and evaluation order are those of the
-// Java code, and the file is compiled with -ffp-contract=off, so results are bit-exact.
+// Work decomposition.  A workgroup = 4 waves.  For a CPE stream the two waves of a "pair" each
+// own one channel of a chunk of consecutive frames (mono: every wave its own stream); the pair
+// meets in LDS (4 workgroup barriers per frame) for M/S and I/S and to interleave the PCM.  The
+// 1024-sample IMDCT overlap of a channel stays in its wave's VGPRs between frames (lane u owns
+// output positions {2u+128j} U {1023-2u-128j}); a chunk that does not start its stream
+// re-decodes the previous frame to rebuild it.  All global inputs of frame f+1 are loaded while
+// frame f is computed.  The 512-point complex IFFT of a frame is 8 complex values per lane in
+// three register passes (bit-reversed radix-4 + one radix-2 stage, then 3 + 3 radix-2 stages)
+// with two XOR-swizzled LDS transposes.  Butterflies, twiddles (the reference's float32
+// recurrence tables) and evaluation order are those of the Java code, and the file is compiled
+// with -ffp-contract=off, so the results are bit-exact.
 #include <hip/hip_runtime.h>
 
 #include "jaad_lc.h"
 
+#ifndef JAAD_WAVES_PER_EU
+#define JAAD_WAVES_PER_EU 4
+#endif
+
 namespace jaad {
 
-struct alignas(16) LdsWave {
-    float buf[1024];      // spectrum / FFT transpose (float2[512]) / short-window OLA time buffer
-    float gain[2][128];   // per band: +-SCALEFACTOR_TABLE[...] as ICStream.scaleFactors holds it
-    uint32_t code[128];   // per band: cb_L | cb_R << 4 | ms_used << 8
+// per pair (CPE) or per two mono streams: band side info, written by the owning wave
+struct alignas(16) PairBands {
+    float gain[2][128];     // +-SCALEFACTOR_TABLE[...] as ICStream.scaleFactors holds it
+    uint8_t sf[2][128];     // raw scalefactor-table index - 100
+    uint8_t cb[2][128];     // section codebook (sfbCB)
+    uint8_t ms[128];        // ms_used bit per band (CPE, written by the left-channel wave)
 };
-
-__device__ __forceinline__ void wave_sync()
-{
-    // LDS traffic of one wave executes in order; this only stops the compiler from moving LDS
-    // accesses across the point (lanes exchange data through LDS inside one wave).
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 // Lane id through a volatile asm: keeps the compiler from hoisting every lane-dependent LDS
 // address out of the frame loop (which otherwise costs >100 VGPRs and all occupancy).
@@ -46,7 +46,26 @@ __device__ __forceinline__ int lane_id()
     return v;
 }
 
-// bit-reversal of 3 bits; element r of a bit-reversed 8-block lives in register BR3[r]
+__device__ __forceinline__ void wave_sync()
+{
+    // LDS traffic of one wave executes in order; this only stops the compiler from moving LDS
+    // accesses across the point (lanes of one wave exchange data through LDS).
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// spectrum layout in a wave's buffer: even bins in [0,512), odd bins in [512,1024), bin-pair
+// index XOR-swizzled so lane-parallel pre-twiddle reads (long and short) are conflict free
+__device__ __forceinline__ int eo_idx(int p)
+{
+    int j = p >> 1;
+    j ^= ((j >> 6) & 3) << 3;
+    return ((p & 1) << 9) + j;
+}
+// IFFT transpose layout (complex index), XOR-swizzled against the bit-reversed write pattern
+__device__ __forceinline__ int xs(int i) { return i ^ ((i >> 4) & 15); }
+
 __device__ constexpr int BR3[8] = {0, 4, 2, 6, 1, 5, 3, 7};
 
 // FFT.java:113-130 radix-2 butterfly (inverse twiddle = column 1 = +sin)
@@ -79,66 +98,61 @@ __device__ __forceinline__ void radix4_inv(float& r0, float& i0, float& r1, floa
 }
 
 // Pass 1 on a lane's 8 elements held in bit-reversed order r <-> register BR3[r]:
-// radix-4 on r=0..3 and r=4..7, then the i=4 radix-2 stage (roots[k*m1], k=0..3).
-__device__ __forceinline__ void fft_pass1(float (&re)[8], float (&im)[8], const float (*roots)[2], int m1)
+// radix-4 on r=0..3 and r=4..7, then the i=4 radix-2 stage with twiddles w[k*wstride], k=0..3.
+__device__ __forceinline__ void fft_pass1(float (&re)[8], float (&im)[8], const float (*w)[2], int wstride)
 {
     radix4_inv(re[BR3[0]], im[BR3[0]], re[BR3[1]], im[BR3[1]], re[BR3[2]], im[BR3[2]], re[BR3[3]], im[BR3[3]]);
     radix4_inv(re[BR3[4]], im[BR3[4]], re[BR3[5]], im[BR3[5]], re[BR3[6]], im[BR3[6]], re[BR3[7]], im[BR3[7]]);
 #pragma unroll
     for (int k = 0; k < 4; k++)
-        bfly(re[BR3[k]], im[BR3[k]], re[BR3[k + 4]], im[BR3[k + 4]], roots[k * m1][0], roots[k * m1][1]);
+        bfly(re[BR3[k]], im[BR3[k]], re[BR3[k + 4]], im[BR3[k + 4]], w[k * wstride][0], w[k * wstride][1]);
 }
 
-// Three radix-2 stages on elements base + b + B*s (s = 0..7, B = 8 or 64): strides B, 2B, 4B.
-// Stage with half-size i = B*2^j has twiddle roots[k * m] with k = (element mod 2i) and
-// m = n / (2i); here m = mB, mB/2, mB/4.
-__device__ __forceinline__ void fft_pass3stages(float (&re)[8], float (&im)[8], const float (*roots)[2], int b,
-                                                int B, int mB)
+// Three radix-2 stages on elements (base + b + B*s), s = 0..7: pairs (s,s+1), (s,s+2), (s,s+4).
+// tw(j) returns the twiddle of "slot" j: 0 for the first stage, 1+(s&1) for the second,
+// 3+s for the third (the tables are pre-arranged that way, see build_lds_tables).
+template <typename TW>
+__device__ __forceinline__ void fft_3stages(float (&re)[8], float (&im)[8], TW tw)
 {
+    {
+        float wr, wi;
+        tw(0, wr, wi);
 #pragma unroll
-    for (int s = 0; s < 8; s += 2) {
-        int k = b;
-        bfly(re[s], im[s], re[s + 1], im[s + 1], roots[k * mB][0], roots[k * mB][1]);
+        for (int s = 0; s < 8; s += 2) bfly(re[s], im[s], re[s + 1], im[s + 1], wr, wi);
     }
 #pragma unroll
-    for (int s0 = 0; s0 < 8; s0 += 4) {
-#pragma unroll
-        for (int t = 0; t < 2; t++) {
-            int s = s0 + t;
-            int k = b + B * (s & 1);
-            bfly(re[s], im[s], re[s + 2], im[s + 2], roots[k * (mB >> 1)][0], roots[k * (mB >> 1)][1]);
-        }
+    for (int e = 0; e < 2; e++) {
+        float wr, wi;
+        tw(1 + e, wr, wi);
+        bfly(re[e], im[e], re[e + 2], im[e + 2], wr, wi);
+        bfly(re[4 + e], im[4 + e], re[6 + e], im[6 + e], wr, wi);
     }
 #pragma unroll
     for (int s = 0; s < 4; s++) {
-        int k = b + B * (s & 3);
-        bfly(re[s], im[s], re[s + 4], im[s + 4], roots[k * (mB >> 2)][0], roots[k * (mB >> 2)][1]);
+        float wr, wi;
+        tw(3 + s, wr, wi);
+        bfly(re[s], im[s], re[s + 4], im[s + 4], wr, wi);
     }
 }
 
-// Math.round(float) (ties toward +inf, NaN -> 0) followed by the short clamp of
-// SampleBuffer.accept (S/SampleBuffer.java:193-206); clamping first is equivalent.
-__device__ __forceinline__ int java_round16(float x)
+// position of IMDCT output slot o = 2s+h for lane u (MDCT.java:56-80 reorder)
+__device__ __forceinline__ int long_pos(int u, int o)
 {
-    if (x != x) return 0;
-    x = fminf(fmaxf(x, -32768.0f), 32767.0f);
-    float r = __builtin_rintf(x);
-    r = (x - r == 0.5f) ? r + 1.0f : r;
-    return (int)r;
-}
-
-__device__ __forceinline__ uint32_t pack16(int v, bool big_endian)
-{
-    uint32_t u = (uint32_t)v & 0xffffu;
-    return big_endian ? (((u & 0xffu) << 8) | (u >> 8)) : u;
-}
-
-// position of FFT slot (s, half) for lane u: see file header / MDCT.java:56-80
-__device__ __forceinline__ int long_pos(int u, int s, int h)
-{
-    int k = u + 64 * s;
+    int s = o >> 1, h = o & 1, k = u + 64 * s;
     if (s < 4) return h ? 512 + 2 * k : 511 - 2 * k;
     return h ? 1535 - 2 * k : 2 * k - 512;
+}
+
+// Math.round(float) (ties toward +inf, NaN -> 0) then the short clamp of SampleBuffer.accept
+// (S/SampleBuffer.java:193-206).  floor/sub/compare are exact; v_cvt_i32_f32 maps NaN to 0
+// and saturates out-of-range values.
+__device__ __forceinline__ int java_round16(float x)
+{
+    float y = __builtin_floorf(x);
+    float r = (x - y >= 0.5f) ? y + 1.0f : y;
+    int v;
+    asm("v_cvt_i32_f32 %0, %1" : "=v"(v) : "v"(r));
+    return v < -32768 ? -32768 : (v > 32767 ? 32767 : v);
 }
 
 struct FrameCtx {
@@ -146,54 +160,56 @@ struct FrameCtx {
 };
 
 // ------------------------------------------------------------------------------------------
-// IMDCT (MDCT.process, N = 2048) + FilterBank window/overlap-add for long window sequences.
-// Reads the channel spectrum from lw.buf, updates ov[] (overlap at long_pos), writes out[].
+// IMDCT N = 2048 (MDCT.process): lane u holds k = u + 64 s.  Reads the spectrum from buf.
 // ------------------------------------------------------------------------------------------
-__device__ __forceinline__ void imdct_long(LdsWave& lw, const LdsTables& T, float (&re)[8], float (&im)[8])
+__device__ __forceinline__ void imdct_long(float* buf, const LdsTables& T, int u, float (&re)[8], float (&im)[8])
 {
-    const int u = lane_id();
-    // pre-IFFT complex multiplication (MDCT.java:39-42) for k = u + 64 s
 #pragma unroll
     for (int s = 0; s < 8; s++) {
         int k = u + 64 * s;
-        float in0 = lw.buf[2 * k];
-        float in1 = lw.buf[1023 - 2 * k];
+        float in0 = buf[eo_idx(2 * k)];
+        float in1 = buf[eo_idx(1023 - 2 * k)];
         float c = T.mdct_l[k][0], sn = T.mdct_l[k][1];
-        im[s] = (in0 * c) + (in1 * sn);
+        im[s] = (in0 * c) + (in1 * sn);  // MDCT.java:39-42
         re[s] = (in1 * c) - (in0 * sn);
     }
     wave_sync();
-    // pass 1: this lane is logical FFT row t = bitrev6(u): rev[8t+r] = buf[u + 64*bitrev3(r)]
-    fft_pass1(re, im, T.roots_l, 64);
-    float2* X = reinterpret_cast<float2*>(lw.buf);
+    // pass 1: this lane is bit-reversed row t = bitrev6(u): rev[8t+r] = buf[u + 64*bitrev3(r)]
+    fft_pass1(re, im, T.tw1, 1);
+    float2* X = reinterpret_cast<float2*>(buf);
     const int t = (int)(__builtin_bitreverse32((uint32_t)u) >> 26);
 #pragma unroll
-    for (int r = 0; r < 8; r++) X[8 * t + r] = make_float2(re[BR3[r]], im[BR3[r]]);
+    for (int r = 0; r < 8; r++) X[xs(8 * t + r)] = make_float2(re[BR3[r]], im[BR3[r]]);
     wave_sync();
-    // pass 2: elements 64a + b + 8s, stages i = 8, 16, 32 (m = 32, 16, 8)
+    // pass 2: elements 64a + b + 8s, stages i = 8, 16, 32
     const int a = u >> 3, b = u & 7;
 #pragma unroll
     for (int s = 0; s < 8; s++) {
-        float2 v = X[64 * a + b + 8 * s];
+        float2 v = X[xs(64 * a + b + 8 * s)];
         re[s] = v.x;
         im[s] = v.y;
     }
-    fft_pass3stages(re, im, T.roots_l, b, 8, 32);
+    fft_3stages(re, im, [&](int j, float& wr, float& wi) {
+        wr = T.tw2[j][b][0];
+        wi = T.tw2[j][b][1];
+    });
 #pragma unroll
-    for (int s = 0; s < 8; s++) X[64 * a + b + 8 * s] = make_float2(re[s], im[s]);
+    for (int s = 0; s < 8; s++) X[xs(64 * a + b + 8 * s)] = make_float2(re[s], im[s]);
     wave_sync();
-    // pass 3: elements u + 64 s, stages i = 64, 128, 256 (m = 4, 2, 1)
+    // pass 3: elements u + 64 s, stages i = 64, 128, 256
 #pragma unroll
     for (int s = 0; s < 8; s++) {
-        float2 v = X[u + 64 * s];
+        float2 v = X[xs(u + 64 * s)];
         re[s] = v.x;
         im[s] = v.y;
     }
     wave_sync();
-    fft_pass3stages(re, im, T.roots_l, u, 64, 4);
-    // post-IFFT complex multiplication (MDCT.java:48-53)
+    fft_3stages(re, im, [&](int j, float& wr, float& wi) {
+        wr = T.tw3[j][u][0];
+        wi = T.tw3[j][u][1];
+    });
 #pragma unroll
-    for (int s = 0; s < 8; s++) {
+    for (int s = 0; s < 8; s++) {  // MDCT.java:48-53
         int k = u + 64 * s;
         float c = T.mdct_l[k][0], sn = T.mdct_l[k][1];
         float t0 = re[s], t1 = im[s];
@@ -202,22 +218,22 @@ __device__ __forceinline__ void imdct_long(LdsWave& lw, const LdsTables& T, floa
     }
 }
 
-// FilterBank.process for ONLY_LONG / LONG_START / LONG_STOP (FilterBank.java:41-70, 102-119)
-__device__ __forceinline__ void ola_long(const LdsTables& T, const FrameCtx& fc, const float (&re)[8],
+// FilterBank.process for ONLY_LONG / LONG_START / LONG_STOP (FilterBank.java:41-70, 102-119).
+// Lane u's slot (s,h) holds output position P = long_pos(u, 2s+h); its mirror 1023-P is slot
+// (s,1-h) of the same lane, so the falling window W[1023-P] is win_slot[shape][o^1][u].
+__device__ __forceinline__ void ola_long(const LdsTables& T, int, const FrameCtx& fc, const float (&re)[8],
                                          const float (&im)[8], float (&ov)[16], float (&out)[16])
 {
     const int u = lane_id();
-    const float* LWp = T.win_long[fc.shape_prev];
-    const float* LWc = T.win_long[fc.shape];
     const float* SWp = T.win_short[fc.shape_prev];
     const float* SWc = T.win_short[fc.shape];
 #pragma unroll
     for (int s = 0; s < 8; s++) {
 #pragma unroll
         for (int h = 0; h < 2; h++) {
-            const int P = long_pos(u, s, h);
-            // first-half (buf[P]) and second-half (buf[1024+P]) IMDCT samples of this slot
-            float f, g;
+            const int o = 2 * s + h;
+            const int P = long_pos(u, o);
+            float f, g;  // IMDCT samples buf[P] and buf[1024+P]
             if (s < 4) {
                 f = h ? re[s] : -re[s];
                 g = -im[s];
@@ -225,21 +241,20 @@ __device__ __forceinline__ void ola_long(const LdsTables& T, const FrameCtx& fc,
                 f = h ? -im[s] : im[s];
                 g = re[s];
             }
-            const int o = 2 * s + h;
             float o_v, n_v;
             if (fc.seq == JAAD_LONG_STOP_SEQUENCE) {
                 if (P < 448) o_v = ov[o];
                 else if (P < 576) o_v = ov[o] + (f * SWp[P - 448]);
                 else o_v = ov[o] + f;
             } else {
-                o_v = ov[o] + (f * LWp[P]);
+                o_v = ov[o] + (f * T.win_slot[fc.shape_prev][o][u]);
             }
             if (fc.seq == JAAD_LONG_START_SEQUENCE) {
                 if (P < 448) n_v = g;
                 else if (P < 576) n_v = g * SWc[127 - (P - 448)];
                 else n_v = 0.0f;
             } else {
-                n_v = g * LWc[1023 - P];
+                n_v = g * T.win_slot[fc.shape][o ^ 1][u];
             }
             out[o] = o_v;
             ov[o] = n_v;
@@ -251,34 +266,38 @@ __device__ __forceinline__ void ola_long(const LdsTables& T, const FrameCtx& fc,
 // EIGHT_SHORT_SEQUENCE: 8 x MDCT(256) (64-point IFFTs), FilterBank.java:71-101.
 // Lane (w = u>>3, b = u&7) holds window w's elements b + 8s.
 // ------------------------------------------------------------------------------------------
-__device__ __forceinline__ void imdct_short(LdsWave& lw, const LdsTables& T, float (&re)[8], float (&im)[8])
+__device__ __forceinline__ void imdct_short(float* buf, const LdsTables& T, int u, float (&re)[8], float (&im)[8])
 {
-    const int u = lane_id();
     const int w = u >> 3, b = u & 7;
 #pragma unroll
     for (int s = 0; s < 8; s++) {
         int k = b + 8 * s;
-        float in0 = lw.buf[128 * w + 2 * k];
-        float in1 = lw.buf[128 * w + 127 - 2 * k];
+        float in0 = buf[eo_idx(128 * w + 2 * k)];
+        float in1 = buf[eo_idx(128 * w + 127 - 2 * k)];
         float c = T.mdct_s[k][0], sn = T.mdct_s[k][1];
         im[s] = (in0 * c) + (in1 * sn);
         re[s] = (in1 * c) - (in0 * sn);
     }
     wave_sync();
     fft_pass1(re, im, T.roots_s, 8);
-    float2* X = reinterpret_cast<float2*>(lw.buf);
+    float2* X = reinterpret_cast<float2*>(buf);
     const int t = (int)(__builtin_bitreverse32((uint32_t)b) >> 29);
 #pragma unroll
-    for (int r = 0; r < 8; r++) X[64 * w + 8 * t + r] = make_float2(re[BR3[r]], im[BR3[r]]);
+    for (int r = 0; r < 8; r++) X[xs(64 * w + 8 * t + r)] = make_float2(re[BR3[r]], im[BR3[r]]);
     wave_sync();
 #pragma unroll
     for (int s = 0; s < 8; s++) {
-        float2 v = X[64 * w + b + 8 * s];
+        float2 v = X[xs(64 * w + b + 8 * s)];
         re[s] = v.x;
         im[s] = v.y;
     }
     wave_sync();
-    fft_pass3stages(re, im, T.roots_s, b, 8, 4);
+    // stages i = 8, 16, 32 of the 64-point IFFT: roots[k*m], m = 4, 2, 1
+    fft_3stages(re, im, [&](int j, float& wr, float& wi) {
+        int idx = j == 0 ? 4 * b : (j < 3 ? 2 * (b + 8 * (j - 1)) : b + 8 * (j - 3));
+        wr = T.roots_s[idx][0];
+        wi = T.roots_s[idx][1];
+    });
 #pragma unroll
     for (int s = 0; s < 8; s++) {
         int k = b + 8 * s;
@@ -307,79 +326,70 @@ __device__ __forceinline__ void short_slot(int b, int s, int j, const float (&re
     }
 }
 
-// Overlap-add of the 8 short windows in Java's evaluation order ((ov + A) + B, A = previous
-// window's falling half, B = this window's rising half) through an LDS time buffer, in two
-// halves of 576 samples (out: t in [448,1024), new overlap: t in [1024,1600)).
-__device__ __forceinline__ void ola_short(LdsWave& lw, const LdsTables& T, const FrameCtx& fc, const float (&re)[8],
-                                          const float (&im)[8], float (&ov)[16], float (&out)[16])
+// Overlap-add of the 8 short windows in Java's evaluation order (FilterBank.java:76-100):
+// out = (ov + A) + B and new overlap = A + B, where A is window m-1's windowed falling half and
+// B window m's windowed rising half at the same time index.  Two LDS phases: all falling halves
+// (A terms) are written and gathered per owned position, then all rising halves (B terms).
+__device__ __forceinline__ void ola_short(float* Tb, const LdsTables& T, int u, const FrameCtx& fc,
+                                          const float (&re)[8], const float (&im)[8], float (&ov)[16],
+                                          float (&out)[16])
 {
-    const int u = lane_id();
     const int w = u >> 3, b = u & 7;
     const float* SWc = T.win_short[fc.shape];
     const float* SWr = T.win_short[w == 0 ? fc.shape_prev : fc.shape];
-    float* Tb = lw.buf;
+    float nv[16];
 #pragma unroll
-    for (int half = 0; half < 2; half++) {
-        const int t0 = half ? 1024 : 448;
-        // init: out half <- overlap, overlap half <- -0.0 (so that -0 + A == A exactly)
-        if (half == 0) {
+    for (int phase = 0; phase < 2; phase++) {  // 0: falling halves (A), 1: rising halves (B)
 #pragma unroll
-            for (int o = 0; o < 16; o++) {
-                int P = long_pos(u, o >> 1, o & 1);
-                if (P >= 448) Tb[P - 448] = ov[o];
+        for (int s = 0; s < 8; s++) {
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                int n;
+                float v;
+                short_slot(b, s, j, re, im, n, v);
+                if ((n < 128) != (phase == 1)) continue;  // j = 0,1 rising; j = 2,3 falling (compile-time)
+                if (phase == 0) Tb[128 * w + (n - 128)] = v * SWc[255 - n];
+                else Tb[128 * w + n] = v * SWr[n];
             }
-        } else {
-#pragma unroll
-            for (int i = 0; i < 9; i++) Tb[u + 64 * i] = -0.0f;
         }
         wave_sync();
-#pragma unroll
-        for (int phase = 0; phase < 2; phase++) {  // 0: falling halves (A), 1: rising halves (B)
-#pragma unroll
-            for (int s = 0; s < 8; s++) {
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    int n;
-                    float v;
-                    short_slot(b, s, j, re, im, n, v);
-                    const bool rising = n < 128;
-                    if (rising != (phase == 1)) continue;
-                    int t = 448 + 128 * w + n;
-                    if ((t >= 1024) != (half == 1)) continue;
-                    float c = rising ? v * SWr[n] : v * SWc[255 - n];
-                    Tb[t - t0] = Tb[t - t0] + c;
-                }
-            }
-            wave_sync();
-        }
+        const int uu = lane_id();  // opaque: stop index math being hoisted/kept across phases
 #pragma unroll
         for (int o = 0; o < 16; o++) {
-            int P = long_pos(u, o >> 1, o & 1);
-            if (half == 0) out[o] = (P >= 448) ? Tb[P - 448] : ov[o];
-            else ov[o] = (P < 576) ? Tb[P] : 0.0f;
+            const int P = long_pos(uu, o);
+            // output sample t = P: window m = (P-448)>>7, offset i; overlap sample t = 1024+P
+            const int mo = (P - 448) >> 7, io = (P - 448) & 127;
+            const int mq = (P + 576) >> 7, iq = (P + 576) & 127;
+            if (phase == 0) {
+                out[o] = (P >= 448 + 128) ? ov[o] + Tb[128 * (mo - 1) + io] : ov[o];
+                nv[o] = (mq <= 8) ? Tb[128 * (mq - 1) + iq] : 0.0f;
+            } else {
+                if (P >= 448) out[o] = out[o] + Tb[128 * mo + io];
+                if (mq <= 7) nv[o] = nv[o] + Tb[128 * mq + iq];
+            }
         }
         wave_sync();
     }
+#pragma unroll
+    for (int o = 0; o < 16; o++) ov[o] = nv[o];
 }
 
 // ------------------------------------------------------------------------------------------
-// TNS, spec mode (ISO/IEC 14496-3 4.6.9.3), in place on lw.buf; one lane per filter.
+// TNS, spec mode (ISO/IEC 14496-3 4.6.9.3), in place on the spectrum; one lane per filter.
 // The reference parses TNS (A/tools/TNS.java:35-61) but its process() is a no-op.
 // ------------------------------------------------------------------------------------------
-__device__ void tns_spec(LdsWave& lw, const LdsTables& T, const jaad_ics_info& info, const jaad_tns* tp)
+__device__ void tns_spec(float* buf, float* scratch, const LdsTables& T, int u, const jaad_ics_info& info,
+                         const jaad_tns* tp)
 {
-    const int u = lane_id();
     const bool is_short = info.window_sequence == JAAD_EIGHT_SHORT_SEQUENCE;
     const int nswb = is_short ? T.nswb_s : T.nswb_l;
     const int16_t* offs = is_short ? T.swb_s : T.swb_l;
     const int tns_max = is_short ? T.tns_max_s : T.tns_max_l;
     const int nf = tp->n_filters;
-    float* scratch = &lw.gain[0][0];  // 384 floats: 8 filters x 48 (band info is dead here)
     if (u < nf && u < 8) {
         const jaad_tns_filter& F = tp->filt[u];
-        // top/bottom band of this filter: walk the filters of the same window parsed before it
         int top = nswb, bottom = nswb;
-        for (int f = 0; f <= u; f++) {
+        for (int f = 0; f <= u; f++) {  // walk this window's filters parsed before this one
             const jaad_tns_filter& G = tp->filt[f];
             if (G.window != F.window) continue;
             top = bottom;
@@ -387,13 +397,14 @@ __device__ void tns_spec(LdsWave& lw, const LdsTables& T, const jaad_ics_info& i
             if (bottom < 0) bottom = 0;
         }
         const int order = F.order > 20 ? 20 : F.order;
-        float* a = scratch + 48 * u;  // a[0..20], b[21..41], tmp2 -> reuse b region
+        float* a = scratch + 24 * u;  // a[0..20]
+        float bb[21];
         const float* tab = T.tns_coef[2 * ((F.flags >> 2) & 1) + ((F.flags >> 1) & 1)];
         a[0] = 1.0f;
         for (int m = 1; m <= order; m++) {
             float tm = -tab[F.coef[m - 1] & 15];
-            for (int i = 1; i < m; i++) a[21 + i] = a[i] + tm * a[m - i];
-            for (int i = 1; i < m; i++) a[i] = a[21 + i];
+            for (int i = 1; i < m; i++) bb[i] = a[i] + tm * a[m - i];
+            for (int i = 1; i < m; i++) a[i] = bb[i];
             a[m] = tm;
         }
         int s = bottom < tns_max ? bottom : tns_max;
@@ -408,14 +419,14 @@ __device__ void tns_spec(LdsWave& lw, const LdsTables& T, const jaad_ics_info& i
                 inc = -1;
                 start = end - 1;
             }
-            float* x = lw.buf + (is_short ? 128 * F.window : 0) + start;
+            const int base = (is_short ? 128 * F.window : 0) + start;
             for (int n = 0; n < size; n++) {
-                float y = x[n * inc];
+                float y = buf[eo_idx(base + n * inc)];
                 for (int j = 0; j < order; j++) {
-                    float st = (n - 1 - j >= 0) ? x[(n - 1 - j) * inc] : 0.0f;
+                    float st = (n - 1 - j >= 0) ? buf[eo_idx(base + (n - 1 - j) * inc)] : 0.0f;
                     y -= st * a[j + 1];
                 }
-                x[n * inc] = y;
+                buf[eo_idx(base + n * inc)] = y;
             }
         }
     }
@@ -425,9 +436,9 @@ __device__ void tns_spec(LdsWave& lw, const LdsTables& T, const jaad_ics_info& i
 // ------------------------------------------------------------------------------------------
 // PNS slow path (ICStream.java:241-257): lane 0 replays the static LCG in parse order.
 // ------------------------------------------------------------------------------------------
-__device__ void pns_fill(LdsWave& lw, const LdsTables& T, const jaad_ics_info& info, int c, const uint8_t* cbrow)
+__device__ void pns_fill(float* buf, const PairBands& pb, int bc, const LdsTables& T, int u, const jaad_ics_info& info)
 {
-    if (lane_id() == 0) {
+    if (u == 0) {
         const bool is_short = info.window_sequence == JAAD_EIGHT_SHORT_SEQUENCE;
         const int16_t* offs = is_short ? T.swb_s : T.swb_l;
         int glen[8], ng = 1;
@@ -441,20 +452,20 @@ __device__ void pns_fill(LdsWave& lw, const LdsTables& T, const jaad_ics_info& i
         const int maxSFB = info.max_sfb;
         for (int g = 0, idx = 0, groupOff = 0; g < ng; g++) {
             for (int sfb = 0; sfb < maxSFB; sfb++, idx++) {
-                if (cbrow[idx] != JAAD_NOISE_HCB) continue;
+                if (pb.cb[bc][idx] != JAAD_NOISE_HCB) continue;
                 int off = groupOff + offs[sfb];
                 int width = offs[sfb + 1] - offs[sfb];
-                float sfv = lw.gain[c][idx];
+                float sfv = pb.gain[bc][idx];
                 for (int w = 0; w < glen[g]; w++, off += 128) {
                     float energy = 0.0f;
                     for (int k = 0; k < width; k++) {
                         rs = 1664525u * rs + 1013904223u;
                         float v = (float)(int32_t)rs;
-                        lw.buf[off + k] = v;
+                        buf[eo_idx(off + k)] = v;
                         energy += v * v;
                     }
                     float scale = (float)((double)sfv / sqrt((double)energy));
-                    for (int k = 0; k < width; k++) lw.buf[off + k] *= scale;
+                    for (int k = 0; k < width; k++) buf[eo_idx(off + k)] *= scale;
                 }
             }
             groupOff += glen[g] << 7;
@@ -463,7 +474,7 @@ __device__ void pns_fill(LdsWave& lw, const LdsTables& T, const jaad_ics_info& i
     wave_sync();
 }
 
-// band index of the quad of bins starting at position p (4-aligned) for this ICS, or -1
+// band index (g*max_sfb + sfb) of the bin quad starting at position p (4-aligned), or -1
 __device__ __forceinline__ int band_of(const LdsTables& T, const jaad_ics_info& info, int p)
 {
     int sfb, g = 0;
@@ -478,24 +489,54 @@ __device__ __forceinline__ int band_of(const LdsTables& T, const jaad_ics_info& 
     return g * info.max_sfb + sfb;
 }
 
-__device__ __forceinline__ float iq_value(const LdsTables& T, const float* __restrict__ iq_table, int qv, float gain)
+// lane u's 16 spectral bins p = 8u + 512h + i (h = 0,1; i = 0..7) <-> buf (E/O layout), as
+// four float4 accesses (bins 8u+512h+{0,2,4,6} and {1,3,5,7})
+__device__ __forceinline__ void store_spec(float* buf, int u, const float (&x)[16])
 {
-    int a = qv < 0 ? -qv : qv;
-    float m = a < 128 ? T.iq_head[a] : iq_table[a > 8190 ? 8190 : a];
-    float x = m * gain;  // (q>0 ? IQ[q] : -IQ[-q]) * sf  ==  +-(IQ[|q|] * sf) exactly (q = 0 -> -0)
-    return qv > 0 ? x : -x;
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        const int p = 8 * u + 512 * h;
+        *reinterpret_cast<float4*>(&buf[eo_idx(p)]) = make_float4(x[8 * h], x[8 * h + 2], x[8 * h + 4], x[8 * h + 6]);
+        *reinterpret_cast<float4*>(&buf[eo_idx(p + 1)]) =
+            make_float4(x[8 * h + 1], x[8 * h + 3], x[8 * h + 5], x[8 * h + 7]);
+    }
+}
+__device__ __forceinline__ void load_spec(const float* buf, int u, float (&x)[16])
+{
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        const int p = 8 * u + 512 * h;
+        float4 e = *reinterpret_cast<const float4*>(&buf[eo_idx(p)]);
+        float4 o = *reinterpret_cast<const float4*>(&buf[eo_idx(p + 1)]);
+        x[8 * h + 0] = e.x; x[8 * h + 2] = e.y; x[8 * h + 4] = e.z; x[8 * h + 6] = e.w;
+        x[8 * h + 1] = o.x; x[8 * h + 3] = o.y; x[8 * h + 5] = o.z; x[8 * h + 7] = o.w;
+    }
 }
 
-#ifndef JAAD_WAVES_PER_EU
-#define JAAD_WAVES_PER_EU 2
-#endif
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
+
+struct Prefetch {
+    v4i q[2];      // own channel bins 8u+512h .. +7
+    uint32_t sfcb;  // lane u < 32: sf bytes 4u..4u+3; lane u >= 32: cb bytes 4(u-32)..
+};
+
+__device__ __forceinline__ void prefetch(const KernelArgs& A, size_t cf, int u, Prefetch& pf)
+{
+    const v4i* q = reinterpret_cast<const v4i*>(A.q + cf * 1024);
+    pf.q[0] = __builtin_nontemporal_load(q + u);
+    pf.q[1] = __builtin_nontemporal_load(q + 64 + u);
+    const uint32_t* row = reinterpret_cast<const uint32_t*>(u < 32 ? A.sf + cf * 128 : A.cb + cf * 128);
+    pf.sfcb = row[u & 31];
+}
+
 template <bool kTnsSpec, int kOut>
-__global__ __launch_bounds__(kWGThreads, JAAD_WAVES_PER_EU) void lc_decode_kernel(KernelArgs A)
+__global__ __launch_bounds__(kWGThreads, kTnsSpec ? 2 : JAAD_WAVES_PER_EU) void lc_decode_kernel(KernelArgs A)
 {
     __shared__ LdsTables T;
-    __shared__ LdsWave W[kWavesPerWG];
+    __shared__ float Wb[kWavesPerWG][1024];
+    __shared__ PairBands PB[kWavesPerWG / 2];
 
-    // stage the constant tables (one coalesced copy per workgroup)
     {
         const uint4* src = reinterpret_cast<const uint4*>(A.tables);
         uint4* dst = reinterpret_cast<uint4*>(&T);
@@ -503,239 +544,262 @@ __global__ __launch_bounds__(kWGThreads, JAAD_WAVES_PER_EU) void lc_decode_kerne
     }
     __syncthreads();
 
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int u = lane_id();
-    LdsWave& lw = W[wave];
-    const int nch = A.nch;
     constexpr bool big_endian = !(kOut & JAAD_PCM_LITTLE_ENDIAN);
     constexpr bool out_f32 = (kOut & JAAD_PCM_FLOAT32) != 0;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const bool stereo = A.nch == 2;
+    const int c = stereo ? (wave & 1) : 0;  // channel of this wave
+    const int bc = wave & 1;                // channel slot in the PairBands record
+    PairBands& pb = PB[wave >> 1];
+    float* buf = Wb[wave];
+    const int per_wg = stereo ? kWavesPerWG / 2 : kWavesPerWG;
+    const int my_idx = stereo ? (wave >> 1) : wave;
+    const int nch = stereo ? 2 : 1;
 
-    for (uint32_t ci = blockIdx.x * kWavesPerWG + wave; ci < A.n_chunks; ci += gridDim.x * kWavesPerWG) {
-        const ChunkDesc cd = A.chunks[ci];
+    for (uint32_t g = blockIdx.x; g * per_wg < A.n_chunks; g += gridDim.x) {
+        // iteration count shared by the whole workgroup (barriers must match)
+        int n_iter = 0;
+        for (int j = 0; j < per_wg; j++) {
+            uint32_t cj = g * per_wg + j;
+            if (cj < A.n_chunks) {
+                uint32_t inf = A.chunks[cj].info;
+                int n = (int)(inf & 0xffff) + ((inf & kChunkPrefix) ? 1 : 0);
+                n_iter = n > n_iter ? n : n_iter;
+            }
+        }
+        const uint32_t ci = g * per_wg + my_idx;
+        ChunkDesc cd{0, 0, 0, 0};
+        if (ci < A.n_chunks) cd = A.chunks[ci];
         const int nfr = cd.info & 0xffff;
         const bool prefix = (cd.info & kChunkPrefix) != 0;
-        float ovL[16], ovR[16];
-        if (cd.info & kChunkLoadState) {
-            const float* st = A.state_in + (size_t)cd.slot * 2048;
-#pragma unroll
-            for (int o = 0; o < 16; o++) {
-                int P = long_pos(u, o >> 1, o & 1);
-                ovL[o] = st[P];
-                ovR[o] = st[1024 + P];
-            }
-        } else {
-#pragma unroll
-            for (int o = 0; o < 16; o++) ovL[o] = ovR[o] = 0.0f;
-        }
+        const int my_n = nfr + (prefix ? 1 : 0);
         const int f_first = (int)cd.frame0 - (prefix ? 1 : 0);
-        const int f_end = (int)cd.frame0 + nfr;
-        for (int f = f_first; f < f_end; f++) {
-            const bool emit = f >= (int)cd.frame0;
-            const size_t cf0 = (size_t)f * nch;
-            const jaad_ics_info iL = A.ics[cf0];
-            const jaad_ics_info iR = nch == 2 ? A.ics[cf0 + 1] : iL;
 
-            // ---- per-band side info -> LDS (gain as ICStream.scaleFactors holds it, codebooks, ms bit)
+        float ov[16];
+        {
+            const int u = lane_id();
+            if (cd.info & kChunkLoadState) {
+                const float* st = A.state_in + (size_t)cd.slot * 2048 + 1024 * c;
 #pragma unroll
-            for (int hb = 0; hb < 2; hb++) {
-                const int idx = u + 64 * hb;
-                uint32_t code = 0;
+                for (int o = 0; o < 16; o++) ov[o] = st[long_pos(u, o)];
+            } else {
 #pragma unroll
-                for (int c = 0; c < 2; c++) {
-                    if (c >= nch) break;
-                    const jaad_ics_info& ic = c ? iR : iL;
-                    const int ng = ic.window_sequence == JAAD_EIGHT_SHORT_SEQUENCE ? 8 - __builtin_popcount(ic.grouping & 0x7f) : 1;
-                    if (idx < ng * ic.max_sfb) {
-                        const size_t row = (cf0 + c) * 128 + idx;
-                        uint32_t cbv = A.cb[row];
-                        float g = T.sf_gain[A.sf[row]];
-                        lw.gain[c][idx] = cbv == JAAD_NOISE_HCB ? -g : g;
-                        code |= (cbv & 15u) << (4 * c);
-                    }
-                }
-                if (nch == 2 && (iL.flags & JAAD_ICS_MS_PRESENT) && A.ms_used)
-                    code |= (uint32_t)((A.ms_used[(size_t)f * 2 + (idx >> 6)] >> (idx & 63)) & 1u) << 8;
-                lw.code[idx] = code;
+                for (int o = 0; o < 16; o++) ov[o] = 0.0f;
             }
-            wave_sync();
+        }
+        Prefetch pf;
+        if (my_n > 0) prefetch(A, (size_t)f_first * nch + c, lane_id(), pf);
 
-            // ---- inverse quantisation: lane owns bins 8u+512h+i (h = 0,1; i = 0..7), i.e. four band quads
-            float x[2][16];
-            int bidx[2][4];
+        for (int it = 0; it < n_iter; it++) {
+            const int u = lane_id();
+            const bool active = it < my_n;
+            const int f = f_first + it;
+            const bool emit = active && f >= (int)cd.frame0;
+            const size_t cf0 = (size_t)(active ? f : 0) * nch;
+            jaad_ics_info ic{}, iL{}, iR{};
+            bool ms_on = false, is_on = false, xchg = false;
+            float x[16];
+
+            // ---------------- phase A: side info, inverse quantisation, PNS ----------------
+            if (active) {
+                iL = A.ics[cf0];
+                iR = stereo ? A.ics[cf0 + 1] : iL;
+                ic = c ? iR : iL;
+                ms_on = stereo && (iL.flags & JAAD_ICS_COMMON_WINDOW) && (iL.flags & JAAD_ICS_MS_PRESENT);
+                is_on = stereo && (iR.flags & JAAD_ICS_HAS_IS);
+                xchg = ms_on || is_on;
+                // raw sf/cb rows of this channel -> pair record
+                reinterpret_cast<uint32_t*>(u < 32 ? pb.sf[bc] : pb.cb[bc])[u & 31] = pf.sfcb;
+                const Prefetch cur = pf;
+                if (it + 1 < my_n) prefetch(A, cf0 + nch + c, u, pf);
+                if (stereo && c == 0) {
+                    uint64_t m0 = 0, m1 = 0;
+                    if (ms_on && A.ms_used) {
+                        m0 = A.ms_used[(size_t)f * 2];
+                        m1 = A.ms_used[(size_t)f * 2 + 1];
+                    }
+                    pb.ms[u] = (uint8_t)((m0 >> u) & 1u);
+                    pb.ms[u + 64] = (uint8_t)((m1 >> u) & 1u);
+                }
+                wave_sync();
 #pragma unroll
-            for (int c = 0; c < 2; c++) {
-                if (c >= nch) break;
-                const jaad_ics_info& ic = c ? iR : iL;
+                for (int hb = 0; hb < 2; hb++) {
+                    const int idx = u + 64 * hb;
+                    const uint32_t cbv = pb.cb[bc][idx];
+                    const float gv = T.sf_gain[pb.sf[bc][idx]];
+                    pb.gain[bc][idx] = cbv == JAAD_NOISE_HCB ? -gv : gv;
+                }
+                wave_sync();
+                // inverse quantisation (ICStream.java:258-271): lane owns bins 8u+512h+i
+                int amax = 0;
 #pragma unroll
                 for (int h = 0; h < 2; h++) {
-                    const int4 qv4 = *reinterpret_cast<const int4*>(A.q + (cf0 + c) * 1024 + 512 * h + 8 * u);
-                    const int16_t* qv = reinterpret_cast<const int16_t*>(&qv4);
+                    const int16_t* qv = reinterpret_cast<const int16_t*>(&cur.q[h]);
 #pragma unroll
                     for (int j = 0; j < 2; j++) {
                         const int bi = band_of(T, ic, 512 * h + 8 * u + 4 * j);
-                        bidx[c][2 * h + j] = bi;
-                        const uint32_t cbv = bi >= 0 ? (lw.code[bi] >> (4 * c)) & 15u : 0u;
-                        const float g = bi >= 0 ? lw.gain[c][bi] : 0.0f;
-                        const bool spectral = cbv != JAAD_ZERO_HCB && cbv != JAAD_NOISE_HCB &&
-                                              cbv != JAAD_INTENSITY_HCB && cbv != JAAD_INTENSITY_HCB2;
+                        const uint32_t cbv = bi >= 0 ? pb.cb[bc][bi] : 0u;
+                        const float gn = bi >= 0 ? pb.gain[bc][bi] : 0.0f;
+                        const bool spectral = cbv != JAAD_ZERO_HCB && cbv < JAAD_NOISE_HCB;
 #pragma unroll
-                        for (int i = 0; i < 4; i++)
-                            x[c][8 * h + 4 * j + i] = spectral ? iq_value(T, A.iq_table, qv[4 * j + i], g) : 0.0f;
+                        for (int i = 0; i < 4; i++) {
+                            const int qq = qv[4 * j + i];
+                            const int aq = qq < 0 ? -qq : qq;
+                            amax = aq > amax ? aq : amax;
+                            const float m = T.iq_head[aq & 127] * gn;  // escapes fixed below
+                            x[8 * h + 4 * j + i] = spectral ? (qq > 0 ? m : -m) : 0.0f;  // q=0 -> -0
+                        }
                     }
                 }
-            }
-            // ---- PNS (rare): fill noise bands through LDS
+                if (__ballot(amax >= 128)) {  // escape values beyond the LDS head of IQ_TABLE
 #pragma unroll
-            for (int c = 0; c < 2; c++) {
-                if (c >= nch) break;
-                const jaad_ics_info& ic = c ? iR : iL;
-                if (ic.flags & JAAD_ICS_HAS_PNS) {
+                    for (int h = 0; h < 2; h++) {
+                        const int16_t* qv = reinterpret_cast<const int16_t*>(&cur.q[h]);
 #pragma unroll
-                    for (int i = 0; i < 16; i++) lw.buf[8 * u + 512 * (i >> 3) + (i & 7)] = x[c][i];
-                    wave_sync();
-                    pns_fill(lw, T, ic, c, A.cb + (cf0 + c) * 128);
-#pragma unroll
-                    for (int i = 0; i < 16; i++) x[c][i] = lw.buf[8 * u + 512 * (i >> 3) + (i & 7)];
-                    wave_sync();
-                }
-            }
-            if (nch == 2) {
-                // ---- M/S (MS.java:17-41): common window, mask present, both codebooks < NOISE_HCB
-                if ((iL.flags & JAAD_ICS_COMMON_WINDOW) && (iL.flags & JAAD_ICS_MS_PRESENT)) {
-#pragma unroll
-                    for (int h = 0; h < 4; h++) {
-                        const int bi = bidx[0][h];
-                        const uint32_t code = bi >= 0 ? lw.code[bi] : 0u;
-                        if (bi >= 0 && (code & 0x100u) && (code & 15u) < JAAD_NOISE_HCB && ((code >> 4) & 15u) < JAAD_NOISE_HCB) {
+                        for (int j = 0; j < 2; j++) {
+                            const int bi = band_of(T, ic, 512 * h + 8 * u + 4 * j);
+                            const uint32_t cbv = bi >= 0 ? pb.cb[bc][bi] : 0u;
+                            const float gn = bi >= 0 ? pb.gain[bc][bi] : 0.0f;
+                            const bool spectral = cbv != JAAD_ZERO_HCB && cbv < JAAD_NOISE_HCB;
 #pragma unroll
                             for (int i = 0; i < 4; i++) {
-                                float l = x[0][4 * h + i], r = x[1][4 * h + i];
-                                float tt = l - r;
-                                x[0][4 * h + i] = l + r;
-                                x[1][4 * h + i] = tt;
+                                const int qq = qv[4 * j + i];
+                                const int aq = qq < 0 ? -qq : qq;
+                                if (aq >= 128 && spectral) {
+                                    const float m = A.iq_table[aq > 8190 ? 8190 : aq] * gn;
+                                    x[8 * h + 4 * j + i] = qq > 0 ? m : -m;
+                                }
                             }
                         }
                     }
                 }
-                // ---- I/S (IS.java:17-53), right channel's bands
-                if (iR.flags & JAAD_ICS_HAS_IS) {
-                    const bool msp = (iL.flags & JAAD_ICS_MS_PRESENT) != 0;
+                store_spec(buf, u, x);
+                if (ic.flags & JAAD_ICS_HAS_PNS) {
+                    wave_sync();
+                    pns_fill(buf, pb, bc, T, u, ic);
+                    load_spec(buf, u, x);
+                }
+            }
+            __syncthreads();  // B1: both channels' spectra + band records visible to the pair
+
+            // ---------------- phase C: M/S (MS.java:17-41) and I/S (IS.java:17-53) ----------------
+            if (active && xchg) {
+                float xp[16];
+                load_spec(Wb[wave ^ 1], u, xp);
 #pragma unroll
-                    for (int h = 0; h < 4; h++) {
-                        const int bi = bidx[1][h];
-                        const uint32_t code = bi >= 0 ? lw.code[bi] : 0u;
-                        const uint32_t cbr = (code >> 4) & 15u;
-                        if (bi >= 0 && (cbr == JAAD_INTENSITY_HCB || cbr == JAAD_INTENSITY_HCB2)) {
-                            int cs = cbr == JAAD_INTENSITY_HCB ? 1 : -1;
-                            if (msp) cs *= (code & 0x100u) ? -1 : 1;
-                            const float scale = (float)cs * lw.gain[1][bi];
+                for (int h = 0; h < 2; h++) {
 #pragma unroll
-                            for (int i = 0; i < 4; i++) x[1][4 * h + i] = x[0][4 * h + i] * scale;
+                    for (int j = 0; j < 2; j++) {
+                        const int p = 512 * h + 8 * u + 4 * j;
+                        if (ms_on) {
+                            const int bi = band_of(T, iL, p);
+                            if (bi >= 0 && pb.ms[bi] && pb.cb[0][bi] < JAAD_NOISE_HCB && pb.cb[1][bi] < JAAD_NOISE_HCB) {
+#pragma unroll
+                                for (int i = 0; i < 4; i++) {
+                                    const int e = 8 * h + 4 * j + i;
+                                    // t = L - R; L += R; R = t
+                                    x[e] = c == 0 ? x[e] + xp[e] : xp[e] - x[e];
+                                }
+                            }
+                        }
+                        if (is_on && c == 1) {
+                            const int bi = band_of(T, iR, p);
+                            const uint32_t cbr = bi >= 0 ? pb.cb[1][bi] : 0u;
+                            if (cbr == JAAD_INTENSITY_HCB || cbr == JAAD_INTENSITY_HCB2) {
+                                int cs = cbr == JAAD_INTENSITY_HCB ? 1 : -1;
+                                if (iL.flags & JAAD_ICS_MS_PRESENT) cs *= pb.ms[bi] ? -1 : 1;
+                                const float scale = (float)cs * pb.gain[1][bi];
+#pragma unroll
+                                for (int i = 0; i < 4; i++) x[8 * h + 4 * j + i] = xp[8 * h + 4 * j + i] * scale;
+                            }
                         }
                     }
                 }
             }
+            __syncthreads();  // B2: the partner has read this wave's spectrum
 
-            // ---- per channel: (TNS) -> IMDCT -> window/OLA -> PCM
-            uint32_t pk[16];   // int16 modes: (L | R << 16) per slot
-            float pf[2][16];   // f32 mode
-#pragma unroll
-            for (int c = 0; c < 2; c++) {
-                if (c >= nch) break;
-                const jaad_ics_info& ic = c ? iR : iL;
-                float(&ov)[16] = c ? ovR : ovL;
-#pragma unroll
-                for (int i = 0; i < 16; i++) lw.buf[8 * u + 512 * (i >> 3) + (i & 7)] = x[c][i];
+            // ---------------- phase D: (TNS) -> IMDCT -> window/OLA -> PCM into LDS ----------------
+            if (active) {
+                if (xchg) store_spec(buf, u, x);
                 wave_sync();
                 const bool dump = A.dbg && ci == 0 && f == (int)cd.frame0;
                 if (dump)
-                    for (int i = 0; i < 16; i++) A.dbg[1024 * c + 8 * u + 512 * (i >> 3) + (i & 7)] = x[c][i];
+                    for (int i = 0; i < 16; i++) {
+                        const int p = 8 * u + 512 * (i >> 3) + (i & 7);
+                        A.dbg[1024 * c + p] = buf[eo_idx(p)];
+                    }
                 if (kTnsSpec && A.tns_mode == JAAD_TNS_SPEC && (ic.flags & JAAD_ICS_TNS) && A.tns)
-                    tns_spec(lw, T, ic, A.tns + cf0 + c);
+                    tns_spec(buf, &pb.gain[bc][0], T, u, ic, A.tns + cf0 + c);
                 FrameCtx fc{ic.window_sequence, ic.window_shape, ic.window_shape_prev};
                 float re[8], im[8], out[16];
-#ifndef JAAD_EXP_NO_SHORT
                 if (fc.seq == JAAD_EIGHT_SHORT_SEQUENCE) {
-                    imdct_short(lw, T, re, im);
-                    ola_short(lw, T, fc, re, im, ov, out);
-                } else
-#endif
-                {
-                    imdct_long(lw, T, re, im);
+                    imdct_short(buf, T, u, re, im);
+                    ola_short(buf, T, u, fc, re, im, ov, out);
+                } else {
+                    imdct_long(buf, T, u, re, im);
                     if (dump)
                         for (int s2 = 0; s2 < 8; s2++) {
                             A.dbg[2048 + 1024 * c + 2 * (u + 64 * s2)] = re[s2];
                             A.dbg[2048 + 1024 * c + 2 * (u + 64 * s2) + 1] = im[s2];
                         }
-                    ola_long(T, fc, re, im, ov, out);
+                    ola_long(T, u, fc, re, im, ov, out);
                 }
                 wave_sync();
                 if (dump)
-                    for (int o = 0; o < 16; o++) A.dbg[4096 + 1024 * c + long_pos(u, o >> 1, o & 1)] = out[o];
+                    for (int o = 0; o < 16; o++) A.dbg[4096 + 1024 * c + long_pos(u, o)] = out[o];
                 if (emit) {
 #pragma unroll
                     for (int o = 0; o < 16; o++) {
-                        if constexpr (out_f32) {
-                            pf[c][o] = out[o];
-                        } else {
-                            uint32_t v = pack16(java_round16(out[o]), big_endian);
-                            pk[o] = c ? (pk[o] | (v << 16)) : v;
-                        }
+                        const int P = long_pos(u, o);
+                        if constexpr (out_f32) buf[P] = out[o];
+                        else reinterpret_cast<int16_t*>(buf)[P] = (int16_t)java_round16(out[o]);
                     }
                 }
             }
-            if (!emit) continue;
-            if (nch == 1) {  // mono -> stereo duplication (SyntacticElements.java:243-245)
-#pragma unroll
-                for (int o = 0; o < 16; o++) {
-                    if constexpr (out_f32) pf[1][o] = pf[0][o];
-                    else pk[o] = pk[o] | (pk[o] << 16);
+            __syncthreads();  // B3: PCM of both channels in LDS
+
+            // ---------------- phase E: interleave + store (stereo: wave c stores samples [512c, 512c+512)) ----
+            if (emit) {
+                const float* bL = stereo ? Wb[wave & ~1] : buf;
+                const float* bR = stereo ? Wb[wave | 1] : buf;
+                const int nj = stereo ? 2 : 4;
+                for (int jj = 0; jj < nj; jj++) {
+                    const int j = stereo ? 2 * c + jj : jj;
+                    const int p = 4 * u + 256 * j;  // samples p..p+3
+                    if constexpr (out_f32) {
+                        float4 l = *reinterpret_cast<const float4*>(bL + p);
+                        float4 r = *reinterpret_cast<const float4*>(bR + p);
+                        float4* dst = reinterpret_cast<float4*>(reinterpret_cast<uint8_t*>(A.pcm) + (size_t)f * 8192 + 8 * p);
+                        dst[0] = make_float4(l.x, r.x, l.y, r.y);
+                        dst[1] = make_float4(l.z, r.z, l.w, r.w);
+                    } else {
+                        uint2 l = *reinterpret_cast<const uint2*>(reinterpret_cast<const int16_t*>(bL) + p);
+                        uint2 r = *reinterpret_cast<const uint2*>(reinterpret_cast<const int16_t*>(bR) + p);
+                        // (L_i, R_i) int16 pairs; big endian swaps the two bytes of every sample.
+                        // v_perm_b32(s0=r, s1=l): selector bytes 0-3 pick l, 4-7 pick r.
+                        const uint32_t sel0 = big_endian ? 0x04050001u : 0x05040100u;
+                        const uint32_t sel1 = big_endian ? 0x06070203u : 0x07060302u;
+                        v4u o;
+                        o.x = __builtin_amdgcn_perm(r.x, l.x, sel0);
+                        o.y = __builtin_amdgcn_perm(r.x, l.x, sel1);
+                        o.z = __builtin_amdgcn_perm(r.y, l.y, sel0);
+                        o.w = __builtin_amdgcn_perm(r.y, l.y, sel1);
+                        v4u* dst = reinterpret_cast<v4u*>(reinterpret_cast<uint8_t*>(A.pcm) + (size_t)f * 4096 + 4 * p);
+                        __builtin_nontemporal_store(o, dst);
+                    }
                 }
             }
-            // ---- PCM store: lane u writes samples 2u+128j and 2u+128j+1 (the latter computed by
-            // lane 63-u as its odd slot 7-j), i.e. 512 contiguous bytes per wave instruction
-            if constexpr (!out_f32) {
-                uint2* dst = reinterpret_cast<uint2*>(reinterpret_cast<uint8_t*>(A.pcm) + (size_t)f * 4096);
-#pragma unroll
-                for (int j = 0; j < 8; j++) {
-                    // even slot of column j and odd slot of column 7-j (see long_pos)
-                    const int se = (j + 4) & 7;           // slot s whose even position is column j
-                    const int oe = 2 * se + (se < 4 ? 1 : 0);
-                    const int so = ((7 - j) + 4) & 7;     // slot s whose odd position is column 7-j
-                    const int oo = 2 * so + (so < 4 ? 0 : 1);
-                    uint32_t partner = (uint32_t)__shfl_xor((int)pk[oo], 63);
-                    dst[u + 64 * j] = make_uint2(pk[oe], partner);
-                }
-            } else {
-                float4* dst = reinterpret_cast<float4*>(reinterpret_cast<uint8_t*>(A.pcm) + (size_t)f * 8192);
-#pragma unroll
-                for (int j = 0; j < 8; j++) {
-                    const int se = (j + 4) & 7;
-                    const int oe = 2 * se + (se < 4 ? 1 : 0);
-                    const int so = ((7 - j) + 4) & 7;
-                    const int oo = 2 * so + (so < 4 ? 0 : 1);
-                    float pl = __shfl_xor(pf[0][oo], 63);
-                    float pr = __shfl_xor(pf[1][oo], 63);
-                    dst[u + 64 * j] = make_float4(pf[0][oe], pf[1][oe], pl, pr);
-                }
-            }
+            __syncthreads();  // B4: PCM staging buffers may be reused
         }
         if (cd.info & kChunkStoreState) {
-            float* st = A.state_out + (size_t)cd.slot * 2048;
+            const int u = lane_id();
+            float* st = A.state_out + (size_t)cd.slot * 2048 + 1024 * c;
 #pragma unroll
-            for (int o = 0; o < 16; o++) {
-                int P = long_pos(u, o >> 1, o & 1);
-                st[P] = ovL[o];
-                st[1024 + P] = nch == 2 ? ovR[o] : 0.0f;
-            }
+            for (int o = 0; o < 16; o++) st[long_pos(u, o)] = ov[o];
         }
     }
 }
 
-
-}  // namespace jaad
-
-namespace jaad {
 hipError_t launch_lc(const KernelArgs& a, int grid, hipStream_t stream, bool tns_spec)
 {
 #define JAAD_LAUNCH(T, O) hipLaunchKernelGGL((lc_decode_kernel<T, O>), dim3(grid), dim3(kWGThreads), 0, stream, a)
@@ -752,4 +816,5 @@ hipError_t launch_lc(const KernelArgs& a, int grid, hipStream_t stream, bool tns
 #undef JAAD_LAUNCH
     return hipGetLastError();
 }
+
 }  // namespace jaad
