@@ -51,6 +51,7 @@ struct jaad_ctx {
     float* d_state[2] = {nullptr, nullptr};  // [slot][2][1024], double-buffered (see plan())
     int parity = 0;                          // d_state[parity] holds the current state
     LdsTables* d_tables = nullptr;
+    GlobalTables* d_gtab = nullptr;
     float* d_iq = nullptr;
     DevBuf d_chunks, d_batch, d_pcm;
     std::vector<ChunkDesc> chunks;
@@ -60,14 +61,16 @@ struct jaad_ctx {
     int n_cu = 256;
     uint32_t chunk_frames = kDefaultChunkFrames;
     float* dbg = nullptr;
+    int dbg_frame = 0;
     std::string err;
 };
 
 namespace jaad {
 
-void build_lds_tables(int sf_index, LdsTables* t)
+void build_lds_tables(int sf_index, LdsTables* t, GlobalTables* gt)
 {
     std::memset(t, 0, sizeof(*t));
+    std::memset(gt, 0, sizeof(*gt));
     const float* LW[2] = {JAAD_SINE_1024, JAAD_KBD_1024};
     for (int sh = 0; sh < 2; sh++)
         for (int o = 0; o < 16; o++)
@@ -90,11 +93,7 @@ void build_lds_tables(int sf_index, LdsTables* t)
         for (int e = 0; e < 2; e++) root(16 * (b + 8 * e), t->tw2[1 + e][b]);
         for (int s = 0; s < 4; s++) root(8 * (b + 8 * s), t->tw2[3 + s][b]);
     }
-    for (int u = 0; u < 64; u++) {
-        root(4 * u, t->tw3[0][u]);
-        for (int e = 0; e < 2; e++) root(2 * (u + 64 * e), t->tw3[1 + e][u]);
-        for (int s = 0; s < 4; s++) root(u + 64 * s, t->tw3[3 + s][u]);
-    }
+    for (int k = 0; k < 256; k++) root(k, t->roots_l[k]);
     std::memcpy(t->mdct_s, JAAD_MDCT_TABLE_128, sizeof(t->mdct_s));
     for (int k = 0; k < 32; k++) {
         t->roots_s[k][0] = JAAD_FFT_TABLE_64[k][0];
@@ -102,18 +101,19 @@ void build_lds_tables(int sf_index, LdsTables* t)
     }
     for (int i = 0; i < 256; i++) {
         t->sf_gain[i] = JAAD_SCALEFACTOR_TABLE[100 + i];
-        if (i < 128) t->iq_head[i] = JAAD_IQ_TABLE[i];
+        const int q = i - 128;  // float of (q>0 ? IQ[q] : -IQ[-q]): q = 0 gives -0.0
+        t->iq_signed[i] = q > 0 ? JAAD_IQ_TABLE[q] : -JAAD_IQ_TABLE[-q];
     }
-    std::memcpy(t->tns_coef[0], JAAD_TNS_COEF_0_3, sizeof(JAAD_TNS_COEF_0_3));
-    std::memcpy(t->tns_coef[1], JAAD_TNS_COEF_0_4, sizeof(JAAD_TNS_COEF_0_4));
-    std::memcpy(t->tns_coef[2], JAAD_TNS_COEF_1_3, sizeof(JAAD_TNS_COEF_1_3));
-    std::memcpy(t->tns_coef[3], JAAD_TNS_COEF_1_4, sizeof(JAAD_TNS_COEF_1_4));
+    std::memcpy(gt->tns_coef[0], JAAD_TNS_COEF_0_3, sizeof(JAAD_TNS_COEF_0_3));
+    std::memcpy(gt->tns_coef[1], JAAD_TNS_COEF_0_4, sizeof(JAAD_TNS_COEF_0_4));
+    std::memcpy(gt->tns_coef[2], JAAD_TNS_COEF_1_3, sizeof(JAAD_TNS_COEF_1_3));
+    std::memcpy(gt->tns_coef[3], JAAD_TNS_COEF_1_4, sizeof(JAAD_TNS_COEF_1_4));
     const short* L = JAAD_SWB_OFFSET_LONG_WINDOW[sf_index];
     const short* S = JAAD_SWB_OFFSET_SHORT_WINDOW[sf_index];
     t->nswb_l = JAAD_SWB_LONG_WINDOW_COUNT[sf_index];
     t->nswb_s = JAAD_SWB_SHORT_WINDOW_COUNT[sf_index];
-    for (int i = 0; i <= t->nswb_l; i++) t->swb_l[i] = L[i];
-    for (int i = 0; i <= t->nswb_s; i++) t->swb_s[i] = S[i];
+    for (int i = 0; i <= t->nswb_l; i++) gt->swb_l[i] = L[i];
+    for (int i = 0; i <= t->nswb_s; i++) gt->swb_s[i] = S[i];
     std::memset(t->quad2band_l, 255, sizeof(t->quad2band_l));
     std::memset(t->quad2band_s, 255, sizeof(t->quad2band_s));
     for (int b = 0; b < t->nswb_l; b++)
@@ -207,6 +207,7 @@ int launch(jaad_ctx* ctx, const jaad_batch* db, void* pcm, uint32_t flags, hipSt
     a.tns = db->tns;
     a.iq_table = ctx->d_iq;
     a.tables = ctx->d_tables;
+    a.gtab = ctx->d_gtab;
     a.chunks = static_cast<const ChunkDesc*>(ctx->d_chunks.p);
     a.state_in = ctx->d_state[ctx->parity];
     a.state_out = ctx->d_state[ctx->parity ^ 1];
@@ -216,6 +217,7 @@ int launch(jaad_ctx* ctx, const jaad_batch* db, void* pcm, uint32_t flags, hipSt
     a.out_mode = flags;
     a.tns_mode = ctx->cfg.tns_mode;
     a.dbg = ctx->dbg;
+    a.dbg_frame = ctx->dbg_frame;
     if (a.n_chunks == 0) return JAAD_OK;
     // slots this call does not touch keep their state: carry them into the other buffer
     size_t slot_bytes = 2048 * sizeof(float);
@@ -277,10 +279,11 @@ const char* jaad_strerror(int status)
 const char* jaad_last_error(const jaad_ctx* ctx) { return ctx ? ctx->err.c_str() : ""; }
 
 // internal (not in the public header): device buffer of 6144 floats receiving stage dumps
-int jaad__debug_attach(jaad_ctx* ctx, void* dev_buf)
+int jaad__debug_attach(jaad_ctx* ctx, void* dev_buf, int frame)
 {
     if (!ctx) return JAAD_ERR_INVALID_ARG;
     ctx->dbg = static_cast<float*>(dev_buf);
+    ctx->dbg_frame = frame;
     return JAAD_OK;
 }
 
@@ -318,11 +321,14 @@ int jaad_ctx_create(const jaad_stream_cfg* cfg, uint32_t n_slots, int device, ja
         if ((e = hipMemset(ctx->d_state[i], 0, sbytes)) != hipSuccess) return bail(e, "hipMemset state");
     }
     LdsTables* h = new (std::nothrow) LdsTables;
+    GlobalTables gt;
     if (!h) {
         jaad_ctx_destroy(ctx);
         return JAAD_ERR_NOMEM;
     }
-    build_lds_tables(cfg->sf_index, h);
+    build_lds_tables(cfg->sf_index, h, &gt);
+    if ((e = hipMalloc(&ctx->d_gtab, sizeof(GlobalTables))) != hipSuccess) { delete h; return bail(e, "hipMalloc gtab"); }
+    if ((e = hipMemcpy(ctx->d_gtab, &gt, sizeof(GlobalTables), hipMemcpyHostToDevice)) != hipSuccess) { delete h; return bail(e, "hipMemcpy gtab"); }
     if ((e = hipMalloc(&ctx->d_tables, sizeof(LdsTables))) != hipSuccess) { delete h; return bail(e, "hipMalloc tables"); }
     e = hipMemcpy(ctx->d_tables, h, sizeof(LdsTables), hipMemcpyHostToDevice);
     delete h;
@@ -342,6 +348,7 @@ void jaad_ctx_destroy(jaad_ctx* ctx)
     for (int i = 0; i < 2; i++)
         if (ctx->d_state[i]) (void)hipFree(ctx->d_state[i]);
     if (ctx->d_tables) (void)hipFree(ctx->d_tables);
+    if (ctx->d_gtab) (void)hipFree(ctx->d_gtab);
     if (ctx->d_iq) (void)hipFree(ctx->d_iq);
     ctx->d_chunks.release();
     ctx->d_batch.release();

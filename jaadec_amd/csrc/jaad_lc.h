@@ -29,20 +29,24 @@ enum : uint32_t { kChunkPrefix = 1u << 16, kChunkLoadState = 1u << 17, kChunkSto
 struct alignas(16) LdsTables {
     float win_slot[2][16][64];  // long window [shape][slot o][lane u] = W[long_pos(u,o)] (SINE/KBD_1024)
     float mdct_l[512][2];       // MDCT_TABLE_2048 (A/filterbank/MDCTTables.java:5), k order
-    float tw3[7][64][2];        // 512-pt IFFT pass-3 twiddles [j][lane]  (FFT_TABLE_512, FFTTables.java:5)
+    float roots_l[256][2];      // FFT_TABLE_512[k][0..1], k < 256 (A/filterbank/FFTTables.java:5)
     float tw2[7][8][2];         // 512-pt IFFT pass-2 twiddles [j][lane&7]
     float tw1[4][2];            // 512-pt IFFT pass-1 (i = 4) twiddles
     float win_short[2][128];    // SINE_128, KBD_128
     float mdct_s[64][2];        // MDCT_TABLE_128 (:519)
     float roots_s[32][2];       // FFT_TABLE_64[k], k < 32 (:519)
     float sf_gain[256];         // SCALEFACTOR_TABLE[100+i] (A/syntax/ScaleFactorTable.java)
-    float iq_head[128];         // IQ_TABLE[i], i < 128 (A/syntax/IQTable.java)
-    float tns_coef[4][16];      // TNS_TABLES (A/tools/TNSTables.java), zero padded
+    float iq_signed[256];       // q = i-128: q>0 ? IQ_TABLE[q] : -IQ_TABLE[-q] (A/syntax/ICStream.java:266)
     uint8_t quad2band_l[256];   // long window: scalefactor band of bins 4i..4i+3 (255 = none)
     uint8_t quad2band_s[32];    // short window
+    int32_t nswb_l, nswb_s, tns_max_l, tns_max_s;
+};
+
+// Tables only the slow paths (PNS, spec TNS) need; read from global memory.
+struct GlobalTables {
+    float tns_coef[4][16];      // TNS_TABLES (A/tools/TNSTables.java), zero padded
     int16_t swb_l[64];          // SWB offsets long (ScaleFactorBands.java), count+1 entries
     int16_t swb_s[16];          // SWB offsets short
-    int32_t nswb_l, nswb_s, tns_max_l, tns_max_s;
 };
 static_assert(sizeof(LdsTables) % 16 == 0, "LdsTables must be 16-byte granular");
 
@@ -55,6 +59,7 @@ struct KernelArgs {
     const jaad_tns* tns;
     const float* iq_table;      // full IQ_TABLE[8191] (device)
     const LdsTables* tables;    // device copy of the LDS image
+    const GlobalTables* gtab;   // slow-path tables
     const ChunkDesc* chunks;
     float* state_in;            // [slot][2][1024] overlap, read by chunks with kChunkLoadState
     float* state_out;           // written by chunks with kChunkStoreState
@@ -63,7 +68,8 @@ struct KernelArgs {
     uint32_t nch;               // 1 (SCE) or 2 (CPE)
     uint32_t out_mode;          // JAAD_PCM_* flags
     uint32_t tns_mode;          // JAAD_TNS_*
-    float* dbg;                 // internal: stage dump of chunk 0's first emitted frame (or null)
+    float* dbg;                 // internal: stage dump of frame dbg_frame of chunk 0 (or null)
+    int dbg_frame;
 };
 
 // position (0..1023) of lane u's IMDCT output slot o = 2s+h (see jaad_lc.hip, long_pos)
@@ -74,7 +80,7 @@ inline int long_pos_host(int u, int o)
     return h ? 1535 - 2 * k : 2 * k - 512;
 }
 
-void build_lds_tables(int sf_index, LdsTables* t);
+void build_lds_tables(int sf_index, LdsTables* t, GlobalTables* g);
 
 }  // namespace jaad
 

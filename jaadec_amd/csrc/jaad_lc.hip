@@ -41,8 +41,13 @@ struct alignas(16) PairBands {
 // address out of the frame loop (which otherwise costs >100 VGPRs and all occupancy).
 __device__ __forceinline__ int lane_id()
 {
+#ifndef JAAD_HOISTABLE_LANE
     int v;
     asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(v));
+#else
+    int v = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+#endif
+    __builtin_assume(v >= 0 && v < 64);
     return v;
 }
 
@@ -55,16 +60,18 @@ __device__ __forceinline__ void wave_sync()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// spectrum layout in a wave's buffer: even bins in [0,512), odd bins in [512,1024), bin-pair
-// index XOR-swizzled so lane-parallel pre-twiddle reads (long and short) are conflict free
+constexpr int kWaveBuf = 1152;  // floats of LDS per wave
+
+// spectrum layout in a wave's buffer: even bins at [0,576), odd bins at [576,1152), bin-pair
+// index j padded by 8 every 64 so the lane-parallel pre-twiddle reads of long (k = u + 64s)
+// and short (k = 64w + b + 8s) windows are conflict free with base + immediate addressing
 __device__ __forceinline__ int eo_idx(int p)
 {
     int j = p >> 1;
-    j ^= ((j >> 6) & 3) << 3;
-    return ((p & 1) << 9) + j;
+    return (p & 1) * 576 + j + 8 * (j >> 6);
 }
-// IFFT transpose layout (complex index), XOR-swizzled against the bit-reversed write pattern
-__device__ __forceinline__ int xs(int i) { return i ^ ((i >> 4) & 15); }
+// IFFT transpose layout (complex index): one pad slot every 16 (<= 2-way conflicts, affine)
+__device__ __forceinline__ int xs(int i) { return i + (i >> 4); }
 
 __device__ constexpr int BR3[8] = {0, 4, 2, 6, 1, 5, 3, 7};
 
@@ -159,6 +166,40 @@ struct FrameCtx {
     int seq, shape, shape_prev;
 };
 
+// jaad_ics_info unpacked into wave-uniform scalars (kept in SGPRs; a struct of bytes selected
+// at run time would be spilled to scratch)
+struct Ics {
+    int seq, shape, shape_prev, max_sfb, grouping, flags;
+    uint32_t pns;
+};
+__device__ __forceinline__ Ics load_ics(const jaad_ics_info* p)
+{
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(p);
+    const uint32_t a = __builtin_amdgcn_readfirstlane(w[0]);
+    const uint32_t b = __builtin_amdgcn_readfirstlane(w[1]);
+    Ics r;
+    r.seq = a & 0xff;
+    r.shape = (a >> 8) & 0xff;
+    r.shape_prev = (a >> 16) & 0xff;
+    r.max_sfb = a >> 24;
+    r.grouping = b & 0xff;
+    r.flags = (b >> 8) & 0xff;
+    r.pns = __builtin_amdgcn_readfirstlane(w[2]);
+    return r;
+}
+__device__ __forceinline__ Ics sel_ics(bool c, const Ics& x, const Ics& y)
+{
+    Ics r;
+    r.seq = c ? x.seq : y.seq;
+    r.shape = c ? x.shape : y.shape;
+    r.shape_prev = c ? x.shape_prev : y.shape_prev;
+    r.max_sfb = c ? x.max_sfb : y.max_sfb;
+    r.grouping = c ? x.grouping : y.grouping;
+    r.flags = c ? x.flags : y.flags;
+    r.pns = c ? x.pns : y.pns;
+    return r;
+}
+
 // ------------------------------------------------------------------------------------------
 // IMDCT N = 2048 (MDCT.process): lane u holds k = u + 64 s.  Reads the spectrum from buf.
 // ------------------------------------------------------------------------------------------
@@ -204,9 +245,11 @@ __device__ __forceinline__ void imdct_long(float* buf, const LdsTables& T, int u
         im[s] = v.y;
     }
     wave_sync();
+    // stages 64 (m = 4, k = u), 128 (m = 2, k = u + 64e), 256 (m = 1, k = u + 64s)
     fft_3stages(re, im, [&](int j, float& wr, float& wi) {
-        wr = T.tw3[j][u][0];
-        wi = T.tw3[j][u][1];
+        const int idx = j == 0 ? 4 * u : (j < 3 ? 2 * (u + 64 * (j - 1)) : u + 64 * (j - 3));
+        wr = T.roots_l[idx][0];
+        wi = T.roots_l[idx][1];
     });
 #pragma unroll
     for (int s = 0; s < 8; s++) {  // MDCT.java:48-53
@@ -378,12 +421,12 @@ __device__ __forceinline__ void ola_short(float* Tb, const LdsTables& T, int u, 
 // TNS, spec mode (ISO/IEC 14496-3 4.6.9.3), in place on the spectrum; one lane per filter.
 // The reference parses TNS (A/tools/TNS.java:35-61) but its process() is a no-op.
 // ------------------------------------------------------------------------------------------
-__device__ void tns_spec(float* buf, float* scratch, const LdsTables& T, int u, const jaad_ics_info& info,
-                         const jaad_tns* tp)
+__device__ void tns_spec(float* buf, float* scratch, const LdsTables& T, const GlobalTables& G, int u,
+                         const Ics& info, const jaad_tns* tp)
 {
-    const bool is_short = info.window_sequence == JAAD_EIGHT_SHORT_SEQUENCE;
+    const bool is_short = info.seq == JAAD_EIGHT_SHORT_SEQUENCE;
     const int nswb = is_short ? T.nswb_s : T.nswb_l;
-    const int16_t* offs = is_short ? T.swb_s : T.swb_l;
+    const int16_t* offs = is_short ? G.swb_s : G.swb_l;
     const int tns_max = is_short ? T.tns_max_s : T.tns_max_l;
     const int nf = tp->n_filters;
     if (u < nf && u < 8) {
@@ -399,7 +442,7 @@ __device__ void tns_spec(float* buf, float* scratch, const LdsTables& T, int u, 
         const int order = F.order > 20 ? 20 : F.order;
         float* a = scratch + 24 * u;  // a[0..20]
         float bb[21];
-        const float* tab = T.tns_coef[2 * ((F.flags >> 2) & 1) + ((F.flags >> 1) & 1)];
+        const float* tab = G.tns_coef[2 * ((F.flags >> 2) & 1) + ((F.flags >> 1) & 1)];
         a[0] = 1.0f;
         for (int m = 1; m <= order; m++) {
             float tm = -tab[F.coef[m - 1] & 15];
@@ -436,11 +479,11 @@ __device__ void tns_spec(float* buf, float* scratch, const LdsTables& T, int u, 
 // ------------------------------------------------------------------------------------------
 // PNS slow path (ICStream.java:241-257): lane 0 replays the static LCG in parse order.
 // ------------------------------------------------------------------------------------------
-__device__ void pns_fill(float* buf, const PairBands& pb, int bc, const LdsTables& T, int u, const jaad_ics_info& info)
+__device__ void pns_fill(float* buf, const PairBands& pb, int bc, const GlobalTables& G, int u, const Ics& info)
 {
     if (u == 0) {
-        const bool is_short = info.window_sequence == JAAD_EIGHT_SHORT_SEQUENCE;
-        const int16_t* offs = is_short ? T.swb_s : T.swb_l;
+        const bool is_short = info.seq == JAAD_EIGHT_SHORT_SEQUENCE;
+        const int16_t* offs = is_short ? G.swb_s : G.swb_l;
         int glen[8], ng = 1;
         glen[0] = 1;
         if (is_short)
@@ -448,7 +491,7 @@ __device__ void pns_fill(float* buf, const PairBands& pb, int bc, const LdsTable
                 if (info.grouping & (1u << i)) glen[ng - 1]++;
                 else glen[ng++] = 1;
             }
-        uint32_t rs = info.pns_state;
+        uint32_t rs = info.pns;
         const int maxSFB = info.max_sfb;
         for (int g = 0, idx = 0, groupOff = 0; g < ng; g++) {
             for (int sfb = 0; sfb < maxSFB; sfb++, idx++) {
@@ -475,10 +518,10 @@ __device__ void pns_fill(float* buf, const PairBands& pb, int bc, const LdsTable
 }
 
 // band index (g*max_sfb + sfb) of the bin quad starting at position p (4-aligned), or -1
-__device__ __forceinline__ int band_of(const LdsTables& T, const jaad_ics_info& info, int p)
+__device__ __forceinline__ int band_of(const LdsTables& T, const Ics& info, int p)
 {
     int sfb, g = 0;
-    if (info.window_sequence == JAAD_EIGHT_SHORT_SEQUENCE) {
+    if (info.seq == JAAD_EIGHT_SHORT_SEQUENCE) {
         int w = p >> 7;
         sfb = T.quad2band_s[(p & 127) >> 2];
         g = w - __builtin_popcount(info.grouping & ((1u << w) - 1u));
@@ -517,24 +560,48 @@ typedef int v4i __attribute__((ext_vector_type(4)));
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
 
 struct Prefetch {
-    v4i q[2];      // own channel bins 8u+512h .. +7
+    v4i q[2];       // own channel bins 8u+512h .. +7
     uint32_t sfcb;  // lane u < 32: sf bytes 4u..4u+3; lane u >= 32: cb bytes 4(u-32)..
+    uint32_t side;  // lane i < 4*nch: dword i of the frame's jaad_ics_info records;
+                    // lanes 8..11: the frame's ms_used words (read back with readlane)
 };
 
-__device__ __forceinline__ void prefetch(const KernelArgs& A, size_t cf, int u, Prefetch& pf)
+// Everything frame f needs from HBM, loaded one frame ahead with vector loads (vmcnt is in
+// order; scalar loads would share lgkmcnt with the LDS traffic and could not be hidden).
+__device__ __forceinline__ void prefetch(const KernelArgs& A, int f, int nch, int c, int u, Prefetch& pf)
 {
+    const size_t cf = (size_t)f * nch + c;
     const v4i* q = reinterpret_cast<const v4i*>(A.q + cf * 1024);
     pf.q[0] = __builtin_nontemporal_load(q + u);
     pf.q[1] = __builtin_nontemporal_load(q + 64 + u);
     const uint32_t* row = reinterpret_cast<const uint32_t*>(u < 32 ? A.sf + cf * 128 : A.cb + cf * 128);
     pf.sfcb = row[u & 31];
+    const uint32_t* side = u < 8 ? reinterpret_cast<const uint32_t*>(A.ics + (size_t)f * nch) + (u < 4 * nch ? u : 0)
+                                 : (A.ms_used ? reinterpret_cast<const uint32_t*>(A.ms_used + (size_t)f * 2) + (u & 3)
+                                              : reinterpret_cast<const uint32_t*>(A.ics));
+    pf.side = *side;
+}
+
+__device__ __forceinline__ Ics ics_from_lanes(uint32_t side, int base)
+{
+    const uint32_t a = __builtin_amdgcn_readlane(side, base);
+    const uint32_t b = __builtin_amdgcn_readlane(side, base + 1);
+    Ics r;
+    r.seq = a & 0xff;
+    r.shape = (a >> 8) & 0xff;
+    r.shape_prev = (a >> 16) & 0xff;
+    r.max_sfb = a >> 24;
+    r.grouping = b & 0xff;
+    r.flags = (b >> 8) & 0xff;
+    r.pns = __builtin_amdgcn_readlane(side, base + 2);
+    return r;
 }
 
 template <bool kTnsSpec, int kOut>
 __global__ __launch_bounds__(kWGThreads, kTnsSpec ? 2 : JAAD_WAVES_PER_EU) void lc_decode_kernel(KernelArgs A)
 {
     __shared__ LdsTables T;
-    __shared__ float Wb[kWavesPerWG][1024];
+    __shared__ float Wb[kWavesPerWG][kWaveBuf];
     __shared__ PairBands PB[kWavesPerWG / 2];
 
     {
@@ -588,7 +655,7 @@ __global__ __launch_bounds__(kWGThreads, kTnsSpec ? 2 : JAAD_WAVES_PER_EU) void 
             }
         }
         Prefetch pf;
-        if (my_n > 0) prefetch(A, (size_t)f_first * nch + c, lane_id(), pf);
+        if (my_n > 0) prefetch(A, f_first, nch, c, lane_id(), pf);
 
         for (int it = 0; it < n_iter; it++) {
             const int u = lane_id();
@@ -596,27 +663,39 @@ __global__ __launch_bounds__(kWGThreads, kTnsSpec ? 2 : JAAD_WAVES_PER_EU) void 
             const int f = f_first + it;
             const bool emit = active && f >= (int)cd.frame0;
             const size_t cf0 = (size_t)(active ? f : 0) * nch;
-            jaad_ics_info ic{}, iL{}, iR{};
+            Ics ic{}, iL{}, iR{};
             bool ms_on = false, is_on = false, xchg = false;
             float x[16];
 
             // ---------------- phase A: side info, inverse quantisation, PNS ----------------
             if (active) {
-                iL = A.ics[cf0];
-                iR = stereo ? A.ics[cf0 + 1] : iL;
-                ic = c ? iR : iL;
+                iL = ics_from_lanes(pf.side, 0);
+                iR = stereo ? ics_from_lanes(pf.side, 4) : iL;
+                ic = sel_ics(c != 0, iR, iL);
                 ms_on = stereo && (iL.flags & JAAD_ICS_COMMON_WINDOW) && (iL.flags & JAAD_ICS_MS_PRESENT);
                 is_on = stereo && (iR.flags & JAAD_ICS_HAS_IS);
                 xchg = ms_on || is_on;
                 // raw sf/cb rows of this channel -> pair record
                 reinterpret_cast<uint32_t*>(u < 32 ? pb.sf[bc] : pb.cb[bc])[u & 31] = pf.sfcb;
                 const Prefetch cur = pf;
-                if (it + 1 < my_n) prefetch(A, cf0 + nch + c, u, pf);
+                if (A.dbg && ci == 0 && u == 0 && f < 16) {
+                    A.dbg[6144 + 32 * f + 8 * c + 0] = (float)ic.seq;
+                    A.dbg[6144 + 32 * f + 8 * c + 1] = (float)ic.shape;
+                    A.dbg[6144 + 32 * f + 8 * c + 2] = (float)ic.shape_prev;
+                    A.dbg[6144 + 32 * f + 8 * c + 3] = (float)ic.max_sfb;
+                    A.dbg[6144 + 32 * f + 8 * c + 4] = (float)ic.flags;
+                    A.dbg[6144 + 32 * f + 8 * c + 5] = (float)(ic.pns & 0xffff);
+                    A.dbg[6144 + 32 * f + 8 * c + 6] = (float)f;
+                }
+                if (it + 1 < my_n) prefetch(A, f + 1, nch, c, u, pf);
                 if (stereo && c == 0) {
                     uint64_t m0 = 0, m1 = 0;
                     if (ms_on && A.ms_used) {
-                        m0 = A.ms_used[(size_t)f * 2];
-                        m1 = A.ms_used[(size_t)f * 2 + 1];
+                        // readlane returns int: widen through uint32_t (no sign extension)
+                        m0 = (uint64_t)(uint32_t)__builtin_amdgcn_readlane(cur.side, 8) |
+                             ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(cur.side, 9) << 32);
+                        m1 = (uint64_t)(uint32_t)__builtin_amdgcn_readlane(cur.side, 10) |
+                             ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(cur.side, 11) << 32);
                     }
                     pb.ms[u] = (uint8_t)((m0 >> u) & 1u);
                     pb.ms[u + 64] = (uint8_t)((m1 >> u) & 1u);
@@ -631,7 +710,7 @@ __global__ __launch_bounds__(kWGThreads, kTnsSpec ? 2 : JAAD_WAVES_PER_EU) void 
                 }
                 wave_sync();
                 // inverse quantisation (ICStream.java:258-271): lane owns bins 8u+512h+i
-                int amax = 0;
+                bool esc = false;
 #pragma unroll
                 for (int h = 0; h < 2; h++) {
                     const int16_t* qv = reinterpret_cast<const int16_t*>(&cur.q[h]);
@@ -644,14 +723,15 @@ __global__ __launch_bounds__(kWGThreads, kTnsSpec ? 2 : JAAD_WAVES_PER_EU) void 
 #pragma unroll
                         for (int i = 0; i < 4; i++) {
                             const int qq = qv[4 * j + i];
-                            const int aq = qq < 0 ? -qq : qq;
-                            amax = aq > amax ? aq : amax;
-                            const float m = T.iq_head[aq & 127] * gn;  // escapes fixed below
-                            x[8 * h + 4 * j + i] = spectral ? (qq > 0 ? m : -m) : 0.0f;  // q=0 -> -0
+                            const int qc = qq < -128 ? -128 : (qq > 127 ? 127 : qq);
+                            esc |= qc != qq;
+                            // (q>0 ? IQ[q] : -IQ[-q]) * sf, sign folded into the table
+                            const float m = T.iq_signed[qc + 128] * gn;
+                            x[8 * h + 4 * j + i] = spectral ? m : 0.0f;
                         }
                     }
                 }
-                if (__ballot(amax >= 128)) {  // escape values beyond the LDS head of IQ_TABLE
+                if (__ballot(esc)) {  // escape values beyond the LDS head of IQ_TABLE
 #pragma unroll
                     for (int h = 0; h < 2; h++) {
                         const int16_t* qv = reinterpret_cast<const int16_t*>(&cur.q[h]);
@@ -665,7 +745,7 @@ __global__ __launch_bounds__(kWGThreads, kTnsSpec ? 2 : JAAD_WAVES_PER_EU) void 
                             for (int i = 0; i < 4; i++) {
                                 const int qq = qv[4 * j + i];
                                 const int aq = qq < 0 ? -qq : qq;
-                                if (aq >= 128 && spectral) {
+                                if ((qq > 127 || qq < -128) && spectral) {
                                     const float m = A.iq_table[aq > 8190 ? 8190 : aq] * gn;
                                     x[8 * h + 4 * j + i] = qq > 0 ? m : -m;
                                 }
@@ -676,11 +756,13 @@ __global__ __launch_bounds__(kWGThreads, kTnsSpec ? 2 : JAAD_WAVES_PER_EU) void 
                 store_spec(buf, u, x);
                 if (ic.flags & JAAD_ICS_HAS_PNS) {
                     wave_sync();
-                    pns_fill(buf, pb, bc, T, u, ic);
+                    pns_fill(buf, pb, bc, *A.gtab, u, ic);
                     load_spec(buf, u, x);
                 }
             }
-            __syncthreads();  // B1: both channels' spectra + band records visible to the pair
+#ifndef JAAD_ABL_NO_BARRIER
+            __syncthreads();  // B1
+#endif  // both channels' spectra + band records visible to the pair
 
             // ---------------- phase C: M/S (MS.java:17-41) and I/S (IS.java:17-53) ----------------
             if (active && xchg) {
@@ -716,22 +798,30 @@ __global__ __launch_bounds__(kWGThreads, kTnsSpec ? 2 : JAAD_WAVES_PER_EU) void 
                     }
                 }
             }
-            __syncthreads();  // B2: the partner has read this wave's spectrum
+#ifndef JAAD_ABL_NO_BARRIER
+            __syncthreads();  // B2
+#endif  // the partner has read this wave's spectrum
 
             // ---------------- phase D: (TNS) -> IMDCT -> window/OLA -> PCM into LDS ----------------
             if (active) {
                 if (xchg) store_spec(buf, u, x);
                 wave_sync();
-                const bool dump = A.dbg && ci == 0 && f == (int)cd.frame0;
+                const bool dump = A.dbg && ci == 0 && f == A.dbg_frame;
                 if (dump)
                     for (int i = 0; i < 16; i++) {
                         const int p = 8 * u + 512 * (i >> 3) + (i & 7);
                         A.dbg[1024 * c + p] = buf[eo_idx(p)];
                     }
                 if (kTnsSpec && A.tns_mode == JAAD_TNS_SPEC && (ic.flags & JAAD_ICS_TNS) && A.tns)
-                    tns_spec(buf, &pb.gain[bc][0], T, u, ic, A.tns + cf0 + c);
-                FrameCtx fc{ic.window_sequence, ic.window_shape, ic.window_shape_prev};
+                    tns_spec(buf, &pb.gain[bc][0], T, *A.gtab, u, ic, A.tns + cf0 + c);
+                FrameCtx fc{ic.seq, ic.shape, ic.shape_prev};
                 float re[8], im[8], out[16];
+#ifdef JAAD_ABL_NO_IMDCT
+                if (true) {
+#pragma unroll
+                    for (int o = 0; o < 16; o++) { out[o] = buf[o * 64 + u] + ov[o]; ov[o] = out[o] * 0.5f; }
+                } else
+#endif
                 if (fc.seq == JAAD_EIGHT_SHORT_SEQUENCE) {
                     imdct_short(buf, T, u, re, im);
                     ola_short(buf, T, u, fc, re, im, ov, out);
@@ -756,10 +846,16 @@ __global__ __launch_bounds__(kWGThreads, kTnsSpec ? 2 : JAAD_WAVES_PER_EU) void 
                     }
                 }
             }
-            __syncthreads();  // B3: PCM of both channels in LDS
+#ifndef JAAD_ABL_NO_BARRIER
+            __syncthreads();  // B3
+#endif  // PCM of both channels in LDS
 
             // ---------------- phase E: interleave + store (stereo: wave c stores samples [512c, 512c+512)) ----
+#ifndef JAAD_ABL_NO_STORE
             if (emit) {
+#else
+            if (emit && A.n_chunks == 0) {
+#endif
                 const float* bL = stereo ? Wb[wave & ~1] : buf;
                 const float* bR = stereo ? Wb[wave | 1] : buf;
                 const int nj = stereo ? 2 : 4;
@@ -789,7 +885,9 @@ __global__ __launch_bounds__(kWGThreads, kTnsSpec ? 2 : JAAD_WAVES_PER_EU) void 
                     }
                 }
             }
-            __syncthreads();  // B4: PCM staging buffers may be reused
+#ifndef JAAD_ABL_NO_BARRIER
+            __syncthreads();  // B4
+#endif  // PCM staging buffers may be reused
         }
         if (cd.info & kChunkStoreState) {
             const int u = lane_id();

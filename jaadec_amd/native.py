@@ -13,7 +13,8 @@ from pathlib import Path
 import numpy as np
 
 PKG = Path(__file__).resolve().parent
-LIB_PATH = PKG / "libjaadgpu.so"
+import os as _os
+LIB_PATH = Path(_os.environ["JAAD_LIB"]) if _os.environ.get("JAAD_LIB") else PKG / "libjaadgpu.so"
 SYNTH_PATH = PKG / "libjaadsynth.so"
 
 ABI_VERSION = 1

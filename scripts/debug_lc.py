@@ -13,9 +13,21 @@ from oracle import oracle as O  # noqa: E402
 
 
 def oracle_stages(cfg, b, f=0):
+    # overlap state entering frame f: run the oracle filterbank over frames < f
+    ovs = np.zeros((2, 1024), np.float32)
     L = O.lib()
     L.orc_ms.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
     L.orc_is.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+    for ff in range(f + 1):
+        iq = stage_iq(cfg, b, ff, L)
+        if ff < f:
+            for c in range(2):
+                ic = b.ics[2 * ff + c]
+                O.filterbank(int(ic["window_sequence"]), int(ic["window_shape"]), int(ic["window_shape_prev"]), iq[c], ovs[c])
+    return finish(cfg, b, f, iq, ovs)
+
+
+def stage_iq(cfg, b, f, L):
     iq = np.zeros((2, 1024), np.float32)
     for c in range(2):
         cf = 2 * f + c
@@ -29,6 +41,10 @@ def oracle_stages(cfg, b, f=0):
                  b.ms_used[f].ctypes.data, iq[0].ctypes.data, iq[1].ctypes.data)
     L.orc_is(iL.ctypes.data, b.ics[2 * f + 1:2 * f + 2].ctypes.data, cfg.sf_index, b.cb[2 * f + 1].ctypes.data,
              b.sf[2 * f + 1].ctypes.data, b.ms_used[f].ctypes.data, iq[0].ctypes.data, iq[1].ctypes.data)
+    return iq
+
+
+def finish(cfg, b, f, iq, ovs):
     fftout = np.zeros((2, 1024), np.float32)
     outs = np.zeros((2, 1024), np.float32)
     for c in range(2):
@@ -38,7 +54,7 @@ def oracle_stages(cfg, b, f=0):
         im = np.where(k < 256, -buf[(1536 + 2 * k) % 2048], buf[(2 * k - 512) % 2048])
         fftout[c, 0::2] = re
         fftout[c, 1::2] = im
-        ov = np.zeros(1024, np.float32)
+        ov = ovs[c].copy()
         ic = b.ics[2 * f + c]
         outs[c] = O.filterbank(int(ic["window_sequence"]), int(ic["window_shape"]), int(ic["window_shape_prev"]), iq[c], ov)
     return iq, fftout, outs
@@ -54,23 +70,32 @@ def cmp(name, g, w):
 
 def main():
     seq = int(sys.argv[1]) if len(sys.argv) > 1 else 2
-    p = N.synth_params(seq, n_streams=1, frames_per_stream=1)
+    nfr = int(sys.argv[2]) if len(sys.argv) > 2 else 1
+    dbgf = int(sys.argv[3]) if len(sys.argv) > 3 else 0
+    p = N.synth_params(seq, n_streams=1, frames_per_stream=nfr)
     b = N.synth_batch(p)
     cfg = N.make_cfg()
-    dbg = torch.zeros(6144, dtype=torch.float32, device="cuda")
+    dbg = torch.zeros(6144 + 32 * 16, dtype=torch.float32, device="cuda")
     with N.Context(cfg, 1) as ctx:
-        N.lib().jaad__debug_attach.argtypes = [C.c_void_p, C.c_void_p]
-        N.lib().jaad__debug_attach(ctx.h, dbg.data_ptr())
+        N.lib().jaad__debug_attach.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
+        N.lib().jaad__debug_attach(ctx.h, dbg.data_ptr(), dbgf)
         got = ctx.decode(b, N.PCM_FLOAT32)
     torch.cuda.synchronize()
     d = dbg.cpu().numpy()
-    iq, fo, outs = oracle_stages(cfg, b)
+    iq, fo, outs = oracle_stages(cfg, b, dbgf)
     print("ics", b.ics[:2])
     for c in range(2):
         cmp(f"spectrum ch{c}", d[1024 * c:1024 * (c + 1)], iq[c])
         cmp(f"fft/post ch{c}", d[2048 + 1024 * c:2048 + 1024 * (c + 1)], fo[c])
         cmp(f"out ch{c}", d[4096 + 1024 * c:4096 + 1024 * (c + 1)], outs[c])
+    side = d[6144:].reshape(16, 4, 8)
+    for f in range(min(nfr, 16)):
+        print("frame", f, "gpu side L", side[f, 0, :7], "R", side[f, 1, :7])
+        print("        host  L", [b.ics[2*f][k] for k in ("window_sequence","window_shape","window_shape_prev","max_sfb","flags")],
+              "R", [b.ics[2*f+1][k] for k in ("window_sequence","window_shape","window_shape_prev","max_sfb","flags")])
     want = O.decode_batch(cfg, b, O.Streams(1), N.PCM_FLOAT32)
+    gw = got.view(np.float32).reshape(nfr, -1); ww = want.view(np.float32).reshape(nfr, -1)
+    print("frames equal:", [bool((gw[i].view(np.uint32) == ww[i].view(np.uint32)).all()) for i in range(nfr)])
     cmp("pcm f32", got.view(np.float32).reshape(-1), want.view(np.float32).reshape(-1))
 
 

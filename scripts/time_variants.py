@@ -1,0 +1,40 @@
+"""Time experimental library variants (JAAD_LIB=...) on the C2 workload; prints ms per batch."""
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+CHILD = r'''
+import sys, time, numpy as np, torch
+sys.path.insert(0, "%s")
+from jaadec_amd import native as N
+cfgid = int(sys.argv[1]) if len(sys.argv) > 1 else 2
+p = N.synth_params(cfgid); b = N.synth_batch(p); cfg = N.make_cfg()
+dev = torch.device("cuda", 0)
+t = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1)).to(dev)
+d = {"q": t(b.q), "sf": t(b.sf), "cb": t(b.cb), "ics": t(b.ics), "ms_used": t(b.ms_used)}
+ptr = {k: v.data_ptr() for k, v in d.items()}
+pcm = torch.empty(b.n_frames * 4096, dtype=torch.uint8, device=dev)
+ctx = N.Context(cfg, 256)
+s = torch.cuda.Stream(dev); torch.cuda.set_stream(s)
+for _ in range(3): ctx.decode_device(ptr, b, pcm.data_ptr(), pcm.numel(), 0, s.cuda_stream)
+torch.cuda.synchronize()
+ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+ev[0].record(s)
+for _ in range(20): ctx.decode_device(ptr, b, pcm.data_ptr(), pcm.numel(), 0, s.cuda_stream)
+ev[1].record(s); torch.cuda.synchronize()
+print("%%.4f" %% (ev[0].elapsed_time(ev[1]) / 20))
+''' % ROOT
+
+def main():
+    libs = sorted((ROOT / ".tmp/exp").glob("lib_*.so"))
+    cfgid = sys.argv[1] if len(sys.argv) > 1 else "2"
+    for lib in libs:
+        env = dict(os.environ, JAAD_LIB=str(lib))
+        r = subprocess.run([sys.executable, "-c", CHILD, cfgid], env=env, capture_output=True, text=True, timeout=300)
+        out = r.stdout.strip().splitlines()
+        print(f"{lib.stem:28s} {out[-1] if out else 'ERR ' + r.stderr[-300:]} ms", flush=True)
+
+if __name__ == "__main__":
+    main()
