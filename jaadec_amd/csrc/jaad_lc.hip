@@ -51,6 +51,25 @@ __device__ __forceinline__ int lane_id()
     return v;
 }
 
+#ifdef JAAD_STAMPS
+__device__ __forceinline__ uint32_t stamp()
+{
+    uint64_t t;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    return (uint32_t)t;
+}
+#define STAMP(k)                                                                                     \
+    do {                                                                                             \
+        uint32_t t_ = stamp();                                                                       \
+        if (A.dbg && lane_id() == 0 && (k) < 32)                                                     \
+            reinterpret_cast<uint32_t*>(A.dbg)[(size_t)(blockIdx.x * kWavesPerWG + wave) * 32 + (k)] = t_; \
+    } while (0)
+#else
+#define STAMP(k) \
+    do {         \
+    } while (0)
+#endif
+
 __device__ __forceinline__ void wave_sync()
 {
     // LDS traffic of one wave executes in order; this only stops the compiler from moving LDS
@@ -264,18 +283,21 @@ __device__ __forceinline__ void imdct_long(float* buf, const LdsTables& T, int u
 // FilterBank.process for ONLY_LONG / LONG_START / LONG_STOP (FilterBank.java:41-70, 102-119).
 // Lane u's slot (s,h) holds output position P = long_pos(u, 2s+h); its mirror 1023-P is slot
 // (s,1-h) of the same lane, so the falling window W[1023-P] is win_slot[shape][o^1][u].
-__device__ __forceinline__ void ola_long(const LdsTables& T, int, const FrameCtx& fc, const float (&re)[8],
-                                         const float (&im)[8], float (&ov)[16], float (&out)[16])
+// Specialised per sequence so the common ONLY_LONG path carries no joint-window logic.
+template <int kSeq>
+__device__ __forceinline__ void ola_long_t(const LdsTables& T, const FrameCtx& fc, const float (&re)[8],
+                                           const float (&im)[8], float (&ov)[16], float (&out)[16])
 {
     const int u = lane_id();
     const float* SWp = T.win_short[fc.shape_prev];
     const float* SWc = T.win_short[fc.shape];
+    const float* Wp = &T.win_slot[fc.shape_prev][0][0];
+    const float* Wc = &T.win_slot[fc.shape][0][0];
 #pragma unroll
     for (int s = 0; s < 8; s++) {
 #pragma unroll
         for (int h = 0; h < 2; h++) {
             const int o = 2 * s + h;
-            const int P = long_pos(u, o);
             float f, g;  // IMDCT samples buf[P] and buf[1024+P]
             if (s < 4) {
                 f = h ? re[s] : -re[s];
@@ -285,24 +307,34 @@ __device__ __forceinline__ void ola_long(const LdsTables& T, int, const FrameCtx
                 g = re[s];
             }
             float o_v, n_v;
-            if (fc.seq == JAAD_LONG_STOP_SEQUENCE) {
+            if constexpr (kSeq == JAAD_LONG_STOP_SEQUENCE) {
+                const int P = long_pos(u, o);
                 if (P < 448) o_v = ov[o];
                 else if (P < 576) o_v = ov[o] + (f * SWp[P - 448]);
                 else o_v = ov[o] + f;
             } else {
-                o_v = ov[o] + (f * T.win_slot[fc.shape_prev][o][u]);
+                o_v = ov[o] + (f * Wp[64 * o + u]);
             }
-            if (fc.seq == JAAD_LONG_START_SEQUENCE) {
+            if constexpr (kSeq == JAAD_LONG_START_SEQUENCE) {
+                const int P = long_pos(u, o);
                 if (P < 448) n_v = g;
                 else if (P < 576) n_v = g * SWc[127 - (P - 448)];
                 else n_v = 0.0f;
             } else {
-                n_v = g * T.win_slot[fc.shape][o ^ 1][u];
+                n_v = g * Wc[64 * (o ^ 1) + u];
             }
             out[o] = o_v;
             ov[o] = n_v;
         }
     }
+}
+
+__device__ __forceinline__ void ola_long(const LdsTables& T, int, const FrameCtx& fc, const float (&re)[8],
+                                         const float (&im)[8], float (&ov)[16], float (&out)[16])
+{
+    if (fc.seq == JAAD_ONLY_LONG_SEQUENCE) ola_long_t<JAAD_ONLY_LONG_SEQUENCE>(T, fc, re, im, ov, out);
+    else if (fc.seq == JAAD_LONG_START_SEQUENCE) ola_long_t<JAAD_LONG_START_SEQUENCE>(T, fc, re, im, ov, out);
+    else ola_long_t<JAAD_LONG_STOP_SEQUENCE>(T, fc, re, im, ov, out);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -614,6 +646,7 @@ __global__ __launch_bounds__(kWGThreads, kTnsSpec ? 2 : JAAD_WAVES_PER_EU) void 
     constexpr bool big_endian = !(kOut & JAAD_PCM_LITTLE_ENDIAN);
     constexpr bool out_f32 = (kOut & JAAD_PCM_FLOAT32) != 0;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    STAMP(0);
     const bool stereo = A.nch == 2;
     const int c = stereo ? (wave & 1) : 0;  // channel of this wave
     const int bc = wave & 1;                // channel slot in the PairBands record
@@ -624,6 +657,7 @@ __global__ __launch_bounds__(kWGThreads, kTnsSpec ? 2 : JAAD_WAVES_PER_EU) void 
     const int nch = stereo ? 2 : 1;
 
     for (uint32_t g = blockIdx.x; g * per_wg < A.n_chunks; g += gridDim.x) {
+        STAMP(1);
         // iteration count shared by the whole workgroup (barriers must match)
         int n_iter = 0;
         for (int j = 0; j < per_wg; j++) {
@@ -654,10 +688,16 @@ __global__ __launch_bounds__(kWGThreads, kTnsSpec ? 2 : JAAD_WAVES_PER_EU) void 
                 for (int o = 0; o < 16; o++) ov[o] = 0.0f;
             }
         }
-        Prefetch pf;
+        // two frames in flight per wave (>= 64 KiB of loads in flight per CU)
+        Prefetch pf, pf2;
         if (my_n > 0) prefetch(A, f_first, nch, c, lane_id(), pf);
+        if (my_n > 1) prefetch(A, f_first + 1, nch, c, lane_id(), pf2);
 
-        for (int it = 0; it < n_iter; it++) {
+        // frame body; pfx holds frame `it`'s inputs and is refilled with frame it+2 (two frames in
+        // flight; the loop is unrolled by 2 so the prefetch registers never need copying, which
+        // would force a vmcnt(0) drain of every outstanding load and store)
+        auto frame = [&](const int it, Prefetch& pfx) {
+            if (it >= 4 && it < 7) STAMP(2 + 9 * (it - 4) + 0);
             const int u = lane_id();
             const bool active = it < my_n;
             const int f = f_first + it;
@@ -669,15 +709,19 @@ __global__ __launch_bounds__(kWGThreads, kTnsSpec ? 2 : JAAD_WAVES_PER_EU) void 
 
             // ---------------- phase A: side info, inverse quantisation, PNS ----------------
             if (active) {
-                iL = ics_from_lanes(pf.side, 0);
-                iR = stereo ? ics_from_lanes(pf.side, 4) : iL;
+                iL = ics_from_lanes(pfx.side, 0);
+                iR = stereo ? ics_from_lanes(pfx.side, 4) : iL;
                 ic = sel_ics(c != 0, iR, iL);
                 ms_on = stereo && (iL.flags & JAAD_ICS_COMMON_WINDOW) && (iL.flags & JAAD_ICS_MS_PRESENT);
                 is_on = stereo && (iR.flags & JAAD_ICS_HAS_IS);
                 xchg = ms_on || is_on;
+#ifdef JAAD_ABL_NO_MS
+                xchg = false;
+#endif
                 // raw sf/cb rows of this channel -> pair record
-                reinterpret_cast<uint32_t*>(u < 32 ? pb.sf[bc] : pb.cb[bc])[u & 31] = pf.sfcb;
-                const Prefetch cur = pf;
+                reinterpret_cast<uint32_t*>(u < 32 ? pb.sf[bc] : pb.cb[bc])[u & 31] = pfx.sfcb;
+                const Prefetch cur = pfx;
+#ifdef JAAD_DEBUG_SIDE
                 if (A.dbg && ci == 0 && u == 0 && f < 16) {
                     A.dbg[6144 + 32 * f + 8 * c + 0] = (float)ic.seq;
                     A.dbg[6144 + 32 * f + 8 * c + 1] = (float)ic.shape;
@@ -687,7 +731,8 @@ __global__ __launch_bounds__(kWGThreads, kTnsSpec ? 2 : JAAD_WAVES_PER_EU) void 
                     A.dbg[6144 + 32 * f + 8 * c + 5] = (float)(ic.pns & 0xffff);
                     A.dbg[6144 + 32 * f + 8 * c + 6] = (float)f;
                 }
-                if (it + 1 < my_n) prefetch(A, f + 1, nch, c, u, pf);
+#endif
+                if (it + 2 < my_n) prefetch(A, f + 2, nch, c, u, pfx);
                 if (stereo && c == 0) {
                     uint64_t m0 = 0, m1 = 0;
                     if (ms_on && A.ms_used) {
@@ -701,6 +746,7 @@ __global__ __launch_bounds__(kWGThreads, kTnsSpec ? 2 : JAAD_WAVES_PER_EU) void 
                     pb.ms[u + 64] = (uint8_t)((m1 >> u) & 1u);
                 }
                 wave_sync();
+                if (it >= 4 && it < 7) STAMP(2 + 9 * (it - 4) + 1);
 #pragma unroll
                 for (int hb = 0; hb < 2; hb++) {
                     const int idx = u + 64 * hb;
@@ -710,6 +756,7 @@ __global__ __launch_bounds__(kWGThreads, kTnsSpec ? 2 : JAAD_WAVES_PER_EU) void 
                 }
                 wave_sync();
                 // inverse quantisation (ICStream.java:258-271): lane owns bins 8u+512h+i
+                if (it >= 4 && it < 7) STAMP(2 + 9 * (it - 4) + 2);
                 bool esc = false;
 #pragma unroll
                 for (int h = 0; h < 2; h++) {
@@ -726,7 +773,11 @@ __global__ __launch_bounds__(kWGThreads, kTnsSpec ? 2 : JAAD_WAVES_PER_EU) void 
                             const int qc = qq < -128 ? -128 : (qq > 127 ? 127 : qq);
                             esc |= qc != qq;
                             // (q>0 ? IQ[q] : -IQ[-q]) * sf, sign folded into the table
+#ifdef JAAD_ABL_NO_IQ
+                            const float m = (float)qc * gn;
+#else
                             const float m = T.iq_signed[qc + 128] * gn;
+#endif
                             x[8 * h + 4 * j + i] = spectral ? m : 0.0f;
                         }
                     }
@@ -753,6 +804,7 @@ __global__ __launch_bounds__(kWGThreads, kTnsSpec ? 2 : JAAD_WAVES_PER_EU) void 
                         }
                     }
                 }
+                if (it >= 4 && it < 7) STAMP(2 + 9 * (it - 4) + 3);
                 store_spec(buf, u, x);
                 if (ic.flags & JAAD_ICS_HAS_PNS) {
                     wave_sync();
@@ -764,6 +816,7 @@ __global__ __launch_bounds__(kWGThreads, kTnsSpec ? 2 : JAAD_WAVES_PER_EU) void 
             __syncthreads();  // B1
 #endif  // both channels' spectra + band records visible to the pair
 
+            if (it >= 4 && it < 7) STAMP(2 + 9 * (it - 4) + 4);
             // ---------------- phase C: M/S (MS.java:17-41) and I/S (IS.java:17-53) ----------------
             if (active && xchg) {
                 float xp[16];
@@ -798,10 +851,12 @@ __global__ __launch_bounds__(kWGThreads, kTnsSpec ? 2 : JAAD_WAVES_PER_EU) void 
                     }
                 }
             }
+            if (it >= 4 && it < 7) STAMP(2 + 9 * (it - 4) + 5);
 #ifndef JAAD_ABL_NO_BARRIER
             __syncthreads();  // B2
 #endif  // the partner has read this wave's spectrum
 
+            if (it >= 4 && it < 7) STAMP(2 + 9 * (it - 4) + 6);
             // ---------------- phase D: (TNS) -> IMDCT -> window/OLA -> PCM into LDS ----------------
             if (active) {
                 if (xchg) store_spec(buf, u, x);
@@ -837,7 +892,11 @@ __global__ __launch_bounds__(kWGThreads, kTnsSpec ? 2 : JAAD_WAVES_PER_EU) void 
                 wave_sync();
                 if (dump)
                     for (int o = 0; o < 16; o++) A.dbg[4096 + 1024 * c + long_pos(u, o)] = out[o];
+#ifdef JAAD_ABL_NO_PCMLDS
+                if (emit && A.n_chunks == 0) {
+#else
                 if (emit) {
+#endif
 #pragma unroll
                     for (int o = 0; o < 16; o++) {
                         const int P = long_pos(u, o);
@@ -850,6 +909,7 @@ __global__ __launch_bounds__(kWGThreads, kTnsSpec ? 2 : JAAD_WAVES_PER_EU) void 
             __syncthreads();  // B3
 #endif  // PCM of both channels in LDS
 
+            if (it >= 4 && it < 7) STAMP(2 + 9 * (it - 4) + 7);
             // ---------------- phase E: interleave + store (stereo: wave c stores samples [512c, 512c+512)) ----
 #ifndef JAAD_ABL_NO_STORE
             if (emit) {
@@ -888,7 +948,12 @@ __global__ __launch_bounds__(kWGThreads, kTnsSpec ? 2 : JAAD_WAVES_PER_EU) void 
 #ifndef JAAD_ABL_NO_BARRIER
             __syncthreads();  // B4
 #endif  // PCM staging buffers may be reused
+                };
+        for (int it = 0; it < n_iter; it += 2) {
+            frame(it, pf);
+            if (it + 1 < n_iter) frame(it + 1, pf2);
         }
+        STAMP(31);
         if (cd.info & kChunkStoreState) {
             const int u = lane_id();
             float* st = A.state_out + (size_t)cd.slot * 2048 + 1024 * c;
