@@ -153,6 +153,15 @@ def main():
                          f"parse excluded on both sides",
                "multicore_value": round(sub.n_frames / dtn, 1), "multicore_threads": thr}
 
+    # HBM bytes per launch measured by rocprofv3 PMC passes of this same command
+    # (scripts/gpu_prof.sh -> scripts/summarize_prof.py -> profiles/current.json)
+    traffic, traffic_src = None, None
+    cur = ROOT / "profiles" / "current.json"
+    if cur.exists() and args.config == 2:
+        prof = json.loads(cur.read_text())
+        traffic = prof.get("hbm_traffic_bytes_per_launch")
+        traffic_src = f"profiles/{prof.get('tag')}.json ({prof.get('hbm_traffic_note')})" if traffic else None
+
     if rank == 0:
         steps = args.steps
         total_frames = n_frames * world * steps
@@ -165,7 +174,8 @@ def main():
             "config": {"workload": WORKLOADS[args.config], "frames_per_gpu": n_frames,
                        "parallelism": f"stream-sharded x{world} (no collectives)", "pcm": "int16 big-endian"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "traffic_source": traffic_src,
                          "algorithmic_bytes_per_launch": ALGO_BYTES_PER_FRAME * n_frames,
                          "kernel_ms": round(kern_ms, 4)},
             "cpu_baseline": cpu,

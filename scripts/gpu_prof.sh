@@ -13,4 +13,5 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/prof/$TAG -o pmc3 --o
 rc=$?; echo "pmc3 rc=$rc" >> gpurun_out/prof/$TAG.pmc3.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE GRBM_GUI_ACTIVE -d gpurun_out/prof/$TAG -o pmc4 --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu > gpurun_out/prof/$TAG.pmc4.log 2>&1
 rc=$?; echo "pmc4 rc=$rc" >> gpurun_out/prof/$TAG.pmc4.log
+python3 scripts/summarize_prof.py gpurun_out/prof/$TAG $TAG gpurun_out/prof > gpurun_out/prof/$TAG.summary.log 2>&1
 exit $rc

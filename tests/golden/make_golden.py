@@ -1,0 +1,58 @@
+"""Generate the committed fixtures in tests/golden/ (inputs + expected PCM).
+
+The expected outputs come from the C restatement of the reference DSP (oracle/), because the
+reference itself (Java) cannot be run in this image and ships no vectors of its own (SURVEY.md
+s4, s8c).  The fixtures pin the restatement, the synthetic-input generator and the HIP path
+against silent drift; their relation to the Java code rests on tests/test_oracle.py.
+
+    python tests/golden/make_golden.py
+"""
+import sys
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+sys.path.insert(0, str(HERE.parents[1]))
+from jaadec_amd import native as N  # noqa: E402
+from oracle import oracle as O  # noqa: E402
+
+CASES = {
+    # name: (config id, overrides, cfg kwargs, flags)
+    "c1_mono_44k_one_frame": (1, dict(), dict(sf_index=4, channel_config=1), N.PCM_BIG_ENDIAN),
+    "c2_stereo_48k_long": (2, dict(n_streams=2, frames_per_stream=5), dict(), N.PCM_BIG_ENDIAN),
+    "c3_switching_tns_compat": (3, dict(n_streams=2, frames_per_stream=12), dict(), N.PCM_BIG_ENDIAN),
+    "c3_switching_tns_spec_f32": (3, dict(n_streams=2, frames_per_stream=10), dict(tns_mode=N.TNS_SPEC), N.PCM_FLOAT32),
+    "pns_is_le": (3, dict(n_streams=2, frames_per_stream=8, pns_percent=10, is_percent=20), dict(), N.PCM_LITTLE_ENDIAN),
+}
+
+
+def save(name, cfgid, over, cfgkw, flags):
+    p = N.synth_params(cfgid, **over)
+    b = N.synth_batch(p)
+    cfg = N.make_cfg(**{"sf_index": p.sf_index, "channel_config": p.channel_config, **cfgkw})
+    pcm = O.decode_batch(cfg, b, O.Streams(int(b.stream_slot.max()) + 1), flags)
+    arrays = dict(q=b.q, sf=b.sf, cb=b.cb, ics=b.ics.view(np.uint8), stream_slot=b.stream_slot,
+                  frame_begin=b.frame_begin, pcm=pcm,
+                  meta=np.array([cfg.sf_index, cfg.channel_config, cfg.tns_mode, flags, b.nch], np.int32))
+    if b.ms_used is not None:
+        arrays["ms_used"] = b.ms_used
+    if b.tns is not None:
+        arrays["tns"] = b.tns.view(np.uint8)
+    np.savez_compressed(HERE / f"{name}.npz", **arrays)
+    print(name, b.n_frames, "frames", pcm.nbytes, "PCM bytes")
+
+
+def load(path):
+    z = np.load(path, allow_pickle=False)
+    sf_index, ch, tns_mode, flags, nch = (int(v) for v in z["meta"])
+    b = N.Batch(z["q"], z["sf"], z["cb"], z["ics"].view(N.ICS_DTYPE).reshape(-1),
+                z["ms_used"] if "ms_used" in z else None,
+                z["tns"].view(N.TNS_DTYPE).reshape(-1) if "tns" in z else None,
+                z["stream_slot"], z["frame_begin"], nch)
+    return b, N.make_cfg(sf_index=sf_index, channel_config=ch, tns_mode=tns_mode), flags, z["pcm"]
+
+
+if __name__ == "__main__":
+    for k, v in CASES.items():
+        save(k, *v)
