@@ -79,10 +79,34 @@ def build_oracle(force: bool = False) -> Path:
     return ORACLE_LIB
 
 
+def jni_include() -> Path | None:
+    """$JAVA_HOME/include when a JDK is installed (none in this image)."""
+    home = os.environ.get("JAVA_HOME")
+    if home and (Path(home) / "include" / "jni.h").exists():
+        return Path(home) / "include"
+    return None
+
+
+def build_jni(force: bool = False) -> Path | None:
+    """libjaadjni.so: the JNI glue over libjaadgpu.so. Skipped without a JDK."""
+    inc = jni_include()
+    if inc is None:
+        print("JNI glue skipped: no $JAVA_HOME/include/jni.h", flush=True)
+        return None
+    out = PKG / "libjaadjni.so"
+    srcs = [CSRC / "jaad_jni.c"]
+    if force or _stale(out, srcs + [LIB]):
+        _run(["gcc", "-O2", "-std=c11", "-fPIC", "-shared", "-Wall", "-I", str(ROOT / "include"), "-I", str(inc),
+              "-I", str(inc / "linux"), "-o", str(out), str(srcs[0]), "-L", str(PKG), "-ljaadgpu",
+              "-Wl,-rpath,$ORIGIN"])
+    return out
+
+
 def build_all(force: bool = False) -> None:
     build_oracle(force)
     build_synth(force)
     build_gpu(force)
+    build_jni(force)
 
 
 if __name__ == "__main__":

@@ -1,0 +1,95 @@
+/* JNI glue for the reference's Java side: net.sourceforge.jaad.aac.gpu.GpuDSP.
+ *
+ * Compiled only where a JDK is installed (build.py looks for $JAVA_HOME/include/jni.h; this
+ * image has none, so here it is documentation that build.py skips).  Every buffer crosses as a
+ * direct java.nio.ByteBuffer in native byte order: no copies, no pinning, no JNI arrays.
+ * A nonzero jaad_status becomes net.sourceforge.jaad.aac.AACException (A/AACException.java),
+ * the exception Decoder.decodeFrame's callers already handle (A/Decoder.java:86-101).
+ */
+#include <jni.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "jaad_gpu.h"
+
+static void throw_aac(JNIEnv* env, jaad_ctx* ctx, int status) {
+    char msg[512];
+    const char* detail = ctx ? jaad_last_error(ctx) : "";
+    snprintf(msg, sizeof msg, "%s%s%s", jaad_strerror(status), detail && *detail ? ": " : "", detail ? detail : "");
+    jclass cls = (*env)->FindClass(env, "net/sourceforge/jaad/aac/AACException");
+    if (cls) (*env)->ThrowNew(env, cls, msg);
+}
+
+static void* addr(JNIEnv* env, jobject bb, jlong need) {
+    if (!bb) return NULL;
+    if ((*env)->GetDirectBufferCapacity(env, bb) < need) return NULL;
+    return (*env)->GetDirectBufferAddress(env, bb);
+}
+
+/* static native long nativeCreate(int sfIndex, int channelConfig, int tnsMode, int nSlots, int device) */
+JNIEXPORT jlong JNICALL Java_net_sourceforge_jaad_aac_gpu_GpuDSP_nativeCreate(JNIEnv* env, jclass cls, jint sf_index,
+                                                                            jint channel_config, jint tns_mode,
+                                                                            jint n_slots, jint device) {
+    (void)cls;
+    jaad_stream_cfg cfg;
+    memset(&cfg, 0, sizeof cfg);
+    cfg.abi_version = JAAD_ABI_VERSION;
+    cfg.profile = 2;
+    cfg.sf_index = (uint8_t)sf_index;
+    cfg.channel_config = (uint8_t)channel_config;
+    cfg.tns_mode = (uint8_t)tns_mode;
+    jaad_ctx* ctx = NULL;
+    int rc = jaad_ctx_create(&cfg, (uint32_t)n_slots, device, &ctx);
+    if (rc) {
+        throw_aac(env, NULL, rc);
+        return 0;
+    }
+    return (jlong)(intptr_t)ctx;
+}
+
+JNIEXPORT void JNICALL Java_net_sourceforge_jaad_aac_gpu_GpuDSP_nativeDestroy(JNIEnv* env, jclass cls, jlong h) {
+    (void)env;
+    (void)cls;
+    jaad_ctx_destroy((jaad_ctx*)(intptr_t)h);
+}
+
+/* static native void nativeDecode(long h, int nFrames, int nRuns, int nch, ByteBuffer streamSlot,
+ *     ByteBuffer frameBegin, ByteBuffer q, ByteBuffer sf, ByteBuffer cb, ByteBuffer ics,
+ *     ByteBuffer msUsed, ByteBuffer tns, ByteBuffer pcm, int flags) */
+JNIEXPORT void JNICALL Java_net_sourceforge_jaad_aac_gpu_GpuDSP_nativeDecode(
+    JNIEnv* env, jclass cls, jlong h, jint n_frames, jint n_runs, jint nch, jobject stream_slot, jobject frame_begin,
+    jobject q, jobject sf, jobject cb, jobject ics, jobject ms_used, jobject tns, jobject pcm, jint flags) {
+    (void)cls;
+    jaad_ctx* ctx = (jaad_ctx*)(intptr_t)h;
+    const jlong ncf = (jlong)n_frames * nch;
+    jaad_batch b;
+    memset(&b, 0, sizeof b);
+    b.n_frames = (uint32_t)n_frames;
+    b.n_runs = (uint32_t)n_runs;
+    b.stream_slot = (const uint32_t*)addr(env, stream_slot, 4LL * n_runs);
+    b.frame_begin = (const uint32_t*)addr(env, frame_begin, 4LL * (n_runs + 1));
+    b.q = (const int16_t*)addr(env, q, 2048LL * ncf);
+    b.sf = (const uint8_t*)addr(env, sf, 128LL * ncf);
+    b.cb = (const uint8_t*)addr(env, cb, 128LL * ncf);
+    b.ics = (const jaad_ics_info*)addr(env, ics, (jlong)sizeof(jaad_ics_info) * ncf);
+    b.ms_used = (const uint64_t*)addr(env, ms_used, 16LL * n_frames);
+    b.tns = (const jaad_tns*)addr(env, tns, (jlong)sizeof(jaad_tns) * ncf);
+    jlong pcm_cap = pcm ? (*env)->GetDirectBufferCapacity(env, pcm) : -1;
+    void* out = pcm ? (*env)->GetDirectBufferAddress(env, pcm) : NULL;
+    if (!ctx || !b.stream_slot || !b.frame_begin || !b.q || !b.sf || !b.cb || !b.ics || !out || pcm_cap < 0 ||
+        (ms_used && !b.ms_used) || (tns && !b.tns)) {
+        throw_aac(env, ctx, JAAD_ERR_INVALID_ARG);
+        return;
+    }
+    int rc = jaad_decode_batch(ctx, &b, out, (size_t)pcm_cap, (uint32_t)flags);
+    if (rc) throw_aac(env, ctx, rc);
+}
+
+JNIEXPORT void JNICALL Java_net_sourceforge_jaad_aac_gpu_GpuDSP_nativeReset(JNIEnv* env, jclass cls, jlong h,
+                                                                          jint slot) {
+    (void)cls;
+    jaad_ctx* ctx = (jaad_ctx*)(intptr_t)h;
+    int rc = jaad_state_reset(ctx, (uint32_t)slot);
+    if (rc) throw_aac(env, ctx, rc);
+}

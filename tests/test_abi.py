@@ -84,3 +84,14 @@ def test_null_arguments_are_rejected():
     assert L.jaad_decode_batch(None, None, None, 0, 0) == N.ERR_INVALID_ARG
     assert L.jaad_state_reset(None, 0) == N.ERR_INVALID_ARG
     L.jaad_ctx_destroy(None)  # no-op
+
+
+def test_jni_glue_matches_java_natives_in_integration_doc():
+    """Every `native` method of the GpuDSP class shown in INTEGRATION.md has a JNI symbol in jaad_jni.c."""
+    doc = (ROOT / "INTEGRATION.md").read_text()
+    natives = set(re.findall(r"private static native \w+ (\w+)\(", doc))
+    glue = (ROOT / "jaadec_amd" / "csrc" / "jaad_jni.c").read_text()
+    defined = set(re.findall(r"Java_net_sourceforge_jaad_aac_gpu_GpuDSP_(\w+)\(", glue))
+    assert natives and natives == defined
+    for fn in re.findall(r"\b(jaad_[a-z_]+)\(", glue):
+        assert fn in N.EXPORTS, fn

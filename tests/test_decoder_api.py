@@ -1,0 +1,93 @@
+"""The host mirror of the reference interface (A/Decoder.java, A/DecoderConfig.java, S/SampleBuffer.java)."""
+import numpy as np
+import pytest
+
+from jaadec_amd import native as N
+from jaadec_amd.decoder import AACException, Decoder, DecoderConfig, SampleBuffer
+
+
+@pytest.mark.parametrize("asc,aot,sfi,ch", [
+    (bytes([0x12, 0x08]), 2, 4, 1),   # C1: LC, 44.1 kHz, mono
+    (bytes([0x11, 0x90]), 2, 3, 2),   # LC, 48 kHz, stereo
+    (bytes([0x11, 0x88]), 2, 3, 1),
+])
+def test_audio_specific_config(asc, aot, sfi, ch):
+    c = DecoderConfig.decode(asc)
+    assert (c.profile, c.sf_index, c.channel_config) == (aot, sfi, ch)
+    assert c.getSampleLength() == 1024
+    assert c.getChannelCount() == 2  # mono is upmixed (A/DecoderConfig.java:108-115)
+    assert c.getSampleFrequency() == [96000, 88200, 64000, 48000, 44100][sfi]
+
+
+def test_explicit_frequency_maps_to_nearest_index():
+    # AOT 2, sfi 15, 24-bit frequency 44100, ch 2, then GASpecificConfig zeros
+    bits = f"{2:05b}{15:04b}{44100:024b}{2:04b}000"
+    bits += "0" * (-len(bits) % 8)
+    asc = int(bits, 2).to_bytes(len(bits) // 8, "big")
+    assert DecoderConfig.decode(asc).sf_index == 4
+
+
+@pytest.mark.parametrize("asc,msg", [
+    (bytes([0x2B, 0x92, 0x08, 0x00]), "profile"),  # AOT 5 (explicit SBR): the next §8 row, not yet here
+    (bytes([0x0A, 0x10]), "profile"),               # AOT 1 (Main): ICPrediction out of scope
+    (bytes([0x12, 0x0C]), "960"),                   # frameLengthFlag
+    (bytes([0x12]), "end"),
+])
+def test_unsupported_or_truncated_config_raises(asc, msg):
+    with pytest.raises(AACException, match=msg):
+        DecoderConfig.decode(asc)
+
+
+def test_samplebuffer_default_big_endian_and_swap():
+    b = SampleBuffer()
+    assert b.isBigEndian()
+    b._set(bytes([0x12, 0x34, 0xAB, 0xCD]), 48000)
+    b.setBigEndian(False)
+    assert b.getData() == bytes([0x34, 0x12, 0xCD, 0xAB]) and not b.isBigEndian()
+    b.setBigEndian(False)  # no change
+    assert b.getData() == bytes([0x34, 0x12, 0xCD, 0xAB])
+
+
+def test_decoder_create_without_gpu_raises_aacexception():
+    from conftest import gpu_available
+    if gpu_available():
+        pytest.skip("a GPU is present")
+    with pytest.raises(AACException, match="device"):
+        Decoder.create(bytes([0x11, 0x90]))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("big_endian", [True, False])
+def test_decode_frames_matches_oracle(big_endian):
+    from oracle import oracle as O
+    full = N.synth_batch(N.synth_params(3, n_streams=1, frames_per_stream=14))
+    batch, tail = full.split_frames(10)
+    dec = Decoder.create(bytes([0x11, 0x90]))
+    bufs = [SampleBuffer(big_endian) for _ in range(batch.n_frames)]
+    dec.decodeFrames(batch, bufs)
+    flags = N.PCM_BIG_ENDIAN if big_endian else N.PCM_LITTLE_ENDIAN
+    want_full = O.decode_batch(N.make_cfg(), full, O.Streams(1), flags)
+    for i, b in enumerate(bufs):
+        assert b.getData() == want_full[i].tobytes()
+        assert (b.sample_rate, b.channels, b.bits_per_sample) == (48000, 2, 16)
+    # frame-at-a-time decodeFrame continues the same stream state
+    for k in range(4):
+        one, tail = tail.split_frames(1)
+        buf = SampleBuffer(big_endian)
+        dec.decodeFrame(one, buf)
+        assert buf.getData() == want_full[10 + k].tobytes()
+    dec.close()
+
+
+@pytest.mark.gpu
+def test_mixed_endianness_buffers():
+    from oracle import oracle as O
+    batch = N.synth_batch(N.synth_params(2, n_streams=1, frames_per_stream=4))
+    dec = Decoder.create(bytes([0x11, 0x90]))
+    bufs = [SampleBuffer(i % 2 == 0) for i in range(4)]
+    dec.decodeFrames(batch, bufs)
+    be = O.decode_batch(N.make_cfg(), batch, O.Streams(1), N.PCM_BIG_ENDIAN)
+    le = O.decode_batch(N.make_cfg(), batch, O.Streams(1), N.PCM_LITTLE_ENDIAN)
+    for i, b in enumerate(bufs):
+        assert b.getData() == (be if i % 2 == 0 else le)[i].tobytes()
+    dec.close()
