@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define JAAD_ABI_VERSION 1u
+#define JAAD_ABI_VERSION 2u
 
 /* ---- status codes (JNI maps every nonzero code to AACException, A/AACException.java) ---- */
 typedef enum jaad_status {
@@ -79,9 +79,12 @@ typedef struct jaad_stream_cfg {
     uint8_t sf_index;         /* core SampleFrequency index 0..11 (A/SampleFrequency.java:15-26) */
     uint8_t channel_config;   /* 1 = one SCE (mono), 2 = one CPE (stereo)                        */
     uint8_t tns_mode;         /* JAAD_TNS_COMPAT | JAAD_TNS_SPEC                                  */
-    uint8_t sbr;              /* 0; explicit SBR (AOT 5/29) arrives in a later ABI revision       */
-    uint8_t ps;               /* 0; see above                                                     */
-    uint8_t reserved[2];
+    uint8_t sbr;              /* 1 = explicit SBR (AOT 5): jaad_batch.sbr carries one record/frame  */
+    uint8_t ps;               /* 0 (parametric stereo, AOT 29, is not in this ABI revision)       */
+    uint8_t ext_sf_index;     /* SBR output SampleFrequency index (extensionSampleFrequency of the
+                                 ASC, A/DecoderConfig.java:184-198); must be the core index - 3,
+                                 i.e. twice the core rate (bs_samplerate_mode = 1)                */
+    uint8_t reserved;
 } jaad_stream_cfg;
 
 /*
@@ -132,6 +135,38 @@ typedef struct jaad_tns {
 } jaad_tns;
 
 /*
+ * SBR side information of one frame, as the reference's parser leaves it after sbr_data
+ * (A/sbr/SBR.java:161-245, SBR1.sbr_data :34-60, SBR2.sbr_data :35-135).  Host memory only.
+ */
+typedef struct jaad_sbr_header {   /* Header.decode (A/sbr/Header.java:24-62), defaults applied */
+    uint8_t amp_res, start_freq, stop_freq, xover_band;
+    uint8_t freq_scale, alter_scale, noise_bands, limiter_bands;
+    uint8_t limiter_gains, interpol_freq, smoothing_mode, reserved;
+} jaad_sbr_header;
+
+typedef struct jaad_sbr_channel {  /* Channel fields after sbr_data (A/sbr/Channel.java) */
+    uint64_t add_harmonic;         /* bit n = bs_add_harmonic[n], n < N_high (sinusoidal_coding)     */
+    int16_t E[5][64];              /* [env][band] envelope scalefactors after extract_envelope_data  */
+    int16_t Q[2][8];               /* [noise env][band] after extract_noise_floor_data (N_Q <= 5)   */
+    uint8_t frame_class;           /* FrameClass ordinal: FIXFIX, FIXVAR, VARFIX, VARVAR            */
+    uint8_t L_E, L_Q, bs_pointer;  /* envelopes (1..5), noise envelopes (1..2), pointer             */
+    uint8_t t_E[6];                /* envelope time borders (envelope_time_border_vector, :455-542) */
+    uint8_t t_Q[3];                /* noise time borders (noise_floor_time_border_vector, :544-556) */
+    uint8_t f[6];                  /* frequency resolution per envelope (0 = LO_RES, 1 = HI_RES)    */
+    uint8_t invf_mode[5];          /* bs_invf_mode per noise band                                   */
+    uint8_t add_harmonic_flag;
+    uint8_t reserved[7];
+} jaad_sbr_channel;                /* 712 bytes */
+
+typedef struct jaad_sbr_frame {
+    uint8_t header_present;        /* bs_header_flag: hdr below is this frame's sbr_header           */
+    uint8_t coupling;              /* bs_coupling (CPE only)                                         */
+    uint8_t reserved[2];
+    jaad_sbr_header hdr;
+    jaad_sbr_channel ch[2];        /* ch[1] unused for an SCE                                        */
+} jaad_sbr_frame;                  /* 1440 bytes */
+
+/*
  * A batch: n_frames frames (raw_data_blocks) of one channel configuration.  Frames are grouped
  * in runs: run r holds consecutive-in-time frames [frame_begin[r], frame_begin[r+1]) of the
  * stream whose persistent DSP state (IMDCT overlap, ...) lives in context slot stream_slot[r].
@@ -158,6 +193,7 @@ typedef struct jaad_batch {
     const jaad_ics_info* ics;     /* [dev] [ch-frame]                                              */
     const uint64_t* ms_used;      /* [dev] [frame][2] bit idx = g*max_sfb+sfb (CPE only, else NULL) */
     const jaad_tns* tns;          /* [dev] [ch-frame] or NULL when no ch-frame sets JAAD_ICS_TNS    */
+    const jaad_sbr_frame* sbr;    /* host [frame] when cfg.sbr, else NULL                            */
 } jaad_batch;
 
 typedef struct jaad_ctx jaad_ctx;

@@ -32,11 +32,12 @@ typedef struct jaad_synth_params {
     uint8_t global_gain;      /* centre of the scalefactor random walk (130)                 */
     uint8_t escape_permille;  /* per-mille of bins replaced by escapes |q| in [16,1023]      */
     uint8_t common_window;    /* CPE: 1 = common_window (C2/C3)                              */
-    uint8_t reserved[2];
+    uint8_t sbr;              /* 1: also emit SBR records (jaad_synth_sbr), C4              */
+    uint8_t sbr_level;        /* centre of the envelope-scalefactor walk, 3 dB units        */
     uint32_t pns_state0;      /* static ICStream.randomState before the first ch-frame       */
 } jaad_synth_params;
 
-/* defaults for a BASELINE.json config id (1..3: C1 mono 44.1k, C2, C3) */
+/* defaults for a BASELINE.json config id (1..4: C1 mono 44.1k, C2, C3, C4 HE-AAC v1) */
 void jaad_synth_default(int config_id, jaad_synth_params* p);
 
 /* Fill caller-allocated arrays (sizes: ch = channel_config, F = n_streams*frames_per_stream):
@@ -47,6 +48,13 @@ void jaad_synth_default(int config_id, jaad_synth_params* p);
 int jaad_synth_generate(const jaad_synth_params* p, int16_t* q, uint8_t* sf, uint8_t* cb, jaad_ics_info* ics,
                         uint64_t* ms_used, jaad_tns* tns, uint32_t* stream_slot, uint32_t* frame_begin,
                         int threads);
+
+/* SBR records (one jaad_sbr_frame per frame, stream-major like jaad_synth_generate) for the C4
+ * workload: header every frame with the Header.java defaults, start_freq 5,
+ * stop_freq 9, xover 0; FIXFIX grids with 1 or 2 envelopes; envelope/noise scalefactors as
+ * bounded random walks; invf_mode uniform; sinusoids rare; no coupling.  Every band of E[][64]
+ * and Q[][8] is filled (the decoder reads only n[f] / N_Q of them). */
+int jaad_synth_sbr(const jaad_synth_params* p, jaad_sbr_frame* out, int threads);
 
 #ifdef __cplusplus
 }

@@ -189,6 +189,64 @@ void gen_stream(const Gen& G, uint32_t s)
     }
 }
 
+void gen_sbr_stream(const jaad_synth_params& P, jaad_sbr_frame* out, uint32_t s)
+{
+    const int nch = P.channel_config == 2 ? 2 : 1;
+    SplitMix64 r{P.seed ^ (0x5B5B5B5Bull + (uint64_t)s * 0xD1B54A32D192ED03ull)};
+    for (int i = 0; i < 4; i++) r.next();
+    int lvl[2][64], qv[2][5];
+    for (int c = 0; c < 2; c++) {
+        for (int k = 0; k < 64; k++) lvl[c][k] = P.sbr_level - (int)r.below(5);
+        for (int k = 0; k < 5; k++) qv[c][k] = 8 + (int)r.below(16);
+    }
+    for (uint32_t fi = 0; fi < P.frames_per_stream; fi++) {
+        jaad_sbr_frame& F = out[(size_t)s * P.frames_per_stream + fi];
+        std::memset(&F, 0, sizeof F);
+        F.header_present = 1;
+        F.coupling = 0;
+        // Header.java defaults (A/sbr/Header.java:12-22,44-60) with start 5 / stop 9 / xover 0
+        F.hdr = jaad_sbr_header{1, 5, 9, 0, 2, 1, 2, 2, 2, 1, 1, 0};
+        for (int c = 0; c < nch; c++) {
+            jaad_sbr_channel& C = F.ch[c];
+            const int L_E = 1 + (int)r.below(2);  // FIXFIX: bs_num_env = 1 << (0|1)
+            const int fres = (int)r.below(2);
+            C.frame_class = 0;
+            C.L_E = (uint8_t)L_E;
+            C.L_Q = (uint8_t)(L_E > 1 ? 2 : 1);
+            C.bs_pointer = 0;
+            // envelope_time_border_vector / noise_floor_time_border_vector for FIXFIX (A/sbr/Channel.java:455-556)
+            C.t_E[0] = 0;
+            C.t_E[L_E] = 32;
+            if (L_E == 2) C.t_E[1] = 16;
+            C.t_Q[0] = 0;
+            C.t_Q[1] = (uint8_t)(L_E == 1 ? 32 : 16);
+            C.t_Q[2] = (uint8_t)(L_E == 1 ? 0 : 32);
+            for (int l = 0; l < L_E; l++) C.f[l] = (uint8_t)fres;
+            const bool amp_res = !(L_E == 1);  // amp_res 1 in the header; FIXFIX with one envelope -> 1.5 dB
+            for (int l = 0; l < L_E; l++)
+                for (int k = 0; k < 64; k++) {
+                    int d = (int)r.below(3) - 1;
+                    lvl[c][k] += d;
+                    if (lvl[c][k] > P.sbr_level) lvl[c][k] = P.sbr_level;
+                    if (lvl[c][k] < P.sbr_level - 6) lvl[c][k] = P.sbr_level - 6;
+                    C.E[l][k] = (int16_t)(amp_res ? lvl[c][k] : 2 * lvl[c][k] + (int)r.below(2));
+                }
+            for (int l = 0; l < C.L_Q; l++)
+                for (int k = 0; k < 5; k++) {
+                    qv[c][k] += (int)r.below(5) - 2;
+                    if (qv[c][k] < 0) qv[c][k] = 0;
+                    if (qv[c][k] > 30) qv[c][k] = 30;
+                    C.Q[l][k] = (int16_t)qv[c][k];
+                }
+            for (int k = 0; k < 5; k++) C.invf_mode[k] = (uint8_t)r.below(4);
+            C.add_harmonic_flag = (uint8_t)r.percent(30);
+            if (C.add_harmonic_flag)
+                for (int k = 0; k < 64; k++)
+                    if (r.percent(5)) C.add_harmonic |= 1ull << k;
+        }
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -202,6 +260,15 @@ void jaad_synth_default(int config_id, jaad_synth_params* p)
     p->common_window = 1;
     p->pns_state0 = 0x1F2E3D4Cu;  // ICStream.randomState initial value (A/syntax/ICStream.java:26)
     switch (config_id) {
+    case 4:  // C4: HE-AAC v1 24 -> 48 kHz stereo, 32 768 frames = 128 streams x 256
+        p->n_streams = 128;
+        p->frames_per_stream = 256;
+        p->sf_index = 6;
+        p->channel_config = 2;
+        p->ms_mode = 1;
+        p->sbr = 1;
+        p->sbr_level = 18;
+        break;
     case 1:  // C1: AAC-LC 44.1 kHz mono, one frame
         p->n_streams = 1;
         p->frames_per_stream = 1;
@@ -272,6 +339,22 @@ int jaad_synth_generate(const jaad_synth_params* p, int16_t* q, uint8_t* sf, uin
         frame_begin[s] = s * p->frames_per_stream;
     }
     frame_begin[ns] = ns * p->frames_per_stream;
+    return JAAD_OK;
+}
+
+int jaad_synth_sbr(const jaad_synth_params* p, jaad_sbr_frame* out, int threads)
+{
+    if (!p || !out || (p->channel_config != 1 && p->channel_config != 2)) return JAAD_ERR_INVALID_ARG;
+    const uint32_t ns = p->n_streams;
+    if (threads <= 0) threads = (int)std::thread::hardware_concurrency();
+    if (threads < 1) threads = 1;
+    if ((uint32_t)threads > ns) threads = (int)(ns ? ns : 1);
+    std::vector<std::thread> pool;
+    for (int t = 0; t < threads; t++)
+        pool.emplace_back([&, t] {
+            for (uint32_t s = t; s < ns; s += threads) gen_sbr_stream(*p, out, s);
+        });
+    for (auto& th : pool) th.join();
     return JAAD_OK;
 }
 

@@ -17,7 +17,7 @@ import os as _os
 LIB_PATH = Path(_os.environ["JAAD_LIB"]) if _os.environ.get("JAAD_LIB") else PKG / "libjaadgpu.so"
 SYNTH_PATH = PKG / "libjaadsynth.so"
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 # status codes (jaad_status)
 OK, ERR_INVALID_ARG, ERR_NO_DEVICE, ERR_HIP, ERR_UNSUPPORTED, ERR_BITSTREAM, ERR_NOMEM, ERR_ABI = 0, -1, -2, -3, -4, -5, -6, -7
@@ -37,17 +37,28 @@ TNS_FILTER_DTYPE = np.dtype([("window", "u1"), ("length", "u1"), ("order", "u1")
 TNS_DTYPE = np.dtype([("n_filters", "u1"), ("reserved", "u1", (3,)), ("filt", TNS_FILTER_DTYPE, (8,))])
 assert TNS_DTYPE.itemsize == 196
 
+SBR_HEADER_DTYPE = np.dtype([(n, "u1") for n in (
+    "amp_res", "start_freq", "stop_freq", "xover_band", "freq_scale", "alter_scale", "noise_bands",
+    "limiter_bands", "limiter_gains", "interpol_freq", "smoothing_mode", "reserved")])
+SBR_CHANNEL_DTYPE = np.dtype([
+    ("add_harmonic", "<u8"), ("E", "<i2", (5, 64)), ("Q", "<i2", (2, 8)), ("frame_class", "u1"), ("L_E", "u1"),
+    ("L_Q", "u1"), ("bs_pointer", "u1"), ("t_E", "u1", (6,)), ("t_Q", "u1", (3,)), ("f", "u1", (6,)),
+    ("invf_mode", "u1", (5,)), ("add_harmonic_flag", "u1"), ("reserved", "u1", (7,))])
+SBR_FRAME_DTYPE = np.dtype([("header_present", "u1"), ("coupling", "u1"), ("reserved", "u1", (2,)),
+                            ("hdr", SBR_HEADER_DTYPE), ("ch", SBR_CHANNEL_DTYPE, (2,))])
+assert SBR_CHANNEL_DTYPE.itemsize == 712 and SBR_FRAME_DTYPE.itemsize == 1440
+
 
 class StreamCfg(C.Structure):
     _fields_ = [("abi_version", C.c_uint32), ("profile", C.c_uint8), ("sf_index", C.c_uint8),
                 ("channel_config", C.c_uint8), ("tns_mode", C.c_uint8), ("sbr", C.c_uint8), ("ps", C.c_uint8),
-                ("reserved", C.c_uint8 * 2)]
+                ("ext_sf_index", C.c_uint8), ("reserved", C.c_uint8)]
 
 
 class BatchStruct(C.Structure):
     _fields_ = [("n_frames", C.c_uint32), ("n_runs", C.c_uint32), ("stream_slot", C.c_void_p),
                 ("frame_begin", C.c_void_p), ("q", C.c_void_p), ("sf", C.c_void_p), ("cb", C.c_void_p),
-                ("ics", C.c_void_p), ("ms_used", C.c_void_p), ("tns", C.c_void_p)]
+                ("ics", C.c_void_p), ("ms_used", C.c_void_p), ("tns", C.c_void_p), ("sbr", C.c_void_p)]
 
 
 class SynthParams(C.Structure):
@@ -55,7 +66,8 @@ class SynthParams(C.Structure):
                 ("sf_index", C.c_uint8), ("channel_config", C.c_uint8), ("window_switching", C.c_uint8),
                 ("tns_percent", C.c_uint8), ("pns_percent", C.c_uint8), ("is_percent", C.c_uint8),
                 ("ms_mode", C.c_uint8), ("global_gain", C.c_uint8), ("escape_permille", C.c_uint8),
-                ("common_window", C.c_uint8), ("reserved", C.c_uint8 * 2), ("pns_state0", C.c_uint32)]
+                ("common_window", C.c_uint8), ("sbr", C.c_uint8), ("sbr_level", C.c_uint8),
+                ("pns_state0", C.c_uint32)]
 
 
 # every symbol include/jaad_gpu.h declares (checked by tests/test_abi.py)
@@ -116,6 +128,7 @@ def synth_lib() -> C.CDLL:
         S.jaad_synth_default.argtypes = [C.c_int, C.POINTER(SynthParams)]
         S.jaad_synth_default.restype = None
         S.jaad_synth_generate.argtypes = [C.POINTER(SynthParams)] + [C.c_void_p] * 8 + [C.c_int]
+        S.jaad_synth_sbr.argtypes = [C.POINTER(SynthParams), C.c_void_p, C.c_int]
         _synth = S
     return _synth
 
@@ -144,6 +157,7 @@ class Batch:
     stream_slot: np.ndarray  # uint32 [n_runs]
     frame_begin: np.ndarray  # uint32 [n_runs+1]
     nch: int
+    sbr: np.ndarray | None = None  # SBR_FRAME_DTYPE [nf] (host) when the config has SBR
 
     @property
     def n_frames(self) -> int:
@@ -154,7 +168,7 @@ class Batch:
             assert a.flags["C_CONTIGUOUS"]
         return BatchStruct(self.n_frames, len(self.stream_slot), _ptr(self.stream_slot), _ptr(self.frame_begin),
                            _ptr(self.q), _ptr(self.sf), _ptr(self.cb), _ptr(self.ics), _ptr(self.ms_used),
-                           _ptr(self.tns))
+                           _ptr(self.tns), _ptr(self.sbr))
 
     def select_runs(self, runs) -> "Batch":
         """Sub-batch made of the given runs (frames renumbered, slots kept)."""
@@ -169,7 +183,8 @@ class Batch:
                      np.ascontiguousarray(self.cb[cfr]), np.ascontiguousarray(self.ics[cfr]),
                      None if self.ms_used is None else np.ascontiguousarray(self.ms_used[frames]),
                      None if self.tns is None else np.ascontiguousarray(self.tns[cfr]),
-                     np.ascontiguousarray(self.stream_slot[runs]).astype(np.uint32), begin, self.nch)
+                     np.ascontiguousarray(self.stream_slot[runs]).astype(np.uint32), begin, self.nch,
+                     None if self.sbr is None else np.ascontiguousarray(self.sbr[frames]))
 
     def split_frames(self, cut: int) -> tuple["Batch", "Batch"]:
         """Split every run at its frame `cut` (for multi-call continuation tests)."""
@@ -192,7 +207,8 @@ class Batch:
                          np.ascontiguousarray(self.cb[cfr]), np.ascontiguousarray(self.ics[cfr]),
                          None if self.ms_used is None else np.ascontiguousarray(self.ms_used[frames]),
                          None if self.tns is None else np.ascontiguousarray(self.tns[cfr]),
-                         self.stream_slot.copy(), begin, self.nch)
+                         self.stream_slot.copy(), begin, self.nch,
+                         None if self.sbr is None else np.ascontiguousarray(self.sbr[frames]))
 
         return mk(a_frames, la), mk(b_frames, lb)
 
@@ -223,15 +239,26 @@ def synth_batch(p: SynthParams, with_tns: bool | None = None, threads: int = 0) 
                                          _ptr(slot), _ptr(begin), threads)
     if rc:
         raise JaadError(rc, "jaad_synth_generate")
-    return Batch(q, sf, cb, ics, ms, tns, slot, begin, nch)
+    sbr = None
+    if p.sbr:
+        sbr = np.zeros(nf, SBR_FRAME_DTYPE)
+        rc = synth_lib().jaad_synth_sbr(C.byref(p), _ptr(sbr), threads)
+        if rc:
+            raise JaadError(rc, "jaad_synth_sbr")
+    return Batch(q, sf, cb, ics, ms, tns, slot, begin, nch, sbr)
 
 
-def make_cfg(sf_index: int = 3, channel_config: int = 2, tns_mode: int = TNS_COMPAT) -> StreamCfg:
-    return StreamCfg(ABI_VERSION, 2, sf_index, channel_config, tns_mode, 0, 0)
+def make_cfg(sf_index: int = 3, channel_config: int = 2, tns_mode: int = TNS_COMPAT, sbr: bool = False) -> StreamCfg:
+    """jaad_stream_cfg; with sbr the output rate is twice the core rate (index - 3)."""
+    return StreamCfg(ABI_VERSION, 2, sf_index, channel_config, tns_mode, int(sbr), 0, sf_index - 3 if sbr else 0, 0)
 
 
-def pcm_frame_bytes(flags: int) -> int:
-    return 1024 * 2 * (4 if flags & PCM_FLOAT32 else 2)
+def cfg_for(p: SynthParams, tns_mode: int = TNS_COMPAT) -> StreamCfg:
+    return make_cfg(p.sf_index, p.channel_config, tns_mode, bool(p.sbr))
+
+
+def pcm_frame_bytes(flags: int, sbr: bool = False) -> int:
+    return (2048 if sbr else 1024) * 2 * (4 if flags & PCM_FLOAT32 else 2)
 
 
 class Context:
@@ -266,7 +293,7 @@ class Context:
 
     def decode(self, batch: Batch, flags: int = PCM_BIG_ENDIAN) -> np.ndarray:
         """Host-buffer batch decode -> PCM bytes (uint8 [n_frames, frame_bytes])."""
-        nb = pcm_frame_bytes(flags)
+        nb = pcm_frame_bytes(flags, bool(self.cfg.sbr))
         out = np.empty((batch.n_frames, nb), np.uint8)
         bs = batch.struct()
         self._check(lib().jaad_decode_batch(self.h, C.byref(bs), _ptr(out), out.nbytes, flags), "jaad_decode_batch")

@@ -436,11 +436,23 @@ int orc_pcm_pack(const float* const* ch, int n_ch, int len, uint32_t flags, void
 /* Frame driver: SCE.process (A/syntax/SCE.java:90-133) / CPE.process (A/syntax/CPE.java:149-208)
  * + SyntacticElements.process mono->stereo duplication (A/syntax/SyntacticElements.java:235-248) */
 /* ------------------------------------------------------------------------------------------ */
+size_t orc_stream_bytes(void) { return sizeof(orc_stream); }
+
+void orc_streams_free(orc_stream* streams, int n)
+{
+    for (int i = 0; i < n; i++) {
+        free(streams[i].sbr);
+        streams[i].sbr = NULL;
+    }
+}
+
+static int frame_samples(const jaad_stream_cfg* cfg) { return cfg->sbr ? 2048 : 1024; }
+
 static int decode_frame(const jaad_stream_cfg* cfg, orc_stream* st, const jaad_batch* b, uint32_t f,
                         uint32_t* rand_state, unsigned char* pcm, uint32_t flags)
 {
     const int nch = cfg->channel_config == 2 ? 2 : 1;
-    float iq[2][1024], data[2][1024];
+    float iq[2][1024], data[2][2048];
     int rc;
     for (int c = 0; c < nch; c++) {
         size_t cf = (size_t)f * nch + c;
@@ -467,6 +479,20 @@ static int decode_frame(const jaad_stream_cfg* cfg, orc_stream* st, const jaad_b
         orc_filterbank(info->window_sequence, info->window_shape, info->window_shape_prev, iq[c], data[c],
                        st->overlap[c]);
     }
+    if (cfg->sbr) {
+        /* CPE.process / SCE.process -> SBR.process (A/syntax/CPE.java:195-204, SCE.java:122-133) */
+        if (!st->sbr) {
+            st->sbr = (orc_sbr*)calloc(1, orc_sbr_bytes());
+            if (!st->sbr) return JAAD_ERR_NOMEM;
+            orc_sbr_init(st->sbr, cfg->ext_sf_index);
+        }
+        rc = orc_sbr_decode(st->sbr, &b->sbr[f], nch);
+        if (rc) return rc;
+        orc_sbr_process(st->sbr, data[0], data[1], nch);
+        const float* chans[2] = {data[0], data[1]};
+        orc_pcm_pack(chans, 2, 2048, flags, pcm);
+        return JAAD_OK;
+    }
     const float* chans[2] = {data[0], nch == 2 ? data[1] : data[0]};
     orc_pcm_pack(chans, 2, 1024, flags, pcm);
     return JAAD_OK;
@@ -476,7 +502,8 @@ static int check_batch(const jaad_stream_cfg* cfg, const jaad_batch* b, size_t p
 {
     if (!cfg || !b || (!b->q && b->n_frames) || !b->sf || !b->cb || !b->ics || !b->frame_begin) return JAAD_ERR_INVALID_ARG;
     if (cfg->channel_config != 1 && cfg->channel_config != 2) return JAAD_ERR_UNSUPPORTED;
-    size_t per = (size_t)1024 * 2 * ((flags & JAAD_PCM_FLOAT32) ? 4 : 2);
+    if (cfg->sbr && (!b->sbr || cfg->ext_sf_index + 3 != cfg->sf_index)) return JAAD_ERR_INVALID_ARG;
+    size_t per = (size_t)frame_samples(cfg) * 2 * ((flags & JAAD_PCM_FLOAT32) ? 4 : 2);
     if (pcm_bytes < per * b->n_frames) return JAAD_ERR_INVALID_ARG;
     return JAAD_OK;
 }
@@ -486,7 +513,7 @@ int orc_decode_batch(const jaad_stream_cfg* cfg, orc_stream* streams, const jaad
 {
     int rc = check_batch(cfg, b, pcm_bytes, flags);
     if (rc) return rc;
-    size_t per = (size_t)1024 * 2 * ((flags & JAAD_PCM_FLOAT32) ? 4 : 2);
+    size_t per = (size_t)frame_samples(cfg) * 2 * ((flags & JAAD_PCM_FLOAT32) ? 4 : 2);
     uint32_t rs = 0;
     for (uint32_t r = 0; r < b->n_runs; r++) {
         orc_stream* st = &streams[b->stream_slot[r]];
@@ -531,7 +558,7 @@ int orc_decode_batch_mt(const jaad_stream_cfg* cfg, orc_stream* streams, const j
     if ((uint32_t)threads > b->n_runs) threads = (int)(b->n_runs ? b->n_runs : 1);
     mt_job jobs[256];
     pthread_t tid[256];
-    size_t per = (size_t)1024 * 2 * ((flags & JAAD_PCM_FLOAT32) ? 4 : 2);
+    size_t per = (size_t)frame_samples(cfg) * 2 * ((flags & JAAD_PCM_FLOAT32) ? 4 : 2);
     for (int t = 0; t < threads; t++) {
         jobs[t] = (mt_job){cfg, streams, b, (unsigned char*)pcm_out, flags, per,
                            (uint32_t)((uint64_t)b->n_runs * t / threads),

@@ -22,10 +22,16 @@
 extern "C" {
 #endif
 
-/* per-stream state of the restated decoder: ICStream.overlap per channel (A/syntax/ICStream.java:47) */
+typedef struct orc_sbr orc_sbr;
+
+/* per-stream state of the restated decoder: ICStream.overlap per channel (A/syntax/ICStream.java:47)
+ * and the SBR object of the channel element (allocated on first use, freed by orc_streams_free) */
 typedef struct orc_stream {
     float overlap[2][1024];
+    orc_sbr* sbr;
 } orc_stream;
+size_t orc_stream_bytes(void);
+void orc_streams_free(orc_stream* streams, int n);
 
 /* FFT.process (A/filterbank/FFT.java:48-135), in place, n = 64 or 512 */
 void orc_fft(float (*data)[2], int n, int forward);
@@ -59,6 +65,22 @@ int orc_decode_batch(const jaad_stream_cfg* cfg, orc_stream* streams, const jaad
 /* Same, multithreaded over runs (runs are independent streams); threads <= 0: all cores */
 int orc_decode_batch_mt(const jaad_stream_cfg* cfg, orc_stream* streams, const jaad_batch* batch,
                         void* pcm_out, size_t pcm_bytes, uint32_t flags, int threads);
+
+/* ---- SBR (jaad_oracle_sbr.c) ---- */
+size_t orc_sbr_bytes(void);
+void orc_sbr_init(orc_sbr* s, int out_sf_index);
+/* SBR.decode for one frame's parsed SBR data (header handling, NoiseEnvelope dequantisation) */
+int orc_sbr_decode(orc_sbr* s, const jaad_sbr_frame* fr, int nch);
+/* SBR2.process / SBR1.process (no PS): 2048-float channel buffers, first 1024 = core output */
+void orc_sbr_process(orc_sbr* s, float* left, float* right, int nch);
+/* DCT.dct4_kernel (A/sbr/DCT.java:347-391) on copies of the inputs */
+void orc_sbr_dct4(const float* in_re, const float* in_im, float* out_re, float* out_im);
+/* AnalysisFilterbank.sbr_qmf_analysis_32 over one frame: X[32][64][2] */
+void orc_qmf_analysis_frame(float* v1280, int* v_index, const float* input1024, float* X, int kx);
+/* SynthesisFilterbank64.synthesis over one frame: X[32][64][2] -> 2048 samples */
+void orc_qmf_synthesis_frame(float* v2560, int* v_index, const float* X, float* output2048);
+/* derived frequency tables for a header: info = k0 k2 kx M N_master N_high N_low N_Q noPatches N_L */
+int orc_sbr_table_info(const jaad_sbr_header* h, int out_sf_index, int* info, int* f_master, int* f_table_lim);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,1175 @@
+/*
+ * jaad_oracle_sbr.c -- TEST INFRASTRUCTURE ONLY (see jaad_oracle.h for the parity status).
+ *
+ * Plain-C restatement of the reference's SBR (HE-AAC v1) path, A/ = aac/src/main/java/net/
+ * sourceforge/jaad/aac/.  Structure follows the Java classes (SBR / SBR1 / SBR2 / Channel /
+ * FBT / NoiseEnvelope / HFGeneration / HFAdjustment / AnalysisFilterbank / SynthesisFilterbank64 /
+ * DCT) so each function can be read against its Java original; every binary32 expression keeps
+ * the Java evaluation order (built with -ffp-contract=off).  Inputs are the values the Java
+ * parser leaves in Channel after sbr_data (grid, envelope/noise scalefactors after delta
+ * decoding, invf modes, sinusoid flags) -- see jaad_sbr_frame in include/jaad_gpu.h.
+ */
+#include "jaad_oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../jaadec_amd/csrc/tables/jaad_sbr_tables.inc"
+
+#if defined(__FP_FAST_FMAF) || defined(__FAST_MATH__)
+#error "the oracle must be compiled without fast-math / FMA contraction"
+#endif
+
+enum { MAX_NTSR = 32, MAX_M = 49, MAX_L_E = 5, T_HFGEN = 8, T_HFADJ = 2, NUM_TIME_SLOTS = 16, RATE = 2,
+       NTSRHFG = 40, LO_RES = 0, HI_RES = 1 };
+enum { FIXFIX = 0, FIXVAR = 1, VARFIX = 2, VARVAR = 3 };
+
+typedef struct orc_sbr_channel {
+    int amp_res;
+    int L_E, L_E_prev, L_Q;
+    int t_E[MAX_L_E + 1], t_Q[3], f[MAX_L_E + 1], f_prev;
+    float G_temp_prev[5][64], Q_temp_prev[5][64];
+    int GQ_ringbuf_index;
+    int E[64][MAX_L_E], E_prev[64];
+    float E_orig[64][MAX_L_E], E_curr[64][MAX_L_E];
+    int Q[64][2];
+    float Q_div[64][2], Q_div2[64][2];
+    int Q_prev[64];
+    int l_A;
+    int bs_invf_mode[MAX_L_E], bs_invf_mode_prev[MAX_L_E];
+    float bwArray[64], bwArray_prev[64];
+    int bs_add_harmonic[64], bs_add_harmonic_prev[64];
+    int index_noise_prev, psi_is_prev, prevEnvIsShort;
+    int bs_frame_class, bs_pointer;
+    int bs_add_harmonic_flag, bs_add_harmonic_flag_prev;
+    float qmfa_v[1280];
+    int qmfa_index;
+    float Xsbr[NTSRHFG][64][2];
+    float qmfs_v[2560];
+    int qmfs_index;
+} orc_sbr_channel;
+
+struct orc_sbr {
+    int out_sf_index; /* SBR.sample_rate (output frequency, A/sbr/SBR.java:102) */
+    int k0, kx, M, N_master, N_high, N_low, N_Q, N_L[4], n[2];
+    int f_master[64], f_table_res[2][64], f_table_noise[64], f_table_lim[4][64], table_map_k_to_g[64];
+    int kx_prev, bsco, bsco_prev, M_prev;
+    int reset, frame;
+    int noPatches, patchNoSubbands[64], patchStartSubband[64];
+    int have_hdr;
+    jaad_sbr_header hdr, hdr_saved;
+    int have_saved;
+    int coupling;
+    orc_sbr_channel ch[2];
+};
+
+size_t orc_sbr_bytes(void) { return sizeof(orc_sbr); }
+
+void orc_sbr_init(orc_sbr* s, int out_sf_index)
+{
+    memset(s, 0, sizeof *s);
+    s->out_sf_index = out_sf_index;
+    for (int c = 0; c < 2; c++) s->ch[c].prevEnvIsShort = -1; /* A/sbr/Channel.java:59 */
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* DCT.fft_dif / dct4_kernel (A/sbr/DCT.java:135-391)                                          */
+/* ------------------------------------------------------------------------------------------ */
+static void fft_dif(float* Real, float* Imag)
+{
+    float w_real, w_imag, p1r, p1i, p2r, p2i;
+    for (int i = 0; i < 16; i++) { /* stage 1 (:143-164) */
+        int i2 = i + 16;
+        p1r = Real[i]; p1i = Imag[i]; p2r = Real[i2]; p2i = Imag[i2];
+        w_real = JAAD_DCT_W_RE[i]; w_imag = JAAD_DCT_W_IM[i];
+        p1r -= p2r; p1i -= p2i;
+        Real[i] += p2r; Imag[i] += p2i;
+        Real[i2] = (p1r * w_real) - (p1i * w_imag);
+        Imag[i2] = (p1r * w_imag) + (p1i * w_real);
+    }
+    for (int j = 0, w_index = 0; j < 8; j++, w_index += 2) { /* stage 2 (:166-207) */
+        w_real = JAAD_DCT_W_RE[w_index]; w_imag = JAAD_DCT_W_IM[w_index];
+        for (int h = 0; h < 2; h++) {
+            int i = j + 16 * h, i2 = i + 8;
+            p1r = Real[i]; p1i = Imag[i]; p2r = Real[i2]; p2i = Imag[i2];
+            p1r -= p2r; p1i -= p2i;
+            Real[i] += p2r; Imag[i] += p2i;
+            Real[i2] = (p1r * w_real) - (p1i * w_imag);
+            Imag[i2] = (p1r * w_imag) + (p1i * w_real);
+        }
+    }
+    for (int i = 0; i < 32; i += 8) { /* stage 3 (:212-227) */
+        int i2 = i + 4;
+        p1r = Real[i]; p1i = Imag[i]; p2r = Real[i2]; p2i = Imag[i2];
+        Real[i] += p2r; Imag[i] += p2i;
+        Real[i2] = p1r - p2r; Imag[i2] = p1i - p2i;
+    }
+    w_real = JAAD_DCT_W_RE[4];
+    for (int i = 1; i < 32; i += 8) { /* :230-249 */
+        int i2 = i + 4;
+        p1r = Real[i]; p1i = Imag[i]; p2r = Real[i2]; p2i = Imag[i2];
+        p1r -= p2r; p1i -= p2i;
+        Real[i] += p2r; Imag[i] += p2i;
+        Real[i2] = (p1r + p1i) * w_real;
+        Imag[i2] = (p1i - p1r) * w_real;
+    }
+    for (int i = 2; i < 32; i += 8) { /* :250-265 */
+        int i2 = i + 4;
+        p1r = Real[i]; p1i = Imag[i]; p2r = Real[i2]; p2i = Imag[i2];
+        Real[i] += p2r; Imag[i] += p2i;
+        Real[i2] = p1i - p2i;
+        Imag[i2] = p2r - p1r;
+    }
+    w_real = JAAD_DCT_W_RE[12];
+    for (int i = 3; i < 32; i += 8) { /* :268-287 */
+        int i2 = i + 4;
+        p1r = Real[i]; p1i = Imag[i]; p2r = Real[i2]; p2i = Imag[i2];
+        p1r -= p2r; p1i -= p2i;
+        Real[i] += p2r; Imag[i] += p2i;
+        Real[i2] = (p1r - p1i) * w_real;
+        Imag[i2] = (p1r + p1i) * w_real;
+    }
+    for (int i = 0; i < 32; i += 4) { /* stage 4 (:291-306) */
+        int i2 = i + 2;
+        p1r = Real[i]; p1i = Imag[i]; p2r = Real[i2]; p2i = Imag[i2];
+        Real[i] += p2r; Imag[i] += p2i;
+        Real[i2] = p1r - p2r; Imag[i2] = p1i - p2i;
+    }
+    for (int i = 1; i < 32; i += 4) { /* :307-322 */
+        int i2 = i + 2;
+        p1r = Real[i]; p1i = Imag[i]; p2r = Real[i2]; p2i = Imag[i2];
+        Real[i] += p2r; Imag[i] += p2i;
+        Real[i2] = p1i - p2i;
+        Imag[i2] = p2r - p1r;
+    }
+    for (int i = 0; i < 32; i += 2) { /* stage 5 (:326-341) */
+        int i2 = i + 1;
+        p1r = Real[i]; p1i = Imag[i]; p2r = Real[i2]; p2i = Imag[i2];
+        Real[i] += p2r; Imag[i] += p2i;
+        Real[i2] = p1r - p2r; Imag[i2] = p1i - p2i;
+    }
+}
+
+/* in_real/in_imag are clobbered, as in the Java */
+static void dct4_kernel(float* in_real, float* in_imag, float* out_real, float* out_imag)
+{
+    const float* t = JAAD_DCT4_64_TAB;
+    for (int i = 0; i < 32; i++) { /* :353-360 */
+        float x_re = in_real[i], x_im = in_imag[i];
+        float tmp = (x_re + x_im) * t[i];
+        in_real[i] = (x_im * t[i + 64]) + tmp;
+        in_imag[i] = (x_re * t[i + 32]) + tmp;
+    }
+    fft_dif(in_real, in_imag);
+    for (int i = 0; i < 16; i++) { /* :368-377 */
+        int r = JAAD_DCT_BIT_REV[i];
+        float x_re = in_real[r], x_im = in_imag[r];
+        float tmp = (x_re + x_im) * t[i + 3 * 32];
+        out_real[i] = (x_im * t[i + 5 * 32]) + tmp;
+        out_imag[i] = (x_re * t[i + 4 * 32]) + tmp;
+    }
+    out_imag[16] = (in_imag[1] - in_real[1]) * t[16 + 3 * 32]; /* :379-380 */
+    out_real[16] = (in_real[1] + in_imag[1]) * t[16 + 3 * 32];
+    for (int i = 17; i < 32; i++) { /* :381-389 */
+        int r = JAAD_DCT_BIT_REV[i];
+        float x_re = in_real[r], x_im = in_imag[r];
+        float tmp = (x_re + x_im) * t[i + 3 * 32];
+        out_real[i] = (x_im * t[i + 5 * 32]) + tmp;
+        out_imag[i] = (x_re * t[i + 4 * 32]) + tmp;
+    }
+}
+
+void orc_sbr_dct4(const float* in_re, const float* in_im, float* out_re, float* out_im)
+{
+    float a[32], b[32];
+    memcpy(a, in_re, sizeof a);
+    memcpy(b, in_im, sizeof b);
+    dct4_kernel(a, b, out_re, out_im);
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* AnalysisFilterbank.sbr_qmf_analysis_32 (A/sbr/AnalysisFilterbank.java:9-73)                 */
+/* ------------------------------------------------------------------------------------------ */
+static void qmf_analysis(float* v, int* v_index, const float* input, float (*X)[64][2], int offset, int kx)
+{
+    float u[64], in_real[32], in_imag[32], out_real[32], out_imag[32];
+    for (int l = 0, in = 0; l < 32; l++) {
+        for (int n = 31; n >= 0; n--) v[*v_index + n] = v[*v_index + n + 320] = input[in++];
+        for (int n = 0; n < 64; n++) {
+            const float* w = v + *v_index;
+            u[n] = (w[n] * JAAD_QMF_C[2 * n]) + (w[n + 64] * JAAD_QMF_C[2 * (n + 64)]) +
+                   (w[n + 128] * JAAD_QMF_C[2 * (n + 128)]) + (w[n + 192] * JAAD_QMF_C[2 * (n + 192)]) +
+                   (w[n + 256] * JAAD_QMF_C[2 * (n + 256)]);
+        }
+        *v_index -= 32;
+        if (*v_index < 0) *v_index = 320 - 32;
+        in_imag[31] = u[1];
+        in_real[0] = u[0];
+        for (int n = 1; n < 31; n++) {
+            in_imag[31 - n] = u[n + 1];
+            in_real[n] = -u[64 - n];
+        }
+        in_imag[0] = u[32];
+        in_real[31] = -u[33];
+        dct4_kernel(in_real, in_imag, out_real, out_imag);
+        float(*row)[2] = X[l + offset];
+        for (int n = 0; n < 16; n++) {
+            if (2 * n + 1 < kx) {
+                row[2 * n][0] = 2.0f * out_real[n];
+                row[2 * n][1] = 2.0f * out_imag[n];
+                row[2 * n + 1][0] = -2.0f * out_imag[31 - n];
+                row[2 * n + 1][1] = -2.0f * out_real[31 - n];
+            } else {
+                if (2 * n < kx) {
+                    row[2 * n][0] = 2.0f * out_real[n];
+                    row[2 * n][1] = 2.0f * out_imag[n];
+                } else {
+                    row[2 * n][0] = 0;
+                    row[2 * n][1] = 0;
+                }
+                row[2 * n + 1][0] = 0;
+                row[2 * n + 1][1] = 0;
+            }
+        }
+    }
+}
+
+/* one frame of analysis with an explicit ring (tests): X[32][64][2] rows 0..31 */
+void orc_qmf_analysis_frame(float* v1280, int* v_index, const float* input1024, float* X, int kx)
+{
+    qmf_analysis(v1280, v_index, input1024, (float(*)[64][2])X, 0, kx);
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* SynthesisFilterbank64.synthesis (A/sbr/SynthesisFilterbank64.java:9-79)                     */
+/* ------------------------------------------------------------------------------------------ */
+static void qmf_synthesis(float* v, int* v_index, float (*X)[64][2], float* output)
+{
+    float in_real1[32], in_imag1[32], out_real1[32], out_imag1[32];
+    float in_real2[32], in_imag2[32], out_real2[32], out_imag2[32];
+    const float scale = 1.f / 64.f;
+    int out = 0;
+    for (int l = 0; l < 32; l++) {
+        float(*pX)[2] = X[l];
+        in_imag1[31] = scale * pX[1][0];
+        in_real1[0] = scale * pX[0][0];
+        in_imag2[31] = scale * pX[63 - 1][1];
+        in_real2[0] = scale * pX[63 - 0][1];
+        for (int k = 1; k < 31; k++) {
+            in_imag1[31 - k] = scale * pX[2 * k + 1][0];
+            in_real1[k] = scale * pX[2 * k][0];
+            in_imag2[31 - k] = scale * pX[63 - (2 * k + 1)][1];
+            in_real2[k] = scale * pX[63 - (2 * k)][1];
+        }
+        in_imag1[0] = scale * pX[63][0];
+        in_real1[31] = scale * pX[62][0];
+        in_imag2[0] = scale * pX[63 - 63][1];
+        in_real2[31] = scale * pX[63 - 62][1];
+        dct4_kernel(in_real1, in_imag1, out_real1, out_imag1);
+        dct4_kernel(in_real2, in_imag2, out_real2, out_imag2);
+        int p1 = *v_index, p3 = p1 + 1280;
+        for (int n = 0; n < 32; n++) {
+            v[p1 + 2 * n] = v[p3 + 2 * n] = out_real2[n] - out_real1[n];
+            v[p1 + 127 - 2 * n] = v[p3 + 127 - 2 * n] = out_real2[n] + out_real1[n];
+            v[p1 + 2 * n + 1] = v[p3 + 2 * n + 1] = out_imag2[31 - n] + out_imag1[31 - n];
+            v[p1 + 127 - (2 * n + 1)] = v[p3 + 127 - (2 * n + 1)] = out_imag2[31 - n] - out_imag1[31 - n];
+        }
+        const float* w = v + *v_index;
+        for (int k = 0; k < 64; k++) {
+            output[out++] = (w[k + 0] * JAAD_QMF_C[k + 0]) + (w[k + 192] * JAAD_QMF_C[k + 64]) +
+                            (w[k + 256] * JAAD_QMF_C[k + 128]) + (w[k + (256 + 192)] * JAAD_QMF_C[k + 192]) +
+                            (w[k + 512] * JAAD_QMF_C[k + 256]) + (w[k + (512 + 192)] * JAAD_QMF_C[k + 320]) +
+                            (w[k + 768] * JAAD_QMF_C[k + 384]) + (w[k + (768 + 192)] * JAAD_QMF_C[k + 448]) +
+                            (w[k + 1024] * JAAD_QMF_C[k + 512]) + (w[k + (1024 + 192)] * JAAD_QMF_C[k + 576]);
+        }
+        *v_index -= 128;
+        if (*v_index < 0) *v_index = 1280 - 128;
+    }
+}
+
+void orc_qmf_synthesis_frame(float* v2560, int* v_index, const float* X, float* output2048)
+{
+    float tmp[32][64][2];
+    memcpy(tmp, X, sizeof tmp);
+    qmf_synthesis(v2560, v_index, tmp, output2048);
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* FBT (A/sbr/FBT.java)                                                                        */
+/* ------------------------------------------------------------------------------------------ */
+/* Math.min(float, float) (NaN-propagating; -0.0f < 0.0f) */
+static float java_minf(float a, float b)
+{
+    if (a != a) return a;
+    if (a == 0.0f && b == 0.0f) return signbit(a) ? a : b;
+    return a <= b ? a : b;
+}
+
+static int cmp_int(const void* a, const void* b)
+{
+    int x = *(const int*)a, y = *(const int*)b;
+    return (x > y) - (x < y);
+}
+static void sort_ints(int* a, int n)
+{
+    if (n > 1) qsort(a, (size_t)n, sizeof(int), cmp_int);
+}
+
+static int qmf_start_channel(int bs_start_freq, int bs_samplerate_mode, int sfi) /* :29-42 */
+{
+    int startMin = JAAD_SBR_START_MIN[sfi];
+    int offsetIndex = JAAD_SBR_OFFSET_INDEX[sfi];
+    if (bs_samplerate_mode != 0) return startMin + JAAD_SBR_OFFSET[offsetIndex][bs_start_freq];
+    return startMin + JAAD_SBR_OFFSET[6][bs_start_freq];
+}
+
+static int qmf_stop_channel(int bs_stop_freq, int sfi, int k0) /* :62-77 */
+{
+    if (bs_stop_freq == 15) return k0 * 3 < 64 ? k0 * 3 : 64;
+    if (bs_stop_freq == 14) return k0 * 2 < 64 ? k0 * 2 : 64;
+    int v = JAAD_SBR_STOP_MIN[sfi] + JAAD_SBR_STOP_OFFSET[sfi][bs_stop_freq < 13 ? bs_stop_freq : 13];
+    return v < 64 ? v : 64;
+}
+
+static int master_frequency_table_fs0(orc_sbr* s, int k0, int k2, int bs_alter_scale) /* :84-129 */
+{
+    int vDk[64] = {0};
+    if (k2 <= k0) {
+        s->N_master = 0;
+        return 1;
+    }
+    int dk = bs_alter_scale ? 2 : 1;
+    int nrBands = bs_alter_scale ? (((k2 - k0 + 2) >> 2) << 1) : (((k2 - k0) >> 1) << 1);
+    nrBands = nrBands < 63 ? nrBands : 63;
+    if (nrBands <= 0) return 1;
+    int k2Achieved = k0 + nrBands * dk;
+    int k2Diff = k2 - k2Achieved;
+    for (int k = 0; k < nrBands; k++) vDk[k] = dk;
+    if (k2Diff != 0) {
+        int incr = (k2Diff > 0) ? -1 : 1;
+        int k = (k2Diff > 0) ? (nrBands - 1) : 0;
+        while (k2Diff != 0) {
+            vDk[k] -= incr;
+            k += incr;
+            k2Diff += incr;
+        }
+    }
+    s->f_master[0] = k0;
+    for (int k = 1; k <= nrBands; k++) s->f_master[k] = s->f_master[k - 1] + vDk[k - 1];
+    s->N_master = nrBands < 64 ? nrBands : 64;
+    return 0;
+}
+
+static int find_bands(int warp, int bands, int a0, int a1) /* :135-141 */
+{
+    float div = (float)log(2.0);
+    if (warp != 0) div *= 1.3f;
+    return (int)(bands * log((double)((float)a1 / (float)a0)) / div + 0.5);
+}
+
+static float find_initial_power(int bands, int a0, int a1) /* :143-145 */
+{
+    return (float)pow((double)((float)a1 / (float)a0), (double)(1.0f / (float)bands));
+}
+
+static int master_frequency_table(orc_sbr* s, int k0, int k2, int bs_freq_scale, int bs_alter_scale) /* :150-256 */
+{
+    (void)bs_alter_scale; /* ignored by the reference */
+    int vDk0[64] = {0}, vDk1[64] = {0}, vk0[64] = {0}, vk1[64] = {0};
+    static const int temp1[] = {6, 5, 4};
+    if (k2 <= k0) {
+        s->N_master = 0;
+        return 1;
+    }
+    int bands = temp1[bs_freq_scale - 1];
+    int twoRegions, k1;
+    if ((double)((float)k2 / (float)k0) > 2.2449) {
+        twoRegions = 1;
+        k1 = k0 << 1;
+    } else {
+        twoRegions = 0;
+        k1 = k2;
+    }
+    int nrBand0 = 2 * find_bands(0, bands, k0, k1);
+    nrBand0 = nrBand0 < 63 ? nrBand0 : 63;
+    if (nrBand0 <= 0) return 1;
+    float q = find_initial_power(nrBand0, k0, k1);
+    float qk = (float)k0;
+    int A_1 = (int)(qk + 0.5f);
+    for (int k = 0; k <= nrBand0; k++) {
+        int A_0 = A_1;
+        qk *= q;
+        A_1 = (int)(qk + 0.5f);
+        vDk0[k] = A_1 - A_0;
+    }
+    sort_ints(vDk0, nrBand0);
+    vk0[0] = k0;
+    for (int k = 1; k <= nrBand0; k++) {
+        vk0[k] = vk0[k - 1] + vDk0[k - 1];
+        if (vDk0[k - 1] == 0) return 1;
+    }
+    if (!twoRegions) {
+        for (int k = 0; k <= nrBand0; k++) s->f_master[k] = vk0[k];
+        s->N_master = nrBand0 < 64 ? nrBand0 : 64;
+        return 0;
+    }
+    int nrBand1 = 2 * find_bands(1, bands, k1, k2);
+    nrBand1 = nrBand1 < 63 ? nrBand1 : 63;
+    q = find_initial_power(nrBand1, k1, k2);
+    qk = (float)k1;
+    A_1 = (int)(qk + 0.5f);
+    for (int k = 0; k <= nrBand1 - 1; k++) {
+        int A_0 = A_1;
+        qk *= q;
+        A_1 = (int)(qk + 0.5f);
+        vDk1[k] = A_1 - A_0;
+    }
+    if (vDk1[0] < vDk0[nrBand0 - 1]) {
+        sort_ints(vDk1, nrBand1 + 1);
+        int change = vDk0[nrBand0 - 1] - vDk1[0];
+        vDk1[0] = vDk0[nrBand0 - 1];
+        vDk1[nrBand1 - 1] = vDk1[nrBand1 - 1] - change;
+    }
+    sort_ints(vDk1, nrBand1);
+    vk1[0] = k1;
+    for (int k = 1; k <= nrBand1; k++) {
+        vk1[k] = vk1[k - 1] + vDk1[k - 1];
+        if (vDk1[k - 1] == 0) return 1;
+    }
+    s->N_master = nrBand0 + nrBand1;
+    s->N_master = s->N_master < 64 ? s->N_master : 64;
+    for (int k = 0; k <= nrBand0; k++) s->f_master[k] = vk0[k];
+    for (int k = nrBand0 + 1; k <= s->N_master; k++) s->f_master[k] = vk1[k - nrBand0];
+    return 0;
+}
+
+static int derived_frequency_table(orc_sbr* s, int bs_xover_band, int k2) /* :259-320 */
+{
+    if (s->N_master <= bs_xover_band) return 1;
+    s->N_high = s->N_master - bs_xover_band;
+    s->N_low = (s->N_high >> 1) + (s->N_high - ((s->N_high >> 1) << 1));
+    s->n[0] = s->N_low;
+    s->n[1] = s->N_high;
+    for (int k = 0; k <= s->N_high; k++) s->f_table_res[HI_RES][k] = s->f_master[k + bs_xover_band];
+    s->M = s->f_table_res[HI_RES][s->N_high] - s->f_table_res[HI_RES][0];
+    s->kx = s->f_table_res[HI_RES][0];
+    if (s->kx > 32) return 1;
+    if (s->kx + s->M > 64) return 1;
+    int minus = (s->N_high & 1) ? 1 : 0;
+    for (int i = 0, k = 0; k <= s->N_low; k++) {
+        if (k > 0) i = 2 * k - minus;
+        s->f_table_res[LO_RES][k] = s->f_table_res[HI_RES][i];
+    }
+    s->N_Q = 0;
+    if (s->hdr.noise_bands == 0) s->N_Q = 1;
+    else {
+        int nq = find_bands(0, s->hdr.noise_bands, s->kx, k2);
+        s->N_Q = nq > 1 ? nq : 1;
+        s->N_Q = s->N_Q < 5 ? s->N_Q : 5;
+    }
+    for (int i = 0, k = 0; k <= s->N_Q; k++) {
+        if (k > 0) i += (s->N_low - i) / (s->N_Q + 1 - k);
+        s->f_table_noise[k] = s->f_table_res[LO_RES][i];
+    }
+    for (int k = 0; k < 64; k++) {
+        for (int g = 0; g < s->N_Q; g++) {
+            if (s->f_table_noise[g] <= k && k < s->f_table_noise[g + 1]) {
+                s->table_map_k_to_g[k] = g;
+                break;
+            }
+        }
+    }
+    return 0;
+}
+
+static void limiter_frequency_table(orc_sbr* s) /* :330-416 */
+{
+    s->f_table_lim[0][0] = s->f_table_res[LO_RES][0] - s->kx;
+    s->f_table_lim[0][1] = s->f_table_res[LO_RES][s->N_low] - s->kx;
+    s->N_L[0] = 1;
+    for (int sidx = 1; sidx < 4; sidx++) {
+        int limTable[100] = {0}, patchBorders[64] = {0};
+        patchBorders[0] = s->kx;
+        for (int k = 1; k <= s->noPatches; k++) patchBorders[k] = patchBorders[k - 1] + s->patchNoSubbands[k - 1];
+        for (int k = 0; k <= s->N_low; k++) limTable[k] = s->f_table_res[LO_RES][k];
+        for (int k = 1; k < s->noPatches; k++) limTable[k + s->N_low] = patchBorders[k];
+        sort_ints(limTable, s->noPatches + s->N_low);
+        int k = 1;
+        int nrLim = s->noPatches + s->N_low - 1;
+        if (nrLim < 0) return;
+        while (k <= nrLim) {
+            float nOctaves;
+            if (limTable[k - 1] != 0) nOctaves = (float)limTable[k] / (float)limTable[k - 1];
+            else nOctaves = 0;
+            if (nOctaves < JAAD_SBR_LIMITER_COMPARE[sidx - 1]) {
+                if (limTable[k] != limTable[k - 1]) {
+                    int found = 0, found2 = 0;
+                    for (int i = 0; i <= s->noPatches; i++)
+                        if (limTable[k] == patchBorders[i]) found = 1;
+                    if (found) {
+                        found2 = 0;
+                        for (int i = 0; i <= s->noPatches; i++)
+                            if (limTable[k - 1] == patchBorders[i]) found2 = 1;
+                        if (found2) {
+                            k++;
+                            continue;
+                        } else {
+                            limTable[k - 1] = s->f_table_res[LO_RES][s->N_low];
+                            sort_ints(limTable, s->noPatches + s->N_low);
+                            nrLim--;
+                            continue;
+                        }
+                    }
+                }
+                limTable[k] = s->f_table_res[LO_RES][s->N_low];
+                sort_ints(limTable, nrLim);
+                nrLim--;
+            } else {
+                k++;
+            }
+        }
+        s->N_L[sidx] = nrLim;
+        for (int l = 0; l <= nrLim; l++) s->f_table_lim[sidx][l] = limTable[l] - s->kx;
+    }
+}
+
+/* SBR.calc_sbr_tables (A/sbr/SBR.java:125-158); bs_samplerate_mode is hard-wired to 1 (:105) */
+static int calc_sbr_tables(orc_sbr* s)
+{
+    int result = 0;
+    const jaad_sbr_header* h = &s->hdr;
+    static const int FREQ[12] = {96000, 88200, 64000, 48000, 44100, 32000, 24000, 22050, 16000, 12000, 11025, 8000};
+    s->k0 = qmf_start_channel(h->start_freq, 1, s->out_sf_index);
+    int k2 = qmf_stop_channel(h->stop_freq, s->out_sf_index, s->k0);
+    int fs = FREQ[s->out_sf_index];
+    if (fs >= 48000) {
+        if (k2 - s->k0 > 32) result += 1;
+    } else if (fs <= 32000) {
+        if (k2 - s->k0 > 48) result += 1;
+    } else if (k2 - s->k0 > 45) result += 1;
+    if (h->freq_scale == 0) result += master_frequency_table_fs0(s, s->k0, k2, h->alter_scale);
+    else result += master_frequency_table(s, s->k0, k2, h->freq_scale, h->alter_scale);
+    result += derived_frequency_table(s, h->xover_band, k2);
+    return result > 0 ? 1 : 0;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* HFGeneration (A/sbr/HFGeneration.java)                                                      */
+/* ------------------------------------------------------------------------------------------ */
+typedef struct {
+    float r01[2], r02[2], r11[2], r12[2], r22[2], det;
+} acorr_coef;
+
+static void auto_correlation(acorr_coef* ac, float (*buffer)[64][2], int bd, int len) /* :100-159 */
+{
+    float r01r = 0, r01i = 0, r02r = 0, r02i = 0, r11r = 0;
+    float t1r, t1i, t2r, t2i, t3r, t3i, t4r, t4i, t5r, t5i;
+    float rel = 1.0f / (1 + 1e-6f);
+    int offset = T_HFADJ;
+    t2r = buffer[offset - 2][bd][0];
+    t2i = buffer[offset - 2][bd][1];
+    t3r = buffer[offset - 1][bd][0];
+    t3i = buffer[offset - 1][bd][1];
+    t4r = t2r; t4i = t2i; t5r = t3r; t5i = t3i;
+    for (int j = offset; j < len + offset; j++) {
+        t1r = t2r; t1i = t2i; t2r = t3r; t2i = t3i;
+        t3r = buffer[j][bd][0];
+        t3i = buffer[j][bd][1];
+        r01r += t3r * t2r + t3i * t2i;
+        r01i += t3i * t2r - t3r * t2i;
+        r02r += t3r * t1r + t3i * t1i;
+        r02i += t3i * t1r - t3r * t1i;
+        r11r += t2r * t2r + t2i * t2i;
+    }
+    ac->r12[0] = r01r - (t3r * t2r + t3i * t2i) + (t5r * t4r + t5i * t4i);
+    ac->r12[1] = r01i - (t3i * t2r - t3r * t2i) + (t5i * t4r - t5r * t4i);
+    ac->r22[0] = r11r - (t2r * t2r + t2i * t2i) + (t4r * t4r + t4i * t4i);
+    ac->r01[0] = r01r;
+    ac->r01[1] = r01i;
+    ac->r02[0] = r02r;
+    ac->r02[1] = r02i;
+    ac->r11[0] = r11r;
+    ac->det = (ac->r11[0] * ac->r22[0]) - (rel * ((ac->r12[0] * ac->r12[0]) + (ac->r12[1] * ac->r12[1])));
+}
+
+static void calc_prediction_coef(float (*Xlow)[64][2], float (*alpha_0)[2], float (*alpha_1)[2], int k) /* :162-196 */
+{
+    float tmp;
+    acorr_coef ac;
+    auto_correlation(&ac, Xlow, k, 32 + 6);
+    if (ac.det == 0) {
+        alpha_1[k][0] = 0;
+        alpha_1[k][1] = 0;
+    } else {
+        tmp = 1.0f / ac.det;
+        alpha_1[k][0] = ((ac.r01[0] * ac.r12[0]) - (ac.r01[1] * ac.r12[1]) - (ac.r02[0] * ac.r11[0])) * tmp;
+        alpha_1[k][1] = ((ac.r01[1] * ac.r12[0]) + (ac.r01[0] * ac.r12[1]) - (ac.r02[1] * ac.r11[0])) * tmp;
+    }
+    if (ac.r11[0] == 0) {
+        alpha_0[k][0] = 0;
+        alpha_0[k][1] = 0;
+    } else {
+        tmp = 1.0f / ac.r11[0];
+        alpha_0[k][0] = -(ac.r01[0] + (alpha_1[k][0] * ac.r12[0]) + (alpha_1[k][1] * ac.r12[1])) * tmp;
+        alpha_0[k][1] = -(ac.r01[1] + (alpha_1[k][1] * ac.r12[0]) - (alpha_1[k][0] * ac.r12[1])) * tmp;
+    }
+    if (((alpha_0[k][0] * alpha_0[k][0]) + (alpha_0[k][1] * alpha_0[k][1]) >= 16.0f) ||
+        ((alpha_1[k][0] * alpha_1[k][0]) + (alpha_1[k][1] * alpha_1[k][1]) >= 16.0f)) {
+        alpha_0[k][0] = 0;
+        alpha_0[k][1] = 0;
+        alpha_1[k][0] = 0;
+        alpha_1[k][1] = 0;
+    }
+}
+
+static float mapNewBw(int invf_mode, int invf_mode_prev) /* :199-223 */
+{
+    switch (invf_mode) {
+    case 1: return invf_mode_prev == 0 ? 0.6f : 0.75f;
+    case 2: return 0.9f;
+    case 3: return 0.98f;
+    default: return invf_mode_prev == 1 ? 0.6f : 0.0f;
+    }
+}
+
+static void calc_chirp_factors(const orc_sbr* s, orc_sbr_channel* ch) /* :226-245 */
+{
+    for (int i = 0; i < s->N_Q; i++) {
+        ch->bwArray[i] = mapNewBw(ch->bs_invf_mode[i], ch->bs_invf_mode_prev[i]);
+        if (ch->bwArray[i] < ch->bwArray_prev[i])
+            ch->bwArray[i] = (ch->bwArray[i] * 0.75f) + (ch->bwArray_prev[i] * 0.25f);
+        else
+            ch->bwArray[i] = (ch->bwArray[i] * 0.90625f) + (ch->bwArray_prev[i] * 0.09375f);
+        if (ch->bwArray[i] < 0.015625f) ch->bwArray[i] = 0.0f;
+        if (ch->bwArray[i] >= 0.99609375f) ch->bwArray[i] = 0.99609375f;
+        ch->bwArray_prev[i] = ch->bwArray[i];
+        ch->bs_invf_mode_prev[i] = ch->bs_invf_mode[i];
+    }
+}
+
+static void patch_construction(orc_sbr* s) /* :247-309 */
+{
+    int msb = s->k0, usb = s->kx;
+    int goalSb = JAAD_SBR_GOAL_SB[s->out_sf_index];
+    s->noPatches = 0;
+    int k = 0;
+    if (goalSb < s->kx + s->M) {
+        for (int i = 0; s->f_master[i] < goalSb; i++) k = i + 1;
+    } else {
+        k = s->N_master;
+    }
+    if (s->N_master == 0) {
+        s->noPatches = 0;
+        s->patchNoSubbands[0] = 0;
+        s->patchStartSubband[0] = 0;
+        return;
+    }
+    int sb;
+    do {
+        int j = k + 1, odd;
+        do {
+            j--;
+            sb = s->f_master[j];
+            odd = (sb - 2 + s->k0) % 2;
+        } while (sb > (s->k0 - 1 + msb - odd));
+        s->patchNoSubbands[s->noPatches] = sb - usb > 0 ? sb - usb : 0;
+        s->patchStartSubband[s->noPatches] = s->k0 - odd - s->patchNoSubbands[s->noPatches];
+        if (s->patchNoSubbands[s->noPatches] > 0) {
+            usb = sb;
+            msb = sb;
+            s->noPatches++;
+        } else {
+            msb = s->kx;
+        }
+        if (s->f_master[k] - sb < 3) k = s->N_master;
+    } while (sb != (s->kx + s->M));
+    if ((s->patchNoSubbands[s->noPatches - 1] < 3) && (s->noPatches > 1)) s->noPatches--;
+    s->noPatches = s->noPatches < 5 ? s->noPatches : 5;
+}
+
+static void hf_generation(orc_sbr* s, orc_sbr_channel* ch, int reset) /* :17-98 */
+{
+    float (*X)[64][2] = ch->Xsbr;
+    float alpha_0[64][2], alpha_1[64][2];
+    int offset = T_HFADJ;
+    int first = ch->t_E[0], last = ch->t_E[ch->L_E];
+    calc_chirp_factors(s, ch);
+    if (reset) patch_construction(s);
+    for (int i = 0; i < s->noPatches; i++) {
+        for (int x = 0; x < s->patchNoSubbands[i]; x++) {
+            int k = s->kx + x;
+            for (int q = 0; q < i; q++) k += s->patchNoSubbands[q];
+            int p = s->patchStartSubband[i] + x;
+            int g = s->table_map_k_to_g[k];
+            float bw = ch->bwArray[g];
+            float bw2 = bw * bw;
+            if (bw2 > 0) {
+                calc_prediction_coef(X, alpha_0, alpha_1, p);
+                float a0_r = alpha_0[p][0] * bw, a1_r = alpha_1[p][0] * bw2;
+                float a0_i = alpha_0[p][1] * bw, a1_i = alpha_1[p][1] * bw2;
+                float t2r = X[first - 2 + offset][p][0], t3r = X[first - 1 + offset][p][0];
+                float t2i = X[first - 2 + offset][p][1], t3i = X[first - 1 + offset][p][1];
+                for (int l = first; l < last; l++) {
+                    float t1r = t2r, t1i = t2i;
+                    t2r = t3r; t2i = t3i;
+                    t3r = X[l + offset][p][0];
+                    t3i = X[l + offset][p][1];
+                    X[l + offset][k][0] = t3r + ((a0_r * t2r) - (a0_i * t2i) + (a1_r * t1r) - (a1_i * t1i));
+                    X[l + offset][k][1] = t3i + ((a0_i * t2r) + (a0_r * t2i) + (a1_i * t1r) + (a1_r * t1i));
+                }
+            } else {
+                for (int l = first; l < last; l++) {
+                    X[l + offset][k][0] = X[l + offset][p][0];
+                    X[l + offset][k][1] = X[l + offset][p][1];
+                }
+            }
+        }
+    }
+    if (s->reset) limiter_frequency_table(s);
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* HFAdjustment (A/sbr/HFAdjustment.java)                                                      */
+/* ------------------------------------------------------------------------------------------ */
+typedef struct {
+    float G_lim_boost[MAX_L_E][MAX_M], Q_M_lim_boost[MAX_L_E][MAX_M], S_M_boost[MAX_L_E][MAX_M];
+} hf_adj;
+
+static int get_S_mapped(const orc_sbr* s, const orc_sbr_channel* ch, int l, int current_band) /* :46-80 */
+{
+    if (ch->f[l] == HI_RES) {
+        if ((l >= ch->l_A) || (ch->bs_add_harmonic_prev[current_band] != 0 && ch->bs_add_harmonic_flag_prev))
+            return ch->bs_add_harmonic[current_band];
+    } else {
+        int lb = 2 * current_band - ((s->N_high & 1) ? 1 : 0);
+        int ub = 2 * (current_band + 1) - ((s->N_high & 1) ? 1 : 0);
+        for (int b = lb; b < ub; b++) {
+            if ((l >= ch->l_A) || (ch->bs_add_harmonic_prev[b] != 0 && ch->bs_add_harmonic_flag_prev)) {
+                if (ch->bs_add_harmonic[b] == 1) return 1;
+            }
+        }
+    }
+    return 0;
+}
+
+static void estimate_current_envelope(const orc_sbr* s, orc_sbr_channel* ch) /* :82-138 */
+{
+    float (*X)[64][2] = ch->Xsbr;
+    float nrg, div;
+    if (s->hdr.interpol_freq) {
+        for (int l = 0; l < ch->L_E; l++) {
+            int l_i = ch->t_E[l], u_i = ch->t_E[l + 1];
+            div = (float)(u_i - l_i);
+            if (div == 0) div = 1;
+            for (int m = 0; m < s->M; m++) {
+                nrg = 0;
+                for (int i = l_i + T_HFADJ; i < u_i + T_HFADJ; i++)
+                    nrg += (X[i][m + s->kx][0] * X[i][m + s->kx][0]) + (X[i][m + s->kx][1] * X[i][m + s->kx][1]);
+                ch->E_curr[m][l] = nrg / div;
+            }
+        }
+    } else {
+        for (int l = 0; l < ch->L_E; l++) {
+            for (int p = 0; p < s->n[ch->f[l]]; p++) {
+                int k_l = s->f_table_res[ch->f[l]][p], k_h = s->f_table_res[ch->f[l]][p + 1];
+                for (int k = k_l; k < k_h; k++) {
+                    nrg = 0;
+                    int l_i = ch->t_E[l], u_i = ch->t_E[l + 1];
+                    div = (float)((u_i - l_i) * (k_h - k_l));
+                    if (div == 0) div = 1;
+                    for (int i = l_i + T_HFADJ; i < u_i + T_HFADJ; i++)
+                        for (int j = k_l; j < k_h; j++)
+                            nrg += (X[i][j][0] * X[i][j][0]) + (X[i][j][1] * X[i][j][1]);
+                    ch->E_curr[k - s->kx][l] = nrg / div;
+                }
+            }
+        }
+    }
+}
+
+static void hf_assembly(const orc_sbr* s, orc_sbr_channel* ch, const hf_adj* a) /* :140-238 */
+{
+    static const int phi_re[] = {1, 0, -1, 0}, phi_im[] = {0, 1, 0, -1};
+    float (*X)[64][2] = ch->Xsbr;
+    int fIndexNoise, fIndexSine, assembly_reset = 0;
+    if (s->reset) {
+        assembly_reset = 1;
+        fIndexNoise = 0;
+    } else {
+        fIndexNoise = ch->index_noise_prev;
+    }
+    fIndexSine = ch->psi_is_prev;
+    for (int l = 0; l < ch->L_E; l++) {
+        int no_noise = (l == ch->l_A || l == ch->prevEnvIsShort);
+        int h_SL = s->hdr.smoothing_mode ? 0 : 4;
+        h_SL = no_noise ? 0 : h_SL;
+        if (assembly_reset) {
+            for (int n = 0; n < 4; n++) {
+                memcpy(ch->G_temp_prev[n], a->G_lim_boost[l], sizeof(float) * s->M);
+                memcpy(ch->Q_temp_prev[n], a->Q_M_lim_boost[l], sizeof(float) * s->M);
+            }
+            ch->GQ_ringbuf_index = 4;
+            assembly_reset = 0;
+        }
+        for (int i = ch->t_E[l]; i < ch->t_E[l + 1]; i++) {
+            memcpy(ch->G_temp_prev[ch->GQ_ringbuf_index], a->G_lim_boost[l], sizeof(float) * s->M);
+            memcpy(ch->Q_temp_prev[ch->GQ_ringbuf_index], a->Q_M_lim_boost[l], sizeof(float) * s->M);
+            for (int m = 0; m < s->M; m++) {
+                float G_filt = 0, Q_filt = 0;
+                if (h_SL != 0) {
+                    int ri = ch->GQ_ringbuf_index;
+                    for (int n = 0; n <= 4; n++) {
+                        float h = JAAD_SBR_H_SMOOTH[n];
+                        ri++;
+                        if (ri >= 5) ri -= 5;
+                        G_filt += (ch->G_temp_prev[ri][m] * h);
+                        Q_filt += (ch->Q_temp_prev[ri][m] * h);
+                    }
+                } else {
+                    G_filt = ch->G_temp_prev[ch->GQ_ringbuf_index][m];
+                    Q_filt = ch->Q_temp_prev[ch->GQ_ringbuf_index][m];
+                }
+                Q_filt = (a->S_M_boost[l][m] != 0 || no_noise) ? 0 : Q_filt;
+                fIndexNoise = (fIndexNoise + 1) & 511;
+                float* x = X[i + T_HFADJ][m + s->kx];
+                x[0] = G_filt * x[0] + (Q_filt * JAAD_SBR_NOISE_TABLE[fIndexNoise][0]);
+                x[1] = G_filt * x[1] + (Q_filt * JAAD_SBR_NOISE_TABLE[fIndexNoise][1]);
+                int rev = ((m + s->kx) & 1) ? -1 : 1;
+                float psi0 = a->S_M_boost[l][m] * (float)phi_re[fIndexSine];
+                x[0] += psi0;
+                float psi1 = (float)rev * a->S_M_boost[l][m] * (float)phi_im[fIndexSine];
+                x[1] += psi1;
+            }
+            fIndexSine = (fIndexSine + 1) & 3;
+            ch->GQ_ringbuf_index++;
+            if (ch->GQ_ringbuf_index >= 5) ch->GQ_ringbuf_index = 0;
+        }
+    }
+    ch->index_noise_prev = fIndexNoise;
+    ch->psi_is_prev = fIndexSine;
+}
+
+static void calculate_gain(const orc_sbr* s, const orc_sbr_channel* ch, hf_adj* a) /* :240-415 */
+{
+    static const float EPS = 1e-12f;
+    int current_t_noise_band = 0, S_mapped;
+    float Q_M_lim[MAX_M], G_lim[MAX_M], S_M[MAX_M], G_boost;
+    const int lb = s->hdr.limiter_bands;
+    for (int l = 0; l < ch->L_E; l++) {
+        int current_f_noise_band = 0, current_res_band = 0, current_res_band2 = 0, current_hi_res_band = 0;
+        float delta = (l == ch->l_A || l == ch->prevEnvIsShort) ? 0 : 1;
+        S_mapped = get_S_mapped(s, ch, l, current_res_band2);
+        if (ch->t_E[l + 1] > ch->t_Q[current_t_noise_band + 1]) current_t_noise_band++;
+        for (int k = 0; k < s->N_L[lb]; k++) {
+            float G_max, den = 0, acc1 = 0, acc2 = 0;
+            int ml1 = s->f_table_lim[lb][k], ml2 = s->f_table_lim[lb][k + 1];
+            for (int m = ml1; m < ml2; m++) {
+                if ((m + s->kx) == s->f_table_res[ch->f[l]][current_res_band + 1]) current_res_band++;
+                acc1 += ch->E_orig[current_res_band][l];
+                acc2 += ch->E_curr[m][l];
+            }
+            G_max = ((EPS + acc1) / (EPS + acc2)) * JAAD_SBR_LIM_GAIN[s->hdr.limiter_gains];
+            G_max = java_minf(G_max, 1e10f);
+            for (int m = ml1; m < ml2; m++) {
+                float Q_M, G, Q_div, Q_div2;
+                int S_index_mapped;
+                if ((m + s->kx) == s->f_table_noise[current_f_noise_band + 1]) current_f_noise_band++;
+                if ((m + s->kx) == s->f_table_res[ch->f[l]][current_res_band2 + 1]) {
+                    current_res_band2++;
+                    S_mapped = get_S_mapped(s, ch, l, current_res_band2);
+                }
+                if ((m + s->kx) == s->f_table_res[HI_RES][current_hi_res_band + 1]) current_hi_res_band++;
+                S_index_mapped = 0;
+                if ((l >= ch->l_A) ||
+                    (ch->bs_add_harmonic_prev[current_hi_res_band] != 0 && ch->bs_add_harmonic_flag_prev)) {
+                    if ((m + s->kx) == (s->f_table_res[HI_RES][current_hi_res_band + 1] +
+                                        s->f_table_res[HI_RES][current_hi_res_band]) >> 1)
+                        S_index_mapped = ch->bs_add_harmonic[current_hi_res_band];
+                }
+                Q_div = ch->Q_div[current_f_noise_band][current_t_noise_band];
+                Q_div2 = ch->Q_div2[current_f_noise_band][current_t_noise_band];
+                Q_M = ch->E_orig[current_res_band2][l] * Q_div2;
+                if (S_index_mapped == 0) {
+                    S_M[m] = 0;
+                } else {
+                    S_M[m] = ch->E_orig[current_res_band2][l] * Q_div;
+                    den += S_M[m];
+                }
+                G = ch->E_orig[current_res_band2][l] / (1.0f + ch->E_curr[m][l]);
+                if ((S_mapped == 0) && (delta == 1)) G *= Q_div;
+                else if (S_mapped == 1) G *= Q_div2;
+                if (G_max > G) {
+                    Q_M_lim[m] = Q_M;
+                    G_lim[m] = G;
+                } else {
+                    Q_M_lim[m] = Q_M * G_max / G;
+                    G_lim[m] = G_max;
+                }
+                den += ch->E_curr[m][l] * G_lim[m];
+                if ((S_index_mapped == 0) && (l != ch->l_A)) den += Q_M_lim[m];
+            }
+            G_boost = (acc1 + EPS) / (den + EPS);
+            G_boost = java_minf(G_boost, 2.51188643f);
+            for (int m = ml1; m < ml2; m++) {
+                a->G_lim_boost[l][m] = (float)sqrt((double)(G_lim[m] * G_boost));
+                a->Q_M_lim_boost[l][m] = (float)sqrt((double)(Q_M_lim[m] * G_boost));
+                if (S_M[m] != 0) a->S_M_boost[l][m] = (float)sqrt((double)(S_M[m] * G_boost));
+                else a->S_M_boost[l][m] = 0;
+            }
+        }
+    }
+}
+
+static void hf_adjustment(const orc_sbr* s, orc_sbr_channel* ch) /* :20-44 */
+{
+    hf_adj a;
+    memset(&a, 0, sizeof a);
+    if (ch->bs_frame_class == FIXFIX) ch->l_A = -1;
+    else if (ch->bs_frame_class == VARFIX) ch->l_A = ch->bs_pointer > 1 ? ch->bs_pointer - 1 : -1;
+    else ch->l_A = ch->bs_pointer == 0 ? -1 : ch->L_E + 1 - ch->bs_pointer;
+    estimate_current_envelope(s, ch);
+    calculate_gain(s, ch, &a);
+    hf_assembly(s, ch, &a);
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* Channel.process_channel (A/sbr/Channel.java:586-647), SBR.sbr_save_* (A/sbr/SBR.java:256-300) */
+/* ------------------------------------------------------------------------------------------ */
+static void process_channel(orc_sbr* s, orc_sbr_channel* ch, float* channel_buf, float (*X)[64][2], int reset)
+{
+    s->bsco = 0;
+    int dont_process = !s->have_hdr;
+    qmf_analysis(ch->qmfa_v, &ch->qmfa_index, channel_buf, ch->Xsbr, T_HFGEN, dont_process ? 32 : s->kx);
+    if (!dont_process) {
+        hf_generation(s, ch, reset);
+        hf_adjustment(s, ch);
+    }
+    for (int l = 0; l < 32; l++) {
+        if (dont_process) {
+            for (int k = 0; k < 32; k++) {
+                X[l][k][0] = ch->Xsbr[l + T_HFADJ][k][0];
+                X[l][k][1] = ch->Xsbr[l + T_HFADJ][k][1];
+            }
+            for (int k = 32; k < 64; k++) X[l][k][0] = X[l][k][1] = 0;
+            continue;
+        }
+        int kx_band, M_band, bsco_band;
+        if (l < ch->t_E[0]) {
+            kx_band = s->kx_prev; M_band = s->M_prev; bsco_band = s->bsco_prev;
+        } else {
+            kx_band = s->kx; M_band = s->M; bsco_band = s->bsco;
+        }
+        for (int k = 0; k < kx_band + bsco_band; k++) {
+            X[l][k][0] = ch->Xsbr[l + T_HFADJ][k][0];
+            X[l][k][1] = ch->Xsbr[l + T_HFADJ][k][1];
+        }
+        for (int k = kx_band + bsco_band; k < kx_band + M_band; k++) {
+            X[l][k][0] = ch->Xsbr[l + T_HFADJ][k][0];
+            X[l][k][1] = ch->Xsbr[l + T_HFADJ][k][1];
+        }
+        int k0 = kx_band + bsco_band > kx_band + M_band ? kx_band + bsco_band : kx_band + M_band;
+        for (int k = k0; k < 64; k++) X[l][k][0] = X[l][k][1] = 0;
+    }
+}
+
+static void sbr_save_prev_data(orc_sbr* s, orc_sbr_channel* ch)
+{
+    s->kx_prev = s->kx;
+    s->M_prev = s->M;
+    s->bsco_prev = s->bsco;
+    ch->L_E_prev = ch->L_E;
+    ch->f_prev = ch->f[ch->L_E - 1];
+    for (int i = 0; i < MAX_M; i++) {
+        ch->E_prev[i] = ch->E[i][ch->L_E - 1];
+        ch->Q_prev[i] = ch->Q[i][ch->L_Q - 1];
+    }
+    for (int i = 0; i < MAX_M; i++) ch->bs_add_harmonic_prev[i] = ch->bs_add_harmonic[i];
+    ch->bs_add_harmonic_flag_prev = ch->bs_add_harmonic_flag;
+    ch->prevEnvIsShort = (ch->l_A == ch->L_E) ? 0 : -1;
+}
+
+static void sbr_save_matrix(orc_sbr_channel* ch)
+{
+    for (int i = 0; i < T_HFGEN; i++) memcpy(ch->Xsbr[i], ch->Xsbr[i + 32], sizeof ch->Xsbr[i]);
+    for (int i = T_HFGEN; i < NTSRHFG; i++) memset(ch->Xsbr[i], 0, sizeof ch->Xsbr[i]);
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* Parse-side state: SBR.decode header handling (A/sbr/SBR.java:161-221), the Channel fields    */
+/* written by sbr_data, and NoiseEnvelope.dequantChannel / unmap (A/sbr/NoiseEnvelope.java)     */
+/* ------------------------------------------------------------------------------------------ */
+static int header_differs(const jaad_sbr_header* a, const jaad_sbr_header* b) /* A/sbr/Header.java:70-78 */
+{
+    return a->start_freq != b->start_freq || a->stop_freq != b->stop_freq || a->freq_scale != b->freq_scale ||
+           a->alter_scale != b->alter_scale || a->xover_band != b->xover_band || a->noise_bands != b->noise_bands;
+}
+
+static float calc_Q_div(const orc_sbr_channel* ch, int m, int l)
+{
+    if (ch->Q[m][l] < 0 || ch->Q[m][l] > 30) return 0;
+    return JAAD_SBR_Q_DIV[ch->Q[m][l]];
+}
+static float calc_Q_div2(const orc_sbr_channel* ch, int m, int l)
+{
+    if (ch->Q[m][l] < 0 || ch->Q[m][l] > 30) return 0;
+    return JAAD_SBR_Q_DIV2[ch->Q[m][l]];
+}
+static float calc_Q_div_c(const orc_sbr* s, int c, int m, int l, int two)
+{
+    int ch0q = s->ch[0].Q[m][l], ch1q = s->ch[1].Q[m][l];
+    if ((ch0q < 0 || ch0q > 30) || (ch1q < 0 || ch1q > 24)) return 0;
+    if (!two) return (c == 0 ? JAAD_SBR_Q_DIV_LEFT : JAAD_SBR_Q_DIV_RIGHT)[ch0q][ch1q >> 1];
+    return (c == 0 ? JAAD_SBR_Q_DIV2_LEFT : JAAD_SBR_Q_DIV2_RIGHT)[ch0q][ch1q >> 1];
+}
+
+static void dequant_channel(const orc_sbr* s, orc_sbr_channel* ch) /* :250-281 */
+{
+    int amp = ch->amp_res ? 0 : 1;
+    for (int l = 0; l < ch->L_E; l++) {
+        for (int k = 0; k < s->n[ch->f[l]]; k++) {
+            int exp = ch->E[k][l] >> amp;
+            if (exp < 0 || exp >= 64) ch->E_orig[k][l] = 0;
+            else {
+                ch->E_orig[k][l] = JAAD_SBR_E_DEQ[exp];
+                if (amp != 0 && (ch->E[k][l] & 1) != 0) ch->E_orig[k][l] = ch->E_orig[k][l] * 1.414213562f;
+            }
+        }
+    }
+    for (int l = 0; l < ch->L_Q; l++)
+        for (int k = 0; k < s->N_Q; k++) {
+            ch->Q_div[k][l] = calc_Q_div(ch, k, l);
+            ch->Q_div2[k][l] = calc_Q_div2(ch, k, l);
+        }
+}
+
+static void unmap(orc_sbr* s) /* :299-344 */
+{
+    orc_sbr_channel *c0 = &s->ch[0], *c1 = &s->ch[1];
+    int amp0 = c0->amp_res ? 0 : 1, amp1 = c1->amp_res ? 0 : 1;
+    for (int l = 0; l < c0->L_E; l++) {
+        for (int k = 0; k < s->n[c0->f[l]]; k++) {
+            int ch0E = c0->E[k][l];
+            int exp0 = (ch0E >> amp0) + 1;
+            int exp1 = c1->E[k][l] >> amp1;
+            if (exp0 < 0 || exp0 >= 64 || exp1 < 0 || exp1 > 24) {
+                c1->E_orig[k][l] = 0;
+                c0->E_orig[k][l] = 0;
+            } else {
+                float tmp = JAAD_SBR_E_DEQ[exp0];
+                if (amp0 != 0 && (ch0E & 1) != 0) tmp = (float)((double)tmp * 1.414213562); /* double literal */
+                c0->E_orig[k][l] = tmp * JAAD_SBR_E_PAN[exp1];
+                c1->E_orig[k][l] = tmp * JAAD_SBR_E_PAN[24 - exp1];
+            }
+        }
+    }
+    for (int l = 0; l < c0->L_Q; l++)
+        for (int k = 0; k < s->N_Q; k++) {
+            c0->Q_div[k][l] = calc_Q_div_c(s, 0, k, l, 0);
+            c1->Q_div[k][l] = calc_Q_div_c(s, 1, k, l, 0);
+            c0->Q_div2[k][l] = calc_Q_div_c(s, 0, k, l, 1);
+            c1->Q_div2[k][l] = calc_Q_div_c(s, 1, k, l, 1);
+        }
+}
+
+/* copy what Channel.sbr_grid / sbr_dtdf / invf_mode / sbr_envelope / sbr_noise /
+ * sinusoidal_coding leave behind (A/sbr/Channel.java:85-437, A/sbr/SBR.java:249-254) */
+static void load_channel(const orc_sbr* s, orc_sbr_channel* ch, const jaad_sbr_channel* in)
+{
+    ch->bs_frame_class = in->frame_class;
+    ch->L_E = in->L_E;
+    ch->L_Q = in->L_Q;
+    ch->bs_pointer = in->bs_pointer;
+    for (int i = 0; i <= MAX_L_E; i++) {
+        ch->t_E[i] = in->t_E[i];
+        ch->f[i] = in->f[i];
+    }
+    for (int i = 0; i < 3; i++) ch->t_Q[i] = in->t_Q[i];
+    for (int n = 0; n < MAX_L_E; n++) ch->bs_invf_mode[n] = in->invf_mode[n];
+    /* sbr_envelope: amp_res (A/sbr/Channel.java:130-133) */
+    ch->amp_res = (ch->L_E == 1 && ch->bs_frame_class == FIXFIX) ? 0 : s->hdr.amp_res;
+    for (int l = 0; l < MAX_L_E; l++)
+        for (int k = 0; k < 64; k++) ch->E[k][l] = in->E[l][k];
+    for (int l = 0; l < 2; l++)
+        for (int k = 0; k < 8; k++) ch->Q[k][l] = in->Q[l][k];
+    /* SBR2/SBR1 sbr_data: bs_add_harmonic cleared, then read for N_high bands */
+    ch->bs_add_harmonic_flag = in->add_harmonic_flag;
+    for (int n = 0; n < 64; n++)
+        ch->bs_add_harmonic[n] = (in->add_harmonic_flag && n < s->N_high) ? (int)((in->add_harmonic >> n) & 1u) : 0;
+}
+
+int orc_sbr_decode(orc_sbr* s, const jaad_sbr_frame* fr, int nch)
+{
+    if (fr->header_present) {
+        int differs = !s->have_hdr || header_differs(&fr->hdr, &s->hdr);
+        s->hdr_saved = s->hdr;
+        s->have_saved = s->have_hdr;
+        s->hdr = fr->hdr;
+        s->have_hdr = 1;
+        s->reset = differs;
+        if (s->reset && calc_sbr_tables(s)) return JAAD_ERR_BITSTREAM; /* the Java would revert the header */
+    } else {
+        s->reset = 0;
+    }
+    if (!s->have_hdr) return JAAD_OK;
+    s->coupling = nch == 2 ? fr->coupling : 0;
+    for (int c = 0; c < nch; c++) {
+        const jaad_sbr_channel* in = &fr->ch[c];
+        if (in->L_E < 1 || in->L_E > MAX_L_E || in->L_Q < 1 || in->L_Q > 2) return JAAD_ERR_BITSTREAM;
+        load_channel(s, &s->ch[c], in);
+    }
+    if (!s->coupling) {
+        for (int c = 0; c < nch; c++) dequant_channel(s, &s->ch[c]);
+    } else {
+        unmap(s);
+    }
+    return JAAD_OK;
+}
+
+/* SBR2.process (A/sbr/SBR2.java:137-157) / SBR1.process without PS (A/sbr/SBR1.java:75-100).
+ * left/right: 2048 floats each, first 1024 = core output; right is ignored when nch == 1
+ * (it receives a copy of left, A/sbr/SBR1.java:79-80). */
+void orc_sbr_process(orc_sbr* s, float* left, float* right, int nch)
+{
+    float Xl[MAX_NTSR][64][2];
+    process_channel(s, &s->ch[0], left, Xl, s->reset);
+    qmf_synthesis(s->ch[0].qmfs_v, &s->ch[0].qmfs_index, Xl, left);
+    if (nch == 2) {
+        process_channel(s, &s->ch[1], right, Xl, 0);
+        qmf_synthesis(s->ch[1].qmfs_v, &s->ch[1].qmfs_index, Xl, right);
+    }
+    if (s->have_hdr) {
+        for (int c = 0; c < nch; c++) sbr_save_prev_data(s, &s->ch[c]);
+    }
+    for (int c = 0; c < nch; c++) sbr_save_matrix(&s->ch[c]);
+    s->frame++;
+    if (nch == 1) memcpy(right, left, 2048 * sizeof(float));
+}
+
+/* derived tables of the current header (tests): k0 k2 kx M N_master N_high N_low N_Q noPatches */
+int orc_sbr_table_info(const jaad_sbr_header* h, int out_sf_index, int* info, int* f_master, int* f_table_lim)
+{
+    orc_sbr* s = (orc_sbr*)calloc(1, sizeof(orc_sbr));
+    if (!s) return JAAD_ERR_NOMEM;
+    s->out_sf_index = out_sf_index;
+    s->hdr = *h;
+    int rc = calc_sbr_tables(s);
+    if (!rc) {
+        patch_construction(s);
+        limiter_frequency_table(s);
+        info[0] = s->k0;
+        info[1] = qmf_stop_channel(h->stop_freq, out_sf_index, s->k0);
+        info[2] = s->kx;
+        info[3] = s->M;
+        info[4] = s->N_master;
+        info[5] = s->N_high;
+        info[6] = s->N_low;
+        info[7] = s->N_Q;
+        info[8] = s->noPatches;
+        info[9] = s->N_L[h->limiter_bands];
+        if (f_master) memcpy(f_master, s->f_master, sizeof s->f_master);
+        if (f_table_lim) memcpy(f_table_lim, s->f_table_lim[h->limiter_bands], sizeof s->f_table_lim[0]);
+    }
+    free(s);
+    return rc ? JAAD_ERR_BITSTREAM : JAAD_OK;
+}

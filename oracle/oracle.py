@@ -35,6 +35,16 @@ def lib() -> C.CDLL:
         L.orc_decode_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_uint32]
         L.orc_decode_batch_mt.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_uint32,
                                           C.c_int]
+        L.orc_stream_bytes.restype = C.c_size_t
+        L.orc_streams_free.argtypes = [C.c_void_p, C.c_int]
+        L.orc_streams_free.restype = None
+        L.orc_sbr_dct4.argtypes = [C.c_void_p] * 4
+        L.orc_sbr_dct4.restype = None
+        L.orc_qmf_analysis_frame.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+        L.orc_qmf_analysis_frame.restype = None
+        L.orc_qmf_synthesis_frame.argtypes = [C.c_void_p] * 4
+        L.orc_qmf_synthesis_frame.restype = None
+        L.orc_sbr_table_info.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
         _lib = L
     return _lib
 
@@ -69,16 +79,69 @@ def pcm_pack(chans: list, flags: int = 0) -> bytes:
     return out.tobytes()
 
 
+def sbr_dct4(re: np.ndarray, im: np.ndarray):
+    a, b = np.ascontiguousarray(re, np.float32), np.ascontiguousarray(im, np.float32)
+    o_re, o_im = np.empty(32, np.float32), np.empty(32, np.float32)
+    lib().orc_sbr_dct4(a.ctypes.data, b.ctypes.data, o_re.ctypes.data, o_im.ctypes.data)
+    return o_re, o_im
+
+
+class QmfAnalysis:
+    """AnalysisFilterbank state (v[1280] ring + index) for frame-by-frame tests."""
+
+    def __init__(self):
+        self.v = np.zeros(1280, np.float32)
+        self.idx = np.zeros(1, np.int32)
+
+    def frame(self, x: np.ndarray, kx: int = 32) -> np.ndarray:
+        x = np.ascontiguousarray(x, np.float32)
+        X = np.zeros((32, 64, 2), np.float32)
+        lib().orc_qmf_analysis_frame(self.v.ctypes.data, self.idx.ctypes.data, x.ctypes.data, X.ctypes.data, kx)
+        return X
+
+
+class QmfSynthesis:
+    """SynthesisFilterbank64 state (v[2560] double ring + index)."""
+
+    def __init__(self):
+        self.v = np.zeros(2560, np.float32)
+        self.idx = np.zeros(1, np.int32)
+
+    def frame(self, X: np.ndarray) -> np.ndarray:
+        X = np.ascontiguousarray(X, np.float32)
+        out = np.empty(2048, np.float32)
+        lib().orc_qmf_synthesis_frame(self.v.ctypes.data, self.idx.ctypes.data, X.ctypes.data, out.ctypes.data)
+        return out
+
+
+def sbr_table_info(hdr, out_sf_index: int):
+    """(info dict, f_master, f_table_lim) of FBT for a header (numpy record of SBR_HEADER_DTYPE)."""
+    h = np.ascontiguousarray(np.array(hdr))
+    info = np.zeros(10, np.int32)
+    fm = np.zeros(64, np.int32)
+    lim = np.zeros(64, np.int32)
+    rc = lib().orc_sbr_table_info(h.ctypes.data, out_sf_index, info.ctypes.data, fm.ctypes.data, lim.ctypes.data)
+    if rc:
+        raise RuntimeError(f"orc_sbr_table_info failed: {rc}")
+    keys = ["k0", "k2", "kx", "M", "N_master", "N_high", "N_low", "N_Q", "noPatches", "N_L"]
+    return dict(zip(keys, map(int, info))), fm, lim
+
+
 class Streams:
-    """Per-slot restated decoder state (orc_stream = ICStream.overlap per channel)."""
+    """Per-slot restated decoder state (orc_stream: ICStream.overlap per channel + SBR object)."""
 
     def __init__(self, n_slots: int):
-        self.state = np.zeros((n_slots, 2, 1024), np.float32)
+        self.n = n_slots
+        self.state = np.zeros((n_slots, lib().orc_stream_bytes()), np.uint8)
+
+    def __del__(self):
+        if _lib is not None and getattr(self, "state", None) is not None:
+            _lib.orc_streams_free(self.state.ctypes.data, self.n)
 
 
 def decode_batch(cfg, batch, streams: Streams, flags: int = 0, threads: int = 1) -> np.ndarray:
     """Decode a jaadec_amd.native.Batch on the CPU restatement; returns uint8 [n_frames, bytes]."""
-    nb = 1024 * 2 * (4 if flags & 2 else 2)
+    nb = (2048 if cfg.sbr else 1024) * 2 * (4 if flags & 2 else 2)
     out = np.empty((batch.n_frames, nb), np.uint8)
     bs = batch.struct()
     if threads == 1:

@@ -1,0 +1,127 @@
+"""Pins the SBR restatement (oracle/jaad_oracle_sbr.c) against closed forms and the reference's
+own derived values (C4 header -> k0 13, k2 45, N_master 16, kx 13, M 32,
+N_high 16, N_low 8, N_Q 4)."""
+import numpy as np
+import pytest
+
+from jaadec_amd import native as N
+from oracle import oracle as O
+
+
+def _table(name: str) -> np.ndarray:
+    src = (N.PKG / "csrc" / "tables" / "jaad_sbr_tables.inc").read_text()
+    i = src.index(name + "[")
+    body = src[src.index("{", i) + 1: src.index("};", i)]
+    toks = [t.strip().rstrip("f") for t in body.replace("{", "").replace("}", "").split(",") if t.strip()]
+    return np.array([float.fromhex(t) if "x" in t else float(t) for t in toks])
+
+
+QMF_C = _table("JAAD_QMF_C")
+
+
+def c4_header():
+    p = N.synth_params(4, n_streams=1, frames_per_stream=1)
+    return N.synth_batch(p).sbr[0]["hdr"]
+
+
+def test_fbt_c4_matches_survey_values():
+    info, f_master, lim = O.sbr_table_info(c4_header(), 3)
+    assert (info["k0"], info["k2"], info["kx"], info["M"]) == (13, 45, 13, 32)
+    assert (info["N_master"], info["N_high"], info["N_low"], info["N_Q"]) == (16, 16, 8, 4)
+    fm = f_master[:17]
+    assert fm[0] == 13 and fm[-1] == 45 and np.all(np.diff(fm) > 0)
+    # limiter table: starts at 0, ends at M, non-decreasing (A/sbr/FBT.java:330-416)
+    nl = info["N_L"]
+    assert lim[0] == 0 and lim[nl] == 32 and np.all(np.diff(lim[:nl + 1]) >= 0)
+
+
+@pytest.mark.parametrize("freq_scale,alter_scale,stop,xover", [(0, 1, 9, 0), (0, 0, 9, 1), (2, 0, 7, 1),
+                                                               (3, 1, 9, 0), (3, 0, 8, 2)])
+def test_fbt_other_headers_are_consistent(freq_scale, alter_scale, stop, xover):
+    h = c4_header().copy()
+    h["freq_scale"], h["alter_scale"], h["stop_freq"], h["xover_band"] = freq_scale, alter_scale, stop, xover
+    info, fm, _ = O.sbr_table_info(h, 3)
+    n = info["N_master"]
+    assert fm[0] == info["k0"] and fm[n] == info["k2"]
+    assert info["kx"] == fm[xover] and info["kx"] + info["M"] == info["k2"]
+    assert info["N_high"] == n - xover and info["N_low"] == (info["N_high"] + 1) // 2
+
+
+def test_qmf_analysis_matches_iso_closed_form():
+    """X(k,l) = 2 sum_n u(n) exp(i pi (k+1/2)(2n-1/2)/64), u from the 640-tap prototype
+    (ISO/IEC 14496-3 4.6.18.4.1); float64 reference, relative error at binary32 level."""
+    rng = np.random.default_rng(1)
+    x = (rng.standard_normal(1024 * 3) * 1000).astype(np.float32)
+    A = O.QmfAnalysis()
+    X = [A.frame(x[i * 1024:(i + 1) * 1024]) for i in range(3)][2]
+    xx = np.concatenate([np.zeros(320), x.astype(np.float64)])
+    k, n = np.arange(32)[:, None], np.arange(64)[None, :]
+    for l in (0, 7, 31):
+        end = 320 + 32 * (64 + l) + 32
+        z = xx[end - 320:end][::-1] * QMF_C[2 * np.arange(320)]
+        u = np.array([z[m::64].sum() for m in range(64)])
+        ref = 2 * (u[None, :] * np.exp(1j * np.pi * (k + 0.5) * (2 * n - 0.5) / 64)).sum(1)
+        got = X[l, :32, 0] + 1j * X[l, :32, 1]
+        assert np.abs(got - ref).max() < 2e-6 * np.abs(ref).max()
+
+
+def test_qmf_analysis_zeroes_bands_above_kx():
+    x = np.random.default_rng(3).standard_normal(1024).astype(np.float32)
+    X = O.QmfAnalysis().frame(x, kx=13)
+    assert np.all(X[:, 13:] == 0) and np.any(X[:, :13] != 0)
+
+
+def test_qmf_synthesis_matches_iso_closed_form():
+    """v(n) = 1/64 sum_k Re(X(k) exp(i pi (k+1/2)(2n-255)/128)), 10-tap window of the 640-tap
+    prototype (ISO/IEC 14496-3 4.6.18.4.2)."""
+    rng = np.random.default_rng(2)
+    Xf = (rng.standard_normal((2, 32, 64, 2)) * 100).astype(np.float32)
+    S = O.QmfSynthesis()
+    got = np.concatenate([S.frame(Xf[i]) for i in range(2)])
+    Xc = (Xf[..., 0].astype(np.float64) + 1j * Xf[..., 1]).reshape(64, 64)
+    k, n = np.arange(64)[None, :], np.arange(128)[:, None]
+    vs = [np.zeros(128)] * 10 + [(np.real(Xc[l][None, :] * np.exp(1j * np.pi * (k + 0.5) * (2 * n - 255) / 128))
+                                  .sum(1) / 64) for l in range(64)]
+    out = []
+    for l in range(64):
+        v = np.concatenate(vs[10 + l::-1][:10])
+        g = np.zeros(640)
+        for i in range(5):
+            g[128 * i:128 * i + 64] = v[256 * i:256 * i + 64]
+            g[128 * i + 64:128 * i + 128] = v[256 * i + 192:256 * i + 256]
+        w = g * QMF_C
+        out.append([w[m::64].sum() for m in range(64)])
+    ref = np.concatenate(out)
+    assert np.abs(got - ref).max() < 2e-6 * np.abs(ref).max()
+
+
+def test_dct4_kernel_is_a_linear_map_of_its_inputs():
+    rng = np.random.default_rng(4)
+    a, b = rng.standard_normal((2, 32)).astype(np.float32)
+    c, d = rng.standard_normal((2, 32)).astype(np.float32)
+    r1, i1 = O.sbr_dct4(a, b)
+    r2, i2 = O.sbr_dct4(c, d)
+    r3, i3 = O.sbr_dct4(a + c, b + d)
+    assert np.allclose(r1 + r2, r3, atol=1e-4) and np.allclose(i1 + i2, i3, atol=1e-4)
+
+
+def test_c4_oracle_decode_levels_and_continuation():
+    p = N.synth_params(4, n_streams=2, frames_per_stream=10)
+    b = N.synth_batch(p)
+    cfg = N.cfg_for(p)
+    assert cfg.sbr == 1 and cfg.ext_sf_index == 3
+    full = O.decode_batch(cfg, b, O.Streams(2), N.PCM_FLOAT32).view(np.float32).reshape(-1, 2048, 2)
+    assert np.isfinite(full).all() and np.abs(full).max() < 32000
+    spec = np.abs(np.fft.rfft(full[4:, :, 0], axis=1)) ** 2
+    hi_lo_db = 10 * np.log10(spec[:, 600:].sum() / spec[:, 30:400].sum())
+    assert -25 < hi_lo_db < -5  # SBR reconstructs a high band at a plausible level
+    # decoding in two calls gives the same bytes as one call (state carried in Streams)
+    a, c = b.split_frames(4)
+    st = O.Streams(2)
+    pa = O.decode_batch(cfg, a, st, N.PCM_BIG_ENDIAN)
+    pc = O.decode_batch(cfg, c, st, N.PCM_BIG_ENDIAN)
+    one = O.decode_batch(cfg, b, O.Streams(2), N.PCM_BIG_ENDIAN)
+    fb = b.frame_begin
+    want = np.concatenate([np.concatenate([one[fb[r]:fb[r] + 4] for r in range(2)]),
+                           np.concatenate([one[fb[r] + 4:fb[r + 1]] for r in range(2)])])
+    assert np.array_equal(np.concatenate([pa, pc]), want)

@@ -41,6 +41,34 @@ TABLES = [
     ("tools/TNSTables.java", "TNS_COEF_1_4", "JAAD_TNS_COEF_1_4", "f32"),
 ]
 
+# SBR (HE-AAC v1) tables -> jaad_sbr_tables.inc.  kind: f32 | f32xN | f32_2d (ragged rows) | i32 | i32_2d
+SBR_OUT = OUT.with_name("jaad_sbr_tables.inc")
+SBR_TABLES = [
+    ("sbr/Filterbank.java", "qmf_c", "JAAD_QMF_C", "f32"),
+    ("sbr/DCT.java", "w_array_real", "JAAD_DCT_W_RE", "f32"),
+    ("sbr/DCT.java", "w_array_imag", "JAAD_DCT_W_IM", "f32"),
+    ("sbr/DCT.java", "dct4_64_tab", "JAAD_DCT4_64_TAB", "f32"),
+    ("sbr/DCT.java", "bit_rev_tab", "JAAD_DCT_BIT_REV", "i32"),
+    ("sbr/NoiseTable.java", "NOISE_TABLE", "JAAD_SBR_NOISE_TABLE", "f32x2"),
+    ("sbr/NoiseEnvelope.java", "E_deq_tab", "JAAD_SBR_E_DEQ", "f32"),
+    ("sbr/NoiseEnvelope.java", "Q_div_tab", "JAAD_SBR_Q_DIV", "f32"),
+    ("sbr/NoiseEnvelope.java", "Q_div2_tab", "JAAD_SBR_Q_DIV2", "f32"),
+    ("sbr/NoiseEnvelope.java", "Q_div_tab_left", "JAAD_SBR_Q_DIV_LEFT", "f32_2d"),
+    ("sbr/NoiseEnvelope.java", "Q_div_tab_right", "JAAD_SBR_Q_DIV_RIGHT", "f32_2d"),
+    ("sbr/NoiseEnvelope.java", "Q_div2_tab_left", "JAAD_SBR_Q_DIV2_LEFT", "f32_2d"),
+    ("sbr/NoiseEnvelope.java", "Q_div2_tab_right", "JAAD_SBR_Q_DIV2_RIGHT", "f32_2d"),
+    ("sbr/NoiseEnvelope.java", "E_pan_tab", "JAAD_SBR_E_PAN", "f32"),
+    ("sbr/HFAdjustment.java", "h_smooth", "JAAD_SBR_H_SMOOTH", "f32"),
+    ("sbr/HFAdjustment.java", "limGain", "JAAD_SBR_LIM_GAIN", "f32"),
+    ("sbr/HFGeneration.java", "goalSbTab", "JAAD_SBR_GOAL_SB", "i32"),
+    ("sbr/FBT.java", "startMinTable", "JAAD_SBR_START_MIN", "i32"),
+    ("sbr/FBT.java", "offsetIndexTable", "JAAD_SBR_OFFSET_INDEX", "i32"),
+    ("sbr/FBT.java", "OFFSET", "JAAD_SBR_OFFSET", "i32_2d"),
+    ("sbr/FBT.java", "stopMinTable", "JAAD_SBR_STOP_MIN", "i32"),
+    ("sbr/FBT.java", "STOP_OFFSET_TABLE", "JAAD_SBR_STOP_OFFSET", "i32_2d"),
+    ("sbr/FBT.java", "limiterBandsCompare", "JAAD_SBR_LIMITER_COMPARE", "f32"),
+]
+
 SWB = [  # ScaleFactorBands: per sampling-frequency-index offset tables
     ("SWB_OFFSET_1024_96", "SWB_OFFSET_1024_64", "SWB_OFFSET_1024_48", "SWB_OFFSET_1024_32",
      "SWB_OFFSET_1024_24", "SWB_OFFSET_1024_16", "SWB_OFFSET_1024_8"),
@@ -142,7 +170,43 @@ def main() -> int:
     OUT.parent.mkdir(parents=True, exist_ok=True)
     OUT.write_text("\n".join(out) + "\n")
     print("wrote", OUT, sum(1 for _ in out), "lines")
+    emit(SBR_TABLES, SBR_OUT)
     return 0
+
+
+def emit(tables, path: Path) -> None:
+    out = ["/* GENERATED by tools/extract_tables.py -- binary32/int constant tables of the",
+           " * reference decoder, carried as data (SURVEY.md s0 item 10). Do not edit. */",
+           "#pragma once", ""]
+    for fname, jname, cname, kind in tables:
+        src = strip_comments((REF / fname).read_text())
+        rows = parse_rows(find_array(src, jname))
+        if kind == "f32":
+            vals = [f32_from_decimal(t) for t in rows]
+            out.append(f"static const float {cname}[{len(vals)}] = {{")
+            for i in range(0, len(vals), 6):
+                out.append("  " + ", ".join(hexf(v) for v in vals[i:i + 6]) + ",")
+        elif kind == "i32":
+            vals = [int(t) for t in rows]
+            out.append(f"static const int {cname}[{len(vals)}] = {{" + ", ".join(map(str, vals)) + ",")
+        elif kind == "i32_2d":
+            ncol = len(rows[0])
+            assert all(len(r) == ncol for r in rows), cname
+            out.append(f"static const int {cname}[{len(rows)}][{ncol}] = {{")
+            for r in rows:
+                out.append("  {" + ", ".join(str(int(t)) for t in r) + "},")
+        else:
+            ncol = len(rows[0]) if kind == "f32_2d" else int(kind[-1])
+            vals = [[f32_from_decimal(t) for t in r[:ncol]] for r in rows]
+            assert all(len(r) == ncol for r in vals), cname
+            out.append(f"static const float {cname}[{len(vals)}][{ncol}] = {{")
+            for r in vals:
+                out.append("  {" + ", ".join(hexf(v) for v in r) + "},")
+        out.append("};")
+        out.append(f"/* from {fname}:{jname} */")
+        out.append("")
+    path.write_text("\n".join(out) + "\n")
+    print("wrote", path, len(out), "lines")
 
 
 if __name__ == "__main__":
