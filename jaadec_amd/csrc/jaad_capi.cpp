@@ -8,7 +8,11 @@
 #include <string>
 #include <vector>
 
+#include <memory>
+
 #include "jaad_lc.h"
+#include "jaad_sbr.h"
+#include "tables/jaad_sbr_tables.inc"
 #include "tables/jaad_tables.inc"
 
 using namespace jaad;
@@ -63,6 +67,15 @@ struct jaad_ctx {
     float* dbg = nullptr;
     int dbg_frame = 0;
     std::string err;
+    // ---- SBR (cfg.sbr) ----
+    std::unique_ptr<SbrHost> sbr_host;
+    std::vector<SbrHostSlot> sbr_slots;          // parameter-side state per slot (host)
+    SbrChState* d_sbr_state[2] = {nullptr, nullptr};  // [slot][2], same parity as d_state
+    float* d_sbr_const = nullptr;                // qmf_c[640] | dct4 tab[192] w_re[16] w_im[16] | noise[1024]
+    DevBuf d_time, d_sbr_recs, d_sbr_epool, d_sbr_tabs, d_sbr_chunks;
+    std::vector<SbrRec> sbr_recs;
+    std::vector<float> sbr_epool;
+    std::vector<SbrChunk> sbr_chunks;
 };
 
 namespace jaad {
@@ -150,7 +163,9 @@ int validate_cfg(const jaad_stream_cfg* cfg)
     if (cfg->sf_index > 11) return JAAD_ERR_UNSUPPORTED;
     if (cfg->channel_config != 1 && cfg->channel_config != 2) return JAAD_ERR_UNSUPPORTED;
     if (cfg->tns_mode > JAAD_TNS_SPEC) return JAAD_ERR_INVALID_ARG;
-    if (cfg->sbr || cfg->ps) return JAAD_ERR_UNSUPPORTED;
+    if (cfg->ps || cfg->sbr > 1) return JAAD_ERR_UNSUPPORTED;
+    // explicit SBR at twice the core rate (bs_samplerate_mode = 1, A/sbr/SBR.java:105)
+    if (cfg->sbr && (cfg->sf_index < 3 || cfg->ext_sf_index + 3 != cfg->sf_index)) return JAAD_ERR_UNSUPPORTED;
     return JAAD_OK;
 }
 
@@ -192,7 +207,94 @@ int plan(jaad_ctx* ctx, const jaad_batch* b)
     return JAAD_OK;
 }
 
-size_t pcm_bytes_per_frame(uint32_t flags) { return (size_t)1024 * 2 * ((flags & JAAD_PCM_FLOAT32) ? 4 : 2); }
+size_t pcm_bytes_per_frame(const jaad_ctx* ctx, uint32_t flags)
+{
+    return (size_t)(ctx->cfg.sbr ? 2048 : 1024) * 2 * ((flags & JAAD_PCM_FLOAT32) ? 4 : 2);
+}
+
+// slots a call does not touch keep their state: carry them into the other parity buffer
+template <typename T>
+int carry_untouched(jaad_ctx* ctx, T* out, const T* in, size_t per_slot, hipStream_t stream)
+{
+    for (uint32_t s = 0; s < ctx->n_slots;) {
+        if (ctx->slot_used[s]) {
+            s++;
+            continue;
+        }
+        uint32_t e = s;
+        while (e < ctx->n_slots && !ctx->slot_used[e]) e++;
+        HIPCHK(hipMemcpyAsync(out + (size_t)s * per_slot, in + (size_t)s * per_slot, (e - s) * per_slot * sizeof(T),
+                              hipMemcpyDeviceToDevice, stream));
+        s = e;
+    }
+    return JAAD_OK;
+}
+
+// SBR: host records in stream order, chunk plan, then the SBR kernel over the core time samples
+int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t flags, hipStream_t stream, int parity)
+{
+    const int nch = ctx->nch;
+    const size_t nf = b->n_frames;
+    ctx->sbr_recs.resize(nf * nch);
+    ctx->sbr_epool.clear();
+    ctx->sbr_chunks.clear();
+    for (uint32_t r = 0; r < b->n_runs; r++) {
+        const uint32_t f0 = b->frame_begin[r], f1 = b->frame_begin[r + 1], slot = b->stream_slot[r];
+        SbrHostSlot& hs = ctx->sbr_slots[slot];
+        for (uint32_t f = f0; f < f1; f++) {
+            int rc = ctx->sbr_host->frame(hs, b->sbr[f], nch, &ctx->sbr_recs[(size_t)f * nch], ctx->sbr_epool);
+            if (rc) {
+                ctx->err = "SBR side info of frame " + std::to_string(f);
+                return rc;
+            }
+        }
+        for (int c = 0; c < nch; c++) {
+            if (f1 == f0) {
+                ctx->sbr_chunks.push_back(SbrChunk{f0, 0, (uint8_t)(kSbrChunkLoad | kSbrChunkStore), (uint8_t)c, slot, 0});
+                continue;
+            }
+            for (uint32_t f = f0; f < f1; f += kSbrChunkFrames) {
+                const uint32_t n = f1 - f < (uint32_t)kSbrChunkFrames ? f1 - f : (uint32_t)kSbrChunkFrames;
+                uint8_t fl = f == f0 ? kSbrChunkLoad : kSbrChunkPrefix;
+                if (f + n == f1) fl |= kSbrChunkStore;
+                ctx->sbr_chunks.push_back(SbrChunk{f, (uint16_t)n, fl, (uint8_t)c, slot, 0});
+            }
+        }
+    }
+    if (ctx->sbr_epool.empty()) ctx->sbr_epool.push_back(0.0f);
+    const auto& tabs = ctx->sbr_host->tabs();
+    HIPCHK(ctx->d_sbr_recs.ensure(ctx->sbr_recs.size() * sizeof(SbrRec) + 256));
+    HIPCHK(ctx->d_sbr_epool.ensure(ctx->sbr_epool.size() * sizeof(float) + 256));
+    HIPCHK(ctx->d_sbr_tabs.ensure((tabs.size() + 1) * sizeof(SbrTab)));
+    HIPCHK(ctx->d_sbr_chunks.ensure(ctx->sbr_chunks.size() * sizeof(SbrChunk) + 256));
+    HIPCHK(hipMemcpyAsync(ctx->d_sbr_recs.p, ctx->sbr_recs.data(), ctx->sbr_recs.size() * sizeof(SbrRec),
+                          hipMemcpyHostToDevice, stream));
+    HIPCHK(hipMemcpyAsync(ctx->d_sbr_epool.p, ctx->sbr_epool.data(), ctx->sbr_epool.size() * sizeof(float),
+                          hipMemcpyHostToDevice, stream));
+    if (!tabs.empty())
+        HIPCHK(hipMemcpyAsync(ctx->d_sbr_tabs.p, tabs.data(), tabs.size() * sizeof(SbrTab), hipMemcpyHostToDevice, stream));
+    HIPCHK(hipMemcpyAsync(ctx->d_sbr_chunks.p, ctx->sbr_chunks.data(), ctx->sbr_chunks.size() * sizeof(SbrChunk),
+                          hipMemcpyHostToDevice, stream));
+    int rc = carry_untouched(ctx, ctx->d_sbr_state[parity ^ 1], ctx->d_sbr_state[parity], 2, stream);
+    if (rc) return rc;
+    SbrArgs a{};
+    a.time = static_cast<const float*>(ctx->d_time.p);
+    a.recs = static_cast<const SbrRec*>(ctx->d_sbr_recs.p);
+    a.epool = static_cast<const float*>(ctx->d_sbr_epool.p);
+    a.tabs = static_cast<const SbrTab*>(ctx->d_sbr_tabs.p);
+    a.chunks = static_cast<const SbrChunk*>(ctx->d_sbr_chunks.p);
+    a.state_in = ctx->d_sbr_state[parity];
+    a.state_out = ctx->d_sbr_state[parity ^ 1];
+    a.pcm = pcm;
+    a.qmf_c = ctx->d_sbr_const;
+    a.dct = ctx->d_sbr_const + 640;
+    a.noise = ctx->d_sbr_const + 640 + 224;
+    a.n_chunks = (uint32_t)ctx->sbr_chunks.size();
+    a.nch = nch;
+    a.out_mode = flags;
+    HIPCHK(launch_sbr(a, stream));
+    return JAAD_OK;
+}
 
 int launch(jaad_ctx* ctx, const jaad_batch* db, void* pcm, uint32_t flags, hipStream_t stream)
 {
@@ -211,31 +313,23 @@ int launch(jaad_ctx* ctx, const jaad_batch* db, void* pcm, uint32_t flags, hipSt
     a.chunks = static_cast<const ChunkDesc*>(ctx->d_chunks.p);
     a.state_in = ctx->d_state[ctx->parity];
     a.state_out = ctx->d_state[ctx->parity ^ 1];
-    a.pcm = pcm;
+    const bool sbr = ctx->cfg.sbr != 0;
+    if (sbr) HIPCHK(ctx->d_time.ensure((size_t)db->n_frames * ctx->nch * 1024 * sizeof(float) + 256));
+    a.pcm = sbr ? ctx->d_time.p : pcm;
     a.n_chunks = (uint32_t)ctx->chunks.size();
     a.nch = (uint32_t)ctx->nch;
-    a.out_mode = flags;
+    a.out_mode = sbr ? kOutPlanarF32 : flags;
     a.tns_mode = ctx->cfg.tns_mode;
     a.dbg = ctx->dbg;
     a.dbg_frame = ctx->dbg_frame;
     if (a.n_chunks == 0) return JAAD_OK;
-    // slots this call does not touch keep their state: carry them into the other buffer
-    size_t slot_bytes = 2048 * sizeof(float);
-    for (uint32_t s = 0; s < ctx->n_slots;) {
-        if (ctx->slot_used[s]) {
-            s++;
-            continue;
-        }
-        uint32_t e = s;
-        while (e < ctx->n_slots && !ctx->slot_used[e]) e++;
-        HIPCHK(hipMemcpyAsync(a.state_out + (size_t)s * 2048, a.state_in + (size_t)s * 2048, (e - s) * slot_bytes,
-                              hipMemcpyDeviceToDevice, stream));
-        s = e;
-    }
+    rc = carry_untouched(ctx, a.state_out, a.state_in, 2048, stream);
+    if (rc) return rc;
     const int per_wg = ctx->nch == 2 ? kWavesPerWG / 2 : kWavesPerWG;
     int grid = (int)((a.n_chunks + per_wg - 1) / per_wg);
     const bool tns_spec = ctx->cfg.tns_mode == JAAD_TNS_SPEC && db->tns != nullptr;
     HIPCHK(launch_lc(a, grid, stream, tns_spec));
+    if (sbr && (rc = launch_sbr_stage(ctx, db, pcm, flags, stream, ctx->parity))) return rc;
     ctx->parity ^= 1;
     return JAAD_OK;
 }
@@ -246,8 +340,8 @@ extern "C" {
 
 int jaad_cfg_sample_length(const jaad_stream_cfg* cfg)
 {
-    (void)cfg;
-    return 1024;  // frameLengthFlag=0, no upsampling SBR (A/DecoderConfig.java:83-86)
+    // frameLengthFlag = 0; doubled by upsampling SBR (A/DecoderConfig.java:83-86)
+    return cfg && cfg->sbr ? 2048 : 1024;
 }
 
 int jaad_cfg_channel_count(const jaad_stream_cfg* cfg)
@@ -336,6 +430,29 @@ int jaad_ctx_create(const jaad_stream_cfg* cfg, uint32_t n_slots, int device, ja
     if ((e = hipMalloc(&ctx->d_iq, sizeof(JAAD_IQ_TABLE))) != hipSuccess) return bail(e, "hipMalloc iq");
     if ((e = hipMemcpy(ctx->d_iq, JAAD_IQ_TABLE, sizeof(JAAD_IQ_TABLE), hipMemcpyHostToDevice)) != hipSuccess)
         return bail(e, "hipMemcpy iq");
+    if (cfg->sbr) {
+        ctx->sbr_host.reset(new (std::nothrow) SbrHost(cfg->ext_sf_index));
+        if (!ctx->sbr_host) {
+            jaad_ctx_destroy(ctx);
+            return JAAD_ERR_NOMEM;
+        }
+        ctx->sbr_slots.resize(n_slots);
+        for (auto& hs : ctx->sbr_slots) SbrHost::reset_slot(hs);
+        const size_t sb = (size_t)n_slots * 2 * sizeof(SbrChState);
+        for (int i = 0; i < 2; i++) {
+            if ((e = hipMalloc(&ctx->d_sbr_state[i], sb)) != hipSuccess) return bail(e, "hipMalloc sbr state");
+            if ((e = hipMemset(ctx->d_sbr_state[i], 0, sb)) != hipSuccess) return bail(e, "hipMemset sbr state");
+        }
+        std::vector<float> k(640 + 224 + 1024);
+        std::memcpy(k.data(), JAAD_QMF_C, sizeof(JAAD_QMF_C));
+        std::memcpy(k.data() + 640, JAAD_DCT4_64_TAB, sizeof(JAAD_DCT4_64_TAB));
+        std::memcpy(k.data() + 640 + 192, JAAD_DCT_W_RE, sizeof(JAAD_DCT_W_RE));
+        std::memcpy(k.data() + 640 + 208, JAAD_DCT_W_IM, sizeof(JAAD_DCT_W_IM));
+        std::memcpy(k.data() + 640 + 224, JAAD_SBR_NOISE_TABLE, sizeof(JAAD_SBR_NOISE_TABLE));
+        if ((e = hipMalloc(&ctx->d_sbr_const, k.size() * sizeof(float))) != hipSuccess) return bail(e, "hipMalloc sbr const");
+        if ((e = hipMemcpy(ctx->d_sbr_const, k.data(), k.size() * sizeof(float), hipMemcpyHostToDevice)) != hipSuccess)
+            return bail(e, "hipMemcpy sbr const");
+    }
     *out = ctx;
     return JAAD_OK;
 }
@@ -350,6 +467,10 @@ void jaad_ctx_destroy(jaad_ctx* ctx)
     if (ctx->d_tables) (void)hipFree(ctx->d_tables);
     if (ctx->d_gtab) (void)hipFree(ctx->d_gtab);
     if (ctx->d_iq) (void)hipFree(ctx->d_iq);
+    for (int i = 0; i < 2; i++)
+        if (ctx->d_sbr_state[i]) (void)hipFree(ctx->d_sbr_state[i]);
+    if (ctx->d_sbr_const) (void)hipFree(ctx->d_sbr_const);
+    for (DevBuf* d : {&ctx->d_time, &ctx->d_sbr_recs, &ctx->d_sbr_epool, &ctx->d_sbr_tabs, &ctx->d_sbr_chunks}) d->release();
     ctx->d_chunks.release();
     ctx->d_batch.release();
     ctx->d_pcm.release();
@@ -362,7 +483,8 @@ static int check_batch(const jaad_ctx* ctx, const jaad_batch* b, size_t pcm_byte
     if (!ctx || !b) return JAAD_ERR_INVALID_ARG;
     if (b->n_frames && (!b->q || !b->sf || !b->cb || !b->ics)) return JAAD_ERR_INVALID_ARG;
     if (ctx->nch == 2 && b->n_frames && !b->ms_used) return JAAD_ERR_INVALID_ARG;
-    if (pcm_bytes < pcm_bytes_per_frame(flags) * b->n_frames) return JAAD_ERR_INVALID_ARG;
+    if (ctx->cfg.sbr && b->n_frames && !b->sbr) return JAAD_ERR_INVALID_ARG;
+    if (pcm_bytes < pcm_bytes_per_frame(ctx, flags) * b->n_frames) return JAAD_ERR_INVALID_ARG;
     if (flags & ~(uint32_t)(JAAD_PCM_LITTLE_ENDIAN | JAAD_PCM_FLOAT32)) return JAAD_ERR_INVALID_ARG;
     return JAAD_OK;
 }
@@ -404,7 +526,7 @@ int jaad_decode_batch(jaad_ctx* ctx, const jaad_batch* b, void* pcm_out, size_t 
     size_t o_ms = al(o_ics + ncf * sizeof(jaad_ics_info)), o_tns = al(o_ms + nf * 16);
     size_t total = al(o_tns + (b->tns ? ncf * sizeof(jaad_tns) : 0));
     HIPCHK(ctx->d_batch.ensure(total + 256));
-    size_t pbytes = pcm_bytes_per_frame(flags) * nf;
+    size_t pbytes = pcm_bytes_per_frame(ctx, flags) * nf;
     HIPCHK(ctx->d_pcm.ensure(pbytes + 256));
     char* base = static_cast<char*>(ctx->d_batch.p);
     hipStream_t s = ctx->stream;
@@ -447,14 +569,25 @@ int jaad_wait(jaad_ctx* ctx)
     return JAAD_OK;
 }
 
-size_t jaad_state_bytes(const jaad_ctx* ctx) { return ctx ? 2048 * sizeof(float) : 0; }
+// per-slot state blob: core overlap [2][1024] f32 | (SBR) device SbrChState[2] | host SbrHostSlot
+size_t jaad_state_bytes(const jaad_ctx* ctx)
+{
+    if (!ctx) return 0;
+    return 2048 * sizeof(float) + (ctx->cfg.sbr ? 2 * sizeof(SbrChState) + sizeof(SbrHostSlot) : 0);
+}
 
 int jaad_state_export(jaad_ctx* ctx, uint32_t slot, void* buf, size_t bytes)
 {
     if (!ctx || !buf || slot >= ctx->n_slots || bytes < jaad_state_bytes(ctx)) return JAAD_ERR_INVALID_ARG;
     HIPCHK(hipSetDevice(ctx->device));
     HIPCHK(hipStreamSynchronize(ctx->stream));
-    HIPCHK(hipMemcpy(buf, ctx->d_state[ctx->parity] + (size_t)slot * 2048, 2048 * sizeof(float), hipMemcpyDeviceToHost));
+    char* o = static_cast<char*>(buf);
+    HIPCHK(hipMemcpy(o, ctx->d_state[ctx->parity] + (size_t)slot * 2048, 2048 * sizeof(float), hipMemcpyDeviceToHost));
+    if (ctx->cfg.sbr) {
+        o += 2048 * sizeof(float);
+        HIPCHK(hipMemcpy(o, ctx->d_sbr_state[ctx->parity] + (size_t)slot * 2, 2 * sizeof(SbrChState), hipMemcpyDeviceToHost));
+        std::memcpy(o + 2 * sizeof(SbrChState), &ctx->sbr_slots[slot], sizeof(SbrHostSlot));
+    }
     return JAAD_OK;
 }
 
@@ -463,7 +596,19 @@ int jaad_state_import(jaad_ctx* ctx, uint32_t slot, const void* buf, size_t byte
     if (!ctx || !buf || slot >= ctx->n_slots || bytes < jaad_state_bytes(ctx)) return JAAD_ERR_INVALID_ARG;
     HIPCHK(hipSetDevice(ctx->device));
     HIPCHK(hipStreamSynchronize(ctx->stream));
-    HIPCHK(hipMemcpy(ctx->d_state[ctx->parity] + (size_t)slot * 2048, buf, 2048 * sizeof(float), hipMemcpyHostToDevice));
+    const char* in = static_cast<const char*>(buf);
+    HIPCHK(hipMemcpy(ctx->d_state[ctx->parity] + (size_t)slot * 2048, in, 2048 * sizeof(float), hipMemcpyHostToDevice));
+    if (ctx->cfg.sbr) {
+        in += 2048 * sizeof(float);
+        SbrHostSlot hs;
+        std::memcpy(&hs, in + 2 * sizeof(SbrChState), sizeof hs);
+        if (hs.have_hdr) {  // re-derive the table index in this context from the saved header
+            hs.table = ctx->sbr_host->table_index(hs.hdr);
+            if (hs.table < 0) return JAAD_ERR_INVALID_ARG;
+        }
+        HIPCHK(hipMemcpy(ctx->d_sbr_state[ctx->parity] + (size_t)slot * 2, in, 2 * sizeof(SbrChState), hipMemcpyHostToDevice));
+        ctx->sbr_slots[slot] = hs;
+    }
     return JAAD_OK;
 }
 
@@ -473,6 +618,10 @@ int jaad_state_reset(jaad_ctx* ctx, uint32_t slot)
     HIPCHK(hipSetDevice(ctx->device));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     HIPCHK(hipMemset(ctx->d_state[ctx->parity] + (size_t)slot * 2048, 0, 2048 * sizeof(float)));
+    if (ctx->cfg.sbr) {
+        HIPCHK(hipMemset(ctx->d_sbr_state[ctx->parity] + (size_t)slot * 2, 0, 2 * sizeof(SbrChState)));
+        SbrHost::reset_slot(ctx->sbr_slots[slot]);
+    }
     return JAAD_OK;
 }
 

@@ -66,7 +66,7 @@ struct KernelArgs {
     void* pcm;                  // frame-major output
     uint32_t n_chunks;
     uint32_t nch;               // 1 (SCE) or 2 (CPE)
-    uint32_t out_mode;          // JAAD_PCM_* flags
+    uint32_t out_mode;          // JAAD_PCM_* flags, or kOutPlanarF32 (SBR input: float [ch-frame][1024])
     uint32_t tns_mode;          // JAAD_TNS_*
     float* dbg;                 // internal: stage dump of frame dbg_frame of chunk 0 (or null)
     int dbg_frame;
@@ -87,6 +87,8 @@ void build_lds_tables(int sf_index, LdsTables* t, GlobalTables* g);
 #ifdef __HIP_PLATFORM_AMD__
 #include <hip/hip_runtime_api.h>
 namespace jaad {
+constexpr uint32_t kOutPlanarF32 = 4;  // internal output mode: core time samples for the SBR kernel
+
 hipError_t launch_lc(const KernelArgs& a, int grid, hipStream_t stream, bool tns_spec);
 }
 #endif

@@ -644,7 +644,8 @@ __global__ __launch_bounds__(kWGThreads, kTnsSpec ? 2 : JAAD_WAVES_PER_EU) void 
     __syncthreads();
 
     constexpr bool big_endian = !(kOut & JAAD_PCM_LITTLE_ENDIAN);
-    constexpr bool out_f32 = (kOut & JAAD_PCM_FLOAT32) != 0;
+    constexpr bool planar = kOut == (int)kOutPlanarF32;
+    constexpr bool out_f32 = (kOut & JAAD_PCM_FLOAT32) != 0 || planar;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     STAMP(0);
     const bool stereo = A.nch == 2;
@@ -919,6 +920,14 @@ __global__ __launch_bounds__(kWGThreads, kTnsSpec ? 2 : JAAD_WAVES_PER_EU) void 
                 const float* bL = stereo ? Wb[wave & ~1] : buf;
                 const float* bR = stereo ? Wb[wave | 1] : buf;
                 const int nj = stereo ? 2 : 4;
+                if constexpr (planar) {  // this wave's channel, time order, for the SBR kernel
+                    float* dst = reinterpret_cast<float*>(A.pcm) + ((size_t)f * nch + c) * 1024;
+#pragma unroll
+                    for (int jj = 0; jj < 4; jj++) {
+                        const int p = 4 * u + 256 * jj;
+                        *reinterpret_cast<float4*>(dst + p) = *reinterpret_cast<const float4*>(buf + p);
+                    }
+                } else
                 for (int jj = 0; jj < nj; jj++) {
                     const int j = stereo ? 2 * c + jj : jj;
                     const int p = 4 * u + 256 * j;  // samples p..p+3
@@ -966,8 +975,11 @@ __global__ __launch_bounds__(kWGThreads, kTnsSpec ? 2 : JAAD_WAVES_PER_EU) void 
 hipError_t launch_lc(const KernelArgs& a, int grid, hipStream_t stream, bool tns_spec)
 {
 #define JAAD_LAUNCH(T, O) hipLaunchKernelGGL((lc_decode_kernel<T, O>), dim3(grid), dim3(kWGThreads), 0, stream, a)
-    const int o = (a.out_mode & JAAD_PCM_FLOAT32) ? 2 : (a.out_mode & JAAD_PCM_LITTLE_ENDIAN) ? 1 : 0;
-    if (tns_spec) {
+    const int o = (a.out_mode == kOutPlanarF32) ? 4 : (a.out_mode & JAAD_PCM_FLOAT32) ? 2 : (a.out_mode & JAAD_PCM_LITTLE_ENDIAN) ? 1 : 0;
+    if (o == 4) {
+        if (tns_spec) JAAD_LAUNCH(true, kOutPlanarF32);
+        else JAAD_LAUNCH(false, kOutPlanarF32);
+    } else if (tns_spec) {
         if (o == 2) JAAD_LAUNCH(true, JAAD_PCM_FLOAT32);
         else if (o == 1) JAAD_LAUNCH(true, JAAD_PCM_LITTLE_ENDIAN);
         else JAAD_LAUNCH(true, JAAD_PCM_BIG_ENDIAN);

@@ -1,0 +1,158 @@
+// SBR (HE-AAC v1) GPU path: records shared by the host builder (jaad_sbr_host.cpp) and the
+// kernel (jaad_sbr.hip).  A/ = aac/src/main/java/net/sourceforge/jaad/aac/ of the reference.
+//
+// Split (SURVEY.md 8a "host -> device per-frame records"): everything that depends only on
+// bitstream parameters -- frequency band tables (A/sbr/FBT.java), patches and limiter tables,
+// envelope/noise dequantisation (A/sbr/NoiseEnvelope.java), chirp factors, l_A, sinusoid maps,
+// noise/sine table indices -- is computed on the host, in stream order, exactly as the Java does;
+// everything that touches samples (QMF analysis, HF generation, envelope estimation, gains,
+// HF assembly, QMF synthesis, PCM) runs in the kernel.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include <vector>
+
+#include "jaad_gpu.h"
+
+namespace jaad {
+
+constexpr int kSbrMaxLE = 5;
+constexpr int kSbrChunkFrames = 16;  // frames per SBR chunk (plus one recomputed prefix frame)
+
+// Tables derived from one header at reset (calc_sbr_tables, patch_construction,
+// limiter_frequency_table) plus the band-counter maps calculate_gain walks through
+// (A/sbr/HFAdjustment.java:250-395), for each limiter-band setting.
+struct SbrTab {
+    uint8_t kx, M, N_Q, N_high, N_low, n_lo, n_hi, pad0;
+    uint8_t N_L[4];
+    uint8_t lim[4][64];       // f_table_lim[s][0..N_L[s]] - kx
+    uint8_t src_p[64];        // HF generation source band of band k (0xFF: not generated)
+    uint8_t g_of_k[64];       // table_map_k_to_g
+    uint8_t res_map[4][2][64];  // [s][f][m]: current_res_band(2) when band m is visited
+    uint8_t noise_map[4][64];   // [s][m]: current_f_noise_band
+    uint8_t f_res[2][64];     // f_table_res (band borders, for interpol_freq == 0)
+};
+
+enum : uint8_t {
+    kSbrReset = 1,       // sbr.reset: assembly ring refill + noise index restart
+    kSbrSmooth = 2,      // bs_smoothing_mode == 0 (h_SL = 4 unless no_noise)
+    kSbrInterpol = 4,    // bs_interpol_freq
+    kSbrProcess = 8,     // a header has been seen (else analysis only, kx = 32)
+};
+
+// One channel-frame.  224 bytes.
+struct SbrRec {
+    uint8_t L_E, table, lim_bands, flags;
+    uint8_t no_noise;           // bit l: l == l_A || l == prevEnvIsShort  (delta = 0, no noise)
+    uint8_t kx_prev, M_prev, sine0;
+    uint16_t noise0;
+    int8_t l_A;
+    uint8_t pad0;
+    uint8_t t_E[6];
+    uint8_t f[6];
+    uint8_t tnb[5];             // current_t_noise_band of envelope l
+    uint8_t pad1[3];
+    float lim_gain;             // limGain[bs_limiter_gains]
+    uint32_t e_off;             // E_orig[l][band] at epool[e_off + sum_{l'<l} n[f[l']] + band]
+    float bw[5];                // bwArray after calc_chirp_factors
+    uint32_t pad2;
+    float q_div[2][5], q_div2[2][5];
+    uint64_t s_index[5];        // bit m: S_index_mapped == 1
+    uint64_t s_mapped[5];       // bit m: S_mapped == 1
+};
+static_assert(sizeof(SbrRec) == 224, "SbrRec layout");
+
+// Per (slot, channel) carried state, in global memory, double-buffered by call parity.
+struct SbrChState {
+    float carry[8][64][2];      // Xsbr rows 0..7 for the next frame (sbr_save_matrix)
+    float vhist[9][128];        // synthesis v blocks of the last 9 slots
+    float tail[288];            // last 288 core samples (analysis ring)
+    float gq[2][5][64];         // G_temp_prev / Q_temp_prev ring [m]
+    uint32_t gq_index;
+    uint32_t pad[3];
+};
+
+enum : uint8_t { kSbrChunkLoad = 1, kSbrChunkPrefix = 2, kSbrChunkStore = 4 };
+
+struct SbrChunk {
+    uint32_t frame0;   // first emitted frame (batch index)
+    uint16_t n;        // emitted frames
+    uint8_t flags;
+    uint8_t ch;
+    uint32_t slot;
+    uint32_t pad;
+};
+
+struct SbrArgs {
+    const float* time;          // [ch-frame][1024] core output (lc kernel, planar f32)
+    const SbrRec* recs;         // [ch-frame]
+    const float* epool;
+    const SbrTab* tabs;
+    const SbrChunk* chunks;
+    const SbrChState* state_in;   // [slot][2]
+    SbrChState* state_out;
+    void* pcm;
+    const float* noise;         // NOISE_TABLE [512][2]
+    const float* qmf_c;         // [640]
+    const float* dct;           // dct4_64_tab [192] + w_re [16] + w_im [16]
+    uint32_t n_chunks;
+    int nch;
+    uint32_t out_mode;          // JAAD_PCM_*
+};
+
+hipError_t launch_sbr(const SbrArgs& a, hipStream_t stream);
+
+// ---------------------------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------------------------
+struct SbrHostCh {
+    float bwArray_prev[64];
+    int invf_prev[5];
+    int add_harmonic_prev[64];
+    int add_harmonic_flag_prev;
+    int prevEnvIsShort;
+    int index_noise_prev, psi_is_prev;
+};
+
+struct SbrHostSlot {
+    int have_hdr;
+    jaad_sbr_header hdr;
+    int table;        // index into the context's table list, -1 before the first header
+    int kx_prev, M_prev;
+    SbrHostCh ch[2];
+};
+
+// Full derived tables of one header (host copy of the SBR object's table fields).
+struct SbrFbt {
+    int k0, k2, kx, M, N_master, N_high, N_low, N_Q, n[2];
+    int f_master[65], f_table_res[2][65], f_table_noise[65], f_table_lim[4][65], N_L[4];
+    int table_map_k_to_g[64];
+    int noPatches, patchNoSubbands[64], patchStartSubband[64];
+    // band counters of calculate_gain per limiter setting s, resolution f, band m
+    int res_map[4][2][64], noise_map[4][64], hi_map[4][64];
+    uint8_t visited[4][64];
+};
+
+class SbrHost {
+public:
+    explicit SbrHost(int out_sf_index) : out_sf_(out_sf_index) {}
+    static void reset_slot(SbrHostSlot& s);
+    // Build the records of one frame of one stream (both channels) in stream order.
+    // Returns 0 or a jaad_status; appends E_orig values to epool.
+    int frame(SbrHostSlot& st, const jaad_sbr_frame& fr, int nch, SbrRec* rec_out, std::vector<float>& epool);
+    const std::vector<SbrTab>& tabs() const { return tabs_; }
+    // table index for a header (built on first use); -1 if its tables are invalid
+    int table_index(const jaad_sbr_header& h) { return table_for(h); }
+
+private:
+    int out_sf_;
+    std::vector<SbrTab> tabs_;
+    std::vector<SbrFbt> fbt_;
+    std::vector<jaad_sbr_header> keys_;
+    int table_for(const jaad_sbr_header& h);
+};
+
+}  // namespace jaad

@@ -1,0 +1,467 @@
+// SBR host-side record builder: the parameter-only half of the reference's SBR path, evaluated in
+// stream order on the host (A/ = aac/src/main/java/net/sourceforge/jaad/aac/).
+//
+//   FBT tables on header reset ........ A/sbr/SBR.java:125-158, A/sbr/FBT.java:29-416
+//   patch construction ................. A/sbr/HFGeneration.java:247-309
+//   chirp factors ...................... A/sbr/HFGeneration.java:199-245
+//   envelope/noise dequantisation ...... A/sbr/NoiseEnvelope.java:190-344
+//   l_A, S_mapped, S_index_mapped ...... A/sbr/HFAdjustment.java:20-80, 250-336
+//   noise / sine index carry ........... A/sbr/HFAdjustment.java:143-237
+//   prev-frame data .................... A/sbr/SBR.java:256-284
+// The signal path (analysis, HF generation, gains, assembly, synthesis) is in jaad_sbr.hip.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+#include "jaad_sbr.h"
+#include "tables/jaad_sbr_tables.inc"
+
+namespace jaad {
+namespace {
+
+enum { LO_RES = 0, HI_RES = 1, FIXFIX = 0, FIXVAR = 1, VARFIX = 2, VARVAR = 3 };
+const int kFreq[12] = {96000, 88200, 64000, 48000, 44100, 32000, 24000, 22050, 16000, 12000, 11025, 8000};
+
+int find_bands(int warp, int bands, int a0, int a1)
+{
+    float div = (float)std::log(2.0);
+    if (warp) div *= 1.3f;
+    return (int)(bands * std::log((double)((float)a1 / (float)a0)) / div + 0.5);
+}
+
+float find_initial_power(int bands, int a0, int a1)
+{
+    return (float)std::pow((double)((float)a1 / (float)a0), (double)(1.0f / (float)bands));
+}
+
+// master frequency band table, bs_freq_scale == 0 (FBT.java:84-129)
+bool master_fs0(SbrFbt& t, int k0, int k2, bool alter)
+{
+    if (k2 <= k0) return false;
+    const int dk = alter ? 2 : 1;
+    int nr = alter ? (((k2 - k0 + 2) >> 2) << 1) : (((k2 - k0) >> 1) << 1);
+    nr = std::min(nr, 63);
+    if (nr <= 0) return false;
+    int vDk[64];
+    for (int k = 0; k < nr; k++) vDk[k] = dk;
+    int diff = k2 - (k0 + nr * dk);
+    if (diff) {
+        const int incr = diff > 0 ? -1 : 1;
+        for (int k = diff > 0 ? nr - 1 : 0; diff; k += incr, diff += incr) vDk[k] -= incr;
+    }
+    t.f_master[0] = k0;
+    for (int k = 1; k <= nr; k++) t.f_master[k] = t.f_master[k - 1] + vDk[k - 1];
+    t.N_master = std::min(nr, 64);
+    return true;
+}
+
+// geometric band steps of one region (FBT.java:181-189 / :215-223)
+void region_steps(int* vDk, int nr, int a0, int a1, int count)
+{
+    const float q = find_initial_power(nr, a0, a1);
+    float qk = (float)a0;
+    int A1 = (int)(qk + 0.5f);
+    for (int k = 0; k < count; k++) {
+        const int A0 = A1;
+        qk *= q;
+        A1 = (int)(qk + 0.5f);
+        vDk[k] = A1 - A0;
+    }
+}
+
+// bs_freq_scale > 0 (FBT.java:150-256); bs_alter_scale is not used by the reference
+bool master_fs(SbrFbt& t, int k0, int k2, int freq_scale)
+{
+    if (k2 <= k0) return false;
+    static const int kBands[3] = {6, 5, 4};
+    const int bands = kBands[freq_scale - 1];
+    const bool two = (double)((float)k2 / (float)k0) > 2.2449;
+    const int k1 = two ? k0 << 1 : k2;
+    int vDk0[65] = {0}, vDk1[65] = {0}, vk0[65], vk1[65];
+    const int nr0 = std::min(2 * find_bands(0, bands, k0, k1), 63);
+    if (nr0 <= 0) return false;
+    region_steps(vDk0, nr0, k0, k1, nr0 + 1);
+    std::sort(vDk0, vDk0 + nr0);
+    vk0[0] = k0;
+    for (int k = 1; k <= nr0; k++) {
+        vk0[k] = vk0[k - 1] + vDk0[k - 1];
+        if (vDk0[k - 1] == 0) return false;
+    }
+    if (!two) {
+        for (int k = 0; k <= nr0; k++) t.f_master[k] = vk0[k];
+        t.N_master = std::min(nr0, 64);
+        return true;
+    }
+    const int nr1 = std::min(2 * find_bands(1, bands, k1, k2), 63);
+    region_steps(vDk1, nr1, k1, k2, nr1);
+    if (vDk1[0] < vDk0[nr0 - 1]) {
+        std::sort(vDk1, vDk1 + nr1 + 1);
+        const int change = vDk0[nr0 - 1] - vDk1[0];
+        vDk1[0] = vDk0[nr0 - 1];
+        vDk1[nr1 - 1] -= change;
+    }
+    std::sort(vDk1, vDk1 + nr1);
+    vk1[0] = k1;
+    for (int k = 1; k <= nr1; k++) {
+        vk1[k] = vk1[k - 1] + vDk1[k - 1];
+        if (vDk1[k - 1] == 0) return false;
+    }
+    t.N_master = std::min(nr0 + nr1, 64);
+    for (int k = 0; k <= nr0; k++) t.f_master[k] = vk0[k];
+    for (int k = nr0 + 1; k <= t.N_master; k++) t.f_master[k] = vk1[k - nr0];
+    return true;
+}
+
+bool derived_tables(SbrFbt& t, int xover, int noise_bands)  // FBT.java:259-320
+{
+    if (t.N_master <= xover) return false;
+    t.N_high = t.N_master - xover;
+    t.N_low = (t.N_high >> 1) + (t.N_high - ((t.N_high >> 1) << 1));
+    t.n[0] = t.N_low;
+    t.n[1] = t.N_high;
+    for (int k = 0; k <= t.N_high; k++) t.f_table_res[HI_RES][k] = t.f_master[k + xover];
+    t.M = t.f_table_res[HI_RES][t.N_high] - t.f_table_res[HI_RES][0];
+    t.kx = t.f_table_res[HI_RES][0];
+    if (t.kx > 32 || t.kx + t.M > 64) return false;
+    const int minus = t.N_high & 1;
+    for (int k = 0, i = 0; k <= t.N_low; k++) {
+        if (k > 0) i = 2 * k - minus;
+        t.f_table_res[LO_RES][k] = t.f_table_res[HI_RES][i];
+    }
+    t.N_Q = noise_bands == 0 ? 1 : std::min(5, std::max(1, find_bands(0, noise_bands, t.kx, t.k2)));
+    for (int k = 0, i = 0; k <= t.N_Q; k++) {
+        if (k > 0) i += (t.N_low - i) / (t.N_Q + 1 - k);
+        t.f_table_noise[k] = t.f_table_res[LO_RES][i];
+    }
+    for (int k = 0; k < 64; k++) {
+        t.table_map_k_to_g[k] = 0;
+        for (int g = 0; g < t.N_Q; g++)
+            if (t.f_table_noise[g] <= k && k < t.f_table_noise[g + 1]) {
+                t.table_map_k_to_g[k] = g;
+                break;
+            }
+    }
+    return true;
+}
+
+void patches(SbrFbt& t, int sfi)  // HFGeneration.java:247-309
+{
+    int msb = t.k0, usb = t.kx, k = 0;
+    const int goal = JAAD_SBR_GOAL_SB[sfi];
+    t.noPatches = 0;
+    if (goal < t.kx + t.M) {
+        for (int i = 0; t.f_master[i] < goal; i++) k = i + 1;
+    } else {
+        k = t.N_master;
+    }
+    if (t.N_master == 0) {
+        t.patchNoSubbands[0] = t.patchStartSubband[0] = 0;
+        return;
+    }
+    int sb;
+    do {
+        int j = k + 1, odd;
+        do {
+            j--;
+            sb = t.f_master[j];
+            odd = (sb - 2 + t.k0) % 2;
+        } while (sb > t.k0 - 1 + msb - odd);
+        t.patchNoSubbands[t.noPatches] = std::max(sb - usb, 0);
+        t.patchStartSubband[t.noPatches] = t.k0 - odd - t.patchNoSubbands[t.noPatches];
+        if (t.patchNoSubbands[t.noPatches] > 0) {
+            usb = msb = sb;
+            t.noPatches++;
+        } else {
+            msb = t.kx;
+        }
+        if (t.f_master[k] - sb < 3) k = t.N_master;
+    } while (sb != t.kx + t.M);
+    if (t.patchNoSubbands[t.noPatches - 1] < 3 && t.noPatches > 1) t.noPatches--;
+    t.noPatches = std::min(t.noPatches, 5);
+}
+
+void limiter_tables(SbrFbt& t)  // FBT.java:330-416
+{
+    t.f_table_lim[0][0] = t.f_table_res[LO_RES][0] - t.kx;
+    t.f_table_lim[0][1] = t.f_table_res[LO_RES][t.N_low] - t.kx;
+    t.N_L[0] = 1;
+    for (int s = 1; s < 4; s++) {
+        int lim[100] = {0}, pb[64] = {0};
+        pb[0] = t.kx;
+        for (int k = 1; k <= t.noPatches; k++) pb[k] = pb[k - 1] + t.patchNoSubbands[k - 1];
+        for (int k = 0; k <= t.N_low; k++) lim[k] = t.f_table_res[LO_RES][k];
+        for (int k = 1; k < t.noPatches; k++) lim[k + t.N_low] = pb[k];
+        std::sort(lim, lim + t.noPatches + t.N_low);
+        int k = 1, nrLim = t.noPatches + t.N_low - 1;
+        if (nrLim < 0) return;
+        auto is_border = [&](int v) {
+            for (int i = 0; i <= t.noPatches; i++)
+                if (v == pb[i]) return true;
+            return false;
+        };
+        while (k <= nrLim) {
+            const float oct = lim[k - 1] != 0 ? (float)lim[k] / (float)lim[k - 1] : 0.0f;
+            if (oct < JAAD_SBR_LIMITER_COMPARE[s - 1]) {
+                if (lim[k] != lim[k - 1] && is_border(lim[k])) {
+                    if (is_border(lim[k - 1])) {
+                        k++;
+                    } else {
+                        lim[k - 1] = t.f_table_res[LO_RES][t.N_low];
+                        std::sort(lim, lim + t.noPatches + t.N_low);
+                        nrLim--;
+                    }
+                    continue;
+                }
+                lim[k] = t.f_table_res[LO_RES][t.N_low];
+                std::sort(lim, lim + nrLim);
+                nrLim--;
+            } else {
+                k++;
+            }
+        }
+        t.N_L[s] = nrLim;
+        for (int l = 0; l <= nrLim; l++) t.f_table_lim[s][l] = lim[l] - t.kx;
+    }
+}
+
+// counters of calculate_gain as the reference walks the limiter bands (HFAdjustment.java:264-323)
+void band_maps(SbrFbt& t)
+{
+    std::memset(t.visited, 0, sizeof t.visited);
+    for (int s = 0; s < 4; s++) {
+        for (int f = 0; f < 2; f++) {
+            int res = 0, noise = 0, hi = 0;
+            for (int k = 0; k < t.N_L[s]; k++)
+                for (int m = t.f_table_lim[s][k]; m < t.f_table_lim[s][k + 1]; m++) {
+                    if (m < 0 || m >= 64) continue;
+                    if (m + t.kx == t.f_table_noise[noise + 1]) noise++;
+                    if (m + t.kx == t.f_table_res[f][res + 1]) res++;
+                    if (m + t.kx == t.f_table_res[HI_RES][hi + 1]) hi++;
+                    t.res_map[s][f][m] = res;
+                    if (f == 0) {
+                        t.noise_map[s][m] = noise;
+                        t.hi_map[s][m] = hi;
+                        t.visited[s][m] = 1;
+                    }
+                }
+        }
+    }
+}
+
+float mapNewBw(int mode, int prev)  // HFGeneration.java:199-223
+{
+    switch (mode) {
+    case 1: return prev == 0 ? 0.6f : 0.75f;
+    case 2: return 0.9f;
+    case 3: return 0.98f;
+    default: return prev == 1 ? 0.6f : 0.0f;
+    }
+}
+
+bool header_differs(const jaad_sbr_header& a, const jaad_sbr_header& b)  // Header.java:70-78
+{
+    return a.start_freq != b.start_freq || a.stop_freq != b.stop_freq || a.freq_scale != b.freq_scale ||
+           a.alter_scale != b.alter_scale || a.xover_band != b.xover_band || a.noise_bands != b.noise_bands;
+}
+
+}  // namespace
+
+void SbrHost::reset_slot(SbrHostSlot& s)
+{
+    std::memset(&s, 0, sizeof s);
+    s.table = -1;
+    for (auto& c : s.ch) c.prevEnvIsShort = -1;
+}
+
+int SbrHost::table_for(const jaad_sbr_header& h)
+{
+    for (size_t i = 0; i < keys_.size(); i++)
+        if (!header_differs(keys_[i], h)) return (int)i;
+    SbrFbt t;
+    std::memset(&t, 0, sizeof t);
+    // SBR.calc_sbr_tables with bs_samplerate_mode = 1 (A/sbr/SBR.java:105,125-158)
+    const int sfi = out_sf_;
+    t.k0 = JAAD_SBR_START_MIN[sfi] + JAAD_SBR_OFFSET[JAAD_SBR_OFFSET_INDEX[sfi]][h.start_freq & 15];
+    if (h.stop_freq == 15) t.k2 = std::min(64, t.k0 * 3);
+    else if (h.stop_freq == 14) t.k2 = std::min(64, t.k0 * 2);
+    else t.k2 = std::min(64, JAAD_SBR_STOP_MIN[sfi] + JAAD_SBR_STOP_OFFSET[sfi][std::min((int)h.stop_freq, 13)]);
+    const int fs = kFreq[sfi];
+    const int span = t.k2 - t.k0;
+    if ((fs >= 48000 && span > 32) || (fs <= 32000 && span > 48) || (fs > 32000 && fs < 48000 && span > 45))
+        return -1;
+    const bool ok = h.freq_scale == 0 ? master_fs0(t, t.k0, t.k2, h.alter_scale != 0)
+                                      : master_fs(t, t.k0, t.k2, h.freq_scale);
+    if (!ok || !derived_tables(t, h.xover_band, h.noise_bands)) return -1;
+    patches(t, sfi);
+    limiter_tables(t);
+    band_maps(t);
+
+    SbrTab g;
+    std::memset(&g, 0, sizeof g);
+    g.kx = (uint8_t)t.kx;
+    g.M = (uint8_t)t.M;
+    g.N_Q = (uint8_t)t.N_Q;
+    g.N_high = (uint8_t)t.N_high;
+    g.N_low = (uint8_t)t.N_low;
+    g.n_lo = (uint8_t)t.n[0];
+    g.n_hi = (uint8_t)t.n[1];
+    for (int s = 0; s < 4; s++) {
+        g.N_L[s] = (uint8_t)t.N_L[s];
+        for (int k = 0; k <= t.N_L[s] && k < 64; k++) g.lim[s][k] = (uint8_t)t.f_table_lim[s][k];
+        for (int m = 0; m < 64; m++) {
+            g.res_map[s][0][m] = (uint8_t)t.res_map[s][0][m];
+            g.res_map[s][1][m] = (uint8_t)t.res_map[s][1][m];
+            g.noise_map[s][m] = (uint8_t)t.noise_map[s][m];
+        }
+    }
+    std::memset(g.src_p, 0xFF, sizeof g.src_p);
+    for (int i = 0, k = t.kx; i < t.noPatches; i++)
+        for (int x = 0; x < t.patchNoSubbands[i]; x++, k++)
+            if (k < 64) g.src_p[k] = (uint8_t)(t.patchStartSubband[i] + x);
+    for (int k = 0; k < 64; k++) g.g_of_k[k] = (uint8_t)t.table_map_k_to_g[k];
+    for (int f = 0; f < 2; f++)
+        for (int k = 0; k <= t.n[f] && k < 64; k++) g.f_res[f][k] = (uint8_t)t.f_table_res[f][k];
+    keys_.push_back(h);
+    fbt_.push_back(t);
+    tabs_.push_back(g);
+    return (int)tabs_.size() - 1;
+}
+
+int SbrHost::frame(SbrHostSlot& st, const jaad_sbr_frame& fr, int nch, SbrRec* rec, std::vector<float>& epool)
+{
+    bool reset = false;
+    if (fr.header_present) {
+        reset = !st.have_hdr || header_differs(fr.hdr, st.hdr);
+        st.hdr = fr.hdr;
+        st.have_hdr = 1;
+        if (reset) {
+            st.table = table_for(fr.hdr);
+            if (st.table < 0) return JAAD_ERR_BITSTREAM;
+        }
+    }
+    if (!st.have_hdr) return JAAD_ERR_UNSUPPORTED;  // frames before the first SBR header
+    if (nch == 2 && fr.coupling) return JAAD_ERR_UNSUPPORTED;
+    const SbrFbt& t = fbt_[st.table];
+    const jaad_sbr_header& h = st.hdr;
+    const int s_lim = h.limiter_bands & 3;
+    for (int c = 0; c < nch; c++) {
+        const jaad_sbr_channel& in = fr.ch[c];
+        SbrHostCh& ch = st.ch[c];
+        SbrRec& r = rec[c];
+        std::memset(&r, 0, sizeof r);
+        const int L_E = in.L_E, L_Q = in.L_Q;
+        if (L_E < 1 || L_E > 5 || L_Q < 1 || L_Q > 2) return JAAD_ERR_BITSTREAM;
+        for (int l = 0; l <= L_E; l++)
+            if (in.t_E[l] > 38 || (l > 0 && in.t_E[l] < in.t_E[l - 1])) return JAAD_ERR_BITSTREAM;
+        for (int l = 0; l < L_E; l++)
+            if (in.f[l] > 1) return JAAD_ERR_BITSTREAM;
+        r.L_E = (uint8_t)L_E;
+        r.table = (uint8_t)st.table;
+        r.lim_bands = (uint8_t)s_lim;
+        r.flags = (uint8_t)((reset ? kSbrReset : 0) | (h.smoothing_mode ? 0 : kSbrSmooth) |
+                            (h.interpol_freq ? kSbrInterpol : 0) | kSbrProcess);
+        r.kx_prev = (uint8_t)st.kx_prev;
+        r.M_prev = (uint8_t)st.M_prev;
+        for (int l = 0; l <= L_E; l++) r.t_E[l] = in.t_E[l];
+        for (int l = 0; l < L_E; l++) r.f[l] = in.f[l];
+        r.lim_gain = JAAD_SBR_LIM_GAIN[h.limiter_gains & 3];
+
+        // l_A (HFAdjustment.java:23-37)
+        int l_A;
+        if (in.frame_class == FIXFIX) l_A = -1;
+        else if (in.frame_class == VARFIX) l_A = in.bs_pointer > 1 ? in.bs_pointer - 1 : -1;
+        else l_A = in.bs_pointer == 0 ? -1 : L_E + 1 - in.bs_pointer;
+        r.l_A = (int8_t)l_A;
+        for (int l = 0; l < L_E; l++)
+            if (l == l_A || l == ch.prevEnvIsShort) r.no_noise |= (uint8_t)(1u << l);
+
+        // current_t_noise_band per envelope (HFAdjustment.java:260-262)
+        for (int l = 0, tnb = 0; l < L_E; l++) {
+            if (in.t_E[l + 1] > in.t_Q[tnb + 1]) tnb++;
+            if (tnb > 1) return JAAD_ERR_BITSTREAM;
+            r.tnb[l] = (uint8_t)tnb;
+        }
+
+        // chirp factors (HFGeneration.java:226-245)
+        for (int i = 0; i < t.N_Q; i++) {
+            float bw = mapNewBw(in.invf_mode[i], ch.invf_prev[i]);
+            if (bw < ch.bwArray_prev[i]) bw = (bw * 0.75f) + (ch.bwArray_prev[i] * 0.25f);
+            else bw = (bw * 0.90625f) + (ch.bwArray_prev[i] * 0.09375f);
+            if (bw < 0.015625f) bw = 0.0f;
+            if (bw >= 0.99609375f) bw = 0.99609375f;
+            r.bw[i] = bw;
+            ch.bwArray_prev[i] = bw;
+            ch.invf_prev[i] = in.invf_mode[i];
+        }
+
+        // dequantisation (NoiseEnvelope.dequantChannel, no coupling)
+        const bool amp_res = !(L_E == 1 && in.frame_class == FIXFIX) && h.amp_res;
+        const int amp = amp_res ? 0 : 1;
+        r.e_off = (uint32_t)epool.size();
+        for (int l = 0; l < L_E; l++)
+            for (int k = 0; k < t.n[in.f[l]]; k++) {
+                const int E = in.E[l][k];
+                const int e = E >> amp;
+                float v = 0.0f;
+                if (e >= 0 && e < 64) {
+                    v = JAAD_SBR_E_DEQ[e];
+                    if (amp != 0 && (E & 1) != 0) v = v * 1.414213562f;
+                }
+                epool.push_back(v);
+            }
+        for (int l = 0; l < L_Q; l++)
+            for (int k = 0; k < t.N_Q; k++) {
+                const int q = in.Q[l][k];
+                const bool ok = q >= 0 && q <= 30;
+                r.q_div[l][k] = ok ? JAAD_SBR_Q_DIV[q] : 0.0f;
+                r.q_div2[l][k] = ok ? JAAD_SBR_Q_DIV2[q] : 0.0f;
+            }
+
+        // sinusoids: bs_add_harmonic cleared, then N_high flags (SBR2.java:63-72, SBR.java:249-254)
+        int harm[64];
+        for (int n = 0; n < 64; n++)
+            harm[n] = (in.add_harmonic_flag && n < t.N_high) ? (int)((in.add_harmonic >> n) & 1u) : 0;
+        auto s_mapped = [&](int l, int band) {  // get_S_mapped (HFAdjustment.java:46-80)
+            if (in.f[l] == HI_RES) {
+                if (l >= l_A || (ch.add_harmonic_prev[band] != 0 && ch.add_harmonic_flag_prev)) return harm[band];
+                return 0;
+            }
+            const int odd = (t.N_high & 1) ? 1 : 0;
+            for (int b = 2 * band - odd; b < 2 * (band + 1) - odd; b++)
+                if (l >= l_A || (ch.add_harmonic_prev[b] != 0 && ch.add_harmonic_flag_prev))
+                    if (harm[b] == 1) return 1;
+            return 0;
+        };
+        for (int l = 0; l < L_E; l++) {
+            uint64_t mi = 0, mm = 0;
+            for (int m = 0; m < t.M && m < 64; m++) {
+                if (!t.visited[s_lim][m]) continue;
+                const int hb = t.hi_map[s_lim][m];
+                if (l >= l_A || (ch.add_harmonic_prev[hb] != 0 && ch.add_harmonic_flag_prev))
+                    if (m + t.kx == (t.f_table_res[HI_RES][hb + 1] + t.f_table_res[HI_RES][hb]) >> 1 && harm[hb])
+                        mi |= 1ull << m;
+                if (s_mapped(l, t.res_map[s_lim][in.f[l]][m])) mm |= 1ull << m;
+            }
+            r.s_index[l] = mi;
+            r.s_mapped[l] = mm;
+        }
+
+        // noise / sine table indices (HFAdjustment.java:151-158, 206, 227, 236-237)
+        const int rows = in.t_E[L_E] - in.t_E[0];
+        const int n0 = reset ? 0 : ch.index_noise_prev;
+        r.noise0 = (uint16_t)n0;
+        r.sine0 = (uint8_t)ch.psi_is_prev;
+        ch.index_noise_prev = (n0 + rows * t.M) & 511;
+        ch.psi_is_prev = (ch.psi_is_prev + rows) & 3;
+
+        // sbr_save_prev_data (SBR.java:256-284)
+        for (int i = 0; i < 49; i++) ch.add_harmonic_prev[i] = harm[i];
+        ch.add_harmonic_flag_prev = in.add_harmonic_flag;
+        ch.prevEnvIsShort = (l_A == L_E) ? 0 : -1;
+    }
+    st.kx_prev = t.kx;
+    st.M_prev = t.M;
+    return JAAD_OK;
+}
+
+}  // namespace jaad

@@ -1,0 +1,139 @@
+"""GPU parity for the SBR (HE-AAC v1) path: the HIP kernels through the C-ABI against the C
+restatement of the reference's SBR (oracle/jaad_oracle_sbr.c).  Bar: bit-exact PCM and bit-exact
+float32 output (SURVEY.md 8d allows |delta| <= 1 LSB / rel-RMS 1e-4; the kernels keep the Java
+binary32 evaluation order, so no tolerance is needed)."""
+import numpy as np
+import pytest
+
+from jaadec_amd import native as N
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _assert_same(got, want, flags):
+    if flags & N.PCM_FLOAT32:
+        g, w = got.view(np.uint32), want.view(np.uint32)
+        bad = np.flatnonzero(g != w)
+        gf, wf = got.view(np.float32).reshape(-1), want.view(np.float32).reshape(-1)
+        assert bad.size == 0, f"{bad.size} float samples differ; first {bad[:4]}: {gf[bad[:4]]} vs {wf[bad[:4]]}"
+    else:
+        bad = np.flatnonzero(got.reshape(-1) != want.reshape(-1))
+        assert bad.size == 0, f"{bad.size} PCM bytes differ, first at byte {bad[:4]}"
+
+
+def _decode_both(p, b, flags, cfg=None):
+    cfg = cfg or N.cfg_for(p)
+    n = int(b.stream_slot.max()) + 1
+    with N.Context(cfg, n) as ctx:
+        got = ctx.decode(b, flags)
+    want = O.decode_batch(cfg, b, O.Streams(n), flags, threads=8)
+    return got, want
+
+
+@pytest.mark.parametrize("flags", [N.PCM_BIG_ENDIAN, N.PCM_LITTLE_ENDIAN, N.PCM_FLOAT32])
+def test_c4_stereo(flags):
+    # 40 frames per stream: chunks at 0 (state), 16 and 32 (recomputed prefix frames)
+    p = N.synth_params(4, n_streams=4, frames_per_stream=40)
+    b = N.synth_batch(p)
+    got, want = _decode_both(p, b, flags)
+    assert got.shape == (b.n_frames, (8192 if not flags & N.PCM_FLOAT32 else 16384))
+    _assert_same(got, want, flags)
+
+
+def test_c4_mono_sbr_duplicated():
+    p = N.synth_params(4, n_streams=3, frames_per_stream=20, channel_config=1)
+    b = N.synth_batch(p)
+    got, want = _decode_both(p, b, N.PCM_FLOAT32)
+    _assert_same(got, want, N.PCM_FLOAT32)
+
+
+def _edit(b, fn):
+    s = b.sbr.copy()
+    fn(s)
+    return N.Batch(b.q, b.sf, b.cb, b.ics, b.ms_used, b.tns, b.stream_slot, b.frame_begin, b.nch, s)
+
+
+@pytest.mark.parametrize("name,fn", [
+    ("smoothing", lambda s: s["hdr"].__setitem__("smoothing_mode", 0)),
+    ("no_interpol", lambda s: s["hdr"].__setitem__("interpol_freq", 0)),
+    ("limiter0", lambda s: s["hdr"].__setitem__("limiter_bands", 0)),
+    ("limiter3_gain0", lambda s: (s["hdr"].__setitem__("limiter_bands", 3), s["hdr"].__setitem__("limiter_gains", 0))),
+    ("freq_scale0", lambda s: s["hdr"].__setitem__("freq_scale", 0)),
+    ("freq_scale3_xover1", lambda s: (s["hdr"].__setitem__("freq_scale", 3), s["hdr"].__setitem__("xover_band", 1))),
+    ("amp_res0", lambda s: s["hdr"].__setitem__("amp_res", 0)),
+])
+def test_c4_header_variants(name, fn):
+    p = N.synth_params(4, n_streams=2, frames_per_stream=34)
+    b = _edit(N.synth_batch(p), fn)
+    got, want = _decode_both(p, b, N.PCM_FLOAT32)
+    _assert_same(got, want, N.PCM_FLOAT32)
+
+
+def _var_grids(s, rng):
+    """Rewrite every second frame as a VARVAR / FIXVAR / VARFIX grid with 2..4 envelopes."""
+    for f in range(1, len(s), 2):
+        for c in range(2):
+            ch = s[f]["ch"][c]
+            if ch["L_E"] == 1:  # FIXFIX with one envelope coded 1.5 dB steps: back to 3 dB units
+                ch["E"] //= 2
+            cls = int(rng.integers(1, 4))
+            L_E = int(rng.integers(2, 5))
+            lead = 0 if cls == 1 else int(rng.integers(0, 3))
+            trail = 16 if cls == 2 else 16 + int(rng.integers(0, 3))
+            inner = np.sort(rng.choice(np.arange(lead + 1, trail), L_E - 1, replace=False))
+            tE = [2 * lead] + [2 * int(x) for x in inner] + [2 * trail]
+            ch["frame_class"], ch["L_E"], ch["L_Q"] = cls, L_E, 2
+            ch["bs_pointer"] = int(rng.integers(0, L_E + 1))
+            ch["t_E"][:] = 0
+            ch["t_E"][:L_E + 1] = tE
+            mid = max(1, min(L_E - 1, L_E // 2))
+            ch["t_Q"][:] = [tE[0], tE[mid], tE[L_E]]
+            ch["f"][:L_E] = rng.integers(0, 2, L_E)
+
+
+def test_c4_variable_grids_and_sinusoids():
+    p = N.synth_params(4, n_streams=2, frames_per_stream=36)
+    b = N.synth_batch(p)
+    rng = np.random.default_rng(7)
+    b = _edit(b, lambda s: _var_grids(s, rng))
+    assert (b.sbr["ch"]["frame_class"] > 0).any() and (b.sbr["ch"]["add_harmonic"] != 0).any()
+    got, want = _decode_both(p, b, N.PCM_FLOAT32)
+    _assert_same(got, want, N.PCM_FLOAT32)
+
+
+def test_c4_continuation_and_state_roundtrip():
+    p = N.synth_params(4, n_streams=3, frames_per_stream=30)
+    b = N.synth_batch(p)
+    cfg = N.cfg_for(p)
+    want = O.decode_batch(cfg, b, O.Streams(3), N.PCM_BIG_ENDIAN)
+    first, second = b.split_frames(13)
+    with N.Context(cfg, 3) as ctx:
+        g1 = ctx.decode(first, N.PCM_BIG_ENDIAN)
+        blob = ctx.state_export(1)
+        with N.Context(cfg, 3) as ctx2:  # resume stream 1 in another context
+            ctx2.state_import(1, blob)
+            g2b = ctx2.decode(second.select_runs([1]), N.PCM_BIG_ENDIAN)
+        g2 = ctx.decode(second, N.PCM_BIG_ENDIAN)
+    fb = b.frame_begin
+    for r in range(3):
+        assert np.array_equal(g1[13 * r:13 * (r + 1)], want[fb[r]:fb[r] + 13])
+        assert np.array_equal(g2[17 * r:17 * (r + 1)], want[fb[r] + 13:fb[r + 1]])
+    assert np.array_equal(g2b, want[fb[1] + 13:fb[2]])
+
+
+def test_c4_single_frame_runs_and_empty_runs():
+    p = N.synth_params(4, n_streams=4, frames_per_stream=9)
+    b = N.synth_batch(p)
+    cfg = N.cfg_for(p)
+    want = O.decode_batch(cfg, b, O.Streams(4), N.PCM_FLOAT32)
+    with N.Context(cfg, 4) as ctx:
+        out = []
+        for cut in range(9):  # one frame per call, every stream
+            one, b2 = b.split_frames(1) if cut == 0 else rest.split_frames(1)
+            rest = b2
+            out.append(ctx.decode(one, N.PCM_FLOAT32))
+    fb = b.frame_begin
+    for k in range(9):
+        for r in range(4):
+            assert np.array_equal(out[k][r], want[fb[r] + k])
