@@ -493,10 +493,10 @@ __global__ __launch_bounds__(64, 1) void sbr_kernel(SbrArgs A)
                 float G_boost = __fdiv_rn(acc1 + EPS, den + EPS);
                 G_boost = java_minf(G_boost, 2.51188643f);
                 for (int mm = ml1; mm < ml2; mm++) {
-                    L.gl[l][mm] = __fsqrt_rn(L.gl[l][mm] * G_boost);
-                    L.ql[l][mm] = __fsqrt_rn(L.ql[l][mm] * G_boost);
+                    L.gl[l][mm] = sqrtf(L.gl[l][mm] * G_boost);
+                    L.ql[l][mm] = sqrtf(L.ql[l][mm] * G_boost);
                     const float sm = L.sl[l][mm];
-                    L.sl[l][mm] = sm != 0.0f ? __fsqrt_rn(sm * G_boost) : 0.0f;
+                    L.sl[l][mm] = sm != 0.0f ? sqrtf(sm * G_boost) : 0.0f;
                 }
             }
         }
@@ -688,3 +688,66 @@ hipError_t launch_sbr(const SbrArgs& a, hipStream_t stream)
 }
 
 }  // namespace jaad
+
+// ---------------------------------------------------------------------------------------------
+// internal self-test entry points (not in the public header): the distributed DCT-IV on its own
+// ---------------------------------------------------------------------------------------------
+namespace jaad {
+namespace {
+__global__ void dct_test_kernel(const float* dct, const float* in_re, const float* in_im, float* out_re,
+                                float* out_im, int n)
+{
+    const int u = lane_id();
+    const int e = u & 31, hb = u & 32;
+    const int v = blockIdx.x * 2 + (u >> 5);
+    DctConst K;
+    const float* wr = dct + 192;
+    const float* wi = dct + 208;
+    K.t0 = dct[e];
+    K.t32 = dct[e + 32];
+    K.t64 = dct[e + 64];
+    K.t96 = dct[e + 96];
+    K.t128 = dct[e + 128];
+    K.t160 = dct[e + 160];
+    K.w1r = wr[e & 15];
+    K.w1i = wi[e & 15];
+    K.w2r = wr[2 * (e & 7)];
+    K.w2i = wi[2 * (e & 7)];
+    K.w3 = (e & 3) == 1 ? wr[4] : wr[12];
+    const int vv = v < n ? v : n - 1;
+    float orr, oi;
+    dct4(K, e, hb, in_re[32 * vv + e], in_im[32 * vv + e], orr, oi);
+    if (v < n) {
+        out_re[32 * v + e] = orr;
+        out_im[32 * v + e] = oi;
+    }
+}
+}  // namespace
+}  // namespace jaad
+
+extern "C" int jaad__sbr_dct_test(const float* dct_dev, const float* in_re, const float* in_im, float* out_re,
+                                  float* out_im, int n)
+{
+    hipLaunchKernelGGL(jaad::dct_test_kernel, dim3((n + 1) / 2), dim3(64), 0, nullptr, dct_dev, in_re, in_im, out_re,
+                       out_im, n);
+    return hipDeviceSynchronize() == hipSuccess ? 0 : -3;
+}
+
+namespace jaad {
+namespace {
+__global__ void math_test_kernel(const float* a, const float* b, float* sq, float* dv, int n)
+{
+    const int i = blockIdx.x * 64 + lane_id();
+    if (i < n) {
+        sq[i] = (float)__dsqrt_rn((double)a[i]);
+        dv[i] = sqrtf(a[i]);
+    }
+}
+}  // namespace
+}  // namespace jaad
+
+extern "C" int jaad__math_test(const float* a, const float* b, float* sq, float* dv, int n)
+{
+    hipLaunchKernelGGL(jaad::math_test_kernel, dim3((n + 63) / 64), dim3(64), 0, nullptr, a, b, sq, dv, n);
+    return hipDeviceSynchronize() == hipSuccess ? 0 : -3;
+}
