@@ -25,12 +25,15 @@ sys.path.insert(0, str(ROOT))
 
 METRIC = "AAC frames/sec (batched) at 1/2/4/8 MI355X; PCM ±1 LSB vs Java ref"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-# algorithmic bytes per long stereo frame = 2 x 4308 + 8 (q, gains, side info, PCM)
-ALGO_BYTES_PER_FRAME = 8624
+# algorithmic bytes per frame.  C2/C3 long stereo frame = 2 x 4308 + 8 (q, gains,
+# side info, PCM); C4 (core + SBR, stereo) = 2 x (2048 q + 188 gains + 16 side + 1300 SBR params
+# + 4096 PCM) = 15296
+ALGO_BYTES = {2: 8624, 3: 8624, 4: 15296}
 
 WORKLOADS = {
     2: "C2: 65536 AAC-LC 48 kHz stereo frames (256 streams x 256), ONLY_LONG windows",
     3: "C3: 65536 AAC-LC 48 kHz stereo frames (256 streams x 256), LONG/START/SHORT/STOP + TNS data (compat)",
+    4: "C4: 32768 HE-AAC v1 frames, 24 kHz AAC-LC stereo core + SBR to 48 kHz (128 streams x 256)",
 }
 
 
@@ -65,10 +68,12 @@ def main():
     p = N.synth_params(args.config)
     p.seed = p.seed + 0x1000 * rank
     batch = N.synth_batch(p)
-    cfg = N.make_cfg(sf_index=p.sf_index, channel_config=p.channel_config)
+    cfg = N.cfg_for(p)
+    sbr = bool(p.sbr)
     n_frames = batch.n_frames
     flags = N.PCM_BIG_ENDIAN
-    pcm_bytes = n_frames * N.pcm_frame_bytes(flags)
+    pcm_bytes = n_frames * N.pcm_frame_bytes(flags, sbr)
+    ALGO_BYTES_PER_FRAME = ALGO_BYTES[args.config]
 
     def to_dev(a):
         if a is None:
@@ -137,7 +142,7 @@ def main():
     cpu = None
     if rank == 0 and not args.no_cpu:
         from oracle import oracle as O
-        ns = min(args.cpu_streams, len(batch.stream_slot))
+        ns = min(args.cpu_streams if not sbr else min(args.cpu_streams, 16), len(batch.stream_slot))
         sub = batch.select_runs(range(ns))
         t1 = time.perf_counter()
         O.decode_batch(cfg, sub, O.Streams(ctx.n_slots), flags, threads=1)
@@ -172,7 +177,8 @@ def main():
             "warmup": args.warmup, "ms_per_step": round(elapsed / steps * 1e3, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {"workload": WORKLOADS[args.config], "frames_per_gpu": n_frames,
-                       "parallelism": f"stream-sharded x{world} (no collectives)", "pcm": "int16 big-endian"},
+                       "parallelism": f"stream-sharded x{world} (no collectives)", "pcm": "int16 big-endian",
+                       "samples_per_frame": 2048 if sbr else 1024},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "traffic_source": traffic_src,

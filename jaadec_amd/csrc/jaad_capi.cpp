@@ -8,7 +8,9 @@
 #include <string>
 #include <vector>
 
+#include <algorithm>
 #include <memory>
+#include <thread>
 
 #include "jaad_lc.h"
 #include "jaad_sbr.h"
@@ -238,16 +240,55 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
     ctx->sbr_recs.resize(nf * nch);
     ctx->sbr_epool.clear();
     ctx->sbr_chunks.clear();
+    // parameter records: runs are independent streams, so they are built in parallel (each
+    // worker owns a contiguous block of runs and its own E_orig pool, rebased afterwards)
+    {
+        unsigned hw = std::thread::hardware_concurrency();
+        int nt = (int)std::min<uint32_t>(b->n_runs, std::min(16u, hw ? hw : 1u));
+        if (nf < 2048) nt = 1;
+        nt = nt < 1 ? 1 : nt;
+        std::vector<std::vector<float>> pools(nt);
+        std::vector<int> rcs(nt, 0), bad(nt, -1);
+        auto work = [&](int t) {
+            const uint32_t r0 = (uint32_t)((uint64_t)b->n_runs * t / nt), r1 = (uint32_t)((uint64_t)b->n_runs * (t + 1) / nt);
+            pools[t].reserve((size_t)(b->frame_begin[r1] - b->frame_begin[r0]) * nch * 40);
+            for (uint32_t r = r0; r < r1 && !rcs[t]; r++) {
+                SbrHostSlot& hs = ctx->sbr_slots[b->stream_slot[r]];
+                for (uint32_t f = b->frame_begin[r]; f < b->frame_begin[r + 1]; f++) {
+                    int rc = ctx->sbr_host->frame(hs, b->sbr[f], nch, &ctx->sbr_recs[(size_t)f * nch], pools[t]);
+                    if (rc) {
+                        rcs[t] = rc;
+                        bad[t] = (int)f;
+                        break;
+                    }
+                }
+            }
+        };
+        std::vector<std::thread> th;
+        for (int t = 1; t < nt; t++) th.emplace_back(work, t);
+        work(0);
+        for (auto& x : th) x.join();
+        size_t base = 0;
+        for (int t = 0; t < nt; t++) {
+            if (rcs[t]) {
+                ctx->err = "SBR side info of frame " + std::to_string(bad[t]);
+                return rcs[t];
+            }
+            const uint32_t r0 = (uint32_t)((uint64_t)b->n_runs * t / nt), r1 = (uint32_t)((uint64_t)b->n_runs * (t + 1) / nt);
+            if (base)
+                for (size_t i = (size_t)b->frame_begin[r0] * nch; i < (size_t)b->frame_begin[r1] * nch; i++)
+                    ctx->sbr_recs[i].e_off += (uint32_t)base;
+            base += pools[t].size();
+        }
+        ctx->sbr_epool.resize(base);
+        base = 0;
+        for (int t = 0; t < nt; t++) {
+            std::memcpy(ctx->sbr_epool.data() + base, pools[t].data(), pools[t].size() * sizeof(float));
+            base += pools[t].size();
+        }
+    }
     for (uint32_t r = 0; r < b->n_runs; r++) {
         const uint32_t f0 = b->frame_begin[r], f1 = b->frame_begin[r + 1], slot = b->stream_slot[r];
-        SbrHostSlot& hs = ctx->sbr_slots[slot];
-        for (uint32_t f = f0; f < f1; f++) {
-            int rc = ctx->sbr_host->frame(hs, b->sbr[f], nch, &ctx->sbr_recs[(size_t)f * nch], ctx->sbr_epool);
-            if (rc) {
-                ctx->err = "SBR side info of frame " + std::to_string(f);
-                return rc;
-            }
-        }
         for (int c = 0; c < nch; c++) {
             if (f1 == f0) {
                 ctx->sbr_chunks.push_back(SbrChunk{f0, 0, (uint8_t)(kSbrChunkLoad | kSbrChunkStore), (uint8_t)c, slot, 0});

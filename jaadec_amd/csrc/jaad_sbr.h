@@ -13,6 +13,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <memory>
+#include <mutex>
 #include <vector>
 
 #include "jaad_gpu.h"
@@ -138,10 +140,16 @@ struct SbrFbt {
 
 class SbrHost {
 public:
-    explicit SbrHost(int out_sf_index) : out_sf_(out_sf_index) {}
+    static constexpr size_t kMaxTables = 1024;  // distinct SBR headers per context
+    explicit SbrHost(int out_sf_index) : out_sf_(out_sf_index)
+    {
+        tabs_.reserve(kMaxTables);
+        fbt_.reserve(kMaxTables);
+        keys_.reserve(kMaxTables);
+    }
     static void reset_slot(SbrHostSlot& s);
     // Build the records of one frame of one stream (both channels) in stream order.
-    // Returns 0 or a jaad_status; appends E_orig values to epool.
+    // Returns 0 or a jaad_status; appends E_orig values to epool.  Thread-safe across slots.
     int frame(SbrHostSlot& st, const jaad_sbr_frame& fr, int nch, SbrRec* rec_out, std::vector<float>& epool);
     const std::vector<SbrTab>& tabs() const { return tabs_; }
     // table index for a header (built on first use); -1 if its tables are invalid
@@ -149,8 +157,9 @@ public:
 
 private:
     int out_sf_;
-    std::vector<SbrTab> tabs_;
-    std::vector<SbrFbt> fbt_;
+    std::mutex mu_;                                  // guards table creation
+    std::vector<SbrTab> tabs_;                       // capacity fixed: elements never move
+    std::vector<std::unique_ptr<SbrFbt>> fbt_;
     std::vector<jaad_sbr_header> keys_;
     int table_for(const jaad_sbr_header& h);
 };

@@ -28,6 +28,7 @@ struct SbrLds {
     float vring[10][128];
     float ecurr[5][64];
     float gl[5][64], ql[5][64], sl[5][64];
+    float gq_eo[64], gq_qm[64], gq_sm[64], gq_g[64];  // per-envelope gain inputs
 };
 
 __device__ __forceinline__ int lane_id() { return (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
@@ -287,6 +288,7 @@ __global__ __launch_bounds__(64, 1) void sbr_kernel(SbrArgs A)
                 xr[8 + 2 * p + s] = re;
                 xi[8 + 2 * p + s] = im;
             }
+            __builtin_amdgcn_sched_barrier(0);
         }
     };
 
@@ -373,6 +375,7 @@ __global__ __launch_bounds__(64, 1) void sbr_kernel(SbrArgs A)
                 p1i = p2i;
                 p2r = sr;
                 p2i = si;
+                __builtin_amdgcn_sched_barrier(0);
             }
         }
 
@@ -439,68 +442,73 @@ __global__ __launch_bounds__(64, 1) void sbr_kernel(SbrArgs A)
         }
         __syncthreads();
 
-        // calculate_gain (:240-415): one lane per (envelope, limiter band), sequential over m
+        // calculate_gain (:240-415).  Per envelope: (1) lanes m evaluate everything that does not
+        // depend on the limiter (Q_M, S_M, the unlimited G) into LDS; (2) one lane per limiter
+        // band walks its bands in order (acc1/acc2, G_max, limiting, den, G_boost) from LDS.
         {
             const int NL = T.N_L[s_lim];
             const float EPS = 1e-12f;
-            for (int idx = u; idx < L_E * NL; idx += 64) {
-                const int l = idx / NL, kb = idx - l * NL;
+            int eo = (int)R.e_off;
+            for (int l = 0; l < L_E; l++) {
                 const int fl = R.f[l];
                 const int tnb = R.tnb[l];
                 const bool delta1 = !((R.no_noise >> l) & 1);
-                int eo = (int)R.e_off;
-                for (int j = 0; j < l; j++) eo += R.f[j] ? T.n_hi : T.n_lo;
-                const float* Eo = A.epool + eo;
-                const int ml1 = T.lim[s_lim][kb], ml2 = T.lim[s_lim][kb + 1];
-                float acc1 = 0.0f, acc2 = 0.0f;
-                for (int mm = ml1; mm < ml2; mm++) {
-                    acc1 += Eo[T.res_map[s_lim][fl][mm]];
-                    acc2 += L.ecurr[l][mm];
-                }
-                float G_max = __fdiv_rn(EPS + acc1, EPS + acc2) * R.lim_gain;
-                G_max = java_minf(G_max, 1e10f);
-                float den = 0.0f;
                 const uint64_t smask = R.s_index[l], mmask = R.s_mapped[l];
-                for (int mm = ml1; mm < ml2; mm++) {
-                    const int nb = T.noise_map[s_lim][mm];
+                if (band) {
+                    const int nb = T.noise_map[s_lim][m];
                     const float Qd = R.q_div[tnb][nb], Qd2 = R.q_div2[tnb][nb];
-                    const float Eom = Eo[T.res_map[s_lim][fl][mm]];
-                    const float Ec = L.ecurr[l][mm];
-                    const bool sidx = (smask >> mm) & 1, smap = (mmask >> mm) & 1;
-                    const float Q_M = Eom * Qd2;
-                    float S_M = 0.0f;
-                    if (sidx) {
-                        S_M = Eom * Qd;
-                        den += S_M;
-                    }
+                    const float Eom = A.epool[eo + T.res_map[s_lim][fl][m]];
+                    const float Ec = L.ecurr[l][m];
+                    const bool sidx = (smask >> m) & 1, smap = (mmask >> m) & 1;
                     float G = __fdiv_rn(Eom, 1.0f + Ec);
                     if (!smap && delta1) G *= Qd;
                     else if (smap) G *= Qd2;
-                    float Ql, Gl;
-                    if (G_max > G) {
-                        Ql = Q_M;
-                        Gl = G;
-                    } else {
-                        Ql = __fdiv_rn(Q_M * G_max, G);
-                        Gl = G_max;
+                    L.gq_eo[m] = Eom;
+                    L.gq_qm[m] = Eom * Qd2;
+                    L.gq_sm[m] = sidx ? Eom * Qd : 0.0f;
+                    L.gq_g[m] = G;
+                }
+                eo += fl ? T.n_hi : T.n_lo;
+                __syncthreads();
+                for (int kb = u; kb < NL; kb += 64) {
+                    const int ml1 = T.lim[s_lim][kb], ml2 = T.lim[s_lim][kb + 1];
+                    float acc1 = 0.0f, acc2 = 0.0f;
+                    for (int mm = ml1; mm < ml2; mm++) {
+                        acc1 += L.gq_eo[mm];
+                        acc2 += L.ecurr[l][mm];
                     }
-                    den += Ec * Gl;
-                    if (!sidx && l != R.l_A) den += Ql;
-                    L.gl[l][mm] = Gl;
-                    L.ql[l][mm] = Ql;
-                    L.sl[l][mm] = S_M;
+                    float G_max = __fdiv_rn(EPS + acc1, EPS + acc2) * R.lim_gain;
+                    G_max = java_minf(G_max, 1e10f);
+                    float den = 0.0f;
+                    for (int mm = ml1; mm < ml2; mm++) {
+                        const bool sidx = (smask >> mm) & 1;
+                        const float Q_M = L.gq_qm[mm], S_M = L.gq_sm[mm], G = L.gq_g[mm], Ec = L.ecurr[l][mm];
+                        if (sidx) den += S_M;
+                        float Ql, Gl;
+                        if (G_max > G) {
+                            Ql = Q_M;
+                            Gl = G;
+                        } else {
+                            Ql = __fdiv_rn(Q_M * G_max, G);
+                            Gl = G_max;
+                        }
+                        den += Ec * Gl;
+                        if (!sidx && l != R.l_A) den += Ql;
+                        L.gl[l][mm] = Gl;
+                        L.ql[l][mm] = Ql;
+                    }
+                    float G_boost = __fdiv_rn(acc1 + EPS, den + EPS);
+                    G_boost = java_minf(G_boost, 2.51188643f);
+                    for (int mm = ml1; mm < ml2; mm++) {
+                        L.gl[l][mm] = sqrtf(L.gl[l][mm] * G_boost);
+                        L.ql[l][mm] = sqrtf(L.ql[l][mm] * G_boost);
+                        const float sm = L.gq_sm[mm];
+                        L.sl[l][mm] = sm != 0.0f ? sqrtf(sm * G_boost) : 0.0f;
+                    }
                 }
-                float G_boost = __fdiv_rn(acc1 + EPS, den + EPS);
-                G_boost = java_minf(G_boost, 2.51188643f);
-                for (int mm = ml1; mm < ml2; mm++) {
-                    L.gl[l][mm] = sqrtf(L.gl[l][mm] * G_boost);
-                    L.ql[l][mm] = sqrtf(L.ql[l][mm] * G_boost);
-                    const float sm = L.sl[l][mm];
-                    L.sl[l][mm] = sm != 0.0f ? sqrtf(sm * G_boost) : 0.0f;
-                }
+                __syncthreads();
             }
         }
-        __syncthreads();
 
         // hf_assembly (:140-238): lane k = m + kx
         {
@@ -571,6 +579,7 @@ __global__ __launch_bounds__(64, 1) void sbr_kernel(SbrArgs A)
                     xi[r] = vi;
                 }
                 gidx = gidx + 1 >= 5 ? 0 : gidx + 1;
+                __builtin_amdgcn_sched_barrier(0);
             }
         }
 
@@ -633,6 +642,7 @@ __global__ __launch_bounds__(64, 1) void sbr_kernel(SbrArgs A)
                     else o[0] = o[1] = (uint16_t)s16;
                 }
             }
+            __builtin_amdgcn_sched_barrier(0);
         }
         carry_shift();
         __syncthreads();

@@ -275,9 +275,12 @@ void SbrHost::reset_slot(SbrHostSlot& s)
 
 int SbrHost::table_for(const jaad_sbr_header& h)
 {
+    std::lock_guard<std::mutex> lock(mu_);
     for (size_t i = 0; i < keys_.size(); i++)
         if (!header_differs(keys_[i], h)) return (int)i;
-    SbrFbt t;
+    if (keys_.size() >= kMaxTables) return -1;
+    auto tp = std::make_unique<SbrFbt>();
+    SbrFbt& t = *tp;
     std::memset(&t, 0, sizeof t);
     // SBR.calc_sbr_tables with bs_samplerate_mode = 1 (A/sbr/SBR.java:105,125-158)
     const int sfi = out_sf_;
@@ -322,7 +325,7 @@ int SbrHost::table_for(const jaad_sbr_header& h)
     for (int f = 0; f < 2; f++)
         for (int k = 0; k <= t.n[f] && k < 64; k++) g.f_res[f][k] = (uint8_t)t.f_table_res[f][k];
     keys_.push_back(h);
-    fbt_.push_back(t);
+    fbt_.push_back(std::move(tp));
     tabs_.push_back(g);
     return (int)tabs_.size() - 1;
 }
@@ -341,7 +344,7 @@ int SbrHost::frame(SbrHostSlot& st, const jaad_sbr_frame& fr, int nch, SbrRec* r
     }
     if (!st.have_hdr) return JAAD_ERR_UNSUPPORTED;  // frames before the first SBR header
     if (nch == 2 && fr.coupling) return JAAD_ERR_UNSUPPORTED;
-    const SbrFbt& t = fbt_[st.table];
+    const SbrFbt& t = *fbt_[st.table];
     const jaad_sbr_header& h = st.hdr;
     const int s_lim = h.limiter_bands & 3;
     for (int c = 0; c < nch; c++) {
@@ -419,6 +422,8 @@ int SbrHost::frame(SbrHostSlot& st, const jaad_sbr_frame& fr, int nch, SbrRec* r
 
         // sinusoids: bs_add_harmonic cleared, then N_high flags (SBR2.java:63-72, SBR.java:249-254)
         int harm[64];
+        const uint64_t hmask = t.N_high >= 64 ? ~0ull : ((1ull << t.N_high) - 1);
+        const bool any_harm = in.add_harmonic_flag && (in.add_harmonic & hmask);
         for (int n = 0; n < 64; n++)
             harm[n] = (in.add_harmonic_flag && n < t.N_high) ? (int)((in.add_harmonic >> n) & 1u) : 0;
         auto s_mapped = [&](int l, int band) {  // get_S_mapped (HFAdjustment.java:46-80)
@@ -432,7 +437,7 @@ int SbrHost::frame(SbrHostSlot& st, const jaad_sbr_frame& fr, int nch, SbrRec* r
                     if (harm[b] == 1) return 1;
             return 0;
         };
-        for (int l = 0; l < L_E; l++) {
+        for (int l = 0; l < L_E && any_harm; l++) {  // no sinusoid flag set: both masks are 0
             uint64_t mi = 0, mm = 0;
             for (int m = 0; m < t.M && m < 64; m++) {
                 if (!t.visited[s_lim][m]) continue;

@@ -303,7 +303,8 @@ class Context:
                       stream_ptr: int | None = None) -> None:
         """Device-resident decode: dev maps array names to device pointers (ints)."""
         bs = BatchStruct(batch.n_frames, len(batch.stream_slot), _ptr(batch.stream_slot), _ptr(batch.frame_begin),
-                         dev["q"], dev["sf"], dev["cb"], dev["ics"], dev.get("ms_used"), dev.get("tns"))
+                         dev["q"], dev["sf"], dev["cb"], dev["ics"], dev.get("ms_used"), dev.get("tns"),
+                         _ptr(batch.sbr))
         self._check(lib().jaad_decode_batch_device(self.h, C.byref(bs), pcm_dev_ptr, pcm_bytes, flags, stream_ptr),
                     "jaad_decode_batch_device")
 
