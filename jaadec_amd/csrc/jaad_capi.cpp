@@ -72,12 +72,14 @@ struct jaad_ctx {
     // ---- SBR (cfg.sbr) ----
     std::unique_ptr<SbrHost> sbr_host;
     std::vector<SbrHostSlot> sbr_slots;          // parameter-side state per slot (host)
-    SbrChState* d_sbr_state[2] = {nullptr, nullptr};  // [slot][2], same parity as d_state
+    SbrChState* d_sbr_state = nullptr;           // [slot][2], rewritten at the end of each call
     float* d_sbr_const = nullptr;                // qmf_c[640] | dct4 tab[192] w_re[16] w_im[16] | noise[1024]
-    DevBuf d_time, d_sbr_recs, d_sbr_epool, d_sbr_tabs, d_sbr_chunks;
+    DevBuf d_time, d_sbr_recs, d_sbr_epool, d_sbr_tabs, d_sbr_chunks, d_sbr_last, d_xlow, d_xsyn, d_xcarry, d_gq;
     std::vector<SbrRec> sbr_recs;
     std::vector<float> sbr_epool;
     std::vector<SbrChunk> sbr_chunks;
+    std::vector<uint32_t> sbr_last;
+    float* sbr_dbg = nullptr;
 };
 
 namespace jaad {
@@ -233,7 +235,7 @@ int carry_untouched(jaad_ctx* ctx, T* out, const T* in, size_t per_slot, hipStre
 }
 
 // SBR: host records in stream order, chunk plan, then the SBR kernel over the core time samples
-int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t flags, hipStream_t stream, int parity)
+int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t flags, hipStream_t stream)
 {
     const int nch = ctx->nch;
     const size_t nf = b->n_frames;
@@ -255,7 +257,8 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
             for (uint32_t r = r0; r < r1 && !rcs[t]; r++) {
                 SbrHostSlot& hs = ctx->sbr_slots[b->stream_slot[r]];
                 for (uint32_t f = b->frame_begin[r]; f < b->frame_begin[r + 1]; f++) {
-                    int rc = ctx->sbr_host->frame(hs, b->sbr[f], nch, &ctx->sbr_recs[(size_t)f * nch], pools[t]);
+                    int rc = ctx->sbr_host->frame(hs, b->sbr[f], nch, f == b->frame_begin[r], b->stream_slot[r],
+                                                  &ctx->sbr_recs[(size_t)f * nch], pools[t]);
                     if (rc) {
                         rcs[t] = rc;
                         bad[t] = (int)f;
@@ -287,52 +290,67 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
             base += pools[t].size();
         }
     }
+    ctx->sbr_last.clear();
+    bool smoothing = false;
+    for (const SbrRec& rr : ctx->sbr_recs) smoothing |= (rr.flags & kSbrSmooth) != 0;
     for (uint32_t r = 0; r < b->n_runs; r++) {
-        const uint32_t f0 = b->frame_begin[r], f1 = b->frame_begin[r + 1], slot = b->stream_slot[r];
+        const uint32_t f0 = b->frame_begin[r], f1 = b->frame_begin[r + 1];
+        if (f1 == f0) continue;  // empty run: the slot state stays as it is
         for (int c = 0; c < nch; c++) {
-            if (f1 == f0) {
-                ctx->sbr_chunks.push_back(SbrChunk{f0, 0, (uint8_t)(kSbrChunkLoad | kSbrChunkStore), (uint8_t)c, slot, 0});
-                continue;
+            for (uint32_t f = f0; f < f1; f += kSbrSynFrames) {
+                const uint32_t n = f1 - f < (uint32_t)kSbrSynFrames ? f1 - f : (uint32_t)kSbrSynFrames;
+                ctx->sbr_chunks.push_back(SbrChunk{f, (uint16_t)n, (uint8_t)c, 0});
             }
-            for (uint32_t f = f0; f < f1; f += kSbrChunkFrames) {
-                const uint32_t n = f1 - f < (uint32_t)kSbrChunkFrames ? f1 - f : (uint32_t)kSbrChunkFrames;
-                uint8_t fl = f == f0 ? kSbrChunkLoad : kSbrChunkPrefix;
-                if (f + n == f1) fl |= kSbrChunkStore;
-                ctx->sbr_chunks.push_back(SbrChunk{f, (uint16_t)n, fl, (uint8_t)c, slot, 0});
-            }
+            ctx->sbr_last.push_back((f1 - 1) * nch + c);
         }
     }
     if (ctx->sbr_epool.empty()) ctx->sbr_epool.push_back(0.0f);
+    const size_t ncf = nf * nch;
     const auto& tabs = ctx->sbr_host->tabs();
     HIPCHK(ctx->d_sbr_recs.ensure(ctx->sbr_recs.size() * sizeof(SbrRec) + 256));
     HIPCHK(ctx->d_sbr_epool.ensure(ctx->sbr_epool.size() * sizeof(float) + 256));
     HIPCHK(ctx->d_sbr_tabs.ensure((tabs.size() + 1) * sizeof(SbrTab)));
     HIPCHK(ctx->d_sbr_chunks.ensure(ctx->sbr_chunks.size() * sizeof(SbrChunk) + 256));
+    HIPCHK(ctx->d_sbr_last.ensure(ctx->sbr_last.size() * sizeof(uint32_t) + 256));
+    HIPCHK(ctx->d_xlow.ensure(ncf * 2048 * sizeof(float) + 256));
+    HIPCHK(ctx->d_xsyn.ensure(ncf * 4096 * sizeof(float) + 256));
+    HIPCHK(ctx->d_xcarry.ensure(ncf * 768 * sizeof(float) + 256));
+    HIPCHK(ctx->d_gq.ensure(ncf * 640 * sizeof(float) + 256));
     HIPCHK(hipMemcpyAsync(ctx->d_sbr_recs.p, ctx->sbr_recs.data(), ctx->sbr_recs.size() * sizeof(SbrRec),
                           hipMemcpyHostToDevice, stream));
     HIPCHK(hipMemcpyAsync(ctx->d_sbr_epool.p, ctx->sbr_epool.data(), ctx->sbr_epool.size() * sizeof(float),
                           hipMemcpyHostToDevice, stream));
     if (!tabs.empty())
         HIPCHK(hipMemcpyAsync(ctx->d_sbr_tabs.p, tabs.data(), tabs.size() * sizeof(SbrTab), hipMemcpyHostToDevice, stream));
-    HIPCHK(hipMemcpyAsync(ctx->d_sbr_chunks.p, ctx->sbr_chunks.data(), ctx->sbr_chunks.size() * sizeof(SbrChunk),
-                          hipMemcpyHostToDevice, stream));
-    int rc = carry_untouched(ctx, ctx->d_sbr_state[parity ^ 1], ctx->d_sbr_state[parity], 2, stream);
-    if (rc) return rc;
+    if (!ctx->sbr_chunks.empty())
+        HIPCHK(hipMemcpyAsync(ctx->d_sbr_chunks.p, ctx->sbr_chunks.data(), ctx->sbr_chunks.size() * sizeof(SbrChunk),
+                              hipMemcpyHostToDevice, stream));
+    if (!ctx->sbr_last.empty())
+        HIPCHK(hipMemcpyAsync(ctx->d_sbr_last.p, ctx->sbr_last.data(), ctx->sbr_last.size() * sizeof(uint32_t),
+                              hipMemcpyHostToDevice, stream));
     SbrArgs a{};
     a.time = static_cast<const float*>(ctx->d_time.p);
     a.recs = static_cast<const SbrRec*>(ctx->d_sbr_recs.p);
     a.epool = static_cast<const float*>(ctx->d_sbr_epool.p);
     a.tabs = static_cast<const SbrTab*>(ctx->d_sbr_tabs.p);
+    a.xlow = static_cast<float*>(ctx->d_xlow.p);
+    a.xsyn = static_cast<float*>(ctx->d_xsyn.p);
+    a.xcarry = static_cast<float*>(ctx->d_xcarry.p);
+    a.gq = static_cast<float*>(ctx->d_gq.p);
     a.chunks = static_cast<const SbrChunk*>(ctx->d_sbr_chunks.p);
-    a.state_in = ctx->d_sbr_state[parity];
-    a.state_out = ctx->d_sbr_state[parity ^ 1];
+    a.last_cf = static_cast<const uint32_t*>(ctx->d_sbr_last.p);
+    a.state = ctx->d_sbr_state;
     a.pcm = pcm;
     a.qmf_c = ctx->d_sbr_const;
     a.dct = ctx->d_sbr_const + 640;
     a.noise = ctx->d_sbr_const + 640 + 224;
+    a.n_cf = (uint32_t)ncf;
     a.n_chunks = (uint32_t)ctx->sbr_chunks.size();
+    a.n_last = (uint32_t)ctx->sbr_last.size();
     a.nch = nch;
     a.out_mode = flags;
+    a.smoothing = smoothing ? 1 : 0;
+    a.dbg = ctx->sbr_dbg;
     HIPCHK(launch_sbr(a, stream));
     return JAAD_OK;
 }
@@ -370,7 +388,7 @@ int launch(jaad_ctx* ctx, const jaad_batch* db, void* pcm, uint32_t flags, hipSt
     int grid = (int)((a.n_chunks + per_wg - 1) / per_wg);
     const bool tns_spec = ctx->cfg.tns_mode == JAAD_TNS_SPEC && db->tns != nullptr;
     HIPCHK(launch_lc(a, grid, stream, tns_spec));
-    if (sbr && (rc = launch_sbr_stage(ctx, db, pcm, flags, stream, ctx->parity))) return rc;
+    if (sbr && (rc = launch_sbr_stage(ctx, db, pcm, flags, stream))) return rc;
     ctx->parity ^= 1;
     return JAAD_OK;
 }
@@ -412,6 +430,14 @@ const char* jaad_strerror(int status)
 }
 
 const char* jaad_last_error(const jaad_ctx* ctx) { return ctx ? ctx->err.c_str() : ""; }
+
+// internal (not in the public header): device buffer receiving SBR stage dumps
+int jaad__sbr_debug_attach(jaad_ctx* ctx, void* dev_buf)
+{
+    if (!ctx) return JAAD_ERR_INVALID_ARG;
+    ctx->sbr_dbg = static_cast<float*>(dev_buf);
+    return JAAD_OK;
+}
 
 // internal (not in the public header): device buffer of 6144 floats receiving stage dumps
 int jaad__debug_attach(jaad_ctx* ctx, void* dev_buf, int frame)
@@ -480,10 +506,8 @@ int jaad_ctx_create(const jaad_stream_cfg* cfg, uint32_t n_slots, int device, ja
         ctx->sbr_slots.resize(n_slots);
         for (auto& hs : ctx->sbr_slots) SbrHost::reset_slot(hs);
         const size_t sb = (size_t)n_slots * 2 * sizeof(SbrChState);
-        for (int i = 0; i < 2; i++) {
-            if ((e = hipMalloc(&ctx->d_sbr_state[i], sb)) != hipSuccess) return bail(e, "hipMalloc sbr state");
-            if ((e = hipMemset(ctx->d_sbr_state[i], 0, sb)) != hipSuccess) return bail(e, "hipMemset sbr state");
-        }
+        if ((e = hipMalloc(&ctx->d_sbr_state, sb)) != hipSuccess) return bail(e, "hipMalloc sbr state");
+        if ((e = hipMemset(ctx->d_sbr_state, 0, sb)) != hipSuccess) return bail(e, "hipMemset sbr state");
         std::vector<float> k(640 + 224 + 1024);
         std::memcpy(k.data(), JAAD_QMF_C, sizeof(JAAD_QMF_C));
         std::memcpy(k.data() + 640, JAAD_DCT4_64_TAB, sizeof(JAAD_DCT4_64_TAB));
@@ -508,10 +532,11 @@ void jaad_ctx_destroy(jaad_ctx* ctx)
     if (ctx->d_tables) (void)hipFree(ctx->d_tables);
     if (ctx->d_gtab) (void)hipFree(ctx->d_gtab);
     if (ctx->d_iq) (void)hipFree(ctx->d_iq);
-    for (int i = 0; i < 2; i++)
-        if (ctx->d_sbr_state[i]) (void)hipFree(ctx->d_sbr_state[i]);
+    if (ctx->d_sbr_state) (void)hipFree(ctx->d_sbr_state);
     if (ctx->d_sbr_const) (void)hipFree(ctx->d_sbr_const);
-    for (DevBuf* d : {&ctx->d_time, &ctx->d_sbr_recs, &ctx->d_sbr_epool, &ctx->d_sbr_tabs, &ctx->d_sbr_chunks}) d->release();
+    for (DevBuf* d : {&ctx->d_time, &ctx->d_sbr_recs, &ctx->d_sbr_epool, &ctx->d_sbr_tabs, &ctx->d_sbr_chunks,
+                      &ctx->d_sbr_last, &ctx->d_xlow, &ctx->d_xsyn, &ctx->d_xcarry, &ctx->d_gq})
+        d->release();
     ctx->d_chunks.release();
     ctx->d_batch.release();
     ctx->d_pcm.release();
@@ -626,7 +651,7 @@ int jaad_state_export(jaad_ctx* ctx, uint32_t slot, void* buf, size_t bytes)
     HIPCHK(hipMemcpy(o, ctx->d_state[ctx->parity] + (size_t)slot * 2048, 2048 * sizeof(float), hipMemcpyDeviceToHost));
     if (ctx->cfg.sbr) {
         o += 2048 * sizeof(float);
-        HIPCHK(hipMemcpy(o, ctx->d_sbr_state[ctx->parity] + (size_t)slot * 2, 2 * sizeof(SbrChState), hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(o, ctx->d_sbr_state + (size_t)slot * 2, 2 * sizeof(SbrChState), hipMemcpyDeviceToHost));
         std::memcpy(o + 2 * sizeof(SbrChState), &ctx->sbr_slots[slot], sizeof(SbrHostSlot));
     }
     return JAAD_OK;
@@ -647,7 +672,7 @@ int jaad_state_import(jaad_ctx* ctx, uint32_t slot, const void* buf, size_t byte
             hs.table = ctx->sbr_host->table_index(hs.hdr);
             if (hs.table < 0) return JAAD_ERR_INVALID_ARG;
         }
-        HIPCHK(hipMemcpy(ctx->d_sbr_state[ctx->parity] + (size_t)slot * 2, in, 2 * sizeof(SbrChState), hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(ctx->d_sbr_state + (size_t)slot * 2, in, 2 * sizeof(SbrChState), hipMemcpyHostToDevice));
         ctx->sbr_slots[slot] = hs;
     }
     return JAAD_OK;
@@ -660,7 +685,7 @@ int jaad_state_reset(jaad_ctx* ctx, uint32_t slot)
     HIPCHK(hipStreamSynchronize(ctx->stream));
     HIPCHK(hipMemset(ctx->d_state[ctx->parity] + (size_t)slot * 2048, 0, 2048 * sizeof(float)));
     if (ctx->cfg.sbr) {
-        HIPCHK(hipMemset(ctx->d_sbr_state[ctx->parity] + (size_t)slot * 2, 0, 2 * sizeof(SbrChState)));
+        HIPCHK(hipMemset(ctx->d_sbr_state + (size_t)slot * 2, 0, 2 * sizeof(SbrChState)));
         SbrHost::reset_slot(ctx->sbr_slots[slot]);
     }
     return JAAD_OK;

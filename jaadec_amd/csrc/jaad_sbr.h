@@ -22,7 +22,7 @@
 namespace jaad {
 
 constexpr int kSbrMaxLE = 5;
-constexpr int kSbrChunkFrames = 16;  // frames per SBR chunk (plus one recomputed prefix frame)
+constexpr int kSbrSynFrames = 4;  // frames per synthesis chunk (its v history is recomputed: 9 slots)
 
 // Tables derived from one header at reset (calc_sbr_tables, patch_construction,
 // limiter_frequency_table) plus the band-counter maps calculate_gain walks through
@@ -52,40 +52,43 @@ struct SbrRec {
     uint8_t kx_prev, M_prev, sine0;
     uint16_t noise0;
     int8_t l_A;
-    uint8_t pad0;
+    uint8_t first;              // first frame of its run: previous-frame data comes from the slot state
     uint8_t t_E[6];
     uint8_t f[6];
     uint8_t tnb[5];             // current_t_noise_band of envelope l
-    uint8_t pad1[3];
+    uint8_t gq0;                // GQ_ringbuf_index when the frame's first row is assembled
+    uint8_t pad1[2];
     float lim_gain;             // limGain[bs_limiter_gains]
     uint32_t e_off;             // E_orig[l][band] at epool[e_off + sum_{l'<l} n[f[l']] + band]
     float bw[5];                // bwArray after calc_chirp_factors
-    uint32_t pad2;
+    uint32_t slot;              // stream slot (state index)
     float q_div[2][5], q_div2[2][5];
     uint64_t s_index[5];        // bit m: S_index_mapped == 1
     uint64_t s_mapped[5];       // bit m: S_mapped == 1
 };
 static_assert(sizeof(SbrRec) == 224, "SbrRec layout");
 
-// Per (slot, channel) carried state, in global memory, double-buffered by call parity.
+// Per (slot, channel) state carried between calls, in global memory.  Read by the kernels of a
+// call for the first frame of a run, rewritten by the last kernel of the call (sbr_state_kernel).
 struct SbrChState {
-    float carry[8][64][2];      // Xsbr rows 0..7 for the next frame (sbr_save_matrix)
-    float vhist[9][128];        // synthesis v blocks of the last 9 slots
-    float tail[288];            // last 288 core samples (analysis ring)
-    float gq[2][5][64];         // G_temp_prev / Q_temp_prev ring [m]
-    uint32_t gq_index;
-    uint32_t pad[3];
+    float tail[288];            // last 288 core samples of the previous frame (analysis ring)
+    float xlow[8][32][2];       // analysis slots 24..31 of the previous frame (Xsbr rows 0..7, k < 32)
+    float xsyn[9][64][2];       // synthesis input rows 23..31 of the previous frame (v history)
+    float xcarry[6][64][2];     // Xsbr rows 34..39 of the previous frame after HF adjustment
+    float gq[2][5][64];         // G/Q smoothing ring after the previous frame [ring position][m]
 };
 
-enum : uint8_t { kSbrChunkLoad = 1, kSbrChunkPrefix = 2, kSbrChunkStore = 4 };
-
+// Frame-parallel pipeline (one launch each, stream-ordered):
+//   sbr_analysis_kernel  [ch-frame]  core time samples -> X_low  (AnalysisFilterbank)
+//   sbr_hf_kernel        [ch-frame]  X_low -> synthesis input X, carry rows, gain ring
+//                                    (HFGeneration, HFAdjustment); twice when smoothing is on
+//   sbr_synthesis_kernel [chunk]     X -> PCM (SynthesisFilterbank64, SampleBuffer.accept)
+//   sbr_state_kernel     [run, ch]   last frame of each run -> SbrChState
 struct SbrChunk {
-    uint32_t frame0;   // first emitted frame (batch index)
-    uint16_t n;        // emitted frames
-    uint8_t flags;
+    uint32_t frame0;   // first frame (batch index)
+    uint16_t n;        // frames
     uint8_t ch;
-    uint32_t slot;
-    uint32_t pad;
+    uint8_t pad;
 };
 
 struct SbrArgs {
@@ -93,16 +96,22 @@ struct SbrArgs {
     const SbrRec* recs;         // [ch-frame]
     const float* epool;
     const SbrTab* tabs;
-    const SbrChunk* chunks;
-    const SbrChState* state_in;   // [slot][2]
-    SbrChState* state_out;
+    float* xlow;                // [ch-frame][32 slots][32 bands][2]
+    float* xsyn;                // [ch-frame][32 slots][64 bands][2]
+    float* xcarry;              // [ch-frame][6][64][2]
+    float* gq;                  // [ch-frame][2][5][64] ring after the frame (smoothing / state)
+    const SbrChunk* chunks;     // synthesis chunks
+    const uint32_t* last_cf;    // ch-frame index of the last frame of each (run, channel)
+    SbrChState* state;          // [slot][2]
     void* pcm;
     const float* noise;         // NOISE_TABLE [512][2]
     const float* qmf_c;         // [640]
     const float* dct;           // dct4_64_tab [192] + w_re [16] + w_im [16]
-    uint32_t n_chunks;
+    uint32_t n_cf, n_chunks, n_last;
     int nch;
     uint32_t out_mode;          // JAAD_PCM_*
+    int smoothing;              // some frame of the batch has bs_smoothing_mode == 0
+    float* dbg;                 // debug dumps (internal, normally null)
 };
 
 hipError_t launch_sbr(const SbrArgs& a, hipStream_t stream);
@@ -117,6 +126,7 @@ struct SbrHostCh {
     int add_harmonic_flag_prev;
     int prevEnvIsShort;
     int index_noise_prev, psi_is_prev;
+    int gq_index;
 };
 
 struct SbrHostSlot {
@@ -150,7 +160,8 @@ public:
     static void reset_slot(SbrHostSlot& s);
     // Build the records of one frame of one stream (both channels) in stream order.
     // Returns 0 or a jaad_status; appends E_orig values to epool.  Thread-safe across slots.
-    int frame(SbrHostSlot& st, const jaad_sbr_frame& fr, int nch, SbrRec* rec_out, std::vector<float>& epool);
+    int frame(SbrHostSlot& st, const jaad_sbr_frame& fr, int nch, bool first, uint32_t slot, SbrRec* rec_out,
+              std::vector<float>& epool);
     const std::vector<SbrTab>& tabs() const { return tabs_; }
     // table index for a header (built on first use); -1 if its tables are invalid
     int table_index(const jaad_sbr_header& h) { return table_for(h); }

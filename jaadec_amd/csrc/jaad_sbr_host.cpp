@@ -330,7 +330,8 @@ int SbrHost::table_for(const jaad_sbr_header& h)
     return (int)tabs_.size() - 1;
 }
 
-int SbrHost::frame(SbrHostSlot& st, const jaad_sbr_frame& fr, int nch, SbrRec* rec, std::vector<float>& epool)
+int SbrHost::frame(SbrHostSlot& st, const jaad_sbr_frame& fr, int nch, bool first, uint32_t slot, SbrRec* rec,
+                   std::vector<float>& epool)
 {
     bool reset = false;
     if (fr.header_present) {
@@ -356,6 +357,8 @@ int SbrHost::frame(SbrHostSlot& st, const jaad_sbr_frame& fr, int nch, SbrRec* r
         if (L_E < 1 || L_E > 5 || L_Q < 1 || L_Q > 2) return JAAD_ERR_BITSTREAM;
         for (int l = 0; l <= L_E; l++)
             if (in.t_E[l] > 38 || (l > 0 && in.t_E[l] < in.t_E[l - 1])) return JAAD_ERR_BITSTREAM;
+        // envelope_time_border_vector: lead border <= 2*3, trail border >= 2*16 (Channel.java:455-542)
+        if (in.t_E[0] > 6 || in.t_E[L_E] < 32) return JAAD_ERR_BITSTREAM;
         for (int l = 0; l < L_E; l++)
             if (in.f[l] > 1) return JAAD_ERR_BITSTREAM;
         r.L_E = (uint8_t)L_E;
@@ -363,6 +366,8 @@ int SbrHost::frame(SbrHostSlot& st, const jaad_sbr_frame& fr, int nch, SbrRec* r
         r.lim_bands = (uint8_t)s_lim;
         r.flags = (uint8_t)((reset ? kSbrReset : 0) | (h.smoothing_mode ? 0 : kSbrSmooth) |
                             (h.interpol_freq ? kSbrInterpol : 0) | kSbrProcess);
+        r.first = first ? 1 : 0;
+        r.slot = slot;
         r.kx_prev = (uint8_t)st.kx_prev;
         r.M_prev = (uint8_t)st.M_prev;
         for (int l = 0; l <= L_E; l++) r.t_E[l] = in.t_E[l];
@@ -458,6 +463,10 @@ int SbrHost::frame(SbrHostSlot& st, const jaad_sbr_frame& fr, int nch, SbrRec* r
         r.sine0 = (uint8_t)ch.psi_is_prev;
         ch.index_noise_prev = (n0 + rows * t.M) & 511;
         ch.psi_is_prev = (ch.psi_is_prev + rows) & 3;
+        // G/Q ring position (HFAdjustment.java:166-173, 229-232)
+        const int gq0 = reset ? 4 : ch.gq_index;
+        r.gq0 = (uint8_t)gq0;
+        ch.gq_index = (gq0 + rows) % 5;
 
         // sbr_save_prev_data (SBR.java:256-284)
         for (int i = 0; i < 49; i++) ch.add_harmonic_prev[i] = harm[i];

@@ -1173,3 +1173,11 @@ int orc_sbr_table_info(const jaad_sbr_header* h, int out_sf_index, int* info, in
     free(s);
     return rc ? JAAD_ERR_BITSTREAM : JAAD_OK;
 }
+
+/* debug: G/Q smoothing ring of channel c after the last processed frame: out[2][5][64], returns index */
+int orc_sbr_debug_ring(const orc_sbr* s, int c, float* out)
+{
+    memcpy(out, s->ch[c].G_temp_prev, sizeof s->ch[c].G_temp_prev);
+    memcpy(out + 320, s->ch[c].Q_temp_prev, sizeof s->ch[c].Q_temp_prev);
+    return s->ch[c].GQ_ringbuf_index;
+}
