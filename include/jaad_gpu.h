@@ -80,7 +80,8 @@ typedef struct jaad_stream_cfg {
     uint8_t channel_config;   /* 1 = one SCE (mono), 2 = one CPE (stereo)                        */
     uint8_t tns_mode;         /* JAAD_TNS_COMPAT | JAAD_TNS_SPEC                                  */
     uint8_t sbr;              /* 1 = explicit SBR (AOT 5): jaad_batch.sbr carries one record/frame  */
-    uint8_t ps;               /* 0 (parametric stereo, AOT 29, is not in this ABI revision)       */
+    uint8_t ps;               /* 1 = parametric stereo (AOT 29): SCE core + SBR + PS -> stereo;
+                                 requires sbr = 1 and channel_config = 1                         */
     uint8_t ext_sf_index;     /* SBR output SampleFrequency index (extensionSampleFrequency of the
                                  ASC, A/DecoderConfig.java:184-198); must be the core index - 3,
                                  i.e. twice the core rate (bs_samplerate_mode = 1)                */
@@ -158,13 +159,29 @@ typedef struct jaad_sbr_channel {  /* Channel fields after sbr_data (A/sbr/Chann
     uint8_t reserved[7];
 } jaad_sbr_channel;                /* 712 bytes */
 
+/*
+ * Parametric stereo parameters of one frame as PSImpl.ps_data_decode leaves them
+ * (A/ps/PSImpl.java:137-199): envelope borders and delta-decoded IID/ICC indices per parameter band.
+ */
+typedef struct jaad_ps_frame {
+    uint8_t iid_mode, icc_mode;    /* IIDMode / ICCMode ids 0..5 (A/ps/IIDMode.java:48-55)           */
+    uint8_t num_env;               /* 1..5 after ps_data_decode                                      */
+    uint8_t ext;                   /* IPD/OPD extension present: must be 0 in this ABI revision      */
+    uint8_t border[6];             /* border_position[0..num_env]                                     */
+    uint8_t reserved[2];
+    int8_t iid[5][34];             /* iid_index[env][bk]  (|.| <= 7 normal, <= 15 fine)              */
+    int8_t icc[5][34];             /* icc_index[env][bk]  (0..7)                                     */
+} jaad_ps_frame;                   /* 352 bytes */
+
 typedef struct jaad_sbr_frame {
     uint8_t header_present;        /* bs_header_flag: hdr below is this frame's sbr_header           */
     uint8_t coupling;              /* bs_coupling (CPE only)                                         */
-    uint8_t reserved[2];
+    uint8_t ps_present;            /* PS data decoded for this frame (SBR1.isPSUsed, A/sbr/SBR1.java:136) */
+    uint8_t reserved;
     jaad_sbr_header hdr;
     jaad_sbr_channel ch[2];        /* ch[1] unused for an SCE                                        */
-} jaad_sbr_frame;                  /* 1440 bytes */
+    jaad_ps_frame ps;              /* valid when ps_present                                          */
+} jaad_sbr_frame;                  /* 1792 bytes */
 
 /*
  * A batch: n_frames frames (raw_data_blocks) of one channel configuration.  Frames are grouped

@@ -32,12 +32,12 @@ typedef struct jaad_synth_params {
     uint8_t global_gain;      /* centre of the scalefactor random walk (130)                 */
     uint8_t escape_permille;  /* per-mille of bins replaced by escapes |q| in [16,1023]      */
     uint8_t common_window;    /* CPE: 1 = common_window (C2/C3)                              */
-    uint8_t sbr;              /* 1: also emit SBR records (jaad_synth_sbr), C4              */
+    uint8_t sbr;              /* 1: also emit SBR records (jaad_synth_sbr), C4; 2: SBR + PS, C5 */
     uint8_t sbr_level;        /* centre of the envelope-scalefactor walk, 3 dB units        */
     uint32_t pns_state0;      /* static ICStream.randomState before the first ch-frame       */
 } jaad_synth_params;
 
-/* defaults for a BASELINE.json config id (1..4: C1 mono 44.1k, C2, C3, C4 HE-AAC v1) */
+/* defaults for a BASELINE.json config id (1..5: C1 mono 44.1k, C2, C3, C4 HE-AAC v1, C5 HE-AAC v2) */
 void jaad_synth_default(int config_id, jaad_synth_params* p);
 
 /* Fill caller-allocated arrays (sizes: ch = channel_config, F = n_streams*frames_per_stream):

@@ -194,7 +194,11 @@ void gen_sbr_stream(const jaad_synth_params& P, jaad_sbr_frame* out, uint32_t s)
     const int nch = P.channel_config == 2 ? 2 : 1;
     SplitMix64 r{P.seed ^ (0x5B5B5B5Bull + (uint64_t)s * 0xD1B54A32D192ED03ull)};
     for (int i = 0; i < 4; i++) r.next();
-    int lvl[2][64], qv[2][5];
+    int lvl[2][64], qv[2][5], iid[34], icc[34];
+    for (int b = 0; b < 34; b++) {
+        iid[b] = (int)r.below(9) - 4;
+        icc[b] = (int)r.below(8);
+    }
     for (int c = 0; c < 2; c++) {
         for (int k = 0; k < 64; k++) lvl[c][k] = P.sbr_level - (int)r.below(5);
         for (int k = 0; k < 5; k++) qv[c][k] = 8 + (int)r.below(16);
@@ -244,6 +248,27 @@ void gen_sbr_stream(const jaad_synth_params& P, jaad_sbr_frame* out, uint32_t s)
                 for (int k = 0; k < 64; k++)
                     if (r.percent(5)) C.add_harmonic |= 1ull << k;
         }
+        if (P.sbr == 2 && nch == 1) {
+            // PS: header every frame, IID mode 1 / ICC mode 1 (20 bands), no extension,
+            // var_borders = 0 with 1 or 2 envelopes (PSImpl.java:103-134, 162-168)
+            F.ps_present = 1;
+            jaad_ps_frame& S = F.ps;
+            S.iid_mode = 1;
+            S.icc_mode = 1;
+            S.ext = 0;
+            const int ne = 1 + (int)r.below(2);
+            S.num_env = (uint8_t)ne;
+            for (int e = 0; e <= ne; e++) S.border[e] = (uint8_t)(e * 32 / ne);
+            for (int e = 0; e < ne; e++)
+                for (int b = 0; b < 20; b++) {
+                    iid[b] += (int)r.below(3) - 1;
+                    iid[b] = iid[b] < -7 ? -7 : (iid[b] > 7 ? 7 : iid[b]);
+                    icc[b] += (int)r.below(3) - 1;
+                    icc[b] = icc[b] < 0 ? 0 : (icc[b] > 7 ? 7 : icc[b]);
+                    S.iid[e][b] = (int8_t)iid[b];
+                    S.icc[e][b] = (int8_t)icc[b];
+                }
+        }
     }
 }
 
@@ -267,6 +292,14 @@ void jaad_synth_default(int config_id, jaad_synth_params* p)
         p->channel_config = 2;
         p->ms_mode = 1;
         p->sbr = 1;
+        p->sbr_level = 18;
+        break;
+    case 5:  // C5: HE-AAC v2 mono core -> SBR -> PS stereo, 262 144 frames = 2048 streams x 128
+        p->n_streams = 2048;
+        p->frames_per_stream = 128;
+        p->sf_index = 6;
+        p->channel_config = 1;
+        p->sbr = 2;
         p->sbr_level = 18;
         break;
     case 1:  // C1: AAC-LC 44.1 kHz mono, one frame

@@ -44,9 +44,12 @@ SBR_CHANNEL_DTYPE = np.dtype([
     ("add_harmonic", "<u8"), ("E", "<i2", (5, 64)), ("Q", "<i2", (2, 8)), ("frame_class", "u1"), ("L_E", "u1"),
     ("L_Q", "u1"), ("bs_pointer", "u1"), ("t_E", "u1", (6,)), ("t_Q", "u1", (3,)), ("f", "u1", (6,)),
     ("invf_mode", "u1", (5,)), ("add_harmonic_flag", "u1"), ("reserved", "u1", (7,))])
-SBR_FRAME_DTYPE = np.dtype([("header_present", "u1"), ("coupling", "u1"), ("reserved", "u1", (2,)),
-                            ("hdr", SBR_HEADER_DTYPE), ("ch", SBR_CHANNEL_DTYPE, (2,))])
-assert SBR_CHANNEL_DTYPE.itemsize == 712 and SBR_FRAME_DTYPE.itemsize == 1440
+PS_FRAME_DTYPE = np.dtype([("iid_mode", "u1"), ("icc_mode", "u1"), ("num_env", "u1"), ("ext", "u1"),
+                           ("border", "u1", (6,)), ("reserved", "u1", (2,)), ("iid", "i1", (5, 34)),
+                           ("icc", "i1", (5, 34))])
+SBR_FRAME_DTYPE = np.dtype([("header_present", "u1"), ("coupling", "u1"), ("ps_present", "u1"), ("reserved", "u1"),
+                            ("hdr", SBR_HEADER_DTYPE), ("ch", SBR_CHANNEL_DTYPE, (2,)), ("ps", PS_FRAME_DTYPE)])
+assert SBR_CHANNEL_DTYPE.itemsize == 712 and PS_FRAME_DTYPE.itemsize == 352 and SBR_FRAME_DTYPE.itemsize == 1792
 
 
 class StreamCfg(C.Structure):
@@ -248,13 +251,16 @@ def synth_batch(p: SynthParams, with_tns: bool | None = None, threads: int = 0) 
     return Batch(q, sf, cb, ics, ms, tns, slot, begin, nch, sbr)
 
 
-def make_cfg(sf_index: int = 3, channel_config: int = 2, tns_mode: int = TNS_COMPAT, sbr: bool = False) -> StreamCfg:
+def make_cfg(sf_index: int = 3, channel_config: int = 2, tns_mode: int = TNS_COMPAT, sbr: bool = False,
+             ps: bool = False) -> StreamCfg:
     """jaad_stream_cfg; with sbr the output rate is twice the core rate (index - 3)."""
-    return StreamCfg(ABI_VERSION, 2, sf_index, channel_config, tns_mode, int(sbr), 0, sf_index - 3 if sbr else 0, 0)
+    sbr = sbr or ps
+    return StreamCfg(ABI_VERSION, 2, sf_index, channel_config, tns_mode, int(sbr), int(ps),
+                     sf_index - 3 if sbr else 0, 0)
 
 
 def cfg_for(p: SynthParams, tns_mode: int = TNS_COMPAT) -> StreamCfg:
-    return make_cfg(p.sf_index, p.channel_config, tns_mode, bool(p.sbr))
+    return make_cfg(p.sf_index, p.channel_config, tns_mode, bool(p.sbr), p.sbr == 2)
 
 
 def pcm_frame_bytes(flags: int, sbr: bool = False) -> int:

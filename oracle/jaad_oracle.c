@@ -441,6 +441,7 @@ size_t orc_stream_bytes(void) { return sizeof(orc_stream); }
 void orc_streams_free(orc_stream* streams, int n)
 {
     for (int i = 0; i < n; i++) {
+        orc_sbr_free(streams[i].sbr);
         free(streams[i].sbr);
         streams[i].sbr = NULL;
     }
@@ -503,6 +504,7 @@ static int check_batch(const jaad_stream_cfg* cfg, const jaad_batch* b, size_t p
     if (!cfg || !b || (!b->q && b->n_frames) || !b->sf || !b->cb || !b->ics || !b->frame_begin) return JAAD_ERR_INVALID_ARG;
     if (cfg->channel_config != 1 && cfg->channel_config != 2) return JAAD_ERR_UNSUPPORTED;
     if (cfg->sbr && (!b->sbr || cfg->ext_sf_index + 3 != cfg->sf_index)) return JAAD_ERR_INVALID_ARG;
+    if (cfg->ps && (!cfg->sbr || cfg->channel_config != 1)) return JAAD_ERR_UNSUPPORTED;
     size_t per = (size_t)frame_samples(cfg) * 2 * ((flags & JAAD_PCM_FLOAT32) ? 4 : 2);
     if (pcm_bytes < per * b->n_frames) return JAAD_ERR_INVALID_ARG;
     return JAAD_OK;

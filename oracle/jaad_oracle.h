@@ -23,6 +23,7 @@ extern "C" {
 #endif
 
 typedef struct orc_sbr orc_sbr;
+typedef struct orc_ps orc_ps;
 
 /* per-stream state of the restated decoder: ICStream.overlap per channel (A/syntax/ICStream.java:47)
  * and the SBR object of the channel element (allocated on first use, freed by orc_streams_free) */
@@ -79,6 +80,14 @@ void orc_sbr_dct4(const float* in_re, const float* in_im, float* out_re, float* 
 void orc_qmf_analysis_frame(float* v1280, int* v_index, const float* input1024, float* X, int kx);
 /* SynthesisFilterbank64.synthesis over one frame: X[32][64][2] -> 2048 samples */
 void orc_qmf_synthesis_frame(float* v2560, int* v_index, const float* X, float* output2048);
+void orc_sbr_free(orc_sbr* s);
+/* ---- PS (jaad_oracle_ps.c) ---- */
+size_t orc_ps_bytes(void);
+void orc_ps_init(orc_ps* ps);
+void orc_ps_set_frame(orc_ps* ps, const jaad_ps_frame* f);
+/* PSImpl.process on X_left/X_right [38][64][2] (A/ps/PSImpl.java:685-707) */
+void orc_ps_process(orc_ps* ps, float (*X_left)[64][2], float (*X_right)[64][2]);
+void orc_ps_hybrid_analysis(const float* X, float* X_hybrid);
 /* derived frequency tables for a header: info = k0 k2 kx M N_master N_high N_low N_Q noPatches N_L */
 int orc_sbr_table_info(const jaad_sbr_header* h, int out_sf_index, int* info, int* f_master, int* f_table_lim);
 

@@ -62,6 +62,11 @@ struct orc_sbr {
     int have_saved;
     int coupling;
     orc_sbr_channel ch[2];
+    /* SBR1 parametric stereo (A/sbr/SBR1.java:23,62-73,102-134) */
+    int ps_used;
+    orc_ps* ps;
+    float qmfs1_v[2560];
+    int qmfs1_index;
 };
 
 size_t orc_sbr_bytes(void) { return sizeof(orc_sbr); }
@@ -1111,6 +1116,20 @@ int orc_sbr_decode(orc_sbr* s, const jaad_sbr_frame* fr, int nch)
     } else {
         s->reset = 0;
     }
+    s->ps_used = 0;
+    if (nch == 1 && fr->ps_present) { /* sbr_extension: PS opened on first use with a fresh qmfs1 */
+        if (!s->ps) {
+            s->ps = (orc_ps*)calloc(1, orc_ps_bytes());
+            if (!s->ps) return JAAD_ERR_NOMEM;
+            orc_ps_init(s->ps);
+            memset(s->qmfs1_v, 0, sizeof s->qmfs1_v);
+            s->qmfs1_index = 0;
+        }
+        if (fr->ps.num_env < 1 || fr->ps.num_env > 5 || fr->ps.ext || fr->ps.iid_mode > 5 || fr->ps.icc_mode > 5)
+            return JAAD_ERR_BITSTREAM;
+        orc_ps_set_frame(s->ps, &fr->ps);
+        s->ps_used = 1;
+    }
     if (!s->have_hdr) return JAAD_OK;
     s->coupling = nch == 2 ? fr->coupling : 0;
     for (int c = 0; c < nch; c++) {
@@ -1129,8 +1148,38 @@ int orc_sbr_decode(orc_sbr* s, const jaad_sbr_frame* fr, int nch)
 /* SBR2.process (A/sbr/SBR2.java:137-157) / SBR1.process without PS (A/sbr/SBR1.java:75-100).
  * left/right: 2048 floats each, first 1024 = core output; right is ignored when nch == 1
  * (it receives a copy of left, A/sbr/SBR1.java:79-80). */
+void orc_sbr_free(orc_sbr* s)
+{
+    if (s) free(s->ps);
+}
+
+/* SBR1.processPS (A/sbr/SBR1.java:102-134) */
+static void process_ps(orc_sbr* s, float* left, float* right)
+{
+    static const int extra = 6;
+    float Xl[MAX_NTSR + 6][64][2], Xr[MAX_NTSR + 6][64][2];
+    memset(Xl, 0, sizeof Xl);
+    memset(Xr, 0, sizeof Xr);
+    process_channel(s, &s->ch[0], left, Xl, s->reset);
+    for (int l = 32; l < 32 + extra; l++)
+        for (int k = 0; k < 5; k++) {
+            Xl[l][k][0] = s->ch[0].Xsbr[T_HFADJ + l][k][0];
+            Xl[l][k][1] = s->ch[0].Xsbr[T_HFADJ + l][k][1];
+        }
+    orc_ps_process(s->ps, Xl, Xr);
+    qmf_synthesis(s->ch[0].qmfs_v, &s->ch[0].qmfs_index, Xl, left);
+    qmf_synthesis(s->qmfs1_v, &s->qmfs1_index, Xr, right);
+    if (s->have_hdr) sbr_save_prev_data(s, &s->ch[0]);
+    sbr_save_matrix(&s->ch[0]);
+    s->frame++;
+}
+
 void orc_sbr_process(orc_sbr* s, float* left, float* right, int nch)
 {
+    if (nch == 1 && s->ps_used) {
+        process_ps(s, left, right);
+        return;
+    }
     float Xl[MAX_NTSR][64][2];
     process_channel(s, &s->ch[0], left, Xl, s->reset);
     qmf_synthesis(s->ch[0].qmfs_v, &s->ch[0].qmfs_index, Xl, left);

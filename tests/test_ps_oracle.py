@@ -1,0 +1,78 @@
+"""Pins the parametric-stereo restatement (oracle/jaad_oracle_ps.c) against closed forms and
+reference properties (A/ps/*.java)."""
+import ctypes as C
+
+import numpy as np
+
+from jaadec_amd import native as N
+from oracle import oracle as O
+
+
+def _tab(name):
+    src = (N.PKG / "csrc" / "tables" / "jaad_ps_tables.inc").read_text()
+    i = src.index(name + "[")
+    body = src[src.index("{", i) + 1: src.index("};", i)]
+    toks = [t.strip().rstrip("f") for t in body.replace("{", "").replace("}", "").split(",") if t.strip()]
+    return np.array([float.fromhex(t) if "x" in t else float(t) for t in toks])
+
+
+def test_hybrid_analysis_matches_modulated_filterbank():
+    """T20 hybrid analysis (A/ps/Filterbank.java:18-68): band 0 is an 8-band complex-modulated
+    13-tap filterbank G_q = sum_k g[k] x[n+k] exp(-j 2 pi/8 (q+1/2)(k-6)) with sub-bands 3+4 and
+    2+5 merged; bands 1, 2 are real 2-band filters cos(pi q (k-6))."""
+    L = O.lib()
+    L.orc_ps_hybrid_analysis.argtypes = [C.c_void_p, C.c_void_p]
+    rng = np.random.default_rng(0)
+    X = rng.standard_normal((38, 64, 2)).astype(np.float32)
+    H = np.zeros((32, 32, 2), np.float32)
+    L.orc_ps_hybrid_analysis(X.ctypes.data, H.ctypes.data)
+    Hc = H[..., 0].astype(np.float64) + 1j * H[..., 1]
+    p8, p2 = _tab("JAAD_PS_P8_13_20"), _tab("JAAD_PS_P2_13_20")
+    g8 = np.concatenate([p8, p8[:6][::-1]])
+    g2 = np.concatenate([p2, p2[:6][::-1]])
+    x = X[..., 0].astype(np.float64) + 1j * X[..., 1]
+    k = np.arange(13)
+
+    def bank(band, g, mod):
+        w = np.concatenate([np.zeros(12), x[6:38, band]])
+        return np.array([[(g * w[n:n + 13] * m).sum() for m in mod] for n in range(32)])
+
+    G8 = bank(0, g8, [np.exp(-1j * 2 * np.pi / 8 * (q + 0.5) * (k - 6)) for q in range(8)])
+    want = np.stack([G8[:, 0], G8[:, 1], G8[:, 2] + G8[:, 5], G8[:, 3] + G8[:, 4], 0 * G8[:, 0], 0 * G8[:, 0],
+                     G8[:, 6], G8[:, 7]], 1)
+    assert np.abs(Hc[:, :8] - want).max() < 1e-5
+    for band, col in ((1, 8), (2, 10)):
+        G2 = bank(band, g2, [np.cos(np.pi * q * (k - 6)) for q in range(2)])
+        assert np.abs(Hc[:, col:col + 2] - G2).max() < 1e-5
+
+
+def test_neutral_parameters_give_identical_channels():
+    """IID = ICC = 0 mixes h11 = h12 = 1, h21 = h22 = 0 (A/ps/PSImpl.java:444-466): once the
+    interpolation from the initial h_prev (:87-92) and the fresh right synthesis ring have been
+    flushed (2 frames), left and right are bit-identical."""
+    p = N.synth_params(5, n_streams=1, frames_per_stream=8)
+    b = N.synth_batch(p)
+    b.sbr["ps"]["iid"][:] = 0
+    b.sbr["ps"]["icc"][:] = 0
+    f = O.decode_batch(N.cfg_for(p), b, O.Streams(1), N.PCM_FLOAT32).view(np.float32).reshape(-1, 2048, 2)
+    assert not np.array_equal(f[0, :, 0], f[0, :, 1])
+    for i in range(2, 8):
+        assert np.array_equal(f[i, :, 0], f[i, :, 1])
+
+
+def test_c5_decorrelates_and_continues_across_calls():
+    p = N.synth_params(5, n_streams=2, frames_per_stream=12)
+    b = N.synth_batch(p)
+    cfg = N.cfg_for(p)
+    assert (cfg.sbr, cfg.ps, cfg.channel_config) == (1, 1, 1)
+    f = O.decode_batch(cfg, b, O.Streams(2), N.PCM_FLOAT32).view(np.float32).reshape(-1, 2048, 2)
+    assert np.isfinite(f).all() and np.abs(f).max() < 32000
+    corr = np.corrcoef(f[..., 0].ravel(), f[..., 1].ravel())[0, 1]
+    assert 0.2 < corr < 0.99  # decorrelated, not independent
+    one = O.decode_batch(cfg, b, O.Streams(2), N.PCM_BIG_ENDIAN)
+    a, c = b.split_frames(5)
+    st = O.Streams(2)
+    got = np.concatenate([O.decode_batch(cfg, a, st, N.PCM_BIG_ENDIAN), O.decode_batch(cfg, c, st, N.PCM_BIG_ENDIAN)])
+    fb = b.frame_begin
+    want = np.concatenate([one[fb[0]:fb[0] + 5], one[fb[1]:fb[1] + 5], one[fb[0] + 5:fb[1]], one[fb[1] + 5:fb[2]]])
+    assert np.array_equal(got, want)

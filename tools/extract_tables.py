@@ -69,6 +69,34 @@ SBR_TABLES = [
     ("sbr/FBT.java", "limiterBandsCompare", "JAAD_SBR_LIMITER_COMPARE", "f32"),
 ]
 
+# PS (HE-AAC v2) tables -> jaad_ps_tables.inc (f32_flat: all numbers of a nested array, in order)
+PS_OUT = OUT.with_name("jaad_ps_tables.inc")
+PS_TABLES = [
+    ("ps/PSTables.java", "filter_a", "JAAD_PS_FILTER_A", "f32"),
+    ("ps/PSTables.java", "group_border20", "JAAD_PS_GROUP_BORDER20", "i32"),
+    ("ps/PSTables.java", "delay_length_d", "JAAD_PS_DELAY_LENGTH_D", "i32"),
+    ("ps/PSTables.java", "Phi_Fract_Qmf", "JAAD_PS_PHI_FRACT_QMF", "f32_2d"),
+    ("ps/PSTables.java", "Phi_Fract_SubQmf20", "JAAD_PS_PHI_FRACT_SUBQMF20", "f32_2d"),
+    ("ps/PSTables.java", "Q_Fract_allpass_Qmf", "JAAD_PS_Q_FRACT_ALLPASS_QMF", "f32_flat"),
+    ("ps/PSTables.java", "Q_Fract_allpass_SubQmf20", "JAAD_PS_Q_FRACT_ALLPASS_SUBQMF20", "f32_flat"),
+    ("ps/PSTables.java", "cos_alphas", "JAAD_PS_COS_ALPHAS", "f32"),
+    ("ps/PSTables.java", "sin_alphas", "JAAD_PS_SIN_ALPHAS", "f32"),
+    ("ps/PSTables.java", "cos_betas_normal", "JAAD_PS_COS_BETAS_NORMAL", "f32_flat"),
+    ("ps/PSTables.java", "sin_betas_normal", "JAAD_PS_SIN_BETAS_NORMAL", "f32_flat"),
+    ("ps/PSTables.java", "cos_betas_fine", "JAAD_PS_COS_BETAS_FINE", "f32_flat"),
+    ("ps/PSTables.java", "sin_betas_fine", "JAAD_PS_SIN_BETAS_FINE", "f32_flat"),
+    ("ps/PSTables.java", "sincos_alphas_B_normal", "JAAD_PS_SINCOS_ALPHAS_B_NORMAL", "f32_flat"),
+    ("ps/PSTables.java", "sincos_alphas_B_fine", "JAAD_PS_SINCOS_ALPHAS_B_FINE", "f32_flat"),
+    ("ps/PSTables.java", "cos_gammas_normal", "JAAD_PS_COS_GAMMAS_NORMAL", "f32_flat"),
+    ("ps/PSTables.java", "cos_gammas_fine", "JAAD_PS_COS_GAMMAS_FINE", "f32_flat"),
+    ("ps/PSTables.java", "sin_gammas_normal", "JAAD_PS_SIN_GAMMAS_NORMAL", "f32_flat"),
+    ("ps/PSTables.java", "sin_gammas_fine", "JAAD_PS_SIN_GAMMAS_FINE", "f32_flat"),
+    ("ps/PSTables.java", "sf_iid_normal", "JAAD_PS_SF_IID_NORMAL", "f32"),
+    ("ps/PSTables.java", "sf_iid_fine", "JAAD_PS_SF_IID_FINE", "f32"),
+    ("ps/Filter8.java", "p8_13_20", "JAAD_PS_P8_13_20", "f32"),
+    ("ps/Filter2.java", "p2_13_20", "JAAD_PS_P2_13_20", "f32"),
+]
+
 SWB = [  # ScaleFactorBands: per sampling-frequency-index offset tables
     ("SWB_OFFSET_1024_96", "SWB_OFFSET_1024_64", "SWB_OFFSET_1024_48", "SWB_OFFSET_1024_32",
      "SWB_OFFSET_1024_24", "SWB_OFFSET_1024_16", "SWB_OFFSET_1024_8"),
@@ -171,6 +199,7 @@ def main() -> int:
     OUT.write_text("\n".join(out) + "\n")
     print("wrote", OUT, sum(1 for _ in out), "lines")
     emit(SBR_TABLES, SBR_OUT)
+    emit(PS_TABLES, PS_OUT)
     return 0
 
 
@@ -183,6 +212,13 @@ def emit(tables, path: Path) -> None:
         rows = parse_rows(find_array(src, jname))
         if kind == "f32":
             vals = [f32_from_decimal(t) for t in rows]
+            out.append(f"static const float {cname}[{len(vals)}] = {{")
+            for i in range(0, len(vals), 6):
+                out.append("  " + ", ".join(hexf(v) for v in vals[i:i + 6]) + ",")
+        elif kind == "f32_flat":
+            body = find_array(src, jname)
+            toks = [t for t in re.split(r"[{},\s]+", body) if t]
+            vals = [f32_from_decimal(t) for t in toks]
             out.append(f"static const float {cname}[{len(vals)}] = {{")
             for i in range(0, len(vals), 6):
                 out.append("  " + ", ".join(hexf(v) for v in vals[i:i + 6]) + ",")
