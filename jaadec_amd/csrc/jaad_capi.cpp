@@ -167,7 +167,8 @@ int validate_cfg(const jaad_stream_cfg* cfg)
     if (cfg->sf_index > 11) return JAAD_ERR_UNSUPPORTED;
     if (cfg->channel_config != 1 && cfg->channel_config != 2) return JAAD_ERR_UNSUPPORTED;
     if (cfg->tns_mode > JAAD_TNS_SPEC) return JAAD_ERR_INVALID_ARG;
-    if (cfg->ps || cfg->sbr > 1) return JAAD_ERR_UNSUPPORTED;
+    if (cfg->sbr > 1 || cfg->ps > 1) return JAAD_ERR_UNSUPPORTED;
+    if (cfg->ps && (!cfg->sbr || cfg->channel_config != 1)) return JAAD_ERR_UNSUPPORTED;
     // explicit SBR at twice the core rate (bs_samplerate_mode = 1, A/sbr/SBR.java:105)
     if (cfg->sbr && (cfg->sf_index < 3 || cfg->ext_sf_index + 3 != cfg->sf_index)) return JAAD_ERR_UNSUPPORTED;
     return JAAD_OK;

@@ -53,16 +53,19 @@ def test_config_queries_mirror_decoderconfig():
     assert L.jaad_frame_pcm_bytes(C.byref(cfg), N.PCM_FLOAT32) == 8192
 
 
-@pytest.mark.parametrize("field,value,status", [
-    ("abi_version", 99, N.ERR_ABI),
-    ("profile", 1, N.ERR_UNSUPPORTED),      # AAC Main: ICPrediction is out of scope
-    ("sf_index", 12, N.ERR_UNSUPPORTED),
-    ("channel_config", 6, N.ERR_UNSUPPORTED),
-    ("sbr", 1, N.ERR_UNSUPPORTED),
+@pytest.mark.parametrize("fields,status", [
+    ({"abi_version": 99}, N.ERR_ABI),
+    ({"profile": 1}, N.ERR_UNSUPPORTED),      # AAC Main: ICPrediction is out of scope
+    ({"sf_index": 12}, N.ERR_UNSUPPORTED),
+    ({"channel_config": 6}, N.ERR_UNSUPPORTED),
+    ({"sbr": 1, "ext_sf_index": 1}, N.ERR_UNSUPPORTED),    # SBR output rate must be 2x the core rate
+    ({"sbr": 1, "sf_index": 1, "ext_sf_index": 0}, N.ERR_UNSUPPORTED),
+    ({"ps": 1, "sbr": 1, "channel_config": 2}, N.ERR_UNSUPPORTED),  # PS needs an SCE core
 ])
-def test_ctx_create_rejects_bad_config(field, value, status):
+def test_ctx_create_rejects_bad_config(fields, status):
     cfg = N.make_cfg()
-    setattr(cfg, field, value)
+    for field, value in fields.items():
+        setattr(cfg, field, value)
     h = C.c_void_p()
     assert N.lib().jaad_ctx_create(C.byref(cfg), 4, 0, C.byref(h)) == status
     assert not h.value
