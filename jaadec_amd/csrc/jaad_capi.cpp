@@ -15,6 +15,7 @@
 #include "jaad_lc.h"
 #include "jaad_sbr.h"
 #include "tables/jaad_sbr_tables.inc"
+#include "tables/jaad_ps_tables.inc"
 #include "tables/jaad_tables.inc"
 
 using namespace jaad;
@@ -80,6 +81,12 @@ struct jaad_ctx {
     std::vector<SbrChunk> sbr_chunks;
     std::vector<uint32_t> sbr_last;
     float* sbr_dbg = nullptr;
+    // ---- PS (cfg.ps) ----
+    PsState* d_ps_state = nullptr;               // [slot]
+    PsConst* d_ps_const = nullptr;
+    DevBuf d_psf, d_xps, d_ps_runs;
+    std::vector<jaad_ps_frame> psf;
+    std::vector<uint32_t> ps_runs;
 };
 
 namespace jaad {
@@ -235,12 +242,59 @@ int carry_untouched(jaad_ctx* ctx, T* out, const T* in, size_t per_slot, hipStre
     return JAAD_OK;
 }
 
+// PS parameters the Java parser can produce (A/ps/PSImpl.java:103-199): borders 0 = b_0 < .. <
+// b_num_env = 32, |IID| <= num_steps, ICC in 0..7; the GPU path needs PS in every frame, no IPD/OPD
+static bool ps_frame_ok(const jaad_sbr_frame& F)
+{
+    const jaad_ps_frame& p = F.ps;
+    if (!F.ps_present || p.ext || p.num_env < 1 || p.num_env > 5 || p.iid_mode > 5 || p.icc_mode > 5) return false;
+    if (p.border[0] != 0 || p.border[p.num_env] != 32) return false;
+    for (int e = 0; e < p.num_env; e++)
+        if (p.border[e + 1] <= p.border[e]) return false;
+    const int steps = p.iid_mode >= 3 ? 15 : 7;
+    for (int e = 0; e < p.num_env; e++)
+        for (int b = 0; b < 20; b++)
+            if (p.iid[e][b] > steps || p.iid[e][b] < -steps || p.icc[e][b] < 0 || p.icc[e][b] > 7) return false;
+    return true;
+}
+
+static void build_ps_const(PsConst* k)
+{
+    std::memset(k, 0, sizeof *k);
+    std::memcpy(k->phi_qmf, JAAD_PS_PHI_FRACT_QMF, sizeof k->phi_qmf);
+    std::memcpy(k->phi_sub, JAAD_PS_PHI_FRACT_SUBQMF20, sizeof k->phi_sub);
+    std::memcpy(k->q_qmf, JAAD_PS_Q_FRACT_ALLPASS_QMF, sizeof k->q_qmf);
+    std::memcpy(k->q_sub, JAAD_PS_Q_FRACT_ALLPASS_SUBQMF20, sizeof k->q_sub);
+    std::memcpy(k->filter_a, JAAD_PS_FILTER_A, sizeof k->filter_a);
+    std::memcpy(k->sf_iid[0], JAAD_PS_SF_IID_NORMAL, sizeof JAAD_PS_SF_IID_NORMAL);
+    std::memcpy(k->sf_iid[1], JAAD_PS_SF_IID_FINE, sizeof JAAD_PS_SF_IID_FINE);
+    std::memcpy(k->cos_alphas, JAAD_PS_COS_ALPHAS, sizeof k->cos_alphas);
+    std::memcpy(k->sin_alphas, JAAD_PS_SIN_ALPHAS, sizeof k->sin_alphas);
+    std::memcpy(k->cos_betas[0], JAAD_PS_COS_BETAS_NORMAL, sizeof JAAD_PS_COS_BETAS_NORMAL);
+    std::memcpy(k->cos_betas[1], JAAD_PS_COS_BETAS_FINE, sizeof JAAD_PS_COS_BETAS_FINE);
+    std::memcpy(k->sin_betas[0], JAAD_PS_SIN_BETAS_NORMAL, sizeof JAAD_PS_SIN_BETAS_NORMAL);
+    std::memcpy(k->sin_betas[1], JAAD_PS_SIN_BETAS_FINE, sizeof JAAD_PS_SIN_BETAS_FINE);
+    // IIDMode hands (sin_gammas, cos_gammas) to IIDTables(cos_gammas, sin_gammas): swapped
+    // (A/ps/IIDMode.java:16-28, A/ps/IIDTables.java:17-21)
+    std::memcpy(k->cos_gammas[0], JAAD_PS_SIN_GAMMAS_NORMAL, sizeof JAAD_PS_SIN_GAMMAS_NORMAL);
+    std::memcpy(k->cos_gammas[1], JAAD_PS_SIN_GAMMAS_FINE, sizeof JAAD_PS_SIN_GAMMAS_FINE);
+    std::memcpy(k->sin_gammas[0], JAAD_PS_COS_GAMMAS_NORMAL, sizeof JAAD_PS_COS_GAMMAS_NORMAL);
+    std::memcpy(k->sin_gammas[1], JAAD_PS_COS_GAMMAS_FINE, sizeof JAAD_PS_COS_GAMMAS_FINE);
+    std::memcpy(k->sincos_b[0], JAAD_PS_SINCOS_ALPHAS_B_NORMAL, sizeof JAAD_PS_SINCOS_ALPHAS_B_NORMAL);
+    std::memcpy(k->sincos_b[1], JAAD_PS_SINCOS_ALPHAS_B_FINE, sizeof JAAD_PS_SINCOS_ALPHAS_B_FINE);
+    std::memcpy(k->p8, JAAD_PS_P8_13_20, sizeof k->p8);
+    std::memcpy(k->p2, JAAD_PS_P2_13_20, sizeof k->p2);
+}
+
 // SBR: host records in stream order, chunk plan, then the SBR kernel over the core time samples
 int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t flags, hipStream_t stream)
 {
     const int nch = ctx->nch;
+    const bool ps = ctx->cfg.ps != 0;
+    const int och = ps ? 2 : nch;  // channels of the QMF synthesis
     const size_t nf = b->n_frames;
     ctx->sbr_recs.resize(nf * nch);
+    if (ps) ctx->psf.resize(nf);
     ctx->sbr_epool.clear();
     ctx->sbr_chunks.clear();
     // parameter records: runs are independent streams, so they are built in parallel (each
@@ -258,6 +312,14 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
             for (uint32_t r = r0; r < r1 && !rcs[t]; r++) {
                 SbrHostSlot& hs = ctx->sbr_slots[b->stream_slot[r]];
                 for (uint32_t f = b->frame_begin[r]; f < b->frame_begin[r + 1]; f++) {
+                    if (ps) {
+                        if (!ps_frame_ok(b->sbr[f])) {
+                            rcs[t] = b->sbr[f].ps_present ? JAAD_ERR_BITSTREAM : JAAD_ERR_UNSUPPORTED;
+                            bad[t] = (int)f;
+                            break;
+                        }
+                        ctx->psf[f] = b->sbr[f].ps;
+                    }
                     int rc = ctx->sbr_host->frame(hs, b->sbr[f], nch, f == b->frame_begin[r], b->stream_slot[r],
                                                   &ctx->sbr_recs[(size_t)f * nch], pools[t]);
                     if (rc) {
@@ -275,7 +337,7 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
         size_t base = 0;
         for (int t = 0; t < nt; t++) {
             if (rcs[t]) {
-                ctx->err = "SBR side info of frame " + std::to_string(bad[t]);
+                ctx->err = (ps ? "SBR/PS side info of frame " : "SBR side info of frame ") + std::to_string(bad[t]);
                 return rcs[t];
             }
             const uint32_t r0 = (uint32_t)((uint64_t)b->n_runs * t / nt), r1 = (uint32_t)((uint64_t)b->n_runs * (t + 1) / nt);
@@ -292,17 +354,21 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
         }
     }
     ctx->sbr_last.clear();
+    ctx->ps_runs.clear();
     bool smoothing = false;
     for (const SbrRec& rr : ctx->sbr_recs) smoothing |= (rr.flags & kSbrSmooth) != 0;
     for (uint32_t r = 0; r < b->n_runs; r++) {
         const uint32_t f0 = b->frame_begin[r], f1 = b->frame_begin[r + 1];
         if (f1 == f0) continue;  // empty run: the slot state stays as it is
-        for (int c = 0; c < nch; c++) {
+        for (int c = 0; c < och; c++)
             for (uint32_t f = f0; f < f1; f += kSbrSynFrames) {
                 const uint32_t n = f1 - f < (uint32_t)kSbrSynFrames ? f1 - f : (uint32_t)kSbrSynFrames;
                 ctx->sbr_chunks.push_back(SbrChunk{f, (uint16_t)n, (uint8_t)c, 0});
             }
-            ctx->sbr_last.push_back((f1 - 1) * nch + c);
+        for (int c = 0; c < nch; c++) ctx->sbr_last.push_back((f1 - 1) * nch + c);
+        if (ps) {
+            ctx->ps_runs.push_back(f0);
+            ctx->ps_runs.push_back(f1 - f0);
         }
     }
     if (ctx->sbr_epool.empty()) ctx->sbr_epool.push_back(0.0f);
@@ -329,6 +395,16 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
     if (!ctx->sbr_last.empty())
         HIPCHK(hipMemcpyAsync(ctx->d_sbr_last.p, ctx->sbr_last.data(), ctx->sbr_last.size() * sizeof(uint32_t),
                               hipMemcpyHostToDevice, stream));
+    if (ps) {
+        HIPCHK(ctx->d_psf.ensure(nf * sizeof(jaad_ps_frame) + 256));
+        HIPCHK(ctx->d_xps.ensure(nf * 8192 * sizeof(float) + 256));
+        HIPCHK(ctx->d_ps_runs.ensure(ctx->ps_runs.size() * sizeof(uint32_t) + 256));
+        if (nf)
+            HIPCHK(hipMemcpyAsync(ctx->d_psf.p, ctx->psf.data(), nf * sizeof(jaad_ps_frame), hipMemcpyHostToDevice, stream));
+        if (!ctx->ps_runs.empty())
+            HIPCHK(hipMemcpyAsync(ctx->d_ps_runs.p, ctx->ps_runs.data(), ctx->ps_runs.size() * sizeof(uint32_t),
+                                  hipMemcpyHostToDevice, stream));
+    }
     SbrArgs a{};
     a.time = static_cast<const float*>(ctx->d_time.p);
     a.recs = static_cast<const SbrRec*>(ctx->d_sbr_recs.p);
@@ -352,6 +428,15 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
     a.out_mode = flags;
     a.smoothing = smoothing ? 1 : 0;
     a.dbg = ctx->sbr_dbg;
+    if (ps) {
+        a.ps = 1;
+        a.psf = static_cast<const jaad_ps_frame*>(ctx->d_psf.p);
+        a.psc = ctx->d_ps_const;
+        a.pss = ctx->d_ps_state;
+        a.xps = static_cast<float*>(ctx->d_xps.p);
+        a.runs = static_cast<const uint32_t*>(ctx->d_ps_runs.p);
+        a.n_runs = (uint32_t)(ctx->ps_runs.size() / 2);
+    }
     HIPCHK(launch_sbr(a, stream));
     return JAAD_OK;
 }
@@ -519,6 +604,20 @@ int jaad_ctx_create(const jaad_stream_cfg* cfg, uint32_t n_slots, int device, ja
         if ((e = hipMemcpy(ctx->d_sbr_const, k.data(), k.size() * sizeof(float), hipMemcpyHostToDevice)) != hipSuccess)
             return bail(e, "hipMemcpy sbr const");
     }
+    if (cfg->ps) {
+        const size_t pb = (size_t)n_slots * sizeof(PsState);
+        if ((e = hipMalloc(&ctx->d_ps_state, pb)) != hipSuccess) return bail(e, "hipMalloc ps state");
+        if ((e = hipMemset(ctx->d_ps_state, 0, pb)) != hipSuccess) return bail(e, "hipMemset ps state");
+        std::unique_ptr<PsConst> k(new (std::nothrow) PsConst);
+        if (!k) {
+            jaad_ctx_destroy(ctx);
+            return JAAD_ERR_NOMEM;
+        }
+        build_ps_const(k.get());
+        if ((e = hipMalloc(&ctx->d_ps_const, sizeof(PsConst))) != hipSuccess) return bail(e, "hipMalloc ps const");
+        if ((e = hipMemcpy(ctx->d_ps_const, k.get(), sizeof(PsConst), hipMemcpyHostToDevice)) != hipSuccess)
+            return bail(e, "hipMemcpy ps const");
+    }
     *out = ctx;
     return JAAD_OK;
 }
@@ -535,8 +634,11 @@ void jaad_ctx_destroy(jaad_ctx* ctx)
     if (ctx->d_iq) (void)hipFree(ctx->d_iq);
     if (ctx->d_sbr_state) (void)hipFree(ctx->d_sbr_state);
     if (ctx->d_sbr_const) (void)hipFree(ctx->d_sbr_const);
+    if (ctx->d_ps_state) (void)hipFree(ctx->d_ps_state);
+    if (ctx->d_ps_const) (void)hipFree(ctx->d_ps_const);
     for (DevBuf* d : {&ctx->d_time, &ctx->d_sbr_recs, &ctx->d_sbr_epool, &ctx->d_sbr_tabs, &ctx->d_sbr_chunks,
-                      &ctx->d_sbr_last, &ctx->d_xlow, &ctx->d_xsyn, &ctx->d_xcarry, &ctx->d_gq})
+                      &ctx->d_sbr_last, &ctx->d_xlow, &ctx->d_xsyn, &ctx->d_xcarry, &ctx->d_gq, &ctx->d_psf, &ctx->d_xps,
+                      &ctx->d_ps_runs})
         d->release();
     ctx->d_chunks.release();
     ctx->d_batch.release();
@@ -637,10 +739,12 @@ int jaad_wait(jaad_ctx* ctx)
 }
 
 // per-slot state blob: core overlap [2][1024] f32 | (SBR) device SbrChState[2] | host SbrHostSlot
+// | (PS) device PsState
 size_t jaad_state_bytes(const jaad_ctx* ctx)
 {
     if (!ctx) return 0;
-    return 2048 * sizeof(float) + (ctx->cfg.sbr ? 2 * sizeof(SbrChState) + sizeof(SbrHostSlot) : 0);
+    return 2048 * sizeof(float) + (ctx->cfg.sbr ? 2 * sizeof(SbrChState) + sizeof(SbrHostSlot) : 0) +
+           (ctx->cfg.ps ? sizeof(PsState) : 0);
 }
 
 int jaad_state_export(jaad_ctx* ctx, uint32_t slot, void* buf, size_t bytes)
@@ -654,6 +758,9 @@ int jaad_state_export(jaad_ctx* ctx, uint32_t slot, void* buf, size_t bytes)
         o += 2048 * sizeof(float);
         HIPCHK(hipMemcpy(o, ctx->d_sbr_state + (size_t)slot * 2, 2 * sizeof(SbrChState), hipMemcpyDeviceToHost));
         std::memcpy(o + 2 * sizeof(SbrChState), &ctx->sbr_slots[slot], sizeof(SbrHostSlot));
+        if (ctx->cfg.ps)
+            HIPCHK(hipMemcpy(o + 2 * sizeof(SbrChState) + sizeof(SbrHostSlot), ctx->d_ps_state + slot, sizeof(PsState),
+                             hipMemcpyDeviceToHost));
     }
     return JAAD_OK;
 }
@@ -674,6 +781,9 @@ int jaad_state_import(jaad_ctx* ctx, uint32_t slot, const void* buf, size_t byte
             if (hs.table < 0) return JAAD_ERR_INVALID_ARG;
         }
         HIPCHK(hipMemcpy(ctx->d_sbr_state + (size_t)slot * 2, in, 2 * sizeof(SbrChState), hipMemcpyHostToDevice));
+        if (ctx->cfg.ps)
+            HIPCHK(hipMemcpy(ctx->d_ps_state + slot, in + 2 * sizeof(SbrChState) + sizeof(SbrHostSlot), sizeof(PsState),
+                             hipMemcpyHostToDevice));
         ctx->sbr_slots[slot] = hs;
     }
     return JAAD_OK;
@@ -688,6 +798,7 @@ int jaad_state_reset(jaad_ctx* ctx, uint32_t slot)
     if (ctx->cfg.sbr) {
         HIPCHK(hipMemset(ctx->d_sbr_state + (size_t)slot * 2, 0, 2 * sizeof(SbrChState)));
         SbrHost::reset_slot(ctx->sbr_slots[slot]);
+        if (ctx->cfg.ps) HIPCHK(hipMemset(ctx->d_ps_state + slot, 0, sizeof(PsState)));
     }
     return JAAD_OK;
 }

@@ -91,6 +91,30 @@ struct SbrChunk {
     uint8_t pad;
 };
 
+// Parametric stereo (A/ps/): device constants and per-slot state (PSImpl fields)
+struct PsConst {
+    float phi_qmf[64][2], phi_sub[12][2];
+    float q_qmf[64][3][2], q_sub[12][3][2];
+    float filter_a[3];
+    float sf_iid[2][31];                 // [fine][num_steps + idx]
+    float cos_alphas[8], sin_alphas[8];
+    float cos_betas[2][16][8], sin_betas[2][16][8];
+    float cos_gammas[2][16][8], sin_gammas[2][16][8];  // as IIDTables holds them (swapped, see PSImpl)
+    float sincos_b[2][31][8];
+    float p8[7], p2[7];
+};
+
+struct PsState {
+    float dq[28][64];      // QMF bands (lane = sb): allpass sb <= 22: [0..3] 2-slot delay, [4..9] link 0
+                           // (3 slots), [10..17] link 1 (4), [18..27] link 2 (5); sb >= 23: 14-slot delay
+    float dh[28][16];      // hybrid sub-bands of groups 0..9 (allpass only), same layout
+    float hyb[3][12][2];   // Filterbank.buffer[band][0..11]
+    float peak[34], smooth[34], pprev[34];
+    float h_prev[22][4];   // h11, h12, h21, h22 real parts per group
+    int32_t saved_delay, ser[3], dD, init;
+    int32_t pad[2];
+};
+
 struct SbrArgs {
     const float* time;          // [ch-frame][1024] core output (lc kernel, planar f32)
     const SbrRec* recs;         // [ch-frame]
@@ -112,9 +136,19 @@ struct SbrArgs {
     uint32_t out_mode;          // JAAD_PCM_*
     int smoothing;              // some frame of the batch has bs_smoothing_mode == 0
     float* dbg;                 // debug dumps (internal, normally null)
+    // parametric stereo (cfg.ps): the SBR stages run on the mono channel, ps_kernel turns
+    // X_left into (X_left', X_right) in xps, the synthesis runs on xps with 2 output channels
+    int ps;
+    const jaad_ps_frame* psf;   // [frame]
+    const PsConst* psc;
+    PsState* pss;               // [slot]
+    float* xps;                 // [frame][2][32][64][2]
+    const uint32_t* runs;       // PS: [run] = (first frame, frame count) pairs
+    uint32_t n_runs;
 };
 
 hipError_t launch_sbr(const SbrArgs& a, hipStream_t stream);
+hipError_t launch_ps(const SbrArgs& a, hipStream_t stream);  // jaad_ps.hip, called by launch_sbr
 
 // ---------------------------------------------------------------------------------------------
 // host side

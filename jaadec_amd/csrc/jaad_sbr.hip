@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include "jaad_sbr.h"
+#include "jaad_wave.h"
 
 namespace jaad {
 namespace {
@@ -26,25 +27,6 @@ struct HfLds {
     float gl[5][64], ql[5][64], sl[5][64];
     float gq_eo[64], gq_qm[64], gq_sm[64], gq_g[64];  // per-envelope gain inputs
 };
-
-// LDS hand-off between lanes of one wave: in-order LDS queue + no compiler motion across
-__device__ __forceinline__ void wave_sync()
-{
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-}
-
-__device__ __forceinline__ int lane_id() { return (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
-
-template <int kXor>
-__device__ __forceinline__ float swz(float v)
-{
-    return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), 0x1F | (kXor << 10)));
-}
-__device__ __forceinline__ float shfl(float v, int src_lane)
-{
-    return __int_as_float(__builtin_amdgcn_ds_bpermute(src_lane << 2, __float_as_int(v)));
-}
 
 // Math.round + short clamp (S/SampleBuffer.java:190-205)
 __device__ __forceinline__ int java_round16(float s)
@@ -634,7 +616,10 @@ __global__ __launch_bounds__(256) void sbr_synthesis_kernel(SbrArgs A)
     const SbrChunk ck = A.chunks[ci];
     const int u = lane_id();
     const int e = u & 31, half = u >> 5, hb = half << 5;
-    const int c = ck.ch, nch = A.nch;
+    // PS: the SBR stages ran on the mono channel (nch = 1); channel c of the output is X_left' /
+    // X_right from ps_kernel (xps), whose rows need no carry patch
+    const int c = ck.ch, nch = A.nch, ps = A.ps;
+    const int rc = ps ? 0 : c;  // channel of the SBR records
     const DctConst K = load_dct_const(A.dct, e);
     float cw[10];
 #pragma unroll
@@ -681,13 +666,13 @@ __global__ __launch_bounds__(256) void sbr_synthesis_kernel(SbrArgs A)
             const size_t n = n0 + u;
             if (A.out_mode & JAAD_PCM_FLOAT32) {
                 float* o = reinterpret_cast<float*>(A.pcm) + 2 * n;
-                if (nch == 2) o[c] = out;
+                if (nch == 2 || ps) o[c] = out;
                 else o[0] = o[1] = out;
             } else {
                 uint32_t s16 = (uint32_t)(uint16_t)(int16_t)java_round16(out);
                 if (!(A.out_mode & JAAD_PCM_LITTLE_ENDIAN)) s16 = ((s16 & 0xFF) << 8) | (s16 >> 8);
                 uint16_t* o = reinterpret_cast<uint16_t*>(A.pcm) + 2 * n;
-                if (nch == 2) o[c] = (uint16_t)s16;
+                if (nch == 2 || ps) o[c] = (uint16_t)s16;
                 else o[0] = o[1] = (uint16_t)s16;
             }
         }
@@ -697,10 +682,11 @@ __global__ __launch_bounds__(256) void sbr_synthesis_kernel(SbrArgs A)
 
     // v history: slots 23..31 of the frame before the chunk
     {
-        const size_t cf0 = (size_t)ck.frame0 * nch + c;
+        const size_t cf0 = (size_t)ck.frame0 * nch + rc;
         const SbrRec& R0 = A.recs[cf0];
+        const float* prev = ps ? A.xps + ((size_t)(ck.frame0 - 1) * 2 + c) * 4096 : A.xsyn + (cf0 - nch) * 4096;
         const float2* xp = R0.first ? reinterpret_cast<const float2*>(&A.state[(size_t)R0.slot * 2 + c].xsyn[0][0][0])
-                                    : reinterpret_cast<const float2*>(A.xsyn + (cf0 - nch) * 4096) + 23 * 64;
+                                    : reinterpret_cast<const float2*>(prev) + 23 * 64;
         for (int l = 0; l < 9; l++) {
             const float2 v = xp[l * 64 + u];
             slot(v.x, v.y, false, 0);
@@ -708,8 +694,16 @@ __global__ __launch_bounds__(256) void sbr_synthesis_kernel(SbrArgs A)
     }
     for (int j = 0; j < (int)ck.n; j++) {
         const uint32_t f = ck.frame0 + j;
-        const size_t cf = (size_t)f * nch + c;
+        const size_t cf = (size_t)f * nch + rc;
         const SbrRec& R = A.recs[cf];
+        if (ps) {
+            const float2* xq = reinterpret_cast<const float2*>(A.xps + ((size_t)f * 2 + c) * 4096);
+            for (int l = 0; l < 32; l++) {
+                const float2 v = xq[l * 64 + u];
+                slot(v.x, v.y, true, (size_t)f * 2048 + 64 * l);
+            }
+            continue;
+        }
         const float2* xs = reinterpret_cast<const float2*>(A.xsyn + cf * 4096);
         // rows l < t_E[0]: Xsbr rows 2..7 carried from frame f-1 (its rows 34..39), kx_prev/M_prev
         const int t0 = R.t_E[0];
@@ -745,8 +739,16 @@ __global__ __launch_bounds__(256) void sbr_state_kernel(SbrArgs A)
     for (int k = u; k < 288; k += 64) S.tail[k] = t[k];
     const float* xl = A.xlow + (size_t)cf * 2048 + 24 * 64;
     for (int k = u; k < 512; k += 64) (&S.xlow[0][0][0])[k] = xl[k];
-    const float* xs = A.xsyn + (size_t)cf * 4096 + 23 * 128;
-    for (int k = u; k < 9 * 128; k += 64) (&S.xsyn[0][0][0])[k] = xs[k];
+    if (A.ps) {  // synthesis history of both output channels comes from xps
+        for (int oc = 0; oc < 2; oc++) {
+            const float* xs = A.xps + ((size_t)cf * 2 + oc) * 4096 + 23 * 128;
+            SbrChState& T = A.state[(size_t)R.slot * 2 + oc];
+            for (int k = u; k < 9 * 128; k += 64) (&T.xsyn[0][0][0])[k] = xs[k];
+        }
+    } else {
+        const float* xs = A.xsyn + (size_t)cf * 4096 + 23 * 128;
+        for (int k = u; k < 9 * 128; k += 64) (&S.xsyn[0][0][0])[k] = xs[k];
+    }
     const float* xc = A.xcarry + (size_t)cf * 768;
     for (int k = u; k < 768; k += 64) (&S.xcarry[0][0][0])[k] = xc[k];
     const float* g = A.gq + (size_t)cf * 640;
@@ -767,6 +769,10 @@ hipError_t launch_sbr(const SbrArgs& a, hipStream_t stream)
         } else {
             hipLaunchKernelGGL(sbr_hf_kernel<0>, g, blk, 0, stream, a);
         }
+    }
+    if (a.ps) {
+        const hipError_t e = launch_ps(a, stream);
+        if (e != hipSuccess) return e;
     }
     if (a.n_chunks)
         hipLaunchKernelGGL(sbr_synthesis_kernel, dim3((a.n_chunks + kWavesPerBlock - 1) / kWavesPerBlock), blk, 0,

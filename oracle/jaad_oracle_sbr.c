@@ -1103,6 +1103,21 @@ static void load_channel(const orc_sbr* s, orc_sbr_channel* ch, const jaad_sbr_c
         ch->bs_add_harmonic[n] = (in->add_harmonic_flag && n < s->N_high) ? (int)((in->add_harmonic >> n) & 1u) : 0;
 }
 
+/* what PSImpl.ps_data_decode can leave behind (A/ps/PSImpl.java:103-199): 1..5 envelopes with
+ * borders 0 = b_0 < .. < b_num_env = 32, |IID| <= num_steps, ICC 0..7; no IPD/OPD extension */
+static int ps_frame_valid(const jaad_ps_frame* p)
+{
+    if (p->num_env < 1 || p->num_env > 5 || p->ext || p->iid_mode > 5 || p->icc_mode > 5) return 0;
+    if (p->border[0] != 0 || p->border[p->num_env] != 32) return 0;
+    for (int e = 0; e < p->num_env; e++)
+        if (p->border[e + 1] <= p->border[e]) return 0;
+    const int steps = p->iid_mode >= 3 ? 15 : 7;
+    for (int e = 0; e < p->num_env; e++)
+        for (int b = 0; b < 20; b++)
+            if (p->iid[e][b] > steps || p->iid[e][b] < -steps || p->icc[e][b] < 0 || p->icc[e][b] > 7) return 0;
+    return 1;
+}
+
 int orc_sbr_decode(orc_sbr* s, const jaad_sbr_frame* fr, int nch)
 {
     if (fr->header_present) {
@@ -1125,8 +1140,7 @@ int orc_sbr_decode(orc_sbr* s, const jaad_sbr_frame* fr, int nch)
             memset(s->qmfs1_v, 0, sizeof s->qmfs1_v);
             s->qmfs1_index = 0;
         }
-        if (fr->ps.num_env < 1 || fr->ps.num_env > 5 || fr->ps.ext || fr->ps.iid_mode > 5 || fr->ps.icc_mode > 5)
-            return JAAD_ERR_BITSTREAM;
+        if (!ps_frame_valid(&fr->ps)) return JAAD_ERR_BITSTREAM;
         orc_ps_set_frame(s->ps, &fr->ps);
         s->ps_used = 1;
     }

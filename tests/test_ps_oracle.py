@@ -3,6 +3,7 @@ reference properties (A/ps/*.java)."""
 import ctypes as C
 
 import numpy as np
+import pytest
 
 from jaadec_amd import native as N
 from oracle import oracle as O
@@ -76,3 +77,21 @@ def test_c5_decorrelates_and_continues_across_calls():
     fb = b.frame_begin
     want = np.concatenate([one[fb[0]:fb[0] + 5], one[fb[1]:fb[1] + 5], one[fb[0] + 5:fb[1]], one[fb[1] + 5:fb[2]]])
     assert np.array_equal(got, want)
+
+
+def test_oracle_rejects_parameters_the_parser_cannot_produce():
+    """Borders must run 0 = b_0 < .. < b_num_env = 32 and |IID| <= num_steps (the bounds
+    PSImpl.ps_data_decode enforces, A/ps/PSImpl.java:103-199); the IPD/OPD extension is not restated."""
+    p = N.synth_params(5, n_streams=1, frames_per_stream=2)
+    b = N.synth_batch(p)
+    cfg = N.cfg_for(p)
+    O.decode_batch(cfg, b, O.Streams(1), N.PCM_BIG_ENDIAN)
+    for edit in (lambda s: s["ps"]["border"].__setitem__((slice(None), 0), 1),
+                 lambda s: s["ps"].__setitem__("ext", 1),
+                 lambda s: s["ps"]["iid"].__setitem__((slice(None), 0, 0), 8),
+                 lambda s: s["ps"]["icc"].__setitem__((slice(None), 0, 0), -1)):
+        s = b.sbr.copy()
+        edit(s)
+        bad = N.Batch(b.q, b.sf, b.cb, b.ics, b.ms_used, b.tns, b.stream_slot, b.frame_begin, b.nch, s)
+        with pytest.raises(RuntimeError):
+            O.decode_batch(cfg, bad, O.Streams(1), N.PCM_BIG_ENDIAN)
