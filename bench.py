@@ -7,7 +7,7 @@ windows) with inputs already resident in HBM.  Multi-GPU: one process per GPU, e
 its own 65 536-frame shard of independent streams (weak scaling, no collectives on the data
 path; the only collectives are the barrier and the max-over-ranks timing reduction).
 
-    python bench.py [--gpus N --steps K --warmup W] [--config 2|3] [--no-cpu]
+    python bench.py [--gpus N --steps K --warmup W] [--config 2|3|4|5] [--no-cpu]
 """
 from __future__ import annotations
 
@@ -27,14 +27,18 @@ METRIC = "AAC frames/sec (batched) at 1/2/4/8 MI355X; PCM ±1 LSB vs Java ref"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # algorithmic bytes per frame.  C2/C3 long stereo frame = 2 x 4308 + 8 (q, gains,
 # side info, PCM); C4 (core + SBR, stereo) = 2 x (2048 q + 188 gains + 16 side + 1300 SBR params
-# + 4096 PCM) = 15296
-ALGO_BYTES = {2: 8624, 3: 8624, 4: 15296}
+# + 4096 PCM) = 15296; C5 (mono core + SBR + PS -> stereo) = 2048 q + 188 gains + 16 side + 1300 SBR
+# params + 352 PS params + 8192 PCM = 12096
+ALGO_BYTES = {2: 8624, 3: 8624, 4: 15296, 5: 12096}
 
 WORKLOADS = {
     2: "C2: 65536 AAC-LC 48 kHz stereo frames (256 streams x 256), ONLY_LONG windows",
     3: "C3: 65536 AAC-LC 48 kHz stereo frames (256 streams x 256), LONG/START/SHORT/STOP + TNS data (compat)",
     4: "C4: 32768 HE-AAC v1 frames, 24 kHz AAC-LC stereo core + SBR to 48 kHz (128 streams x 256)",
+    5: "C5: HE-AAC v2, 24 kHz mono core + SBR + PS to 48 kHz stereo; 32768 frames per GPU (256 streams x 128), "
+       "the 8-GPU job is the 262144-frame batch",
 }
+SHARD_OVERRIDES = {5: {"n_streams": 256}}  # C5 is quoted for 8 GPUs: each rank decodes 1/8 of it
 
 
 def parse():
@@ -65,7 +69,7 @@ def main():
     torch.cuda.set_device(dev)
 
     # ---- this rank's shard: its own 256 independent streams (seeded by rank)
-    p = N.synth_params(args.config)
+    p = N.synth_params(args.config, **SHARD_OVERRIDES.get(args.config, {}))
     p.seed = p.seed + 0x1000 * rank
     batch = N.synth_batch(p)
     cfg = N.cfg_for(p)

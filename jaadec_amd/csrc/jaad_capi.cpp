@@ -84,7 +84,7 @@ struct jaad_ctx {
     // ---- PS (cfg.ps) ----
     PsState* d_ps_state = nullptr;               // [slot]
     PsConst* d_ps_const = nullptr;
-    DevBuf d_psf, d_xps, d_ps_runs;
+    DevBuf d_psf, d_xps, d_xhl, d_xhr, d_pg, d_ps_runs;
     std::vector<jaad_ps_frame> psf;
     std::vector<uint32_t> ps_runs;
 };
@@ -398,6 +398,9 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
     if (ps) {
         HIPCHK(ctx->d_psf.ensure(nf * sizeof(jaad_ps_frame) + 256));
         HIPCHK(ctx->d_xps.ensure(nf * 8192 * sizeof(float) + 256));
+        HIPCHK(ctx->d_xhl.ensure(nf * 768 * sizeof(float) + 256));
+        HIPCHK(ctx->d_xhr.ensure(nf * 768 * sizeof(float) + 256));
+        HIPCHK(ctx->d_pg.ensure(nf * 640 * sizeof(float) + 256));
         HIPCHK(ctx->d_ps_runs.ensure(ctx->ps_runs.size() * sizeof(uint32_t) + 256));
         if (nf)
             HIPCHK(hipMemcpyAsync(ctx->d_psf.p, ctx->psf.data(), nf * sizeof(jaad_ps_frame), hipMemcpyHostToDevice, stream));
@@ -434,6 +437,9 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
         a.psc = ctx->d_ps_const;
         a.pss = ctx->d_ps_state;
         a.xps = static_cast<float*>(ctx->d_xps.p);
+        a.xhl = static_cast<float*>(ctx->d_xhl.p);
+        a.xhr = static_cast<float*>(ctx->d_xhr.p);
+        a.pg = static_cast<float*>(ctx->d_pg.p);
         a.runs = static_cast<const uint32_t*>(ctx->d_ps_runs.p);
         a.n_runs = (uint32_t)(ctx->ps_runs.size() / 2);
     }
@@ -638,7 +644,7 @@ void jaad_ctx_destroy(jaad_ctx* ctx)
     if (ctx->d_ps_const) (void)hipFree(ctx->d_ps_const);
     for (DevBuf* d : {&ctx->d_time, &ctx->d_sbr_recs, &ctx->d_sbr_epool, &ctx->d_sbr_tabs, &ctx->d_sbr_chunks,
                       &ctx->d_sbr_last, &ctx->d_xlow, &ctx->d_xsyn, &ctx->d_xcarry, &ctx->d_gq, &ctx->d_psf, &ctx->d_xps,
-                      &ctx->d_ps_runs})
+                      &ctx->d_xhl, &ctx->d_xhr, &ctx->d_pg, &ctx->d_ps_runs})
         d->release();
     ctx->d_chunks.release();
     ctx->d_batch.release();

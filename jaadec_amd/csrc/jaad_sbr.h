@@ -104,15 +104,18 @@ struct PsConst {
     float p8[7], p2[7];
 };
 
+// Rings are stored rotated so that index 0 is the next read position (the kernels run exactly
+// 32 slots per frame, so every ring index inside a frame is a compile-time constant).
 struct PsState {
-    float dq[28][64];      // QMF bands (lane = sb): allpass sb <= 22: [0..3] 2-slot delay, [4..9] link 0
-                           // (3 slots), [10..17] link 1 (4), [18..27] link 2 (5); sb >= 23: 14-slot delay
-    float dh[28][16];      // hybrid sub-bands of groups 0..9 (allpass only), same layout
+    float2 ap[14][64];     // QMF bands <= 22 (lane = sb): [0..1] 2-slot delay, [2..4] link 0, [5..8] link 1,
+                           // [9..13] link 2 (PSImpl delay_Qmf / delay_Qmf_ser)
+    float2 dl[14][64];     // QMF bands 23..34: 14-slot delay; bands >= 35: dl[0] is the 1-slot delay
+    float2 aph[14][16];    // hybrid groups 0..9 (delay_SubQmf / delay_SubQmf_ser), same layout as ap
     float hyb[3][12][2];   // Filterbank.buffer[band][0..11]
-    float peak[34], smooth[34], pprev[34];
+    float peak[20], smooth[20], pprev[20];
     float h_prev[22][4];   // h11, h12, h21, h22 real parts per group
-    int32_t saved_delay, ser[3], dD, init;
-    int32_t pad[2];
+    int32_t init;
+    int32_t pad[3];
 };
 
 struct SbrArgs {
@@ -136,14 +139,17 @@ struct SbrArgs {
     uint32_t out_mode;          // JAAD_PCM_*
     int smoothing;              // some frame of the batch has bs_smoothing_mode == 0
     float* dbg;                 // debug dumps (internal, normally null)
-    // parametric stereo (cfg.ps): the SBR stages run on the mono channel, ps_kernel turns
+    // parametric stereo (cfg.ps): the SBR stages run on the mono channel; the PS kernels turn
     // X_left into (X_left', X_right) in xps, the synthesis runs on xps with 2 output channels
     int ps;
     const jaad_ps_frame* psf;   // [frame]
     const PsConst* psc;
     PsState* pss;               // [slot]
-    float* xps;                 // [frame][2][32][64][2]
-    const uint32_t* runs;       // PS: [run] = (first frame, frame count) pairs
+    float* xps;                 // [frame][2][32][64][2]: X_left / raw all-pass output, then mixed
+    float* xhl;                 // [frame][32][12][2] hybrid X_left
+    float* xhr;                 // [frame][32][12][2] hybrid all-pass output
+    float* pg;                  // [frame][32][20] P, then G_TransientRatio
+    const uint32_t* runs;       // [run] = (first frame, frame count)
     uint32_t n_runs;
 };
 
