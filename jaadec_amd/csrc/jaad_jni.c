@@ -27,10 +27,12 @@ static void* addr(JNIEnv* env, jobject bb, jlong need) {
     return (*env)->GetDirectBufferAddress(env, bb);
 }
 
-/* static native long nativeCreate(int sfIndex, int channelConfig, int tnsMode, int nSlots, int device) */
+/* static native long nativeCreate(int sfIndex, int channelConfig, int tnsMode, int sbr, int ps,
+ *     int nSlots, int device); sfIndex is the core (AAC) rate, the SBR rate is twice it */
 JNIEXPORT jlong JNICALL Java_net_sourceforge_jaad_aac_gpu_GpuDSP_nativeCreate(JNIEnv* env, jclass cls, jint sf_index,
                                                                             jint channel_config, jint tns_mode,
-                                                                            jint n_slots, jint device) {
+                                                                            jint sbr, jint ps, jint n_slots,
+                                                                            jint device) {
     (void)cls;
     jaad_stream_cfg cfg;
     memset(&cfg, 0, sizeof cfg);
@@ -39,6 +41,9 @@ JNIEXPORT jlong JNICALL Java_net_sourceforge_jaad_aac_gpu_GpuDSP_nativeCreate(JN
     cfg.sf_index = (uint8_t)sf_index;
     cfg.channel_config = (uint8_t)channel_config;
     cfg.tns_mode = (uint8_t)tns_mode;
+    cfg.sbr = (uint8_t)(sbr || ps);
+    cfg.ps = (uint8_t)ps;
+    cfg.ext_sf_index = (uint8_t)(cfg.sbr ? sf_index - 3 : 0);
     jaad_ctx* ctx = NULL;
     int rc = jaad_ctx_create(&cfg, (uint32_t)n_slots, device, &ctx);
     if (rc) {
@@ -56,10 +61,11 @@ JNIEXPORT void JNICALL Java_net_sourceforge_jaad_aac_gpu_GpuDSP_nativeDestroy(JN
 
 /* static native void nativeDecode(long h, int nFrames, int nRuns, int nch, ByteBuffer streamSlot,
  *     ByteBuffer frameBegin, ByteBuffer q, ByteBuffer sf, ByteBuffer cb, ByteBuffer ics,
- *     ByteBuffer msUsed, ByteBuffer tns, ByteBuffer pcm, int flags) */
+ *     ByteBuffer msUsed, ByteBuffer tns, ByteBuffer sbr, ByteBuffer pcm, int flags);
+ * sbr: one jaad_sbr_frame (1792 B) per frame for SBR/PS streams, else null */
 JNIEXPORT void JNICALL Java_net_sourceforge_jaad_aac_gpu_GpuDSP_nativeDecode(
     JNIEnv* env, jclass cls, jlong h, jint n_frames, jint n_runs, jint nch, jobject stream_slot, jobject frame_begin,
-    jobject q, jobject sf, jobject cb, jobject ics, jobject ms_used, jobject tns, jobject pcm, jint flags) {
+    jobject q, jobject sf, jobject cb, jobject ics, jobject ms_used, jobject tns, jobject sbr, jobject pcm, jint flags) {
     (void)cls;
     jaad_ctx* ctx = (jaad_ctx*)(intptr_t)h;
     const jlong ncf = (jlong)n_frames * nch;
@@ -75,10 +81,11 @@ JNIEXPORT void JNICALL Java_net_sourceforge_jaad_aac_gpu_GpuDSP_nativeDecode(
     b.ics = (const jaad_ics_info*)addr(env, ics, (jlong)sizeof(jaad_ics_info) * ncf);
     b.ms_used = (const uint64_t*)addr(env, ms_used, 16LL * n_frames);
     b.tns = (const jaad_tns*)addr(env, tns, (jlong)sizeof(jaad_tns) * ncf);
+    b.sbr = (const jaad_sbr_frame*)addr(env, sbr, (jlong)sizeof(jaad_sbr_frame) * n_frames);
     jlong pcm_cap = pcm ? (*env)->GetDirectBufferCapacity(env, pcm) : -1;
     void* out = pcm ? (*env)->GetDirectBufferAddress(env, pcm) : NULL;
     if (!ctx || !b.stream_slot || !b.frame_begin || !b.q || !b.sf || !b.cb || !b.ics || !out || pcm_cap < 0 ||
-        (ms_used && !b.ms_used) || (tns && !b.tns)) {
+        (ms_used && !b.ms_used) || (tns && !b.tns) || (sbr && !b.sbr)) {
         throw_aac(env, ctx, JAAD_ERR_INVALID_ARG);
         return;
     }

@@ -24,17 +24,26 @@ CASES = {
     "c3_switching_tns_compat": (3, dict(n_streams=2, frames_per_stream=12), dict(), N.PCM_BIG_ENDIAN),
     "c3_switching_tns_spec_f32": (3, dict(n_streams=2, frames_per_stream=10), dict(tns_mode=N.TNS_SPEC), N.PCM_FLOAT32),
     "pns_is_le": (3, dict(n_streams=2, frames_per_stream=8, pns_percent=10, is_percent=20), dict(), N.PCM_LITTLE_ENDIAN),
+    # HE-AAC: SBR records (jaad_sbr_frame) ride along; cfg from the synthetic parameters
+    "c4_sbr_stereo_f32": (4, dict(n_streams=2, frames_per_stream=6), None, N.PCM_FLOAT32),
+    "c5_sbr_ps_be": (5, dict(n_streams=2, frames_per_stream=6), None, N.PCM_BIG_ENDIAN),
 }
 
 
 def save(name, cfgid, over, cfgkw, flags):
     p = N.synth_params(cfgid, **over)
     b = N.synth_batch(p)
-    cfg = N.make_cfg(**{"sf_index": p.sf_index, "channel_config": p.channel_config, **cfgkw})
+    if cfgkw is None:
+        cfg = N.cfg_for(p)
+    else:
+        cfg = N.make_cfg(**{"sf_index": p.sf_index, "channel_config": p.channel_config, **cfgkw})
     pcm = O.decode_batch(cfg, b, O.Streams(int(b.stream_slot.max()) + 1), flags)
     arrays = dict(q=b.q, sf=b.sf, cb=b.cb, ics=b.ics.view(np.uint8), stream_slot=b.stream_slot,
                   frame_begin=b.frame_begin, pcm=pcm,
-                  meta=np.array([cfg.sf_index, cfg.channel_config, cfg.tns_mode, flags, b.nch], np.int32))
+                  meta=np.array([cfg.sf_index, cfg.channel_config, cfg.tns_mode, flags, b.nch,
+                                 cfg.sbr, cfg.ps, cfg.ext_sf_index], np.int32))
+    if b.sbr is not None:
+        arrays["sbr"] = b.sbr.view(np.uint8)
     if b.ms_used is not None:
         arrays["ms_used"] = b.ms_used
     if b.tns is not None:
@@ -45,14 +54,20 @@ def save(name, cfgid, over, cfgkw, flags):
 
 def load(path):
     z = np.load(path, allow_pickle=False)
-    sf_index, ch, tns_mode, flags, nch = (int(v) for v in z["meta"])
+    meta = [int(v) for v in z["meta"]] + [0, 0, 0]
+    sf_index, ch, tns_mode, flags, nch, sbr, ps, ext_sf = meta[:8]
     b = N.Batch(z["q"], z["sf"], z["cb"], z["ics"].view(N.ICS_DTYPE).reshape(-1),
                 z["ms_used"] if "ms_used" in z else None,
                 z["tns"].view(N.TNS_DTYPE).reshape(-1) if "tns" in z else None,
-                z["stream_slot"], z["frame_begin"], nch)
-    return b, N.make_cfg(sf_index=sf_index, channel_config=ch, tns_mode=tns_mode), flags, z["pcm"]
+                z["stream_slot"], z["frame_begin"], nch,
+                z["sbr"].view(N.SBR_FRAME_DTYPE).reshape(-1) if "sbr" in z else None)
+    cfg = N.make_cfg(sf_index=sf_index, channel_config=ch, tns_mode=tns_mode, sbr=bool(sbr), ps=bool(ps))
+    assert cfg.ext_sf_index == ext_sf
+    return b, cfg, flags, z["pcm"]
 
 
 if __name__ == "__main__":
     for k, v in CASES.items():
+        if len(sys.argv) > 1 and k not in sys.argv[1:]:
+            continue
         save(k, *v)
