@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define JAAD_ABI_VERSION 2u
+#define JAAD_ABI_VERSION 3u
 
 /* ---- status codes (JNI maps every nonzero code to AACException, A/AACException.java) ---- */
 typedef enum jaad_status {
@@ -161,17 +161,23 @@ typedef struct jaad_sbr_channel {  /* Channel fields after sbr_data (A/sbr/Chann
 
 /*
  * Parametric stereo parameters of one frame as PSImpl.ps_data_decode leaves them
- * (A/ps/PSImpl.java:137-199): envelope borders and delta-decoded IID/ICC indices per parameter band.
+ * (A/ps/PSImpl.java:137-199): envelope borders and delta-decoded IID/ICC (and IPD/OPD) indices
+ * per parameter band.
  */
 typedef struct jaad_ps_frame {
     uint8_t iid_mode, icc_mode;    /* IIDMode / ICCMode ids 0..5 (A/ps/IIDMode.java:48-55)           */
     uint8_t num_env;               /* 1..5 after ps_data_decode                                      */
-    uint8_t ext;                   /* IPD/OPD extension present: must be 0 in this ABI revision      */
+    uint8_t nr_ipdopd_par;         /* Extension.nr_par(): 0 without the IPD/OPD extension, else 11
+                                      or 17 (A/ps/Extension.java:81-86, A/ps/ExtData.java:55-60)     */
     uint8_t border[6];             /* border_position[0..num_env]                                     */
     uint8_t reserved[2];
     int8_t iid[5][34];             /* iid_index[env][bk]  (|.| <= 7 normal, <= 15 fine)              */
     int8_t icc[5][34];             /* icc_index[env][bk]  (0..7)                                     */
-} jaad_ps_frame;                   /* 352 bytes */
+    int8_t ipd[5][17];             /* ipd_index[env][bk]  (0..7, PDMode.clip)                        */
+    int8_t opd[5][17];             /* opd_index[env][bk]; carried as parsed, but the reference's
+                                      mixing reads the IPD index for both (A/ps/PSImpl.java:502-503) */
+    uint8_t pad[6];
+} jaad_ps_frame;                   /* 528 bytes */
 
 typedef struct jaad_sbr_frame {
     uint8_t header_present;        /* bs_header_flag: hdr below is this frame's sbr_header           */
@@ -181,7 +187,7 @@ typedef struct jaad_sbr_frame {
     jaad_sbr_header hdr;
     jaad_sbr_channel ch[2];        /* ch[1] unused for an SCE                                        */
     jaad_ps_frame ps;              /* valid when ps_present                                          */
-} jaad_sbr_frame;                  /* 1792 bytes */
+} jaad_sbr_frame;                  /* 1968 bytes */
 
 /*
  * A batch: n_frames frames (raw_data_blocks) of one channel configuration.  Frames are grouped

@@ -49,7 +49,7 @@ def _deps(*globs: str) -> list[Path]:
 def build_gpu(force: bool = False, out: Path | None = None, defines: list[str] | None = None) -> Path:
     """Build the product library (or, with `defines`, an experimental variant at `out`)."""
     out = out or LIB
-    srcs = [CSRC / "jaad_lc.hip", CSRC / "jaad_sbr.hip", CSRC / "jaad_capi.cpp", CSRC / "jaad_sbr_host.cpp"]
+    srcs = [CSRC / "jaad_lc.hip", CSRC / "jaad_sbr.hip", CSRC / "jaad_ps.hip", CSRC / "jaad_capi.cpp", CSRC / "jaad_sbr_host.cpp"]
     deps = srcs + _deps("jaadec_amd/csrc/*.h", "jaadec_amd/csrc/tables/*.inc", "include/*.h")
     if force or defines or _stale(out, deps):
         tmp = out.with_suffix(".so.tmp")

@@ -84,7 +84,7 @@ struct jaad_ctx {
     // ---- PS (cfg.ps) ----
     PsState* d_ps_state = nullptr;               // [slot]
     PsConst* d_ps_const = nullptr;
-    DevBuf d_psf, d_xps, d_xhl, d_xhr, d_pg, d_ps_runs;
+    DevBuf d_psf, d_xps, d_xhl, d_xhr, d_pg, d_hb, d_ps_runs;
     std::vector<jaad_ps_frame> psf;
     std::vector<uint32_t> ps_runs;
 };
@@ -242,12 +242,16 @@ int carry_untouched(jaad_ctx* ctx, T* out, const T* in, size_t per_slot, hipStre
     return JAAD_OK;
 }
 
+static_assert(sizeof(jaad_ps_frame) == 528 && sizeof(jaad_sbr_frame) == 1968, "jaad_gpu.h record sizes");
+
 // PS parameters the Java parser can produce (A/ps/PSImpl.java:103-199): borders 0 = b_0 < .. <
-// b_num_env = 32, |IID| <= num_steps, ICC in 0..7; the GPU path needs PS in every frame, no IPD/OPD
+// b_num_env = 32, |IID| <= num_steps, ICC and IPD/OPD in 0..7, nr_ipdopd_par 0 / 11 / 17; the GPU
+// path needs PS data in every frame of a PS stream
 static bool ps_frame_ok(const jaad_sbr_frame& F)
 {
     const jaad_ps_frame& p = F.ps;
-    if (!F.ps_present || p.ext || p.num_env < 1 || p.num_env > 5 || p.iid_mode > 5 || p.icc_mode > 5) return false;
+    if (!F.ps_present || p.num_env < 1 || p.num_env > 5 || p.iid_mode > 5 || p.icc_mode > 5) return false;
+    if (p.nr_ipdopd_par != 0 && p.nr_ipdopd_par != 11 && p.nr_ipdopd_par != 17) return false;
     if (p.border[0] != 0 || p.border[p.num_env] != 32) return false;
     for (int e = 0; e < p.num_env; e++)
         if (p.border[e + 1] <= p.border[e]) return false;
@@ -255,6 +259,9 @@ static bool ps_frame_ok(const jaad_sbr_frame& F)
     for (int e = 0; e < p.num_env; e++)
         for (int b = 0; b < 20; b++)
             if (p.iid[e][b] > steps || p.iid[e][b] < -steps || p.icc[e][b] < 0 || p.icc[e][b] > 7) return false;
+    for (int e = 0; e < p.num_env; e++)
+        for (int b = 0; b < p.nr_ipdopd_par; b++)
+            if (p.ipd[e][b] < 0 || p.ipd[e][b] > 7 || p.opd[e][b] < 0 || p.opd[e][b] > 7) return false;
     return true;
 }
 
@@ -284,6 +291,8 @@ static void build_ps_const(PsConst* k)
     std::memcpy(k->sincos_b[1], JAAD_PS_SINCOS_ALPHAS_B_FINE, sizeof JAAD_PS_SINCOS_ALPHAS_B_FINE);
     std::memcpy(k->p8, JAAD_PS_P8_13_20, sizeof k->p8);
     std::memcpy(k->p2, JAAD_PS_P2_13_20, sizeof k->p2);
+    std::memcpy(k->ipdopd_cos, JAAD_PS_IPDOPD_COS, sizeof k->ipdopd_cos);
+    std::memcpy(k->ipdopd_sin, JAAD_PS_IPDOPD_SIN, sizeof k->ipdopd_sin);
 }
 
 // SBR: host records in stream order, chunk plan, then the SBR kernel over the core time samples
@@ -401,6 +410,7 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
         HIPCHK(ctx->d_xhl.ensure(nf * 768 * sizeof(float) + 256));
         HIPCHK(ctx->d_xhr.ensure(nf * 768 * sizeof(float) + 256));
         HIPCHK(ctx->d_pg.ensure(nf * 640 * sizeof(float) + 256));
+        HIPCHK(ctx->d_hb.ensure(nf * 5 * 22 * 16 * sizeof(float) + 256));
         HIPCHK(ctx->d_ps_runs.ensure(ctx->ps_runs.size() * sizeof(uint32_t) + 256));
         if (nf)
             HIPCHK(hipMemcpyAsync(ctx->d_psf.p, ctx->psf.data(), nf * sizeof(jaad_ps_frame), hipMemcpyHostToDevice, stream));
@@ -440,6 +450,7 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
         a.xhl = static_cast<float*>(ctx->d_xhl.p);
         a.xhr = static_cast<float*>(ctx->d_xhr.p);
         a.pg = static_cast<float*>(ctx->d_pg.p);
+        a.hb = static_cast<float*>(ctx->d_hb.p);
         a.runs = static_cast<const uint32_t*>(ctx->d_ps_runs.p);
         a.n_runs = (uint32_t)(ctx->ps_runs.size() / 2);
     }
@@ -644,7 +655,7 @@ void jaad_ctx_destroy(jaad_ctx* ctx)
     if (ctx->d_ps_const) (void)hipFree(ctx->d_ps_const);
     for (DevBuf* d : {&ctx->d_time, &ctx->d_sbr_recs, &ctx->d_sbr_epool, &ctx->d_sbr_tabs, &ctx->d_sbr_chunks,
                       &ctx->d_sbr_last, &ctx->d_xlow, &ctx->d_xsyn, &ctx->d_xcarry, &ctx->d_gq, &ctx->d_psf, &ctx->d_xps,
-                      &ctx->d_xhl, &ctx->d_xhr, &ctx->d_pg, &ctx->d_ps_runs})
+                      &ctx->d_xhl, &ctx->d_xhr, &ctx->d_pg, &ctx->d_hb, &ctx->d_ps_runs})
         d->release();
     ctx->d_chunks.release();
     ctx->d_batch.release();

@@ -1,7 +1,8 @@
 // Parametric stereo (HE-AAC v2) for gfx950, A/ = aac/src/main/java/net/sourceforge/jaad/aac/ of the
 // reference: PSImpl.process (A/ps/PSImpl.java:685-707) = hybrid analysis (A/ps/Filterbank.java:
-// 18-68, T20), decorrelation (:202-400), mixing without IPD/OPD (:406-681), hybrid synthesis
+// 18-68, T20), decorrelation (:202-400), mixing (:406-681), hybrid synthesis
 // (A/ps/Filterbank.java:70-86).  Same binary32 evaluation order as the Java (-ffp-contract=off).
+// IPD/OPD phase rotation included (nr_ipdopd_par 11 / 17), with the reference's index quirks.
 //
 // Only two parts of PS are recurrences across frames: the all-pass / delay lines of the
 // decorrelator and the transient detector's peak/smooth IIRs.  Everything else reaches back at
@@ -9,13 +10,14 @@
 // HBM:
 //   ps_analysis_kernel  X_left (SBR output, carry-patched) -> xps[f][0]; hybrid analysis -> xhl;
 //                       band energies P -> pg                                  (wave per frame)
-//   ps_decor_kernel     per run, three waves: QMF bands (lane = band) / hybrid groups / transient
-//                       detector, sequential over the run's frames; rings in VGPRs with
-//                       compile-time indices (32 slots per frame), raw all-pass output -> xps[f][1],
-//                       xhr; G_TransientRatio -> pg                           (block per run)
-//   ps_mix_kernel       H interpolation (h_prev rebuilt from frame f-1's parameters), G scaling,
-//                       mixing, hybrid synthesis -> xps[f][0..1]              (wave per frame)
-//   ps_state_kernel     filterbank history and h_prev of each run's last frame -> slot state
+//   ps_decor_kernel     per run, four waves: QMF bands (lane = band) / hybrid groups / transient
+//                       detector / mixing-parameter scan (IPD/OPD phase history, h_prev),
+//                       sequential over the run's frames; rings in VGPRs with compile-time
+//                       indices (32 slots per frame), raw all-pass output -> xps[f][1], xhr;
+//                       G_TransientRatio -> pg; H start/delta per (env, group) -> hb (block per run)
+//   ps_mix_kernel       H interpolation, G scaling, mixing (+ IPD/OPD rotation), hybrid
+//                       synthesis -> xps[f][0..1]                              (wave per frame)
+//   ps_state_kernel     filterbank history of each run's last frame -> slot state
 #include <hip/hip_runtime.h>
 
 #include <type_traits>
@@ -27,7 +29,6 @@ namespace jaad {
 namespace {
 
 constexpr int kBorder[23] = {6, 7, 0, 1, 2, 3, 9, 8, 10, 11, 3, 4, 5, 6, 7, 8, 9, 11, 14, 18, 23, 35, 64};
-constexpr int kSubGroup[12] = {2, 3, 4, 5, -1, -1, 0, 1, 7, 6, 8, 9};  // hybrid sub-band -> group
 constexpr float kAlphaDecay = 0.76592833836465f, kAlphaSmooth = 0.25f, kDecaySlope = 0.05f;
 constexpr float kCoefSqrt2 = 1.4142135623731f;
 constexpr int kPsWaves = 4;  // frames per block of the frame-parallel kernels
@@ -216,6 +217,162 @@ __global__ __launch_bounds__(256) void ps_analysis_kernel(SbrArgs A)
 }
 
 // ---------------------------------------------------------------------------------------------
+// mixing parameters (PSImpl.ps_mix_phase :419-590): parameter-only, but the IPD/OPD phase history
+// and h_prev run through every frame, so one wave per run scans them (lane = parameter band)
+// ---------------------------------------------------------------------------------------------
+// target mixing coefficients (real parts) of envelope env, group gr (:433-482)
+__device__ __forceinline__ void ps_h(const PsConst& K, const jaad_ps_frame& P, int env, int gr, float h[4])
+{
+    const int bk = group_bk(gr);
+    const int fine = P.iid_mode >= 3;
+    const int steps = fine ? 15 : 7;
+    int iid = P.iid[env][bk];
+    const int sign = iid < 0 ? -1 : 1;
+    iid = iid < 0 ? -iid : iid;
+    const int icc = P.icc[env][bk];
+    if (P.icc_mode < 3) {  // type 'A'
+        const float c1 = K.sf_iid[fine][steps + iid], c2 = K.sf_iid[fine][steps - iid];
+        const float cosa = K.cos_alphas[icc], sina = K.sin_alphas[icc];
+        const float cosb = K.cos_betas[fine][iid][icc];
+        const float sinb = K.sin_betas[fine][iid][icc] * (float)sign;
+        const float ab1 = (cosb * cosa), ab2 = (sinb * sina), ab3 = (sinb * cosa), ab4 = (cosb * sina);
+        h[0] = (c2 * (ab1 - ab2));
+        h[1] = (c1 * (ab1 + ab2));
+        h[2] = (c2 * (ab3 + ab4));
+        h[3] = (c1 * (ab3 - ab4));
+    } else {  // type 'B'
+        const float cosa = K.sincos_b[fine][steps + iid][icc];
+        const float sina = K.sincos_b[fine][2 * steps - (steps + iid)][icc];
+        const float cosg = K.cos_gammas[fine][iid][icc], sing = K.sin_gammas[fine][iid][icc];
+        h[0] = (kCoefSqrt2 * (cosa * cosg));
+        h[1] = (kCoefSqrt2 * (sina * cosg));
+        h[2] = (kCoefSqrt2 * (-cosa * sing));
+        h[3] = (kCoefSqrt2 * (sina * sing));
+    }
+}
+
+__device__ __forceinline__ float magnitude_c(float re, float im)
+{
+    // (float)Math.sqrt(double) of a float argument == correctly rounded sqrtf (:402-404)
+    return sqrtf((re * re) + (im * im));
+}
+
+// Lane bk walks its groups in group order (bk 0: groups 1, 2; bk 1: groups 0, 3; else bk + 2)
+// over every envelope of every frame of the run.  The shared phase_hist counter flips once per
+// (group, envelope) with bk < nr_ipdopd_par; those groups are always 0 .. nr + 1, so the
+// counter at (gr, env) is phase_hist(frame start) + gr * num_env + env.
+__device__ void ps_param_scan(const SbrArgs& A, uint32_t f0, uint32_t nfr, PsState& S, bool fresh, int u)
+{
+    if (u >= 20) return;
+    const PsConst& K = *A.psc;
+    const int bk = u;
+    const int grs[2] = {bk == 0 ? 1 : (bk == 1 ? 0 : bk + 2), bk == 0 ? 2 : (bk == 1 ? 3 : -1)};
+    float hp[2][8];
+    for (int j = 0; j < 2; j++)
+        for (int k = 0; k < 8; k++) {
+            const int gr = grs[j] < 0 ? 0 : grs[j];
+            // PSImpl constructor (:87-92): h11_prev = (1, 0), h12_prev = (0, 1), h21/h22 = 0
+            hp[j][k] = fresh ? (k == 0 || k == 5 ? 1.0f : 0.0f) : S.h_prev[gr][k];
+        }
+    float ipd[2][2], opd[2][2];
+    for (int ph = 0; ph < 2; ph++)
+        for (int c = 0; c < 2; c++) {
+            ipd[ph][c] = fresh ? 0.0f : S.ipd_prev[bk][ph][c];
+            opd[ph][c] = fresh ? 0.0f : S.opd_prev[bk][ph][c];
+        }
+    int phase = fresh ? 0 : S.phase_hist;
+    for (uint32_t j = 0; j < nfr; j++) {
+        const uint32_t f = f0 + j;
+        const jaad_ps_frame& P = A.psf[f];
+        const int E = P.num_env, nr = P.nr_ipdopd_par;
+        const bool elig = bk < nr;
+        float* hbf = A.hb + (size_t)f * (5 * 22 * 16);
+        for (int g = 0; g < 2; g++) {
+            const int gr = grs[g];
+            if (gr < 0) break;
+            for (int env = 0; env < E; env++) {
+                float h[8];
+                ps_h(K, P, env, gr, h);
+                h[4] = h[5] = h[6] = h[7] = 0.0f;
+                if (elig) {  // phase rotation (:484-567)
+                    const int ph = (phase + gr * E + env) & 1;
+                    float* ip = ipd[ph];
+                    float* op = opd[ph];
+                    float tl0 = (ip[0] * 0.25f), tl1 = (ip[1] * 0.25f);
+                    float tr0 = (op[0] * 0.25f), tr1 = (op[1] * 0.25f);
+                    const int idx = P.ipd[env][bk] < 0 ? -P.ipd[env][bk] : P.ipd[env][bk];  // IPD for both
+                    ip[0] = K.ipdopd_cos[idx];
+                    ip[1] = K.ipdopd_sin[idx];
+                    op[0] = K.ipdopd_cos[idx];
+                    op[1] = K.ipdopd_sin[idx];
+                    tl0 += ip[0];
+                    tl1 += ip[1];
+                    tr0 += op[0];
+                    tr1 += op[1];
+                    const float* pp = opd[ph ^ 1];  // value before previous: opd.prev for both
+                    tl0 += (pp[0] * 0.5f);
+                    tl1 += (pp[1] * 0.5f);
+                    tr0 += (pp[0] * 0.5f);
+                    tr1 += (pp[1] * 0.5f);
+                    const float xy = magnitude_c(tr0, tr1), pq = magnitude_c(tl0, tl1);
+                    float pl0 = 0.0f, pl1 = 0.0f, pr0 = 0.0f, pr1 = 0.0f;
+                    if (xy != 0.0f) {
+                        pl0 = __fdiv_rn(tr0, xy);
+                        pl1 = __fdiv_rn(tr1, xy);
+                    }
+                    const float xypq = (xy * pq);
+                    if (xypq != 0.0f) {
+                        const float tmp1 = (tr0 * tl0) + (tr1 * tl1);
+                        const float tmp2 = (tr1 * tl0) - (tr0 * tl1);
+                        pr0 = __fdiv_rn(tmp1, xypq);
+                        pr1 = __fdiv_rn(tmp2, xypq);
+                    }
+                    h[4] = (h[0] * pl1);
+                    h[5] = (h[1] * pr1);
+                    h[6] = (h[2] * pl1);
+                    h[7] = (h[3] * pr1);
+                    h[0] = (h[0] * pl0);
+                    h[1] = (h[1] * pr0);
+                    h[2] = (h[2] * pl0);
+                    h[3] = (h[3] * pr0);
+                }
+                const float Lf = (float)(P.border[env + 1] - P.border[env]);
+                float* o = hbf + (env * 22 + gr) * 16;
+                for (int k = 0; k < 4; k++) {
+                    o[8 + k] = __fdiv_rn(h[k] - hp[g][k], Lf);
+                    o[k] = hp[g][k];
+                    hp[g][k] = h[k];
+                }
+                for (int k = 4; k < 8; k++) {
+                    float d = 0.0f, st = 0.0f;
+                    if (elig) {
+                        d = __fdiv_rn(h[k] - hp[g][k], Lf);
+                        st = hp[g][k];
+                        if (bk != 0) {  // FBType.bkm tests the band bits (A/ps/FBType.java:71-73)
+                            d = -d;
+                            st = -st;
+                        }
+                        hp[g][k] = h[k];
+                    }
+                    o[8 + k] = d;
+                    o[k] = st;
+                }
+            }
+        }
+        if (nr) phase = (phase + (nr + 2) * E) & 1;
+    }
+    for (int g = 0; g < 2; g++)
+        if (grs[g] >= 0)
+            for (int k = 0; k < 8; k++) S.h_prev[grs[g]][k] = hp[g][k];
+    for (int ph = 0; ph < 2; ph++)
+        for (int c = 0; c < 2; c++) {
+            S.ipd_prev[bk][ph][c] = ipd[ph][c];
+            S.opd_prev[bk][ph][c] = opd[ph][c];
+        }
+    if (u == 0) S.phase_hist = phase;
+}
+
+// ---------------------------------------------------------------------------------------------
 // decorrelator recurrences
 // ---------------------------------------------------------------------------------------------
 // ring layout of one all-pass lane: [0..1] 2-slot delay, [2..4] link 0, [5..8] link 1, [9..13] link 2
@@ -277,7 +434,7 @@ __device__ __forceinline__ void run_frames(uint32_t f0, uint32_t nfr, Load&& loa
     }
 }
 
-__global__ __launch_bounds__(192) void ps_decor_kernel(SbrArgs A)
+__global__ __launch_bounds__(256) void ps_decor_kernel(SbrArgs A)
 {
     const uint32_t run = blockIdx.x;
     const uint32_t f0 = A.runs[2 * run], nfr = A.runs[2 * run + 1];
@@ -362,6 +519,8 @@ __global__ __launch_bounds__(192) void ps_decor_kernel(SbrArgs A)
         run_frames(f0, nfr, load, step);
 #pragma unroll
         for (int k = 0; k < 14; k++) S.aph[k][u] = ap[k];
+    } else if (wave == 3) {
+        ps_param_scan(A, f0, nfr, S, fresh, u);
     } else {
         // ---- transient detector (lane = parameter band), PSImpl.java:238-270 ----
         if (u >= 20) return;
@@ -396,41 +555,51 @@ __global__ __launch_bounds__(192) void ps_decor_kernel(SbrArgs A)
 }
 
 // ---------------------------------------------------------------------------------------------
-// mixing
+// mixing (PSImpl.ps_mix_phase :592-679) + hybrid synthesis (A/ps/Filterbank.java:70-86)
 // ---------------------------------------------------------------------------------------------
-// target mixing coefficients of envelope env, group gr (PSImpl.java:419-482, IPD/OPD absent)
-__device__ __forceinline__ void ps_h(const PsConst& K, const jaad_ps_frame& P, int env, int gr, float h[4])
+// Walk the 32 slots of a frame for one (sub)band of group gr (inputs already in registers): H
+// advances by its delta every slot and restarts at each envelope border, as the Java interpolates.
+template <typename Store>
+__device__ __forceinline__ void mix_band(const SbrArgs& A, const jaad_ps_frame& P, uint32_t f, int gr, bool rot,
+                                         const float2 (&l)[32], const float2 (&r0)[32], const float (&G)[32],
+                                         Store&& store)
 {
-    const int bk = group_bk(gr);
-    const int fine = P.iid_mode >= 3;
-    const int steps = fine ? 15 : 7;
-    int iid = P.iid[env][bk];
-    const int sign = iid < 0 ? -1 : 1;
-    iid = iid < 0 ? -iid : iid;
-    const int icc = P.icc[env][bk];
-    if (P.icc_mode < 3) {  // type 'A'
-        const float c1 = K.sf_iid[fine][steps + iid], c2 = K.sf_iid[fine][steps - iid];
-        const float cosa = K.cos_alphas[icc], sina = K.sin_alphas[icc];
-        const float cosb = K.cos_betas[fine][iid][icc];
-        const float sinb = K.sin_betas[fine][iid][icc] * (float)sign;
-        const float ab1 = (cosb * cosa), ab2 = (sinb * sina), ab3 = (sinb * cosa), ab4 = (cosb * sina);
-        h[0] = (c2 * (ab1 - ab2));
-        h[1] = (c1 * (ab1 + ab2));
-        h[2] = (c2 * (ab3 + ab4));
-        h[3] = (c1 * (ab3 - ab4));
-    } else {  // type 'B'
-        const float cosa = K.sincos_b[fine][steps + iid][icc];
-        const float sina = K.sincos_b[fine][2 * steps - (steps + iid)][icc];
-        const float cosg = K.cos_gammas[fine][iid][icc], sing = K.sin_gammas[fine][iid][icc];
-        h[0] = (kCoefSqrt2 * (cosa * cosg));
-        h[1] = (kCoefSqrt2 * (sina * cosg));
-        h[2] = (kCoefSqrt2 * (-cosa * sing));
-        h[3] = (kCoefSqrt2 * (sina * sing));
+    const float* hbf = A.hb + (size_t)f * (5 * 22 * 16);
+    float H[8], D[8];
+    int env = 0, next = 0;
+#pragma unroll
+    for (int n = 0; n < 32; n++) {
+        if (n == next) {  // uniform: the borders are per frame
+            const float* hv = hbf + (env * 22 + gr) * 16;
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                H[k] = hv[k];
+                D[k] = hv[8 + k];
+            }
+            env++;
+            next = P.border[env];
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++) H[k] += D[k];
+        if (rot)
+#pragma unroll
+            for (int k = 4; k < 8; k++) H[k] += D[k];
+        const float2 x = l[n];
+        const float2 r = make_float2((G[n] * r0[n].x), (G[n] * r0[n].y));
+        float2 ol = make_float2((H[0] * x.x) + (H[2] * r.x), (H[0] * x.y) + (H[2] * r.y));
+        float2 orr = make_float2((H[1] * x.x) + (H[3] * r.x), (H[1] * x.y) + (H[3] * r.y));
+        if (rot) {
+            ol.x -= (H[4] * x.y) + (H[6] * r.y);
+            ol.y += (H[4] * x.x) + (H[6] * r.x);
+            orr.x -= (H[5] * x.y) + (H[7] * r.y);
+            orr.y += (H[5] * x.x) + (H[7] * r.x);
+        }
+        store(n, ol, orr);
     }
 }
 
 struct MixLds {
-    float4 H[32][22];  // H11, H12, H21, H22 at slot n (after the n-th increment)
+    float2 ml[32][12], mr[32][12];
 };
 
 __global__ __launch_bounds__(256) void ps_mix_kernel(SbrArgs A)
@@ -440,102 +609,72 @@ __global__ __launch_bounds__(256) void ps_mix_kernel(SbrArgs A)
     const uint32_t f = blockIdx.x * kPsWaves + wave;
     if (f >= A.n_cf) return;
     MixLds& L = lds_s[wave];
-    const SbrRec& R = A.recs[f];
     const jaad_ps_frame& P = A.psf[f];
-    const PsConst& K = *A.psc;
-    const int num_env = P.num_env;
-
-    // ---- H per slot and group: h_prev = frame f-1's last envelope (or the slot state) ----
-    if (u < 22) {
-        float hp[4];
-        if (R.first) {
-            const PsState& S = A.pss[R.slot];
-            for (int k = 0; k < 4; k++) hp[k] = S.init ? S.h_prev[u][k] : (k == 0 ? 1.0f : 0.0f);
-        } else {
-            const jaad_ps_frame& Pp = A.psf[f - 1];
-            ps_h(K, Pp, Pp.num_env - 1, u, hp);
-        }
-        for (int env = 0; env < num_env; env++) {
-            float h[4], d[4], H[4];
-            ps_h(K, P, env, u, h);
-            const float Lf = (float)(P.border[env + 1] - P.border[env]);
-            for (int k = 0; k < 4; k++) {
-                d[k] = __fdiv_rn(h[k] - hp[k], Lf);
-                H[k] = hp[k];
-                hp[k] = h[k];
+    const int nr = P.nr_ipdopd_par;
+    const float* pg = A.pg + (size_t)f * 640;
+    float2* xl = reinterpret_cast<float2*>(A.xps + (size_t)f * 8192);
+    float2* xr = xl + 2048;
+    // ---- QMF bands 3..63 (lane = band), then hybrid groups 0..9 (lane = group, one sub-band
+    // each, into LDS); all 32 slots of inputs are loaded before the mixing walk ----
+    const float2* hl = reinterpret_cast<const float2*>(A.xhl + (size_t)f * 768);
+    const float2* hr = reinterpret_cast<const float2*>(A.xhr + (size_t)f * 768);
+    {
+        float2 l[32], r[32];
+        float G[32];
+        if (u >= 3) {
+            int gr = 10;
+            for (int g = 10; g < 22; g++)
+                if (u >= kBorder[g]) gr = g;
+            const int bk = gr - 2;
+#pragma unroll
+            for (int n = 0; n < 32; n++) {
+                l[n] = xl[n * 64 + u];
+                r[n] = xr[n * 64 + u];
+                G[n] = pg[n * 20 + bk];
             }
-            for (int n = P.border[env]; n < P.border[env + 1]; n++) {
-                for (int k = 0; k < 4; k++) H[k] += d[k];
-                L.H[n][u] = make_float4(H[0], H[1], H[2], H[3]);
+            mix_band(A, P, f, gr, bk < nr, l, r, G,
+                     [&](int n, float2 a, float2 b) { xl[n * 64 + u] = a; xr[n * 64 + u] = b; });
+        }
+        if (u < 10) {
+            const int sb = kBorder[u], bk = group_bk(u);
+#pragma unroll
+            for (int n = 0; n < 32; n++) {
+                l[n] = hl[n * 12 + sb];
+                r[n] = hr[n * 12 + sb];
+                G[n] = pg[n * 20 + bk];
+            }
+            mix_band(A, P, f, u, bk < nr, l, r, G,
+                     [&](int n, float2 a, float2 b) { L.ml[n][sb] = a; L.mr[n][sb] = b; });
+        } else if (u < 12) {  // sub-bands 4, 5: zero after grouping, never decorrelated or mixed
+            const int sb = u - 6;
+            for (int n = 0; n < 32; n++) {
+                L.ml[n][sb] = hl[n * 12 + sb];
+                L.mr[n][sb] = make_float2(0.0f, 0.0f);
             }
         }
     }
     wave_sync();
-
-    const float* pg = A.pg + (size_t)f * 640;
-    float2* xl = reinterpret_cast<float2*>(A.xps + (size_t)f * 8192);
-    float2* xr = xl + 2048;
-    // ---- QMF bands 3..63 (lane = band) ----
-    if (u >= 3) {
-        int gr = 10;
-        for (int g = 10; g < 22; g++)
-            if (u >= kBorder[g]) gr = g;
-        const int bk = gr - 2;
-        float2 l[32], r[32];
-        float G[32];
-#pragma unroll
-        for (int n = 0; n < 32; n++) {
-            l[n] = xl[n * 64 + u];
-            r[n] = xr[n * 64 + u];
-            G[n] = pg[n * 20 + bk];
-        }
-#pragma unroll
-        for (int n = 0; n < 32; n++) {
-            const float4 H = L.H[n][gr];
-            const float2 rr = make_float2((G[n] * r[n].x), (G[n] * r[n].y));
-            xl[n * 64 + u] = make_float2((H.x * l[n].x) + (H.z * rr.x), (H.x * l[n].y) + (H.z * rr.y));
-            xr[n * 64 + u] = make_float2((H.y * l[n].x) + (H.w * rr.x), (H.y * l[n].y) + (H.w * rr.y));
-        }
-    }
-    // ---- hybrid sub-bands (lane = slot): mixing + hybrid synthesis into bands 0..2 ----
-    if (u < 32) {
-        const int n = u;
-        const float2* hl = reinterpret_cast<const float2*>(A.xhl + (size_t)f * 768) + n * 12;
-        const float2* hr = reinterpret_cast<const float2*>(A.xhr + (size_t)f * 768) + n * 12;
-        float2 ml[12], mr[12];
-#pragma unroll
-        for (int k = 0; k < 12; k++) {
-            const int gr = kSubGroup[k];
-            if (gr < 0) {  // sub-bands 4, 5: zero after grouping, never decorrelated or mixed
-                ml[k] = hl[k];
-                mr[k] = make_float2(0.0f, 0.0f);
-                continue;
-            }
-            const float G = pg[n * 20 + group_bk(gr)];
-            const float2 l = hl[k], r0 = hr[k];
-            const float2 rr = make_float2((G * r0.x), (G * r0.y));
-            const float4 H = L.H[n][gr];
-            ml[k] = make_float2((H.x * l.x) + (H.z * rr.x), (H.x * l.y) + (H.z * rr.y));
-            mr[k] = make_float2((H.y * l.x) + (H.w * rr.x), (H.y * l.y) + (H.w * rr.y));
-        }
+    // ---- hybrid synthesis (lane = slot; 0..31 left, 32..63 right) into bands 0..2 ----
+    {
+        const int n = u & 31;
+        const float2* m = u < 32 ? L.ml[n] : L.mr[n];
+        float2* x = u < 32 ? xl : xr;
         const int res[3] = {8, 2, 2};
         for (int band = 0, off = 0; band < 3; band++) {
-            float lr = 0.0f, li = 0.0f, rr = 0.0f, ri = 0.0f;
+            float re = 0.0f, im = 0.0f;
             for (int k = 0; k < res[band]; k++) {
-                lr += ml[off + k].x;
-                li += ml[off + k].y;
-                rr += mr[off + k].x;
-                ri += mr[off + k].y;
+                re += m[off + k].x;
+                im += m[off + k].y;
             }
-            xl[n * 64 + band] = make_float2(lr, li);
-            xr[n * 64 + band] = make_float2(rr, ri);
+            x[n * 64 + band] = make_float2(re, im);
             off += res[band];
         }
     }
 }
 
 // ---------------------------------------------------------------------------------------------
-// per-run state after its last frame (the recurrences' state is written by ps_decor_kernel)
+// per-run state after its last frame: filterbank history (the recurrences' and the mixing
+// parameters' state is written by ps_decor_kernel)
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(64) void ps_state_kernel(SbrArgs A)
 {
@@ -549,12 +688,6 @@ __global__ __launch_bounds__(64) void ps_state_kernel(SbrArgs A)
         S.hyb[u / 12][u % 12][0] = h.x;
         S.hyb[u / 12][u % 12][1] = h.y;
     }
-    if (u < 22) {
-        const jaad_ps_frame& P = A.psf[fl];
-        float h[4];
-        ps_h(*A.psc, P, P.num_env - 1, u, h);
-        for (int k = 0; k < 4; k++) S.h_prev[u][k] = h[k];
-    }
     wave_sync();
     if (u == 0) S.init = 1;
 }
@@ -566,7 +699,7 @@ hipError_t launch_ps(const SbrArgs& a, hipStream_t stream)
     if (!a.n_runs) return hipSuccess;
     const dim3 g((a.n_cf + kPsWaves - 1) / kPsWaves);
     hipLaunchKernelGGL(ps_analysis_kernel, g, dim3(64 * kPsWaves), 0, stream, a);
-    hipLaunchKernelGGL(ps_decor_kernel, dim3(a.n_runs), dim3(192), 0, stream, a);
+    hipLaunchKernelGGL(ps_decor_kernel, dim3(a.n_runs), dim3(256), 0, stream, a);
     hipLaunchKernelGGL(ps_mix_kernel, g, dim3(64 * kPsWaves), 0, stream, a);
     hipLaunchKernelGGL(ps_state_kernel, dim3(a.n_runs), dim3(64), 0, stream, a);
     return hipGetLastError();

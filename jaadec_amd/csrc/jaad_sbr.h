@@ -102,6 +102,7 @@ struct PsConst {
     float cos_gammas[2][16][8], sin_gammas[2][16][8];  // as IIDTables holds them (swapped, see PSImpl)
     float sincos_b[2][31][8];
     float p8[7], p2[7];
+    float ipdopd_cos[9], ipdopd_sin[9];
 };
 
 // Rings are stored rotated so that index 0 is the next read position (the kernels run exactly
@@ -113,9 +114,11 @@ struct PsState {
     float2 aph[14][16];    // hybrid groups 0..9 (delay_SubQmf / delay_SubQmf_ser), same layout as ap
     float hyb[3][12][2];   // Filterbank.buffer[band][0..11]
     float peak[20], smooth[20], pprev[20];
-    float h_prev[22][4];   // h11, h12, h21, h22 real parts per group
+    float h_prev[22][8];   // h11, h12, h21, h22 real parts, then imaginary parts, per group
+    float ipd_prev[20][2][2], opd_prev[20][2][2];  // PDData.prev per parameter band and phase slot
+    int32_t phase_hist;
     int32_t init;
-    int32_t pad[3];
+    int32_t pad[2];
 };
 
 struct SbrArgs {
@@ -149,6 +152,7 @@ struct SbrArgs {
     float* xhl;                 // [frame][32][12][2] hybrid X_left
     float* xhr;                 // [frame][32][12][2] hybrid all-pass output
     float* pg;                  // [frame][32][20] P, then G_TransientRatio
+    float* hb;                  // [frame][env 5][group 22][16]: H start (re 4, im 4), delta (re 4, im 4)
     const uint32_t* runs;       // [run] = (first frame, frame count)
     uint32_t n_runs;
 };

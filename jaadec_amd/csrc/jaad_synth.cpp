@@ -255,7 +255,7 @@ void gen_sbr_stream(const jaad_synth_params& P, jaad_sbr_frame* out, uint32_t s)
             jaad_ps_frame& S = F.ps;
             S.iid_mode = 1;
             S.icc_mode = 1;
-            S.ext = 0;
+            S.nr_ipdopd_par = 0;
             const int ne = 1 + (int)r.below(2);
             S.num_env = (uint8_t)ne;
             for (int e = 0; e <= ne; e++) S.border[e] = (uint8_t)(e * 32 / ne);

@@ -17,7 +17,7 @@ import os as _os
 LIB_PATH = Path(_os.environ["JAAD_LIB"]) if _os.environ.get("JAAD_LIB") else PKG / "libjaadgpu.so"
 SYNTH_PATH = PKG / "libjaadsynth.so"
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 # status codes (jaad_status)
 OK, ERR_INVALID_ARG, ERR_NO_DEVICE, ERR_HIP, ERR_UNSUPPORTED, ERR_BITSTREAM, ERR_NOMEM, ERR_ABI = 0, -1, -2, -3, -4, -5, -6, -7
@@ -44,12 +44,13 @@ SBR_CHANNEL_DTYPE = np.dtype([
     ("add_harmonic", "<u8"), ("E", "<i2", (5, 64)), ("Q", "<i2", (2, 8)), ("frame_class", "u1"), ("L_E", "u1"),
     ("L_Q", "u1"), ("bs_pointer", "u1"), ("t_E", "u1", (6,)), ("t_Q", "u1", (3,)), ("f", "u1", (6,)),
     ("invf_mode", "u1", (5,)), ("add_harmonic_flag", "u1"), ("reserved", "u1", (7,))])
-PS_FRAME_DTYPE = np.dtype([("iid_mode", "u1"), ("icc_mode", "u1"), ("num_env", "u1"), ("ext", "u1"),
+PS_FRAME_DTYPE = np.dtype([("iid_mode", "u1"), ("icc_mode", "u1"), ("num_env", "u1"), ("nr_ipdopd_par", "u1"),
                            ("border", "u1", (6,)), ("reserved", "u1", (2,)), ("iid", "i1", (5, 34)),
-                           ("icc", "i1", (5, 34))])
+                           ("icc", "i1", (5, 34)), ("ipd", "i1", (5, 17)), ("opd", "i1", (5, 17)),
+                           ("pad", "u1", (6,))])
 SBR_FRAME_DTYPE = np.dtype([("header_present", "u1"), ("coupling", "u1"), ("ps_present", "u1"), ("reserved", "u1"),
                             ("hdr", SBR_HEADER_DTYPE), ("ch", SBR_CHANNEL_DTYPE, (2,)), ("ps", PS_FRAME_DTYPE)])
-assert SBR_CHANNEL_DTYPE.itemsize == 712 and PS_FRAME_DTYPE.itemsize == 352 and SBR_FRAME_DTYPE.itemsize == 1792
+assert SBR_CHANNEL_DTYPE.itemsize == 712 and PS_FRAME_DTYPE.itemsize == 528 and SBR_FRAME_DTYPE.itemsize == 1968
 
 
 class StreamCfg(C.Structure):

@@ -4,8 +4,8 @@
  * Plain-C restatement of the reference's parametric stereo (HE-AAC v2) path, A/ = aac/src/main/
  * java/net/sourceforge/jaad/aac/: PSImpl (decorrelation, mixing), ps/Filterbank + Filter8 +
  * Filter2 (hybrid analysis/synthesis, T20 -- FBType.max always yields T20, A/ps/FBType.java:17-19).
- * Inputs are the values ps_data_decode leaves behind (jaad_ps_frame).  IPD/OPD (the PS extension)
- * is not restated: nr_ipdopd_par is 0 without it (A/ps/Extension.java:81-86).
+ * Inputs are the values ps_data_decode leaves behind (jaad_ps_frame), including the IPD/OPD
+ * indices of the PS extension and Extension.nr_par() (A/ps/Extension.java:81-86).
  */
 #include "jaad_oracle.h"
 
@@ -39,9 +39,11 @@ struct orc_ps {
     float delay_Qmf_ser[NO_ALLPASS_LINKS][5][64][2], delay_SubQmf_ser[NO_ALLPASS_LINKS][5][32][2];
     float P_PeakDecayNrg[34], P_prev[34], P_SmoothPeakDecayDiffNrg_prev[34];
     float h11_prev[50][2], h12_prev[50][2], h21_prev[50][2], h22_prev[50][2];
+    float ipd_prev[20][2][2], opd_prev[20][2][2]; /* PDData.prev (A/ps/PDData.java:13) */
+    int phase_hist;
     /* parameters of the current frame */
-    int num_env, border_position[6], iid_mode, icc_mode;
-    int iid_index[5][34], icc_index[5][34];
+    int num_env, border_position[6], iid_mode, icc_mode, nr_ipdopd_par;
+    int iid_index[5][34], icc_index[5][34], ipd_index[5][17];
 };
 
 size_t orc_ps_bytes(void) { return sizeof(orc_ps); }
@@ -63,12 +65,15 @@ void orc_ps_set_frame(orc_ps* ps, const jaad_ps_frame* f)
     ps->num_env = f->num_env;
     ps->iid_mode = f->iid_mode;
     ps->icc_mode = f->icc_mode;
+    ps->nr_ipdopd_par = f->nr_ipdopd_par;
     for (int e = 0; e <= f->num_env && e < 6; e++) ps->border_position[e] = f->border[e];
     for (int e = 0; e < 5; e++)
         for (int b = 0; b < 34; b++) {
             ps->iid_index[e][b] = f->iid[e][b];
             ps->icc_index[e][b] = f->icc[e][b];
         }
+    for (int e = 0; e < 5; e++)
+        for (int b = 0; b < 17; b++) ps->ipd_index[e][b] = f->ipd[e][b];
 }
 
 /* Filter8.DCT3_4_unscaled (A/ps/Filter8.java:122-137), y may alias x */
@@ -322,7 +327,10 @@ static void ps_decorrelate(orc_ps* ps, float (*X_left)[64][2], float (*X_right)[
     memcpy(ps->delay_buf_index_ser, temp_delay_ser, sizeof temp_delay_ser);
 }
 
-/* PSImpl.ps_mix_phase without IPD/OPD (A/ps/PSImpl.java:406-681) */
+/* PSImpl.magnitude_c (A/ps/PSImpl.java:402-404) */
+static float magnitude_c(const float* c) { return (float)sqrt((double)((c[0] * c[0]) + (c[1] * c[1]))); }
+
+/* PSImpl.ps_mix_phase (A/ps/PSImpl.java:406-681) */
 static void ps_mix_phase(orc_ps* ps, float (*X_left)[64][2], float (*X_right)[64][2], float (*X_hybrid_left)[32][2],
                          float (*X_hybrid_right)[32][2])
 {
@@ -337,7 +345,10 @@ static void ps_mix_phase(orc_ps* ps, float (*X_left)[64][2], float (*X_right)[64
     const float* sin_gammas = fine ? JAAD_PS_COS_GAMMAS_FINE : JAAD_PS_COS_GAMMAS_NORMAL;
     const float* sincos_alphas_b = fine ? JAAD_PS_SINCOS_ALPHAS_B_FINE : JAAD_PS_SINCOS_ALPHAS_B_NORMAL;
     float h11[2] = {0, 0}, h12[2] = {0, 0}, h21[2] = {0, 0}, h22[2] = {0, 0};
-    float H11[2], H12[2], H21[2], H22[2], deltaH11[2], deltaH12[2], deltaH21[2], deltaH22[2];
+    float H11[2] = {0, 0}, H12[2] = {0, 0}, H21[2] = {0, 0}, H22[2] = {0, 0};
+    float deltaH11[2] = {0, 0}, deltaH12[2] = {0, 0}, deltaH21[2] = {0, 0}, deltaH22[2] = {0, 0};
+    float tempLeft[2], tempRight[2], phaseLeft[2], phaseRight[2];
+    const int nr_ipdopd_par = ps->nr_ipdopd_par;
     for (int gr = 0; gr < T20_NUM_GROUPS; gr++) {
         const int bk = t20_bk(gr);
         const int maxsb = gr < T20_NUM_HYBRID_GROUPS ? JAAD_PS_GROUP_BORDER20[gr] + 1 : JAAD_PS_GROUP_BORDER20[gr + 1];
@@ -368,6 +379,60 @@ static void ps_mix_phase(orc_ps* ps, float (*X_left)[64][2], float (*X_right)[64
                 h21[0] = (COEF_SQRT2 * (-cosa * sing));
                 h22[0] = (COEF_SQRT2 * (sina * sing));
             }
+            if (bk < nr_ipdopd_par) { /* phase rotation (:484-567) */
+                float* ipd_prev = ps->ipd_prev[bk][ps->phase_hist];
+                float* opd_prev = ps->opd_prev[bk][ps->phase_hist];
+                tempLeft[0] = (ipd_prev[0] * 0.25f);
+                tempLeft[1] = (ipd_prev[1] * 0.25f);
+                tempRight[0] = (opd_prev[0] * 0.25f);
+                tempRight[1] = (opd_prev[1] * 0.25f);
+                /* both indices are read from the IPD data (:502-503) */
+                const int ipd_index = abs(ps->ipd_index[env][bk]);
+                const int opd_index = abs(ps->ipd_index[env][bk]);
+                ipd_prev[0] = JAAD_PS_IPDOPD_COS[ipd_index];
+                ipd_prev[1] = JAAD_PS_IPDOPD_SIN[ipd_index];
+                opd_prev[0] = JAAD_PS_IPDOPD_COS[opd_index];
+                opd_prev[1] = JAAD_PS_IPDOPD_SIN[opd_index];
+                tempLeft[0] += ipd_prev[0];
+                tempLeft[1] += ipd_prev[1];
+                tempRight[0] += opd_prev[0];
+                tempRight[1] += opd_prev[1];
+                ps->phase_hist = (ps->phase_hist + 1) % 2;
+                /* the value before previous comes from opd.prev for both (:519-520) */
+                ipd_prev = ps->opd_prev[bk][ps->phase_hist];
+                opd_prev = ps->opd_prev[bk][ps->phase_hist];
+                tempLeft[0] += (ipd_prev[0] * 0.5f);
+                tempLeft[1] += (ipd_prev[1] * 0.5f);
+                tempRight[0] += (opd_prev[0] * 0.5f);
+                tempRight[1] += (opd_prev[1] * 0.5f);
+                const float xy = magnitude_c(tempRight);
+                const float pq = magnitude_c(tempLeft);
+                if (xy != 0) {
+                    phaseLeft[0] = (tempRight[0] / xy);
+                    phaseLeft[1] = (tempRight[1] / xy);
+                } else {
+                    phaseLeft[0] = 0;
+                    phaseLeft[1] = 0;
+                }
+                const float xypq = (xy * pq);
+                if (xypq != 0) {
+                    const float tmp1 = (tempRight[0] * tempLeft[0]) + (tempRight[1] * tempLeft[1]);
+                    const float tmp2 = (tempRight[1] * tempLeft[0]) - (tempRight[0] * tempLeft[1]);
+                    phaseRight[0] = (tmp1 / xypq);
+                    phaseRight[1] = (tmp2 / xypq);
+                } else {
+                    phaseRight[0] = 0;
+                    phaseRight[1] = 0;
+                }
+                h11[1] = (h11[0] * phaseLeft[1]);
+                h12[1] = (h12[0] * phaseRight[1]);
+                h21[1] = (h21[0] * phaseLeft[1]);
+                h22[1] = (h22[0] * phaseRight[1]);
+                h11[0] = (h11[0] * phaseLeft[0]);
+                h12[0] = (h12[0] * phaseRight[0]);
+                h21[0] = (h21[0] * phaseLeft[0]);
+                h22[0] = (h22[0] * phaseRight[0]);
+            }
             const float L = (float)(ps->border_position[env + 1] - ps->border_position[env]);
             deltaH11[0] = (h11[0] - ps->h11_prev[gr][0]) / L;
             deltaH12[0] = (h12[0] - ps->h12_prev[gr][0]) / L;
@@ -381,11 +446,41 @@ static void ps_mix_phase(orc_ps* ps, float (*X_left)[64][2], float (*X_right)[64
             ps->h12_prev[gr][0] = h12[0];
             ps->h21_prev[gr][0] = h21[0];
             ps->h22_prev[gr][0] = h22[0];
+            if (bk < nr_ipdopd_par) {
+                deltaH11[1] = (h11[1] - ps->h11_prev[gr][1]) / L;
+                deltaH12[1] = (h12[1] - ps->h12_prev[gr][1]) / L;
+                deltaH21[1] = (h21[1] - ps->h21_prev[gr][1]) / L;
+                deltaH22[1] = (h22[1] - ps->h22_prev[gr][1]) / L;
+                H11[1] = ps->h11_prev[gr][1];
+                H12[1] = ps->h12_prev[gr][1];
+                H21[1] = ps->h21_prev[gr][1];
+                H22[1] = ps->h22_prev[gr][1];
+                if (bk != 0) { /* FBType.bkm tests the band bits, not NEGATE_IPD_MASK (A/ps/FBType.java:71-73) */
+                    deltaH11[1] = -deltaH11[1];
+                    deltaH12[1] = -deltaH12[1];
+                    deltaH21[1] = -deltaH21[1];
+                    deltaH22[1] = -deltaH22[1];
+                    H11[1] = -H11[1];
+                    H12[1] = -H12[1];
+                    H21[1] = -H21[1];
+                    H22[1] = -H22[1];
+                }
+                ps->h11_prev[gr][1] = h11[1];
+                ps->h12_prev[gr][1] = h12[1];
+                ps->h21_prev[gr][1] = h21[1];
+                ps->h22_prev[gr][1] = h22[1];
+            }
             for (int n = ps->border_position[env]; n < ps->border_position[env + 1]; n++) {
                 H11[0] += deltaH11[0];
                 H12[0] += deltaH12[0];
                 H21[0] += deltaH21[0];
                 H22[0] += deltaH22[0];
+                if (bk < nr_ipdopd_par) {
+                    H11[1] += deltaH11[1];
+                    H12[1] += deltaH12[1];
+                    H21[1] += deltaH21[1];
+                    H22[1] += deltaH22[1];
+                }
                 for (int sb = JAAD_PS_GROUP_BORDER20[gr]; sb < maxsb; sb++) {
                     float inLeft[2], inRight[2], tl[2], tr[2];
                     const int hyb = gr < T20_NUM_HYBRID_GROUPS;
@@ -397,6 +492,12 @@ static void ps_mix_phase(orc_ps* ps, float (*X_left)[64][2], float (*X_right)[64
                     tl[1] = (H11[0] * inLeft[1]) + (H21[0] * inRight[1]);
                     tr[0] = (H12[0] * inLeft[0]) + (H22[0] * inRight[0]);
                     tr[1] = (H12[0] * inLeft[1]) + (H22[0] * inRight[1]);
+                    if (bk < nr_ipdopd_par) {
+                        tl[0] -= (H11[1] * inLeft[1]) + (H21[1] * inRight[1]);
+                        tl[1] += (H11[1] * inLeft[0]) + (H21[1] * inRight[0]);
+                        tr[0] -= (H12[1] * inLeft[1]) + (H22[1] * inRight[1]);
+                        tr[1] += (H12[1] * inLeft[0]) + (H22[1] * inRight[0]);
+                    }
                     float* ol = hyb ? X_hybrid_left[n][sb] : X_left[n][sb];
                     float* orr = hyb ? X_hybrid_right[n][sb] : X_right[n][sb];
                     ol[0] = tl[0];

@@ -1104,10 +1104,12 @@ static void load_channel(const orc_sbr* s, orc_sbr_channel* ch, const jaad_sbr_c
 }
 
 /* what PSImpl.ps_data_decode can leave behind (A/ps/PSImpl.java:103-199): 1..5 envelopes with
- * borders 0 = b_0 < .. < b_num_env = 32, |IID| <= num_steps, ICC 0..7; no IPD/OPD extension */
+ * borders 0 = b_0 < .. < b_num_env = 32, |IID| <= num_steps, ICC 0..7, IPD/OPD 0..7 (PDMode.clip)
+ * for the nr_ipdopd_par (0, 11 or 17) bands */
 static int ps_frame_valid(const jaad_ps_frame* p)
 {
-    if (p->num_env < 1 || p->num_env > 5 || p->ext || p->iid_mode > 5 || p->icc_mode > 5) return 0;
+    if (p->num_env < 1 || p->num_env > 5 || p->iid_mode > 5 || p->icc_mode > 5) return 0;
+    if (p->nr_ipdopd_par != 0 && p->nr_ipdopd_par != 11 && p->nr_ipdopd_par != 17) return 0;
     if (p->border[0] != 0 || p->border[p->num_env] != 32) return 0;
     for (int e = 0; e < p->num_env; e++)
         if (p->border[e + 1] <= p->border[e]) return 0;
@@ -1115,6 +1117,9 @@ static int ps_frame_valid(const jaad_ps_frame* p)
     for (int e = 0; e < p->num_env; e++)
         for (int b = 0; b < 20; b++)
             if (p->iid[e][b] > steps || p->iid[e][b] < -steps || p->icc[e][b] < 0 || p->icc[e][b] > 7) return 0;
+    for (int e = 0; e < p->num_env; e++)
+        for (int b = 0; b < p->nr_ipdopd_par; b++)
+            if (p->ipd[e][b] < 0 || p->ipd[e][b] > 7 || p->opd[e][b] < 0 || p->opd[e][b] > 7) return 0;
     return 1;
 }
 

@@ -60,6 +60,33 @@ def test_c5_variable_envelopes_and_transients():
     _assert_same(got, want, N.PCM_FLOAT32)
 
 
+@pytest.mark.parametrize("nr", [11, 17])
+def test_c5_ipd_opd_phase_rotation(nr):
+    """PS extension: IPD/OPD phase history and complex H interpolation (A/ps/PSImpl.java:484-679),
+    toggled on and off between frames so h_prev's imaginary parts persist through frames without it."""
+    p = N.synth_params(5, n_streams=3, frames_per_stream=14)
+    rng = np.random.default_rng(nr)
+
+    def fn(s):
+        ps = s["ps"]
+        ps["nr_ipdopd_par"] = np.where(rng.random(len(s)) < 0.8, nr, 0)
+        ps["ipd"][:] = rng.integers(0, 8, ps["ipd"].shape)
+        ps["opd"][:] = rng.integers(0, 8, ps["opd"].shape)
+        _var_envelopes(s, rng)
+
+    b = _edit(N.synth_batch(p), fn)
+    got, want = _decode_both(p, b, N.PCM_FLOAT32)
+    _assert_same(got, want, N.PCM_FLOAT32)
+    cfg = N.cfg_for(p)
+    first, second = b.split_frames(6)
+    with N.Context(cfg, 3) as ctx:
+        g = np.concatenate([ctx.decode(first, N.PCM_FLOAT32), ctx.decode(second, N.PCM_FLOAT32)])
+    fb = b.frame_begin
+    order = np.concatenate([np.arange(fb[r], fb[r] + 6) for r in range(3)] +
+                           [np.arange(fb[r] + 6, fb[r + 1]) for r in range(3)])
+    _assert_same(g, want[order], N.PCM_FLOAT32)
+
+
 def test_c5_continuation_and_state_roundtrip():
     p = N.synth_params(5, n_streams=3, frames_per_stream=16)
     b = N.synth_batch(p)
@@ -98,7 +125,7 @@ def test_c5_single_frame_calls():
 
 @pytest.mark.parametrize("name,fn,status", [
     ("no_ps_data", lambda s: s.__setitem__("ps_present", 0), N.ERR_UNSUPPORTED),
-    ("ipd_extension", lambda s: s["ps"].__setitem__("ext", 1), N.ERR_BITSTREAM),
+    ("bad_nr_ipdopd_par", lambda s: s["ps"].__setitem__("nr_ipdopd_par", 12), N.ERR_BITSTREAM),
     ("border_not_32", lambda s: s["ps"]["border"].__setitem__((slice(None), 1), 30), N.ERR_BITSTREAM),
     ("iid_out_of_range", lambda s: s["ps"]["iid"].__setitem__((slice(None), 0, 3), 9), N.ERR_BITSTREAM),
 ])

@@ -81,13 +81,15 @@ def test_c5_decorrelates_and_continues_across_calls():
 
 def test_oracle_rejects_parameters_the_parser_cannot_produce():
     """Borders must run 0 = b_0 < .. < b_num_env = 32 and |IID| <= num_steps (the bounds
-    PSImpl.ps_data_decode enforces, A/ps/PSImpl.java:103-199); the IPD/OPD extension is not restated."""
+    PSImpl.ps_data_decode enforces, A/ps/PSImpl.java:103-199); IPD/OPD indices are 0..7 (PDMode.clip)
+    and Extension.nr_par() is 0, 11 or 17."""
     p = N.synth_params(5, n_streams=1, frames_per_stream=2)
     b = N.synth_batch(p)
     cfg = N.cfg_for(p)
     O.decode_batch(cfg, b, O.Streams(1), N.PCM_BIG_ENDIAN)
     for edit in (lambda s: s["ps"]["border"].__setitem__((slice(None), 0), 1),
-                 lambda s: s["ps"].__setitem__("ext", 1),
+                 lambda s: s["ps"].__setitem__("nr_ipdopd_par", 5),
+                 lambda s: (s["ps"].__setitem__("nr_ipdopd_par", 11), s["ps"]["ipd"].__setitem__((slice(None), 0, 3), 8)),
                  lambda s: s["ps"]["iid"].__setitem__((slice(None), 0, 0), 8),
                  lambda s: s["ps"]["icc"].__setitem__((slice(None), 0, 0), -1)):
         s = b.sbr.copy()
@@ -95,3 +97,39 @@ def test_oracle_rejects_parameters_the_parser_cannot_produce():
         bad = N.Batch(b.q, b.sf, b.cb, b.ics, b.ms_used, b.tns, b.stream_slot, b.frame_begin, b.nch, s)
         with pytest.raises(RuntimeError):
             O.decode_batch(cfg, bad, O.Streams(1), N.PCM_BIG_ENDIAN)
+
+
+def _with_ipd(b, nr, ipd):
+    s = b.sbr.copy()
+    s["ps"]["nr_ipdopd_par"] = nr
+    s["ps"]["ipd"][:] = ipd
+    s["ps"]["opd"][:] = ipd
+    return N.Batch(b.q, b.sf, b.cb, b.ics, b.ms_used, b.tns, b.stream_slot, b.frame_begin, b.nch, s)
+
+
+def test_zero_phase_ipd_leaves_the_mix_unchanged():
+    """IPD/OPD index 0 everywhere (A/ps/PSImpl.java:484-567): tempLeft = tempRight = a positive real,
+    so phaseLeft = phaseRight = (1, 0) and the rotated mix equals the plain one; only frame 0 differs,
+    where H12's imaginary part interpolates from h12_prev = (0, 1) (:87-92) to 0, and frame 1 through
+    the synthesis ring."""
+    p = N.synth_params(5, n_streams=1, frames_per_stream=8)
+    b = N.synth_batch(p)
+    cfg = N.cfg_for(p)
+    plain = O.decode_batch(cfg, b, O.Streams(1), N.PCM_BIG_ENDIAN)
+    for nr in (11, 17):
+        rot = O.decode_batch(cfg, _with_ipd(b, nr, 0), O.Streams(1), N.PCM_BIG_ENDIAN)
+        assert not np.array_equal(rot[0], plain[0])
+        assert np.array_equal(rot[2:], plain[2:])
+
+
+def test_nonzero_ipd_changes_only_the_rotated_bands():
+    p = N.synth_params(5, n_streams=1, frames_per_stream=6)
+    b = N.synth_batch(p)
+    cfg = N.cfg_for(p)
+    rng = np.random.default_rng(5)
+    plain = O.decode_batch(cfg, b, O.Streams(1), N.PCM_FLOAT32).view(np.float32).reshape(-1, 2048, 2)
+    rot = O.decode_batch(cfg, _with_ipd(b, 11, rng.integers(0, 8, (len(b.sbr), 5, 17))), O.Streams(1),
+                         N.PCM_FLOAT32).view(np.float32).reshape(-1, 2048, 2)
+    assert np.isfinite(rot).all()
+    d = np.abs(rot - plain).max()
+    assert 0 < d < 4 * np.abs(plain).max()

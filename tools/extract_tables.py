@@ -93,6 +93,8 @@ PS_TABLES = [
     ("ps/PSTables.java", "sin_gammas_fine", "JAAD_PS_SIN_GAMMAS_FINE", "f32_flat"),
     ("ps/PSTables.java", "sf_iid_normal", "JAAD_PS_SF_IID_NORMAL", "f32"),
     ("ps/PSTables.java", "sf_iid_fine", "JAAD_PS_SF_IID_FINE", "f32"),
+    ("ps/PSTables.java", "ipdopd_cos_tab", "JAAD_PS_IPDOPD_COS", "f32"),
+    ("ps/PSTables.java", "ipdopd_sin_tab", "JAAD_PS_IPDOPD_SIN", "f32"),
     ("ps/Filter8.java", "p8_13_20", "JAAD_PS_P8_13_20", "f32"),
     ("ps/Filter2.java", "p2_13_20", "JAAD_PS_P2_13_20", "f32"),
 ]
@@ -109,6 +111,8 @@ def f32_from_decimal(tok: str) -> np.float32:
     """Nearest-even binary32 to the exact decimal value (Float.parseFloat semantics)."""
     tok = tok.strip().rstrip("fFdD")
     exact = Fraction(tok)
+    if exact == 0:  # Java keeps the sign of a zero literal: -0.0f is negative zero
+        return np.float32(-0.0) if tok.lstrip().startswith("-") else np.float32(0.0)
     cand = np.float32(float(exact))  # may suffer double rounding: fix below
     best = None
     for c in (np.nextafter(cand, np.float32(-np.inf)), cand, np.nextafter(cand, np.float32(np.inf))):
