@@ -47,6 +47,41 @@ struct DevBuf {
     }
 };
 
+// page-locked host staging (grows, never shrinks)
+struct PinnedBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t n)
+    {
+        if (n <= cap) return hipSuccess;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        const size_t want = n + n / 2;
+        hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    void release()
+    {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+// One call's SBR/PS parameter records: built on the host straight into page-locked staging,
+// copied on the context's copy stream while the previous call's kernels run.  Two sets
+// alternate between calls; `copied` guards the staging, `used` the device copy.
+//   part 1 (sizes known before the build): recs | psf | chunks | last | runs
+//   part 2 (known after it):               epool | tabs
+struct RecSet {
+    PinnedBuf h1, h2;
+    DevBuf d1, d2;
+    hipEvent_t copied = nullptr, used = nullptr;
+    bool live = false;
+};
+
 }  // namespace
 
 struct jaad_ctx {
@@ -75,17 +110,17 @@ struct jaad_ctx {
     std::vector<SbrHostSlot> sbr_slots;          // parameter-side state per slot (host)
     SbrChState* d_sbr_state = nullptr;           // [slot][2], rewritten at the end of each call
     float* d_sbr_const = nullptr;                // qmf_c[640] | dct4 tab[192] w_re[16] w_im[16] | noise[1024]
-    DevBuf d_time, d_sbr_recs, d_sbr_epool, d_sbr_tabs, d_sbr_chunks, d_sbr_last, d_xlow, d_xsyn, d_xcarry, d_gq;
-    std::vector<SbrRec> sbr_recs;
-    std::vector<float> sbr_epool;
+    DevBuf d_time, d_xlow, d_xsyn, d_xcarry, d_gq;
+    hipStream_t cstream = nullptr;               // record uploads
+    RecSet rsets[2];
+    int rset = 0;
     std::vector<SbrChunk> sbr_chunks;
     std::vector<uint32_t> sbr_last;
     float* sbr_dbg = nullptr;
     // ---- PS (cfg.ps) ----
     PsState* d_ps_state = nullptr;               // [slot]
     PsConst* d_ps_const = nullptr;
-    DevBuf d_psf, d_xps, d_xhl, d_xhr, d_pg, d_hb, d_ps_runs;
-    std::vector<jaad_ps_frame> psf;
+    DevBuf d_xps, d_xhl, d_xhr, d_pg, d_hb;
     std::vector<uint32_t> ps_runs;
 };
 
@@ -301,71 +336,13 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
     const int nch = ctx->nch;
     const bool ps = ctx->cfg.ps != 0;
     const int och = ps ? 2 : nch;  // channels of the QMF synthesis
-    const size_t nf = b->n_frames;
-    ctx->sbr_recs.resize(nf * nch);
-    if (ps) ctx->psf.resize(nf);
-    ctx->sbr_epool.clear();
+    const size_t nf = b->n_frames, ncf = nf * nch;
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+
+    // chunk plan (depends on the runs only)
     ctx->sbr_chunks.clear();
-    // parameter records: runs are independent streams, so they are built in parallel (each
-    // worker owns a contiguous block of runs and its own E_orig pool, rebased afterwards)
-    {
-        unsigned hw = std::thread::hardware_concurrency();
-        int nt = (int)std::min<uint32_t>(b->n_runs, std::min(16u, hw ? hw : 1u));
-        if (nf < 2048) nt = 1;
-        nt = nt < 1 ? 1 : nt;
-        std::vector<std::vector<float>> pools(nt);
-        std::vector<int> rcs(nt, 0), bad(nt, -1);
-        auto work = [&](int t) {
-            const uint32_t r0 = (uint32_t)((uint64_t)b->n_runs * t / nt), r1 = (uint32_t)((uint64_t)b->n_runs * (t + 1) / nt);
-            pools[t].reserve((size_t)(b->frame_begin[r1] - b->frame_begin[r0]) * nch * 40);
-            for (uint32_t r = r0; r < r1 && !rcs[t]; r++) {
-                SbrHostSlot& hs = ctx->sbr_slots[b->stream_slot[r]];
-                for (uint32_t f = b->frame_begin[r]; f < b->frame_begin[r + 1]; f++) {
-                    if (ps) {
-                        if (!ps_frame_ok(b->sbr[f])) {
-                            rcs[t] = b->sbr[f].ps_present ? JAAD_ERR_BITSTREAM : JAAD_ERR_UNSUPPORTED;
-                            bad[t] = (int)f;
-                            break;
-                        }
-                        ctx->psf[f] = b->sbr[f].ps;
-                    }
-                    int rc = ctx->sbr_host->frame(hs, b->sbr[f], nch, f == b->frame_begin[r], b->stream_slot[r],
-                                                  &ctx->sbr_recs[(size_t)f * nch], pools[t]);
-                    if (rc) {
-                        rcs[t] = rc;
-                        bad[t] = (int)f;
-                        break;
-                    }
-                }
-            }
-        };
-        std::vector<std::thread> th;
-        for (int t = 1; t < nt; t++) th.emplace_back(work, t);
-        work(0);
-        for (auto& x : th) x.join();
-        size_t base = 0;
-        for (int t = 0; t < nt; t++) {
-            if (rcs[t]) {
-                ctx->err = (ps ? "SBR/PS side info of frame " : "SBR side info of frame ") + std::to_string(bad[t]);
-                return rcs[t];
-            }
-            const uint32_t r0 = (uint32_t)((uint64_t)b->n_runs * t / nt), r1 = (uint32_t)((uint64_t)b->n_runs * (t + 1) / nt);
-            if (base)
-                for (size_t i = (size_t)b->frame_begin[r0] * nch; i < (size_t)b->frame_begin[r1] * nch; i++)
-                    ctx->sbr_recs[i].e_off += (uint32_t)base;
-            base += pools[t].size();
-        }
-        ctx->sbr_epool.resize(base);
-        base = 0;
-        for (int t = 0; t < nt; t++) {
-            std::memcpy(ctx->sbr_epool.data() + base, pools[t].data(), pools[t].size() * sizeof(float));
-            base += pools[t].size();
-        }
-    }
     ctx->sbr_last.clear();
     ctx->ps_runs.clear();
-    bool smoothing = false;
-    for (const SbrRec& rr : ctx->sbr_recs) smoothing |= (rr.flags & kSbrSmooth) != 0;
     for (uint32_t r = 0; r < b->n_runs; r++) {
         const uint32_t f0 = b->frame_begin[r], f1 = b->frame_begin[r + 1];
         if (f1 == f0) continue;  // empty run: the slot state stays as it is
@@ -380,55 +357,135 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
             ctx->ps_runs.push_back(f1 - f0);
         }
     }
-    if (ctx->sbr_epool.empty()) ctx->sbr_epool.push_back(0.0f);
-    const size_t ncf = nf * nch;
+    const size_t o_recs = 0, o_psf = al(ncf * sizeof(SbrRec));
+    const size_t o_chunks = al(o_psf + (ps ? nf * sizeof(jaad_ps_frame) : 0));
+    const size_t o_last = al(o_chunks + ctx->sbr_chunks.size() * sizeof(SbrChunk));
+    const size_t o_runs = al(o_last + ctx->sbr_last.size() * sizeof(uint32_t));
+    const size_t n1 = al(o_runs + ctx->ps_runs.size() * sizeof(uint32_t));
+
+    RecSet& S = ctx->rsets[ctx->rset];
+    ctx->rset ^= 1;
+    if (S.live) HIPCHK(hipEventSynchronize(S.copied));  // its staging may be rewritten
+    HIPCHK(S.h1.ensure(n1));
+    char* h1 = static_cast<char*>(S.h1.p);
+    SbrRec* recs = reinterpret_cast<SbrRec*>(h1 + o_recs);
+    jaad_ps_frame* psf = reinterpret_cast<jaad_ps_frame*>(h1 + o_psf);
+    if (!ctx->sbr_chunks.empty())
+        std::memcpy(h1 + o_chunks, ctx->sbr_chunks.data(), ctx->sbr_chunks.size() * sizeof(SbrChunk));
+    if (!ctx->sbr_last.empty())
+        std::memcpy(h1 + o_last, ctx->sbr_last.data(), ctx->sbr_last.size() * sizeof(uint32_t));
+    if (!ctx->ps_runs.empty())
+        std::memcpy(h1 + o_runs, ctx->ps_runs.data(), ctx->ps_runs.size() * sizeof(uint32_t));
+
+    // parameter records: runs are independent streams, so they are built in parallel (each
+    // worker owns a contiguous block of runs and its own E_orig pool, rebased afterwards)
+    unsigned hw = std::thread::hardware_concurrency();
+    int nt = (int)std::min<uint32_t>(b->n_runs, std::min(16u, hw ? hw : 1u));
+    if (nf < 2048) nt = 1;
+    nt = nt < 1 ? 1 : nt;
+    std::vector<std::vector<float>> pools(nt);
+    std::vector<int> rcs(nt, 0), bad(nt, -1);
+    std::vector<size_t> pbase(nt + 1, 0);
+    std::vector<char> smooth(nt, 0);
+    auto run_range = [&](int t, uint32_t& r0, uint32_t& r1) {
+        r0 = (uint32_t)((uint64_t)b->n_runs * t / nt);
+        r1 = (uint32_t)((uint64_t)b->n_runs * (t + 1) / nt);
+    };
+    auto work = [&](int t) {
+        uint32_t r0, r1;
+        run_range(t, r0, r1);
+        pools[t].reserve((size_t)(b->frame_begin[r1] - b->frame_begin[r0]) * nch * 40);
+        for (uint32_t r = r0; r < r1 && !rcs[t]; r++) {
+            SbrHostSlot& hs = ctx->sbr_slots[b->stream_slot[r]];
+            for (uint32_t f = b->frame_begin[r]; f < b->frame_begin[r + 1]; f++) {
+                if (ps) {
+                    if (!ps_frame_ok(b->sbr[f])) {
+                        rcs[t] = b->sbr[f].ps_present ? JAAD_ERR_BITSTREAM : JAAD_ERR_UNSUPPORTED;
+                        bad[t] = (int)f;
+                        break;
+                    }
+                    psf[f] = b->sbr[f].ps;
+                }
+                int rc = ctx->sbr_host->frame(hs, b->sbr[f], nch, f == b->frame_begin[r], b->stream_slot[r],
+                                              &recs[(size_t)f * nch], pools[t]);
+                if (rc) {
+                    rcs[t] = rc;
+                    bad[t] = (int)f;
+                    break;
+                }
+            }
+        }
+    };
+    auto parallel = [&](auto&& fn) {
+        std::vector<std::thread> th;
+        for (int t = 1; t < nt; t++) th.emplace_back(fn, t);
+        fn(0);
+        for (auto& x : th) x.join();
+    };
+    parallel(work);
+    for (int t = 0; t < nt; t++) {
+        if (rcs[t]) {
+            ctx->err = (ps ? "SBR/PS side info of frame " : "SBR side info of frame ") + std::to_string(bad[t]);
+            return rcs[t];
+        }
+        pbase[t + 1] = pbase[t] + pools[t].size();
+    }
+    const size_t n_epool = pbase[nt] ? pbase[nt] : 1;
     const auto& tabs = ctx->sbr_host->tabs();
-    HIPCHK(ctx->d_sbr_recs.ensure(ctx->sbr_recs.size() * sizeof(SbrRec) + 256));
-    HIPCHK(ctx->d_sbr_epool.ensure(ctx->sbr_epool.size() * sizeof(float) + 256));
-    HIPCHK(ctx->d_sbr_tabs.ensure((tabs.size() + 1) * sizeof(SbrTab)));
-    HIPCHK(ctx->d_sbr_chunks.ensure(ctx->sbr_chunks.size() * sizeof(SbrChunk) + 256));
-    HIPCHK(ctx->d_sbr_last.ensure(ctx->sbr_last.size() * sizeof(uint32_t) + 256));
+    const size_t o_tabs = al(n_epool * sizeof(float));
+    const size_t n2 = o_tabs + (tabs.size() + 1) * sizeof(SbrTab);
+    HIPCHK(S.h2.ensure(n2));
+    char* h2 = static_cast<char*>(S.h2.p);
+    // second pass: rebase e_off, move each pool into the staging, find smoothing frames
+    parallel([&](int t) {
+        uint32_t r0, r1;
+        run_range(t, r0, r1);
+        bool sm = false;
+        for (size_t i = (size_t)b->frame_begin[r0] * nch; i < (size_t)b->frame_begin[r1] * nch; i++) {
+            recs[i].e_off += (uint32_t)pbase[t];
+            sm |= (recs[i].flags & kSbrSmooth) != 0;
+        }
+        smooth[t] = sm;
+        if (!pools[t].empty())
+            std::memcpy(h2 + pbase[t] * sizeof(float), pools[t].data(), pools[t].size() * sizeof(float));
+    });
+    bool smoothing = false;
+    for (int t = 0; t < nt; t++) smoothing |= smooth[t] != 0;
+    if (!tabs.empty()) std::memcpy(h2 + o_tabs, tabs.data(), tabs.size() * sizeof(SbrTab));
+
+    // device side: intermediates (stream-ordered) and this set's record copy (copy stream)
     HIPCHK(ctx->d_xlow.ensure(ncf * 2048 * sizeof(float) + 256));
     HIPCHK(ctx->d_xsyn.ensure(ncf * 4096 * sizeof(float) + 256));
     HIPCHK(ctx->d_xcarry.ensure(ncf * 768 * sizeof(float) + 256));
     HIPCHK(ctx->d_gq.ensure(ncf * 640 * sizeof(float) + 256));
-    HIPCHK(hipMemcpyAsync(ctx->d_sbr_recs.p, ctx->sbr_recs.data(), ctx->sbr_recs.size() * sizeof(SbrRec),
-                          hipMemcpyHostToDevice, stream));
-    HIPCHK(hipMemcpyAsync(ctx->d_sbr_epool.p, ctx->sbr_epool.data(), ctx->sbr_epool.size() * sizeof(float),
-                          hipMemcpyHostToDevice, stream));
-    if (!tabs.empty())
-        HIPCHK(hipMemcpyAsync(ctx->d_sbr_tabs.p, tabs.data(), tabs.size() * sizeof(SbrTab), hipMemcpyHostToDevice, stream));
-    if (!ctx->sbr_chunks.empty())
-        HIPCHK(hipMemcpyAsync(ctx->d_sbr_chunks.p, ctx->sbr_chunks.data(), ctx->sbr_chunks.size() * sizeof(SbrChunk),
-                              hipMemcpyHostToDevice, stream));
-    if (!ctx->sbr_last.empty())
-        HIPCHK(hipMemcpyAsync(ctx->d_sbr_last.p, ctx->sbr_last.data(), ctx->sbr_last.size() * sizeof(uint32_t),
-                              hipMemcpyHostToDevice, stream));
     if (ps) {
-        HIPCHK(ctx->d_psf.ensure(nf * sizeof(jaad_ps_frame) + 256));
         HIPCHK(ctx->d_xps.ensure(nf * 8192 * sizeof(float) + 256));
         HIPCHK(ctx->d_xhl.ensure(nf * 768 * sizeof(float) + 256));
         HIPCHK(ctx->d_xhr.ensure(nf * 768 * sizeof(float) + 256));
         HIPCHK(ctx->d_pg.ensure(nf * 640 * sizeof(float) + 256));
         HIPCHK(ctx->d_hb.ensure(nf * 5 * 22 * 16 * sizeof(float) + 256));
-        HIPCHK(ctx->d_ps_runs.ensure(ctx->ps_runs.size() * sizeof(uint32_t) + 256));
-        if (nf)
-            HIPCHK(hipMemcpyAsync(ctx->d_psf.p, ctx->psf.data(), nf * sizeof(jaad_ps_frame), hipMemcpyHostToDevice, stream));
-        if (!ctx->ps_runs.empty())
-            HIPCHK(hipMemcpyAsync(ctx->d_ps_runs.p, ctx->ps_runs.data(), ctx->ps_runs.size() * sizeof(uint32_t),
-                                  hipMemcpyHostToDevice, stream));
     }
+    HIPCHK(S.d1.ensure(n1 + 256));
+    HIPCHK(S.d2.ensure(n2 + 256));
+    if (S.live) HIPCHK(hipStreamWaitEvent(ctx->cstream, S.used, 0));  // kernels of two calls ago
+    HIPCHK(hipMemcpyAsync(S.d1.p, h1, n1, hipMemcpyHostToDevice, ctx->cstream));
+    HIPCHK(hipMemcpyAsync(S.d2.p, h2, n2, hipMemcpyHostToDevice, ctx->cstream));
+    HIPCHK(hipEventRecord(S.copied, ctx->cstream));
+    HIPCHK(hipStreamWaitEvent(stream, S.copied, 0));
+    const char* d1 = static_cast<const char*>(S.d1.p);
+    const char* d2 = static_cast<const char*>(S.d2.p);
+
     SbrArgs a{};
     a.time = static_cast<const float*>(ctx->d_time.p);
-    a.recs = static_cast<const SbrRec*>(ctx->d_sbr_recs.p);
-    a.epool = static_cast<const float*>(ctx->d_sbr_epool.p);
-    a.tabs = static_cast<const SbrTab*>(ctx->d_sbr_tabs.p);
+    a.recs = reinterpret_cast<const SbrRec*>(d1 + o_recs);
+    a.epool = reinterpret_cast<const float*>(d2);
+    a.tabs = reinterpret_cast<const SbrTab*>(d2 + o_tabs);
     a.xlow = static_cast<float*>(ctx->d_xlow.p);
     a.xsyn = static_cast<float*>(ctx->d_xsyn.p);
     a.xcarry = static_cast<float*>(ctx->d_xcarry.p);
     a.gq = static_cast<float*>(ctx->d_gq.p);
-    a.chunks = static_cast<const SbrChunk*>(ctx->d_sbr_chunks.p);
-    a.last_cf = static_cast<const uint32_t*>(ctx->d_sbr_last.p);
+    a.chunks = reinterpret_cast<const SbrChunk*>(d1 + o_chunks);
+    a.last_cf = reinterpret_cast<const uint32_t*>(d1 + o_last);
     a.state = ctx->d_sbr_state;
     a.pcm = pcm;
     a.qmf_c = ctx->d_sbr_const;
@@ -443,7 +500,7 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
     a.dbg = ctx->sbr_dbg;
     if (ps) {
         a.ps = 1;
-        a.psf = static_cast<const jaad_ps_frame*>(ctx->d_psf.p);
+        a.psf = reinterpret_cast<const jaad_ps_frame*>(d1 + o_psf);
         a.psc = ctx->d_ps_const;
         a.pss = ctx->d_ps_state;
         a.xps = static_cast<float*>(ctx->d_xps.p);
@@ -451,10 +508,12 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
         a.xhr = static_cast<float*>(ctx->d_xhr.p);
         a.pg = static_cast<float*>(ctx->d_pg.p);
         a.hb = static_cast<float*>(ctx->d_hb.p);
-        a.runs = static_cast<const uint32_t*>(ctx->d_ps_runs.p);
+        a.runs = reinterpret_cast<const uint32_t*>(d1 + o_runs);
         a.n_runs = (uint32_t)(ctx->ps_runs.size() / 2);
     }
     HIPCHK(launch_sbr(a, stream));
+    HIPCHK(hipEventRecord(S.used, stream));
+    S.live = true;
     return JAAD_OK;
 }
 
@@ -608,6 +667,12 @@ int jaad_ctx_create(const jaad_stream_cfg* cfg, uint32_t n_slots, int device, ja
         }
         ctx->sbr_slots.resize(n_slots);
         for (auto& hs : ctx->sbr_slots) SbrHost::reset_slot(hs);
+        if ((e = hipStreamCreateWithFlags(&ctx->cstream, hipStreamNonBlocking)) != hipSuccess)
+            return bail(e, "hipStreamCreate copy");
+        for (RecSet& r : ctx->rsets) {
+            if ((e = hipEventCreateWithFlags(&r.copied, hipEventDisableTiming)) != hipSuccess) return bail(e, "hipEventCreate");
+            if ((e = hipEventCreateWithFlags(&r.used, hipEventDisableTiming)) != hipSuccess) return bail(e, "hipEventCreate");
+        }
         const size_t sb = (size_t)n_slots * 2 * sizeof(SbrChState);
         if ((e = hipMalloc(&ctx->d_sbr_state, sb)) != hipSuccess) return bail(e, "hipMalloc sbr state");
         if ((e = hipMemset(ctx->d_sbr_state, 0, sb)) != hipSuccess) return bail(e, "hipMemset sbr state");
@@ -653,10 +718,19 @@ void jaad_ctx_destroy(jaad_ctx* ctx)
     if (ctx->d_sbr_const) (void)hipFree(ctx->d_sbr_const);
     if (ctx->d_ps_state) (void)hipFree(ctx->d_ps_state);
     if (ctx->d_ps_const) (void)hipFree(ctx->d_ps_const);
-    for (DevBuf* d : {&ctx->d_time, &ctx->d_sbr_recs, &ctx->d_sbr_epool, &ctx->d_sbr_tabs, &ctx->d_sbr_chunks,
-                      &ctx->d_sbr_last, &ctx->d_xlow, &ctx->d_xsyn, &ctx->d_xcarry, &ctx->d_gq, &ctx->d_psf, &ctx->d_xps,
-                      &ctx->d_xhl, &ctx->d_xhr, &ctx->d_pg, &ctx->d_hb, &ctx->d_ps_runs})
+    if (ctx->cstream) (void)hipStreamSynchronize(ctx->cstream);
+    for (DevBuf* d : {&ctx->d_time, &ctx->d_xlow, &ctx->d_xsyn, &ctx->d_xcarry, &ctx->d_gq, &ctx->d_xps, &ctx->d_xhl,
+                      &ctx->d_xhr, &ctx->d_pg, &ctx->d_hb})
         d->release();
+    for (RecSet& r : ctx->rsets) {
+        r.h1.release();
+        r.h2.release();
+        r.d1.release();
+        r.d2.release();
+        if (r.copied) (void)hipEventDestroy(r.copied);
+        if (r.used) (void)hipEventDestroy(r.used);
+    }
+    if (ctx->cstream) (void)hipStreamDestroy(ctx->cstream);
     ctx->d_chunks.release();
     ctx->d_batch.release();
     ctx->d_pcm.release();
