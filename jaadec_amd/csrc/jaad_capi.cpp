@@ -10,6 +10,11 @@
 
 #include <algorithm>
 #include <memory>
+#include <chrono>
+#include <condition_variable>
+#include <cstdlib>
+#include <functional>
+#include <mutex>
 #include <thread>
 
 #include "jaad_lc.h"
@@ -70,11 +75,75 @@ struct PinnedBuf {
     }
 };
 
+// Persistent host workers for the per-call record build (fn(t) for t < size(); the caller runs
+// t = 0), so a call does not pay thread start-up.
+class WorkerPool {
+public:
+    explicit WorkerPool(int n) : n_(n < 1 ? 1 : n)
+    {
+        for (int t = 1; t < n_; t++) th_.emplace_back([this, t] { loop(t); });
+    }
+    ~WorkerPool()
+    {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& x : th_) x.join();
+    }
+    int size() const { return n_; }
+    void run(const std::function<void(int)>& fn)
+    {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            fn_ = &fn;
+            pending_ = n_ - 1;
+            gen_++;
+        }
+        cv_.notify_all();
+        fn(0);
+        std::unique_lock<std::mutex> lk(mu_);
+        done_.wait(lk, [this] { return pending_ == 0; });
+        fn_ = nullptr;
+    }
+
+private:
+    void loop(int t)
+    {
+        uint64_t seen = 0;
+        for (;;) {
+            const std::function<void(int)>* fn;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+                if (stop_) return;
+                seen = gen_;
+                fn = fn_;
+            }
+            (*fn)(t);
+            {
+                std::lock_guard<std::mutex> g(mu_);
+                if (--pending_ == 0) done_.notify_one();
+            }
+        }
+    }
+    int n_;
+    std::vector<std::thread> th_;
+    std::mutex mu_;
+    std::condition_variable cv_, done_;
+    const std::function<void(int)>* fn_ = nullptr;
+    uint64_t gen_ = 0;
+    int pending_ = 0;
+    bool stop_ = false;
+};
+
 // One call's SBR/PS parameter records: built on the host straight into page-locked staging,
 // copied on the context's copy stream while the previous call's kernels run.  Two sets
 // alternate between calls; `copied` guards the staging, `used` the device copy.
-//   part 1 (sizes known before the build): recs | psf | chunks | last | runs
-//   part 2 (known after it):               epool | tabs
+//   part 1: recs | psf | chunks | last | runs
+//   part 2: one E_orig region per worker (sized for the worst case, only the used prefix is
+//           uploaded) | tabs
 struct RecSet {
     PinnedBuf h1, h2;
     DevBuf d1, d2;
@@ -114,6 +183,7 @@ struct jaad_ctx {
     hipStream_t cstream = nullptr;               // record uploads
     RecSet rsets[2];
     int rset = 0;
+    std::unique_ptr<WorkerPool> workers;
     std::vector<SbrChunk> sbr_chunks;
     std::vector<uint32_t> sbr_last;
     float* sbr_dbg = nullptr;
@@ -363,9 +433,14 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
     const size_t o_runs = al(o_last + ctx->sbr_last.size() * sizeof(uint32_t));
     const size_t n1 = al(o_runs + ctx->ps_runs.size() * sizeof(uint32_t));
 
+    // JAAD_TRACE_HOST=1: per-call host timings of this stage on stderr (tuning aid)
+    static const bool trace = std::getenv("JAAD_TRACE_HOST") != nullptr;
+    using clk = std::chrono::steady_clock;
+    const auto t_start = clk::now();
     RecSet& S = ctx->rsets[ctx->rset];
     ctx->rset ^= 1;
     if (S.live) HIPCHK(hipEventSynchronize(S.copied));  // its staging may be rewritten
+    const auto t_synced = clk::now();
     HIPCHK(S.h1.ensure(n1));
     char* h1 = static_cast<char*>(S.h1.p);
     SbrRec* recs = reinterpret_cast<SbrRec*>(h1 + o_recs);
@@ -377,27 +452,37 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
     if (!ctx->ps_runs.empty())
         std::memcpy(h1 + o_runs, ctx->ps_runs.data(), ctx->ps_runs.size() * sizeof(uint32_t));
 
-    // parameter records: runs are independent streams, so they are built in parallel (each
-    // worker owns a contiguous block of runs and its own E_orig pool, rebased afterwards)
-    unsigned hw = std::thread::hardware_concurrency();
-    int nt = (int)std::min<uint32_t>(b->n_runs, std::min(16u, hw ? hw : 1u));
+    // parameter records: runs are independent streams, so they are built in parallel; each
+    // worker owns a contiguous block of runs and writes its E_orig values into its own region
+    int nt = ctx->workers ? ctx->workers->size() : 1;
     if (nf < 2048) nt = 1;
-    nt = nt < 1 ? 1 : nt;
-    std::vector<std::vector<float>> pools(nt);
+    if ((uint32_t)nt > b->n_runs) nt = b->n_runs ? (int)b->n_runs : 1;
+    std::vector<uint32_t> rr(nt + 1);
+    for (int t = 0; t <= nt; t++) rr[t] = (uint32_t)((uint64_t)b->n_runs * t / nt);
+    std::vector<size_t> rbase(nt + 1, 0);  // region offsets in floats
+    for (int t = 0; t < nt; t++)
+        rbase[t + 1] = rbase[t] + ((size_t)(b->frame_begin[rr[t + 1]] - b->frame_begin[rr[t]]) * nch *
+                                       SbrHost::kMaxEorig + 63) / 64 * 64;
+    const auto& tabs = ctx->sbr_host->tabs();
+    const size_t o_tabs = al(rbase[nt] * sizeof(float) + sizeof(float));
+    const size_t n2 = o_tabs + SbrHost::kMaxTables * sizeof(SbrTab);
+    HIPCHK(S.h2.ensure(n2));
+    char* h2 = static_cast<char*>(S.h2.p);
     std::vector<int> rcs(nt, 0), bad(nt, -1);
-    std::vector<size_t> pbase(nt + 1, 0);
+    std::vector<uint32_t> used(nt, 0);
     std::vector<char> smooth(nt, 0);
-    auto run_range = [&](int t, uint32_t& r0, uint32_t& r1) {
-        r0 = (uint32_t)((uint64_t)b->n_runs * t / nt);
-        r1 = (uint32_t)((uint64_t)b->n_runs * (t + 1) / nt);
-    };
-    auto work = [&](int t) {
-        uint32_t r0, r1;
-        run_range(t, r0, r1);
-        pools[t].reserve((size_t)(b->frame_begin[r1] - b->frame_begin[r0]) * nch * 40);
-        for (uint32_t r = r0; r < r1 && !rcs[t]; r++) {
+    std::function<void(int)> work = [&](int t) {
+        if (t >= nt) return;  // the pool may be wider than this call's run blocks
+        float* region = reinterpret_cast<float*>(h2) + rbase[t];
+        uint32_t epos = 0;
+        bool sm = false;
+        for (uint32_t r = rr[t]; r < rr[t + 1] && !rcs[t]; r++) {
             SbrHostSlot& hs = ctx->sbr_slots[b->stream_slot[r]];
-            for (uint32_t f = b->frame_begin[r]; f < b->frame_begin[r + 1]; f++) {
+            const uint32_t fe = b->frame_begin[r + 1];
+            for (uint32_t f = b->frame_begin[r]; f < fe; f++) {
+                if (f + 2 < fe)  // the records are large and sparse-read: pull frame f+2 in early
+                    for (size_t o = 0; o < sizeof(jaad_sbr_frame); o += 64)
+                        __builtin_prefetch(reinterpret_cast<const char*>(&b->sbr[f + 2]) + o);
                 if (ps) {
                     if (!ps_frame_ok(b->sbr[f])) {
                         rcs[t] = b->sbr[f].ps_present ? JAAD_ERR_BITSTREAM : JAAD_ERR_UNSUPPORTED;
@@ -406,52 +491,33 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
                     }
                     psf[f] = b->sbr[f].ps;
                 }
-                int rc = ctx->sbr_host->frame(hs, b->sbr[f], nch, f == b->frame_begin[r], b->stream_slot[r],
-                                              &recs[(size_t)f * nch], pools[t]);
+                SbrRec* rec = &recs[(size_t)f * nch];
+                int rc = ctx->sbr_host->frame(hs, b->sbr[f], nch, f == b->frame_begin[r], b->stream_slot[r], rec,
+                                              region, epos, (uint32_t)rbase[t]);
                 if (rc) {
                     rcs[t] = rc;
                     bad[t] = (int)f;
                     break;
                 }
+                sm |= (rec[0].flags & kSbrSmooth) != 0;
             }
         }
+        used[t] = epos;
+        smooth[t] = sm;
     };
-    auto parallel = [&](auto&& fn) {
-        std::vector<std::thread> th;
-        for (int t = 1; t < nt; t++) th.emplace_back(fn, t);
-        fn(0);
-        for (auto& x : th) x.join();
-    };
-    parallel(work);
+    if (nt > 1) ctx->workers->run(work);
+    else work(0);
+    const auto t_built = clk::now();
+    bool smoothing = false;
     for (int t = 0; t < nt; t++) {
         if (rcs[t]) {
             ctx->err = (ps ? "SBR/PS side info of frame " : "SBR side info of frame ") + std::to_string(bad[t]);
             return rcs[t];
         }
-        pbase[t + 1] = pbase[t] + pools[t].size();
+        smoothing |= smooth[t] != 0;
     }
-    const size_t n_epool = pbase[nt] ? pbase[nt] : 1;
-    const auto& tabs = ctx->sbr_host->tabs();
-    const size_t o_tabs = al(n_epool * sizeof(float));
-    const size_t n2 = o_tabs + (tabs.size() + 1) * sizeof(SbrTab);
-    HIPCHK(S.h2.ensure(n2));
-    char* h2 = static_cast<char*>(S.h2.p);
-    // second pass: rebase e_off, move each pool into the staging, find smoothing frames
-    parallel([&](int t) {
-        uint32_t r0, r1;
-        run_range(t, r0, r1);
-        bool sm = false;
-        for (size_t i = (size_t)b->frame_begin[r0] * nch; i < (size_t)b->frame_begin[r1] * nch; i++) {
-            recs[i].e_off += (uint32_t)pbase[t];
-            sm |= (recs[i].flags & kSbrSmooth) != 0;
-        }
-        smooth[t] = sm;
-        if (!pools[t].empty())
-            std::memcpy(h2 + pbase[t] * sizeof(float), pools[t].data(), pools[t].size() * sizeof(float));
-    });
-    bool smoothing = false;
-    for (int t = 0; t < nt; t++) smoothing |= smooth[t] != 0;
     if (!tabs.empty()) std::memcpy(h2 + o_tabs, tabs.data(), tabs.size() * sizeof(SbrTab));
+    const auto t_packed = clk::now();
 
     // device side: intermediates (stream-ordered) and this set's record copy (copy stream)
     HIPCHK(ctx->d_xlow.ensure(ncf * 2048 * sizeof(float) + 256));
@@ -469,7 +535,13 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
     HIPCHK(S.d2.ensure(n2 + 256));
     if (S.live) HIPCHK(hipStreamWaitEvent(ctx->cstream, S.used, 0));  // kernels of two calls ago
     HIPCHK(hipMemcpyAsync(S.d1.p, h1, n1, hipMemcpyHostToDevice, ctx->cstream));
-    HIPCHK(hipMemcpyAsync(S.d2.p, h2, n2, hipMemcpyHostToDevice, ctx->cstream));
+    for (int t = 0; t < nt; t++)
+        if (used[t])
+            HIPCHK(hipMemcpyAsync(static_cast<char*>(S.d2.p) + rbase[t] * sizeof(float), h2 + rbase[t] * sizeof(float),
+                                  used[t] * sizeof(float), hipMemcpyHostToDevice, ctx->cstream));
+    if (!tabs.empty())
+        HIPCHK(hipMemcpyAsync(static_cast<char*>(S.d2.p) + o_tabs, h2 + o_tabs, tabs.size() * sizeof(SbrTab),
+                              hipMemcpyHostToDevice, ctx->cstream));
     HIPCHK(hipEventRecord(S.copied, ctx->cstream));
     HIPCHK(hipStreamWaitEvent(stream, S.copied, 0));
     const char* d1 = static_cast<const char*>(S.d1.p);
@@ -514,6 +586,14 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
     HIPCHK(launch_sbr(a, stream));
     HIPCHK(hipEventRecord(S.used, stream));
     S.live = true;
+    if (trace) {
+        auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+        size_t eu = 0;
+        for (int t = 0; t < nt; t++) eu += used[t];
+        std::fprintf(stderr, "jaad sbr host: wait %.3f build %.3f pack %.3f enqueue %.3f ms (threads %d, %zu+%zu B)\n",
+                     ms(t_start, t_synced), ms(t_synced, t_built), ms(t_built, t_packed), ms(t_packed, clk::now()), nt,
+                     n1, eu * sizeof(float));
+    }
     return JAAD_OK;
 }
 
@@ -669,6 +749,11 @@ int jaad_ctx_create(const jaad_stream_cfg* cfg, uint32_t n_slots, int device, ja
         for (auto& hs : ctx->sbr_slots) SbrHost::reset_slot(hs);
         if ((e = hipStreamCreateWithFlags(&ctx->cstream, hipStreamNonBlocking)) != hipSuccess)
             return bail(e, "hipStreamCreate copy");
+        {
+            const unsigned hw = std::thread::hardware_concurrency();
+            const int nw = (int)std::min(16u, hw ? hw : 1u);  // the box's CPU share per GPU
+            ctx->workers.reset(new (std::nothrow) WorkerPool(nw));
+        }
         for (RecSet& r : ctx->rsets) {
             if ((e = hipEventCreateWithFlags(&r.copied, hipEventDisableTiming)) != hipSuccess) return bail(e, "hipEventCreate");
             if ((e = hipEventCreateWithFlags(&r.used, hipEventDisableTiming)) != hipSuccess) return bail(e, "hipEventCreate");

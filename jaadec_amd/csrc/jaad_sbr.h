@@ -166,7 +166,7 @@ hipError_t launch_ps(const SbrArgs& a, hipStream_t stream);  // jaad_ps.hip, cal
 struct SbrHostCh {
     float bwArray_prev[64];
     int invf_prev[5];
-    int add_harmonic_prev[64];
+    uint64_t add_harmonic_prev;  // bit n = bs_add_harmonic_prev[n] (n < 49)
     int add_harmonic_flag_prev;
     int prevEnvIsShort;
     int index_noise_prev, psi_is_prev;
@@ -203,9 +203,12 @@ public:
     }
     static void reset_slot(SbrHostSlot& s);
     // Build the records of one frame of one stream (both channels) in stream order.
-    // Returns 0 or a jaad_status; appends E_orig values to epool.  Thread-safe across slots.
+    // Returns 0 or a jaad_status; writes the E_orig values at epool[epos..] (epos advances; the
+    // record's e_off is e_base + epos) -- room for kMaxEorig floats per channel is the caller's.
+    // Thread-safe across slots.
+    static constexpr int kMaxEorig = 5 * 49;
     int frame(SbrHostSlot& st, const jaad_sbr_frame& fr, int nch, bool first, uint32_t slot, SbrRec* rec_out,
-              std::vector<float>& epool);
+              float* epool, uint32_t& epos, uint32_t e_base);
     const std::vector<SbrTab>& tabs() const { return tabs_; }
     // table index for a header (built on first use); -1 if its tables are invalid
     int table_index(const jaad_sbr_header& h) { return table_for(h); }

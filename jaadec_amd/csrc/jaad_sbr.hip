@@ -248,6 +248,10 @@ template <int kPhase>
 __global__ __launch_bounds__(256) void sbr_hf_kernel(SbrArgs A)
 {
     __shared__ HfLds Ls[kWavesPerBlock];
+    __shared__ float2 noise_s[512];  // NoiseTable.NOISE_TABLE (A/sbr/NoiseTable.java:6), read per slot
+    for (int i = threadIdx.x; i < 512; i += blockDim.x)
+        noise_s[i] = reinterpret_cast<const float2*>(A.noise)[i];
+    __syncthreads();
     const int wave = threadIdx.x >> 6;
     const uint32_t cf = blockIdx.x * kWavesPerBlock + wave;
     if (cf >= A.n_cf) return;
@@ -301,6 +305,7 @@ __global__ __launch_bounds__(256) void sbr_hf_kernel(SbrArgs A)
 
     // ---------- HF generation (A/sbr/HFGeneration.java:17-98, 100-196) ----------
     float a0r = 0, a0i = 0, a1r = 0, a1i = 0;
+#ifndef JAAD_HF_SKIP_GEN
     {
         float r01r = 0, r01i = 0, r02r = 0, r02i = 0, r11r = 0;
         float t1r, t1i, t2r = xr[0], t2i = xi[0], t3r = xr[1], t3i = xi[1];
@@ -344,9 +349,17 @@ __global__ __launch_bounds__(256) void sbr_hf_kernel(SbrArgs A)
         const float A0r = shfl(a0r, ps) * bw, A1r = shfl(a1r, ps) * bw2;
         const float A0i = shfl(a0i, ps) * bw, A1i = shfl(a1i, ps) * bw2;
         float p1r = 0, p1i = 0, p2r = 0, p2i = 0;  // source rows r-2, r-1
+        float sbr_[8], sbi_[8];  // source rows, fetched 8 at a time
 #pragma unroll
         for (int r = 0; r < 40; r++) {
-            const float sr = shfl(xr[r], ps), si = shfl(xi[r], ps);
+            if ((r & 7) == 0) {
+#pragma unroll
+                for (int q = 0; q < 8; q++) {
+                    sbr_[q] = shfl(xr[r + q], ps);
+                    sbi_[q] = shfl(xi[r + q], ps);
+                }
+            }
+            const float sr = sbr_[r & 7], si = sbi_[r & 7];
             const int l = r - 2;
             if (gen && l >= first && l < last) {
                 if (bw2 > 0.0f) {
@@ -361,15 +374,20 @@ __global__ __launch_bounds__(256) void sbr_hf_kernel(SbrArgs A)
             p1i = p2i;
             p2r = sr;
             p2i = si;
-            __builtin_amdgcn_sched_barrier(0);
+            if ((r & 7) == 7) __builtin_amdgcn_sched_barrier(0);
         }
     }
+#endif
 
     // ---------- HF adjustment (A/sbr/HFAdjustment.java) ----------
     const int m = u - kx;
     const bool band = m >= 0 && m < M;
     // estimate_current_envelope (:82-138)
+#ifdef JAAD_HF_SKIP_EST
+    if (false) {
+#else
     if (R.flags & kSbrInterpol) {
+#endif
         float acc[5] = {0, 0, 0, 0, 0};
 #pragma unroll
         for (int r = 2; r < 40; r++) {
@@ -431,6 +449,7 @@ __global__ __launch_bounds__(256) void sbr_hf_kernel(SbrArgs A)
     // calculate_gain (:240-415).  Per envelope: (1) lanes m evaluate everything that does not
     // depend on the limiter (Q_M, S_M, the unlimited G) into LDS; (2) one lane per limiter
     // band walks its bands in order (acc1/acc2, G_max, limiting, den, G_boost) from LDS.
+#ifndef JAAD_HF_SKIP_GAIN
     {
         const int NL = T.N_L[s_lim];
         const float EPS = 1e-12f;
@@ -495,6 +514,7 @@ __global__ __launch_bounds__(256) void sbr_hf_kernel(SbrArgs A)
             wave_sync();
         }
     }
+#endif
 
     // G/Q ring after this frame: the last 5 assembled rows (rows >= 26 always, see the host check)
     {
@@ -513,6 +533,7 @@ __global__ __launch_bounds__(256) void sbr_hf_kernel(SbrArgs A)
     if (kPhase == 1) return;
 
     // hf_assembly (:140-238): lane k = m + kx
+#ifndef JAAD_HF_SKIP_ASM
     {
         const int mi = band ? m : 0;
         const bool smooth = (R.flags & kSbrSmooth) != 0;
@@ -525,7 +546,6 @@ __global__ __launch_bounds__(256) void sbr_hf_kernel(SbrArgs A)
             }
             gidx = 4;
         }
-        const float* noise = A.noise;
         const float rev = (u & 1) ? -1.0f : 1.0f;
 #pragma unroll
         for (int r = 2; r < 40; r++) {
@@ -570,7 +590,8 @@ __global__ __launch_bounds__(256) void sbr_hf_kernel(SbrArgs A)
             const int fi = (int)((R.noise0 + (uint32_t)(i - first) * (uint32_t)M + (uint32_t)mi + 1u) & 511u);
             const int fs = (int)((R.sine0 + (uint32_t)(i - first)) & 3u);
             if (band) {
-                const float nr = noise[2 * fi], ni = noise[2 * fi + 1];
+                const float2 nz = noise_s[fi];
+                const float nr = nz.x, ni = nz.y;
                 float vr = G_filt * xr[r] + (Q_filt * nr);
                 float vi = G_filt * xi[r] + (Q_filt * ni);
                 const float phr = fs == 0 ? 1.0f : fs == 2 ? -1.0f : 0.0f;
@@ -584,6 +605,7 @@ __global__ __launch_bounds__(256) void sbr_hf_kernel(SbrArgs A)
             __builtin_amdgcn_sched_barrier(0);
         }
     }
+#endif
 
 
     // ---------- outputs ----------

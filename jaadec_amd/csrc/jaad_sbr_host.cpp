@@ -331,7 +331,7 @@ int SbrHost::table_for(const jaad_sbr_header& h)
 }
 
 int SbrHost::frame(SbrHostSlot& st, const jaad_sbr_frame& fr, int nch, bool first, uint32_t slot, SbrRec* rec,
-                   std::vector<float>& epool)
+                   float* epool, uint32_t& epos, uint32_t e_base)
 {
     bool reset = false;
     if (fr.header_present) {
@@ -405,18 +405,23 @@ int SbrHost::frame(SbrHostSlot& st, const jaad_sbr_frame& fr, int nch, bool firs
         // dequantisation (NoiseEnvelope.dequantChannel, no coupling)
         const bool amp_res = !(L_E == 1 && in.frame_class == FIXFIX) && h.amp_res;
         const int amp = amp_res ? 0 : 1;
-        r.e_off = (uint32_t)epool.size();
-        for (int l = 0; l < L_E; l++)
-            for (int k = 0; k < t.n[in.f[l]]; k++) {
-                const int E = in.E[l][k];
+        r.e_off = e_base + epos;
+        for (int l = 0; l < L_E; l++) {
+            const int nb = t.n[in.f[l]];
+            const int16_t* Er = in.E[l];
+            float* out = epool + epos;
+            for (int k = 0; k < nb; k++) {
+                const int E = Er[k];
                 const int e = E >> amp;
                 float v = 0.0f;
                 if (e >= 0 && e < 64) {
                     v = JAAD_SBR_E_DEQ[e];
                     if (amp != 0 && (E & 1) != 0) v = v * 1.414213562f;
                 }
-                epool.push_back(v);
+                out[k] = v;
             }
+            epos += (uint32_t)nb;
+        }
         for (int l = 0; l < L_Q; l++)
             for (int k = 0; k < t.N_Q; k++) {
                 const int q = in.Q[l][k];
@@ -426,20 +431,19 @@ int SbrHost::frame(SbrHostSlot& st, const jaad_sbr_frame& fr, int nch, bool firs
             }
 
         // sinusoids: bs_add_harmonic cleared, then N_high flags (SBR2.java:63-72, SBR.java:249-254)
-        int harm[64];
         const uint64_t hmask = t.N_high >= 64 ? ~0ull : ((1ull << t.N_high) - 1);
-        const bool any_harm = in.add_harmonic_flag && (in.add_harmonic & hmask);
-        for (int n = 0; n < 64; n++)
-            harm[n] = (in.add_harmonic_flag && n < t.N_high) ? (int)((in.add_harmonic >> n) & 1u) : 0;
+        const uint64_t harm = in.add_harmonic_flag ? (in.add_harmonic & hmask) : 0;  // bit n = bs_add_harmonic[n]
+        const bool any_harm = harm != 0;
+        auto hbit = [](uint64_t m, int b) { return b >= 0 && b < 64 ? (int)((m >> b) & 1u) : 0; };
         auto s_mapped = [&](int l, int band) {  // get_S_mapped (HFAdjustment.java:46-80)
             if (in.f[l] == HI_RES) {
-                if (l >= l_A || (ch.add_harmonic_prev[band] != 0 && ch.add_harmonic_flag_prev)) return harm[band];
+                if (l >= l_A || (hbit(ch.add_harmonic_prev, band) && ch.add_harmonic_flag_prev)) return hbit(harm, band);
                 return 0;
             }
             const int odd = (t.N_high & 1) ? 1 : 0;
             for (int b = 2 * band - odd; b < 2 * (band + 1) - odd; b++)
-                if (l >= l_A || (ch.add_harmonic_prev[b] != 0 && ch.add_harmonic_flag_prev))
-                    if (harm[b] == 1) return 1;
+                if (l >= l_A || (hbit(ch.add_harmonic_prev, b) && ch.add_harmonic_flag_prev))
+                    if (hbit(harm, b)) return 1;
             return 0;
         };
         for (int l = 0; l < L_E && any_harm; l++) {  // no sinusoid flag set: both masks are 0
@@ -447,8 +451,8 @@ int SbrHost::frame(SbrHostSlot& st, const jaad_sbr_frame& fr, int nch, bool firs
             for (int m = 0; m < t.M && m < 64; m++) {
                 if (!t.visited[s_lim][m]) continue;
                 const int hb = t.hi_map[s_lim][m];
-                if (l >= l_A || (ch.add_harmonic_prev[hb] != 0 && ch.add_harmonic_flag_prev))
-                    if (m + t.kx == (t.f_table_res[HI_RES][hb + 1] + t.f_table_res[HI_RES][hb]) >> 1 && harm[hb])
+                if (l >= l_A || (hbit(ch.add_harmonic_prev, hb) && ch.add_harmonic_flag_prev))
+                    if (m + t.kx == (t.f_table_res[HI_RES][hb + 1] + t.f_table_res[HI_RES][hb]) >> 1 && hbit(harm, hb))
                         mi |= 1ull << m;
                 if (s_mapped(l, t.res_map[s_lim][in.f[l]][m])) mm |= 1ull << m;
             }
@@ -469,7 +473,7 @@ int SbrHost::frame(SbrHostSlot& st, const jaad_sbr_frame& fr, int nch, bool firs
         ch.gq_index = (gq0 + rows) % 5;
 
         // sbr_save_prev_data (SBR.java:256-284)
-        for (int i = 0; i < 49; i++) ch.add_harmonic_prev[i] = harm[i];
+        ch.add_harmonic_prev = harm & ((1ull << 49) - 1);
         ch.add_harmonic_flag_prev = in.add_harmonic_flag;
         ch.prevEnvIsShort = (l_A == L_E) ? 0 : -1;
     }

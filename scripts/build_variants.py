@@ -8,13 +8,11 @@ from jaadec_amd import build as B  # noqa: E402
 
 VARIANTS = {
     "a_base": [],
-    "b_no_iq": ["JAAD_ABL_NO_IQ"],
-    "c_no_ms": ["JAAD_ABL_NO_MS"],
-    "d_no_imdct": ["JAAD_ABL_NO_IMDCT"],
-    "e_no_pcmlds": ["JAAD_ABL_NO_PCMLDS"],
-    "f_no_store": ["JAAD_ABL_NO_STORE"],
-    "g_no_barrier": ["JAAD_ABL_NO_BARRIER"],
-    "h_w2": ["JAAD_WAVES_PER_EU=2"],
+    "b_hf_no_gen": ["JAAD_HF_SKIP_GEN"],
+    "c_hf_no_est": ["JAAD_HF_SKIP_EST"],
+    "d_hf_no_gain": ["JAAD_HF_SKIP_GAIN"],
+    "e_hf_no_asm": ["JAAD_HF_SKIP_ASM"],
+    "f_hf_none": ["JAAD_HF_SKIP_GEN", "JAAD_HF_SKIP_EST", "JAAD_HF_SKIP_GAIN", "JAAD_HF_SKIP_ASM"],
 }
 
 if __name__ == "__main__":
