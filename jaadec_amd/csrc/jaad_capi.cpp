@@ -2,6 +2,7 @@
 // host/device batch entry points.  Host code only; kernels live in jaad_lc.hip.
 #include <hip/hip_runtime.h>
 
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <new>
@@ -170,7 +171,8 @@ struct jaad_ctx {
     std::vector<uint8_t> slot_used;
     bool plan_valid = false;
     int n_cu = 256;
-    uint32_t chunk_frames = kDefaultChunkFrames;
+    uint32_t lc_waves = 0;       // LC kernel waves resident on the whole device (one per chunk)
+    uint32_t chunk_frames = 0;   // 0 = size chunks from lc_waves; JAAD_CHUNK_FRAMES overrides
     float* dbg = nullptr;
     int dbg_frame = 0;
     std::string err;
@@ -297,6 +299,15 @@ int plan(jaad_ctx* ctx, const jaad_batch* b)
     if (same) return JAAD_OK;
     ctx->chunks.clear();
     std::fill(ctx->slot_used.begin(), ctx->slot_used.end(), 0);
+    // One wave decodes one chunk; a chunk that does not start its run re-decodes one frame.
+    // Chunk length L is chosen so that the chunks fill the device's resident waves about once
+    // (balanced, no tail round), but never shorter than kMinChunkFrames (prefix overhead).
+    uint32_t L = ctx->chunk_frames;
+    if (!L) {
+        const uint64_t cap = ctx->lc_waves ? ctx->lc_waves : 4096;
+        L = (uint32_t)std::max<uint64_t>(kMinChunkFrames, (b->n_frames + cap - 1) / cap);
+    }
+    L = std::min<uint32_t>(L, 0xffff);
     for (uint32_t r = 0; r < b->n_runs; r++) {
         uint32_t f0 = b->frame_begin[r], f1 = b->frame_begin[r + 1];
         uint32_t slot = b->stream_slot[r];
@@ -308,11 +319,14 @@ int plan(jaad_ctx* ctx, const jaad_batch* b)
             ctx->chunks.push_back(cd);
             continue;
         }
-        for (uint32_t f = f0; f < f1; f += ctx->chunk_frames) {
-            uint32_t n = f1 - f < ctx->chunk_frames ? f1 - f : ctx->chunk_frames;
-            uint32_t info = n;
+        // split the run into `parts` chunks of equal length (+-1 frame)
+        const uint32_t len = f1 - f0, parts = (len + L - 1) / L;
+        for (uint32_t i = 0; i < parts; i++) {
+            const uint32_t f = f0 + (uint32_t)((uint64_t)len * i / parts);
+            const uint32_t fe = f0 + (uint32_t)((uint64_t)len * (i + 1) / parts);
+            uint32_t info = fe - f;
             info |= (f == f0) ? kChunkLoadState : kChunkPrefix;
-            if (f + n == f1) info |= kChunkStoreState;
+            if (fe == f1) info |= kChunkStoreState;
             ctx->chunks.push_back(ChunkDesc{f, info, slot, 0});
         }
     }
@@ -626,10 +640,8 @@ int launch(jaad_ctx* ctx, const jaad_batch* db, void* pcm, uint32_t flags, hipSt
     if (a.n_chunks == 0) return JAAD_OK;
     rc = carry_untouched(ctx, a.state_out, a.state_in, 2048, stream);
     if (rc) return rc;
-    const int per_wg = ctx->nch == 2 ? kWavesPerWG / 2 : kWavesPerWG;
-    int grid = (int)((a.n_chunks + per_wg - 1) / per_wg);
     const bool tns_spec = ctx->cfg.tns_mode == JAAD_TNS_SPEC && db->tns != nullptr;
-    HIPCHK(launch_lc(a, grid, stream, tns_spec));
+    HIPCHK(launch_lc(a, stream, tns_spec));
     if (sbr && (rc = launch_sbr_stage(ctx, db, pcm, flags, stream))) return rc;
     ctx->parity ^= 1;
     return JAAD_OK;
@@ -710,6 +722,7 @@ int jaad_ctx_create(const jaad_stream_cfg* cfg, uint32_t n_slots, int device, ja
     ctx->n_slots = n_slots;
     ctx->n_cu = prop.multiProcessorCount;
     ctx->slot_used.assign(n_slots, 0);
+    if (const char* ev = std::getenv("JAAD_CHUNK_FRAMES")) ctx->chunk_frames = (uint32_t)std::atoi(ev);
     auto bail = [&](hipError_t e, const char* what) {
         std::fprintf(stderr, "jaad_ctx_create: %s: %s\n", what, hipGetErrorString(e));
         jaad_ctx_destroy(ctx);
@@ -730,6 +743,7 @@ int jaad_ctx_create(const jaad_stream_cfg* cfg, uint32_t n_slots, int device, ja
         return JAAD_ERR_NOMEM;
     }
     build_lds_tables(cfg->sf_index, h, &gt);
+    ctx->lc_waves = (uint32_t)lc_resident_waves_per_cu(cfg->tns_mode == JAAD_TNS_SPEC) * (uint32_t)ctx->n_cu;
     if ((e = hipMalloc(&ctx->d_gtab, sizeof(GlobalTables))) != hipSuccess) { delete h; return bail(e, "hipMalloc gtab"); }
     if ((e = hipMemcpy(ctx->d_gtab, &gt, sizeof(GlobalTables), hipMemcpyHostToDevice)) != hipSuccess) { delete h; return bail(e, "hipMemcpy gtab"); }
     if ((e = hipMalloc(&ctx->d_tables, sizeof(LdsTables))) != hipSuccess) { delete h; return bail(e, "hipMalloc tables"); }
@@ -947,6 +961,12 @@ int jaad_state_import(jaad_ctx* ctx, uint32_t slot, const void* buf, size_t byte
     HIPCHK(hipSetDevice(ctx->device));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     const char* in = static_cast<const char*>(buf);
+    {  // the overlap must be finite (the LC kernel's PCM rounding relies on it, jaad_lc.hip round_pk16)
+        float ov[2048];
+        std::memcpy(ov, in, sizeof ov);
+        for (float v : ov)
+            if (!std::isfinite(v)) return JAAD_ERR_INVALID_ARG;
+    }
     HIPCHK(hipMemcpy(ctx->d_state[ctx->parity] + (size_t)slot * 2048, in, 2048 * sizeof(float), hipMemcpyHostToDevice));
     if (ctx->cfg.sbr) {
         in += 2048 * sizeof(float);

@@ -6,9 +6,7 @@
 
 namespace jaad {
 
-constexpr int kWavesPerWG = 4;
-constexpr int kWGThreads = 64 * kWavesPerWG;
-constexpr int kDefaultChunkFrames = 8;  // frames one wave (pair) decodes back to back
+constexpr int kMinChunkFrames = 8;  // shortest chunk the planner makes (one re-decoded prefix frame per chunk)
 
 // One unit of work = up to N consecutive frames of one run.  A chunk that does not start its
 // run first re-decodes the frame before it to rebuild the IMDCT overlap (the overlap written by
@@ -89,6 +87,9 @@ void build_lds_tables(int sf_index, LdsTables* t, GlobalTables* g);
 namespace jaad {
 constexpr uint32_t kOutPlanarF32 = 4;  // internal output mode: core time samples for the SBR kernel
 
-hipError_t launch_lc(const KernelArgs& a, int grid, hipStream_t stream, bool tns_spec);
+// one wave per chunk (grid derived from a.n_chunks)
+hipError_t launch_lc(const KernelArgs& a, hipStream_t stream, bool tns_spec);
+// LC kernel waves that can be resident on one CU (occupancy query; 0 on failure)
+int lc_resident_waves_per_cu(bool tns_spec);
 }
 #endif

@@ -8,17 +8,21 @@
 //   SampleBuffer.accept PCM packing           S/SampleBuffer.java:168-209
 // in ONE pass over HBM: quantised int16 spectra in, interleaved PCM out.
 //
-// Work decomposition.  A workgroup = 4 waves.  For a CPE stream the two waves of a "pair" each
-// own one channel of a chunk of consecutive frames (mono: every wave its own stream); the pair
-// meets in LDS (4 workgroup barriers per frame) for M/S and I/S and to interleave the PCM.  The
-// 1024-sample IMDCT overlap of a channel stays in its wave's VGPRs between frames (lane u owns
-// output positions {2u+128j} U {1023-2u-128j}); a chunk that does not start its stream
-// re-decodes the previous frame to rebuild it.  All global inputs of frame f+1 are loaded while
-// frame f is computed.  The 512-point complex IFFT of a frame is 8 complex values per lane in
-// three register passes (bit-reversed radix-4 + one radix-2 stage, then 3 + 3 radix-2 stages)
-// with two XOR-swizzled LDS transposes.  Butterflies, twiddles (the reference's float32
-// recurrence tables) and evaluation order are those of the Java code, and the file is compiled
-// with -ffp-contract=off, so the results are bit-exact.
+// Work decomposition.  One wave owns a chunk of consecutive frames of one stream and decodes
+// BOTH channels of a CPE itself: lane u holds bins 8u+512h+i (h = 0,1; i = 0..7) of the left
+// and the right spectrum in registers, so M/S and I/S are plain register arithmetic and the
+// interleaved PCM is assembled in the wave's own LDS area.  Waves never wait for each other
+// inside the frame loop (no workgroup barrier after the table prologue), so the VALU, LDS and
+// memory phases of the 16 waves of a CU drift apart and overlap.  The 1024-sample IMDCT
+// overlap of each channel stays in VGPRs between frames (lane u owns output positions
+// {2u+128j} U {1023-2u-128j}); a chunk that does not start its stream re-decodes the previous
+// frame to rebuild it.  Frame f+1's inputs are loaded while frame f's two IMDCTs run.
+//
+// The 512-point complex IFFT of a frame is 8 complex values per lane in three register passes
+// (bit-reversed radix-4 + one radix-2 stage, then 3 + 3 radix-2 stages) with two padded LDS
+// transposes.  Butterflies, twiddles (the reference's float32 recurrence tables) and
+// evaluation order are those of the Java code and the file is compiled with
+// -ffp-contract=off, so the results are bit-exact.
 #include <hip/hip_runtime.h>
 
 #include "jaad_lc.h"
@@ -29,16 +33,6 @@
 
 namespace jaad {
 
-// per pair (CPE) or per two mono streams: band side info, written by the owning wave
-struct alignas(16) PairBands {
-    float gain[2][128];     // +-SCALEFACTOR_TABLE[...] as ICStream.scaleFactors holds it
-    uint8_t sf[2][128];     // raw scalefactor-table index - 100
-    uint8_t cb[2][128];     // section codebook (sfbCB)
-    uint8_t ms[128];        // ms_used bit per band (CPE, written by the left-channel wave)
-};
-
-// Lane id through a volatile asm: keeps the compiler from hoisting every lane-dependent LDS
-// address out of the frame loop (which otherwise costs >100 VGPRs and all occupancy).
 __device__ __forceinline__ int lane_id()
 {
 #ifndef JAAD_HOISTABLE_LANE
@@ -50,25 +44,6 @@ __device__ __forceinline__ int lane_id()
     __builtin_assume(v >= 0 && v < 64);
     return v;
 }
-
-#ifdef JAAD_STAMPS
-__device__ __forceinline__ uint32_t stamp()
-{
-    uint64_t t;
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-    return (uint32_t)t;
-}
-#define STAMP(k)                                                                                     \
-    do {                                                                                             \
-        uint32_t t_ = stamp();                                                                       \
-        if (A.dbg && lane_id() == 0 && (k) < 32)                                                     \
-            reinterpret_cast<uint32_t*>(A.dbg)[(size_t)(blockIdx.x * kWavesPerWG + wave) * 32 + (k)] = t_; \
-    } while (0)
-#else
-#define STAMP(k) \
-    do {         \
-    } while (0)
-#endif
 
 __device__ __forceinline__ void wave_sync()
 {
@@ -169,33 +144,20 @@ __device__ __forceinline__ int long_pos(int u, int o)
     return h ? 1535 - 2 * k : 2 * k - 512;
 }
 
-// Math.round(float) (ties toward +inf, NaN -> 0) then the short clamp of SampleBuffer.accept
-// (S/SampleBuffer.java:193-206).  floor/sub/compare are exact; v_cvt_i32_f32 maps NaN to 0
-// and saturates out-of-range values.
-__device__ __forceinline__ int java_round16(float x)
-{
-    float y = __builtin_floorf(x);
-    float r = (x - y >= 0.5f) ? y + 1.0f : y;
-    int v;
-    asm("v_cvt_i32_f32 %0, %1" : "=v"(v) : "v"(r));
-    return v < -32768 ? -32768 : (v > 32767 ? 32767 : v);
-}
-
 struct FrameCtx {
     int seq, shape, shape_prev;
 };
 
-// jaad_ics_info unpacked into wave-uniform scalars (kept in SGPRs; a struct of bytes selected
-// at run time would be spilled to scratch)
+// jaad_ics_info unpacked into wave-uniform scalars
 struct Ics {
     int seq, shape, shape_prev, max_sfb, grouping, flags;
     uint32_t pns;
+    int nbands;  // number of (group, sfb) bands = groups * max_sfb
 };
-__device__ __forceinline__ Ics load_ics(const jaad_ics_info* p)
+__device__ __forceinline__ Ics ics_from_lanes(uint32_t side, int base)
 {
-    const uint32_t* w = reinterpret_cast<const uint32_t*>(p);
-    const uint32_t a = __builtin_amdgcn_readfirstlane(w[0]);
-    const uint32_t b = __builtin_amdgcn_readfirstlane(w[1]);
+    const uint32_t a = __builtin_amdgcn_readlane(side, base);
+    const uint32_t b = __builtin_amdgcn_readlane(side, base + 1);
     Ics r;
     r.seq = a & 0xff;
     r.shape = (a >> 8) & 0xff;
@@ -203,19 +165,9 @@ __device__ __forceinline__ Ics load_ics(const jaad_ics_info* p)
     r.max_sfb = a >> 24;
     r.grouping = b & 0xff;
     r.flags = (b >> 8) & 0xff;
-    r.pns = __builtin_amdgcn_readfirstlane(w[2]);
-    return r;
-}
-__device__ __forceinline__ Ics sel_ics(bool c, const Ics& x, const Ics& y)
-{
-    Ics r;
-    r.seq = c ? x.seq : y.seq;
-    r.shape = c ? x.shape : y.shape;
-    r.shape_prev = c ? x.shape_prev : y.shape_prev;
-    r.max_sfb = c ? x.max_sfb : y.max_sfb;
-    r.grouping = c ? x.grouping : y.grouping;
-    r.flags = c ? x.flags : y.flags;
-    r.pns = c ? x.pns : y.pns;
+    r.pns = __builtin_amdgcn_readlane(side, base + 2);
+    const int groups = r.seq == JAAD_EIGHT_SHORT_SEQUENCE ? 8 - __builtin_popcount(r.grouping & 0x7f) : 1;
+    r.nbands = groups * r.max_sfb;
     return r;
 }
 
@@ -508,62 +460,6 @@ __device__ void tns_spec(float* buf, float* scratch, const LdsTables& T, const G
     wave_sync();
 }
 
-// ------------------------------------------------------------------------------------------
-// PNS slow path (ICStream.java:241-257): lane 0 replays the static LCG in parse order.
-// ------------------------------------------------------------------------------------------
-__device__ void pns_fill(float* buf, const PairBands& pb, int bc, const GlobalTables& G, int u, const Ics& info)
-{
-    if (u == 0) {
-        const bool is_short = info.seq == JAAD_EIGHT_SHORT_SEQUENCE;
-        const int16_t* offs = is_short ? G.swb_s : G.swb_l;
-        int glen[8], ng = 1;
-        glen[0] = 1;
-        if (is_short)
-            for (int i = 0; i < 7; i++) {
-                if (info.grouping & (1u << i)) glen[ng - 1]++;
-                else glen[ng++] = 1;
-            }
-        uint32_t rs = info.pns;
-        const int maxSFB = info.max_sfb;
-        for (int g = 0, idx = 0, groupOff = 0; g < ng; g++) {
-            for (int sfb = 0; sfb < maxSFB; sfb++, idx++) {
-                if (pb.cb[bc][idx] != JAAD_NOISE_HCB) continue;
-                int off = groupOff + offs[sfb];
-                int width = offs[sfb + 1] - offs[sfb];
-                float sfv = pb.gain[bc][idx];
-                for (int w = 0; w < glen[g]; w++, off += 128) {
-                    float energy = 0.0f;
-                    for (int k = 0; k < width; k++) {
-                        rs = 1664525u * rs + 1013904223u;
-                        float v = (float)(int32_t)rs;
-                        buf[eo_idx(off + k)] = v;
-                        energy += v * v;
-                    }
-                    float scale = (float)((double)sfv / sqrt((double)energy));
-                    for (int k = 0; k < width; k++) buf[eo_idx(off + k)] *= scale;
-                }
-            }
-            groupOff += glen[g] << 7;
-        }
-    }
-    wave_sync();
-}
-
-// band index (g*max_sfb + sfb) of the bin quad starting at position p (4-aligned), or -1
-__device__ __forceinline__ int band_of(const LdsTables& T, const Ics& info, int p)
-{
-    int sfb, g = 0;
-    if (info.seq == JAAD_EIGHT_SHORT_SEQUENCE) {
-        int w = p >> 7;
-        sfb = T.quad2band_s[(p & 127) >> 2];
-        g = w - __builtin_popcount(info.grouping & ((1u << w) - 1u));
-    } else {
-        sfb = T.quad2band_l[p >> 2];
-    }
-    if (sfb >= info.max_sfb) return -1;
-    return g * info.max_sfb + sfb;
-}
-
 // lane u's 16 spectral bins p = 8u + 512h + i (h = 0,1; i = 0..7) <-> buf (E/O layout), as
 // four float4 accesses (bins 8u+512h+{0,2,4,6} and {1,3,5,7})
 __device__ __forceinline__ void store_spec(float* buf, int u, const float (&x)[16])
@@ -591,390 +487,513 @@ __device__ __forceinline__ void load_spec(const float* buf, int u, float (&x)[16
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
 
+// Math.round(float) followed by SampleBuffer's short clamp (S/SampleBuffer.java:193-206), two
+// samples at a time.  v_cvt_rpi_i32_f32 = (int)floor(x + 0.5) evaluated exactly, which equals
+// Math.round for every float except NaN (checked exhaustively over all 2^32 bit patterns on
+// MI355X, tools/probe_round.hip); v_cvt_pk_i16_i32 saturates to int16.  A NaN cannot reach
+// this point: |spectral value| <= IQ[8191] * 2^(155/4) < 2^57, so no IMDCT/OLA sum overflows,
+// PNS energy is a sum of squares of consecutive (distinct) LCG states and never 0, and
+// jaad_state_import rejects non-finite overlap values.
+__device__ __forceinline__ uint32_t round_pk16(float a, float b)
+{
+    int ia, ib;
+    uint32_t w;
+    asm("v_cvt_rpi_i32_f32 %0, %1" : "=v"(ia) : "v"(a));
+    asm("v_cvt_rpi_i32_f32 %0, %1" : "=v"(ib) : "v"(b));
+    asm("v_cvt_pk_i16_i32 %0, %1, %2" : "=v"(w) : "v"(ia), "v"(ib));
+    return w;
+}
+
+// per-wave LDS area: 8.5 KiB (12 waves + the table image: 123 KiB of a CU's 160 KiB)
+//   buf  band records [0,512) + raw sf/cb rows [512,640) -> spectrum (E/O) -> IFFT transposes ->
+//        OLA scratch -> PCM staging
+//   rsp  the right channel's spectrum while the left one is transformed (PNS: raw row copy)
+template <bool kTns>
+struct alignas(16) WaveLds {
+    float buf[kWaveBuf];
+    float rsp[1024];
+};
+template <>
+struct alignas(16) WaveLds<true> {
+    float buf[kWaveBuf];
+    float rsp[1024];
+    float tns[192];  // spec-TNS LPC scratch (8 filters x 24)
+};
+template <bool kTns>
+constexpr int waves_per_wg()
+{
+    return kTns ? 8 : 12;
+}
+constexpr int kRawOff = 512;  // raw rows in buf: channel c's 64 dwords at buf[kRawOff + 64c]
+
+// One scalefactor band (index g*max_sfb+sfb) of one frame, both channels:
+//   gl / gr   gain applied to IQ values, 0 for bands that are not spectral (ZERO/NOISE/IS)
+//   ms        1.0 where M/S applies (ms_used bit and both codebooks < NOISE_HCB, MS.java:25-27)
+//   is        +-gain_R where the right band is intensity coded (IS.java:26-40), else 0
+struct alignas(16) BandRec {
+    float gl, ms, gr, is;
+};
+constexpr int kNoBand = 127;  // a record index that is always all-zero (bands < 8*15 = 120)
+
+// record index of the bin quad starting at position p (4-aligned); long windows use the
+// lane's precomputed band byte
+__device__ __forceinline__ int band_short(const LdsTables& T, const Ics& ic, int p)
+{
+    const int w = p >> 7;
+    const int sfb = T.quad2band_s[(p & 127) >> 2];
+    const int g = w - __builtin_popcount(ic.grouping & ((1u << w) - 1u));
+    return sfb < ic.max_sfb ? g * ic.max_sfb + sfb : kNoBand;
+}
+
+// PNS (ICStream.java:241-257): lane 0 replays the static LCG in parse order over the channel's
+// noise bands; gain = -SCALEFACTOR_TABLE[...] (ICStream.java:205-206).
+__device__ void pns_fill(float* buf, const uint32_t* raw, const LdsTables& T, const GlobalTables& G, int u,
+                         const Ics& info)
+{
+    if (u == 0) {
+        const uint8_t* sfr = reinterpret_cast<const uint8_t*>(raw);
+        const uint8_t* cbr = sfr + 128;
+        const bool is_short = info.seq == JAAD_EIGHT_SHORT_SEQUENCE;
+        const int16_t* offs = is_short ? G.swb_s : G.swb_l;
+        int glen[8], ng = 1;
+        glen[0] = 1;
+        if (is_short)
+            for (int i = 0; i < 7; i++) {
+                if (info.grouping & (1u << i)) glen[ng - 1]++;
+                else glen[ng++] = 1;
+            }
+        uint32_t rs = info.pns;
+        const int maxSFB = info.max_sfb;
+        for (int g = 0, idx = 0, groupOff = 0; g < ng; g++) {
+            for (int sfb = 0; sfb < maxSFB; sfb++, idx++) {
+                if (cbr[idx] != JAAD_NOISE_HCB) continue;
+                int off = groupOff + offs[sfb];
+                const int width = offs[sfb + 1] - offs[sfb];
+                const float sfv = -T.sf_gain[sfr[idx]];
+                for (int w = 0; w < glen[g]; w++, off += 128) {
+                    float energy = 0.0f;
+                    for (int k = 0; k < width; k++) {
+                        rs = 1664525u * rs + 1013904223u;
+                        const float v = (float)(int32_t)rs;
+                        buf[eo_idx(off + k)] = v;
+                        energy += v * v;
+                    }
+                    const float scale = (float)((double)sfv / sqrt((double)energy));
+                    for (int k = 0; k < width; k++) buf[eo_idx(off + k)] *= scale;
+                }
+            }
+            groupOff += glen[g] << 7;
+        }
+    }
+    wave_sync();
+}
+
 struct Prefetch {
-    v4i q[2];       // own channel bins 8u+512h .. +7
-    uint32_t sfcb;  // lane u < 32: sf bytes 4u..4u+3; lane u >= 32: cb bytes 4(u-32)..
-    uint32_t side;  // lane i < 4*nch: dword i of the frame's jaad_ics_info records;
-                    // lanes 8..11: the frame's ms_used words (read back with readlane)
+    v4i q[2][2];       // [channel][h]: bins 8u+512h .. +7
+    uint32_t sfcb[2];  // [channel] lane u < 32: sf bytes 4u..4u+3; lane u >= 32: cb bytes 4(u-32)..
+    uint32_t side;     // lane i < 4*nch: dword i of the frame's jaad_ics_info records;
+                       // lanes 8..11: the frame's ms_used words (read back with readlane)
 };
 
-// Everything frame f needs from HBM, loaded one frame ahead with vector loads (vmcnt is in
-// order; scalar loads would share lgkmcnt with the LDS traffic and could not be hidden).
-__device__ __forceinline__ void prefetch(const KernelArgs& A, int f, int nch, int c, int u, Prefetch& pf)
+// Everything frame f needs from HBM, as vector loads (vmcnt is in order; scalar loads would
+// share lgkmcnt with the LDS traffic and could not be left in flight).
+__device__ __forceinline__ void prefetch(const KernelArgs& A, int f, bool stereo, int u, Prefetch& pf)
 {
-    const size_t cf = (size_t)f * nch + c;
-    const v4i* q = reinterpret_cast<const v4i*>(A.q + cf * 1024);
-    pf.q[0] = __builtin_nontemporal_load(q + u);
-    pf.q[1] = __builtin_nontemporal_load(q + 64 + u);
-    const uint32_t* row = reinterpret_cast<const uint32_t*>(u < 32 ? A.sf + cf * 128 : A.cb + cf * 128);
-    pf.sfcb = row[u & 31];
+    const int nch = stereo ? 2 : 1;
+#pragma unroll
+    for (int c = 0; c < 2; c++) {
+        if (c == 1 && !stereo) break;
+        const size_t cf = (size_t)f * nch + c;
+        const v4i* q = reinterpret_cast<const v4i*>(A.q + cf * 1024);
+        pf.q[c][0] = __builtin_nontemporal_load(q + u);
+        pf.q[c][1] = __builtin_nontemporal_load(q + 64 + u);
+        const uint32_t* row = reinterpret_cast<const uint32_t*>(u < 32 ? A.sf + cf * 128 : A.cb + cf * 128);
+        pf.sfcb[c] = row[u & 31];
+    }
     const uint32_t* side = u < 8 ? reinterpret_cast<const uint32_t*>(A.ics + (size_t)f * nch) + (u < 4 * nch ? u : 0)
                                  : (A.ms_used ? reinterpret_cast<const uint32_t*>(A.ms_used + (size_t)f * 2) + (u & 3)
                                               : reinterpret_cast<const uint32_t*>(A.ics));
     pf.side = *side;
 }
 
-__device__ __forceinline__ Ics ics_from_lanes(uint32_t side, int base)
+// inverse quantisation of one channel's 16 bins (ICStream.java:258-271):
+// x = gain != 0 ? (q>0 ? IQ[q] : -IQ[-q]) * gain : 0
+__device__ __forceinline__ void iq_channel(const LdsTables& T, const float* iq_global, const v4i (&q)[2],
+                                           const float (&g)[4], float (&x)[16])
 {
-    const uint32_t a = __builtin_amdgcn_readlane(side, base);
-    const uint32_t b = __builtin_amdgcn_readlane(side, base + 1);
-    Ics r;
-    r.seq = a & 0xff;
-    r.shape = (a >> 8) & 0xff;
-    r.shape_prev = (a >> 16) & 0xff;
-    r.max_sfb = a >> 24;
-    r.grouping = b & 0xff;
-    r.flags = (b >> 8) & 0xff;
-    r.pns = __builtin_amdgcn_readlane(side, base + 2);
-    return r;
+    bool esc = false;
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        const int16_t* qv = reinterpret_cast<const int16_t*>(&q[h]);
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+            const float gn = g[2 * h + j];
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const int qq = qv[4 * j + i];
+                const int qc = qq < -128 ? -128 : (qq > 127 ? 127 : qq);
+                esc |= qc != qq;
+                const float m = T.iq_signed[qc + 128] * gn;
+                x[8 * h + 4 * j + i] = gn != 0.0f ? m : 0.0f;
+            }
+        }
+    }
+    if (__builtin_expect(__ballot(esc) != 0, 0)) {  // escape values beyond the LDS head of IQ_TABLE
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const int16_t* qv = reinterpret_cast<const int16_t*>(&q[h]);
+#pragma unroll
+            for (int j = 0; j < 2; j++) {
+                const float gn = g[2 * h + j];
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const int qq = qv[4 * j + i];
+                    const int aq = qq < 0 ? -qq : qq;
+                    if ((qq > 127 || qq < -128) && gn != 0.0f) {
+                        const float m = iq_global[aq > 8190 ? 8190 : aq] * gn;
+                        x[8 * h + 4 * j + i] = qq > 0 ? m : -m;
+                    }
+                }
+            }
+        }
+    }
+}
+
+// (TNS) -> IMDCT -> window/OLA of one channel whose spectrum is in buf (E/O layout); result
+// in out (slot o = position long_pos(u, o)), new overlap in ov
+template <bool kTnsSpec>
+__device__ __forceinline__ void synth_channel(const KernelArgs& A, const LdsTables& T, WaveLds<kTnsSpec>& W, const Ics& ic,
+                                              size_t cf, float (&ov)[16], float (&out)[16])
+{
+    const int u = lane_id();
+    float* buf = W.buf;
+    if constexpr (kTnsSpec)
+        if (A.tns_mode == JAAD_TNS_SPEC && (ic.flags & JAAD_ICS_TNS) && A.tns) tns_spec(buf, W.tns, T, *A.gtab, u, ic, A.tns + cf);
+    const FrameCtx fc{ic.seq, ic.shape, ic.shape_prev};
+    float re[8], im[8];
+    if (fc.seq == JAAD_EIGHT_SHORT_SEQUENCE) {
+        imdct_short(buf, T, u, re, im);
+        ola_short(buf, T, u, fc, re, im, ov, out);
+    } else {
+        imdct_long(buf, T, u, re, im);
+        ola_long(T, u, fc, re, im, ov, out);
+    }
+    wave_sync();
 }
 
 template <bool kTnsSpec, int kOut>
-__global__ __launch_bounds__(kWGThreads, kTnsSpec ? 2 : JAAD_WAVES_PER_EU) void lc_decode_kernel(KernelArgs A)
+__global__ __launch_bounds__(64 * waves_per_wg<kTnsSpec>()) void lc_decode_kernel(KernelArgs A)
 {
-    __shared__ LdsTables T;
-    __shared__ float Wb[kWavesPerWG][kWaveBuf];
-    __shared__ PairBands PB[kWavesPerWG / 2];
+    constexpr int kW = waves_per_wg<kTnsSpec>();
+    constexpr int kThreads = 64 * kW;
+    // one LDS object with the tables first: every table access is a 16-bit immediate offset
+    struct Lds {
+        LdsTables T;
+        WaveLds<kTnsSpec> W[kW];
+    };
+    __shared__ Lds S;
+    LdsTables& T = S.T;
 
     {
         const uint4* src = reinterpret_cast<const uint4*>(A.tables);
         uint4* dst = reinterpret_cast<uint4*>(&T);
-        for (int i = threadIdx.x; i < (int)(sizeof(LdsTables) / 16); i += kWGThreads) dst[i] = src[i];
+        for (int i = threadIdx.x; i < (int)(sizeof(LdsTables) / 16); i += kThreads) dst[i] = src[i];
     }
-    __syncthreads();
+    __syncthreads();  // the only workgroup barrier: waves are independent from here on
 
     constexpr bool big_endian = !(kOut & JAAD_PCM_LITTLE_ENDIAN);
     constexpr bool planar = kOut == (int)kOutPlanarF32;
-    constexpr bool out_f32 = (kOut & JAAD_PCM_FLOAT32) != 0 || planar;
+    constexpr bool out_f32 = (kOut & JAAD_PCM_FLOAT32) != 0 && !planar;
+    constexpr bool out_i16 = !planar && !out_f32;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    STAMP(0);
     const bool stereo = A.nch == 2;
-    const int c = stereo ? (wave & 1) : 0;  // channel of this wave
-    const int bc = wave & 1;                // channel slot in the PairBands record
-    PairBands& pb = PB[wave >> 1];
-    float* buf = Wb[wave];
-    const int per_wg = stereo ? kWavesPerWG / 2 : kWavesPerWG;
-    const int my_idx = stereo ? (wave >> 1) : wave;
     const int nch = stereo ? 2 : 1;
+    WaveLds<kTnsSpec>& W = S.W[wave];
+    uint32_t* raw = reinterpret_cast<uint32_t*>(W.buf + kRawOff);
+    BandRec* rec = reinterpret_cast<BandRec*>(W.buf);
 
-    for (uint32_t g = blockIdx.x; g * per_wg < A.n_chunks; g += gridDim.x) {
-        STAMP(1);
-        // iteration count shared by the whole workgroup (barriers must match)
-        int n_iter = 0;
-        for (int j = 0; j < per_wg; j++) {
-            uint32_t cj = g * per_wg + j;
-            if (cj < A.n_chunks) {
-                uint32_t inf = A.chunks[cj].info;
-                int n = (int)(inf & 0xffff) + ((inf & kChunkPrefix) ? 1 : 0);
-                n_iter = n > n_iter ? n : n_iter;
-            }
+    // long-window band of each of the lane's 4 bin quads (frame invariant)
+    uint32_t q2b_long = 0;
+    {
+        const int u = lane_id();
+#pragma unroll
+        for (int qd = 0; qd < 4; qd++) {
+            const uint32_t b = T.quad2band_l[(512 * (qd >> 1) + 8 * u + 4 * (qd & 1)) >> 2];
+            q2b_long |= (b > kNoBand ? kNoBand : b) << (8 * qd);
         }
-        const uint32_t ci = g * per_wg + my_idx;
-        ChunkDesc cd{0, 0, 0, 0};
-        if (ci < A.n_chunks) cd = A.chunks[ci];
+    }
+
+    for (uint32_t ci = blockIdx.x * kW + wave; ci < A.n_chunks; ci += gridDim.x * kW) {
+        const ChunkDesc cd = A.chunks[ci];
         const int nfr = cd.info & 0xffff;
         const bool prefix = (cd.info & kChunkPrefix) != 0;
         const int my_n = nfr + (prefix ? 1 : 0);
         const int f_first = (int)cd.frame0 - (prefix ? 1 : 0);
 
-        float ov[16];
+        float ovL[16], ovR[16];
         {
             const int u = lane_id();
             if (cd.info & kChunkLoadState) {
-                const float* st = A.state_in + (size_t)cd.slot * 2048 + 1024 * c;
+                const float* st = A.state_in + (size_t)cd.slot * 2048;
 #pragma unroll
-                for (int o = 0; o < 16; o++) ov[o] = st[long_pos(u, o)];
+                for (int o = 0; o < 16; o++) {
+                    ovL[o] = st[long_pos(u, o)];
+                    ovR[o] = st[1024 + long_pos(u, o)];
+                }
             } else {
 #pragma unroll
-                for (int o = 0; o < 16; o++) ov[o] = 0.0f;
+                for (int o = 0; o < 16; o++) ovL[o] = ovR[o] = 0.0f;
             }
         }
-        // two frames in flight per wave (>= 64 KiB of loads in flight per CU)
-        Prefetch pf, pf2;
-        if (my_n > 0) prefetch(A, f_first, nch, c, lane_id(), pf);
-        if (my_n > 1) prefetch(A, f_first + 1, nch, c, lane_id(), pf2);
+        Prefetch pf;
+        if (my_n > 0) prefetch(A, f_first, stereo, lane_id(), pf);
 
-        // frame body; pfx holds frame `it`'s inputs and is refilled with frame it+2 (two frames in
-        // flight; the loop is unrolled by 2 so the prefetch registers never need copying, which
-        // would force a vmcnt(0) drain of every outstanding load and store)
-        auto frame = [&](const int it, Prefetch& pfx) {
-            if (it >= 4 && it < 7) STAMP(2 + 9 * (it - 4) + 0);
+        for (int it = 0; it < my_n; it++) {
             const int u = lane_id();
-            const bool active = it < my_n;
             const int f = f_first + it;
-            const bool emit = active && f >= (int)cd.frame0;
-            const size_t cf0 = (size_t)(active ? f : 0) * nch;
-            Ics ic{}, iL{}, iR{};
-            bool ms_on = false, is_on = false, xchg = false;
-            float x[16];
+            const bool emit = f >= (int)cd.frame0;
+            const size_t cf0 = (size_t)f * nch;
+            const Prefetch cur = pf;
 
-            // ---------------- phase A: side info, inverse quantisation, PNS ----------------
-            if (active) {
-                iL = ics_from_lanes(pfx.side, 0);
-                iR = stereo ? ics_from_lanes(pfx.side, 4) : iL;
-                ic = sel_ics(c != 0, iR, iL);
-                ms_on = stereo && (iL.flags & JAAD_ICS_COMMON_WINDOW) && (iL.flags & JAAD_ICS_MS_PRESENT);
-                is_on = stereo && (iR.flags & JAAD_ICS_HAS_IS);
-                xchg = ms_on || is_on;
-#ifdef JAAD_ABL_NO_MS
-                xchg = false;
-#endif
-                // raw sf/cb rows of this channel -> pair record
-                reinterpret_cast<uint32_t*>(u < 32 ? pb.sf[bc] : pb.cb[bc])[u & 31] = pfx.sfcb;
-                const Prefetch cur = pfx;
-#ifdef JAAD_DEBUG_SIDE
-                if (A.dbg && ci == 0 && u == 0 && f < 16) {
-                    A.dbg[6144 + 32 * f + 8 * c + 0] = (float)ic.seq;
-                    A.dbg[6144 + 32 * f + 8 * c + 1] = (float)ic.shape;
-                    A.dbg[6144 + 32 * f + 8 * c + 2] = (float)ic.shape_prev;
-                    A.dbg[6144 + 32 * f + 8 * c + 3] = (float)ic.max_sfb;
-                    A.dbg[6144 + 32 * f + 8 * c + 4] = (float)ic.flags;
-                    A.dbg[6144 + 32 * f + 8 * c + 5] = (float)(ic.pns & 0xffff);
-                    A.dbg[6144 + 32 * f + 8 * c + 6] = (float)f;
-                }
-#endif
-                if (it + 2 < my_n) prefetch(A, f + 2, nch, c, u, pfx);
-                if (stereo && c == 0) {
-                    uint64_t m0 = 0, m1 = 0;
-                    if (ms_on && A.ms_used) {
-                        // readlane returns int: widen through uint32_t (no sign extension)
-                        m0 = (uint64_t)(uint32_t)__builtin_amdgcn_readlane(cur.side, 8) |
-                             ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(cur.side, 9) << 32);
-                        m1 = (uint64_t)(uint32_t)__builtin_amdgcn_readlane(cur.side, 10) |
-                             ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(cur.side, 11) << 32);
+            // ---------------- side info ----------------
+            const Ics iL = ics_from_lanes(cur.side, 0);
+            const Ics iR = stereo ? ics_from_lanes(cur.side, 4) : iL;
+            const bool ms_on = stereo && (iL.flags & JAAD_ICS_COMMON_WINDOW) && (iL.flags & JAAD_ICS_MS_PRESENT);
+            const bool is_on = stereo && (iR.flags & JAAD_ICS_HAS_IS);
+            const bool same_bands = !stereo || (iL.seq == iR.seq && iL.max_sfb == iR.max_sfb && iL.grouping == iR.grouping);
+            uint64_t m0 = 0, m1 = 0;
+            if (ms_on && A.ms_used) {
+                // readlane returns int: widen through uint32_t (no sign extension)
+                m0 = (uint64_t)(uint32_t)__builtin_amdgcn_readlane(cur.side, 8) |
+                     ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(cur.side, 9) << 32);
+                m1 = (uint64_t)(uint32_t)__builtin_amdgcn_readlane(cur.side, 10) |
+                     ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(cur.side, 11) << 32);
+            }
+
+            // ---------------- band records (lane u: bands 2u, 2u+1) ----------------
+            wave_sync();
+            raw[u] = cur.sfcb[0];
+            if (stereo) raw[64 + u] = cur.sfcb[1];
+            wave_sync();
+            {
+                const uint16_t* r0 = reinterpret_cast<const uint16_t*>(raw);
+                const uint16_t* r1 = reinterpret_cast<const uint16_t*>(raw + 64);
+                const uint32_t sfL2 = r0[u], cbL2 = r0[64 + u];
+                const uint32_t sfR2 = stereo ? (uint32_t)r1[u] : 0u, cbR2 = stereo ? (uint32_t)r1[64 + u] : 0u;
+                const uint64_t mw = u < 32 ? m0 : m1;
+                const uint32_t msb = (uint32_t)(mw >> ((2 * u) & 63)) & 3u;
+                BandRec br[2];
+#pragma unroll
+                for (int e = 0; e < 2; e++) {
+                    const int b = 2 * u + e;
+                    const uint32_t sfL = (sfL2 >> (8 * e)) & 255u, cbL = (cbL2 >> (8 * e)) & 255u;
+                    const uint32_t sfR = (sfR2 >> (8 * e)) & 255u, cbR = (cbR2 >> (8 * e)) & 255u;
+                    const bool inL = b < iL.nbands, inR = b < iR.nbands;
+                    const bool msbit = (msb >> e) & 1u;
+                    const float gvL = T.sf_gain[sfL];
+                    br[e].gl = (inL && cbL != JAAD_ZERO_HCB && cbL < JAAD_NOISE_HCB) ? gvL : 0.0f;
+                    br[e].ms = (ms_on && inL && msbit && cbL < JAAD_NOISE_HCB && cbR < JAAD_NOISE_HCB) ? 1.0f : 0.0f;
+                    float gr = 0.0f, is = 0.0f;
+                    if (stereo) {
+                        const float gvR = T.sf_gain[sfR];
+                        gr = (inR && cbR != JAAD_ZERO_HCB && cbR < JAAD_NOISE_HCB) ? gvR : 0.0f;
+                        if (is_on && inR && (cbR == JAAD_INTENSITY_HCB || cbR == JAAD_INTENSITY_HCB2)) {
+                            float cs = cbR == JAAD_INTENSITY_HCB ? 1.0f : -1.0f;
+                            if ((iL.flags & JAAD_ICS_MS_PRESENT) && msbit) cs = -cs;
+                            is = cs * gvR;
+                        }
                     }
-                    pb.ms[u] = (uint8_t)((m0 >> u) & 1u);
-                    pb.ms[u + 64] = (uint8_t)((m1 >> u) & 1u);
+                    br[e].gr = gr;
+                    br[e].is = is;
                 }
                 wave_sync();
-                if (it >= 4 && it < 7) STAMP(2 + 9 * (it - 4) + 1);
+                reinterpret_cast<float4*>(rec)[2 * u] = make_float4(br[0].gl, br[0].ms, br[0].gr, br[0].is);
+                reinterpret_cast<float4*>(rec)[2 * u + 1] = make_float4(br[1].gl, br[1].ms, br[1].gr, br[1].is);
+            }
+            wave_sync();
+
+            // ---------------- inverse quantisation, PNS, M/S, I/S ----------------
+            float gL[4], gR[4], msq[4], isq[4];
 #pragma unroll
-                for (int hb = 0; hb < 2; hb++) {
-                    const int idx = u + 64 * hb;
-                    const uint32_t cbv = pb.cb[bc][idx];
-                    const float gv = T.sf_gain[pb.sf[bc][idx]];
-                    pb.gain[bc][idx] = cbv == JAAD_NOISE_HCB ? -gv : gv;
+            for (int qd = 0; qd < 4; qd++) {
+                const int p = 512 * (qd >> 1) + 8 * u + 4 * (qd & 1);
+                const int bl = iL.seq == JAAD_EIGHT_SHORT_SEQUENCE ? band_short(T, iL, p) : (int)((q2b_long >> (8 * qd)) & 255u);
+                const float4 r = reinterpret_cast<const float4*>(rec)[bl];
+                gL[qd] = r.x;
+                msq[qd] = r.y;
+                if (same_bands) {
+                    gR[qd] = r.z;
+                    isq[qd] = r.w;
+                } else {
+                    const int br = iR.seq == JAAD_EIGHT_SHORT_SEQUENCE ? band_short(T, iR, p) : (int)((q2b_long >> (8 * qd)) & 255u);
+                    const float2 rr = reinterpret_cast<const float2*>(rec)[2 * br + 1];
+                    gR[qd] = rr.x;
+                    isq[qd] = rr.y;
                 }
+            }
+            float xL[16], xR[16];
+            iq_channel(T, A.iq_table, cur.q[0], gL, xL);
+            if (stereo) iq_channel(T, A.iq_table, cur.q[1], gR, xR);
+            // the inputs are consumed: frame f+1's loads fly while this frame's IMDCTs run
+            if (it + 1 < my_n) prefetch(A, f + 1, stereo, u, pf);
+
+            if ((iL.flags | (stereo ? iR.flags : 0)) & JAAD_ICS_HAS_PNS) {  // rare: lane 0 replays the LCG
+                // the spectrum overwrites the raw rows: pns_fill reads a copy in rsp
+                uint32_t* rcopy = reinterpret_cast<uint32_t*>(W.rsp);
                 wave_sync();
-                // inverse quantisation (ICStream.java:258-271): lane owns bins 8u+512h+i
-                if (it >= 4 && it < 7) STAMP(2 + 9 * (it - 4) + 2);
-                bool esc = false;
+                rcopy[u] = raw[u];
+                if (stereo) rcopy[64 + u] = raw[64 + u];
+                if (iL.flags & JAAD_ICS_HAS_PNS) {
+                    wave_sync();
+                    store_spec(W.buf, u, xL);
+                    wave_sync();
+                    pns_fill(W.buf, rcopy, T, *A.gtab, u, iL);
+                    load_spec(W.buf, u, xL);
+                }
+                if (stereo && (iR.flags & JAAD_ICS_HAS_PNS)) {
+                    wave_sync();
+                    store_spec(W.buf, u, xR);
+                    wave_sync();
+                    pns_fill(W.buf, rcopy + 64, T, *A.gtab, u, iR);
+                    load_spec(W.buf, u, xR);
+                }
+            }
+            if (ms_on) {  // MS.java:28-33: L' = L + R, R' = L - R (no scaling)
 #pragma unroll
-                for (int h = 0; h < 2; h++) {
-                    const int16_t* qv = reinterpret_cast<const int16_t*>(&cur.q[h]);
-#pragma unroll
-                    for (int j = 0; j < 2; j++) {
-                        const int bi = band_of(T, ic, 512 * h + 8 * u + 4 * j);
-                        const uint32_t cbv = bi >= 0 ? pb.cb[bc][bi] : 0u;
-                        const float gn = bi >= 0 ? pb.gain[bc][bi] : 0.0f;
-                        const bool spectral = cbv != JAAD_ZERO_HCB && cbv < JAAD_NOISE_HCB;
+                for (int qd = 0; qd < 4; qd++) {
+                    if (msq[qd] != 0.0f) {
 #pragma unroll
                         for (int i = 0; i < 4; i++) {
-                            const int qq = qv[4 * j + i];
-                            const int qc = qq < -128 ? -128 : (qq > 127 ? 127 : qq);
-                            esc |= qc != qq;
-                            // (q>0 ? IQ[q] : -IQ[-q]) * sf, sign folded into the table
-#ifdef JAAD_ABL_NO_IQ
-                            const float m = (float)qc * gn;
-#else
-                            const float m = T.iq_signed[qc + 128] * gn;
-#endif
-                            x[8 * h + 4 * j + i] = spectral ? m : 0.0f;
+                            const int e = 8 * (qd >> 1) + 4 * (qd & 1) + i;
+                            const float l = xL[e], r = xR[e];
+                            xL[e] = l + r;
+                            xR[e] = l - r;
                         }
                     }
                 }
-                if (__ballot(esc)) {  // escape values beyond the LDS head of IQ_TABLE
+            }
+            if (is_on) {  // IS.java:41-46: R = L * (+-gain); never on an M/S band (cb_R >= 14)
 #pragma unroll
-                    for (int h = 0; h < 2; h++) {
-                        const int16_t* qv = reinterpret_cast<const int16_t*>(&cur.q[h]);
+                for (int qd = 0; qd < 4; qd++) {
+                    if (isq[qd] != 0.0f) {
 #pragma unroll
-                        for (int j = 0; j < 2; j++) {
-                            const int bi = band_of(T, ic, 512 * h + 8 * u + 4 * j);
-                            const uint32_t cbv = bi >= 0 ? pb.cb[bc][bi] : 0u;
-                            const float gn = bi >= 0 ? pb.gain[bc][bi] : 0.0f;
-                            const bool spectral = cbv != JAAD_ZERO_HCB && cbv < JAAD_NOISE_HCB;
-#pragma unroll
-                            for (int i = 0; i < 4; i++) {
-                                const int qq = qv[4 * j + i];
-                                const int aq = qq < 0 ? -qq : qq;
-                                if ((qq > 127 || qq < -128) && spectral) {
-                                    const float m = A.iq_table[aq > 8190 ? 8190 : aq] * gn;
-                                    x[8 * h + 4 * j + i] = qq > 0 ? m : -m;
-                                }
-                            }
+                        for (int i = 0; i < 4; i++) {
+                            const int e = 8 * (qd >> 1) + 4 * (qd & 1) + i;
+                            xR[e] = xL[e] * isq[qd];
                         }
                     }
                 }
-                if (it >= 4 && it < 7) STAMP(2 + 9 * (it - 4) + 3);
-                store_spec(buf, u, x);
-                if (ic.flags & JAAD_ICS_HAS_PNS) {
+            }
+
+            // left spectrum -> buf (E/O layout); right spectrum parked in rsp (lane-linear)
+            wave_sync();
+            store_spec(W.buf, u, xL);
+            if (stereo) {
+#pragma unroll
+                for (int k = 0; k < 4; k++)
+                    *reinterpret_cast<float4*>(W.rsp + 4 * u + 256 * k) = make_float4(xR[4 * k], xR[4 * k + 1], xR[4 * k + 2], xR[4 * k + 3]);
+            }
+            wave_sync();
+
+            // ---------------- per channel: IMDCT, window/OLA, PCM ----------------
+            // int16 PCM is staged in rsp as the frame's interleaved SampleBuffer image (word P =
+            // sample P of L and R); channel c's samples wait in pk until rsp is free.
+            uint16_t* stage16 = reinterpret_cast<uint16_t*>(W.rsp);
+            uint32_t pk[8];
+            auto channel = [&](const int c, float (&ov)[16]) {
+                const Ics& ic = c ? iR : iL;
+                if (c == 1) {
+                    const int u2 = lane_id();
+                    float x[16];
+#pragma unroll
+                    for (int k = 0; k < 4; k++) {
+                        const float4 v = *reinterpret_cast<const float4*>(W.rsp + 4 * u2 + 256 * k);
+                        x[4 * k] = v.x;
+                        x[4 * k + 1] = v.y;
+                        x[4 * k + 2] = v.z;
+                        x[4 * k + 3] = v.w;
+                    }
+                    store_spec(W.buf, u2, x);
+                    if constexpr (out_i16) {
+                        if (emit) {
+                            wave_sync();
+#pragma unroll
+                            for (int o = 0; o < 16; o++) stage16[2 * long_pos(u2, o)] = (uint16_t)(pk[o >> 1] >> (16 * (o & 1)));
+                        }
+                    }
                     wave_sync();
-                    pns_fill(buf, pb, bc, *A.gtab, u, ic);
-                    load_spec(buf, u, x);
                 }
-            }
-#ifndef JAAD_ABL_NO_BARRIER
-            __syncthreads();  // B1
-#endif  // both channels' spectra + band records visible to the pair
-
-            if (it >= 4 && it < 7) STAMP(2 + 9 * (it - 4) + 4);
-            // ---------------- phase C: M/S (MS.java:17-41) and I/S (IS.java:17-53) ----------------
-            if (active && xchg) {
-                float xp[16];
-                load_spec(Wb[wave ^ 1], u, xp);
-#pragma unroll
-                for (int h = 0; h < 2; h++) {
-#pragma unroll
-                    for (int j = 0; j < 2; j++) {
-                        const int p = 512 * h + 8 * u + 4 * j;
-                        if (ms_on) {
-                            const int bi = band_of(T, iL, p);
-                            if (bi >= 0 && pb.ms[bi] && pb.cb[0][bi] < JAAD_NOISE_HCB && pb.cb[1][bi] < JAAD_NOISE_HCB) {
-#pragma unroll
-                                for (int i = 0; i < 4; i++) {
-                                    const int e = 8 * h + 4 * j + i;
-                                    // t = L - R; L += R; R = t
-                                    x[e] = c == 0 ? x[e] + xp[e] : xp[e] - x[e];
-                                }
-                            }
-                        }
-                        if (is_on && c == 1) {
-                            const int bi = band_of(T, iR, p);
-                            const uint32_t cbr = bi >= 0 ? pb.cb[1][bi] : 0u;
-                            if (cbr == JAAD_INTENSITY_HCB || cbr == JAAD_INTENSITY_HCB2) {
-                                int cs = cbr == JAAD_INTENSITY_HCB ? 1 : -1;
-                                if (iL.flags & JAAD_ICS_MS_PRESENT) cs *= pb.ms[bi] ? -1 : 1;
-                                const float scale = (float)cs * pb.gain[1][bi];
-#pragma unroll
-                                for (int i = 0; i < 4; i++) x[8 * h + 4 * j + i] = xp[8 * h + 4 * j + i] * scale;
-                            }
-                        }
-                    }
-                }
-            }
-            if (it >= 4 && it < 7) STAMP(2 + 9 * (it - 4) + 5);
-#ifndef JAAD_ABL_NO_BARRIER
-            __syncthreads();  // B2
-#endif  // the partner has read this wave's spectrum
-
-            if (it >= 4 && it < 7) STAMP(2 + 9 * (it - 4) + 6);
-            // ---------------- phase D: (TNS) -> IMDCT -> window/OLA -> PCM into LDS ----------------
-            if (active) {
-                if (xchg) store_spec(buf, u, x);
-                wave_sync();
-                const bool dump = A.dbg && ci == 0 && f == A.dbg_frame;
-                if (dump)
-                    for (int i = 0; i < 16; i++) {
-                        const int p = 8 * u + 512 * (i >> 3) + (i & 7);
-                        A.dbg[1024 * c + p] = buf[eo_idx(p)];
-                    }
-                if (kTnsSpec && A.tns_mode == JAAD_TNS_SPEC && (ic.flags & JAAD_ICS_TNS) && A.tns)
-                    tns_spec(buf, &pb.gain[bc][0], T, *A.gtab, u, ic, A.tns + cf0 + c);
-                FrameCtx fc{ic.seq, ic.shape, ic.shape_prev};
-                float re[8], im[8], out[16];
-#ifdef JAAD_ABL_NO_IMDCT
-                if (true) {
-#pragma unroll
-                    for (int o = 0; o < 16; o++) { out[o] = buf[o * 64 + u] + ov[o]; ov[o] = out[o] * 0.5f; }
-                } else
-#endif
-                if (fc.seq == JAAD_EIGHT_SHORT_SEQUENCE) {
-                    imdct_short(buf, T, u, re, im);
-                    ola_short(buf, T, u, fc, re, im, ov, out);
-                } else {
-                    imdct_long(buf, T, u, re, im);
-                    if (dump)
-                        for (int s2 = 0; s2 < 8; s2++) {
-                            A.dbg[2048 + 1024 * c + 2 * (u + 64 * s2)] = re[s2];
-                            A.dbg[2048 + 1024 * c + 2 * (u + 64 * s2) + 1] = im[s2];
-                        }
-                    ola_long(T, u, fc, re, im, ov, out);
-                }
-                wave_sync();
-                if (dump)
-                    for (int o = 0; o < 16; o++) A.dbg[4096 + 1024 * c + long_pos(u, o)] = out[o];
-#ifdef JAAD_ABL_NO_PCMLDS
-                if (emit && A.n_chunks == 0) {
-#else
+                float out[16];
+                synth_channel<kTnsSpec>(A, T, W, ic, cf0 + c, ov, out);
                 if (emit) {
-#endif
+                    const int u2 = lane_id();
+                    if constexpr (planar) {
+                        float* dst = reinterpret_cast<float*>(A.pcm) + (cf0 + c) * 1024;
+#pragma unroll
+                        for (int o = 0; o < 16; o++) W.buf[long_pos(u2, o)] = out[o];
+                        wave_sync();
+#pragma unroll
+                        for (int jj = 0; jj < 4; jj++)
+                            *reinterpret_cast<float4*>(dst + 4 * u2 + 256 * jj) = *reinterpret_cast<const float4*>(W.buf + 4 * u2 + 256 * jj);
+                    } else if constexpr (out_f32) {  // tolerance/debug format: strided stores
+                        float* dst = reinterpret_cast<float*>(reinterpret_cast<uint8_t*>(A.pcm) + (size_t)f * 8192);
+#pragma unroll
+                        for (int o = 0; o < 16; o++) {
+                            const int P = long_pos(u2, o);
+                            dst[2 * P + c] = out[o];
+                            if (!stereo) dst[2 * P + 1] = out[o];
+                        }
+                    } else {
+                        // big endian swaps the two bytes of every sample
+                        const uint32_t sel = big_endian ? 0x02030001u : 0x03020100u;
+#pragma unroll
+                        for (int m = 0; m < 8; m++) pk[m] = __builtin_amdgcn_perm(0u, round_pk16(out[2 * m], out[2 * m + 1]), sel);
+                    }
+                }
+            };
+            channel(0, ovL);
+            if (stereo) channel(1, ovR);
+            if constexpr (out_i16) {
+                if (emit) {
+                    const int u2 = lane_id();
+                    wave_sync();
 #pragma unroll
                     for (int o = 0; o < 16; o++) {
-                        const int P = long_pos(u, o);
-                        if constexpr (out_f32) buf[P] = out[o];
-                        else reinterpret_cast<int16_t*>(buf)[P] = (int16_t)java_round16(out[o]);
+                        const uint16_t v = (uint16_t)(pk[o >> 1] >> (16 * (o & 1)));
+                        const int P = long_pos(u2, o);
+                        if (stereo) {
+                            stage16[2 * P + 1] = v;
+                        } else {
+                            stage16[2 * P] = v;
+                            stage16[2 * P + 1] = v;
+                        }
                     }
-                }
-            }
-#ifndef JAAD_ABL_NO_BARRIER
-            __syncthreads();  // B3
-#endif  // PCM of both channels in LDS
-
-            if (it >= 4 && it < 7) STAMP(2 + 9 * (it - 4) + 7);
-            // ---------------- phase E: interleave + store (stereo: wave c stores samples [512c, 512c+512)) ----
-#ifndef JAAD_ABL_NO_STORE
-            if (emit) {
-#else
-            if (emit && A.n_chunks == 0) {
-#endif
-                const float* bL = stereo ? Wb[wave & ~1] : buf;
-                const float* bR = stereo ? Wb[wave | 1] : buf;
-                const int nj = stereo ? 2 : 4;
-                if constexpr (planar) {  // this wave's channel, time order, for the SBR kernel
-                    float* dst = reinterpret_cast<float*>(A.pcm) + ((size_t)f * nch + c) * 1024;
+                    wave_sync();
+                    uint8_t* dst = reinterpret_cast<uint8_t*>(A.pcm) + (size_t)f * 4096;
 #pragma unroll
-                    for (int jj = 0; jj < 4; jj++) {
-                        const int p = 4 * u + 256 * jj;
-                        *reinterpret_cast<float4*>(dst + p) = *reinterpret_cast<const float4*>(buf + p);
-                    }
-                } else
-                for (int jj = 0; jj < nj; jj++) {
-                    const int j = stereo ? 2 * c + jj : jj;
-                    const int p = 4 * u + 256 * j;  // samples p..p+3
-                    if constexpr (out_f32) {
-                        float4 l = *reinterpret_cast<const float4*>(bL + p);
-                        float4 r = *reinterpret_cast<const float4*>(bR + p);
-                        float4* dst = reinterpret_cast<float4*>(reinterpret_cast<uint8_t*>(A.pcm) + (size_t)f * 8192 + 8 * p);
-                        dst[0] = make_float4(l.x, r.x, l.y, r.y);
-                        dst[1] = make_float4(l.z, r.z, l.w, r.w);
-                    } else {
-                        uint2 l = *reinterpret_cast<const uint2*>(reinterpret_cast<const int16_t*>(bL) + p);
-                        uint2 r = *reinterpret_cast<const uint2*>(reinterpret_cast<const int16_t*>(bR) + p);
-                        // (L_i, R_i) int16 pairs; big endian swaps the two bytes of every sample.
-                        // v_perm_b32(s0=r, s1=l): selector bytes 0-3 pick l, 4-7 pick r.
-                        const uint32_t sel0 = big_endian ? 0x04050001u : 0x05040100u;
-                        const uint32_t sel1 = big_endian ? 0x06070203u : 0x07060302u;
-                        v4u o;
-                        o.x = __builtin_amdgcn_perm(r.x, l.x, sel0);
-                        o.y = __builtin_amdgcn_perm(r.x, l.x, sel1);
-                        o.z = __builtin_amdgcn_perm(r.y, l.y, sel0);
-                        o.w = __builtin_amdgcn_perm(r.y, l.y, sel1);
-                        v4u* dst = reinterpret_cast<v4u*>(reinterpret_cast<uint8_t*>(A.pcm) + (size_t)f * 4096 + 4 * p);
-                        __builtin_nontemporal_store(o, dst);
-                    }
+                    for (int jj = 0; jj < 4; jj++)
+                        __builtin_nontemporal_store(*reinterpret_cast<const v4u*>(W.rsp + 4 * u2 + 256 * jj),
+                                                    reinterpret_cast<v4u*>(dst + 16 * u2 + 1024 * jj));
                 }
             }
-#ifndef JAAD_ABL_NO_BARRIER
-            __syncthreads();  // B4
-#endif  // PCM staging buffers may be reused
-                };
-        for (int it = 0; it < n_iter; it += 2) {
-            frame(it, pf);
-            if (it + 1 < n_iter) frame(it + 1, pf2);
         }
-        STAMP(31);
         if (cd.info & kChunkStoreState) {
             const int u = lane_id();
-            float* st = A.state_out + (size_t)cd.slot * 2048 + 1024 * c;
+            float* st = A.state_out + (size_t)cd.slot * 2048;
 #pragma unroll
-            for (int o = 0; o < 16; o++) st[long_pos(u, o)] = ov[o];
+            for (int o = 0; o < 16; o++) {
+                st[long_pos(u, o)] = ovL[o];
+                if (stereo) st[1024 + long_pos(u, o)] = ovR[o];
+            }
         }
     }
 }
 
-hipError_t launch_lc(const KernelArgs& a, int grid, hipStream_t stream, bool tns_spec)
+hipError_t launch_lc(const KernelArgs& a, hipStream_t stream, bool tns_spec)
 {
-#define JAAD_LAUNCH(T, O) hipLaunchKernelGGL((lc_decode_kernel<T, O>), dim3(grid), dim3(kWGThreads), 0, stream, a)
+#define JAAD_LAUNCH(T, O)                                                                                  \
+    hipLaunchKernelGGL((lc_decode_kernel<T, O>), dim3((a.n_chunks + waves_per_wg<T>() - 1) / waves_per_wg<T>()), \
+                       dim3(64 * waves_per_wg<T>()), 0, stream, a)
     const int o = (a.out_mode == kOutPlanarF32) ? 4 : (a.out_mode & JAAD_PCM_FLOAT32) ? 2 : (a.out_mode & JAAD_PCM_LITTLE_ENDIAN) ? 1 : 0;
     if (o == 4) {
         if (tns_spec) JAAD_LAUNCH(true, kOutPlanarF32);
@@ -990,6 +1009,17 @@ hipError_t launch_lc(const KernelArgs& a, int grid, hipStream_t stream, bool tns
     }
 #undef JAAD_LAUNCH
     return hipGetLastError();
+}
+
+int lc_resident_waves_per_cu(bool tns_spec)
+{
+    int blocks = 0;
+    hipError_t e = tns_spec ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, lc_decode_kernel<true, JAAD_PCM_BIG_ENDIAN>,
+                                                                            64 * waves_per_wg<true>(), 0)
+                            : hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, lc_decode_kernel<false, JAAD_PCM_BIG_ENDIAN>,
+                                                                            64 * waves_per_wg<false>(), 0);
+    if (e != hipSuccess) return 0;
+    return blocks * (tns_spec ? waves_per_wg<true>() : waves_per_wg<false>());
 }
 
 }  // namespace jaad

@@ -1,4 +1,4 @@
-"""Build experimental variants of libjaadgpu.so into .tmp/exp/ (ablation macros of jaad_lc.hip)."""
+"""Build experimental variants of libjaadgpu.so into .tmp/exp/ (ablation macros of the kernels)."""
 import sys
 from pathlib import Path
 
@@ -8,11 +8,14 @@ from jaadec_amd import build as B  # noqa: E402
 
 VARIANTS = {
     "a_base": [],
-    "b_hf_no_gen": ["JAAD_HF_SKIP_GEN"],
-    "c_hf_no_est": ["JAAD_HF_SKIP_EST"],
-    "d_hf_no_gain": ["JAAD_HF_SKIP_GAIN"],
-    "e_hf_no_asm": ["JAAD_HF_SKIP_ASM"],
-    "f_hf_none": ["JAAD_HF_SKIP_GEN", "JAAD_HF_SKIP_EST", "JAAD_HF_SKIP_GAIN", "JAAD_HF_SKIP_ASM"],
+    "b_no_barrier": ["JAAD_ABL_NO_BARRIER"],
+    "c_no_imdct": ["JAAD_ABL_NO_IMDCT"],
+    "d_no_ms": ["JAAD_ABL_NO_MS"],
+    "e_no_iq": ["JAAD_ABL_NO_IQ"],
+    "f_no_store": ["JAAD_ABL_NO_STORE"],
+    "g_no_pcmlds": ["JAAD_ABL_NO_PCMLDS"],
+    "h_skeleton": ["JAAD_ABL_NO_IMDCT", "JAAD_ABL_NO_MS", "JAAD_ABL_NO_IQ"],
+    "i_skel_nobar": ["JAAD_ABL_NO_IMDCT", "JAAD_ABL_NO_MS", "JAAD_ABL_NO_IQ", "JAAD_ABL_NO_BARRIER"],
 }
 
 if __name__ == "__main__":
@@ -21,7 +24,7 @@ if __name__ == "__main__":
     for f in out.glob("lib_*.so"):
         f.unlink()
     only = set(sys.argv[1:])
-    for name, defs in VARIANTS.items():
-        if only and name not in only:
-            continue
-        B.build_gpu(out=out / f"lib_{name}.so", defines=defs)
+    from concurrent.futures import ThreadPoolExecutor
+    todo = [(n, d) for n, d in VARIANTS.items() if not only or n in only]
+    with ThreadPoolExecutor(6) as ex:
+        list(ex.map(lambda nd: B.build_gpu(out=out / f"lib_{nd[0]}.so", defines=nd[1]), todo))
