@@ -46,17 +46,18 @@ def _deps(*globs: str) -> list[Path]:
     return out
 
 
-def build_gpu(force: bool = False, out: Path | None = None, defines: list[str] | None = None) -> Path:
+def build_gpu(force: bool = False, out: Path | None = None, defines: list[str] | None = None,
+              extra: list[str] | None = None) -> Path:
     """Build the product library (or, with `defines`, an experimental variant at `out`)."""
     out = out or LIB
     srcs = [CSRC / "jaad_lc.hip", CSRC / "jaad_sbr.hip", CSRC / "jaad_ps.hip", CSRC / "jaad_capi.cpp", CSRC / "jaad_sbr_host.cpp"]
     deps = srcs + _deps("jaadec_amd/csrc/*.h", "jaadec_amd/csrc/tables/*.inc", "include/*.h")
-    if force or defines or _stale(out, deps):
+    if force or defines or extra or _stale(out, deps):
         tmp = out.with_suffix(".so.tmp")
         _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-              "-ffp-contract=off", "-fno-gpu-rdc", "-Wall", "-Wno-unused-function",
+              "-ffp-contract=off", "-fno-slp-vectorize", "-fno-gpu-rdc", "-Wall", "-Wno-unused-function",
               "-I", str(ROOT / "include"), "-o", str(tmp)] + [f"-D{d}" for d in (defines or [])]
-             + [str(s) for s in srcs])
+             + (extra or []) + [str(s) for s in srcs])
         tmp.replace(out)
     return out
 

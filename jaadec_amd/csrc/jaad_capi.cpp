@@ -224,7 +224,11 @@ void build_lds_tables(int sf_index, LdsTables* t, GlobalTables* gt)
         for (int e = 0; e < 2; e++) root(16 * (b + 8 * e), t->tw2[1 + e][b]);
         for (int s = 0; s < 4; s++) root(8 * (b + 8 * s), t->tw2[3 + s][b]);
     }
-    for (int k = 0; k < 256; k++) root(k, t->roots_l[k]);
+    for (int u = 0; u < 64; u++) {  // pass 3: j = 0 -> 4u, j = 1,2 -> 2(u + 64e), j = 3..6 -> u + 64s
+        root(4 * u, t->tw3[0][u]);
+        for (int e = 0; e < 2; e++) root(2 * (u + 64 * e), t->tw3[1 + e][u]);
+        for (int s = 0; s < 4; s++) root(u + 64 * s, t->tw3[3 + s][u]);
+    }
     std::memcpy(t->mdct_s, JAAD_MDCT_TABLE_128, sizeof(t->mdct_s));
     for (int k = 0; k < 32; k++) {
         t->roots_s[k][0] = JAAD_FFT_TABLE_64[k][0];

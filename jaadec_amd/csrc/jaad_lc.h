@@ -27,7 +27,7 @@ enum : uint32_t { kChunkPrefix = 1u << 16, kChunkLoadState = 1u << 17, kChunkSto
 struct alignas(16) LdsTables {
     float win_slot[2][16][64];  // long window [shape][slot o][lane u] = W[long_pos(u,o)] (SINE/KBD_1024)
     float mdct_l[512][2];       // MDCT_TABLE_2048 (A/filterbank/MDCTTables.java:5), k order
-    float roots_l[256][2];      // FFT_TABLE_512[k][0..1], k < 256 (A/filterbank/FFTTables.java:5)
+    float tw3[7][64][2];        // 512-pt IFFT pass-3 twiddles [j][lane] (FFT_TABLE_512, A/filterbank/FFTTables.java:5)
     float tw2[7][8][2];         // 512-pt IFFT pass-2 twiddles [j][lane&7]
     float tw1[4][2];            // 512-pt IFFT pass-1 (i = 4) twiddles
     float win_short[2][128];    // SINE_128, KBD_128

@@ -66,6 +66,14 @@ __device__ __forceinline__ int eo_idx(int p)
 }
 // IFFT transpose layout (complex index): one pad slot every 16 (<= 2-way conflicts, affine)
 __device__ __forceinline__ int xs(int i) { return i + (i >> 4); }
+// long-window IFFT transpose layout: slot = sum of per-bit weights {1,2,4,8,16,33,72,138,276}
+// (550 slots).  Additive per bit, so the compile-time index bits of every access fold into the
+// instruction offset; the weights were searched (tools/lds_sim.py model of the gfx950 LDS
+// lane groups) to leave 16 extra bank cycles over the 32 transpose accesses (i + i/16: 96).
+__device__ __forceinline__ int xs_l(int i)
+{
+    return (i & 31) + ((i >> 5) & 1) * 33 + ((i >> 6) & 1) * 72 + ((i >> 7) & 1) * 138 + ((i >> 8) & 1) * 276;
+}
 
 __device__ constexpr int BR3[8] = {0, 4, 2, 6, 1, 5, 3, 7};
 
@@ -190,14 +198,16 @@ __device__ __forceinline__ void imdct_long(float* buf, const LdsTables& T, int u
     fft_pass1(re, im, T.tw1, 1);
     float2* X = reinterpret_cast<float2*>(buf);
     const int t = (int)(__builtin_bitreverse32((uint32_t)u) >> 26);
+    const int x1 = xs_l(8 * t);
 #pragma unroll
-    for (int r = 0; r < 8; r++) X[xs(8 * t + r)] = make_float2(re[BR3[r]], im[BR3[r]]);
+    for (int r = 0; r < 8; r++) X[x1 + r] = make_float2(re[BR3[r]], im[BR3[r]]);
     wave_sync();
     // pass 2: elements 64a + b + 8s, stages i = 8, 16, 32
     const int a = u >> 3, b = u & 7;
+    const int x2 = xs_l(64 * a + b);
 #pragma unroll
     for (int s = 0; s < 8; s++) {
-        float2 v = X[xs(64 * a + b + 8 * s)];
+        float2 v = X[x2 + xs_l(8 * s)];
         re[s] = v.x;
         im[s] = v.y;
     }
@@ -206,21 +216,21 @@ __device__ __forceinline__ void imdct_long(float* buf, const LdsTables& T, int u
         wi = T.tw2[j][b][1];
     });
 #pragma unroll
-    for (int s = 0; s < 8; s++) X[xs(64 * a + b + 8 * s)] = make_float2(re[s], im[s]);
+    for (int s = 0; s < 8; s++) X[x2 + xs_l(8 * s)] = make_float2(re[s], im[s]);
     wave_sync();
     // pass 3: elements u + 64 s, stages i = 64, 128, 256
+    const int x3 = xs_l(u);
 #pragma unroll
     for (int s = 0; s < 8; s++) {
-        float2 v = X[xs(u + 64 * s)];
+        float2 v = X[x3 + xs_l(64 * s)];
         re[s] = v.x;
         im[s] = v.y;
     }
     wave_sync();
     // stages 64 (m = 4, k = u), 128 (m = 2, k = u + 64e), 256 (m = 1, k = u + 64s)
     fft_3stages(re, im, [&](int j, float& wr, float& wi) {
-        const int idx = j == 0 ? 4 * u : (j < 3 ? 2 * (u + 64 * (j - 1)) : u + 64 * (j - 3));
-        wr = T.roots_l[idx][0];
-        wi = T.roots_l[idx][1];
+        wr = T.tw3[j][u][0];
+        wi = T.tw3[j][u][1];
     });
 #pragma unroll
     for (int s = 0; s < 8; s++) {  // MDCT.java:48-53
@@ -603,7 +613,11 @@ __device__ __forceinline__ void prefetch(const KernelArgs& A, int f, bool stereo
 #pragma unroll
     for (int c = 0; c < 2; c++) {
         if (c == 1 && !stereo) break;
+#ifdef JAAD_ABL_NO_LOADS
+        const size_t cf = (size_t)(f & 7) * nch + c;  // ablation: inputs stay cache resident
+#else
         const size_t cf = (size_t)f * nch + c;
+#endif
         const v4i* q = reinterpret_cast<const v4i*>(A.q + cf * 1024);
         pf.q[c][0] = __builtin_nontemporal_load(q + u);
         pf.q[c][1] = __builtin_nontemporal_load(q + 64 + u);
@@ -622,21 +636,25 @@ __device__ __forceinline__ void iq_channel(const LdsTables& T, const float* iq_g
                                            const float (&g)[4], float (&x)[16])
 {
     bool esc = false;
+    // all 16 table reads are issued before the first is consumed (one LDS round trip, not 16)
+    float v[16];
 #pragma unroll
-    for (int h = 0; h < 2; h++) {
-        const int16_t* qv = reinterpret_cast<const int16_t*>(&q[h]);
+    for (int e = 0; e < 16; e++) {
+        const int qq = reinterpret_cast<const int16_t*>(&q[e >> 3])[e & 7];
+        const int qc = qq < -128 ? -128 : (qq > 127 ? 127 : qq);
+        esc |= qc != qq;
+#ifdef JAAD_ABL_NO_IQ
+        v[e] = (float)qc;
+#else
+        v[e] = T.iq_signed[qc + 128];
+#endif
+    }
+    __builtin_amdgcn_sched_group_barrier(0x0100, 16, 0);  // the 16 DS reads first
+    __builtin_amdgcn_sched_group_barrier(0x0002, 64, 0);  // then the VALU
 #pragma unroll
-        for (int j = 0; j < 2; j++) {
-            const float gn = g[2 * h + j];
-#pragma unroll
-            for (int i = 0; i < 4; i++) {
-                const int qq = qv[4 * j + i];
-                const int qc = qq < -128 ? -128 : (qq > 127 ? 127 : qq);
-                esc |= qc != qq;
-                const float m = T.iq_signed[qc + 128] * gn;
-                x[8 * h + 4 * j + i] = gn != 0.0f ? m : 0.0f;
-            }
-        }
+    for (int e = 0; e < 16; e++) {
+        const float gn = g[e >> 2];
+        x[e] = gn != 0.0f ? v[e] * gn : 0.0f;
     }
     if (__builtin_expect(__ballot(esc) != 0, 0)) {  // escape values beyond the LDS head of IQ_TABLE
 #pragma unroll
@@ -675,11 +693,35 @@ __device__ __forceinline__ void synth_channel(const KernelArgs& A, const LdsTabl
         imdct_short(buf, T, u, re, im);
         ola_short(buf, T, u, fc, re, im, ov, out);
     } else {
+#ifdef JAAD_ABL_NO_IMDCT
+#pragma unroll
+        for (int o = 0; o < 16; o++) {
+            out[o] = buf[o * 64 + u] + ov[o];
+            ov[o] = out[o] * 0.5f;
+        }
+#else
         imdct_long(buf, T, u, re, im);
         ola_long(T, u, fc, re, im, ov, out);
+#endif
     }
     wave_sync();
 }
+
+#ifdef JAAD_STAMPS
+// per-phase wave-time accounting (ablation/profiling builds only): phase k gets the s_memtime
+// ticks since the previous stamp; lane 0 writes the 16 totals of each wave to A.dbg
+#define STAMP(k)                                                  \
+    do {                                                          \
+        uint64_t t_;                                              \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
+        st_acc[k] += (uint32_t)(t_ - st_prev);                    \
+        st_prev = t_;                                             \
+    } while (0)
+#else
+#define STAMP(k) \
+    do {         \
+    } while (0)
+#endif
 
 template <bool kTnsSpec, int kOut>
 __global__ __launch_bounds__(64 * waves_per_wg<kTnsSpec>()) void lc_decode_kernel(KernelArgs A)
@@ -723,6 +765,11 @@ __global__ __launch_bounds__(64 * waves_per_wg<kTnsSpec>()) void lc_decode_kerne
         }
     }
 
+#ifdef JAAD_STAMPS
+    uint32_t st_acc[16] = {};
+    uint64_t st_prev;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_prev)::"memory");
+#endif
     for (uint32_t ci = blockIdx.x * kW + wave; ci < A.n_chunks; ci += gridDim.x * kW) {
         const ChunkDesc cd = A.chunks[ci];
         const int nfr = cd.info & 0xffff;
@@ -770,6 +817,7 @@ __global__ __launch_bounds__(64 * waves_per_wg<kTnsSpec>()) void lc_decode_kerne
                      ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(cur.side, 11) << 32);
             }
 
+            STAMP(0);
             // ---------------- band records (lane u: bands 2u, 2u+1) ----------------
             wave_sync();
             raw[u] = cur.sfcb[0];
@@ -813,6 +861,7 @@ __global__ __launch_bounds__(64 * waves_per_wg<kTnsSpec>()) void lc_decode_kerne
             wave_sync();
 
             // ---------------- inverse quantisation, PNS, M/S, I/S ----------------
+            STAMP(1);
             float gL[4], gR[4], msq[4], isq[4];
 #pragma unroll
             for (int qd = 0; qd < 4; qd++) {
@@ -858,6 +907,7 @@ __global__ __launch_bounds__(64 * waves_per_wg<kTnsSpec>()) void lc_decode_kerne
                     load_spec(W.buf, u, xR);
                 }
             }
+            STAMP(2);
             if (ms_on) {  // MS.java:28-33: L' = L + R, R' = L - R (no scaling)
 #pragma unroll
                 for (int qd = 0; qd < 4; qd++) {
@@ -885,6 +935,7 @@ __global__ __launch_bounds__(64 * waves_per_wg<kTnsSpec>()) void lc_decode_kerne
                 }
             }
 
+            STAMP(3);
             // left spectrum -> buf (E/O layout); right spectrum parked in rsp (lane-linear)
             wave_sync();
             store_spec(W.buf, u, xL);
@@ -895,6 +946,7 @@ __global__ __launch_bounds__(64 * waves_per_wg<kTnsSpec>()) void lc_decode_kerne
             }
             wave_sync();
 
+            STAMP(4);
             // ---------------- per channel: IMDCT, window/OLA, PCM ----------------
             // int16 PCM is staged in rsp as the frame's interleaved SampleBuffer image (word P =
             // sample P of L and R); channel c's samples wait in pk until rsp is free.
@@ -923,8 +975,10 @@ __global__ __launch_bounds__(64 * waves_per_wg<kTnsSpec>()) void lc_decode_kerne
                     }
                     wave_sync();
                 }
+                STAMP(c ? 7 : 5);
                 float out[16];
                 synth_channel<kTnsSpec>(A, T, W, ic, cf0 + c, ov, out);
+                STAMP(c ? 8 : 6);
                 if (emit) {
                     const int u2 = lane_id();
                     if constexpr (planar) {
@@ -953,6 +1007,7 @@ __global__ __launch_bounds__(64 * waves_per_wg<kTnsSpec>()) void lc_decode_kerne
             };
             channel(0, ovL);
             if (stereo) channel(1, ovR);
+            STAMP(9);
             if constexpr (out_i16) {
                 if (emit) {
                     const int u2 = lane_id();
@@ -972,11 +1027,16 @@ __global__ __launch_bounds__(64 * waves_per_wg<kTnsSpec>()) void lc_decode_kerne
                     uint8_t* dst = reinterpret_cast<uint8_t*>(A.pcm) + (size_t)f * 4096;
 #pragma unroll
                     for (int jj = 0; jj < 4; jj++)
+#ifdef JAAD_ABL_NO_STORE
+                        if (A.n_chunks == 0)
+#endif
                         __builtin_nontemporal_store(*reinterpret_cast<const v4u*>(W.rsp + 4 * u2 + 256 * jj),
                                                     reinterpret_cast<v4u*>(dst + 16 * u2 + 1024 * jj));
                 }
             }
+            STAMP(10);
         }
+        STAMP(11);
         if (cd.info & kChunkStoreState) {
             const int u = lane_id();
             float* st = A.state_out + (size_t)cd.slot * 2048;
@@ -987,6 +1047,12 @@ __global__ __launch_bounds__(64 * waves_per_wg<kTnsSpec>()) void lc_decode_kerne
             }
         }
     }
+#ifdef JAAD_STAMPS
+    if (A.dbg && lane_id() == 0) {
+        uint32_t* o = reinterpret_cast<uint32_t*>(A.dbg) + (size_t)(blockIdx.x * kW + wave) * 16;
+        for (int k = 0; k < 16; k++) o[k] = st_acc[k];
+    }
+#endif
 }
 
 hipError_t launch_lc(const KernelArgs& a, hipStream_t stream, bool tns_spec)

@@ -7,15 +7,8 @@ sys.path.insert(0, str(ROOT))
 from jaadec_amd import build as B  # noqa: E402
 
 VARIANTS = {
-    "a_base": [],
-    "b_no_barrier": ["JAAD_ABL_NO_BARRIER"],
-    "c_no_imdct": ["JAAD_ABL_NO_IMDCT"],
-    "d_no_ms": ["JAAD_ABL_NO_MS"],
-    "e_no_iq": ["JAAD_ABL_NO_IQ"],
-    "f_no_store": ["JAAD_ABL_NO_STORE"],
-    "g_no_pcmlds": ["JAAD_ABL_NO_PCMLDS"],
-    "h_skeleton": ["JAAD_ABL_NO_IMDCT", "JAAD_ABL_NO_MS", "JAAD_ABL_NO_IQ"],
-    "i_skel_nobar": ["JAAD_ABL_NO_IMDCT", "JAAD_ABL_NO_MS", "JAAD_ABL_NO_IQ", "JAAD_ABL_NO_BARRIER"],
+    "a_base": ([], []),
+    "s_stamps": (["JAAD_STAMPS"], []),
 }
 
 if __name__ == "__main__":
@@ -27,4 +20,4 @@ if __name__ == "__main__":
     from concurrent.futures import ThreadPoolExecutor
     todo = [(n, d) for n, d in VARIANTS.items() if not only or n in only]
     with ThreadPoolExecutor(6) as ex:
-        list(ex.map(lambda nd: B.build_gpu(out=out / f"lib_{nd[0]}.so", defines=nd[1]), todo))
+        list(ex.map(lambda nd: B.build_gpu(out=out / f"lib_{nd[0]}.so", defines=nd[1][0], extra=nd[1][1]), todo))

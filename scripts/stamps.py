@@ -1,6 +1,6 @@
-"""Run a JAAD_STAMPS build on C2 and summarize per-wave phase timings (s_memtime ticks)."""
+"""Run a JAAD_STAMPS build (JAAD_LIB=...) on C2 and print the per-phase share of wave time
+(s_memtime ticks summed over each wave's frames; median over waves)."""
 import ctypes as C
-import os
 import sys
 from pathlib import Path
 
@@ -11,27 +11,30 @@ ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 from jaadec_amd import native as N  # noqa: E402
 
-p = N.synth_params(2); b = N.synth_batch(p); cfg = N.make_cfg()
+cfgid = int(sys.argv[1]) if len(sys.argv) > 1 else 2
+p = N.synth_params(cfgid); b = N.synth_batch(p); cfg = N.cfg_for(p)
 dev = torch.device("cuda", 0)
 t = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1)).to(dev)
-d = {"q": t(b.q), "sf": t(b.sf), "cb": t(b.cb), "ics": t(b.ics), "ms_used": t(b.ms_used)}
+d = {"q": t(b.q), "sf": t(b.sf), "cb": t(b.cb), "ics": t(b.ics)}
+if b.ms_used is not None: d["ms_used"] = t(b.ms_used)
 ptr = {k: v.data_ptr() for k, v in d.items()}
-pcm = torch.empty(b.n_frames * 4096, dtype=torch.uint8, device=dev)
-ctx = N.Context(cfg, 256)
-nw = 4096 * 4
-dbg = torch.zeros(nw * 32, dtype=torch.int32, device=dev)
+ptr.setdefault("ms_used", None); ptr["tns"] = None
+pcm = torch.empty(b.n_frames * N.pcm_frame_bytes(0, bool(p.sbr)), dtype=torch.uint8, device=dev)
+ctx = N.Context(cfg, int(b.stream_slot.max()) + 1)
+nw = 8192
+dbg = torch.zeros(nw * 16, dtype=torch.int32, device=dev)
 N.lib().jaad__debug_attach.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
 N.lib().jaad__debug_attach(ctx.h, dbg.data_ptr(), -1)
 for _ in range(3):
     ctx.decode_device(ptr, b, pcm.data_ptr(), pcm.numel(), 0, None)
 torch.cuda.synchronize()
-S = dbg.cpu().numpy().view(np.uint32).reshape(nw, 32).astype(np.int64)
-names = ["iter start", "side->LDS raw", "gain table", "IQ", "store_spec(+PNS) + B1 wait", "phase C", "B2 wait", "D: IMDCT+OLA+PCM->LDS", ]
-for it in range(3):
-    b0 = 2 + 9 * it
-    row = []
-    for k in range(7):
-        d = (S[:, b0 + k + 1] - S[:, b0 + k]) & 0xffffffff
-        row.append(np.median(d))
-    nxt = (S[:, b0 + 9] if it < 2 else S[:, 31])
-    print("it", 4 + it, " ".join(f"{names[k+1]}={row[k]:.0f}" for k in range(7)))
+S = dbg.cpu().numpy().view(np.uint32).reshape(nw, 16).astype(np.int64)
+S = S[S.sum(1) > 0]
+names = ["top: wait inputs, side info", "band records", "IQ (+prefetch issue)", "PNS/MS/IS", "store L, park R",
+         "c0 pre", "L synth (IMDCT+OLA)", "L PCM, unpark R, stage L", "R synth (IMDCT+OLA)", "R PCM",
+         "stage R + stores", "chunk tail"]
+med = np.median(S, axis=0)
+tot = med[:12].sum()
+for k in range(12):
+    print(f"{k:2d} {names[k]:32s} {med[k]:12.0f} ticks {100 * med[k] / tot:5.1f} %")
+print("waves", S.shape[0], "total median ticks", tot)
