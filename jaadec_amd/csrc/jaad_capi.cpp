@@ -205,7 +205,7 @@ void build_lds_tables(int sf_index, LdsTables* t, GlobalTables* gt)
     const float* LW[2] = {JAAD_SINE_1024, JAAD_KBD_1024};
     for (int sh = 0; sh < 2; sh++)
         for (int o = 0; o < 16; o++)
-            for (int u = 0; u < 64; u++) t->win_slot[sh][o][u] = LW[sh][long_pos_host(u, o)];
+            for (int u = 0; u < 64; u++) t->win_pair[sh][o >> 1][u][o & 1] = LW[sh][long_pos_host(u, o)];
     std::memcpy(t->win_short[0], JAAD_SINE_128, sizeof(t->win_short[0]));
     std::memcpy(t->win_short[1], JAAD_KBD_128, sizeof(t->win_short[1]));
     std::memcpy(t->mdct_l, JAAD_MDCT_TABLE_2048, sizeof(t->mdct_l));

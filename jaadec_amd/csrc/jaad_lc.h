@@ -25,7 +25,7 @@ enum : uint32_t { kChunkPrefix = 1u << 16, kChunkLoadState = 1u << 17, kChunkSto
 // csrc/tables/jaad_tables.inc), pre-permuted so that every lane-parallel read is
 // bank-conflict free.  Built by the host (build_lds_tables), copied verbatim by the prologue.
 struct alignas(16) LdsTables {
-    float win_slot[2][16][64];  // long window [shape][slot o][lane u] = W[long_pos(u,o)] (SINE/KBD_1024)
+    float win_pair[2][8][64][2];  // long window [shape][s][lane u][h] = W[long_pos(u,2s+h)] (SINE/KBD_1024)
     float mdct_l[512][2];       // MDCT_TABLE_2048 (A/filterbank/MDCTTables.java:5), k order
     float tw3[7][64][2];        // 512-pt IFFT pass-3 twiddles [j][lane] (FFT_TABLE_512, A/filterbank/FFTTables.java:5)
     float tw2[7][8][2];         // 512-pt IFFT pass-2 twiddles [j][lane&7]

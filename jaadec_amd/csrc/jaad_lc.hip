@@ -52,6 +52,9 @@ __device__ __forceinline__ void wave_sync()
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // and no forwarding of a lane's own LDS stores across the point either: values parked in
+    // LDS (e.g. the right spectrum during the left IMDCT) must leave the registers
+    asm volatile("" ::: "memory");
 }
 
 constexpr int kWaveBuf = 1152;  // floats of LDS per wave
@@ -244,7 +247,7 @@ __device__ __forceinline__ void imdct_long(float* buf, const LdsTables& T, int u
 
 // FilterBank.process for ONLY_LONG / LONG_START / LONG_STOP (FilterBank.java:41-70, 102-119).
 // Lane u's slot (s,h) holds output position P = long_pos(u, 2s+h); its mirror 1023-P is slot
-// (s,1-h) of the same lane, so the falling window W[1023-P] is win_slot[shape][o^1][u].
+// (s,1-h) of the same lane, so the falling window W[1023-P] is the other half of the pair.
 // Specialised per sequence so the common ONLY_LONG path carries no joint-window logic.
 template <int kSeq>
 __device__ __forceinline__ void ola_long_t(const LdsTables& T, const FrameCtx& fc, const float (&re)[8],
@@ -253,10 +256,14 @@ __device__ __forceinline__ void ola_long_t(const LdsTables& T, const FrameCtx& f
     const int u = lane_id();
     const float* SWp = T.win_short[fc.shape_prev];
     const float* SWc = T.win_short[fc.shape];
-    const float* Wp = &T.win_slot[fc.shape_prev][0][0];
-    const float* Wc = &T.win_slot[fc.shape][0][0];
+    // win_pair[shape][s][u] = {W[pos(u, 2s)], W[pos(u, 2s+1)]}: one 8-byte read per slot pair
+    const float2* Wp = reinterpret_cast<const float2*>(&T.win_pair[fc.shape_prev][0][0][0]);
+    const float2* Wc = reinterpret_cast<const float2*>(&T.win_pair[fc.shape][0][0][0]);
 #pragma unroll
     for (int s = 0; s < 8; s++) {
+        float2 wp = make_float2(0.0f, 0.0f), wc = make_float2(0.0f, 0.0f);
+        if constexpr (kSeq != JAAD_LONG_STOP_SEQUENCE) wp = Wp[64 * s + u];
+        if constexpr (kSeq != JAAD_LONG_START_SEQUENCE) wc = Wc[64 * s + u];
 #pragma unroll
         for (int h = 0; h < 2; h++) {
             const int o = 2 * s + h;
@@ -275,7 +282,7 @@ __device__ __forceinline__ void ola_long_t(const LdsTables& T, const FrameCtx& f
                 else if (P < 576) o_v = ov[o] + (f * SWp[P - 448]);
                 else o_v = ov[o] + f;
             } else {
-                o_v = ov[o] + (f * Wp[64 * o + u]);
+                o_v = ov[o] + (f * (h ? wp.y : wp.x));  // rising window W[P]
             }
             if constexpr (kSeq == JAAD_LONG_START_SEQUENCE) {
                 const int P = long_pos(u, o);
@@ -283,7 +290,7 @@ __device__ __forceinline__ void ola_long_t(const LdsTables& T, const FrameCtx& f
                 else if (P < 576) n_v = g * SWc[127 - (P - 448)];
                 else n_v = 0.0f;
             } else {
-                n_v = g * Wc[64 * (o ^ 1) + u];
+                n_v = g * (h ? wc.x : wc.y);  // falling window W[1023-P] = slot o^1
             }
             out[o] = o_v;
             ov[o] = n_v;
@@ -514,7 +521,7 @@ __device__ __forceinline__ uint32_t round_pk16(float a, float b)
     return w;
 }
 
-// per-wave LDS area: 8.5 KiB (12 waves + the table image: 123 KiB of a CU's 160 KiB)
+// per-wave LDS area: 8.5 KiB (16 waves + the 20 KiB table image fill a CU's 160 KiB)
 //   buf  band records [0,512) + raw sf/cb rows [512,640) -> spectrum (E/O) -> IFFT transposes ->
 //        OLA scratch -> PCM staging
 //   rsp  the right channel's spectrum while the left one is transformed (PNS: raw row copy)
@@ -529,10 +536,13 @@ struct alignas(16) WaveLds<true> {
     float rsp[1024];
     float tns[192];  // spec-TNS LPC scratch (8 filters x 24)
 };
+#ifndef JAAD_LC_WAVES
+#define JAAD_LC_WAVES 16
+#endif
 template <bool kTns>
 constexpr int waves_per_wg()
 {
-    return kTns ? 8 : 12;
+    return kTns ? 8 : JAAD_LC_WAVES;
 }
 constexpr int kRawOff = 512;  // raw rows in buf: channel c's 64 dwords at buf[kRawOff + 64c]
 
@@ -657,22 +667,15 @@ __device__ __forceinline__ void iq_channel(const LdsTables& T, const float* iq_g
         x[e] = gn != 0.0f ? v[e] * gn : 0.0f;
     }
     if (__builtin_expect(__ballot(esc) != 0, 0)) {  // escape values beyond the LDS head of IQ_TABLE
+        // uniform branch; every lane loads and selects (no exec-masked partial register writes)
 #pragma unroll
-        for (int h = 0; h < 2; h++) {
-            const int16_t* qv = reinterpret_cast<const int16_t*>(&q[h]);
-#pragma unroll
-            for (int j = 0; j < 2; j++) {
-                const float gn = g[2 * h + j];
-#pragma unroll
-                for (int i = 0; i < 4; i++) {
-                    const int qq = qv[4 * j + i];
-                    const int aq = qq < 0 ? -qq : qq;
-                    if ((qq > 127 || qq < -128) && gn != 0.0f) {
-                        const float m = iq_global[aq > 8190 ? 8190 : aq] * gn;
-                        x[8 * h + 4 * j + i] = qq > 0 ? m : -m;
-                    }
-                }
-            }
+        for (int e = 0; e < 16; e++) {
+            const int qq = reinterpret_cast<const int16_t*>(&q[e >> 3])[e & 7];
+            const int aq = qq < 0 ? -qq : qq;
+            const float gn = g[e >> 2];
+            const float m = iq_global[aq > 8190 ? 8190 : aq] * gn;
+            const bool big = (qq > 127 || qq < -128) && gn != 0.0f;
+            x[e] = big ? (qq > 0 ? m : -m) : x[e];
         }
     }
 }
@@ -723,7 +726,7 @@ __device__ __forceinline__ void synth_channel(const KernelArgs& A, const LdsTabl
     } while (0)
 #endif
 
-template <bool kTnsSpec, int kOut>
+template <bool kTnsSpec, int kOut, bool kStereo>
 __global__ __launch_bounds__(64 * waves_per_wg<kTnsSpec>()) void lc_decode_kernel(KernelArgs A)
 {
     constexpr int kW = waves_per_wg<kTnsSpec>();
@@ -748,8 +751,10 @@ __global__ __launch_bounds__(64 * waves_per_wg<kTnsSpec>()) void lc_decode_kerne
     constexpr bool out_f32 = (kOut & JAAD_PCM_FLOAT32) != 0 && !planar;
     constexpr bool out_i16 = !planar && !out_f32;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const bool stereo = A.nch == 2;
-    const int nch = stereo ? 2 : 1;
+    // channel count is a template parameter: a run-time flag would leave the register allocator
+    // with paths where the right channel's values live across frames
+    constexpr bool stereo = kStereo;
+    constexpr int nch = stereo ? 2 : 1;
     WaveLds<kTnsSpec>& W = S.W[wave];
     uint32_t* raw = reinterpret_cast<uint32_t*>(W.buf + kRawOff);
     BandRec* rec = reinterpret_cast<BandRec*>(W.buf);
@@ -863,10 +868,12 @@ __global__ __launch_bounds__(64 * waves_per_wg<kTnsSpec>()) void lc_decode_kerne
             // ---------------- inverse quantisation, PNS, M/S, I/S ----------------
             STAMP(1);
             float gL[4], gR[4], msq[4], isq[4];
+            uint32_t q2b = q2b_long;
+            asm volatile("" : "+v"(q2b));  // one packed register across frames, unpacked here
 #pragma unroll
             for (int qd = 0; qd < 4; qd++) {
                 const int p = 512 * (qd >> 1) + 8 * u + 4 * (qd & 1);
-                const int bl = iL.seq == JAAD_EIGHT_SHORT_SEQUENCE ? band_short(T, iL, p) : (int)((q2b_long >> (8 * qd)) & 255u);
+                const int bl = iL.seq == JAAD_EIGHT_SHORT_SEQUENCE ? band_short(T, iL, p) : (int)((q2b >> (8 * qd)) & 255u);
                 const float4 r = reinterpret_cast<const float4*>(rec)[bl];
                 gL[qd] = r.x;
                 msq[qd] = r.y;
@@ -874,16 +881,19 @@ __global__ __launch_bounds__(64 * waves_per_wg<kTnsSpec>()) void lc_decode_kerne
                     gR[qd] = r.z;
                     isq[qd] = r.w;
                 } else {
-                    const int br = iR.seq == JAAD_EIGHT_SHORT_SEQUENCE ? band_short(T, iR, p) : (int)((q2b_long >> (8 * qd)) & 255u);
+                    const int br = iR.seq == JAAD_EIGHT_SHORT_SEQUENCE ? band_short(T, iR, p) : (int)((q2b >> (8 * qd)) & 255u);
                     const float2 rr = reinterpret_cast<const float2*>(rec)[2 * br + 1];
                     gR[qd] = rr.x;
                     isq[qd] = rr.y;
                 }
             }
             float xL[16], xR[16];
+            STAMP(14);
             iq_channel(T, A.iq_table, cur.q[0], gL, xL);
+            STAMP(13);
             if (stereo) iq_channel(T, A.iq_table, cur.q[1], gR, xR);
             // the inputs are consumed: frame f+1's loads fly while this frame's IMDCTs run
+            STAMP(12);
             if (it + 1 < my_n) prefetch(A, f + 1, stereo, u, pf);
 
             if ((iL.flags | (stereo ? iR.flags : 0)) & JAAD_ICS_HAS_PNS) {  // rare: lane 0 replays the LCG
@@ -952,6 +962,8 @@ __global__ __launch_bounds__(64 * waves_per_wg<kTnsSpec>()) void lc_decode_kerne
             // sample P of L and R); channel c's samples wait in pk until rsp is free.
             uint16_t* stage16 = reinterpret_cast<uint16_t*>(W.rsp);
             uint32_t pk[8];
+            // PCM values are computed and staged for every frame (emit only gates the HBM stores):
+            // a staging step guarded by its own run-time test would keep pk live across frames
             auto channel = [&](const int c, float (&ov)[16]) {
                 const Ics& ic = c ? iR : iL;
                 if (c == 1) {
@@ -967,11 +979,9 @@ __global__ __launch_bounds__(64 * waves_per_wg<kTnsSpec>()) void lc_decode_kerne
                     }
                     store_spec(W.buf, u2, x);
                     if constexpr (out_i16) {
-                        if (emit) {
-                            wave_sync();
+                        wave_sync();
 #pragma unroll
-                            for (int o = 0; o < 16; o++) stage16[2 * long_pos(u2, o)] = (uint16_t)(pk[o >> 1] >> (16 * (o & 1)));
-                        }
+                        for (int o = 0; o < 16; o++) stage16[2 * long_pos(u2, o)] = (uint16_t)(pk[o >> 1] >> (16 * (o & 1)));
                     }
                     wave_sync();
                 }
@@ -979,9 +989,9 @@ __global__ __launch_bounds__(64 * waves_per_wg<kTnsSpec>()) void lc_decode_kerne
                 float out[16];
                 synth_channel<kTnsSpec>(A, T, W, ic, cf0 + c, ov, out);
                 STAMP(c ? 8 : 6);
-                if (emit) {
-                    const int u2 = lane_id();
-                    if constexpr (planar) {
+                const int u2 = lane_id();
+                if constexpr (planar) {
+                    if (emit) {
                         float* dst = reinterpret_cast<float*>(A.pcm) + (cf0 + c) * 1024;
 #pragma unroll
                         for (int o = 0; o < 16; o++) W.buf[long_pos(u2, o)] = out[o];
@@ -989,7 +999,9 @@ __global__ __launch_bounds__(64 * waves_per_wg<kTnsSpec>()) void lc_decode_kerne
 #pragma unroll
                         for (int jj = 0; jj < 4; jj++)
                             *reinterpret_cast<float4*>(dst + 4 * u2 + 256 * jj) = *reinterpret_cast<const float4*>(W.buf + 4 * u2 + 256 * jj);
-                    } else if constexpr (out_f32) {  // tolerance/debug format: strided stores
+                    }
+                } else if constexpr (out_f32) {  // tolerance/debug format: strided stores
+                    if (emit) {
                         float* dst = reinterpret_cast<float*>(reinterpret_cast<uint8_t*>(A.pcm) + (size_t)f * 8192);
 #pragma unroll
                         for (int o = 0; o < 16; o++) {
@@ -997,33 +1009,33 @@ __global__ __launch_bounds__(64 * waves_per_wg<kTnsSpec>()) void lc_decode_kerne
                             dst[2 * P + c] = out[o];
                             if (!stereo) dst[2 * P + 1] = out[o];
                         }
-                    } else {
-                        // big endian swaps the two bytes of every sample
-                        const uint32_t sel = big_endian ? 0x02030001u : 0x03020100u;
-#pragma unroll
-                        for (int m = 0; m < 8; m++) pk[m] = __builtin_amdgcn_perm(0u, round_pk16(out[2 * m], out[2 * m + 1]), sel);
                     }
+                } else {
+                    // big endian swaps the two bytes of every sample
+                    const uint32_t sel = big_endian ? 0x02030001u : 0x03020100u;
+#pragma unroll
+                    for (int m = 0; m < 8; m++) pk[m] = __builtin_amdgcn_perm(0u, round_pk16(out[2 * m], out[2 * m + 1]), sel);
                 }
             };
             channel(0, ovL);
             if (stereo) channel(1, ovR);
             STAMP(9);
             if constexpr (out_i16) {
-                if (emit) {
-                    const int u2 = lane_id();
-                    wave_sync();
+                const int u2 = lane_id();
+                wave_sync();
 #pragma unroll
-                    for (int o = 0; o < 16; o++) {
-                        const uint16_t v = (uint16_t)(pk[o >> 1] >> (16 * (o & 1)));
-                        const int P = long_pos(u2, o);
-                        if (stereo) {
-                            stage16[2 * P + 1] = v;
-                        } else {
-                            stage16[2 * P] = v;
-                            stage16[2 * P + 1] = v;
-                        }
+                for (int o = 0; o < 16; o++) {
+                    const uint16_t v = (uint16_t)(pk[o >> 1] >> (16 * (o & 1)));
+                    const int P = long_pos(u2, o);
+                    if (stereo) {
+                        stage16[2 * P + 1] = v;
+                    } else {
+                        stage16[2 * P] = v;
+                        stage16[2 * P + 1] = v;
                     }
-                    wave_sync();
+                }
+                wave_sync();
+                if (emit) {
                     uint8_t* dst = reinterpret_cast<uint8_t*>(A.pcm) + (size_t)f * 4096;
 #pragma unroll
                     for (int jj = 0; jj < 4; jj++)
@@ -1055,10 +1067,11 @@ __global__ __launch_bounds__(64 * waves_per_wg<kTnsSpec>()) void lc_decode_kerne
 #endif
 }
 
-hipError_t launch_lc(const KernelArgs& a, hipStream_t stream, bool tns_spec)
+template <bool kStereo>
+static hipError_t launch_lc_ch(const KernelArgs& a, hipStream_t stream, bool tns_spec)
 {
-#define JAAD_LAUNCH(T, O)                                                                                  \
-    hipLaunchKernelGGL((lc_decode_kernel<T, O>), dim3((a.n_chunks + waves_per_wg<T>() - 1) / waves_per_wg<T>()), \
+#define JAAD_LAUNCH(T, O)                                                                                           \
+    hipLaunchKernelGGL((lc_decode_kernel<T, O, kStereo>), dim3((a.n_chunks + waves_per_wg<T>() - 1) / waves_per_wg<T>()), \
                        dim3(64 * waves_per_wg<T>()), 0, stream, a)
     const int o = (a.out_mode == kOutPlanarF32) ? 4 : (a.out_mode & JAAD_PCM_FLOAT32) ? 2 : (a.out_mode & JAAD_PCM_LITTLE_ENDIAN) ? 1 : 0;
     if (o == 4) {
@@ -1077,12 +1090,17 @@ hipError_t launch_lc(const KernelArgs& a, hipStream_t stream, bool tns_spec)
     return hipGetLastError();
 }
 
+hipError_t launch_lc(const KernelArgs& a, hipStream_t stream, bool tns_spec)
+{
+    return a.nch == 2 ? launch_lc_ch<true>(a, stream, tns_spec) : launch_lc_ch<false>(a, stream, tns_spec);
+}
+
 int lc_resident_waves_per_cu(bool tns_spec)
 {
     int blocks = 0;
-    hipError_t e = tns_spec ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, lc_decode_kernel<true, JAAD_PCM_BIG_ENDIAN>,
+    hipError_t e = tns_spec ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, lc_decode_kernel<true, JAAD_PCM_BIG_ENDIAN, true>,
                                                                             64 * waves_per_wg<true>(), 0)
-                            : hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, lc_decode_kernel<false, JAAD_PCM_BIG_ENDIAN>,
+                            : hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, lc_decode_kernel<false, JAAD_PCM_BIG_ENDIAN, true>,
                                                                             64 * waves_per_wg<false>(), 0);
     if (e != hipSuccess) return 0;
     return blocks * (tns_spec ? waves_per_wg<true>() : waves_per_wg<false>());

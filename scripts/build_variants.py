@@ -7,8 +7,7 @@ sys.path.insert(0, str(ROOT))
 from jaadec_amd import build as B  # noqa: E402
 
 VARIANTS = {
-    "a_base": ([], []),
-    "s_stamps": (["JAAD_STAMPS"], []),
+    "s_stamps16": (["JAAD_STAMPS", "JAAD_LC_WAVES=16"], []),
 }
 
 if __name__ == "__main__":

@@ -32,9 +32,9 @@ S = dbg.cpu().numpy().view(np.uint32).reshape(nw, 16).astype(np.int64)
 S = S[S.sum(1) > 0]
 names = ["top: wait inputs, side info", "band records", "IQ (+prefetch issue)", "PNS/MS/IS", "store L, park R",
          "c0 pre", "L synth (IMDCT+OLA)", "L PCM, unpark R, stage L", "R synth (IMDCT+OLA)", "R PCM",
-         "stage R + stores", "chunk tail"]
+         "stage R + stores", "chunk tail", "IQ R (13->12)", "IQ L (14->13)", "rec reads (1->14)"]
 med = np.median(S, axis=0)
-tot = med[:12].sum()
-for k in range(12):
-    print(f"{k:2d} {names[k]:32s} {med[k]:12.0f} ticks {100 * med[k] / tot:5.1f} %")
+tot = med[:15].sum()
+for k in range(15):
+    print(f"{k:2d} {names[k]:32.32s} {med[k]:12.0f} ticks {100 * med[k] / tot:5.1f} %")
 print("waves", S.shape[0], "total median ticks", tot)

@@ -100,6 +100,11 @@ def main():
     if nctx:
         for i in range(max(0, peak - nctx), min(n, peak + nctx)):
             print(f'{i:6d} {len(live_in[i]):4d}  {insts[i]}')
+    # for every register live at the peak: the next instruction (in layout order, wrapping) that reads it
+    if len(sys.argv) > 6:
+        for r in sorted(live_in[peak]):
+            nxt = next((j for j in list(range(peak, n)) + list(range(0, peak)) if r in uses[j]), None)
+            print(f'  v{r:<4d} next use #{nxt}: {insts[nxt] if nxt is not None else "-"}'[:130])
     # live ranges spanning the peak: where each live register was last defined before it
     lastdef = {}
     for i in range(peak):
