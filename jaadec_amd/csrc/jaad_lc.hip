@@ -200,6 +200,31 @@ __device__ __forceinline__ void imdct_long(float* buf, const LdsTables& T, int u
     // pass 1: this lane is bit-reversed row t = bitrev6(u): rev[8t+r] = buf[u + 64*bitrev3(r)]
     fft_pass1(re, im, T.tw1, 1);
     float2* X = reinterpret_cast<float2*>(buf);
+#ifdef JAAD_PROBE_VALU  // sensitivity probe: +JAAD_PROBE_VALU dependent-free VALU ops per channel
+#pragma unroll
+    for (int i = 0; i < JAAD_PROBE_VALU / 16; i++)
+#pragma unroll
+        for (int s = 0; s < 8; s++) {
+            asm volatile("v_add_f32 %0, %0, 0" : "+v"(re[s]));
+            asm volatile("v_add_f32 %0, %0, 0" : "+v"(im[s]));
+        }
+#endif
+#ifdef JAAD_PROBE_LDS  // sensitivity probe: one extra transpose round trip (8 b64 writes + 8 reads)
+    {
+        const int t0 = (int)(__builtin_bitreverse32((uint32_t)u) >> 26);
+        const int xp = xs_l(8 * t0);
+#pragma unroll
+        for (int r = 0; r < 8; r++) X[xp + r] = make_float2(re[r], im[r]);
+        wave_sync();
+#pragma unroll
+        for (int r = 0; r < 8; r++) {
+            const float2 v = X[xp + r];
+            re[r] = v.x;
+            im[r] = v.y;
+        }
+        wave_sync();
+    }
+#endif
     const int t = (int)(__builtin_bitreverse32((uint32_t)u) >> 26);
     const int x1 = xs_l(8 * t);
 #pragma unroll
@@ -806,6 +831,9 @@ __global__ __launch_bounds__(64 * waves_per_wg<kTnsSpec>()) void lc_decode_kerne
             const bool emit = f >= (int)cd.frame0;
             const size_t cf0 = (size_t)f * nch;
             const Prefetch cur = pf;
+#ifdef JAAD_EARLY_PREFETCH
+            if (it + 1 < my_n) prefetch(A, f + 1, stereo, u, pf);
+#endif
 
             // ---------------- side info ----------------
             const Ics iL = ics_from_lanes(cur.side, 0);
@@ -894,7 +922,9 @@ __global__ __launch_bounds__(64 * waves_per_wg<kTnsSpec>()) void lc_decode_kerne
             if (stereo) iq_channel(T, A.iq_table, cur.q[1], gR, xR);
             // the inputs are consumed: frame f+1's loads fly while this frame's IMDCTs run
             STAMP(12);
+#ifndef JAAD_EARLY_PREFETCH
             if (it + 1 < my_n) prefetch(A, f + 1, stereo, u, pf);
+#endif
 
             if ((iL.flags | (stereo ? iR.flags : 0)) & JAAD_ICS_HAS_PNS) {  // rare: lane 0 replays the LCG
                 // the spectrum overwrites the raw rows: pns_fill reads a copy in rsp
@@ -1042,8 +1072,12 @@ __global__ __launch_bounds__(64 * waves_per_wg<kTnsSpec>()) void lc_decode_kerne
 #ifdef JAAD_ABL_NO_STORE
                         if (A.n_chunks == 0)
 #endif
+#ifdef JAAD_TEMPORAL_STORE
+                        *reinterpret_cast<v4u*>(dst + 16 * u2 + 1024 * jj) = *reinterpret_cast<const v4u*>(W.rsp + 4 * u2 + 256 * jj);
+#else
                         __builtin_nontemporal_store(*reinterpret_cast<const v4u*>(W.rsp + 4 * u2 + 256 * jj),
                                                     reinterpret_cast<v4u*>(dst + 16 * u2 + 1024 * jj));
+#endif
                 }
             }
             STAMP(10);

@@ -7,7 +7,11 @@ sys.path.insert(0, str(ROOT))
 from jaadec_amd import build as B  # noqa: E402
 
 VARIANTS = {
-    "s_stamps16": (["JAAD_STAMPS", "JAAD_LC_WAVES=16"], []),
+    "a_base": ([], []),
+    "b_early": (["JAAD_EARLY_PREFETCH"], []),
+    "c_tstore": (["JAAD_TEMPORAL_STORE"], []),
+    "d_early_t": (["JAAD_EARLY_PREFETCH", "JAAD_TEMPORAL_STORE"], []),
+    "e_w12_early": (["JAAD_EARLY_PREFETCH", "JAAD_LC_WAVES=12"], []),
 }
 
 if __name__ == "__main__":
