@@ -25,7 +25,9 @@ namespace {
 struct HfLds {
     float ecurr[5][64];
     float gl[5][64], ql[5][64], sl[5][64];
-    float gq_eo[64], gq_qm[64], gq_sm[64], gq_g[64];  // per-envelope gain inputs
+    float gq_eo[64];                        // per-envelope E_orig of band m
+    float den_s[64], den_e[64], den_q[64];  // per-band terms of the limiter band's den sum
+    float lim_gmax[64], lim_acc1[64], lim_boost[64];  // per limiter band
 };
 
 // Math.round + short clamp (S/SampleBuffer.java:190-205)
@@ -446,70 +448,119 @@ __global__ __launch_bounds__(256) void sbr_hf_kernel(SbrArgs A)
     }
     wave_sync();
 
-    // calculate_gain (:240-415).  Per envelope: (1) lanes m evaluate everything that does not
-    // depend on the limiter (Q_M, S_M, the unlimited G) into LDS; (2) one lane per limiter
-    // band walks its bands in order (acc1/acc2, G_max, limiting, den, G_boost) from LDS.
 #ifndef JAAD_HF_SKIP_GAIN
+    // calculate_gain (:240-415), per envelope, with every per-band step lane-parallel:
+    //   (1) lane m: E_orig, E_curr, Q_M, S_M and the unlimited G;
+    //   (2) lane kb (limiter band): acc1, acc2 as the Java's ordered sums over its bands -> G_max;
+    //   (3) lane m: limiting (G_max vs G, Q_M*G_max/G) and its three den terms;
+    //   (4) lane kb: den as the ordered sum of those terms -> G_boost;
+    //   (5) lane m: the boosted square roots.
+    // A skipped den term is written as +0: every term is >= 0 and den starts at +0, so adding
+    // +0 leaves the sum bit-identical.  Ordered sums read up to 16 band values in one batch.
     {
         const int NL = T.N_L[s_lim];
         const float EPS = 1e-12f;
         int eo = (int)R.e_off;
+        // limiter band of band m (lane); bands outside every limiter band keep G = Q = S = 0
+        int kbm = 0;
+        for (int kb = 1; kb < NL; kb++)
+            if (m >= (int)T.lim[s_lim][kb]) kbm = kb;
+        const bool covered = band && m >= (int)T.lim[s_lim][0] && m < (int)T.lim[s_lim][NL];
+        const int kb = u;
+        const bool lim_lane = kb < NL;
+        const int ml1 = lim_lane ? T.lim[s_lim][kb] : 0, ml2 = lim_lane ? T.lim[s_lim][kb + 1] : 0;
+        int wmax = 0;
+        for (int j = 0; j < NL; j++) wmax = max(wmax, (int)T.lim[s_lim][j + 1] - (int)T.lim[s_lim][j]);
         for (int l = 0; l < L_E; l++) {
             const int fl = R.f[l];
             const int tnb = R.tnb[l];
             const bool delta1 = !((R.no_noise >> l) & 1);
             const uint64_t smask = R.s_index[l], mmask = R.s_mapped[l];
-            if (band) {
+            const bool sidx = band && ((smask >> m) & 1);
+            float Eom = 0.0f, Ec = 0.0f, Q_M = 0.0f, S_M = 0.0f, G = 0.0f;
+            if (band) {  // (1)
                 const int nb = T.noise_map[s_lim][m];
                 const float Qd = R.q_div[tnb][nb], Qd2 = R.q_div2[tnb][nb];
-                const float Eom = A.epool[eo + T.res_map[s_lim][fl][m]];
-                const float Ec = L.ecurr[l][m];
-                const bool sidx = (smask >> m) & 1, smap = (mmask >> m) & 1;
-                float G = __fdiv_rn(Eom, 1.0f + Ec);
+                Eom = A.epool[eo + T.res_map[s_lim][fl][m]];
+                Ec = L.ecurr[l][m];
+                const bool smap = (mmask >> m) & 1;
+                G = __fdiv_rn(Eom, 1.0f + Ec);
                 if (!smap && delta1) G *= Qd;
                 else if (smap) G *= Qd2;
                 L.gq_eo[m] = Eom;
-                L.gq_qm[m] = Eom * Qd2;
-                L.gq_sm[m] = sidx ? Eom * Qd : 0.0f;
-                L.gq_g[m] = G;
+                Q_M = Eom * Qd2;
+                S_M = sidx ? Eom * Qd : 0.0f;
             }
             eo += fl ? T.n_hi : T.n_lo;
             wave_sync();
-            for (int kb = u; kb < NL; kb += 64) {
-                const int ml1 = T.lim[s_lim][kb], ml2 = T.lim[s_lim][kb + 1];
+            if (lim_lane) {  // (2)
                 float acc1 = 0.0f, acc2 = 0.0f;
-                for (int mm = ml1; mm < ml2; mm++) {
-                    acc1 += L.gq_eo[mm];
-                    acc2 += L.ecurr[l][mm];
+                if (wmax <= 16) {
+                    float ve[16], vc[16];
+#pragma unroll
+                    for (int j = 0; j < 16; j++) {
+                        const int mm = ml1 + j < ml2 ? ml1 + j : ml1;
+                        ve[j] = L.gq_eo[mm];
+                        vc[j] = L.ecurr[l][mm];
+                    }
+#pragma unroll
+                    for (int j = 0; j < 16; j++)
+                        if (ml1 + j < ml2) {
+                            acc1 += ve[j];
+                            acc2 += vc[j];
+                        }
+                } else {
+                    for (int mm = ml1; mm < ml2; mm++) {
+                        acc1 += L.gq_eo[mm];
+                        acc2 += L.ecurr[l][mm];
+                    }
                 }
                 float G_max = __fdiv_rn(EPS + acc1, EPS + acc2) * R.lim_gain;
-                G_max = java_minf(G_max, 1e10f);
+                L.lim_gmax[kb] = java_minf(G_max, 1e10f);
+                L.lim_acc1[kb] = acc1;
+            }
+            wave_sync();
+            float Gl = 0.0f, Ql = 0.0f;
+            if (covered) {  // (3)
+                const float G_max = L.lim_gmax[kbm];
+                if (G_max > G) {
+                    Ql = Q_M;
+                    Gl = G;
+                } else {
+                    Ql = __fdiv_rn(Q_M * G_max, G);
+                    Gl = G_max;
+                }
+                L.den_s[m] = sidx ? S_M : 0.0f;
+                L.den_e[m] = Ec * Gl;
+                L.den_q[m] = (!sidx && l != R.l_A) ? Ql : 0.0f;
+            }
+            wave_sync();
+            if (lim_lane) {  // (4)
                 float den = 0.0f;
-                for (int mm = ml1; mm < ml2; mm++) {
-                    const bool sidx = (smask >> mm) & 1;
-                    const float Q_M = L.gq_qm[mm], S_M = L.gq_sm[mm], G = L.gq_g[mm], Ec = L.ecurr[l][mm];
-                    if (sidx) den += S_M;
-                    float Ql, Gl;
-                    if (G_max > G) {
-                        Ql = Q_M;
-                        Gl = G;
-                    } else {
-                        Ql = __fdiv_rn(Q_M * G_max, G);
-                        Gl = G_max;
+                if (wmax <= 16) {
+                    float ts[16], te[16], tq[16];
+#pragma unroll
+                    for (int j = 0; j < 16; j++) {
+                        const int mm = ml1 + j < ml2 ? ml1 + j : ml1;
+                        ts[j] = L.den_s[mm];
+                        te[j] = L.den_e[mm];
+                        tq[j] = L.den_q[mm];
                     }
-                    den += Ec * Gl;
-                    if (!sidx && l != R.l_A) den += Ql;
-                    L.gl[l][mm] = Gl;
-                    L.ql[l][mm] = Ql;
+#pragma unroll
+                    for (int j = 0; j < 16; j++)
+                        if (ml1 + j < ml2) den = ((den + ts[j]) + te[j]) + tq[j];
+                } else {
+                    for (int mm = ml1; mm < ml2; mm++) den = ((den + L.den_s[mm]) + L.den_e[mm]) + L.den_q[mm];
                 }
-                float G_boost = __fdiv_rn(acc1 + EPS, den + EPS);
-                G_boost = java_minf(G_boost, 2.51188643f);
-                for (int mm = ml1; mm < ml2; mm++) {
-                    L.gl[l][mm] = sqrtf(L.gl[l][mm] * G_boost);
-                    L.ql[l][mm] = sqrtf(L.ql[l][mm] * G_boost);
-                    const float sm = L.gq_sm[mm];
-                    L.sl[l][mm] = sm != 0.0f ? sqrtf(sm * G_boost) : 0.0f;
-                }
+                const float G_boost = __fdiv_rn(L.lim_acc1[kb] + EPS, den + EPS);
+                L.lim_boost[kb] = java_minf(G_boost, 2.51188643f);
+            }
+            wave_sync();
+            if (covered) {  // (5)
+                const float Gb = L.lim_boost[kbm];
+                L.gl[l][m] = sqrtf(Gl * Gb);
+                L.ql[l][m] = sqrtf(Ql * Gb);
+                L.sl[l][m] = S_M != 0.0f ? sqrtf(S_M * Gb) : 0.0f;
             }
             wave_sync();
         }
@@ -547,6 +598,34 @@ __global__ __launch_bounds__(256) void sbr_hf_kernel(SbrArgs A)
             gidx = 4;
         }
         const float rev = (u & 1) ? -1.0f : 1.0f;
+        if (!smooth) {
+            // bs_smoothing_mode == 1: G_filt/Q_filt are the row's envelope values, no ring
+            // (the G/Q ring output above is built from gl/ql directly)
+#pragma unroll
+            for (int r = 2; r < 40; r++) {
+                const int i = r - 2;
+                if (i < first || i >= last) continue;
+                int l = 0;
+                for (int j = 1; j < L_E; j++)
+                    if (i >= R.t_E[j]) l = j;
+                const bool no_noise = (R.no_noise >> l) & 1;
+                const float G_filt = L.gl[l][mi], qnew = L.ql[l][mi], S = L.sl[l][mi];
+                const float Q_filt = (S != 0.0f || no_noise) ? 0.0f : qnew;
+                const int fi = (int)((R.noise0 + (uint32_t)(i - first) * (uint32_t)M + (uint32_t)mi + 1u) & 511u);
+                const int fs = (int)((R.sine0 + (uint32_t)(i - first)) & 3u);
+                if (band) {
+                    const float2 nz = noise_s[fi];
+                    float vr = G_filt * xr[r] + (Q_filt * nz.x);
+                    float vi = G_filt * xi[r] + (Q_filt * nz.y);
+                    const float phr = fs == 0 ? 1.0f : fs == 2 ? -1.0f : 0.0f;
+                    const float phi = fs == 1 ? 1.0f : fs == 3 ? -1.0f : 0.0f;
+                    vr += S * phr;
+                    vi += (rev * S) * phi;
+                    xr[r] = vr;
+                    xi[r] = vi;
+                }
+            }
+        } else
 #pragma unroll
         for (int r = 2; r < 40; r++) {
             const int i = r - 2;

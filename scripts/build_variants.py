@@ -8,10 +8,11 @@ from jaadec_amd import build as B  # noqa: E402
 
 VARIANTS = {
     "a_base": ([], []),
-    "b_early": (["JAAD_EARLY_PREFETCH"], []),
-    "c_tstore": (["JAAD_TEMPORAL_STORE"], []),
-    "d_early_t": (["JAAD_EARLY_PREFETCH", "JAAD_TEMPORAL_STORE"], []),
-    "e_w12_early": (["JAAD_EARLY_PREFETCH", "JAAD_LC_WAVES=12"], []),
+    "b_hf_no_gen": (["JAAD_HF_SKIP_GEN"], []),
+    "c_hf_no_est": (["JAAD_HF_SKIP_EST"], []),
+    "d_hf_no_gain": (["JAAD_HF_SKIP_GAIN"], []),
+    "e_hf_no_asm": (["JAAD_HF_SKIP_ASM"], []),
+    "f_hf_none": (["JAAD_HF_SKIP_GEN", "JAAD_HF_SKIP_EST", "JAAD_HF_SKIP_GAIN", "JAAD_HF_SKIP_ASM"], []),
 }
 
 if __name__ == "__main__":

@@ -1,6 +1,4 @@
-"""Print the top kernels of a rocprofv3 kernel_stats.csv."""
-import csv
-import sys
-
-for x in list(csv.DictReader(open(sys.argv[1])))[:int(sys.argv[2]) if len(sys.argv) > 2 else 12]:
-    print(f"{x['Name'][:64]:64s} calls={x['Calls']:>5s} avg_us={float(x['AverageNs'])/1e3:9.1f} pct={float(x['Percentage']):6.2f}")
+"""Per-kernel average durations from a rocprofv3 kernel_stats.csv: python scripts/kstats.py FILE"""
+import csv, sys
+for r in csv.DictReader(open(sys.argv[1])):
+    print(f"{r['Name'][:70]:70s} {float(r['AverageNs'])/1e3:10.1f} us  x{r['Calls']}")
