@@ -27,8 +27,10 @@
 
 #include "jaad_lc.h"
 
-#ifndef JAAD_WAVES_PER_EU
-#define JAAD_WAVES_PER_EU 4
+// The two channels of a CPE run their long-window IMDCTs in lockstep (JAAD_LC_NODUAL: one after
+// the other, the right spectrum parked in LDS meanwhile)
+#ifndef JAAD_LC_NODUAL
+#define JAAD_LC_DUAL 1
 #endif
 
 namespace jaad {
@@ -185,88 +187,99 @@ __device__ __forceinline__ Ics ics_from_lanes(uint32_t side, int base)
 // ------------------------------------------------------------------------------------------
 // IMDCT N = 2048 (MDCT.process): lane u holds k = u + 64 s.  Reads the spectrum from buf.
 // ------------------------------------------------------------------------------------------
-__device__ __forceinline__ void imdct_long(float* buf, const LdsTables& T, int u, float (&re)[8], float (&im)[8])
+// N channel transforms in lockstep (N = 2: the two channels of a CPE share every LDS round
+// trip and give the scheduler two independent dependency chains)
+template <int N>
+__device__ __forceinline__ void imdct_long_n(float* const (&bufs)[N], const LdsTables& T, int u, float (&re)[N][8],
+                                             float (&im)[N][8])
 {
 #pragma unroll
-    for (int s = 0; s < 8; s++) {
-        int k = u + 64 * s;
-        float in0 = buf[eo_idx(2 * k)];
-        float in1 = buf[eo_idx(1023 - 2 * k)];
-        float c = T.mdct_l[k][0], sn = T.mdct_l[k][1];
-        im[s] = (in0 * c) + (in1 * sn);  // MDCT.java:39-42
-        re[s] = (in1 * c) - (in0 * sn);
-    }
-    wave_sync();
-    // pass 1: this lane is bit-reversed row t = bitrev6(u): rev[8t+r] = buf[u + 64*bitrev3(r)]
-    fft_pass1(re, im, T.tw1, 1);
-    float2* X = reinterpret_cast<float2*>(buf);
-#ifdef JAAD_PROBE_VALU  // sensitivity probe: +JAAD_PROBE_VALU dependent-free VALU ops per channel
-#pragma unroll
-    for (int i = 0; i < JAAD_PROBE_VALU / 16; i++)
+    for (int n = 0; n < N; n++)
 #pragma unroll
         for (int s = 0; s < 8; s++) {
-            asm volatile("v_add_f32 %0, %0, 0" : "+v"(re[s]));
-            asm volatile("v_add_f32 %0, %0, 0" : "+v"(im[s]));
+            int k = u + 64 * s;
+            float in0 = bufs[n][eo_idx(2 * k)];
+            float in1 = bufs[n][eo_idx(1023 - 2 * k)];
+            float c = T.mdct_l[k][0], sn = T.mdct_l[k][1];
+            im[n][s] = (in0 * c) + (in1 * sn);  // MDCT.java:39-42
+            re[n][s] = (in1 * c) - (in0 * sn);
         }
-#endif
-#ifdef JAAD_PROBE_LDS  // sensitivity probe: one extra transpose round trip (8 b64 writes + 8 reads)
-    {
-        const int t0 = (int)(__builtin_bitreverse32((uint32_t)u) >> 26);
-        const int xp = xs_l(8 * t0);
-#pragma unroll
-        for (int r = 0; r < 8; r++) X[xp + r] = make_float2(re[r], im[r]);
-        wave_sync();
-#pragma unroll
-        for (int r = 0; r < 8; r++) {
-            const float2 v = X[xp + r];
-            re[r] = v.x;
-            im[r] = v.y;
-        }
-        wave_sync();
-    }
-#endif
+    wave_sync();
+    // pass 1: this lane is bit-reversed row t = bitrev6(u): rev[8t+r] = buf[u + 64*bitrev3(r)]
     const int t = (int)(__builtin_bitreverse32((uint32_t)u) >> 26);
     const int x1 = xs_l(8 * t);
 #pragma unroll
-    for (int r = 0; r < 8; r++) X[x1 + r] = make_float2(re[BR3[r]], im[BR3[r]]);
+    for (int n = 0; n < N; n++) {
+        fft_pass1(re[n], im[n], T.tw1, 1);
+        float2* X = reinterpret_cast<float2*>(bufs[n]);
+#pragma unroll
+        for (int r = 0; r < 8; r++) X[x1 + r] = make_float2(re[n][BR3[r]], im[n][BR3[r]]);
+    }
     wave_sync();
     // pass 2: elements 64a + b + 8s, stages i = 8, 16, 32
     const int a = u >> 3, b = u & 7;
     const int x2 = xs_l(64 * a + b);
 #pragma unroll
-    for (int s = 0; s < 8; s++) {
-        float2 v = X[x2 + xs_l(8 * s)];
-        re[s] = v.x;
-        im[s] = v.y;
-    }
-    fft_3stages(re, im, [&](int j, float& wr, float& wi) {
-        wr = T.tw2[j][b][0];
-        wi = T.tw2[j][b][1];
-    });
+    for (int n = 0; n < N; n++) {
+        const float2* X = reinterpret_cast<const float2*>(bufs[n]);
 #pragma unroll
-    for (int s = 0; s < 8; s++) X[x2 + xs_l(8 * s)] = make_float2(re[s], im[s]);
+        for (int s = 0; s < 8; s++) {
+            float2 v = X[x2 + xs_l(8 * s)];
+            re[n][s] = v.x;
+            im[n][s] = v.y;
+        }
+    }
+#pragma unroll
+    for (int n = 0; n < N; n++) {
+        fft_3stages(re[n], im[n], [&](int j, float& wr, float& wi) {
+            wr = T.tw2[j][b][0];
+            wi = T.tw2[j][b][1];
+        });
+        float2* X = reinterpret_cast<float2*>(bufs[n]);
+#pragma unroll
+        for (int s = 0; s < 8; s++) X[x2 + xs_l(8 * s)] = make_float2(re[n][s], im[n][s]);
+    }
     wave_sync();
     // pass 3: elements u + 64 s, stages i = 64, 128, 256
     const int x3 = xs_l(u);
 #pragma unroll
-    for (int s = 0; s < 8; s++) {
-        float2 v = X[x3 + xs_l(64 * s)];
-        re[s] = v.x;
-        im[s] = v.y;
+    for (int n = 0; n < N; n++) {
+        const float2* X = reinterpret_cast<const float2*>(bufs[n]);
+#pragma unroll
+        for (int s = 0; s < 8; s++) {
+            float2 v = X[x3 + xs_l(64 * s)];
+            re[n][s] = v.x;
+            im[n][s] = v.y;
+        }
     }
     wave_sync();
-    // stages 64 (m = 4, k = u), 128 (m = 2, k = u + 64e), 256 (m = 1, k = u + 64s)
-    fft_3stages(re, im, [&](int j, float& wr, float& wi) {
-        wr = T.tw3[j][u][0];
-        wi = T.tw3[j][u][1];
-    });
 #pragma unroll
-    for (int s = 0; s < 8; s++) {  // MDCT.java:48-53
-        int k = u + 64 * s;
-        float c = T.mdct_l[k][0], sn = T.mdct_l[k][1];
-        float t0 = re[s], t1 = im[s];
-        im[s] = (t1 * c) + (t0 * sn);
-        re[s] = (t0 * c) - (t1 * sn);
+    for (int n = 0; n < N; n++) {
+        // stages 64 (m = 4, k = u), 128 (m = 2, k = u + 64e), 256 (m = 1, k = u + 64s)
+        fft_3stages(re[n], im[n], [&](int j, float& wr, float& wi) {
+            wr = T.tw3[j][u][0];
+            wi = T.tw3[j][u][1];
+        });
+#pragma unroll
+        for (int s = 0; s < 8; s++) {  // MDCT.java:48-53
+            int k = u + 64 * s;
+            float c = T.mdct_l[k][0], sn = T.mdct_l[k][1];
+            float t0 = re[n][s], t1 = im[n][s];
+            im[n][s] = (t1 * c) + (t0 * sn);
+            re[n][s] = (t0 * c) - (t1 * sn);
+        }
+    }
+}
+
+__device__ __forceinline__ void imdct_long(float* buf, const LdsTables& T, int u, float (&re)[8], float (&im)[8])
+{
+    float* const bufs[1] = {buf};
+    float r1[1][8], i1[1][8];
+    imdct_long_n<1>(bufs, T, u, r1, i1);
+#pragma unroll
+    for (int s = 0; s < 8; s++) {
+        re[s] = r1[0][s];
+        im[s] = i1[0][s];
     }
 }
 
@@ -550,19 +563,28 @@ __device__ __forceinline__ uint32_t round_pk16(float a, float b)
 //   buf  band records [0,512) + raw sf/cb rows [512,640) -> spectrum (E/O) -> IFFT transposes ->
 //        OLA scratch -> PCM staging
 //   rsp  the right channel's spectrum while the left one is transformed (PNS: raw row copy)
+#ifdef JAAD_LC_DUAL
+constexpr int kRspFloats = kWaveBuf;  // second channel buffer (spectrum + transposes)
+#else
+constexpr int kRspFloats = 1024;
+#endif
 template <bool kTns>
 struct alignas(16) WaveLds {
     float buf[kWaveBuf];
-    float rsp[1024];
+    float rsp[kRspFloats];
 };
 template <>
 struct alignas(16) WaveLds<true> {
     float buf[kWaveBuf];
-    float rsp[1024];
+    float rsp[kRspFloats];
     float tns[192];  // spec-TNS LPC scratch (8 filters x 24)
 };
 #ifndef JAAD_LC_WAVES
+#ifdef JAAD_LC_DUAL
+#define JAAD_LC_WAVES 12
+#else
 #define JAAD_LC_WAVES 16
+#endif
 #endif
 template <bool kTns>
 constexpr int waves_per_wg()
@@ -708,11 +730,10 @@ __device__ __forceinline__ void iq_channel(const LdsTables& T, const float* iq_g
 // (TNS) -> IMDCT -> window/OLA of one channel whose spectrum is in buf (E/O layout); result
 // in out (slot o = position long_pos(u, o)), new overlap in ov
 template <bool kTnsSpec>
-__device__ __forceinline__ void synth_channel(const KernelArgs& A, const LdsTables& T, WaveLds<kTnsSpec>& W, const Ics& ic,
-                                              size_t cf, float (&ov)[16], float (&out)[16])
+__device__ __forceinline__ void synth_channel(const KernelArgs& A, const LdsTables& T, WaveLds<kTnsSpec>& W, float* buf,
+                                              const Ics& ic, size_t cf, float (&ov)[16], float (&out)[16])
 {
     const int u = lane_id();
-    float* buf = W.buf;
     if constexpr (kTnsSpec)
         if (A.tns_mode == JAAD_TNS_SPEC && (ic.flags & JAAD_ICS_TNS) && A.tns) tns_spec(buf, W.tns, T, *A.gtab, u, ic, A.tns + cf);
     const FrameCtx fc{ic.seq, ic.shape, ic.shape_prev};
@@ -976,6 +997,83 @@ __global__ __launch_bounds__(64 * waves_per_wg<kTnsSpec>()) void lc_decode_kerne
             }
 
             STAMP(3);
+#ifdef JAAD_LC_DUAL
+            // both spectra to LDS (E/O layout): left in buf, right in rsp
+            wave_sync();
+            store_spec(W.buf, u, xL);
+            if (stereo) store_spec(W.rsp, u, xR);
+            wave_sync();
+            STAMP(4);
+            float outL[16], outR[16];
+            if (stereo && iL.seq != JAAD_EIGHT_SHORT_SEQUENCE && iR.seq != JAAD_EIGHT_SHORT_SEQUENCE) {
+                // the two long-window IMDCTs in lockstep: one set of LDS round trips, two chains
+                if constexpr (kTnsSpec) {
+                    if (A.tns_mode == JAAD_TNS_SPEC && A.tns) {
+                        if (iL.flags & JAAD_ICS_TNS) tns_spec(W.buf, W.tns, T, *A.gtab, u, iL, A.tns + cf0);
+                        if (iR.flags & JAAD_ICS_TNS) tns_spec(W.rsp, W.tns, T, *A.gtab, u, iR, A.tns + cf0 + 1);
+                    }
+                }
+                float* const bufs[2] = {W.buf, W.rsp};
+                float re[2][8], im[2][8];
+                imdct_long_n<2>(bufs, T, lane_id(), re, im);
+                ola_long(T, u, FrameCtx{iL.seq, iL.shape, iL.shape_prev}, re[0], im[0], ovL, outL);
+                ola_long(T, u, FrameCtx{iR.seq, iR.shape, iR.shape_prev}, re[1], im[1], ovR, outR);
+                wave_sync();
+            } else {
+                synth_channel<kTnsSpec>(A, T, W, W.buf, iL, cf0, ovL, outL);
+                if (stereo) synth_channel<kTnsSpec>(A, T, W, W.rsp, iR, cf0 + 1, ovR, outR);
+            }
+            STAMP(8);
+            {
+                const int u2 = lane_id();
+                if constexpr (planar) {
+                    if (emit) {
+#pragma unroll
+                        for (int o = 0; o < 16; o++) {
+                            W.buf[long_pos(u2, o)] = outL[o];
+                            if (stereo) W.rsp[long_pos(u2, o)] = outR[o];
+                        }
+                        wave_sync();
+#pragma unroll
+                        for (int c = 0; c < nch; c++) {
+                            float* dst = reinterpret_cast<float*>(A.pcm) + (cf0 + c) * 1024;
+                            const float* srcb = c ? W.rsp : W.buf;
+#pragma unroll
+                            for (int jj = 0; jj < 4; jj++)
+                                *reinterpret_cast<float4*>(dst + 4 * u2 + 256 * jj) = *reinterpret_cast<const float4*>(srcb + 4 * u2 + 256 * jj);
+                        }
+                    }
+                } else if constexpr (out_f32) {  // tolerance/debug format: strided stores
+                    if (emit) {
+                        float2* dst = reinterpret_cast<float2*>(reinterpret_cast<uint8_t*>(A.pcm) + (size_t)f * 8192);
+#pragma unroll
+                        for (int o = 0; o < 16; o++) dst[long_pos(u2, o)] = make_float2(outL[o], stereo ? outR[o] : outL[o]);
+                    }
+                } else {
+                    // word P = (L_P, R_P), staged in buf; big endian swaps the bytes of each sample.
+                    // v_perm_b32(s0 = R pair, s1 = L pair): selector bytes 0-3 pick L, 4-7 pick R.
+                    const uint32_t sel0 = big_endian ? 0x04050001u : 0x05040100u;
+                    const uint32_t sel1 = big_endian ? 0x06070203u : 0x07060302u;
+                    uint32_t* stage = reinterpret_cast<uint32_t*>(W.buf);
+#pragma unroll
+                    for (int m = 0; m < 8; m++) {
+                        const uint32_t pl = round_pk16(outL[2 * m], outL[2 * m + 1]);
+                        const uint32_t pr = stereo ? round_pk16(outR[2 * m], outR[2 * m + 1]) : pl;
+                        stage[long_pos(u2, 2 * m)] = __builtin_amdgcn_perm(pr, pl, sel0);
+                        stage[long_pos(u2, 2 * m + 1)] = __builtin_amdgcn_perm(pr, pl, sel1);
+                    }
+                    wave_sync();
+                    if (emit) {
+                        uint8_t* dst = reinterpret_cast<uint8_t*>(A.pcm) + (size_t)f * 4096;
+#pragma unroll
+                        for (int jj = 0; jj < 4; jj++)
+                            __builtin_nontemporal_store(*reinterpret_cast<const v4u*>(stage + 4 * u2 + 256 * jj),
+                                                        reinterpret_cast<v4u*>(dst + 16 * u2 + 1024 * jj));
+                    }
+                    wave_sync();
+                }
+            }
+#else
             // left spectrum -> buf (E/O layout); right spectrum parked in rsp (lane-linear)
             wave_sync();
             store_spec(W.buf, u, xL);
@@ -1017,7 +1115,7 @@ __global__ __launch_bounds__(64 * waves_per_wg<kTnsSpec>()) void lc_decode_kerne
                 }
                 STAMP(c ? 7 : 5);
                 float out[16];
-                synth_channel<kTnsSpec>(A, T, W, ic, cf0 + c, ov, out);
+                synth_channel<kTnsSpec>(A, T, W, W.buf, ic, cf0 + c, ov, out);
                 STAMP(c ? 8 : 6);
                 const int u2 = lane_id();
                 if constexpr (planar) {
@@ -1080,6 +1178,7 @@ __global__ __launch_bounds__(64 * waves_per_wg<kTnsSpec>()) void lc_decode_kerne
 #endif
                 }
             }
+#endif
             STAMP(10);
         }
         STAMP(11);

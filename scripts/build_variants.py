@@ -8,11 +8,8 @@ from jaadec_amd import build as B  # noqa: E402
 
 VARIANTS = {
     "a_base": ([], []),
-    "b_hf_no_gen": (["JAAD_HF_SKIP_GEN"], []),
-    "c_hf_no_est": (["JAAD_HF_SKIP_EST"], []),
-    "d_hf_no_gain": (["JAAD_HF_SKIP_GAIN"], []),
-    "e_hf_no_asm": (["JAAD_HF_SKIP_ASM"], []),
-    "f_hf_none": (["JAAD_HF_SKIP_GEN", "JAAD_HF_SKIP_EST", "JAAD_HF_SKIP_GAIN", "JAAD_HF_SKIP_ASM"], []),
+    "b_dual": (["JAAD_LC_DUAL"], []),
+    "c_dual_w10": (["JAAD_LC_DUAL", "JAAD_LC_WAVES=10"], []),
 }
 
 if __name__ == "__main__":
