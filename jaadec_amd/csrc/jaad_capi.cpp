@@ -368,12 +368,14 @@ int carry_untouched(jaad_ctx* ctx, T* out, const T* in, size_t per_slot, hipStre
 static_assert(sizeof(jaad_ps_frame) == 528 && sizeof(jaad_sbr_frame) == 1968, "jaad_gpu.h record sizes");
 
 // PS parameters the Java parser can produce (A/ps/PSImpl.java:103-199): borders 0 = b_0 < .. <
-// b_num_env = 32, |IID| <= num_steps, ICC and IPD/OPD in 0..7, nr_ipdopd_par 0 / 11 / 17; the GPU
-// path needs PS data in every frame of a PS stream
+// b_num_env = 32, |IID| <= num_steps, ICC and IPD/OPD in 0..7, nr_ipdopd_par 0 / 11 / 17.  A frame
+// without PS data is decoded as SBR1.process does then: mono, copied to the right channel
+// (A/sbr/SBR1.java:75-81); the PS state waits for the next PS frame.
 static bool ps_frame_ok(const jaad_sbr_frame& F)
 {
     const jaad_ps_frame& p = F.ps;
-    if (!F.ps_present || p.num_env < 1 || p.num_env > 5 || p.iid_mode > 5 || p.icc_mode > 5) return false;
+    if (!F.ps_present) return true;
+    if (p.num_env < 1 || p.num_env > 5 || p.iid_mode > 5 || p.icc_mode > 5) return false;
     if (p.nr_ipdopd_par != 0 && p.nr_ipdopd_par != 11 && p.nr_ipdopd_par != 17) return false;
     if (p.border[0] != 0 || p.border[p.num_env] != 32) return false;
     for (int e = 0; e < p.num_env; e++)
@@ -449,7 +451,8 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
     const size_t o_chunks = al(o_psf + (ps ? nf * sizeof(jaad_ps_frame) : 0));
     const size_t o_last = al(o_chunks + ctx->sbr_chunks.size() * sizeof(SbrChunk));
     const size_t o_runs = al(o_last + ctx->sbr_last.size() * sizeof(uint32_t));
-    const size_t n1 = al(o_runs + ctx->ps_runs.size() * sizeof(uint32_t));
+    const size_t o_pslist = al(o_runs + ctx->ps_runs.size() * sizeof(uint32_t));
+    const size_t n1 = al(o_pslist + (ps ? nf * sizeof(uint32_t) : 0));
 
     // JAAD_TRACE_HOST=1: per-call host timings of this stage on stderr (tuning aid)
     static const bool trace = std::getenv("JAAD_TRACE_HOST") != nullptr;
@@ -467,8 +470,8 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
         std::memcpy(h1 + o_chunks, ctx->sbr_chunks.data(), ctx->sbr_chunks.size() * sizeof(SbrChunk));
     if (!ctx->sbr_last.empty())
         std::memcpy(h1 + o_last, ctx->sbr_last.data(), ctx->sbr_last.size() * sizeof(uint32_t));
-    if (!ctx->ps_runs.empty())
-        std::memcpy(h1 + o_runs, ctx->ps_runs.data(), ctx->ps_runs.size() * sizeof(uint32_t));
+    uint32_t* ps_runs_h = reinterpret_cast<uint32_t*>(h1 + o_runs);
+    uint32_t* ps_list_h = reinterpret_cast<uint32_t*>(h1 + o_pslist);
 
     // parameter records: runs are independent streams, so they are built in parallel; each
     // worker owns a contiguous block of runs and writes its E_orig values into its own region
@@ -493,6 +496,7 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
         if (t >= nt) return;  // the pool may be wider than this call's run blocks
         float* region = reinterpret_cast<float*>(h2) + rbase[t];
         uint32_t epos = 0;
+        uint32_t last_ps = UINT32_MAX;
         bool sm = false;
         for (uint32_t r = rr[t]; r < rr[t + 1] && !rcs[t]; r++) {
             SbrHostSlot& hs = ctx->sbr_slots[b->stream_slot[r]];
@@ -503,11 +507,11 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
                         __builtin_prefetch(reinterpret_cast<const char*>(&b->sbr[f + 2]) + o);
                 if (ps) {
                     if (!ps_frame_ok(b->sbr[f])) {
-                        rcs[t] = b->sbr[f].ps_present ? JAAD_ERR_BITSTREAM : JAAD_ERR_UNSUPPORTED;
+                        rcs[t] = JAAD_ERR_BITSTREAM;
                         bad[t] = (int)f;
                         break;
                     }
-                    psf[f] = b->sbr[f].ps;
+                    if (b->sbr[f].ps_present) psf[f] = b->sbr[f].ps;
                 }
                 SbrRec* rec = &recs[(size_t)f * nch];
                 int rc = ctx->sbr_host->frame(hs, b->sbr[f], nch, f == b->frame_begin[r], b->stream_slot[r], rec,
@@ -516,6 +520,22 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
                     rcs[t] = rc;
                     bad[t] = (int)f;
                     break;
+                }
+                if (ps) {  // PS frames of the run (the PS kernels walk only these)
+                    if (f == b->frame_begin[r]) last_ps = UINT32_MAX;
+                    rec->ps_back = 0;
+                    if (last_ps != UINT32_MAX) {
+                        if (f - last_ps > 0xffffu) {
+                            rcs[t] = JAAD_ERR_UNSUPPORTED;  // > 65535 frames without PS data in one call
+                            bad[t] = (int)f;
+                            break;
+                        }
+                        rec->ps_back = (uint16_t)(f - last_ps);
+                    }
+                    if (b->sbr[f].ps_present) {
+                        rec->flags |= kSbrPsOn;
+                        last_ps = f;
+                    }
                 }
                 sm |= (rec[0].flags & kSbrSmooth) != 0;
             }
@@ -533,6 +553,19 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
             return rcs[t];
         }
         smoothing |= smooth[t] != 0;
+    }
+    if (ps) {  // per run: (offset, count) of its PS frames in ps_list
+        uint32_t np = 0, ri = 0;
+        for (uint32_t r = 0; r < b->n_runs; r++) {
+            const uint32_t f0 = b->frame_begin[r], f1 = b->frame_begin[r + 1];
+            if (f1 == f0) continue;
+            const uint32_t off = np;
+            for (uint32_t f = f0; f < f1; f++)
+                if (b->sbr[f].ps_present) ps_list_h[np++] = f;
+            ps_runs_h[2 * ri] = off;
+            ps_runs_h[2 * ri + 1] = np - off;
+            ri++;
+        }
     }
     if (!tabs.empty()) std::memcpy(h2 + o_tabs, tabs.data(), tabs.size() * sizeof(SbrTab));
     const auto t_packed = clk::now();
@@ -599,6 +632,7 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
         a.pg = static_cast<float*>(ctx->d_pg.p);
         a.hb = static_cast<float*>(ctx->d_hb.p);
         a.runs = reinterpret_cast<const uint32_t*>(d1 + o_runs);
+        a.ps_list = reinterpret_cast<const uint32_t*>(d1 + o_pslist);
         a.n_runs = (uint32_t)(ctx->ps_runs.size() / 2);
     }
     HIPCHK(launch_sbr(a, stream));

@@ -161,15 +161,19 @@ __global__ __launch_bounds__(256) void ps_analysis_kernel(SbrArgs A)
             L.xl[l][u] = v;
             xo[l * 64 + u] = v;
         }
+        // a frame without PS data only hands its X (qmfs0 input) to the synthesis
+        if (!(R.flags & kSbrPsOn)) return;
         for (int l = 32; l < 38; l++) L.xl[l][u] = u < 5 ? xn[(l - 32) * 64 + u] : make_float2(0.0f, 0.0f);
         if (u < 36) {
+            // Filterbank.buffer as the previous PS frame left it (frames without PS data do not
+            // run the hybrid analysis)
             const int b = u / 12, i = u % 12;
             float2 h;
-            if (R.first) {
+            if (R.ps_back == 0) {
                 const PsState& S = A.pss[R.slot];
                 h = S.init ? make_float2(S.hyb[b][i][0], S.hyb[b][i][1]) : make_float2(0.0f, 0.0f);
             } else {
-                h = hyb_history_after(A, f - 1, b, i);
+                h = hyb_history_after(A, f - R.ps_back, b, i);
             }
             L.hist[b][i] = h;
         }
@@ -261,7 +265,7 @@ __device__ __forceinline__ float magnitude_c(float re, float im)
 // over every envelope of every frame of the run.  The shared phase_hist counter flips once per
 // (group, envelope) with bk < nr_ipdopd_par; those groups are always 0 .. nr + 1, so the
 // counter at (gr, env) is phase_hist(frame start) + gr * num_env + env.
-__device__ void ps_param_scan(const SbrArgs& A, uint32_t f0, uint32_t nfr, PsState& S, bool fresh, int u)
+__device__ void ps_param_scan(const SbrArgs& A, const uint32_t* fl, uint32_t nfr, PsState& S, bool fresh, int u)
 {
     if (u >= 20) return;
     const PsConst& K = *A.psc;
@@ -282,7 +286,7 @@ __device__ void ps_param_scan(const SbrArgs& A, uint32_t f0, uint32_t nfr, PsSta
         }
     int phase = fresh ? 0 : S.phase_hist;
     for (uint32_t j = 0; j < nfr; j++) {
-        const uint32_t f = f0 + j;
+        const uint32_t f = fl[j];
         const jaad_ps_frame& P = A.psf[f];
         const int E = P.num_env, nr = P.nr_ipdopd_par;
         const bool elig = bk < nr;
@@ -421,25 +425,28 @@ __device__ __forceinline__ void rotate_allpass(float2 (&d)[14])
 
 // walk the frames of a run with the next frame's 32 inputs in flight while this one computes
 template <typename Load, typename Step>
-__device__ __forceinline__ void run_frames(uint32_t f0, uint32_t nfr, Load&& load, Step&& step)
+__device__ __forceinline__ void run_frames(const uint32_t* fl, uint32_t nfr, Load&& load, Step&& step)
 {
     float2 xa[32], xb[32];
-    if (nfr) load(xa, f0);
+    if (nfr) load(xa, fl[0]);
     for (uint32_t j = 0; j < nfr; j += 2) {
-        if (j + 1 < nfr) load(xb, f0 + j + 1);
-        step(xa, f0 + j);
+        if (j + 1 < nfr) load(xb, fl[j + 1]);
+        step(xa, fl[j]);
         if (j + 1 >= nfr) break;
-        if (j + 2 < nfr) load(xa, f0 + j + 2);
-        step(xb, f0 + j + 1);
+        if (j + 2 < nfr) load(xa, fl[j + 2]);
+        step(xb, fl[j + 1]);
     }
 }
 
 __global__ __launch_bounds__(256) void ps_decor_kernel(SbrArgs A)
 {
+    // the run's frames that carry PS data, in time order: the recurrences advance only there
     const uint32_t run = blockIdx.x;
-    const uint32_t f0 = A.runs[2 * run], nfr = A.runs[2 * run + 1];
+    const uint32_t* fl = A.ps_list + A.runs[2 * run];
+    const uint32_t nfr = A.runs[2 * run + 1];
+    if (nfr == 0) return;
     const int wave = threadIdx.x >> 6, u = lane_id();
-    PsState& S = A.pss[A.recs[f0].slot];
+    PsState& S = A.pss[A.recs[fl[0]].slot];
     const PsConst& K = *A.psc;
     const bool fresh = S.init == 0;
 
@@ -483,7 +490,7 @@ __global__ __launch_bounds__(256) void ps_decor_kernel(SbrArgs A)
             rotate_allpass(ap);
             rotate<0, 14, 32 % 14>(dl);
         };
-        run_frames(f0, nfr, load, step);
+        run_frames(fl, nfr, load, step);
         if (!is14) dl[0] = d1;
 #pragma unroll
         for (int k = 0; k < 14; k++) {
@@ -516,11 +523,11 @@ __global__ __launch_bounds__(256) void ps_decor_kernel(SbrArgs A)
             });
             rotate_allpass(ap);
         };
-        run_frames(f0, nfr, load, step);
+        run_frames(fl, nfr, load, step);
 #pragma unroll
         for (int k = 0; k < 14; k++) S.aph[k][u] = ap[k];
     } else if (wave == 3) {
-        ps_param_scan(A, f0, nfr, S, fresh, u);
+        ps_param_scan(A, fl, nfr, S, fresh, u);
     } else {
         // ---- transient detector (lane = parameter band), PSImpl.java:238-270 ----
         if (u >= 20) return;
@@ -547,7 +554,7 @@ __global__ __launch_bounds__(256) void ps_decor_kernel(SbrArgs A)
                 dst[n * 20 + u] = (sm * gamma) <= nrg ? 1.0f : __fdiv_rn(nrg, (sm * gamma));
             }
         };
-        run_frames(f0, nfr, load, step);
+        run_frames(fl, nfr, load, step);
         S.peak[u] = peak;
         S.smooth[u] = smooth;
         S.pprev[u] = pprev;
@@ -608,6 +615,7 @@ __global__ __launch_bounds__(256) void ps_mix_kernel(SbrArgs A)
     const int wave = threadIdx.x >> 6, u = lane_id();
     const uint32_t f = blockIdx.x * kPsWaves + wave;
     if (f >= A.n_cf) return;
+    if (!(A.recs[f].flags & kSbrPsOn)) return;  // X_left stays as the analysis wrote it
     MixLds& L = lds_s[wave];
     const jaad_ps_frame& P = A.psf[f];
     const int nr = P.nr_ipdopd_par;
@@ -679,10 +687,11 @@ __global__ __launch_bounds__(256) void ps_mix_kernel(SbrArgs A)
 __global__ __launch_bounds__(64) void ps_state_kernel(SbrArgs A)
 {
     const uint32_t run = blockIdx.x;
-    const uint32_t f0 = A.runs[2 * run], nfr = A.runs[2 * run + 1];
-    const uint32_t fl = f0 + nfr - 1;
+    const uint32_t nfr = A.runs[2 * run + 1];
+    if (nfr == 0) return;  // no PS frame in this call: the slot's PS state stays
+    const uint32_t fl = A.ps_list[A.runs[2 * run] + nfr - 1];
     const int u = lane_id();
-    PsState& S = A.pss[A.recs[f0].slot];
+    PsState& S = A.pss[A.recs[fl].slot];
     if (u < 36) {
         const float2 h = hyb_history_after(A, fl, u / 12, u % 12);
         S.hyb[u / 12][u % 12][0] = h.x;

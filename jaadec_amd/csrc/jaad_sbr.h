@@ -43,6 +43,7 @@ enum : uint8_t {
     kSbrSmooth = 2,      // bs_smoothing_mode == 0 (h_SL = 4 unless no_noise)
     kSbrInterpol = 4,    // bs_interpol_freq
     kSbrProcess = 8,     // a header has been seen (else analysis only, kx = 32)
+    kSbrPsOn = 16,       // PS config: this frame carries PS data (SBR1.isPSUsed, A/sbr/SBR1.java:136)
 };
 
 // One channel-frame.  224 bytes.
@@ -57,7 +58,8 @@ struct SbrRec {
     uint8_t f[6];
     uint8_t tnb[5];             // current_t_noise_band of envelope l
     uint8_t gq0;                // GQ_ringbuf_index when the frame's first row is assembled
-    uint8_t pad1[2];
+    uint16_t ps_back;           // PS config: frames back to the previous PS frame of the run in this
+                                // call (0: none, the PS state of the slot holds it)
     float lim_gain;             // limGain[bs_limiter_gains]
     uint32_t e_off;             // E_orig[l][band] at epool[e_off + sum_{l'<l} n[f[l']] + band]
     float bw[5];                // bwArray after calc_chirp_factors
@@ -153,7 +155,8 @@ struct SbrArgs {
     float* xhr;                 // [frame][32][12][2] hybrid all-pass output
     float* pg;                  // [frame][32][20] P, then G_TransientRatio
     float* hb;                  // [frame][env 5][group 22][16]: H start (re 4, im 4), delta (re 4, im 4)
-    const uint32_t* runs;       // [run] = (first frame, frame count)
+    const uint32_t* runs;       // [run] = (offset into ps_list, PS frame count)
+    const uint32_t* ps_list;    // frames carrying PS data, run by run in time order
     uint32_t n_runs;
 };
 

@@ -729,7 +729,7 @@ __global__ __launch_bounds__(256) void sbr_synthesis_kernel(SbrArgs A)
     int vpos = 0;
 
     // one slot: DCT-IV pair -> v block (:99-129); emit: window (:134-146) + PCM
-    auto slot = [&](float Xr, float Xi, bool emit, size_t n0) {
+    auto slot = [&](float Xr, float Xi, bool emit, size_t n0, bool dup = false) {
         // DCT inputs: d = 0: real parts (in_real1[e] = X[2e], in_imag1[e] = X[63-2e]);
         //             d = 1: imag parts (in_real2[e] = X[63-2e], in_imag2[e] = X[2e])
         const float ar = shfl(Xr, 2 * e), br = shfl(Xr, 63 - 2 * e);
@@ -767,13 +767,13 @@ __global__ __launch_bounds__(256) void sbr_synthesis_kernel(SbrArgs A)
             const size_t n = n0 + u;
             if (A.out_mode & JAAD_PCM_FLOAT32) {
                 float* o = reinterpret_cast<float*>(A.pcm) + 2 * n;
-                if (nch == 2 || ps) o[c] = out;
+                if ((nch == 2 || ps) && !dup) o[c] = out;
                 else o[0] = o[1] = out;
             } else {
                 uint32_t s16 = (uint32_t)(uint16_t)(int16_t)java_round16(out);
                 if (!(A.out_mode & JAAD_PCM_LITTLE_ENDIAN)) s16 = ((s16 & 0xFF) << 8) | (s16 >> 8);
                 uint16_t* o = reinterpret_cast<uint16_t*>(A.pcm) + 2 * n;
-                if (nch == 2 || ps) o[c] = (uint16_t)s16;
+                if ((nch == 2 || ps) && !dup) o[c] = (uint16_t)s16;
                 else o[0] = o[1] = (uint16_t)s16;
             }
         }
@@ -785,9 +785,11 @@ __global__ __launch_bounds__(256) void sbr_synthesis_kernel(SbrArgs A)
     {
         const size_t cf0 = (size_t)ck.frame0 * nch + rc;
         const SbrRec& R0 = A.recs[cf0];
-        const float* prev = ps ? A.xps + ((size_t)(ck.frame0 - 1) * 2 + c) * 4096 : A.xsyn + (cf0 - nch) * 4096;
-        const float2* xp = R0.first ? reinterpret_cast<const float2*>(&A.state[(size_t)R0.slot * 2 + c].xsyn[0][0][0])
-                                    : reinterpret_cast<const float2*>(prev) + 23 * 64;
+        // PS right channel (qmfs1): history of the previous frame that carried PS data
+        const uint32_t back = (ps && c == 1) ? R0.ps_back : (R0.first ? 0u : 1u);
+        const float* prev = ps ? A.xps + ((size_t)(ck.frame0 - back) * 2 + c) * 4096 : A.xsyn + (cf0 - nch) * 4096;
+        const float2* xp = back == 0 ? reinterpret_cast<const float2*>(&A.state[(size_t)R0.slot * 2 + c].xsyn[0][0][0])
+                                     : reinterpret_cast<const float2*>(prev) + 23 * 64;
         for (int l = 0; l < 9; l++) {
             const float2 v = xp[l * 64 + u];
             slot(v.x, v.y, false, 0);
@@ -798,10 +800,14 @@ __global__ __launch_bounds__(256) void sbr_synthesis_kernel(SbrArgs A)
         const size_t cf = (size_t)f * nch + rc;
         const SbrRec& R = A.recs[cf];
         if (ps) {
+            // a frame without PS data: SBR1.process synthesises X with qmfs0 and copies the left
+            // channel to the right one (A/sbr/SBR1.java:75-81); qmfs1 does not run
+            const bool ps_on = (R.flags & kSbrPsOn) != 0;
+            if (c == 1 && !ps_on) continue;
             const float2* xq = reinterpret_cast<const float2*>(A.xps + ((size_t)f * 2 + c) * 4096);
             for (int l = 0; l < 32; l++) {
                 const float2 v = xq[l * 64 + u];
-                slot(v.x, v.y, true, (size_t)f * 2048 + 64 * l);
+                slot(v.x, v.y, true, (size_t)f * 2048 + 64 * l, !ps_on);
             }
             continue;
         }
@@ -842,7 +848,13 @@ __global__ __launch_bounds__(256) void sbr_state_kernel(SbrArgs A)
     for (int k = u; k < 512; k += 64) (&S.xlow[0][0][0])[k] = xl[k];
     if (A.ps) {  // synthesis history of both output channels comes from xps
         for (int oc = 0; oc < 2; oc++) {
-            const float* xs = A.xps + ((size_t)cf * 2 + oc) * 4096 + 23 * 128;
+            // the right channel's synthesis (qmfs1) last ran on the run's last PS frame
+            size_t fs = cf;
+            if (oc == 1 && !(R.flags & kSbrPsOn)) {
+                if (R.ps_back == 0) continue;  // no PS frame in this call: its history stays
+                fs = cf - R.ps_back;
+            }
+            const float* xs = A.xps + (fs * 2 + oc) * 4096 + 23 * 128;
             SbrChState& T = A.state[(size_t)R.slot * 2 + oc];
             for (int k = u; k < 9 * 128; k += 64) (&T.xsyn[0][0][0])[k] = xs[k];
         }

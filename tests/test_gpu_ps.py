@@ -123,8 +123,50 @@ def test_c5_single_frame_calls():
             assert np.array_equal(out[k][r], want[fb[r] + k])
 
 
+def _ps_gaps(s, pattern):
+    """ps_present per frame of each stream from `pattern` (1 = PS data)."""
+    for f in range(len(s)):
+        s[f]["ps_present"] = pattern[f % len(pattern)]
+
+
+@pytest.mark.parametrize("pattern", [
+    (0, 0, 0, 1, 1, 1, 1, 1, 1, 1, 1, 1),  # stream starts without PS: mono copies, then PS opens fresh
+    (1, 1, 0, 1, 0, 0, 1, 1, 1, 0, 1, 1),  # PS data missing in some frames: mono copies, PS state waits
+    (0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0),  # never any PS data
+])
+@pytest.mark.parametrize("flags", [N.PCM_BIG_ENDIAN, N.PCM_FLOAT32])
+def test_c5_frames_without_ps_data(pattern, flags):
+    """SBR1.process without PS data (A/sbr/SBR1.java:75-81, isPSUsed :136): the mono SBR output is
+    copied to the right channel, PSImpl and qmfs1 keep their state for the next PS frame."""
+    p = N.synth_params(5, n_streams=3, frames_per_stream=12)
+    b = _edit(N.synth_batch(p), lambda s: _ps_gaps(s, pattern))
+    got, want = _decode_both(p, b, flags)
+    _assert_same(got, want, flags)
+
+
+def test_c5_ps_gaps_across_calls():
+    """A PS gap spanning a call boundary: the next call's first PS frame takes the filterbank
+    history and the right synthesis ring from the slot state."""
+    p = N.synth_params(5, n_streams=2, frames_per_stream=10)
+    pattern = (1, 1, 1, 0, 0, 0, 0, 1, 1, 0)
+    b = _edit(N.synth_batch(p), lambda s: _ps_gaps(s, pattern))
+    cfg = N.cfg_for(p)
+    want = O.decode_batch(cfg, b, O.Streams(2), N.PCM_BIG_ENDIAN)
+    out, rest = [], b
+    with N.Context(cfg, 2) as ctx:
+        for n in (4, 2, 4):
+            part, rest = rest.split_frames(n)
+            out.append(ctx.decode(part, N.PCM_BIG_ENDIAN))
+    fb = b.frame_begin
+    k0 = 0
+    for part, n in zip(out, (4, 2, 4)):
+        for r in range(2):
+            for k in range(n):
+                assert np.array_equal(part[r * n + k], want[fb[r] + k0 + k]), (r, k0 + k)
+        k0 += n
+
+
 @pytest.mark.parametrize("name,fn,status", [
-    ("no_ps_data", lambda s: s.__setitem__("ps_present", 0), N.ERR_UNSUPPORTED),
     ("bad_nr_ipdopd_par", lambda s: s["ps"].__setitem__("nr_ipdopd_par", 12), N.ERR_BITSTREAM),
     ("border_not_32", lambda s: s["ps"]["border"].__setitem__((slice(None), 1), 30), N.ERR_BITSTREAM),
     ("iid_out_of_range", lambda s: s["ps"]["iid"].__setitem__((slice(None), 0, 3), 9), N.ERR_BITSTREAM),
