@@ -77,101 +77,165 @@ __device__ __forceinline__ DctConst load_dct_const(const float* dct, int e)
 
 // DCT.dct4_kernel distributed over the 32 lanes of a half-wave: (xr, xi) = input element e,
 // returns output element e.  Each stage performs, per element, exactly the operation the
-// sequential Java loop performs on it.
-__device__ __forceinline__ void dct4(const DctConst& K, int e, int half_base, float xr, float xi, float& orr,
-                                     float& oi)
+// sequential Java loop performs on it.  N independent transforms run in lockstep (their lane
+// exchanges overlap).
+template <int N>
+__device__ __forceinline__ void dct4_n(const DctConst& K, int e, int half_base, const float (&xr)[N], const float (&xi)[N],
+                                       float (&orr)[N], float (&oi)[N])
 {
-    float tmp = (xr + xi) * K.t0;
-    float r = (xi * K.t64) + tmp;
-    float i = (xr * K.t32) + tmp;
+    float r[N], i[N];
+#pragma unroll
+    for (int n = 0; n < N; n++) {
+        const float tmp = (xr[n] + xi[n]) * K.t0;
+        r[n] = (xi[n] * K.t64) + tmp;
+        i[n] = (xr[n] * K.t32) + tmp;
+    }
     // stage 1 (DCT.java:143-164): pairs (i, i+16)
     {
-        const float pr = swz<16>(r), pi = swz<16>(i);
-        if (e < 16) {
-            r = r + pr;
-            i = i + pi;
-        } else {
-            const float tr = pr - r, ti = pi - i;
-            r = (tr * K.w1r) - (ti * K.w1i);
-            i = (tr * K.w1i) + (ti * K.w1r);
+        float pr[N], pi[N];
+#pragma unroll
+        for (int n = 0; n < N; n++) {
+            pr[n] = swz<16>(r[n]);
+            pi[n] = swz<16>(i[n]);
+        }
+#pragma unroll
+        for (int n = 0; n < N; n++) {
+            if (e < 16) {
+                r[n] = r[n] + pr[n];
+                i[n] = i[n] + pi[n];
+            } else {
+                const float tr = pr[n] - r[n], ti = pi[n] - i[n];
+                r[n] = (tr * K.w1r) - (ti * K.w1i);
+                i[n] = (tr * K.w1i) + (ti * K.w1r);
+            }
         }
     }
     // stage 2 (:166-207): pairs (i, i+8) in each 16-group, twiddle w[2j]
     {
-        const float pr = swz<8>(r), pi = swz<8>(i);
-        if (!(e & 8)) {
-            r = r + pr;
-            i = i + pi;
-        } else {
-            const float tr = pr - r, ti = pi - i;
-            r = (tr * K.w2r) - (ti * K.w2i);
-            i = (tr * K.w2i) + (ti * K.w2r);
+        float pr[N], pi[N];
+#pragma unroll
+        for (int n = 0; n < N; n++) {
+            pr[n] = swz<8>(r[n]);
+            pi[n] = swz<8>(i[n]);
+        }
+#pragma unroll
+        for (int n = 0; n < N; n++) {
+            if (!(e & 8)) {
+                r[n] = r[n] + pr[n];
+                i[n] = i[n] + pi[n];
+            } else {
+                const float tr = pr[n] - r[n], ti = pi[n] - i[n];
+                r[n] = (tr * K.w2r) - (ti * K.w2i);
+                i[n] = (tr * K.w2i) + (ti * K.w2r);
+            }
         }
     }
     // stage 3 (:212-287): pairs (i, i+4) in each 8-group; four bottom variants
     {
-        const float pr = swz<4>(r), pi = swz<4>(i);
-        if (!(e & 4)) {
-            r = r + pr;
-            i = i + pi;
-        } else {
-            const int v = e & 3;
-            const float tr = pr - r, ti = pi - i;
-            if (v == 0) {
-                r = tr;
-                i = ti;
-            } else if (v == 1) {
-                const float a = tr + ti, b = ti - tr;
-                r = a * K.w3;
-                i = b * K.w3;
-            } else if (v == 2) {
-                const float nr = ti, ni = r - pr;
-                r = nr;
-                i = ni;
+        float pr[N], pi[N];
+#pragma unroll
+        for (int n = 0; n < N; n++) {
+            pr[n] = swz<4>(r[n]);
+            pi[n] = swz<4>(i[n]);
+        }
+#pragma unroll
+        for (int n = 0; n < N; n++) {
+            if (!(e & 4)) {
+                r[n] = r[n] + pr[n];
+                i[n] = i[n] + pi[n];
             } else {
-                const float a = tr - ti, b = tr + ti;
-                r = a * K.w3;
-                i = b * K.w3;
+                const int v = e & 3;
+                const float tr = pr[n] - r[n], ti = pi[n] - i[n];
+                if (v == 0) {
+                    r[n] = tr;
+                    i[n] = ti;
+                } else if (v == 1) {
+                    const float a = tr + ti, b = ti - tr;
+                    r[n] = a * K.w3;
+                    i[n] = b * K.w3;
+                } else if (v == 2) {
+                    const float nr = ti, ni = r[n] - pr[n];
+                    r[n] = nr;
+                    i[n] = ni;
+                } else {
+                    const float a = tr - ti, b = tr + ti;
+                    r[n] = a * K.w3;
+                    i[n] = b * K.w3;
+                }
             }
         }
     }
     // stage 4 (:291-322): pairs (i, i+2) in each 4-group
     {
-        const float pr = swz<2>(r), pi = swz<2>(i);
-        if (!(e & 2)) {
-            r = r + pr;
-            i = i + pi;
-        } else if (!(e & 1)) {
-            r = pr - r;
-            i = pi - i;
-        } else {
-            const float nr = pi - i, ni = r - pr;
-            r = nr;
-            i = ni;
+        float pr[N], pi[N];
+#pragma unroll
+        for (int n = 0; n < N; n++) {
+            pr[n] = swz<2>(r[n]);
+            pi[n] = swz<2>(i[n]);
+        }
+#pragma unroll
+        for (int n = 0; n < N; n++) {
+            if (!(e & 2)) {
+                r[n] = r[n] + pr[n];
+                i[n] = i[n] + pi[n];
+            } else if (!(e & 1)) {
+                r[n] = pr[n] - r[n];
+                i[n] = pi[n] - i[n];
+            } else {
+                const float nr = pi[n] - i[n], ni = r[n] - pr[n];
+                r[n] = nr;
+                i[n] = ni;
+            }
         }
     }
     // stage 5 (:326-341): pairs (i, i+1)
     {
-        const float pr = swz<1>(r), pi = swz<1>(i);
-        if (!(e & 1)) {
-            r = r + pr;
-            i = i + pi;
-        } else {
-            r = pr - r;
-            i = pi - i;
+        float pr[N], pi[N];
+#pragma unroll
+        for (int n = 0; n < N; n++) {
+            pr[n] = swz<1>(r[n]);
+            pi[n] = swz<1>(i[n]);
+        }
+#pragma unroll
+        for (int n = 0; n < N; n++) {
+            if (!(e & 1)) {
+                r[n] = r[n] + pr[n];
+                i[n] = i[n] + pi[n];
+            } else {
+                r[n] = pr[n] - r[n];
+                i[n] = pi[n] - i[n];
+            }
         }
     }
     // post-modulation with bit-reversed reads (:368-389)
     const int br = (int)(__builtin_bitreverse32((uint32_t)e) >> 27);
-    const float x_re = shfl(r, half_base + br), x_im = shfl(i, half_base + br);
-    if (e == 16) {
-        orr = (x_re + x_im) * K.t96;
-        oi = (x_im - x_re) * K.t96;
-    } else {
-        const float t = (x_re + x_im) * K.t96;
-        orr = (x_im * K.t160) + t;
-        oi = (x_re * K.t128) + t;
+    float x_re[N], x_im[N];
+#pragma unroll
+    for (int n = 0; n < N; n++) {
+        x_re[n] = shfl(r[n], half_base + br);
+        x_im[n] = shfl(i[n], half_base + br);
     }
+#pragma unroll
+    for (int n = 0; n < N; n++) {
+        if (e == 16) {
+            orr[n] = (x_re[n] + x_im[n]) * K.t96;
+            oi[n] = (x_im[n] - x_re[n]) * K.t96;
+        } else {
+            const float t = (x_re[n] + x_im[n]) * K.t96;
+            orr[n] = (x_im[n] * K.t160) + t;
+            oi[n] = (x_re[n] * K.t128) + t;
+        }
+    }
+}
+
+__device__ __forceinline__ void dct4(const DctConst& K, int e, int half_base, float xr, float xi, float& orr,
+                                     float& oi)
+{
+    const float a[1] = {xr}, b[1] = {xi};
+    float o1[1], o2[1];
+    dct4_n<1>(K, e, half_base, a, b, o1, o2);
+    orr = o1[0];
+    oi = o2[0];
 }
 
 
