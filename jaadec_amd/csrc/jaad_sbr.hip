@@ -13,7 +13,7 @@
 //   sbr_synthesis_kernel  one wave per chunk of kSbrSynFrames frames (9 history slots recomputed)
 //   sbr_state_kernel      last frame of each run -> slot state
 // A 32-point DCT-IV (A/sbr/DCT.java) is spread over 32 lanes, one complex point per lane; the
-// radix-2 DIF stages exchange partners with ds_swizzle (xor 16..1).
+// radix-2 DIF stages exchange partners with v_permlane16_swap (xor 16) and DPP (xor 8..1).
 #include <hip/hip_runtime.h>
 
 #include "jaad_sbr.h"
@@ -48,15 +48,16 @@ __device__ __forceinline__ float java_minf(float a, float b)
     return a <= b ? a : b;
 }
 
-// per-lane constants of a 32-point DCT-IV element e (A/sbr/DCT.java:347-391)
+// per-lane constants of a 32-point DCT-IV (A/sbr/DCT.java:347-391): lane e's butterfly twiddles
+// and the post-modulation constants of the output element E the lane returns
 struct DctConst {
-    float t0, t32, t64;        // pre-modulation
-    float t96, t128, t160;     // post-modulation
+    float t0, t32, t64;        // pre-modulation (element e)
+    float t96, t128, t160;     // post-modulation (element E)
     float w1r, w1i, w2r, w2i;  // stage 1/2 twiddles of the bottom lanes
     float w3;                  // stage 3 constant (w[4] or w[12])
 };
 
-__device__ __forceinline__ DctConst load_dct_const(const float* dct, int e)
+__device__ __forceinline__ DctConst load_dct_const(const float* dct, int e, int E)
 {
     DctConst K;
     const float* wr = dct + 192;
@@ -64,9 +65,9 @@ __device__ __forceinline__ DctConst load_dct_const(const float* dct, int e)
     K.t0 = dct[e];
     K.t32 = dct[e + 32];
     K.t64 = dct[e + 64];
-    K.t96 = dct[e + 96];
-    K.t128 = dct[e + 128];
-    K.t160 = dct[e + 160];
+    K.t96 = dct[E + 96];
+    K.t128 = dct[E + 128];
+    K.t160 = dct[E + 160];
     K.w1r = wr[e & 15];
     K.w1i = wi[e & 15];
     K.w2r = wr[2 * (e & 7)];
@@ -75,12 +76,14 @@ __device__ __forceinline__ DctConst load_dct_const(const float* dct, int e)
     return K;
 }
 
-// DCT.dct4_kernel distributed over the 32 lanes of a half-wave: (xr, xi) = input element e,
-// returns output element e.  Each stage performs, per element, exactly the operation the
-// sequential Java loop performs on it.  N independent transforms run in lockstep (their lane
-// exchanges overlap).
+// DCT.dct4_kernel distributed over the 32 lanes of a half-wave: (xr, xi) = input element e.  Each
+// stage performs, per element, exactly the operation the sequential Java loop performs on it; the
+// butterfly partners come through DPP (lane ^ 1, 2, 4, 8) and v_permlane16_swap (lane ^ 16), not
+// LDS.  The Java post-modulation reads the stage outputs in bit-reversed order (:368-389); here
+// they stay where the stages leave them, so lane e returns output element E = bitrev5(e)
+// (K = load_dct_const(dct, e, E)).  N independent transforms run in lockstep.
 template <int N>
-__device__ __forceinline__ void dct4_n(const DctConst& K, int e, int half_base, const float (&xr)[N], const float (&xi)[N],
+__device__ __forceinline__ void dct4_n(const DctConst& K, int e, int E, const float (&xr)[N], const float (&xi)[N],
                                        float (&orr)[N], float (&oi)[N])
 {
     float r[N], i[N];
@@ -95,8 +98,8 @@ __device__ __forceinline__ void dct4_n(const DctConst& K, int e, int half_base, 
         float pr[N], pi[N];
 #pragma unroll
         for (int n = 0; n < N; n++) {
-            pr[n] = swz<16>(r[n]);
-            pi[n] = swz<16>(i[n]);
+            pr[n] = xor16(r[n], e);
+            pi[n] = xor16(i[n], e);
         }
 #pragma unroll
         for (int n = 0; n < N; n++) {
@@ -207,33 +210,25 @@ __device__ __forceinline__ void dct4_n(const DctConst& K, int e, int half_base, 
             }
         }
     }
-    // post-modulation with bit-reversed reads (:368-389)
-    const int br = (int)(__builtin_bitreverse32((uint32_t)e) >> 27);
-    float x_re[N], x_im[N];
+    // post-modulation of output element E, whose bit-reversed input the stages left in this lane
 #pragma unroll
     for (int n = 0; n < N; n++) {
-        x_re[n] = shfl(r[n], half_base + br);
-        x_im[n] = shfl(i[n], half_base + br);
-    }
-#pragma unroll
-    for (int n = 0; n < N; n++) {
-        if (e == 16) {
-            orr[n] = (x_re[n] + x_im[n]) * K.t96;
-            oi[n] = (x_im[n] - x_re[n]) * K.t96;
+        if (E == 16) {
+            orr[n] = (r[n] + i[n]) * K.t96;
+            oi[n] = (i[n] - r[n]) * K.t96;
         } else {
-            const float t = (x_re[n] + x_im[n]) * K.t96;
-            orr[n] = (x_im[n] * K.t160) + t;
-            oi[n] = (x_re[n] * K.t128) + t;
+            const float t = (r[n] + i[n]) * K.t96;
+            orr[n] = (i[n] * K.t160) + t;
+            oi[n] = (r[n] * K.t128) + t;
         }
     }
 }
 
-__device__ __forceinline__ void dct4(const DctConst& K, int e, int half_base, float xr, float xi, float& orr,
-                                     float& oi)
+__device__ __forceinline__ void dct4(const DctConst& K, int e, int E, float xr, float xi, float& orr, float& oi)
 {
     const float a[1] = {xr}, b[1] = {xi};
     float o1[1], o2[1];
-    dct4_n<1>(K, e, half_base, a, b, o1, o2);
+    dct4_n<1>(K, e, E, a, b, o1, o2);
     orr = o1[0];
     oi = o2[0];
 }
@@ -256,7 +251,8 @@ __global__ __launch_bounds__(256) void sbr_analysis_kernel(SbrArgs A)
     const float* cur = A.time + (size_t)cf * 1024;
     // samples before the frame: previous frame of the run, or the slot state (first frame)
     const float* prev = R.first ? A.state[(size_t)R.slot * 2 + c].tail : A.time + (size_t)(cf - A.nch) * 1024 + 736;
-    const DctConst K = load_dct_const(A.dct, e);
+    const int E = bitrev5(e);
+    const DctConst K = load_dct_const(A.dct, e, E);
     float ca[5], cb[5];
 #pragma unroll
     for (int j = 0; j < 5; j++) {
@@ -286,11 +282,11 @@ __global__ __launch_bounds__(256) void sbr_analysis_kernel(SbrArgs A)
         const float in_r = e == 0 ? ulo : -shi;
         const float in_i = e == 0 ? uhi : slo;
         float orr, oi;
-        dct4(K, e, hb, in_r, in_i, orr, oi);
+        dct4(K, e, E, in_r, in_i, orr, oi);
         // X[2n] = 2 out[n], X[2n+1] = -2 swap(out[31-n]) (:52-71): lane (half, k) stores band k of
-        // slot 2p + half
+        // slot 2p + half (the DCT left output element m in lane bitrev5(m))
         const int k = e;
-        const int srcl = hb + ((k & 1) ? 31 - (k >> 1) : (k >> 1));
+        const int srcl = hb + bitrev5((k & 1) ? 31 - (k >> 1) : (k >> 1));
         const float vr = shfl(orr, srcl), vi = shfl(oi, srcl);
         float re = 0.0f, im = 0.0f;
         if (k < kx) {
@@ -785,7 +781,8 @@ __global__ __launch_bounds__(256) void sbr_synthesis_kernel(SbrArgs A)
     // X_right from ps_kernel (xps), whose rows need no carry patch
     const int c = ck.ch, nch = A.nch, ps = A.ps;
     const int rc = ps ? 0 : c;  // channel of the SBR records
-    const DctConst K = load_dct_const(A.dct, e);
+    const int E = bitrev5(e);  // output element of this lane's DCT-IV
+    const DctConst K = load_dct_const(A.dct, e, E);
     float cw[10];
 #pragma unroll
     for (int t = 0; t < 10; t++) cw[t] = A.qmf_c[u + 64 * t];
@@ -801,17 +798,17 @@ __global__ __launch_bounds__(256) void sbr_synthesis_kernel(SbrArgs A)
         const float in_r = scale * (half ? bi : ar);
         const float in_i = scale * (half ? ai : br);
         float orr, oi;
-        dct4(K, e, hb, in_r, in_i, orr, oi);
+        dct4(K, e, E, in_r, in_i, orr, oi);
         const float Ap = shfl(orr, u ^ 32);
         const float Bp = shfl(oi, 32 + (31 - e));
         const float Cp = shfl(oi, 31 - e);
         float* vb = vring[vpos];
         if (!half) {
-            vb[2 * e] = Ap - orr;
-            vb[127 - 2 * e] = Ap + orr;
+            vb[2 * E] = Ap - orr;
+            vb[127 - 2 * E] = Ap + orr;
         } else {
-            vb[2 * e + 1] = Bp + Cp;
-            vb[126 - 2 * e] = Bp - Cp;
+            vb[2 * E + 1] = Bp + Cp;
+            vb[126 - 2 * E] = Bp - Cp;
         }
         wave_sync();
         if (emit) {
@@ -970,28 +967,15 @@ __global__ void dct_test_kernel(const float* dct, const float* in_re, const floa
                                 float* out_im, int n)
 {
     const int u = lane_id();
-    const int e = u & 31, hb = u & 32;
+    const int e = u & 31, E = bitrev5(e);
     const int v = blockIdx.x * 2 + (u >> 5);
-    DctConst K;
-    const float* wr = dct + 192;
-    const float* wi = dct + 208;
-    K.t0 = dct[e];
-    K.t32 = dct[e + 32];
-    K.t64 = dct[e + 64];
-    K.t96 = dct[e + 96];
-    K.t128 = dct[e + 128];
-    K.t160 = dct[e + 160];
-    K.w1r = wr[e & 15];
-    K.w1i = wi[e & 15];
-    K.w2r = wr[2 * (e & 7)];
-    K.w2i = wi[2 * (e & 7)];
-    K.w3 = (e & 3) == 1 ? wr[4] : wr[12];
+    const DctConst K = load_dct_const(dct, e, E);
     const int vv = v < n ? v : n - 1;
     float orr, oi;
-    dct4(K, e, hb, in_re[32 * vv + e], in_im[32 * vv + e], orr, oi);
-    if (v < n) {
-        out_re[32 * v + e] = orr;
-        out_im[32 * v + e] = oi;
+    dct4(K, e, E, in_re[32 * vv + e], in_im[32 * vv + e], orr, oi);
+    if (v < n) {  // lane e holds output element E
+        out_re[32 * v + E] = orr;
+        out_im[32 * v + E] = oi;
     }
 }
 }  // namespace
