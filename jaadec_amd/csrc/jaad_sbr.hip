@@ -660,17 +660,22 @@ __global__ __launch_bounds__(256) void sbr_hf_kernel(SbrArgs A)
         const float rev = (u & 1) ? -1.0f : 1.0f;
         if (!smooth) {
             // bs_smoothing_mode == 1: G_filt/Q_filt are the row's envelope values, no ring
-            // (the G/Q ring output above is built from gl/ql directly)
+            // (the G/Q ring output above is built from gl/ql directly); the rows walk the
+            // envelopes in order, so each envelope's values are read from LDS once
+            int l = -1, next = first;  // next: first row of the envelope after l
+            float G_filt = 0.0f, Q_filt = 0.0f, S = 0.0f;
 #pragma unroll
             for (int r = 2; r < 40; r++) {
                 const int i = r - 2;
                 if (i < first || i >= last) continue;
-                int l = 0;
-                for (int j = 1; j < L_E; j++)
-                    if (i >= R.t_E[j]) l = j;
-                const bool no_noise = (R.no_noise >> l) & 1;
-                const float G_filt = L.gl[l][mi], qnew = L.ql[l][mi], S = L.sl[l][mi];
-                const float Q_filt = (S != 0.0f || no_noise) ? 0.0f : qnew;
+                if (i >= next) {  // wave-uniform
+                    while (l + 1 < L_E && i >= R.t_E[l + 1]) l++;
+                    next = l + 1 < L_E ? R.t_E[l + 1] : 64;
+                    const bool no_noise = (R.no_noise >> l) & 1;
+                    G_filt = L.gl[l][mi];
+                    S = L.sl[l][mi];
+                    Q_filt = (S != 0.0f || no_noise) ? 0.0f : L.ql[l][mi];
+                }
                 const int fi = (int)((R.noise0 + (uint32_t)(i - first) * (uint32_t)M + (uint32_t)mi + 1u) & 511u);
                 const int fs = (int)((R.sine0 + (uint32_t)(i - first)) & 3u);
                 if (band) {
