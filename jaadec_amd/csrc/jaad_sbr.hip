@@ -690,16 +690,22 @@ __global__ __launch_bounds__(256) void sbr_hf_kernel(SbrArgs A)
                     xi[r] = vi;
                 }
             }
-        } else
+        } else {
+        int l = -1, next = first;  // envelope walk as above
+        bool no_noise = false;
+        float gnew = 0.0f, qnew = 0.0f, S = 0.0f;
 #pragma unroll
         for (int r = 2; r < 40; r++) {
             const int i = r - 2;
             if (i < first || i >= last) continue;
-            int l = 0;
-            for (int j = 1; j < L_E; j++)
-                if (i >= R.t_E[j]) l = j;
-            const bool no_noise = (R.no_noise >> l) & 1;
-            const float gnew = L.gl[l][mi], qnew = L.ql[l][mi], S = L.sl[l][mi];
+            if (i >= next) {  // wave-uniform
+                while (l + 1 < L_E && i >= R.t_E[l + 1]) l++;
+                next = l + 1 < L_E ? R.t_E[l + 1] : 64;
+                no_noise = (R.no_noise >> l) & 1;
+                gnew = L.gl[l][mi];
+                qnew = L.ql[l][mi];
+                S = L.sl[l][mi];
+            }
 #pragma unroll
             for (int j = 0; j < 5; j++) {
                 if (j == gidx) {
@@ -747,6 +753,7 @@ __global__ __launch_bounds__(256) void sbr_hf_kernel(SbrArgs A)
             }
             gidx = gidx + 1 >= 5 ? 0 : gidx + 1;
             __builtin_amdgcn_sched_barrier(0);
+        }
         }
     }
 #endif
