@@ -241,8 +241,10 @@ constexpr int kWavesPerBlock = 4;
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void sbr_analysis_kernel(SbrArgs A)
 {
+    __shared__ float win_s[kWavesPerBlock][288 + 1024];  // the 288 samples before the frame + the frame
     const uint32_t cf = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
     if (cf >= A.n_cf) return;
+    float* win = win_s[threadIdx.x >> 6];
     const int u = lane_id();
     const int e = u & 31, half = u >> 5, hb = half << 5;
     const int c = (int)(cf % (uint32_t)A.nch);
@@ -259,7 +261,11 @@ __global__ __launch_bounds__(256) void sbr_analysis_kernel(SbrArgs A)
         ca[j] = A.qmf_c[2 * (e + 64 * j)];
         cb[j] = A.qmf_c[2 * (e + 32 + 64 * j)];
     }
-    auto smp = [&](int g) { return g >= 0 ? cur[g] : prev[288 + g]; };
+    // the window's 1312 samples are staged in LDS with coalesced loads; the 160 taps per lane are
+    // LDS reads (consecutive lanes, consecutive addresses)
+    for (int i = u; i < 288 + 1024; i += 64) win[i] = i < 288 ? prev[i] : cur[i - 288];
+    wave_sync();
+    auto smp = [&](int g) { return win[288 + g]; };
     float* out = A.xlow + (size_t)cf * 32 * 32 * 2;
     for (int p = 0; p < 16; p++) {
         // v[v_index + x] = sample (32 l + 31 - x); u[n] = sum_j v[n + 64 j] * c[2 (n + 64 j)]  (:19-30)
