@@ -794,7 +794,7 @@ __global__ __launch_bounds__(256) void sbr_synthesis_kernel(SbrArgs A)
     float(*vring)[128] = vring_s[wave];
     const SbrChunk ck = A.chunks[ci];
     const int u = lane_id();
-    const int e = u & 31, half = u >> 5, hb = half << 5;
+    const int e = u & 31, half = u >> 5;
     // PS: the SBR stages ran on the mono channel (nch = 1); channel c of the output is X_left' /
     // X_right from ps_kernel (xps), whose rows need no carry patch
     const int c = ck.ch, nch = A.nch, ps = A.ps;
