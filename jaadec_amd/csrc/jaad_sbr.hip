@@ -239,9 +239,11 @@ constexpr int kWavesPerBlock = 4;
 // ---------------------------------------------------------------------------------------------
 // AnalysisFilterbank.sbr_qmf_analysis_32 (A/sbr/AnalysisFilterbank.java:9-73)
 // ---------------------------------------------------------------------------------------------
+static_assert(sizeof(SbrChState) % 16 == 0 && offsetof(SbrChState, tail) % 16 == 0, "analysis reads tail as float4");
+
 __global__ __launch_bounds__(256) void sbr_analysis_kernel(SbrArgs A)
 {
-    __shared__ float win_s[kWavesPerBlock][288 + 1024];  // the 288 samples before the frame + the frame
+    __shared__ __attribute__((aligned(16))) float win_s[kWavesPerBlock][288 + 1024];  // the 288 samples before the frame + the frame
     const uint32_t cf = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
     if (cf >= A.n_cf) return;
     float* win = win_s[threadIdx.x >> 6];
@@ -263,7 +265,13 @@ __global__ __launch_bounds__(256) void sbr_analysis_kernel(SbrArgs A)
     }
     // the window's 1312 samples are staged in LDS with coalesced loads; the 160 taps per lane are
     // LDS reads (consecutive lanes, consecutive addresses)
-    for (int i = u; i < 288 + 1024; i += 64) win[i] = i < 288 ? prev[i] : cur[i - 288];
+    // (16-byte loads: tail and frame offsets are multiples of 4 floats, sizeof(SbrChState) of 16 B)
+    {
+        const float4* p4 = reinterpret_cast<const float4*>(prev);
+        const float4* c4 = reinterpret_cast<const float4*>(cur);
+        float4* w4 = reinterpret_cast<float4*>(win);
+        for (int i = u; i < (288 + 1024) / 4; i += 64) w4[i] = i < 72 ? p4[i] : c4[i - 72];
+    }
     wave_sync();
     auto smp = [&](int g) { return win[288 + g]; };
     float* out = A.xlow + (size_t)cf * 32 * 32 * 2;
