@@ -233,6 +233,10 @@ size_t jaad_frame_pcm_bytes(const jaad_stream_cfg* cfg, uint32_t flags);
  * (each as freshly created by Decoder.create: overlap zero, window shapes sine).            */
 int jaad_ctx_create(const jaad_stream_cfg* cfg, uint32_t n_slots, int device, jaad_ctx** out);
 void jaad_ctx_destroy(jaad_ctx* ctx);
+/* channels per ch-frame record of the context's batches: 1 (SCE core) or 2 (CPE core); this,
+ * not jaad_cfg_channel_count (the PCM channel count), sizes q/sf/cb/ics/tns.  Used by the JNI
+ * glue to check the Java side's buffers against the context.                               */
+int jaad_ctx_core_channels(const jaad_ctx* ctx);
 
 /* Synchronous host-buffer entry: copies the batch to the device, runs the DSP, copies
  * n_frames * jaad_frame_pcm_bytes(flags) bytes of PCM back to pcm_out (frame-major).       */
@@ -241,7 +245,14 @@ int jaad_decode_batch(jaad_ctx* ctx, const jaad_batch* batch, void* pcm_out, siz
 
 /* Device-resident entry: all [dev] arrays and pcm_dev are device pointers; work is queued on
  * `hip_stream` (a hipStream_t, NULL = the context's stream) and the call returns without
- * waiting.  Calls on one context must not overlap.                                         */
+ * waiting.  Calls on one context must not overlap in time on the host; on the device every
+ * call is ordered after the context's previous call whatever stream either was queued on,
+ * and jaad_wait / jaad_state_* wait for all of them.
+ * The side info is NOT range-checked on the host here (that would read device memory): the
+ * kernels clamp it instead (window_sequence & 3, window shapes & 1, max_sfb to the window's
+ * swb count, |q| to 8190, TNS window & 7 / order <= 20), so a malformed batch decodes to
+ * garbage PCM but never reads or writes outside its buffers.  jaad_decode_batch rejects the
+ * same batch with JAAD_ERR_BITSTREAM.                                                     */
 int jaad_decode_batch_device(jaad_ctx* ctx, const jaad_batch* batch, void* pcm_dev, size_t pcm_bytes,
                              uint32_t flags, void* hip_stream);
 int jaad_wait(jaad_ctx* ctx);

@@ -166,6 +166,14 @@ struct jaad_ctx {
     GlobalTables* d_gtab = nullptr;
     float* d_iq = nullptr;
     DevBuf d_chunks, d_batch, d_pcm;
+    PinnedBuf h_chunks;                  // staging of the chunk table's upload
+    hipEvent_t chunks_copied = nullptr;  // h_chunks may be rewritten once this has completed
+    bool chunks_live = false;
+    // Every call's device work (whatever stream it is queued on) waits for the previous call's
+    // `done`: the chunk table, the double-buffered state and the SBR/PS state are reused call
+    // after call.  The state_* entry points and jaad_wait wait for it too.
+    hipEvent_t done = nullptr;
+    bool done_live = false;
     std::vector<ChunkDesc> chunks;
     std::vector<uint32_t> plan_slots, plan_begin;  // plan cache key
     std::vector<uint8_t> slot_used;
@@ -292,8 +300,11 @@ int validate_cfg(const jaad_stream_cfg* cfg)
     return JAAD_OK;
 }
 
-// (Re)build the chunk table for the batch's runs; cached when the run layout repeats.
-int plan(jaad_ctx* ctx, const jaad_batch* b)
+// (Re)build the chunk table for the batch's runs; cached when the run layout repeats.  The new
+// table is built in locals and committed (cache key, slot_used, device copy) only once it is
+// complete, so a rejected batch leaves the previous plan intact.  The upload is queued on the
+// call's stream (ordered after the previous call by launch()) from page-locked staging.
+int plan(jaad_ctx* ctx, const jaad_batch* b, hipStream_t stream)
 {
     if (!b->stream_slot || !b->frame_begin) return JAAD_ERR_INVALID_ARG;
     if (b->frame_begin[0] != 0 || b->frame_begin[b->n_runs] != b->n_frames) return JAAD_ERR_INVALID_ARG;
@@ -301,8 +312,8 @@ int plan(jaad_ctx* ctx, const jaad_batch* b)
                 std::memcmp(ctx->plan_slots.data(), b->stream_slot, b->n_runs * sizeof(uint32_t)) == 0 &&
                 std::memcmp(ctx->plan_begin.data(), b->frame_begin, (b->n_runs + 1) * sizeof(uint32_t)) == 0;
     if (same) return JAAD_OK;
-    ctx->chunks.clear();
-    std::fill(ctx->slot_used.begin(), ctx->slot_used.end(), 0);
+    std::vector<ChunkDesc> chunks;
+    std::vector<uint8_t> used(ctx->n_slots, 0);
     // One wave decodes one chunk; a chunk that does not start its run re-decodes one frame.
     // Chunk length L is chosen so that the chunks fill the device's resident waves about once
     // (balanced, no tail round), but never shorter than kMinChunkFrames (prefix overhead).
@@ -316,11 +327,10 @@ int plan(jaad_ctx* ctx, const jaad_batch* b)
         uint32_t f0 = b->frame_begin[r], f1 = b->frame_begin[r + 1];
         uint32_t slot = b->stream_slot[r];
         if (f1 < f0 || slot >= ctx->n_slots) return JAAD_ERR_INVALID_ARG;
-        if (ctx->slot_used[slot]) return JAAD_ERR_INVALID_ARG;  // one run per stream per call
-        ctx->slot_used[slot] = 1;
+        if (used[slot]) return JAAD_ERR_INVALID_ARG;  // one run per stream per call
+        used[slot] = 1;
         if (f1 == f0) {  // empty run: carry the state over unchanged
-            ChunkDesc cd{f0, kChunkLoadState | kChunkStoreState, slot, 0};
-            ctx->chunks.push_back(cd);
+            chunks.push_back(ChunkDesc{f0, kChunkLoadState | kChunkStoreState, slot, 0});
             continue;
         }
         // split the run into `parts` chunks of equal length (+-1 frame)
@@ -331,14 +341,34 @@ int plan(jaad_ctx* ctx, const jaad_batch* b)
             uint32_t info = fe - f;
             info |= (f == f0) ? kChunkLoadState : kChunkPrefix;
             if (fe == f1) info |= kChunkStoreState;
-            ctx->chunks.push_back(ChunkDesc{f, info, slot, 0});
+            chunks.push_back(ChunkDesc{f, info, slot, 0});
         }
     }
-    HIPCHK(ctx->d_chunks.ensure(ctx->chunks.size() * sizeof(ChunkDesc) + 16));
-    HIPCHK(hipMemcpy(ctx->d_chunks.p, ctx->chunks.data(), ctx->chunks.size() * sizeof(ChunkDesc), hipMemcpyHostToDevice));
+    ctx->plan_valid = false;  // from here on the cached layout no longer describes d_chunks
+    const size_t bytes = chunks.size() * sizeof(ChunkDesc);
+    if (ctx->chunks_live) HIPCHK(hipEventSynchronize(ctx->chunks_copied));  // staging in use?
+    HIPCHK(ctx->h_chunks.ensure(bytes + 16));
+    HIPCHK(ctx->d_chunks.ensure(bytes + 16));
+    if (bytes) {
+        std::memcpy(ctx->h_chunks.p, chunks.data(), bytes);
+        HIPCHK(hipMemcpyAsync(ctx->d_chunks.p, ctx->h_chunks.p, bytes, hipMemcpyHostToDevice, stream));
+        HIPCHK(hipEventRecord(ctx->chunks_copied, stream));
+        ctx->chunks_live = true;
+    }
+    ctx->chunks.swap(chunks);
+    ctx->slot_used.swap(used);
     ctx->plan_slots.assign(b->stream_slot, b->stream_slot + b->n_runs);
     ctx->plan_begin.assign(b->frame_begin, b->frame_begin + b->n_runs + 1);
     ctx->plan_valid = true;
+    return JAAD_OK;
+}
+
+// wait (host) until every call queued on the context so far has finished on the device
+int sync_ctx(jaad_ctx* ctx)
+{
+    HIPCHK(hipSetDevice(ctx->device));
+    if (ctx->done_live) HIPCHK(hipEventSynchronize(ctx->done));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
     return JAAD_OK;
 }
 
@@ -492,6 +522,10 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
     std::vector<int> rcs(nt, 0), bad(nt, -1);
     std::vector<uint32_t> used(nt, 0);
     std::vector<char> smooth(nt, 0);
+    // a failed call must leave every slot's host SBR state as it found it (the device state and
+    // the core overlap are untouched then): each run's slot is saved before its first frame
+    std::vector<SbrHostSlot> saved(b->n_runs);
+    std::vector<char> saved_ok(b->n_runs, 0);
     std::function<void(int)> work = [&](int t) {
         if (t >= nt) return;  // the pool may be wider than this call's run blocks
         float* region = reinterpret_cast<float*>(h2) + rbase[t];
@@ -500,6 +534,8 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
         bool sm = false;
         for (uint32_t r = rr[t]; r < rr[t + 1] && !rcs[t]; r++) {
             SbrHostSlot& hs = ctx->sbr_slots[b->stream_slot[r]];
+            saved[r] = hs;
+            saved_ok[r] = 1;
             const uint32_t fe = b->frame_begin[r + 1];
             for (uint32_t f = b->frame_begin[r]; f < fe; f++) {
                 if (f + 2 < fe)  // the records are large and sparse-read: pull frame f+2 in early
@@ -549,6 +585,9 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
     bool smoothing = false;
     for (int t = 0; t < nt; t++) {
         if (rcs[t]) {
+            // restore every run any worker started (a worker stops at its first bad frame)
+            for (uint32_t r = 0; r < b->n_runs; r++)
+                if (saved_ok[r]) ctx->sbr_slots[b->stream_slot[r]] = saved[r];
             ctx->err = (ps ? "SBR/PS side info of frame " : "SBR side info of frame ") + std::to_string(bad[t]);
             return rcs[t];
         }
@@ -649,9 +688,9 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
     return JAAD_OK;
 }
 
-int launch(jaad_ctx* ctx, const jaad_batch* db, void* pcm, uint32_t flags, hipStream_t stream)
+int launch_work(jaad_ctx* ctx, const jaad_batch* db, void* pcm, uint32_t flags, hipStream_t stream)
 {
-    int rc = plan(ctx, db);
+    int rc = plan(ctx, db, stream);
     if (rc) return rc;
     KernelArgs a{};
     a.q = db->q;
@@ -683,6 +722,16 @@ int launch(jaad_ctx* ctx, const jaad_batch* db, void* pcm, uint32_t flags, hipSt
     if (sbr && (rc = launch_sbr_stage(ctx, db, pcm, flags, stream))) return rc;
     ctx->parity ^= 1;
     return JAAD_OK;
+}
+
+int launch(jaad_ctx* ctx, const jaad_batch* db, void* pcm, uint32_t flags, hipStream_t stream)
+{
+    if (ctx->done_live) HIPCHK(hipStreamWaitEvent(stream, ctx->done, 0));
+    const int rc = launch_work(ctx, db, pcm, flags, stream);
+    // recorded on failure too: whatever part of the call was queued is covered by the next wait
+    HIPCHK(hipEventRecord(ctx->done, stream));
+    ctx->done_live = true;
+    return rc;
 }
 
 }  // namespace
@@ -769,6 +818,9 @@ int jaad_ctx_create(const jaad_stream_cfg* cfg, uint32_t n_slots, int device, ja
     hipError_t e;
     if ((e = hipSetDevice(device)) != hipSuccess) return bail(e, "hipSetDevice");
     if ((e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking)) != hipSuccess) return bail(e, "hipStreamCreate");
+    if ((e = hipEventCreateWithFlags(&ctx->done, hipEventDisableTiming)) != hipSuccess) return bail(e, "hipEventCreate");
+    if ((e = hipEventCreateWithFlags(&ctx->chunks_copied, hipEventDisableTiming)) != hipSuccess)
+        return bail(e, "hipEventCreate");
     size_t sbytes = (size_t)n_slots * 2048 * sizeof(float);
     for (int i = 0; i < 2; i++) {
         if ((e = hipMalloc(&ctx->d_state[i], sbytes)) != hipSuccess) return bail(e, "hipMalloc state");
@@ -845,6 +897,7 @@ void jaad_ctx_destroy(jaad_ctx* ctx)
 {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
+    if (ctx->done_live) (void)hipEventSynchronize(ctx->done);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     for (int i = 0; i < 2; i++)
         if (ctx->d_state[i]) (void)hipFree(ctx->d_state[i]);
@@ -869,6 +922,9 @@ void jaad_ctx_destroy(jaad_ctx* ctx)
     }
     if (ctx->cstream) (void)hipStreamDestroy(ctx->cstream);
     ctx->d_chunks.release();
+    ctx->h_chunks.release();
+    if (ctx->done) (void)hipEventDestroy(ctx->done);
+    if (ctx->chunks_copied) (void)hipEventDestroy(ctx->chunks_copied);
     ctx->d_batch.release();
     ctx->d_pcm.release();
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -962,9 +1018,10 @@ int jaad_decode_batch_device(jaad_ctx* ctx, const jaad_batch* b, void* pcm_dev, 
 int jaad_wait(jaad_ctx* ctx)
 {
     if (!ctx) return JAAD_ERR_INVALID_ARG;
-    HIPCHK(hipDeviceSynchronize());
-    return JAAD_OK;
+    return sync_ctx(ctx);
 }
+
+int jaad_ctx_core_channels(const jaad_ctx* ctx) { return ctx ? ctx->nch : JAAD_ERR_INVALID_ARG; }
 
 // per-slot state blob: core overlap [2][1024] f32 | (SBR) device SbrChState[2] | host SbrHostSlot
 // | (PS) device PsState
@@ -978,8 +1035,8 @@ size_t jaad_state_bytes(const jaad_ctx* ctx)
 int jaad_state_export(jaad_ctx* ctx, uint32_t slot, void* buf, size_t bytes)
 {
     if (!ctx || !buf || slot >= ctx->n_slots || bytes < jaad_state_bytes(ctx)) return JAAD_ERR_INVALID_ARG;
-    HIPCHK(hipSetDevice(ctx->device));
-    HIPCHK(hipStreamSynchronize(ctx->stream));
+    int rc = sync_ctx(ctx);
+    if (rc) return rc;
     char* o = static_cast<char*>(buf);
     HIPCHK(hipMemcpy(o, ctx->d_state[ctx->parity] + (size_t)slot * 2048, 2048 * sizeof(float), hipMemcpyDeviceToHost));
     if (ctx->cfg.sbr) {
@@ -996,8 +1053,8 @@ int jaad_state_export(jaad_ctx* ctx, uint32_t slot, void* buf, size_t bytes)
 int jaad_state_import(jaad_ctx* ctx, uint32_t slot, const void* buf, size_t bytes)
 {
     if (!ctx || !buf || slot >= ctx->n_slots || bytes < jaad_state_bytes(ctx)) return JAAD_ERR_INVALID_ARG;
-    HIPCHK(hipSetDevice(ctx->device));
-    HIPCHK(hipStreamSynchronize(ctx->stream));
+    int rc = sync_ctx(ctx);
+    if (rc) return rc;
     const char* in = static_cast<const char*>(buf);
     {  // the overlap must be finite (the LC kernel's PCM rounding relies on it, jaad_lc.hip round_pk16)
         float ov[2048];
@@ -1026,8 +1083,8 @@ int jaad_state_import(jaad_ctx* ctx, uint32_t slot, const void* buf, size_t byte
 int jaad_state_reset(jaad_ctx* ctx, uint32_t slot)
 {
     if (!ctx || slot >= ctx->n_slots) return JAAD_ERR_INVALID_ARG;
-    HIPCHK(hipSetDevice(ctx->device));
-    HIPCHK(hipStreamSynchronize(ctx->stream));
+    int rc = sync_ctx(ctx);
+    if (rc) return rc;
     HIPCHK(hipMemset(ctx->d_state[ctx->parity] + (size_t)slot * 2048, 0, 2048 * sizeof(float)));
     if (ctx->cfg.sbr) {
         HIPCHK(hipMemset(ctx->d_sbr_state + (size_t)slot * 2, 0, 2 * sizeof(SbrChState)));

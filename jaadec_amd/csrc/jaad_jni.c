@@ -62,12 +62,18 @@ JNIEXPORT void JNICALL Java_net_sourceforge_jaad_aac_gpu_GpuDSP_nativeDestroy(JN
 /* static native void nativeDecode(long h, int nFrames, int nRuns, int nch, ByteBuffer streamSlot,
  *     ByteBuffer frameBegin, ByteBuffer q, ByteBuffer sf, ByteBuffer cb, ByteBuffer ics,
  *     ByteBuffer msUsed, ByteBuffer tns, ByteBuffer sbr, ByteBuffer pcm, int flags);
- * sbr: one jaad_sbr_frame (1792 B) per frame for SBR/PS streams, else null */
+ * nch: channels per ch-frame record (1 SCE core, 2 CPE core); must equal the context's
+ * (jaad_ctx_core_channels), since every buffer capacity below is checked against it.
+ * sbr: one jaad_sbr_frame (1968 B, sizeof(jaad_sbr_frame)) per frame for SBR/PS streams, else null */
 JNIEXPORT void JNICALL Java_net_sourceforge_jaad_aac_gpu_GpuDSP_nativeDecode(
     JNIEnv* env, jclass cls, jlong h, jint n_frames, jint n_runs, jint nch, jobject stream_slot, jobject frame_begin,
     jobject q, jobject sf, jobject cb, jobject ics, jobject ms_used, jobject tns, jobject sbr, jobject pcm, jint flags) {
     (void)cls;
     jaad_ctx* ctx = (jaad_ctx*)(intptr_t)h;
+    if (!ctx || n_frames < 0 || n_runs < 0 || nch != jaad_ctx_core_channels(ctx)) {
+        throw_aac(env, ctx, JAAD_ERR_INVALID_ARG);
+        return;
+    }
     const jlong ncf = (jlong)n_frames * nch;
     jaad_batch b;
     memset(&b, 0, sizeof b);

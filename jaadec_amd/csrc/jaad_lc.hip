@@ -167,15 +167,18 @@ struct Ics {
     uint32_t pns;
     int nbands;  // number of (group, sfb) bands = groups * max_sfb
 };
-__device__ __forceinline__ Ics ics_from_lanes(uint32_t side, int base)
+// The fields are clamped to what the kernel can index safely: jaad_decode_batch rejects out-of-
+// range side info on the host, jaad_decode_batch_device does not look at it (jaad_gpu.h).
+__device__ __forceinline__ Ics ics_from_lanes(uint32_t side, int base, const LdsTables& T)
 {
     const uint32_t a = __builtin_amdgcn_readlane(side, base);
     const uint32_t b = __builtin_amdgcn_readlane(side, base + 1);
     Ics r;
-    r.seq = a & 0xff;
-    r.shape = (a >> 8) & 0xff;
-    r.shape_prev = (a >> 16) & 0xff;
-    r.max_sfb = a >> 24;
+    r.seq = a & 3;
+    r.shape = (a >> 8) & 1;
+    r.shape_prev = (a >> 16) & 1;
+    const int lim = r.seq == JAAD_EIGHT_SHORT_SEQUENCE ? T.nswb_s : T.nswb_l;
+    r.max_sfb = min((int)(a >> 24), lim);
     r.grouping = b & 0xff;
     r.flags = (b >> 8) & 0xff;
     r.pns = __builtin_amdgcn_readlane(side, base + 2);
@@ -501,7 +504,7 @@ __device__ void tns_spec(float* buf, float* scratch, const LdsTables& T, const G
                 inc = -1;
                 start = end - 1;
             }
-            const int base = (is_short ? 128 * F.window : 0) + start;
+            const int base = (is_short ? 128 * (F.window & 7) : 0) + start;
             for (int n = 0; n < size; n++) {
                 float y = buf[eo_idx(base + n * inc)];
                 for (int j = 0; j < order; j++) {
@@ -857,8 +860,8 @@ __global__ __launch_bounds__(64 * waves_per_wg<kTnsSpec>()) void lc_decode_kerne
 #endif
 
             // ---------------- side info ----------------
-            const Ics iL = ics_from_lanes(cur.side, 0);
-            const Ics iR = stereo ? ics_from_lanes(cur.side, 4) : iL;
+            const Ics iL = ics_from_lanes(cur.side, 0, T);
+            const Ics iR = stereo ? ics_from_lanes(cur.side, 4, T) : iL;
             const bool ms_on = stereo && (iL.flags & JAAD_ICS_COMMON_WINDOW) && (iL.flags & JAAD_ICS_MS_PRESENT);
             const bool is_on = stereo && (iR.flags & JAAD_ICS_HAS_IS);
             const bool same_bands = !stereo || (iL.seq == iR.seq && iL.max_sfb == iR.max_sfb && iL.grouping == iR.grouping);

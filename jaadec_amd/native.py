@@ -76,7 +76,7 @@ class SynthParams(C.Structure):
 
 # every symbol include/jaad_gpu.h declares (checked by tests/test_abi.py)
 EXPORTS = ["jaad_cfg_sample_length", "jaad_cfg_channel_count", "jaad_frame_pcm_bytes", "jaad_ctx_create",
-           "jaad_ctx_destroy", "jaad_decode_batch", "jaad_decode_batch_device", "jaad_wait", "jaad_state_bytes",
+           "jaad_ctx_destroy", "jaad_ctx_core_channels", "jaad_decode_batch", "jaad_decode_batch_device", "jaad_wait", "jaad_state_bytes",
            "jaad_state_export", "jaad_state_import", "jaad_state_reset", "jaad_strerror", "jaad_last_error"]
 
 
@@ -106,6 +106,7 @@ def lib() -> C.CDLL:
         L.jaad_ctx_create.argtypes = [C.POINTER(StreamCfg), C.c_uint32, C.c_int, C.POINTER(C.c_void_p)]
         L.jaad_ctx_destroy.argtypes = [C.c_void_p]
         L.jaad_ctx_destroy.restype = None
+        L.jaad_ctx_core_channels.argtypes = [C.c_void_p]
         L.jaad_decode_batch.argtypes = [C.c_void_p, C.POINTER(BatchStruct), C.c_void_p, C.c_size_t, C.c_uint32]
         L.jaad_decode_batch_device.argtypes = [C.c_void_p, C.POINTER(BatchStruct), C.c_void_p, C.c_size_t,
                                                C.c_uint32, C.c_void_p]
