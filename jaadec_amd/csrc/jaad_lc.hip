@@ -794,6 +794,10 @@ __global__ __launch_bounds__(64 * waves_per_wg<kTnsSpec>()) void lc_decode_kerne
         for (int i = threadIdx.x; i < (int)(sizeof(LdsTables) / 16); i += kThreads) dst[i] = src[i];
     }
     __syncthreads();  // the only workgroup barrier: waves are independent from here on
+#ifdef JAAD_WAVETIME
+    const uint64_t wt0 = __builtin_amdgcn_s_memrealtime();
+    uint32_t wt_frames = 0;
+#endif
 
     constexpr bool big_endian = !(kOut & JAAD_PCM_LITTLE_ENDIAN);
     constexpr bool planar = kOut == (int)kOutPlanarF32;
@@ -850,6 +854,23 @@ __global__ __launch_bounds__(64 * waves_per_wg<kTnsSpec>()) void lc_decode_kerne
         if (my_n > 0) prefetch(A, f_first, stereo, lane_id(), pf);
 
         for (int it = 0; it < my_n; it++) {
+#ifndef JAAD_LC_NOPRIO
+            // Issue arbitration between the waves of a SIMD favours the oldest wave, so the
+            // waves of a SIMD would finish one after another and the last ones run with their
+            // latency exposed.  A wave's priority drops as it advances through its chunk: the
+            // waves that are behind catch up (C2: wave lifetimes 83 -> 89 % of the kernel span,
+            // batch time -5 %, scripts/wavetime.py).
+            {
+                const int q4 = (4 * it) / my_n;
+                if (q4 == 0) __builtin_amdgcn_s_setprio(3);
+                else if (q4 == 1) __builtin_amdgcn_s_setprio(2);
+                else if (q4 == 2) __builtin_amdgcn_s_setprio(1);
+                else __builtin_amdgcn_s_setprio(0);
+            }
+#endif
+#ifdef JAAD_WAVETIME
+            wt_frames++;
+#endif
             const int u = lane_id();
             const int f = f_first + it;
             const bool emit = f >= (int)cd.frame0;
@@ -1195,6 +1216,18 @@ __global__ __launch_bounds__(64 * waves_per_wg<kTnsSpec>()) void lc_decode_kerne
             }
         }
     }
+#ifdef JAAD_WAVETIME
+    {   // profiling builds only: first/last s_memrealtime of each wave (scripts/wavetime.py)
+        const uint64_t wt1 = __builtin_amdgcn_s_memrealtime();
+        if (A.dbg && lane_id() == 0) {
+            uint64_t* o = reinterpret_cast<uint64_t*>(A.dbg) + (size_t)(blockIdx.x * kW + wave) * 4;
+            o[0] = wt0;
+            o[1] = wt1;
+            o[2] = (uint64_t)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11));  // HW_REG_XCC_ID[3:0]
+            o[3] = (uint64_t)wt_frames;
+        }
+    }
+#endif
 #ifdef JAAD_STAMPS
     if (A.dbg && lane_id() == 0) {
         uint32_t* o = reinterpret_cast<uint32_t*>(A.dbg) + (size_t)(blockIdx.x * kW + wave) * 16;
