@@ -35,7 +35,9 @@ typedef enum jaad_status {
     JAAD_ERR_UNSUPPORTED = -4,   /* profile/config not decodable (A/Decoder.java:115-116)     */
     JAAD_ERR_BITSTREAM = -5,     /* side info out of range, e.g. max_sfb > swb count          */
     JAAD_ERR_NOMEM = -6,
-    JAAD_ERR_ABI = -7            /* jaad_stream_cfg.abi_version mismatch                      */
+    JAAD_ERR_ABI = -7,           /* jaad_stream_cfg.abi_version mismatch                      */
+    JAAD_ERR_EOS = -8            /* a frame's bitstream ended early (EOSException: the reference
+                                    drops the frame, A/Decoder.java:96-100)                    */
 } jaad_status;
 
 /* ---- ICSInfo.WindowSequence ordinals (A/syntax/ICSInfo.java:26-53) ---- */

@@ -1,0 +1,89 @@
+/*
+ * jaad_parse.h -- host-side bitstream front end feeding the jaad_gpu.h batch layout.
+ *
+ * The reference parses on the JVM: Decoder.decode0 (A/Decoder.java:103-121)
+ * calls syntacticElements.decode(in) (A/syntax/SyntacticElements.java:57-132) and then the DSP.
+ * In the drop-in the DSP is jaad_decode_batch*; this library is the parse half for hosts that
+ * have no JVM parser: it turns raw_data_blocks (ADTS payloads, MP4 samples) into exactly the
+ * records the JVM-side emitter would write -- quantised spectra, scalefactor/codebook rows,
+ * jaad_ics_info, M/S masks, TNS records -- with the reference's parse semantics:
+ *
+ *   element loop / FIL / DSE / PCE   A/syntax/SyntacticElements.java:57-203, DSE.java, PCE.java
+ *   CPE / SCE                        A/syntax/CPE.java:85-123, SCE.java
+ *   ics_info                         A/syntax/ICSInfo.java:86-119
+ *   section data, scalefactors       A/syntax/ICStream.java:113-146, 172-220
+ *   pulse data (parsed, not applied) A/syntax/ICStream.java:148-170
+ *   TNS data                         A/tools/TNS.java:35-61
+ *   spectral Huffman + escapes       A/syntax/ICStream.java:222-275, A/huffman/Huffman.java:15-84
+ *   static PNS LCG state             A/syntax/ICStream.java:26,247 (one LCG per parser)
+ *   AudioSpecificConfig              A/DecoderConfig.java:175-291
+ *   ADTS header / sync search        S/adts/ADTSFrame.java, S/adts/ADTSDemultiplexer.java:25-58
+ *
+ * Plain C types only; every entry point returns 0 or a negative jaad_status.
+ */
+#ifndef JAAD_PARSE_H
+#define JAAD_PARSE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "jaad_gpu.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* AudioSpecificConfig -> stream configuration (DecoderConfig.decode).  AOT 2 (LC), 5 (SBR) and
+ * 29 (PS) with an LC core; frameLengthFlag = 1 (960-sample frames) is rejected as the
+ * reference rejects it (JAAD_ERR_UNSUPPORTED). */
+int jaad_asc_parse(const uint8_t* asc, size_t bytes, jaad_stream_cfg* cfg);
+
+/* ADTS fixed + variable header (S/adts/ADTSFrame.java:48-111) */
+typedef struct jaad_adts_header {
+    uint8_t profile;            /* audio object type = profile_ObjectType + 1 (2 = LC)          */
+    uint8_t sf_index;
+    uint8_t channel_config;
+    uint8_t protection_absent;
+    uint8_t n_raw_blocks;       /* number_of_raw_data_blocks_in_frame + 1                         */
+    uint8_t reserved[3];
+    uint32_t frame_length;      /* aac_frame_length: header + payload bytes                      */
+    uint32_t header_bytes;      /* 7, or 9 with the CRC word                                      */
+} jaad_adts_header;
+
+/* Find the next ADTS sync word (0xFFF, layer 0) at or after buf[0] within the reference's
+ * search window (ADTSDemultiplexer.MAXIMUM_FRAME_SIZE = 6144 bytes) and decode its header.
+ * *offset = byte offset of the header.  JAAD_ERR_EOS when no complete header is found. */
+int jaad_adts_find(const uint8_t* buf, size_t bytes, size_t* offset, jaad_adts_header* h);
+/* stream configuration implied by an ADTS header (AAC LC only) */
+int jaad_adts_cfg(const jaad_adts_header* h, jaad_stream_cfg* cfg);
+
+typedef struct jaad_parser jaad_parser;
+
+int jaad_parser_create(const jaad_stream_cfg* cfg, jaad_parser** out);
+void jaad_parser_destroy(jaad_parser* p);
+/* the static ICStream.randomState (PNS) the next ch-frame starts from; 0x1F2E3D4C initially */
+uint32_t jaad_parser_pns_state(const jaad_parser* p);
+void jaad_parser_set_pns_state(jaad_parser* p, uint32_t state);
+
+/* Where one frame's records go: this frame's slot in each jaad_batch array (nch = 1 for an
+ * SCE config, 2 for a CPE config).  tns may be NULL (TNS data is then parsed and dropped:
+ * the reference does not apply it either); sbr is required when cfg.sbr is set. */
+typedef struct jaad_frame_out {
+    int16_t* q;            /* [nch][1024] */
+    uint8_t* sf;           /* [nch][128]  */
+    uint8_t* cb;           /* [nch][128]  */
+    jaad_ics_info* ics;    /* [nch]       */
+    uint64_t* ms_used;     /* [2], CPE only */
+    jaad_tns* tns;         /* [nch] or NULL */
+    jaad_sbr_frame* sbr;   /* [1] when cfg.sbr */
+} jaad_frame_out;
+
+/* Parse one raw_data_block (SyntacticElements.decode) into *out.  On error nothing of the
+ * parser's state (window shapes, PNS LCG, SBR/PS history) changes, so the caller may drop
+ * the frame as Decoder.decodeFrame drops an EOS frame (A/Decoder.java:96-100). */
+int jaad_parse_frame(jaad_parser* p, const uint8_t* data, size_t bytes, jaad_frame_out* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* JAAD_PARSE_H */

@@ -50,7 +50,8 @@ def build_gpu(force: bool = False, out: Path | None = None, defines: list[str] |
               extra: list[str] | None = None) -> Path:
     """Build the product library (or, with `defines`, an experimental variant at `out`)."""
     out = out or LIB
-    srcs = [CSRC / "jaad_lc.hip", CSRC / "jaad_sbr.hip", CSRC / "jaad_ps.hip", CSRC / "jaad_capi.cpp", CSRC / "jaad_sbr_host.cpp"]
+    srcs = [CSRC / "jaad_lc.hip", CSRC / "jaad_sbr.hip", CSRC / "jaad_ps.hip", CSRC / "jaad_capi.cpp", CSRC / "jaad_sbr_host.cpp",
+            CSRC / "jaad_parse.cpp", CSRC / "jaad_parse_sbr.cpp"]
     deps = srcs + _deps("jaadec_amd/csrc/*.h", "jaadec_amd/csrc/tables/*.inc", "include/*.h")
     if force or defines or extra or _stale(out, deps):
         tmp = out.with_suffix(".so.tmp")
@@ -72,7 +73,8 @@ def build_synth(force: bool = False) -> Path:
 
 
 def build_oracle(force: bool = False) -> Path:
-    srcs = [ROOT / "oracle" / "jaad_oracle.c", ROOT / "oracle" / "jaad_oracle_sbr.c", ROOT / "oracle" / "jaad_oracle_ps.c"]
+    srcs = [ROOT / "oracle" / "jaad_oracle.c", ROOT / "oracle" / "jaad_oracle_sbr.c", ROOT / "oracle" / "jaad_oracle_ps.c",
+            ROOT / "oracle" / "jaad_writer.c"]
     deps = srcs + _deps("oracle/*.h", "include/*.h", "jaadec_amd/csrc/tables/*.inc")
     if force or _stale(ORACLE_LIB, deps):
         _run(["gcc", "-O2", "-std=c11", "-fPIC", "-shared", "-ffp-contract=off", "-fno-fast-math",

@@ -766,6 +766,7 @@ const char* jaad_strerror(int status)
     case JAAD_ERR_BITSTREAM: return "bitstream side info out of range";
     case JAAD_ERR_NOMEM: return "out of memory";
     case JAAD_ERR_ABI: return "ABI version mismatch";
+    case JAAD_ERR_EOS: return "end of bitstream inside a frame";
     default: return "unknown status";
     }
 }

@@ -1,0 +1,649 @@
+// Host bitstream front end (include/jaad_parse.h): raw_data_block -> jaad_gpu.h records.
+//
+// Follows the reference's parse (A/ = aac/src/main/java/net/sourceforge/jaad/aac/), element by
+// element, with the same validity checks; where the reference would throw (AACException,
+// EOSException, or an ArrayIndexOutOfBounds its tables would raise) the frame is rejected
+// with JAAD_ERR_BITSTREAM / JAAD_ERR_EOS / JAAD_ERR_UNSUPPORTED and the parser's state is left
+// as it was.  SBR/PS extension payloads go to jaad_parse_sbr.cpp.
+#include "../../include/jaad_parse.h"
+
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <vector>
+
+#include "jaad_parse_internal.h"
+#include "tables/jaad_huffman_tables.inc"
+#include "tables/jaad_tables.inc"
+
+namespace jaad {
+namespace parse {
+
+// ------------------------------------------------------------------------------------------
+// Huffman codebooks (A/huffman/Codebooks.java rows {length, codeword, values...}) as two-level
+// lookup tables over the next `maxlen` bits.  For every valid codeword the result is the row
+// Huffman.findOffset's linear scan (A/huffman/Huffman.java:15-28) stops at; a bit pattern that
+// no codeword prefixes (the scan would run off the table) is an error.
+// ------------------------------------------------------------------------------------------
+struct Lut {
+    int maxlen = 0, pbits = 0;
+    std::vector<uint32_t> e;  // primary [1<<pbits], then secondaries; entry: len<<16 | row,
+                              // 0x80000000 | base of a secondary table, or 0xFFFFFFFF invalid
+    void build(const int* rows, int nrows, int stride)
+    {
+        maxlen = 0;
+        for (int i = 0; i < nrows; i++) maxlen = rows[i * stride] > maxlen ? rows[i * stride] : maxlen;
+        pbits = maxlen < 10 ? maxlen : 10;
+        const int sbits = maxlen - pbits;
+        e.assign((size_t)1 << pbits, 0xFFFFFFFFu);
+        for (int i = 0; i < nrows; i++) {
+            const int len = rows[i * stride];
+            const uint32_t cw = (uint32_t)rows[i * stride + 1];
+            const uint32_t ent = ((uint32_t)len << 16) | (uint32_t)i;
+            if (len <= pbits) {
+                const uint32_t lo = cw << (pbits - len), n = 1u << (pbits - len);
+                for (uint32_t k = 0; k < n; k++) e[lo + k] = ent;
+            } else {
+                const uint32_t pre = cw >> (len - pbits);
+                if (e[pre] == 0xFFFFFFFFu) {
+                    e[pre] = 0x80000000u | (uint32_t)e.size();
+                    e.resize(e.size() + ((size_t)1 << sbits), 0xFFFFFFFFu);
+                }
+                const uint32_t base = e[pre] & 0x7FFFFFFFu;
+                const int rest = len - pbits;
+                const uint32_t lo = (cw & ((1u << rest) - 1u)) << (sbits - rest), n = 1u << (sbits - rest);
+                for (uint32_t k = 0; k < n; k++) e[base + lo + k] = ent;
+            }
+        }
+    }
+    // row index, or -1 (no codeword) / -2 (bitstream ended)
+    int decode(BitReader& br) const
+    {
+        const uint32_t peek = br.peek(maxlen);
+        uint32_t ent = e[peek >> (maxlen - pbits)];
+        if (ent != 0xFFFFFFFFu && (ent & 0x80000000u))
+            ent = e[(ent & 0x7FFFFFFFu) + (peek & ((1u << (maxlen - pbits)) - 1u))];
+        if (ent == 0xFFFFFFFFu) return br.left() < maxlen ? -2 : -1;
+        const int len = (int)(ent >> 16);
+        if (br.left() < len) return -2;
+        br.skip(len);
+        return (int)(ent & 0xFFFFu);
+    }
+};
+
+struct Books {
+    Lut spec[11], sf;
+    const int* rows[11];
+    int stride[11];
+};
+
+const Books& books()
+{
+    static Books B;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        const int* r[11] = {&JAAD_HCB1[0][0], &JAAD_HCB2[0][0], &JAAD_HCB3[0][0], &JAAD_HCB4[0][0], &JAAD_HCB5[0][0],
+                            &JAAD_HCB6[0][0], &JAAD_HCB7[0][0], &JAAD_HCB8[0][0], &JAAD_HCB9[0][0], &JAAD_HCB10[0][0],
+                            &JAAD_HCB11[0][0]};
+        const int n[11] = {81, 81, 81, 81, 81, 81, 64, 64, 169, 169, 289};
+        for (int i = 0; i < 11; i++) {
+            B.rows[i] = r[i];
+            B.stride[i] = i < 4 ? 6 : 4;
+            B.spec[i].build(r[i], n[i], B.stride[i]);
+        }
+        B.sf.build(&JAAD_HCB_SF[0][0], 121, 3);
+    });
+    return B;
+}
+
+// ------------------------------------------------------------------------------------------
+// ICS parse
+// ------------------------------------------------------------------------------------------
+struct IcsInfo {  // ICSInfo after decode / setCommonData
+    int seq = 0, shape = 0, max_sfb = 0, grouping = 0;
+    int ngroups = 1, glen[8] = {1};
+};
+
+// ICSInfo.decode (A/syntax/ICSInfo.java:86-119); prediction data is not part of AAC LC
+// (readPredictionData throws for every other profile, :122-138)
+int read_ics_info(BitReader& br, const Cfg& C, IcsInfo& I)
+{
+    if (br.left() < 11) return JAAD_ERR_EOS;
+    br.skip(1);  // ics_reserved_bit
+    I.seq = (int)br.read(2);
+    I.shape = (int)br.read(1);
+    I.ngroups = 1;
+    I.glen[0] = 1;
+    I.grouping = 0;
+    if (I.seq == JAAD_EIGHT_SHORT_SEQUENCE) {
+        I.max_sfb = (int)br.read(4);
+        for (int i = 0; i < 7; i++) {
+            if (br.read(1)) {
+                I.glen[I.ngroups - 1]++;
+                I.grouping |= 1 << i;
+            } else {
+                I.glen[I.ngroups++] = 1;
+            }
+        }
+        if (I.max_sfb > C.nswb_s) return JAAD_ERR_BITSTREAM;
+    } else {
+        I.max_sfb = (int)br.read(6);
+        if (br.left() < 1) return JAAD_ERR_EOS;
+        if (br.read(1)) return JAAD_ERR_UNSUPPORTED;  // predictor_data_present: AAC Main / LTP only
+        if (I.max_sfb > C.nswb_l) return JAAD_ERR_BITSTREAM;
+    }
+    return br.overrun() ? JAAD_ERR_EOS : JAAD_OK;
+}
+
+// ICStream.decode (A/syntax/ICStream.java:60-111) of one channel into its records.
+// `prev_shape` is ICSInfo.windowShape[CURRENT] of the previous frame of this channel.
+int read_ics(BitReader& br, const Cfg& C, bool common_window, IcsInfo& I, int prev_shape, uint32_t& pns,
+             ChOut& o)
+{
+    const Books& B = books();
+    if (br.left() < 8) return JAAD_ERR_EOS;
+    const int global_gain = (int)br.read(8);
+    if (!common_window) {
+        const int st = read_ics_info(br, C, I);
+        if (st) return st;
+    }
+    const bool is_short = I.seq == JAAD_EIGHT_SHORT_SEQUENCE;
+    const short* swb = is_short ? JAAD_SWB_OFFSET_SHORT_WINDOW[C.sf_index] : JAAD_SWB_OFFSET_LONG_WINDOW[C.sf_index];
+    const int nswb = is_short ? C.nswb_s : C.nswb_l;
+    const int max_sfb = I.max_sfb;
+
+    // ---- section data (decodeSectionData, :113-146)
+    uint8_t cb[128] = {0};
+    uint8_t sect_end[128] = {0};
+    {
+        const int bits = is_short ? 3 : 5, esc = (1 << bits) - 1;
+        int idx = 0;
+        for (int g = 0; g < I.ngroups; g++) {
+            for (int k = 0; k < max_sfb;) {
+                int end = k;
+                if (br.left() < 4) return JAAD_ERR_EOS;
+                const int c = (int)br.read(4);
+                if (c == 12) return JAAD_ERR_BITSTREAM;  // "invalid huffman codebook: 12"
+                int incr;
+                do {
+                    if (br.left() < bits) return JAAD_ERR_EOS;
+                    incr = (int)br.read(bits);
+                    end += incr;
+                } while (incr == esc);
+                if (end > max_sfb) return JAAD_ERR_BITSTREAM;  // "too many bands"
+                for (; k < end; k++, idx++) {
+                    cb[idx] = (uint8_t)c;
+                    sect_end[idx] = (uint8_t)end;
+                }
+            }
+        }
+    }
+    // ---- scalefactors (decodeScaleFactors, :172-220) -> table index - 100
+    uint8_t sf[128] = {0};
+    int has_pns = 0, has_is = 0;
+    {
+        int off0 = global_gain, off1 = global_gain - 90, off2 = 0;
+        bool noise_flag = true;
+        for (int g = 0, idx = 0; g < I.ngroups; g++) {
+            for (int s = 0; s < max_sfb;) {
+                const int end = sect_end[idx];
+                const int c = cb[idx];
+                for (; s < end; s++, idx++) {
+                    if (c == JAAD_ZERO_HCB) {
+                        sf[idx] = 0;
+                        continue;
+                    }
+                    int d;
+                    if (c == JAAD_NOISE_HCB && noise_flag) {
+                        if (br.left() < 9) return JAAD_ERR_EOS;
+                        d = (int)br.read(9) - 256;
+                        noise_flag = false;
+                    } else {
+                        const int r = B.sf.decode(br);
+                        if (r < 0) return r == -2 ? JAAD_ERR_EOS : JAAD_ERR_BITSTREAM;
+                        d = JAAD_HCB_SF[r][2] - 60;
+                    }
+                    if (c == JAAD_INTENSITY_HCB || c == JAAD_INTENSITY_HCB2) {
+                        off2 += d;
+                        const int t = off2 < -155 ? -155 : (off2 > 100 ? 100 : off2);
+                        sf[idx] = (uint8_t)(100 - t);  // SCALEFACTOR_TABLE[-t + 200]
+                        has_is = 1;
+                    } else if (c == JAAD_NOISE_HCB) {
+                        off1 += d;
+                        const int t = off1 < -100 ? -100 : (off1 > 155 ? 155 : off1);
+                        sf[idx] = (uint8_t)(t + 100);  // -SCALEFACTOR_TABLE[t + 200]
+                        has_pns = 1;
+                    } else {
+                        off0 += d;
+                        if (off0 > 255) return JAAD_ERR_BITSTREAM;  // "scalefactor out of range"
+                        if (off0 < 0) return JAAD_ERR_BITSTREAM;    // (table index < 100: outside the sf range)
+                        sf[idx] = (uint8_t)off0;                      // SCALEFACTOR_TABLE[off0 - 100 + 200]
+                    }
+                }
+            }
+        }
+    }
+    // ---- pulse data: parsed, never applied (:17, :148-170)
+    if (br.left() < 1) return JAAD_ERR_EOS;
+    if (br.read(1)) {
+        if (is_short) return JAAD_ERR_BITSTREAM;  // "pulse data not allowed for short frames"
+        if (br.left() < 8) return JAAD_ERR_EOS;
+        const int count = (int)br.read(2) + 1;
+        const int start = (int)br.read(6);
+        if (start >= nswb) return JAAD_ERR_BITSTREAM;
+        int offs = swb[start];
+        for (int i = 0; i < count; i++) {
+            if (br.left() < 9) return JAAD_ERR_EOS;
+            offs += (int)br.read(5);
+            br.skip(4);  // amplitude
+            if (i > 0 && offs > 1023) return JAAD_ERR_BITSTREAM;
+        }
+    }
+    // ---- TNS data (TNS.decode, A/tools/TNS.java:35-61)
+    jaad_tns tns;
+    std::memset(&tns, 0, sizeof tns);
+    if (br.left() < 1) return JAAD_ERR_EOS;
+    const bool tns_present = br.read(1) != 0;
+    if (tns_present) {
+        const int nwin = is_short ? 8 : 1;
+        const int b0 = is_short ? 1 : 2, b1 = is_short ? 4 : 6, b2 = is_short ? 3 : 5;
+        for (int w = 0; w < nwin; w++) {
+            if (br.left() < b0) return JAAD_ERR_EOS;
+            const int nf = (int)br.read(b0);
+            if (!nf) continue;
+            if (br.left() < 1) return JAAD_ERR_EOS;
+            const int res = (int)br.read(1);
+            for (int f = 0; f < nf; f++) {
+                if (br.left() < b1 + b2) return JAAD_ERR_EOS;
+                jaad_tns_filter& F = tns.filt[tns.n_filters < 8 ? tns.n_filters : 7];
+                if (tns.n_filters >= 8) return JAAD_ERR_BITSTREAM;
+                tns.n_filters++;
+                F.window = (uint8_t)w;
+                F.length = (uint8_t)br.read(b1);
+                const int order = (int)br.read(b2);
+                if (order > 20) return JAAD_ERR_BITSTREAM;  // "TNS filter out of range"
+                F.order = (uint8_t)order;
+                F.flags = (uint8_t)(res << 1);
+                if (order) {
+                    if (br.left() < 2) return JAAD_ERR_EOS;
+                    const int dir = (int)br.read(1), comp = (int)br.read(1);
+                    const int len = res + 3 - comp;
+                    F.flags = (uint8_t)(dir | (res << 1) | (comp << 2));
+                    for (int i = 0; i < order; i++) {
+                        if (br.left() < len) return JAAD_ERR_EOS;
+                        F.coef[i] = (uint8_t)br.read(len);
+                    }
+                }
+            }
+        }
+    }
+    // ---- gain control: AAC SSR only
+    if (br.left() < 1) return JAAD_ERR_EOS;
+    if (br.read(1)) return JAAD_ERR_UNSUPPORTED;
+
+    // ---- spectral data (decodeSpectralData, :222-275): quantised values, window-major
+    int16_t q[1024];
+    std::memset(q, 0, sizeof q);
+    uint64_t noise_steps = 0;
+    for (int g = 0, idx = 0, group_off = 0; g < I.ngroups; g++) {
+        const int gl = I.glen[g];
+        for (int s = 0; s < max_sfb; s++, idx++) {
+            const int c = cb[idx];
+            const int width = swb[s + 1] - swb[s];
+            if (c == JAAD_ZERO_HCB || c == JAAD_INTENSITY_HCB || c == JAAD_INTENSITY_HCB2) continue;
+            if (c == JAAD_NOISE_HCB) {
+                noise_steps += (uint64_t)gl * (uint64_t)width;
+                continue;
+            }
+            if (c > JAAD_ESCAPE_HCB) return JAAD_ERR_BITSTREAM;  // "unknown spectral codebook"
+            const Lut& L = B.spec[c - 1];
+            const int* rows = B.rows[c - 1];
+            const int stride = B.stride[c - 1];
+            const int num = c >= JAAD_FIRST_PAIR_HCB ? 2 : 4;
+            const bool unsigned_cb = c == 3 || c == 4 || c == 7 || c == 8 || c == 9 || c == 10 || c == 11;
+            for (int w = 0; w < gl; w++) {
+                const int off = group_off + w * 128 + swb[s];
+                for (int k = 0; k < width; k += num) {
+                    const int r = L.decode(br);
+                    if (r < 0) return r == -2 ? JAAD_ERR_EOS : JAAD_ERR_BITSTREAM;
+                    int v[4];
+                    for (int j = 0; j < num; j++) v[j] = rows[r * stride + 2 + j];
+                    if (unsigned_cb)  // Huffman.signValues (:30-37)
+                        for (int j = 0; j < num; j++)
+                            if (v[j] != 0) {
+                                if (br.left() < 1) return JAAD_ERR_EOS;
+                                if (br.read(1)) v[j] = -v[j];
+                            }
+                    if (c == JAAD_ESCAPE_HCB)  // Huffman.getEscape (:39-50)
+                        for (int j = 0; j < 2; j++) {
+                            if (v[j] != 16 && v[j] != -16) continue;
+                            int n = 4;
+                            for (;;) {
+                                if (br.left() < 1) return JAAD_ERR_EOS;
+                                if (!br.read(1)) break;
+                                if (++n > 12) return JAAD_ERR_BITSTREAM;  // |q| > 8191: beyond IQ_TABLE
+                            }
+                            if (br.left() < n) return JAAD_ERR_EOS;
+                            const int m = (int)br.read(n) | (1 << n);
+                            v[j] = v[j] < 0 ? -m : m;
+                        }
+                    for (int j = 0; j < num; j++) {
+                        // IQ_TABLE has 8191 entries (A/syntax/IQTable.java): |q| <= 8190
+                        if (v[j] > 8190 || v[j] < -8190) return JAAD_ERR_BITSTREAM;
+                        if (k + j < width) q[off + k + j] = (int16_t)v[j];
+                    }
+                }
+            }
+        }
+        group_off += gl << 7;
+    }
+    if (br.overrun()) return JAAD_ERR_EOS;
+
+    // ---- records
+    std::memcpy(o.q, q, sizeof q);
+    std::memcpy(o.sf, sf, 128);
+    std::memcpy(o.cb, cb, 128);
+    jaad_ics_info& ic = *o.ics;
+    std::memset(&ic, 0, sizeof ic);
+    ic.window_sequence = (uint8_t)I.seq;
+    ic.window_shape = (uint8_t)I.shape;
+    ic.window_shape_prev = (uint8_t)prev_shape;
+    ic.max_sfb = (uint8_t)max_sfb;
+    ic.grouping = (uint8_t)I.grouping;
+    ic.flags = (uint8_t)((has_pns ? JAAD_ICS_HAS_PNS : 0) | (has_is ? JAAD_ICS_HAS_IS : 0) |
+                         (tns_present ? JAAD_ICS_TNS : 0) | (common_window ? JAAD_ICS_COMMON_WINDOW : 0));
+    ic.pns_state = pns;
+    // the static LCG advances once per noise bin (ICStream.java:247)
+    for (uint64_t i = 0; i < noise_steps; i++) pns = 1664525u * pns + 1013904223u;
+    if (o.tns) *o.tns = tns;
+    return JAAD_OK;
+}
+
+}  // namespace parse
+}  // namespace jaad
+
+using namespace jaad::parse;
+
+struct jaad_parser {
+    Cfg C;
+    ParseState st;
+};
+
+namespace {
+
+int sf_counts(int sf_index, Cfg& C)
+{
+    if (sf_index < 0 || sf_index > 11) return JAAD_ERR_UNSUPPORTED;
+    C.sf_index = sf_index;
+    C.nswb_l = JAAD_SWB_LONG_WINDOW_COUNT[sf_index];
+    C.nswb_s = JAAD_SWB_SHORT_WINDOW_COUNT[sf_index];
+    return JAAD_OK;
+}
+
+// DSE (A/syntax/DSE.java:37-48)
+int skip_dse(BitReader& br)
+{
+    if (br.left() < 9) return JAAD_ERR_EOS;
+    const bool align = br.read(1) != 0;
+    int count = (int)br.read(8);
+    if (count == 255) {
+        if (br.left() < 8) return JAAD_ERR_EOS;
+        count += (int)br.read(8);
+    }
+    if (align) br.byte_align();
+    if (br.left() < 8 * count) return JAAD_ERR_EOS;
+    br.skip(8 * count);
+    return JAAD_OK;
+}
+
+// PCE (A/syntax/PCE.java:110-160): read and dropped
+int skip_pce(BitReader& br)
+{
+    if (br.left() < 2 + 4 + 4 + 4 + 4 + 2 + 3 + 4) return JAAD_ERR_EOS;
+    br.skip(2);
+    if (br.read(4) == 15) br.skip(24);  // SampleFrequency.decode: explicit frequency
+    const int nfront = (int)br.read(4), nside = (int)br.read(4), nback = (int)br.read(4);
+    const int nlfe = (int)br.read(2), nassoc = (int)br.read(3), ncc = (int)br.read(4);
+    if (br.read(1)) br.skip(4);
+    if (br.read(1)) br.skip(4);
+    if (br.read(1)) br.skip(3);
+    br.skip(5 * (nfront + nside + nback) + 4 * nlfe + 4 * nassoc + 5 * ncc);
+    br.byte_align();
+    if (br.left() < 8) return JAAD_ERR_EOS;
+    const int ncomment = (int)br.read(8);
+    br.skip(8 * ncomment);
+    return br.overrun() ? JAAD_ERR_EOS : JAAD_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int jaad_asc_parse(const uint8_t* asc, size_t bytes, jaad_stream_cfg* cfg)
+{
+    if (!asc || !cfg) return JAAD_ERR_INVALID_ARG;
+    BitReader br(asc, bytes);
+    auto profile = [&]() {  // DecoderConfig.readProfile
+        int i = (int)br.read(5);
+        if (i == 31) i = 32 + (int)br.read(6);
+        return i;
+    };
+    auto rate = [&]() {  // SampleRate.decode -> nominal index (SampleFrequency.nominalFrequency)
+        int idx = (int)br.read(4);
+        if (idx != 15) return idx;
+        const int freq = (int)br.read(24);
+        static const int F[12] = {96000, 88200, 64000, 48000, 44100, 32000, 24000, 22050, 16000, 12000, 11025, 8000};
+        int best = 0;
+        float dev = 1e30f;
+        for (int i = 0; i < 12; i++) {
+            const float d = (float)(freq > F[i] ? freq - F[i] : F[i] - freq) / (float)F[i];
+            if (d == 0.0f) return i;
+            if (d < dev) {
+                best = i;
+                dev = d;
+            }
+            if (F[i] < freq) break;
+        }
+        return best;
+    };
+    std::memset(cfg, 0, sizeof *cfg);
+    cfg->abi_version = JAAD_ABI_VERSION;
+    cfg->tns_mode = JAAD_TNS_COMPAT;
+    int aot = profile();
+    int sfi = rate();
+    const int chc = (int)br.read(4);
+    if (aot == 5 || aot == 29) {  // AAC_SBR / AAC_PS: extension rate, core profile; no GASpecificConfig
+        cfg->sbr = 1;
+        cfg->ps = aot == 29;
+        cfg->ext_sf_index = (uint8_t)rate();
+        aot = profile();
+    } else if (aot == 2) {
+        if (br.read(1)) return br.overrun() ? JAAD_ERR_EOS : JAAD_ERR_UNSUPPORTED;  // frameLengthFlag: 960
+        if (br.read(1)) br.skip(14);                  // dependsOnCoreCoder -> coreCoderDelay
+        if (br.read(1)) br.skip(1);                   // extensionFlag -> extensionFlag3
+        if (br.overrun()) return JAAD_ERR_EOS;
+        if (chc == 0) return JAAD_ERR_UNSUPPORTED;    // PCE channel layouts: not a 1/2-channel config
+        // sync extension (readSyncExtension, :255-285) is read only when sbrEnabled: the
+        // implicit/backward-compatible signalling keeps the core rate
+    }
+    if (br.overrun()) return JAAD_ERR_EOS;
+    if (aot != 2) return JAAD_ERR_UNSUPPORTED;
+    if (sfi > 11 || (cfg->sbr && cfg->ext_sf_index > 11)) return JAAD_ERR_UNSUPPORTED;
+    if (chc != 1 && chc != 2) return JAAD_ERR_UNSUPPORTED;
+    cfg->profile = 2;
+    cfg->sf_index = (uint8_t)sfi;
+    cfg->channel_config = (uint8_t)chc;
+    return JAAD_OK;
+}
+
+int jaad_adts_find(const uint8_t* buf, size_t bytes, size_t* offset, jaad_adts_header* h)
+{
+    if (!buf || !offset || !h) return JAAD_ERR_INVALID_ARG;
+    // ADTSDemultiplexer.findNextFrame: scan at most MAXIMUM_FRAME_SIZE bytes for 0xFF followed
+    // by a byte with (b & 0xF6) == 0xF0
+    const size_t lim = bytes < 6144 ? bytes : 6144;
+    for (size_t i = 0; i + 1 < lim || (i + 1 < bytes && i < lim); i++) {
+        if (buf[i] != 0xFF || (buf[i + 1] & 0xF6) != 0xF0) continue;
+        if (i + 7 > bytes) return JAAD_ERR_EOS;
+        const uint8_t* b = buf + i + 1;  // ADTSFrame.readHeader starts after the 0xFF
+        std::memset(h, 0, sizeof *h);
+        h->protection_absent = b[0] & 1;
+        h->profile = (uint8_t)(((b[1] & 0xC0) >> 6) + 1);
+        h->sf_index = (uint8_t)((b[1] & 0x3C) >> 2);
+        h->channel_config = (uint8_t)(((b[1] & 0x01) << 2) | ((b[2] & 0xC0) >> 6));
+        h->frame_length = (uint32_t)(((b[2] & 0x03) << 11) | (b[3] << 3) | ((b[4] & 0xE0) >> 5));
+        h->n_raw_blocks = (uint8_t)((b[5] & 0x03) + 1);
+        h->header_bytes = h->protection_absent ? 7 : 9;
+        *offset = i;
+        return JAAD_OK;
+    }
+    return JAAD_ERR_EOS;
+}
+
+int jaad_adts_cfg(const jaad_adts_header* h, jaad_stream_cfg* cfg)
+{
+    if (!h || !cfg) return JAAD_ERR_INVALID_ARG;
+    if (h->profile != 2 || h->sf_index > 11 || (h->channel_config != 1 && h->channel_config != 2))
+        return JAAD_ERR_UNSUPPORTED;
+    std::memset(cfg, 0, sizeof *cfg);
+    cfg->abi_version = JAAD_ABI_VERSION;
+    cfg->profile = 2;
+    cfg->sf_index = h->sf_index;
+    cfg->channel_config = h->channel_config;
+    cfg->tns_mode = JAAD_TNS_COMPAT;
+    return JAAD_OK;
+}
+
+int jaad_parser_create(const jaad_stream_cfg* cfg, jaad_parser** out)
+{
+    if (!cfg || !out) return JAAD_ERR_INVALID_ARG;
+    *out = nullptr;
+    if (cfg->abi_version != JAAD_ABI_VERSION) return JAAD_ERR_ABI;
+    if (cfg->profile != 2 || (cfg->channel_config != 1 && cfg->channel_config != 2)) return JAAD_ERR_UNSUPPORTED;
+    if (cfg->ps && (!cfg->sbr || cfg->channel_config != 1)) return JAAD_ERR_UNSUPPORTED;
+    jaad_parser* p = new (std::nothrow) jaad_parser;
+    if (!p) return JAAD_ERR_NOMEM;
+    p->C.cfg = *cfg;
+    p->C.nch = cfg->channel_config == 2 ? 2 : 1;
+    const int st = sf_counts(cfg->sf_index, p->C);
+    if (st) {
+        delete p;
+        return st;
+    }
+    books();
+    *out = p;
+    return JAAD_OK;
+}
+
+void jaad_parser_destroy(jaad_parser* p) { delete p; }
+
+uint32_t jaad_parser_pns_state(const jaad_parser* p) { return p ? p->st.pns : 0u; }
+void jaad_parser_set_pns_state(jaad_parser* p, uint32_t s)
+{
+    if (p) p->st.pns = s;
+}
+
+int jaad_parse_frame(jaad_parser* p, const uint8_t* data, size_t bytes, jaad_frame_out* out)
+{
+    if (!p || !out || (!data && bytes) || !out->q || !out->sf || !out->cb || !out->ics) return JAAD_ERR_INVALID_ARG;
+    const Cfg& C = p->C;
+    if (C.nch == 2 && !out->ms_used) return JAAD_ERR_INVALID_ARG;
+    if (C.cfg.sbr && !out->sbr) return JAAD_ERR_INVALID_ARG;
+    BitReader br(data, bytes);
+    ParseState ns = p->st;  // committed only when the whole frame parsed
+    bool have_channels = false;
+    int sbr_seen = 0;
+    if (C.cfg.sbr) std::memset(out->sbr, 0, sizeof *out->sbr);
+    for (;;) {
+        if (br.left() < 3) return JAAD_ERR_EOS;
+        const int id = (int)br.read(3);
+        if (id == 7) break;  // END
+        if (id == 6) {       // FIL (SyntacticElements.decodeFIL, :169-203)
+            if (br.left() < 4) return JAAD_ERR_EOS;
+            int count = (int)br.read(4);
+            if (count == 15) {
+                if (br.left() < 8) return JAAD_ERR_EOS;
+                count += (int)br.read(8) - 1;
+            }
+            if (!count) continue;
+            if (br.left() < 8 * count) return JAAD_ERR_EOS;
+            BitReader sub = br.sub(8 * count);
+            br.skip(8 * count);
+            const int type = (int)sub.read(4);
+            if ((type == 13 || type == 14) && have_channels && C.cfg.sbr) {  // EXT_SBR_DATA(_CRC)
+                const int st = parse_sbr(sub, C, type == 14, ns, *out->sbr);
+                if (st) return st;
+                sbr_seen = 1;
+            }
+            continue;
+        }
+        if (br.left() < 4) return JAAD_ERR_EOS;
+        br.skip(4);  // element_instance_tag
+        if (id == 4) {  // DSE
+            const int st = skip_dse(br);
+            if (st) return st;
+            continue;
+        }
+        if (id == 5) {  // PCE
+            const int st = skip_pce(br);
+            if (st) return st;
+            continue;
+        }
+        if (id == 2 || id == 3) return JAAD_ERR_UNSUPPORTED;  // CCE, LFE: multichannel layouts
+        // SCE (0) / CPE (1): exactly the one channel element of a mono / stereo configuration
+        if (have_channels || (id == 1) != (C.nch == 2)) return JAAD_ERR_UNSUPPORTED;
+        have_channels = true;
+        if (id == 0) {
+            IcsInfo I;
+            ChOut o{out->q, out->sf, out->cb, out->ics, out->tns};
+            const int st = read_ics(br, C, false, I, ns.shape[0], ns.pns, o);
+            if (st) return st;
+            ns.shape[0] = I.shape;
+        } else {
+            // CPE.decode (A/syntax/CPE.java:85-123)
+            if (br.left() < 1) return JAAD_ERR_EOS;
+            const bool common = br.read(1) != 0;
+            IcsInfo IL, IR;
+            uint64_t ms[2] = {0, 0};
+            bool ms_present = false;
+            if (common) {
+                int st = read_ics_info(br, C, IL);
+                if (st) return st;
+                IR = IL;  // ICSInfo.setCommonData
+                if (br.left() < 2) return JAAD_ERR_EOS;
+                const int mask = (int)br.read(2);
+                const int nb = IL.ngroups * IL.max_sfb;
+                if (mask == 1) {
+                    if (br.left() < nb) return JAAD_ERR_EOS;
+                    for (int i = 0; i < nb; i++)
+                        if (br.read(1)) ms[i >> 6] |= 1ull << (i & 63);
+                } else if (mask == 2) {
+                    for (int i = 0; i < nb; i++) ms[i >> 6] |= 1ull << (i & 63);
+                } else if (mask == 3) {
+                    return JAAD_ERR_BITSTREAM;  // "reserved MS mask type used"
+                }
+                ms_present = mask != 0;
+            }
+            ChOut oL{out->q, out->sf, out->cb, out->ics, out->tns};
+            ChOut oR{out->q + 1024, out->sf + 128, out->cb + 128, out->ics + 1, out->tns ? out->tns + 1 : nullptr};
+            int st = read_ics(br, C, common, IL, ns.shape[0], ns.pns, oL);
+            if (st) return st;
+            st = read_ics(br, C, common, IR, ns.shape[1], ns.pns, oR);
+            if (st) return st;
+            ns.shape[0] = IL.shape;
+            ns.shape[1] = IR.shape;
+            if (ms_present) out->ics[0].flags |= JAAD_ICS_MS_PRESENT;
+            out->ms_used[0] = ms[0];
+            out->ms_used[1] = ms[1];
+        }
+    }
+    if (!have_channels) return JAAD_ERR_BITSTREAM;  // a frame without audio: nothing to decode
+    if (C.cfg.sbr && !sbr_seen) {
+        const int st = sbr_missing(C, ns, *out->sbr);
+        if (st) return st;
+    }
+    p->st = ns;
+    return JAAD_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,110 @@
+// Internal pieces shared by the host bitstream front end (jaad_parse.cpp, jaad_parse_sbr.cpp).
+#pragma once
+#include <stdint.h>
+
+#include <cstddef>
+
+#include "../../include/jaad_gpu.h"
+
+namespace jaad {
+namespace parse {
+
+// MSB-first bit reader over [data, data + bytes) (A/syntax/ByteArrayBitStream.java).  Reads
+// past the end return zero bits and set overrun(); callers check left() first where the
+// reference would throw EOSException.  sub() is readSubStream: a window of the next n bits
+// sharing the parent's absolute position (byte alignment stays absolute, as in the reference).
+class BitReader {
+public:
+    BitReader(const uint8_t* d, size_t bytes) : d_(d), end_(bytes * 8), pos_(0) {}
+    int64_t left() const { return (int64_t)end_ - (int64_t)pos_; }
+    bool overrun() const { return pos_ > end_; }
+    size_t pos() const { return pos_; }
+    uint32_t peek(int n) const
+    {
+        uint64_t v = 0;
+        size_t p = pos_;
+        for (int i = 0; i < n; i++, p++) v = (v << 1) | (p < end_ ? ((d_[p >> 3] >> (7 - (p & 7))) & 1u) : 0u);
+        return (uint32_t)v;
+    }
+    uint32_t read(int n)
+    {
+        if (n <= 0) return 0;
+        uint32_t v;
+        if (pos_ + (size_t)n <= end_ && n <= 25) {  // fast path: one unaligned 32-bit window
+            const size_t byte = pos_ >> 3;
+            const int sh = (int)(pos_ & 7);
+            uint32_t w = 0;
+            const size_t avail = (end_ + 7) / 8 - byte;
+            for (size_t i = 0; i < 4; i++) w = (w << 8) | (i < avail ? d_[byte + i] : 0u);
+            v = (w << sh) >> (32 - n);
+        } else {
+            v = peek(n);
+        }
+        pos_ += (size_t)n;
+        return v;
+    }
+    void skip(int64_t n) { pos_ += (size_t)(n > 0 ? n : 0); }
+    void byte_align() { pos_ = (pos_ + 7) & ~(size_t)7; }
+    BitReader sub(int64_t n) const
+    {
+        BitReader r = *this;
+        r.end_ = pos_ + (size_t)n < end_ ? pos_ + (size_t)n : end_;
+        return r;
+    }
+
+private:
+    const uint8_t* d_;
+    size_t end_, pos_;
+};
+
+struct Cfg {
+    jaad_stream_cfg cfg;
+    int nch = 1;            // channels per ch-frame record (1 SCE, 2 CPE)
+    int sf_index = 0, nswb_l = 0, nswb_s = 0;
+};
+
+// SBR / PS bitstream state that persists between frames (jaad_parse_sbr.cpp)
+struct SbrParseState {
+    bool have_header = false;
+    jaad_sbr_header hdr{};
+    int kx = 0, M = 0, N_high = 0, N_low = 0, N_Q = 0;  // derived tables of the current header
+    int n[2] = {0, 0};                                  // N_low, N_high
+    bool valid = false;
+    struct Ch {
+        int L_E_prev = 0, L_Q_prev = 0, f_prev_last = 0;
+        int E_prev[64] = {0}, Q_prev[8] = {0};
+        int t_E_prev_last = 0;
+        int frame_class_prev = 0, bs_pointer_prev = 0;
+        int bs_add_harmonic_prev[64] = {0};
+        int add_harmonic_flag_prev = 0;
+        int invf_prev[5] = {0};
+    } ch[2];
+    struct Ps {
+        bool header_seen = false;
+        int iid_mode = 0, icc_mode = 0, ext = 0, ipd_mode_prev = 0;
+        int iid_prev[34] = {0}, icc_prev[34] = {0}, ipd_prev[17] = {0}, opd_prev[17] = {0};
+        bool enable_iid = false, enable_icc = false, enable_ipdopd = false;
+    } ps;
+};
+
+struct ParseState {
+    uint32_t pns = 0x1F2E3D4Cu;  // static ICStream.randomState (A/syntax/ICStream.java:26)
+    int shape[2] = {0, 0};       // ICSInfo.windowShape[CURRENT] of the previous frame
+    SbrParseState sbr;
+};
+
+struct ChOut {
+    int16_t* q;
+    uint8_t* sf;
+    uint8_t* cb;
+    jaad_ics_info* ics;
+    jaad_tns* tns;
+};
+
+// one sbr_extension_data payload (after the 4-bit extension type) into rec
+int parse_sbr(BitReader& br, const Cfg& C, bool crc, ParseState& st, jaad_sbr_frame& rec);
+// a frame of an SBR configuration that carried no SBR payload
+int sbr_missing(const Cfg& C, ParseState& st, jaad_sbr_frame& rec);
+
+}  // namespace parse
+}  // namespace jaad

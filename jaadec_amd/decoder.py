@@ -2,14 +2,17 @@
 
 Names and behaviour follow the Java classes a caller of the reference uses:
 
-* ``DecoderConfig.decode(asc)``   -- A/DecoderConfig.java:175-254 (AudioSpecificConfig, LC only)
+* ``DecoderConfig.decode(asc)``   -- A/DecoderConfig.java:175-254 (AudioSpecificConfig)
 * ``Decoder.create(asc|config)``  -- A/Decoder.java:36-54
 * ``Decoder.decodeFrame(frame, buffer)`` -- A/Decoder.java:89-101 (one parsed frame)
 * ``Decoder.decodeFrames(batch, buffers)`` -- the batched entry the drop-in adds
 * ``SampleBuffer`` -- S/SampleBuffer.java (big-endian by default, setBigEndian swaps in place)
 
-A "parsed frame" is what the reference's ``syntacticElements.decode(in)`` leaves behind, in the
-jaad_gpu.h layout: this module does not parse bitstreams.
+* ``ADTSDemultiplexer``           -- S/adts/ADTSDemultiplexer.java (readNextFrame)
+
+A frame is either a raw_data_block (bytes: parsed by the native host front end,
+include/jaad_parse.h, as ``syntacticElements.decode(in)`` parses it) or an already parsed
+frame in the jaad_gpu.h layout (a ``native.Batch``, what a JVM-side emitter hands over).
 Errors surface as ``AACException`` (the JNI glue maps every nonzero jaad_status the same way).
 """
 from __future__ import annotations
@@ -27,59 +30,48 @@ class AACException(RuntimeError):
 SAMPLE_FREQUENCIES = [96000, 88200, 64000, 48000, 44100, 32000, 24000, 22050, 16000, 12000, 11025, 8000]
 
 
-class _Bits:
-    def __init__(self, data: bytes):
-        self.data, self.pos = data, 0
-
-    def read(self, n: int) -> int:
-        v = 0
-        for _ in range(n):
-            if self.pos >= 8 * len(self.data):
-                raise AACException("unexpected end of AudioSpecificConfig")
-            v = (v << 1) | ((self.data[self.pos >> 3] >> (7 - (self.pos & 7))) & 1)
-            self.pos += 1
-        return v
-
-
 class DecoderConfig:
-    """The subset of A/DecoderConfig.java the DSP path needs."""
+    """DecoderConfig (A/DecoderConfig.java) for the DSP path: AAC LC core, optionally with
+    explicit SBR (AOT 5) or SBR + PS (AOT 29)."""
 
-    def __init__(self, profile: int = 2, sf_index: int = 3, channel_config: int = 2, tns_mode: int = N.TNS_COMPAT):
+    def __init__(self, profile: int = 2, sf_index: int = 3, channel_config: int = 2, tns_mode: int = N.TNS_COMPAT,
+                 sbr: bool = False, ps: bool = False, ext_sf_index: int | None = None):
         self.profile, self.sf_index, self.channel_config, self.tns_mode = profile, sf_index, channel_config, tns_mode
+        self.sbr, self.ps = bool(sbr), bool(ps)
+        self.ext_sf_index = (sf_index - 3) if ext_sf_index is None and sbr else (ext_sf_index or 0)
 
     @classmethod
     def decode(cls, asc: bytes) -> "DecoderConfig":
-        """AudioSpecificConfig (A/DecoderConfig.java:175-254): AOT, sampling frequency, channels."""
-        b = _Bits(bytes(asc))
-        aot = b.read(5)
-        if aot == 31:
-            aot = 32 + b.read(6)
-        sfi = b.read(4)
-        if sfi == 15:  # explicit frequency
-            freq = b.read(24)
-            sfi = min(range(12), key=lambda i: abs(SAMPLE_FREQUENCIES[i] - freq))
-        ch = b.read(4)
-        if aot != 2:
-            raise AACException(f"profile not supported: {aot}")
-        frame_length_flag = b.read(1)
-        if frame_length_flag:
-            raise AACException("config uses 960-sample frames, not yet supported")  # DecoderConfig.java:206-207
-        if b.read(1):  # dependsOnCoreCoder
-            b.read(14)
-        b.read(1)  # extensionFlag
-        return cls(aot, sfi, ch)
+        """AudioSpecificConfig (A/DecoderConfig.java:175-254) through the native front end
+        (include/jaad_parse.h: jaad_asc_parse); errors as the reference words them."""
+        asc = bytes(asc)
+        aot = asc[0] >> 3 if asc else -1
+        try:
+            c = N.asc_parse(asc)
+        except N.JaadError as e:
+            if e.status == N.ERR_EOS or not asc:
+                raise AACException("unexpected end of AudioSpecificConfig") from e
+            if aot not in (2, 5, 29):
+                raise AACException(f"profile not supported: {aot}") from e
+            if aot == 2 and len(asc) > 1 and (asc[1] >> 2) & 1:
+                raise AACException("config uses 960-sample frames, not yet supported") from e  # :206-207
+            raise AACException(f"unsupported configuration ({e})") from e
+        return cls(c.profile, c.sf_index, c.channel_config, N.TNS_COMPAT, bool(c.sbr), bool(c.ps), c.ext_sf_index)
 
     def getChannelCount(self) -> int:  # noqa: N802  (Java name)
         return 2  # mono -> stereo while sbrEnabled (A/DecoderConfig.java:108-115)
 
     def getSampleLength(self) -> int:  # noqa: N802
-        return 1024
+        return 2048 if self.sbr else 1024  # A/DecoderConfig.java:83-86 (upsampled SBR)
 
     def getSampleFrequency(self) -> int:  # noqa: N802
         return SAMPLE_FREQUENCIES[self.sf_index]
 
+    def getOutputFrequency(self) -> int:  # noqa: N802
+        return SAMPLE_FREQUENCIES[self.ext_sf_index] if self.sbr else self.getSampleFrequency()
+
     def cfg(self) -> N.StreamCfg:
-        return N.make_cfg(self.sf_index, self.channel_config, self.tns_mode)
+        return N.make_cfg(self.sf_index, self.channel_config, self.tns_mode, sbr=self.sbr, ps=self.ps)
 
 
 class SampleBuffer:
@@ -149,6 +141,7 @@ class Decoder:
         self._own = context is None
         self.slot = slot
         self.frames = 0
+        self._parser = None  # host bitstream front end, created on the first raw frame
 
     @classmethod
     def create(cls, data) -> "Decoder":
@@ -164,29 +157,76 @@ class Decoder:
     def _flags(self, buf: SampleBuffer) -> int:
         return N.PCM_BIG_ENDIAN if buf.big_endian else N.PCM_LITTLE_ENDIAN
 
-    def decodeFrames(self, batch: N.Batch, buffers: list[SampleBuffer]) -> None:  # noqa: N802
-        """Decode consecutive parsed frames of this stream; buffer i receives frame i's PCM."""
+    def _parse(self, frames: list) -> N.Batch:
+        if self._parser is None:
+            self._parser = N.Parser(self.config.cfg())
+        try:
+            return self._parser.parse(frames, self.slot)
+        except N.JaadError as e:
+            raise AACException(str(e)) from e
+
+    def decodeFrames(self, batch, buffers: list[SampleBuffer]) -> None:  # noqa: N802
+        """Decode consecutive frames of this stream -- a list of raw_data_blocks or a parsed
+        ``native.Batch`` -- buffer i receives frame i's PCM."""
+        if isinstance(batch, (list, tuple)):
+            batch = self._parse(list(batch))
         if len(buffers) != batch.n_frames:
             raise AACException("one SampleBuffer per frame expected")
         b = N.Batch(batch.q, batch.sf, batch.cb, batch.ics, batch.ms_used, batch.tns,
-                    np.array([self.slot], np.uint32), np.array([0, batch.n_frames], np.uint32), batch.nch)
+                    np.array([self.slot], np.uint32), np.array([0, batch.n_frames], np.uint32), batch.nch,
+                    batch.sbr)
         flags = self._flags(buffers[0]) if buffers else 0
         try:
             pcm = self._ctx.decode(b, flags)
         except N.JaadError as e:
             raise AACException(str(e)) from e
-        rate = self.config.getSampleFrequency()
+        rate = self.config.getOutputFrequency()
         for i, buf in enumerate(buffers):
             want = buf.big_endian
-            buf._set(pcm[i].tobytes(), rate)
+            buf._set(pcm[i].tobytes(), rate, self.config.getSampleLength())
             buf.big_endian = flags == N.PCM_BIG_ENDIAN
             buf.setBigEndian(want)  # no-op unless this buffer asked for the other byte order
         self.frames += batch.n_frames
 
-    def decodeFrame(self, frame: N.Batch, buffer: SampleBuffer) -> None:  # noqa: N802
-        """A/Decoder.java:89-101 for one parsed frame."""
-        self.decodeFrames(frame, [buffer])
+    def decodeFrame(self, frame, buffer: SampleBuffer) -> None:  # noqa: N802
+        """A/Decoder.java:89-101 for one frame (raw_data_block bytes or a parsed Batch)."""
+        self.decodeFrames([frame] if isinstance(frame, (bytes, bytearray, memoryview)) else frame, [buffer])
 
     def close(self) -> None:
         if self._own:
             self._ctx.close()
+        if self._parser is not None:
+            self._parser.close()
+
+
+class ADTSDemultiplexer:
+    """S/adts/ADTSDemultiplexer.java over a byte string: readNextFrame() returns the next
+    raw_data_block (EOFError at the end), the stream parameters come from the ADTS header."""
+
+    def __init__(self, data: bytes):
+        self._frames = N.adts_frames(bytes(data))
+        try:
+            self._first = next(self._frames)
+        except StopIteration:
+            raise OSError("no ADTS header found") from None  # ADTSDemultiplexer.java:21-22
+        self._next = self._first
+
+    def readNextFrame(self) -> bytes:  # noqa: N802
+        if self._next is None:
+            try:
+                self._next = next(self._frames)
+            except StopIteration:
+                raise EOFError() from None
+        h, payload = self._next
+        self._next = None
+        return payload
+
+    def getSampleFrequency(self) -> int:  # noqa: N802
+        return SAMPLE_FREQUENCIES[self._first[0].sf_index]
+
+    def getChannelCount(self) -> int:  # noqa: N802
+        return self._first[0].channel_config
+
+    def getDecoderInfo(self) -> DecoderConfig:  # noqa: N802
+        c = N.adts_cfg(self._first[0])
+        return DecoderConfig(c.profile, c.sf_index, c.channel_config)

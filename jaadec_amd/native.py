@@ -20,7 +20,7 @@ SYNTH_PATH = PKG / "libjaadsynth.so"
 ABI_VERSION = 3
 
 # status codes (jaad_status)
-OK, ERR_INVALID_ARG, ERR_NO_DEVICE, ERR_HIP, ERR_UNSUPPORTED, ERR_BITSTREAM, ERR_NOMEM, ERR_ABI = 0, -1, -2, -3, -4, -5, -6, -7
+OK, ERR_INVALID_ARG, ERR_NO_DEVICE, ERR_HIP, ERR_UNSUPPORTED, ERR_BITSTREAM, ERR_NOMEM, ERR_ABI, ERR_EOS = 0, -1, -2, -3, -4, -5, -6, -7, -8
 
 ONLY_LONG_SEQUENCE, LONG_START_SEQUENCE, EIGHT_SHORT_SEQUENCE, LONG_STOP_SEQUENCE = 0, 1, 2, 3
 ZERO_HCB, NOISE_HCB, INTENSITY_HCB2, INTENSITY_HCB = 0, 13, 14, 15
@@ -78,6 +78,20 @@ class SynthParams(C.Structure):
 EXPORTS = ["jaad_cfg_sample_length", "jaad_cfg_channel_count", "jaad_frame_pcm_bytes", "jaad_ctx_create",
            "jaad_ctx_destroy", "jaad_ctx_core_channels", "jaad_decode_batch", "jaad_decode_batch_device", "jaad_wait", "jaad_state_bytes",
            "jaad_state_export", "jaad_state_import", "jaad_state_reset", "jaad_strerror", "jaad_last_error"]
+# every symbol include/jaad_parse.h declares
+PARSE_EXPORTS = ["jaad_asc_parse", "jaad_adts_find", "jaad_adts_cfg", "jaad_parser_create", "jaad_parser_destroy",
+                 "jaad_parser_pns_state", "jaad_parser_set_pns_state", "jaad_parse_frame"]
+
+
+class AdtsHeader(C.Structure):
+    _fields_ = [("profile", C.c_uint8), ("sf_index", C.c_uint8), ("channel_config", C.c_uint8),
+                ("protection_absent", C.c_uint8), ("n_raw_blocks", C.c_uint8), ("reserved", C.c_uint8 * 3),
+                ("frame_length", C.c_uint32), ("header_bytes", C.c_uint32)]
+
+
+class FrameOut(C.Structure):
+    _fields_ = [("q", C.c_void_p), ("sf", C.c_void_p), ("cb", C.c_void_p), ("ics", C.c_void_p),
+                ("ms_used", C.c_void_p), ("tns", C.c_void_p), ("sbr", C.c_void_p)]
 
 
 class JaadError(RuntimeError):
@@ -120,6 +134,17 @@ def lib() -> C.CDLL:
         L.jaad_strerror.restype = C.c_char_p
         L.jaad_last_error.argtypes = [C.c_void_p]
         L.jaad_last_error.restype = C.c_char_p
+        L.jaad_asc_parse.argtypes = [C.c_char_p, C.c_size_t, C.POINTER(StreamCfg)]
+        L.jaad_adts_find.argtypes = [C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t), C.POINTER(AdtsHeader)]
+        L.jaad_adts_cfg.argtypes = [C.POINTER(AdtsHeader), C.POINTER(StreamCfg)]
+        L.jaad_parser_create.argtypes = [C.POINTER(StreamCfg), C.POINTER(C.c_void_p)]
+        L.jaad_parser_destroy.argtypes = [C.c_void_p]
+        L.jaad_parser_destroy.restype = None
+        L.jaad_parser_pns_state.argtypes = [C.c_void_p]
+        L.jaad_parser_pns_state.restype = C.c_uint32
+        L.jaad_parser_set_pns_state.argtypes = [C.c_void_p, C.c_uint32]
+        L.jaad_parser_set_pns_state.restype = None
+        L.jaad_parse_frame.argtypes = [C.c_void_p, C.c_char_p, C.c_size_t, C.POINTER(FrameOut)]
         _lib = L
     return _lib
 
@@ -328,3 +353,93 @@ class Context:
 
     def state_reset(self, slot: int) -> None:
         self._check(lib().jaad_state_reset(self.h, slot), "jaad_state_reset")
+
+
+# ---------------------------------------------------------------------------------------------
+# host bitstream front end (include/jaad_parse.h)
+# ---------------------------------------------------------------------------------------------
+def asc_parse(asc: bytes) -> StreamCfg:
+    """AudioSpecificConfig -> StreamCfg (DecoderConfig.decode, A/DecoderConfig.java:175-291)."""
+    cfg = StreamCfg()
+    rc = lib().jaad_asc_parse(bytes(asc), len(asc), C.byref(cfg))
+    if rc:
+        raise JaadError(rc, "jaad_asc_parse")
+    return cfg
+
+
+def adts_frames(data: bytes):
+    """Split an ADTS byte stream (S/adts/ADTSDemultiplexer.java): yields (header, raw_data_block)."""
+    pos = 0
+    h = AdtsHeader()
+    off = C.c_size_t()
+    while pos < len(data):
+        rc = lib().jaad_adts_find(data[pos:], len(data) - pos, C.byref(off), C.byref(h))
+        if rc == ERR_EOS:
+            return
+        if rc:
+            raise JaadError(rc, "jaad_adts_find")
+        start = pos + off.value + h.header_bytes
+        end = pos + off.value + h.frame_length
+        if h.frame_length < h.header_bytes or end > len(data):
+            return  # truncated last frame (EOF inside the payload)
+        yield AdtsHeader.from_buffer_copy(h), data[start:end]
+        pos = end
+
+
+def adts_cfg(h: AdtsHeader) -> StreamCfg:
+    cfg = StreamCfg()
+    rc = lib().jaad_adts_cfg(C.byref(h), C.byref(cfg))
+    if rc:
+        raise JaadError(rc, "jaad_adts_cfg")
+    return cfg
+
+
+class Parser:
+    """One stream's host parser state (window shapes, static PNS LCG, SBR/PS history)."""
+
+    def __init__(self, cfg: StreamCfg):
+        self.cfg = cfg
+        self.nch = 2 if cfg.channel_config == 2 else 1
+        h = C.c_void_p()
+        rc = lib().jaad_parser_create(C.byref(cfg), C.byref(h))
+        if rc:
+            raise JaadError(rc, "jaad_parser_create")
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().jaad_parser_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    @property
+    def pns_state(self) -> int:
+        return int(lib().jaad_parser_pns_state(self.h))
+
+    @pns_state.setter
+    def pns_state(self, v: int) -> None:
+        lib().jaad_parser_set_pns_state(self.h, v)
+
+    def parse(self, frames: list, slot: int = 0) -> Batch:
+        """raw_data_blocks (bytes) of this stream -> one-run Batch in the jaad_gpu.h layout."""
+        nf, nch = len(frames), self.nch
+        q = np.zeros((nf * nch, 1024), np.int16)
+        sf = np.zeros((nf * nch, 128), np.uint8)
+        cb = np.zeros((nf * nch, 128), np.uint8)
+        ics = np.zeros(nf * nch, ICS_DTYPE)
+        ms = np.zeros((nf, 2), np.uint64) if nch == 2 else None
+        tns = np.zeros(nf * nch, TNS_DTYPE)
+        sbr = np.zeros(nf, SBR_FRAME_DTYPE) if self.cfg.sbr else None
+        for i, fr in enumerate(frames):
+            o = FrameOut(q[i * nch:].ctypes.data, sf[i * nch:].ctypes.data, cb[i * nch:].ctypes.data,
+                         ics[i * nch:].ctypes.data, ms[i:].ctypes.data if ms is not None else None,
+                         tns[i * nch:].ctypes.data, sbr[i:].ctypes.data if sbr is not None else None)
+            rc = lib().jaad_parse_frame(self.h, bytes(fr), len(fr), C.byref(o))
+            if rc:
+                raise JaadError(rc, f"jaad_parse_frame (frame {i})")
+        if not (ics["flags"] & ICS_TNS).any():
+            tns = None
+        b = Batch(q, sf, cb, ics, ms, tns, np.array([slot], np.uint32), np.array([0, nf], np.uint32), nch)
+        b.sbr = sbr
+        return b

@@ -45,6 +45,9 @@ def lib() -> C.CDLL:
         L.orc_qmf_synthesis_frame.argtypes = [C.c_void_p] * 4
         L.orc_qmf_synthesis_frame.restype = None
         L.orc_sbr_table_info.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.jaad_write_frame.argtypes = [C.c_int, C.c_int] + [C.c_void_p] * 6 + [C.c_int, C.c_void_p, C.c_size_t]
+        L.jaad_write_frame.restype = C.c_long
+        L.jaad_write_adts_header.argtypes = [C.c_int, C.c_int, C.c_size_t, C.c_void_p]
         _lib = L
     return _lib
 
@@ -125,6 +128,40 @@ def sbr_table_info(hdr, out_sf_index: int):
         raise RuntimeError(f"orc_sbr_table_info failed: {rc}")
     keys = ["k0", "k2", "kx", "M", "N_master", "N_high", "N_low", "N_Q", "noPatches", "N_L"]
     return dict(zip(keys, map(int, info))), fm, lim
+
+
+def write_frames(batch, sf_index: int, frames=None, extras: int = 0) -> list:
+    """TEST WRITER: raw_data_block bytes of the given frames of a native.Batch (oracle/jaad_writer.c).
+    extras bit 0 adds a DSE and a FIL fill element, bit 1 pulse data (both dropped by the parser)."""
+    nch = batch.nch
+    frames = range(batch.n_frames) if frames is None else frames
+    buf = np.zeros(16384, np.uint8)
+    out = []
+    for f in frames:
+        cf = f * nch
+        q = np.ascontiguousarray(batch.q[cf:cf + nch])
+        sf = np.ascontiguousarray(batch.sf[cf:cf + nch])
+        cb = np.ascontiguousarray(batch.cb[cf:cf + nch])
+        ics = np.ascontiguousarray(batch.ics[cf:cf + nch])
+        ms = np.ascontiguousarray(batch.ms_used[f]) if batch.ms_used is not None else np.zeros(2, np.uint64)
+        tns = np.ascontiguousarray(batch.tns[cf:cf + nch]) if batch.tns is not None else None
+        n = lib().jaad_write_frame(sf_index, nch, q.ctypes.data, sf.ctypes.data, cb.ctypes.data, ics.ctypes.data,
+                                   ms.ctypes.data, tns.ctypes.data if tns is not None else None, extras,
+                                   buf.ctypes.data, buf.nbytes)
+        if n < 0:
+            raise ValueError(f"frame {f} cannot be written")
+        out.append(buf[:n].tobytes())
+    return out
+
+
+def adts_wrap(payloads: list, sf_index: int, channel_config: int) -> bytes:
+    """TEST WRITER: an ADTS stream (no CRC) of raw_data_block payloads."""
+    hdr = np.zeros(7, np.uint8)
+    parts = []
+    for p in payloads:
+        lib().jaad_write_adts_header(sf_index, channel_config, len(p), hdr.ctypes.data)
+        parts += [hdr.tobytes(), p]
+    return b"".join(parts)
 
 
 class Streams:

@@ -52,6 +52,28 @@ def save(name, cfgid, over, cfgkw, flags):
     print(name, b.n_frames, "frames", pcm.nbytes, "PCM bytes")
 
 
+# bitstream fixtures: the synthetic records written as raw_data_blocks / an ADTS stream by the
+# test writer (oracle/jaad_writer.c); expected PCM = the restatement's decode of those records
+BITSTREAMS = {
+    # name: (config id, overrides, container, writer extras)
+    "c1_raw_frame": (1, dict(), "raw", 0),
+    "c3_adts_stream": (3, dict(n_streams=1, frames_per_stream=24, pns_percent=5, is_percent=10), "adts", 3),
+}
+
+
+def save_bitstream(name, cfgid, over, container, extras):
+    p = N.synth_params(cfgid, **over)
+    b = N.synth_batch(p)
+    cfg = N.make_cfg(sf_index=p.sf_index, channel_config=p.channel_config)
+    frames = O.write_frames(b, p.sf_index, extras=extras)
+    data = frames[0] if container == "raw" else O.adts_wrap(frames, p.sf_index, p.channel_config)
+    pcm = O.decode_batch(cfg, b, O.Streams(1), N.PCM_BIG_ENDIAN)
+    np.savez_compressed(HERE / f"{name}.npz", data=np.frombuffer(data, np.uint8), pcm=pcm,
+                        meta=np.array([p.sf_index, p.channel_config, int(b.ics["pns_state"][0]),
+                                       len(frames)], np.int64))
+    print(name, len(frames), "frames", len(data), "bytes")
+
+
 def load(path):
     z = np.load(path, allow_pickle=False)
     meta = [int(v) for v in z["meta"]] + [0, 0, 0]
@@ -71,3 +93,7 @@ if __name__ == "__main__":
         if len(sys.argv) > 1 and k not in sys.argv[1:]:
             continue
         save(k, *v)
+    for k, v in BITSTREAMS.items():
+        if len(sys.argv) > 1 and k not in sys.argv[1:]:
+            continue
+        save_bitstream(k, *v)

@@ -27,8 +27,15 @@ def test_explicit_frequency_maps_to_nearest_index():
     assert DecoderConfig.decode(asc).sf_index == 4
 
 
+def test_explicit_sbr_and_ps_configs():
+    c = DecoderConfig.decode(bytes([0x2B, 0x11, 0x88, 0x00]))  # AOT 5, 24 kHz core -> 48 kHz, stereo
+    assert (c.sbr, c.ps, c.sf_index, c.ext_sf_index, c.getSampleLength(), c.getOutputFrequency()) == \
+        (True, False, 6, 3, 2048, 48000)
+    c = DecoderConfig.decode(bytes([0xEB, 0x09, 0x88, 0x00]))  # AOT 29: mono core + SBR + PS
+    assert (c.sbr, c.ps, c.channel_config, c.getChannelCount()) == (True, True, 1, 2)
+
+
 @pytest.mark.parametrize("asc,msg", [
-    (bytes([0x2B, 0x92, 0x08, 0x00]), "profile"),  # AOT 5 (explicit SBR): the next §8 row, not yet here
     (bytes([0x0A, 0x10]), "profile"),               # AOT 1 (Main): ICPrediction out of scope
     (bytes([0x12, 0x0C]), "960"),                   # frameLengthFlag
     (bytes([0x12]), "end"),
@@ -90,4 +97,40 @@ def test_mixed_endianness_buffers():
     le = O.decode_batch(N.make_cfg(), batch, O.Streams(1), N.PCM_LITTLE_ENDIAN)
     for i, b in enumerate(bufs):
         assert b.getData() == (be if i % 2 == 0 else le)[i].tobytes()
+    dec.close()
+
+
+def test_adts_demultiplexer_mirror():
+    from jaadec_amd.decoder import ADTSDemultiplexer
+    from oracle import oracle as O
+    p = N.synth_params(2, n_streams=1, frames_per_stream=3)
+    b = N.synth_batch(p)
+    frames = O.write_frames(b, p.sf_index)
+    demux = ADTSDemultiplexer(O.adts_wrap(frames, p.sf_index, p.channel_config))
+    assert (demux.getSampleFrequency(), demux.getChannelCount()) == (48000, 2)
+    assert demux.getDecoderInfo().cfg().sf_index == 3
+    got = [demux.readNextFrame() for _ in range(3)]
+    assert got == frames
+    with pytest.raises(EOFError):
+        demux.readNextFrame()
+    with pytest.raises(OSError):
+        ADTSDemultiplexer(bytes(100))
+
+
+@pytest.mark.gpu
+def test_decode_raw_frames_from_adts_matches_oracle():
+    """Main.decodeAAC's loop (S/Main.java:82-111): ADTS -> decodeFrame(raw bytes) -> SampleBuffer."""
+    from jaadec_amd.decoder import ADTSDemultiplexer
+    from oracle import oracle as O
+    p = N.synth_params(3, n_streams=1, frames_per_stream=12)
+    b = N.synth_batch(p)
+    demux = ADTSDemultiplexer(O.adts_wrap(O.write_frames(b, p.sf_index), p.sf_index, p.channel_config))
+    dec = Decoder.create(demux.getDecoderInfo())
+    dec._parse([])  # parser up front so the PNS LCG can be seeded like the synthetic batch's
+    dec._parser.pns_state = int(b.ics["pns_state"][0])
+    want = O.decode_batch(N.make_cfg(), b, O.Streams(1), N.PCM_BIG_ENDIAN)
+    for i in range(12):
+        buf = SampleBuffer()
+        dec.decodeFrame(demux.readNextFrame(), buf)
+        assert buf.getData() == want[i].tobytes()
     dec.close()

@@ -8,7 +8,7 @@ import pytest
 from oracle import oracle as O
 
 HERE = Path(__file__).resolve().parent
-GOLD = sorted((HERE / "golden").glob("*.npz"))
+GOLD = sorted(g for g in (HERE / "golden").glob("*.npz") if not g.stem.endswith(("_raw_frame", "_adts_stream")))
 
 
 def _load(path):

@@ -99,6 +99,20 @@ PS_TABLES = [
     ("ps/Filter2.java", "p2_13_20", "JAAD_PS_P2_13_20", "f32"),
 ]
 
+# Huffman codebooks -> jaad_huffman_tables.inc (host parser): AAC spectral/scalefactor codebooks
+# as {length, codeword, values...} rows (A/huffman/Codebooks.java), SBR and PS binary trees as
+# {child0, child1} rows, negative = leaf (A/sbr/HuffmanTables.java, A/ps/Huffman.java)
+HUFF_OUT = OUT.with_name("jaad_huffman_tables.inc")
+HUFF_TABLES = [("huffman/Codebooks.java", n, "JAAD_" + n, "i32_2d") for n in
+               ["HCB1", "HCB2", "HCB3", "HCB4", "HCB5", "HCB6", "HCB7", "HCB8", "HCB9", "HCB10", "HCB11", "HCB_SF"]]
+HUFF_TABLES += [("sbr/HuffmanTables.java", n, "JAAD_SBR_" + n, "i32_2d") for n in
+                ["T_HUFFMAN_ENV_1_5DB", "F_HUFFMAN_ENV_1_5DB", "T_HUFFMAN_ENV_BAL_1_5DB", "F_HUFFMAN_ENV_BAL_1_5DB",
+                 "T_HUFFMAN_ENV_3_0DB", "F_HUFFMAN_ENV_3_0DB", "T_HUFFMAN_ENV_BAL_3_0DB", "F_HUFFMAN_ENV_BAL_3_0DB",
+                 "T_HUFFMAN_NOISE_3_0DB", "T_HUFFMAN_NOISE_BAL_3_0DB"]]
+HUFF_TABLES += [("ps/Huffman.java", n, "JAAD_PS_" + n.upper(), "i32_2d") for n in
+                ["f_huff_iid_def", "t_huff_iid_def", "f_huff_iid_fine", "t_huff_iid_fine", "f_huff_icc", "t_huff_icc",
+                 "f_huff_ipd", "t_huff_ipd", "f_huff_opd", "t_huff_opd"]]
+
 SWB = [  # ScaleFactorBands: per sampling-frequency-index offset tables
     ("SWB_OFFSET_1024_96", "SWB_OFFSET_1024_64", "SWB_OFFSET_1024_48", "SWB_OFFSET_1024_32",
      "SWB_OFFSET_1024_24", "SWB_OFFSET_1024_16", "SWB_OFFSET_1024_8"),
@@ -204,6 +218,7 @@ def main() -> int:
     print("wrote", OUT, sum(1 for _ in out), "lines")
     emit(SBR_TABLES, SBR_OUT)
     emit(PS_TABLES, PS_OUT)
+    emit(HUFF_TABLES, HUFF_OUT)
     return 0
 
 
