@@ -174,6 +174,7 @@ struct jaad_ctx {
     // after call.  The state_* entry points and jaad_wait wait for it too.
     hipEvent_t done = nullptr;
     bool done_live = false;
+    hipStream_t last_stream = nullptr;  // stream of the previous device call
     std::vector<ChunkDesc> chunks;
     std::vector<uint32_t> plan_slots, plan_begin;  // plan cache key
     std::vector<uint8_t> slot_used;
@@ -726,11 +727,14 @@ int launch_work(jaad_ctx* ctx, const jaad_batch* db, void* pcm, uint32_t flags, 
 
 int launch(jaad_ctx* ctx, const jaad_batch* db, void* pcm, uint32_t flags, hipStream_t stream)
 {
-    if (ctx->done_live) HIPCHK(hipStreamWaitEvent(stream, ctx->done, 0));
+    // a call on the stream of the previous call is ordered after it by the stream itself; only a
+    // switch of streams needs the wait (an extra barrier packet per call otherwise)
+    if (ctx->done_live && stream != ctx->last_stream) HIPCHK(hipStreamWaitEvent(stream, ctx->done, 0));
     const int rc = launch_work(ctx, db, pcm, flags, stream);
     // recorded on failure too: whatever part of the call was queued is covered by the next wait
     HIPCHK(hipEventRecord(ctx->done, stream));
     ctx->done_live = true;
+    ctx->last_stream = stream;
     return rc;
 }
 
