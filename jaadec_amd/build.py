@@ -74,7 +74,8 @@ def build_synth(force: bool = False) -> Path:
 
 def build_oracle(force: bool = False) -> Path:
     srcs = [ROOT / "oracle" / "jaad_oracle.c", ROOT / "oracle" / "jaad_oracle_sbr.c", ROOT / "oracle" / "jaad_oracle_ps.c",
-            ROOT / "oracle" / "jaad_writer.c"]
+            ROOT / "oracle" / "jaad_writer.c",
+            ROOT / "oracle" / "jaad_writer_sbr.c"]
     deps = srcs + _deps("oracle/*.h", "include/*.h", "jaadec_amd/csrc/tables/*.inc")
     if force or _stale(ORACLE_LIB, deps):
         _run(["gcc", "-O2", "-std=c11", "-fPIC", "-shared", "-ffp-contract=off", "-fno-fast-math",

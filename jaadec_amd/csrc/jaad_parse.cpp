@@ -570,7 +570,11 @@ int jaad_parse_frame(jaad_parser* p, const uint8_t* data, size_t bytes, jaad_fra
             BitReader sub = br.sub(8 * count);
             br.skip(8 * count);
             const int type = (int)sub.read(4);
-            if ((type == 13 || type == 14) && have_channels && C.cfg.sbr) {  // EXT_SBR_DATA(_CRC)
+            if ((type == 13 || type == 14) && have_channels) {  // EXT_SBR_DATA(_CRC)
+                // implicit SBR: the reference (sbrEnabled by default, A/DecoderConfig.java:47-53)
+                // would decode it and double the output rate; the caller must re-open the
+                // stream with cfg.sbr = 1 (and cfg.ps = 1 for a mono core, SCE.isStereo)
+                if (!C.cfg.sbr) return JAAD_ERR_UNSUPPORTED;
                 const int st = parse_sbr(sub, C, type == 14, ns, *out->sbr);
                 if (st) return st;
                 sbr_seen = 1;

@@ -63,27 +63,35 @@ struct Cfg {
     int sf_index = 0, nswb_l = 0, nswb_s = 0;
 };
 
-// SBR / PS bitstream state that persists between frames (jaad_parse_sbr.cpp)
+// SBR / PS bitstream state that persists between frames (jaad_parse_sbr.cpp): what the
+// reference keeps in SBR (header, derived band counts), Channel (grid, E/Q of the previous frame,
+// A/sbr/Channel.java, A/sbr/SBR.java:256-284) and PSImpl / EnvData (A/ps/PSImpl.java,
+// A/ps/EnvData.java, A/ps/Envelope.java) between frames
+struct PsEnvData {
+    int mode = -1;              // EnvMode id, -1 = null (disabled)
+    int first[34] = {0};        // EnvData.first: the last envelope of the previous PS frame
+    int index[5][34] = {{0}};   // Envelope.index of envs[0..4] (persist across frames)
+    bool dt[5] = {false};
+};
 struct SbrParseState {
-    bool have_header = false;
+    bool have_hdr = false;
     jaad_sbr_header hdr{};
-    int kx = 0, M = 0, N_high = 0, N_low = 0, N_Q = 0;  // derived tables of the current header
-    int n[2] = {0, 0};                                  // N_low, N_high
-    bool valid = false;
-    struct Ch {
-        int L_E_prev = 0, L_Q_prev = 0, f_prev_last = 0;
-        int E_prev[64] = {0}, Q_prev[8] = {0};
-        int t_E_prev_last = 0;
-        int frame_class_prev = 0, bs_pointer_prev = 0;
-        int bs_add_harmonic_prev[64] = {0};
-        int add_harmonic_flag_prev = 0;
-        int invf_prev[5] = {0};
+    int n[2] = {0, 0}, N_Q = 0, N_high = 0, N_low = 0;  // derived tables of the current header
+    int f_table_res[2][65] = {{0}};
+    struct Ch {  // the parse-side fields of Channel; arrays keep stale entries as the Java ones do
+        int frame_class = 0, L_E = 0, L_Q = 0, bs_pointer = 0;
+        int t_E[6] = {0}, t_Q[3] = {0}, f[6] = {0};
+        int df_env[9] = {0}, df_noise[3] = {0}, invf[5] = {0};
+        int E[64][5] = {{0}}, Q[64][2] = {{0}};
+        int add_harmonic_flag = 0;
+        uint64_t add_harmonic = 0;
+        int E_prev[64] = {0}, Q_prev[64] = {0}, f_prev = 0;  // sbr_save_prev_data
     } ch[2];
     struct Ps {
-        bool header_seen = false;
-        int iid_mode = 0, icc_mode = 0, ext = 0, ipd_mode_prev = 0;
-        int iid_prev[34] = {0}, icc_prev[34] = {0}, ipd_prev[17] = {0}, opd_prev[17] = {0};
-        bool enable_iid = false, enable_icc = false, enable_ipdopd = false;
+        bool var_borders = false;
+        int border[6] = {0};
+        PsEnvData iid, icc, ipd, opd;
+        bool ext_enabled = false, ext_data = false, ext_data_enabled = false;
     } ps;
 };
 

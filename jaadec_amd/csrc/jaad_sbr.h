@@ -195,6 +195,9 @@ struct SbrFbt {
     uint8_t visited[4][64];
 };
 
+// SBR.calc_sbr_tables for the bitstream parser (jaad_parse_sbr.cpp): band counts and f_table_res
+bool sbr_tables_for_parse(int out_sf, const jaad_sbr_header& h, SbrFbt& t);
+
 class SbrHost {
 public:
     static constexpr size_t kMaxTables = 1024;  // distinct SBR headers per context

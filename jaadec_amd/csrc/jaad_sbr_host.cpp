@@ -273,6 +273,26 @@ void SbrHost::reset_slot(SbrHostSlot& s)
     for (auto& c : s.ch) c.prevEnvIsShort = -1;
 }
 
+// the frequency tables the bitstream parse needs (band counts, f_table_res): SBR.calc_sbr_tables
+// (A/sbr/SBR.java:125-158) for a header at output rate index out_sf; false where the reference's
+// table checks fail
+bool sbr_tables_for_parse(int out_sf, const jaad_sbr_header& h, SbrFbt& t)
+{
+    std::memset(&t, 0, sizeof t);
+    const int sfi = out_sf;
+    if (sfi < 0 || sfi > 11) return false;
+    t.k0 = JAAD_SBR_START_MIN[sfi] + JAAD_SBR_OFFSET[JAAD_SBR_OFFSET_INDEX[sfi]][h.start_freq & 15];
+    if (h.stop_freq == 15) t.k2 = std::min(64, t.k0 * 3);
+    else if (h.stop_freq == 14) t.k2 = std::min(64, t.k0 * 2);
+    else t.k2 = std::min(64, JAAD_SBR_STOP_MIN[sfi] + JAAD_SBR_STOP_OFFSET[sfi][std::min((int)h.stop_freq, 13)]);
+    const int fs = kFreq[sfi];
+    const int span = t.k2 - t.k0;
+    if ((fs >= 48000 && span > 32) || (fs <= 32000 && span > 48) || (fs > 32000 && fs < 48000 && span > 45))
+        return false;
+    const bool ok = h.freq_scale == 0 ? master_fs0(t, t.k0, t.k2, h.alter_scale != 0) : master_fs(t, t.k0, t.k2, h.freq_scale);
+    return ok && derived_tables(t, h.xover_band, h.noise_bands);
+}
+
 int SbrHost::table_for(const jaad_sbr_header& h)
 {
     std::lock_guard<std::mutex> lock(mu_);

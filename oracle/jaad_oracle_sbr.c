@@ -1242,6 +1242,27 @@ int orc_sbr_table_info(const jaad_sbr_header* h, int out_sf_index, int* info, in
     return rc ? JAAD_ERR_BITSTREAM : JAAD_OK;
 }
 
+/* band counts of the bitstream syntax for a header (test writer): info = n[0] n[1] N_Q N_high N_low,
+ * ftr = f_table_res[2][64] */
+int orc_sbr_res_tables(const jaad_sbr_header* h, int out_sf_index, int* info, int* ftr)
+{
+    orc_sbr* s = (orc_sbr*)calloc(1, sizeof(orc_sbr));
+    if (!s) return JAAD_ERR_NOMEM;
+    s->out_sf_index = out_sf_index;
+    s->hdr = *h;
+    const int rc = calc_sbr_tables(s);
+    if (!rc) {
+        info[0] = s->n[0];
+        info[1] = s->n[1];
+        info[2] = s->N_Q;
+        info[3] = s->N_high;
+        info[4] = s->N_low;
+        memcpy(ftr, s->f_table_res, sizeof s->f_table_res);
+    }
+    free(s);
+    return rc ? JAAD_ERR_BITSTREAM : JAAD_OK;
+}
+
 /* debug: G/Q smoothing ring of channel c after the last processed frame: out[2][5][64], returns index */
 int orc_sbr_debug_ring(const orc_sbr* s, int c, float* out)
 {

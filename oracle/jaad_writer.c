@@ -258,14 +258,18 @@ static int put_ics(Bw* w, int sf_index, int common, const int16_t* q, const uint
     return 0;
 }
 
+long jaad_sbr_fil_bits(void* state, int nch, const jaad_sbr_frame* rec, uint8_t* out, size_t cap);
+
 /*
  * One raw_data_block of the frame's records (nch = 1: SCE, 2: CPE), optionally wrapped in
- * extra DSE / FIL(fill) elements (extras bit 0) and carrying pulse data (bit 1).
- * Returns the byte count, or -1 when a record cannot be represented / cap is too small.
+ * extra DSE / FIL(fill) elements (extras bit 0) and carrying pulse data (bit 1); with `sbr`
+ * (and the stream's writer state, jaad_writer_sbr.c) the SBR record follows the channel
+ * element as a FIL element.  Returns the byte count, or -1 when a record cannot be
+ * represented / cap is too small.
  */
-long jaad_write_frame(int sf_index, int nch, const int16_t* q, const uint8_t* sf, const uint8_t* cb,
-                      const jaad_ics_info* ics, const uint64_t* ms_used, const jaad_tns* tns, int extras,
-                      uint8_t* out, size_t cap)
+long jaad_write_frame_sbr(int sf_index, int nch, const int16_t* q, const uint8_t* sf, const uint8_t* cb,
+                          const jaad_ics_info* ics, const uint64_t* ms_used, const jaad_tns* tns, int extras,
+                          const jaad_sbr_frame* sbr, void* sbr_state, uint8_t* out, size_t cap)
 {
     Bw w = {out, cap, 0, 0};
     memset(out, 0, cap);
@@ -308,6 +312,12 @@ long jaad_write_frame(int sf_index, int nch, const int16_t* q, const uint8_t* sf
         if (put_ics(&w, sf_index, common, q + 1024, sf + 128, cb + 128, &ics[1], tns ? tns + 1 : NULL, extras & 2))
             return -1;
     }
+    if (sbr) {
+        uint8_t fil[512];
+        const long nbits = jaad_sbr_fil_bits(sbr_state, nch, sbr, fil, sizeof fil);
+        if (nbits < 0) return -1;
+        for (long i = 0; i < nbits; i++) put(&w, (fil[i >> 3] >> (7 - (i & 7))) & 1u, 1);
+    }
     if (extras & 1) { /* FIL element: 2 bytes of EXT_FILL_DATA */
         put(&w, 6, 3);
         put(&w, 2, 4);
@@ -317,6 +327,13 @@ long jaad_write_frame(int sf_index, int nch, const int16_t* q, const uint8_t* sf
     put(&w, 7, 3); /* END */
     align(&w);
     return w.overflow ? -1 : (long)(w.pos / 8);
+}
+
+long jaad_write_frame(int sf_index, int nch, const int16_t* q, const uint8_t* sf, const uint8_t* cb,
+                      const jaad_ics_info* ics, const uint64_t* ms_used, const jaad_tns* tns, int extras,
+                      uint8_t* out, size_t cap)
+{
+    return jaad_write_frame_sbr(sf_index, nch, q, sf, cb, ics, ms_used, tns, extras, NULL, NULL, out, cap);
 }
 
 /* ADTS header (S/adts/ADTSFrame.java:48-111) for a payload of `payload` bytes, no CRC */

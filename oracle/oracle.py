@@ -47,6 +47,13 @@ def lib() -> C.CDLL:
         L.orc_sbr_table_info.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
         L.jaad_write_frame.argtypes = [C.c_int, C.c_int] + [C.c_void_p] * 6 + [C.c_int, C.c_void_p, C.c_size_t]
         L.jaad_write_frame.restype = C.c_long
+        L.jaad_write_frame_sbr.argtypes = ([C.c_int, C.c_int] + [C.c_void_p] * 6 + [C.c_int, C.c_void_p, C.c_void_p,
+                                           C.c_void_p, C.c_size_t])
+        L.jaad_write_frame_sbr.restype = C.c_long
+        L.jaad_sbr_wstate_size.restype = C.c_size_t
+        L.jaad_sbr_wstate_init.argtypes = [C.c_void_p, C.c_int, C.c_uint64]
+        L.jaad_sbr_wstate_init.restype = None
+        L.orc_sbr_res_tables.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
         L.jaad_write_adts_header.argtypes = [C.c_int, C.c_int, C.c_size_t, C.c_void_p]
         _lib = L
     return _lib
@@ -130,9 +137,30 @@ def sbr_table_info(hdr, out_sf_index: int):
     return dict(zip(keys, map(int, info))), fm, lim
 
 
-def write_frames(batch, sf_index: int, frames=None, extras: int = 0) -> list:
+def sbr_res_tables(hdr, out_sf_index: int):
+    """(n[0], n[1], N_Q, N_high, N_low), f_table_res[2][64] of a header (calc_sbr_tables)."""
+    h = np.ascontiguousarray(np.array(hdr))
+    info = np.zeros(5, np.int32)
+    ftr = np.zeros((2, 64), np.int32)
+    rc = lib().orc_sbr_res_tables(h.ctypes.data, out_sf_index, info.ctypes.data, ftr.ctypes.data)
+    if rc:
+        raise RuntimeError(f"orc_sbr_res_tables failed: {rc}")
+    return tuple(int(v) for v in info), ftr
+
+
+class SbrWriter:
+    """TEST WRITER state of one SBR stream (oracle/jaad_writer_sbr.c): tables of the current header
+    and the previous frame's values its time-delta coding starts from."""
+
+    def __init__(self, out_sf_index: int, seed: int = 1):
+        self.buf = np.zeros(lib().jaad_sbr_wstate_size(), np.uint8)
+        lib().jaad_sbr_wstate_init(self.buf.ctypes.data, out_sf_index, seed)
+
+
+def write_frames(batch, sf_index: int, frames=None, extras: int = 0, sbr_writer: SbrWriter | None = None) -> list:
     """TEST WRITER: raw_data_block bytes of the given frames of a native.Batch (oracle/jaad_writer.c).
-    extras bit 0 adds a DSE and a FIL fill element, bit 1 pulse data (both dropped by the parser)."""
+    extras bit 0 adds a DSE and a FIL fill element, bit 1 pulse data (both dropped by the parser).
+    With sbr_writer, each frame's SBR record (batch.sbr) follows its channel element as a FIL."""
     nch = batch.nch
     frames = range(batch.n_frames) if frames is None else frames
     buf = np.zeros(16384, np.uint8)
@@ -145,9 +173,12 @@ def write_frames(batch, sf_index: int, frames=None, extras: int = 0) -> list:
         ics = np.ascontiguousarray(batch.ics[cf:cf + nch])
         ms = np.ascontiguousarray(batch.ms_used[f]) if batch.ms_used is not None else np.zeros(2, np.uint64)
         tns = np.ascontiguousarray(batch.tns[cf:cf + nch]) if batch.tns is not None else None
-        n = lib().jaad_write_frame(sf_index, nch, q.ctypes.data, sf.ctypes.data, cb.ctypes.data, ics.ctypes.data,
-                                   ms.ctypes.data, tns.ctypes.data if tns is not None else None, extras,
-                                   buf.ctypes.data, buf.nbytes)
+        rec = np.ascontiguousarray(batch.sbr[f:f + 1]) if sbr_writer is not None else None
+        n = lib().jaad_write_frame_sbr(sf_index, nch, q.ctypes.data, sf.ctypes.data, cb.ctypes.data, ics.ctypes.data,
+                                       ms.ctypes.data, tns.ctypes.data if tns is not None else None, extras,
+                                       rec.ctypes.data if rec is not None else None,
+                                       sbr_writer.buf.ctypes.data if sbr_writer is not None else None,
+                                       buf.ctypes.data, buf.nbytes)
         if n < 0:
             raise ValueError(f"frame {f} cannot be written")
         out.append(buf[:n].tobytes())
