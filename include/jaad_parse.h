@@ -18,6 +18,8 @@
  *   static PNS LCG state             A/syntax/ICStream.java:26,247 (one LCG per parser)
  *   AudioSpecificConfig              A/DecoderConfig.java:175-291
  *   ADTS header / sync search        S/adts/ADTSFrame.java, S/adts/ADTSDemultiplexer.java:25-58
+ *   SBR / PS extension payloads      A/sbr/SBR.java:161-284, SBR1.java, SBR2.java, Channel.java:85-583,
+ *                                    A/ps/PSImpl.java:103-199, EnvData.java, Envelope.java
  *
  * Plain C types only; every entry point returns 0 or a negative jaad_status.
  */
@@ -35,7 +37,9 @@ extern "C" {
 
 /* AudioSpecificConfig -> stream configuration (DecoderConfig.decode).  AOT 2 (LC), 5 (SBR) and
  * 29 (PS) with an LC core; frameLengthFlag = 1 (960-sample frames) is rejected as the
- * reference rejects it (JAAD_ERR_UNSUPPORTED). */
+ * reference rejects it (JAAD_ERR_UNSUPPORTED).  A mono AOT 5 stream gets ps = 1: the reference
+ * has PS enabled by default (A/DecoderConfig.java:36, A/sbr/SBR1.java:62-73), so PS data it
+ * meets is applied, and frames without it duplicate the SBR channel as ps = 0 would. */
 int jaad_asc_parse(const uint8_t* asc, size_t bytes, jaad_stream_cfg* cfg);
 
 /* ADTS fixed + variable header (S/adts/ADTSFrame.java:48-111) */
@@ -82,6 +86,15 @@ typedef struct jaad_frame_out {
  * parser's state (window shapes, PNS LCG, SBR/PS history) changes, so the caller may drop
  * the frame as Decoder.decodeFrame drops an EOS frame (A/Decoder.java:96-100). */
 int jaad_parse_frame(jaad_parser* p, const uint8_t* data, size_t bytes, jaad_frame_out* out);
+
+/* Implicit SBR signalling (ADTS, LC-only AudioSpecificConfig): the reference opens SBR when it
+ * meets an SBR extension payload (A/syntax/ChannelElement.java:63-74) and doubles the output
+ * rate when it can (DecoderConfig.setSBRPresent, A/DecoderConfig.java:124-135).  This tells a
+ * host whether a raw_data_block of a core configuration carries one (*found bit 0), so it can
+ * re-open the stream with sbr = 1, ext_sf_index = sf_index - 3 (and ps = 1 for a mono core);
+ * sf_index < 3 has no doubled rate (the reference's downsampled SBR, not supported).
+ * jaad_parse_frame itself refuses an SBR payload in a core configuration (UNSUPPORTED). */
+int jaad_probe_sbr(const jaad_stream_cfg* cfg, const uint8_t* data, size_t bytes, uint32_t* found);
 
 #ifdef __cplusplus
 }

@@ -454,7 +454,7 @@ int jaad_asc_parse(const uint8_t* asc, size_t bytes, jaad_stream_cfg* cfg)
     const int chc = (int)br.read(4);
     if (aot == 5 || aot == 29) {  // AAC_SBR / AAC_PS: extension rate, core profile; no GASpecificConfig
         cfg->sbr = 1;
-        cfg->ps = aot == 29;
+        cfg->ps = aot == 29 || chc == 1;  // mono: PS enabled by default (jaad_parse.h)
         cfg->ext_sf_index = (uint8_t)rate();
         aot = profile();
     } else if (aot == 2) {
@@ -543,7 +543,12 @@ void jaad_parser_set_pns_state(jaad_parser* p, uint32_t s)
     if (p) p->st.pns = s;
 }
 
-int jaad_parse_frame(jaad_parser* p, const uint8_t* data, size_t bytes, jaad_frame_out* out)
+}  // extern "C"
+
+namespace {
+// probe != nullptr: stop at the first SBR extension payload after the channel element
+// (bit 0 of *probe) and commit nothing
+int parse_frame(jaad_parser* p, const uint8_t* data, size_t bytes, jaad_frame_out* out, uint32_t* probe)
 {
     if (!p || !out || (!data && bytes) || !out->q || !out->sf || !out->cb || !out->ics) return JAAD_ERR_INVALID_ARG;
     const Cfg& C = p->C;
@@ -574,6 +579,10 @@ int jaad_parse_frame(jaad_parser* p, const uint8_t* data, size_t bytes, jaad_fra
                 // implicit SBR: the reference (sbrEnabled by default, A/DecoderConfig.java:47-53)
                 // would decode it and double the output rate; the caller must re-open the
                 // stream with cfg.sbr = 1 (and cfg.ps = 1 for a mono core, SCE.isStereo)
+                if (probe) {
+                    *probe |= 1u;
+                    return JAAD_OK;
+                }
                 if (!C.cfg.sbr) return JAAD_ERR_UNSUPPORTED;
                 const int st = parse_sbr(sub, C, type == 14, ns, *out->sbr);
                 if (st) return st;
@@ -646,8 +655,37 @@ int jaad_parse_frame(jaad_parser* p, const uint8_t* data, size_t bytes, jaad_fra
         const int st = sbr_missing(C, ns, *out->sbr);
         if (st) return st;
     }
-    p->st = ns;
+    if (!probe) p->st = ns;
     return JAAD_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int jaad_parse_frame(jaad_parser* p, const uint8_t* data, size_t bytes, jaad_frame_out* out)
+{
+    return parse_frame(p, data, bytes, out, nullptr);
+}
+
+int jaad_probe_sbr(const jaad_stream_cfg* cfg, const uint8_t* data, size_t bytes, uint32_t* found)
+{
+    if (!cfg || !found || (!data && bytes)) return JAAD_ERR_INVALID_ARG;
+    *found = 0;
+    jaad_stream_cfg core = *cfg;
+    core.sbr = core.ps = 0;
+    core.ext_sf_index = 0;
+    jaad_parser* p = nullptr;
+    int st = jaad_parser_create(&core, &p);
+    if (st) return st;
+    std::vector<int16_t> q(2048);
+    std::vector<uint8_t> sf(256), cb(256);
+    jaad_ics_info ics[2];
+    jaad_tns tns[2];
+    uint64_t ms[2];
+    jaad_frame_out o{q.data(), sf.data(), cb.data(), ics, ms, tns, nullptr};
+    st = parse_frame(p, data, bytes, &o, found);
+    jaad_parser_destroy(p);
+    return st;
 }
 
 }  // extern "C"

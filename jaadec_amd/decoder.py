@@ -157,8 +157,28 @@ class Decoder:
     def _flags(self, buf: SampleBuffer) -> int:
         return N.PCM_BIG_ENDIAN if buf.big_endian else N.PCM_LITTLE_ENDIAN
 
+    def _implicit_sbr(self, first: bytes) -> None:
+        """A core configuration whose first frame carries SBR data is upgraded as the reference
+        upgrades its DecoderConfig (A/syntax/ChannelElement.java:63-74, SBR.java:100): doubled
+        output rate, stereo output, PS applied if present."""
+        c = self.config
+        try:
+            if c.sbr or not N.probe_sbr(c.cfg(), first):
+                return
+            up = N.implicit_sbr_cfg(c.cfg())
+        except N.JaadError as e:
+            raise AACException(str(e)) from e
+        if not self._own:
+            raise AACException("implicit SBR in a stream decoded on a shared core-only context")
+        self._ctx.close()
+        self.config = DecoderConfig(c.profile, c.sf_index, c.channel_config, c.tns_mode, True, bool(up.ps),
+                                    up.ext_sf_index)
+        self._ctx = N.Context(self.config.cfg(), 1)
+
     def _parse(self, frames: list) -> N.Batch:
         if self._parser is None:
+            if frames and self.frames == 0:
+                self._implicit_sbr(bytes(frames[0]))
             self._parser = N.Parser(self.config.cfg())
         try:
             return self._parser.parse(frames, self.slot)

@@ -80,7 +80,7 @@ EXPORTS = ["jaad_cfg_sample_length", "jaad_cfg_channel_count", "jaad_frame_pcm_b
            "jaad_state_export", "jaad_state_import", "jaad_state_reset", "jaad_strerror", "jaad_last_error"]
 # every symbol include/jaad_parse.h declares
 PARSE_EXPORTS = ["jaad_asc_parse", "jaad_adts_find", "jaad_adts_cfg", "jaad_parser_create", "jaad_parser_destroy",
-                 "jaad_parser_pns_state", "jaad_parser_set_pns_state", "jaad_parse_frame"]
+                 "jaad_parser_pns_state", "jaad_parser_set_pns_state", "jaad_parse_frame", "jaad_probe_sbr"]
 
 
 class AdtsHeader(C.Structure):
@@ -145,6 +145,7 @@ def lib() -> C.CDLL:
         L.jaad_parser_set_pns_state.argtypes = [C.c_void_p, C.c_uint32]
         L.jaad_parser_set_pns_state.restype = None
         L.jaad_parse_frame.argtypes = [C.c_void_p, C.c_char_p, C.c_size_t, C.POINTER(FrameOut)]
+        L.jaad_probe_sbr.argtypes = [C.POINTER(StreamCfg), C.c_char_p, C.c_size_t, C.POINTER(C.c_uint32)]
         _lib = L
     return _lib
 
@@ -392,6 +393,24 @@ def adts_cfg(h: AdtsHeader) -> StreamCfg:
     if rc:
         raise JaadError(rc, "jaad_adts_cfg")
     return cfg
+
+
+def probe_sbr(cfg: StreamCfg, frame: bytes) -> bool:
+    """Does this raw_data_block of a core configuration carry an SBR payload (implicit SBR)?"""
+    found = C.c_uint32()
+    rc = lib().jaad_probe_sbr(C.byref(cfg), bytes(frame), len(frame), C.byref(found))
+    if rc:
+        raise JaadError(rc, "jaad_probe_sbr")
+    return bool(found.value & 1)
+
+
+def implicit_sbr_cfg(cfg: StreamCfg) -> StreamCfg:
+    """The configuration the reference switches to when it meets SBR data in a core stream
+    (DecoderConfig.setSBRPresent, A/DecoderConfig.java:124-135): doubled output rate; a mono
+    core decodes to stereo (SCE.isStereo) with PS applied when present (psEnabled)."""
+    if cfg.sf_index < 3:
+        raise JaadError(ERR_UNSUPPORTED, "implicit SBR without a doubled rate (downsampled SBR)")
+    return make_cfg(cfg.sf_index, cfg.channel_config, cfg.tns_mode, sbr=True, ps=cfg.channel_config == 1)
 
 
 class Parser:

@@ -280,3 +280,55 @@ def test_he_aac_bitstream_decodes_on_the_gpu(cfgid):
     with N.Context(cfg, 1) as ctx:
         pcm = ctx.decode(got, N.PCM_BIG_ENDIAN)
     assert pcm.tobytes() == want.tobytes()
+
+
+def test_implicit_sbr_probe_and_upgraded_config():
+    """ADTS / LC-only signalling: SBR is found in the payload (implicit SBR)."""
+    for cfgid in (4, 5):
+        p, b = _stream(cfgid, 2, 3, header_gaps=False)
+        cfg = N.cfg_for(p)
+        sbr_frames = O.write_frames(b, p.sf_index, sbr_writer=O.SbrWriter(cfg.ext_sf_index, 3))
+        lc_frames = O.write_frames(b, p.sf_index)
+        core = N.make_cfg(p.sf_index, p.channel_config)
+        assert N.probe_sbr(core, sbr_frames[0]) and not N.probe_sbr(core, lc_frames[0])
+        up = N.implicit_sbr_cfg(core)
+        assert (up.sbr, up.ps, up.ext_sf_index) == (1, int(p.channel_config == 1), p.sf_index - 3)
+        # the upgraded configuration parses the stream to the records it was written from
+        P = N.Parser(up)
+        P.pns_state = int(b.ics["pns_state"][0])
+        got = P.parse(sbr_frames)
+        _assert_sbr_equal(got.sbr, b.sbr, b.nch, up.ext_sf_index)
+    with pytest.raises(N.JaadError) as e:  # 64 kHz core: no doubled rate (downsampled SBR)
+        N.implicit_sbr_cfg(N.make_cfg(2, 2))
+    assert e.value.status == N.ERR_UNSUPPORTED
+    # explicit AOT 5 mono: PS stays enabled, as psEnabled is by default
+    cfg = N.asc_parse(bytes([0x2B, 0x09, 0x88, 0x00]))
+    assert (cfg.sbr, cfg.ps, cfg.channel_config) == (1, 1, 1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfgid", [4, 5])
+def test_adts_he_aac_with_implicit_sbr_through_the_decoder_facade(cfgid):
+    """An ADTS HE-AAC stream (the header says LC at the core rate) through ADTSDemultiplexer +
+    Decoder: the façade finds the SBR payload, re-opens at the doubled rate, and the PCM equals
+    the restatement's decode of the records, byte for byte."""
+    from jaadec_amd.decoder import ADTSDemultiplexer, Decoder, SampleBuffer
+    p, b = _stream(cfgid, 12, 9, ps_modes=cfgid == 5)
+    cfg = N.cfg_for(p)
+    frames = O.write_frames(b, p.sf_index, sbr_writer=O.SbrWriter(cfg.ext_sf_index, 9))
+    stream = O.adts_wrap(frames, p.sf_index, p.channel_config)
+    demux = ADTSDemultiplexer(stream)
+    dec = Decoder.create(demux.getDecoderInfo())
+    payloads = []
+    while True:
+        try:
+            payloads.append(demux.readNextFrame())
+        except EOFError:
+            break
+    bufs = [SampleBuffer() for _ in payloads]
+    assert not dec.getConfig().sbr
+    dec.decodeFrames(payloads, bufs)  # no PNS bands in C4/C5: the parser's LCG start is moot
+    assert dec.getConfig().getSampleLength() == 2048 and dec.getConfig().getOutputFrequency() == 48000
+    want = O.decode_batch(cfg, b, O.Streams(1), N.PCM_BIG_ENDIAN)
+    assert b"".join(x.data for x in bufs) == want.tobytes()
+    dec.close()
