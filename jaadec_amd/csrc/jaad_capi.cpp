@@ -28,6 +28,11 @@ using namespace jaad;
 
 namespace {
 
+// offsets (in floats) into the SBR constant buffer, after qmf_c | dct4 | noise
+constexpr size_t kSbrConstTw32 = 640 + 224 + 1024;
+constexpr size_t kSbrConstDct32 = kSbrConstTw32 + 64;  // 8-byte aligned: double table
+static_assert(kSbrConstDct32 % 2 == 0, "double table alignment");
+
 // SampleFrequency maxTNS_SFB {long, short} (A/SampleFrequency.java:15-26)
 const unsigned char kMaxTnsSfb[12][2] = {{31, 9}, {31, 9}, {34, 10}, {40, 14}, {42, 14}, {51, 14},
                                          {46, 14}, {46, 14}, {42, 14}, {42, 14}, {42, 14}, {39, 14}};
@@ -189,7 +194,8 @@ struct jaad_ctx {
     std::unique_ptr<SbrHost> sbr_host;
     std::vector<SbrHostSlot> sbr_slots;          // parameter-side state per slot (host)
     SbrChState* d_sbr_state = nullptr;           // [slot][2], rewritten at the end of each call
-    float* d_sbr_const = nullptr;                // qmf_c[640] | dct4 tab[192] w_re[16] w_im[16] | noise[1024]
+    float* d_sbr_const = nullptr;                // qmf_c[640] | dct4 tab[192] w_re[16] w_im[16] | noise[1024] |
+                                                 // tw32[64] | dct32 double[2][32][32]
     DevBuf d_time, d_xlow, d_xsyn, d_xcarry, d_gq;
     hipStream_t cstream = nullptr;               // record uploads
     RecSet rsets[2];
@@ -296,8 +302,10 @@ int validate_cfg(const jaad_stream_cfg* cfg)
     if (cfg->tns_mode > JAAD_TNS_SPEC) return JAAD_ERR_INVALID_ARG;
     if (cfg->sbr > 1 || cfg->ps > 1) return JAAD_ERR_UNSUPPORTED;
     if (cfg->ps && (!cfg->sbr || cfg->channel_config != 1)) return JAAD_ERR_UNSUPPORTED;
-    // explicit SBR at twice the core rate (bs_samplerate_mode = 1, A/sbr/SBR.java:105)
-    if (cfg->sbr && (cfg->sf_index < 3 || cfg->ext_sf_index + 3 != cfg->sf_index)) return JAAD_ERR_UNSUPPORTED;
+    // SBR at twice the core rate (bs_samplerate_mode = 1, A/sbr/SBR.java:105), or downsampled
+    // (extension rate = core rate: SBR.downSampled, 32-band synthesis, A/sbr/SBR.java:35-37,100)
+    if (cfg->sbr && cfg->ext_sf_index != cfg->sf_index && (cfg->sf_index < 3 || cfg->ext_sf_index + 3 != cfg->sf_index))
+        return JAAD_ERR_UNSUPPORTED;
     return JAAD_OK;
 }
 
@@ -373,9 +381,11 @@ int sync_ctx(jaad_ctx* ctx)
     return JAAD_OK;
 }
 
+bool sbr_downsampled(const jaad_stream_cfg& c) { return c.sbr && c.ext_sf_index == c.sf_index; }
+
 size_t pcm_bytes_per_frame(const jaad_ctx* ctx, uint32_t flags)
 {
-    return (size_t)(ctx->cfg.sbr ? 2048 : 1024) * 2 * ((flags & JAAD_PCM_FLOAT32) ? 4 : 2);
+    return jaad_frame_pcm_bytes(&ctx->cfg, flags);
 }
 
 // slots a call does not touch keep their state: carry them into the other parity buffer
@@ -654,6 +664,9 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
     a.qmf_c = ctx->d_sbr_const;
     a.dct = ctx->d_sbr_const + 640;
     a.noise = ctx->d_sbr_const + 640 + 224;
+    a.down = sbr_downsampled(ctx->cfg) ? 1 : 0;
+    a.tw32 = ctx->d_sbr_const + kSbrConstTw32;
+    a.dct32 = reinterpret_cast<const double*>(ctx->d_sbr_const + kSbrConstDct32);
     a.n_cf = (uint32_t)ncf;
     a.n_chunks = (uint32_t)ctx->sbr_chunks.size();
     a.n_last = (uint32_t)ctx->sbr_last.size();
@@ -745,7 +758,7 @@ extern "C" {
 int jaad_cfg_sample_length(const jaad_stream_cfg* cfg)
 {
     // frameLengthFlag = 0; doubled by upsampling SBR (A/DecoderConfig.java:83-86)
-    return cfg && cfg->sbr ? 2048 : 1024;
+    return cfg && cfg->sbr && cfg->ext_sf_index != cfg->sf_index ? 2048 : 1024;
 }
 
 int jaad_cfg_channel_count(const jaad_stream_cfg* cfg)
@@ -870,12 +883,25 @@ int jaad_ctx_create(const jaad_stream_cfg* cfg, uint32_t n_slots, int device, ja
         const size_t sb = (size_t)n_slots * 2 * sizeof(SbrChState);
         if ((e = hipMalloc(&ctx->d_sbr_state, sb)) != hipSuccess) return bail(e, "hipMalloc sbr state");
         if ((e = hipMemset(ctx->d_sbr_state, 0, sb)) != hipSuccess) return bail(e, "hipMemset sbr state");
-        std::vector<float> k(640 + 224 + 1024);
+        std::vector<float> k(kSbrConstDct32 + 2 * 2 * 32 * 32);
         std::memcpy(k.data(), JAAD_QMF_C, sizeof(JAAD_QMF_C));
         std::memcpy(k.data() + 640, JAAD_DCT4_64_TAB, sizeof(JAAD_DCT4_64_TAB));
         std::memcpy(k.data() + 640 + 192, JAAD_DCT_W_RE, sizeof(JAAD_DCT_W_RE));
         std::memcpy(k.data() + 640 + 208, JAAD_DCT_W_IM, sizeof(JAAD_DCT_W_IM));
         std::memcpy(k.data() + 640 + 224, JAAD_SBR_NOISE_TABLE, sizeof(JAAD_SBR_NOISE_TABLE));
+        // downsampled synthesis: qmf32_pre_twiddle (A/sbr/SynthesisFilterbank32.java:5-38) as
+        // (float) cos / -sin of pi(2k+1)/256, and the 32-point DCT-IV / DST-IV rows in double
+        for (int q = 0; q < 32; q++) {
+            k[kSbrConstTw32 + 2 * q] = (float)std::cos(M_PI * (2 * q + 1) / 256.0);
+            k[kSbrConstTw32 + 2 * q + 1] = -(float)std::sin(M_PI * (2 * q + 1) / 256.0);
+        }
+        double* d32 = reinterpret_cast<double*>(k.data() + kSbrConstDct32);
+        for (int h = 0; h < 2; h++)
+            for (int r = 0; r < 32; r++)
+                for (int n = 0; n < 32; n++) {
+                    const double ph = M_PI / 128.0 * (double)((2 * n + 1) * (2 * r + 1));
+                    d32[(h * 32 + r) * 32 + n] = h ? std::sin(ph) : std::cos(ph);
+                }
         if ((e = hipMalloc(&ctx->d_sbr_const, k.size() * sizeof(float))) != hipSuccess) return bail(e, "hipMalloc sbr const");
         if ((e = hipMemcpy(ctx->d_sbr_const, k.data(), k.size() * sizeof(float), hipMemcpyHostToDevice)) != hipSuccess)
             return bail(e, "hipMemcpy sbr const");

@@ -139,6 +139,10 @@ struct SbrArgs {
     const float* noise;         // NOISE_TABLE [512][2]
     const float* qmf_c;         // [640]
     const float* dct;           // dct4_64_tab [192] + w_re [16] + w_im [16]
+    // downsampled SBR (extension rate = core rate): 32-band synthesis, 1024 samples per frame
+    int down;
+    const float* tw32;          // qmf32_pre_twiddle [32][2] (cos, -sin of pi(2k+1)/256)
+    const double* dct32;        // [2][32][32]: cos / sin (pi(2n+1)(2k+1)/128), row k
     uint32_t n_cf, n_chunks, n_last;
     int nch;
     uint32_t out_mode;          // JAAD_PCM_*

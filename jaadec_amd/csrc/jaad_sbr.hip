@@ -793,9 +793,15 @@ __global__ __launch_bounds__(256) void sbr_hf_kernel(SbrArgs A)
 // ---------------------------------------------------------------------------------------------
 // SynthesisFilterbank64.synthesis (A/sbr/SynthesisFilterbank64.java:9-79) + SampleBuffer PCM
 // ---------------------------------------------------------------------------------------------
+// kDown: SynthesisFilterbank32 (downsampled SBR, A/sbr/SynthesisFilterbank32.java:44-93), bands
+// 0..31, 32 samples per slot.  Its DCT-IV / DST-IV are evaluated as double sums over host-built
+// double coefficients (the reference's generated DCT4_32 / DST4_32 are not restated, so this path
+// matches the oracle's restatement bit for bit and the reference within +-1 LSB; jaad_oracle_sbr.c).
+template <bool kDown>
 __global__ __launch_bounds__(256) void sbr_synthesis_kernel(SbrArgs A)
 {
     __shared__ float vring_s[kWavesPerBlock][10][128];
+    __shared__ float xin_s[kWavesPerBlock][64];
     const int wave = threadIdx.x >> 6;
     const uint32_t ci = blockIdx.x * kWavesPerBlock + wave;
     if (ci >= A.n_chunks) return;
@@ -811,12 +817,75 @@ __global__ __launch_bounds__(256) void sbr_synthesis_kernel(SbrArgs A)
     const DctConst K = load_dct_const(A.dct, e, E);
     float cw[10];
 #pragma unroll
-    for (int t = 0; t < 10; t++) cw[t] = A.qmf_c[u + 64 * t];
+    for (int t = 0; t < 10; t++) cw[t] = kDown ? A.qmf_c[64 * t + 2 * e] : A.qmf_c[u + 64 * t];
     const float scale = 1.f / 64.f;
     int vpos = 0;
+    // downsampled: pre-twiddle of band e and lane (half, e)'s row of the DCT-IV (half 0) / DST-IV
+    // (half 1) matrix, output element e
+    float tw_c = 0.0f, tw_s = 0.0f;
+    double cm[kDown ? 32 : 1];
+    if constexpr (kDown) {
+        tw_c = A.tw32[2 * e];
+        tw_s = A.tw32[2 * e + 1];
+#pragma unroll
+        for (int n = 0; n < 32; n++) cm[n] = A.dct32[(half * 32 + e) * 32 + n];
+    }
+    float* xin = xin_s[wave];
+
+    auto store_pcm = [&](float out, size_t n, bool dup) {
+        if (A.out_mode & JAAD_PCM_FLOAT32) {
+            float* o = reinterpret_cast<float*>(A.pcm) + 2 * n;
+            if ((nch == 2 || ps) && !dup) o[c] = out;
+            else o[0] = o[1] = out;
+        } else {
+            uint32_t s16 = (uint32_t)(uint16_t)(int16_t)java_round16(out);
+            if (!(A.out_mode & JAAD_PCM_LITTLE_ENDIAN)) s16 = ((s16 & 0xFF) << 8) | (s16 >> 8);
+            uint16_t* o = reinterpret_cast<uint16_t*>(A.pcm) + 2 * n;
+            if ((nch == 2 || ps) && !dup) o[c] = (uint16_t)s16;
+            else o[0] = o[1] = (uint16_t)s16;
+        }
+    };
+
+    // downsampled slot (:50-92): pre-twiddle, DCT-IV / DST-IV, v block of 64, 32 windowed outputs
+    auto slot32 = [&](float Xr, float Xi, bool emit, size_t n0, bool dup) {
+        const float xr = shfl(Xr, e), xi = shfl(Xi, e);  // X[l][e]
+        float x1 = (xr * tw_c) - (xi * tw_s);
+        float x2 = (xi * tw_c) + (xr * tw_s);
+        x1 *= scale;
+        x2 *= scale;
+        xin[u] = half ? x2 : x1;
+        wave_sync();
+        double acc = 0.0;
+#pragma unroll
+        for (int n = 0; n < 32; n++) acc = acc + ((double)xin[half * 32 + n] * cm[n]);
+        const float y = (float)acc;          // half 0: DCT-IV(x1)[e], half 1: DST-IV(x2)[e]
+        const float o = shfl(y, u ^ 32);     // the other transform's element e
+        float* vb = vring[vpos];
+        if (!half) vb[e] = -y + o;           // v[n] = -x1[n] + x2[n]
+        else vb[63 - e] = o + y;             // v[63 - n] = x1[n] + x2[n]
+        wave_sync();
+        if (emit && !half) {
+            const float* v0 = vring[vpos];
+            const float* v1 = vring[(vpos + 9) % 10];
+            const float* v2 = vring[(vpos + 8) % 10];
+            const float* v3 = vring[(vpos + 7) % 10];
+            const float* v4 = vring[(vpos + 6) % 10];
+            const float* v5 = vring[(vpos + 5) % 10];
+            const float* v6 = vring[(vpos + 4) % 10];
+            const float* v7 = vring[(vpos + 3) % 10];
+            const float* v8 = vring[(vpos + 2) % 10];
+            const float* v9 = vring[(vpos + 1) % 10];
+            const float out = (v0[e] * cw[0]) + (v1[32 + e] * cw[1]) + (v2[e] * cw[2]) + (v3[32 + e] * cw[3]) +
+                              (v4[e] * cw[4]) + (v5[32 + e] * cw[5]) + (v6[e] * cw[6]) + (v7[32 + e] * cw[7]) +
+                              (v8[e] * cw[8]) + (v9[32 + e] * cw[9]);
+            store_pcm(out, n0 + e, dup);
+        }
+        wave_sync();
+        vpos = vpos == 9 ? 0 : vpos + 1;
+    };
 
     // one slot: DCT-IV pair -> v block (:99-129); emit: window (:134-146) + PCM
-    auto slot = [&](float Xr, float Xi, bool emit, size_t n0, bool dup = false) {
+    auto slot64 = [&](float Xr, float Xi, bool emit, size_t n0, bool dup) {
         // DCT inputs: d = 0: real parts (in_real1[e] = X[2e], in_imag1[e] = X[63-2e]);
         //             d = 1: imag parts (in_real2[e] = X[63-2e], in_imag2[e] = X[2e])
         const float ar = shfl(Xr, 2 * e), br = shfl(Xr, 63 - 2 * e);
@@ -851,21 +920,16 @@ __global__ __launch_bounds__(256) void sbr_synthesis_kernel(SbrArgs A)
             const float out = (v0[u] * cw[0]) + (v1[64 + u] * cw[1]) + (v2[u] * cw[2]) + (v3[64 + u] * cw[3]) +
                               (v4[u] * cw[4]) + (v5[64 + u] * cw[5]) + (v6[u] * cw[6]) + (v7[64 + u] * cw[7]) +
                               (v8[u] * cw[8]) + (v9[64 + u] * cw[9]);
-            const size_t n = n0 + u;
-            if (A.out_mode & JAAD_PCM_FLOAT32) {
-                float* o = reinterpret_cast<float*>(A.pcm) + 2 * n;
-                if ((nch == 2 || ps) && !dup) o[c] = out;
-                else o[0] = o[1] = out;
-            } else {
-                uint32_t s16 = (uint32_t)(uint16_t)(int16_t)java_round16(out);
-                if (!(A.out_mode & JAAD_PCM_LITTLE_ENDIAN)) s16 = ((s16 & 0xFF) << 8) | (s16 >> 8);
-                uint16_t* o = reinterpret_cast<uint16_t*>(A.pcm) + 2 * n;
-                if ((nch == 2 || ps) && !dup) o[c] = (uint16_t)s16;
-                else o[0] = o[1] = (uint16_t)s16;
-            }
+            store_pcm(out, n0 + u, dup);
         }
         wave_sync();
         vpos = vpos == 9 ? 0 : vpos + 1;
+    };
+
+    const size_t spf = kDown ? 1024 : 2048, sps = kDown ? 32 : 64;  // output samples per frame / slot
+    auto slot = [&](float Xr, float Xi, bool emit, size_t n0, bool dup = false) {
+        if constexpr (kDown) slot32(Xr, Xi, emit, n0, dup);
+        else slot64(Xr, Xi, emit, n0, dup);
     };
 
     // v history: slots 23..31 of the frame before the chunk
@@ -894,7 +958,7 @@ __global__ __launch_bounds__(256) void sbr_synthesis_kernel(SbrArgs A)
             const float2* xq = reinterpret_cast<const float2*>(A.xps + ((size_t)f * 2 + c) * 4096);
             for (int l = 0; l < 32; l++) {
                 const float2 v = xq[l * 64 + u];
-                slot(v.x, v.y, true, (size_t)f * 2048 + 64 * l, !ps_on);
+                slot(v.x, v.y, true, (size_t)f * spf + sps * l, !ps_on);
             }
             continue;
         }
@@ -912,7 +976,7 @@ __global__ __launch_bounds__(256) void sbr_synthesis_kernel(SbrArgs A)
             } else {
                 v = xs[l * 64 + u];
             }
-            slot(v.x, v.y, true, (size_t)f * 2048 + 64 * l);
+            slot(v.x, v.y, true, (size_t)f * spf + sps * l);
         }
     }
 }
@@ -974,9 +1038,11 @@ hipError_t launch_sbr(const SbrArgs& a, hipStream_t stream)
         const hipError_t e = launch_ps(a, stream);
         if (e != hipSuccess) return e;
     }
-    if (a.n_chunks)
-        hipLaunchKernelGGL(sbr_synthesis_kernel, dim3((a.n_chunks + kWavesPerBlock - 1) / kWavesPerBlock), blk, 0,
-                           stream, a);
+    if (a.n_chunks) {
+        const dim3 g((a.n_chunks + kWavesPerBlock - 1) / kWavesPerBlock);
+        if (a.down) hipLaunchKernelGGL(sbr_synthesis_kernel<true>, g, blk, 0, stream, a);
+        else hipLaunchKernelGGL(sbr_synthesis_kernel<false>, g, blk, 0, stream, a);
+    }
     if (a.n_last)
         hipLaunchKernelGGL(sbr_state_kernel, dim3((a.n_last + kWavesPerBlock - 1) / kWavesPerBlock), blk, 0, stream, a);
     return hipGetLastError();

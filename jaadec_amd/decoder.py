@@ -62,7 +62,8 @@ class DecoderConfig:
         return 2  # mono -> stereo while sbrEnabled (A/DecoderConfig.java:108-115)
 
     def getSampleLength(self) -> int:  # noqa: N802
-        return 2048 if self.sbr else 1024  # A/DecoderConfig.java:83-86 (upsampled SBR)
+        # A/DecoderConfig.java:83-86: doubled only by upsampling SBR (not downsampled SBR)
+        return 2048 if self.sbr and self.ext_sf_index != self.sf_index else 1024
 
     def getSampleFrequency(self) -> int:  # noqa: N802
         return SAMPLE_FREQUENCIES[self.sf_index]
@@ -71,7 +72,8 @@ class DecoderConfig:
         return SAMPLE_FREQUENCIES[self.ext_sf_index] if self.sbr else self.getSampleFrequency()
 
     def cfg(self) -> N.StreamCfg:
-        return N.make_cfg(self.sf_index, self.channel_config, self.tns_mode, sbr=self.sbr, ps=self.ps)
+        return N.make_cfg(self.sf_index, self.channel_config, self.tns_mode, sbr=self.sbr, ps=self.ps,
+                          down=self.sbr and self.ext_sf_index == self.sf_index)
 
 
 class SampleBuffer:

@@ -280,19 +280,24 @@ def synth_batch(p: SynthParams, with_tns: bool | None = None, threads: int = 0) 
 
 
 def make_cfg(sf_index: int = 3, channel_config: int = 2, tns_mode: int = TNS_COMPAT, sbr: bool = False,
-             ps: bool = False) -> StreamCfg:
-    """jaad_stream_cfg; with sbr the output rate is twice the core rate (index - 3)."""
+             ps: bool = False, down: bool = False) -> StreamCfg:
+    """jaad_stream_cfg; with sbr the output rate is twice the core rate (index - 3), or the core
+    rate itself with down (downsampled SBR: extension rate = core rate)."""
     sbr = sbr or ps
     return StreamCfg(ABI_VERSION, 2, sf_index, channel_config, tns_mode, int(sbr), int(ps),
-                     sf_index - 3 if sbr else 0, 0)
+                     (sf_index if down else sf_index - 3) if sbr else 0, 0)
+
+
+def sbr_downsampled(cfg: StreamCfg) -> bool:
+    return bool(cfg.sbr) and cfg.ext_sf_index == cfg.sf_index
 
 
 def cfg_for(p: SynthParams, tns_mode: int = TNS_COMPAT) -> StreamCfg:
     return make_cfg(p.sf_index, p.channel_config, tns_mode, bool(p.sbr), p.sbr == 2)
 
 
-def pcm_frame_bytes(flags: int, sbr: bool = False) -> int:
-    return (2048 if sbr else 1024) * 2 * (4 if flags & PCM_FLOAT32 else 2)
+def pcm_frame_bytes(flags: int, sbr: bool = False, down: bool = False) -> int:
+    return (2048 if sbr and not down else 1024) * 2 * (4 if flags & PCM_FLOAT32 else 2)
 
 
 class Context:
@@ -327,7 +332,7 @@ class Context:
 
     def decode(self, batch: Batch, flags: int = PCM_BIG_ENDIAN) -> np.ndarray:
         """Host-buffer batch decode -> PCM bytes (uint8 [n_frames, frame_bytes])."""
-        nb = pcm_frame_bytes(flags, bool(self.cfg.sbr))
+        nb = pcm_frame_bytes(flags, bool(self.cfg.sbr), sbr_downsampled(self.cfg))
         out = np.empty((batch.n_frames, nb), np.uint8)
         bs = batch.struct()
         self._check(lib().jaad_decode_batch(self.h, C.byref(bs), _ptr(out), out.nbytes, flags), "jaad_decode_batch")
@@ -408,9 +413,10 @@ def implicit_sbr_cfg(cfg: StreamCfg) -> StreamCfg:
     """The configuration the reference switches to when it meets SBR data in a core stream
     (DecoderConfig.setSBRPresent, A/DecoderConfig.java:124-135): doubled output rate; a mono
     core decodes to stereo (SCE.isStereo) with PS applied when present (psEnabled)."""
-    if cfg.sf_index < 3:
-        raise JaadError(ERR_UNSUPPORTED, "implicit SBR without a doubled rate (downsampled SBR)")
-    return make_cfg(cfg.sf_index, cfg.channel_config, cfg.tns_mode, sbr=True, ps=cfg.channel_config == 1)
+    # no doubled rate above 48 kHz: SampleFrequency.duplicated() is SF_NONE, the SBR runs
+    # downsampled (A/DecoderConfig.java:124-135, A/sbr/SBR.java:100)
+    return make_cfg(cfg.sf_index, cfg.channel_config, cfg.tns_mode, sbr=True, ps=cfg.channel_config == 1,
+                    down=cfg.sf_index < 3)
 
 
 class Parser:

@@ -447,7 +447,9 @@ void orc_streams_free(orc_stream* streams, int n)
     }
 }
 
-static int frame_samples(const jaad_stream_cfg* cfg) { return cfg->sbr ? 2048 : 1024; }
+/* SBR doubles the output rate unless it runs downsampled (extension rate = core rate) */
+static int sbr_down(const jaad_stream_cfg* cfg) { return cfg->sbr && cfg->ext_sf_index == cfg->sf_index; }
+static int frame_samples(const jaad_stream_cfg* cfg) { return cfg->sbr && !sbr_down(cfg) ? 2048 : 1024; }
 
 static int decode_frame(const jaad_stream_cfg* cfg, orc_stream* st, const jaad_batch* b, uint32_t f,
                         uint32_t* rand_state, unsigned char* pcm, uint32_t flags)
@@ -486,12 +488,13 @@ static int decode_frame(const jaad_stream_cfg* cfg, orc_stream* st, const jaad_b
             st->sbr = (orc_sbr*)calloc(1, orc_sbr_bytes());
             if (!st->sbr) return JAAD_ERR_NOMEM;
             orc_sbr_init(st->sbr, cfg->ext_sf_index);
+            orc_sbr_set_downsampled(st->sbr, sbr_down(cfg));
         }
         rc = orc_sbr_decode(st->sbr, &b->sbr[f], nch);
         if (rc) return rc;
         orc_sbr_process(st->sbr, data[0], data[1], nch);
         const float* chans[2] = {data[0], data[1]};
-        orc_pcm_pack(chans, 2, 2048, flags, pcm);
+        orc_pcm_pack(chans, 2, frame_samples(cfg), flags, pcm);
         return JAAD_OK;
     }
     const float* chans[2] = {data[0], nch == 2 ? data[1] : data[0]};
@@ -503,7 +506,7 @@ static int check_batch(const jaad_stream_cfg* cfg, const jaad_batch* b, size_t p
 {
     if (!cfg || !b || (!b->q && b->n_frames) || !b->sf || !b->cb || !b->ics || !b->frame_begin) return JAAD_ERR_INVALID_ARG;
     if (cfg->channel_config != 1 && cfg->channel_config != 2) return JAAD_ERR_UNSUPPORTED;
-    if (cfg->sbr && (!b->sbr || cfg->ext_sf_index + 3 != cfg->sf_index)) return JAAD_ERR_INVALID_ARG;
+    if (cfg->sbr && (!b->sbr || (cfg->ext_sf_index + 3 != cfg->sf_index && !sbr_down(cfg)))) return JAAD_ERR_INVALID_ARG;
     if (cfg->ps && (!cfg->sbr || cfg->channel_config != 1)) return JAAD_ERR_UNSUPPORTED;
     size_t per = (size_t)frame_samples(cfg) * 2 * ((flags & JAAD_PCM_FLOAT32) ? 4 : 2);
     if (pcm_bytes < per * b->n_frames) return JAAD_ERR_INVALID_ARG;

@@ -74,6 +74,10 @@ void orc_sbr_init(orc_sbr* s, int out_sf_index);
 int orc_sbr_decode(orc_sbr* s, const jaad_sbr_frame* fr, int nch);
 /* SBR2.process / SBR1.process (no PS): 2048-float channel buffers, first 1024 = core output */
 void orc_sbr_process(orc_sbr* s, float* left, float* right, int nch);
+/* SBR.downSampled (extension rate = core rate): 32-band synthesis, 1024 samples per channel */
+void orc_sbr_set_downsampled(orc_sbr* s, int down);
+/* SynthesisFilterbank32.synthesis over one frame: X[32][64][2] (bands < 32) -> 1024 samples */
+void orc_qmf_synthesis32_frame(float* v1280, int* v_index, const float* X, float* output1024);
 /* DCT.dct4_kernel (A/sbr/DCT.java:347-391) on copies of the inputs */
 void orc_sbr_dct4(const float* in_re, const float* in_im, float* out_re, float* out_im);
 /* AnalysisFilterbank.sbr_qmf_analysis_32 over one frame: X[32][64][2] */

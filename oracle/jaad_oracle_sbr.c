@@ -17,6 +17,10 @@
 
 #include "../jaadec_amd/csrc/tables/jaad_sbr_tables.inc"
 
+#ifndef M_PI
+#define M_PI 3.14159265358979323846
+#endif
+
 #if defined(__FP_FAST_FMAF) || defined(__FAST_MATH__)
 #error "the oracle must be compiled without fast-math / FMA contraction"
 #endif
@@ -52,6 +56,7 @@ typedef struct orc_sbr_channel {
 
 struct orc_sbr {
     int out_sf_index; /* SBR.sample_rate (output frequency, A/sbr/SBR.java:102) */
+    int down;         /* SBR.downSampled: 32-band synthesis, core-rate output (A/sbr/SBR.java:35-37,100) */
     int k0, kx, M, N_master, N_high, N_low, N_Q, N_L[4], n[2];
     int f_master[64], f_table_res[2][64], f_table_noise[64], f_table_lim[4][64], table_map_k_to_g[64];
     int kx_prev, bsco, bsco_prev, M_prev;
@@ -69,12 +74,21 @@ struct orc_sbr {
     int qmfs1_index;
 };
 
+static void qmf_synthesis(float* v, int* v_index, float (*X)[64][2], float* output);
+static void qmf_synthesis32(float* v, int* v_index, float (*X)[64][2], float* output);
 size_t orc_sbr_bytes(void) { return sizeof(orc_sbr); }
+
+static void synthesis(const orc_sbr* s, float* v, int* v_index, float (*X)[64][2], float* output)
+{
+    if (s->down) qmf_synthesis32(v, v_index, X, output);
+    else qmf_synthesis(v, v_index, X, output);
+}
 
 void orc_sbr_init(orc_sbr* s, int out_sf_index)
 {
     memset(s, 0, sizeof *s);
     s->out_sf_index = out_sf_index;
+    s->down = 0;
     for (int c = 0; c < 2; c++) s->ch[c].prevEnvIsShort = -1; /* A/sbr/Channel.java:59 */
 }
 
@@ -291,6 +305,72 @@ static void qmf_synthesis(float* v, int* v_index, float (*X)[64][2], float* outp
         *v_index -= 128;
         if (*v_index < 0) *v_index = 1280 - 128;
     }
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* SynthesisFilterbank32.synthesis (A/sbr/SynthesisFilterbank32.java:44-93): downsampled SBR    */
+/* ------------------------------------------------------------------------------------------ */
+/* PARITY UNPINNED in the transform: the reference's DCT4_32 / DST4_32 (:95-940) are machine-
+ * generated fast factorisations of the 32-point DCT-IV y[k] = sum x[n] cos(pi(2n+1)(2k+1)/128) and
+ * DST-IV (sin); their identity was read off their structure (the final rotations by (2k+1)pi/128
+ * and the 1/(2 sin((2k+1)pi/128)) output scales), not executed.  Here both are evaluated as double
+ * sums of the float inputs, rounded once to float; the pre-twiddle, scale, v ring and the
+ * 10-tap window keep the reference's binary32 order.  Expected distance to the reference: a few
+ * ulp in v, i.e. PCM within +-1 LSB (the metric's tolerance).  The structure (signs, twiddle,
+ * ring taps) is pinned by the analysis -> synthesis reconstruction test (tests/test_sbr_oracle.py). */
+static void dct4_dst4_32(const float* x1, const float* x2, float* c1, float* s2)
+{
+    for (int k = 0; k < 32; k++) {
+        double a = 0.0, b = 0.0;
+        for (int n = 0; n < 32; n++) {
+            const double ph = M_PI / 128.0 * (double)((2 * n + 1) * (2 * k + 1));
+            a += (double)x1[n] * cos(ph);
+            b += (double)x2[n] * sin(ph);
+        }
+        c1[k] = (float)a;
+        s2[k] = (float)b;
+    }
+}
+
+static void qmf_synthesis32(float* v, int* v_index, float (*X)[64][2], float* output)
+{
+    const float scale = 1.f / 64.f;
+    float x1[32], x2[32], c1[32], s2[32];
+    int out = 0;
+    for (int l = 0; l < 32; l++) {
+        for (int k = 0; k < 32; k++) {
+            /* qmf32_pre_twiddle[k] = (cos, -sin) of pi(2k+1)/256 as float */
+            const float tc = (float)cos(M_PI * (2 * k + 1) / 256.0), ts = -(float)sin(M_PI * (2 * k + 1) / 256.0);
+            x1[k] = (X[l][k][0] * tc) - (X[l][k][1] * ts);
+            x2[k] = (X[l][k][1] * tc) + (X[l][k][0] * ts);
+            x1[k] *= scale;
+            x2[k] *= scale;
+        }
+        dct4_dst4_32(x1, x2, c1, s2);
+        const int vi = *v_index;
+        for (int n = 0; n < 32; n++) {
+            v[vi + n] = v[vi + 640 + n] = -c1[n] + s2[n];
+            v[vi + 63 - n] = v[vi + 640 + 63 - n] = c1[n] + s2[n];
+        }
+        const float* w = v + vi;
+        for (int k = 0; k < 32; k++) {
+            output[out++] = (w[k] * JAAD_QMF_C[2 * k]) + (w[96 + k] * JAAD_QMF_C[64 + 2 * k]) +
+                            (w[128 + k] * JAAD_QMF_C[128 + 2 * k]) + (w[224 + k] * JAAD_QMF_C[192 + 2 * k]) +
+                            (w[256 + k] * JAAD_QMF_C[256 + 2 * k]) + (w[352 + k] * JAAD_QMF_C[320 + 2 * k]) +
+                            (w[384 + k] * JAAD_QMF_C[384 + 2 * k]) + (w[480 + k] * JAAD_QMF_C[448 + 2 * k]) +
+                            (w[512 + k] * JAAD_QMF_C[512 + 2 * k]) + (w[608 + k] * JAAD_QMF_C[576 + 2 * k]);
+        }
+        *v_index -= 64;
+        if (*v_index < 0) *v_index = 640 - 64;
+    }
+}
+
+/* one frame of the downsampled synthesis with an explicit ring (tests): X[32][64][2] -> 1024 */
+void orc_qmf_synthesis32_frame(float* v1280, int* v_index, const float* X, float* output1024)
+{
+    float tmp[32][64][2];
+    memcpy(tmp, X, sizeof tmp);
+    qmf_synthesis32(v1280, v_index, tmp, output1024);
 }
 
 void orc_qmf_synthesis_frame(float* v2560, int* v_index, const float* X, float* output2048)
@@ -1186,8 +1266,8 @@ static void process_ps(orc_sbr* s, float* left, float* right)
             Xl[l][k][1] = s->ch[0].Xsbr[T_HFADJ + l][k][1];
         }
     orc_ps_process(s->ps, Xl, Xr);
-    qmf_synthesis(s->ch[0].qmfs_v, &s->ch[0].qmfs_index, Xl, left);
-    qmf_synthesis(s->qmfs1_v, &s->qmfs1_index, Xr, right);
+    synthesis(s, s->ch[0].qmfs_v, &s->ch[0].qmfs_index, Xl, left);
+    synthesis(s, s->qmfs1_v, &s->qmfs1_index, Xr, right);
     if (s->have_hdr) sbr_save_prev_data(s, &s->ch[0]);
     sbr_save_matrix(&s->ch[0]);
     s->frame++;
@@ -1201,18 +1281,20 @@ void orc_sbr_process(orc_sbr* s, float* left, float* right, int nch)
     }
     float Xl[MAX_NTSR][64][2];
     process_channel(s, &s->ch[0], left, Xl, s->reset);
-    qmf_synthesis(s->ch[0].qmfs_v, &s->ch[0].qmfs_index, Xl, left);
+    synthesis(s, s->ch[0].qmfs_v, &s->ch[0].qmfs_index, Xl, left);
     if (nch == 2) {
         process_channel(s, &s->ch[1], right, Xl, 0);
-        qmf_synthesis(s->ch[1].qmfs_v, &s->ch[1].qmfs_index, Xl, right);
+        synthesis(s, s->ch[1].qmfs_v, &s->ch[1].qmfs_index, Xl, right);
     }
     if (s->have_hdr) {
         for (int c = 0; c < nch; c++) sbr_save_prev_data(s, &s->ch[c]);
     }
     for (int c = 0; c < nch; c++) sbr_save_matrix(&s->ch[c]);
     s->frame++;
-    if (nch == 1) memcpy(right, left, 2048 * sizeof(float));
+    if (nch == 1) memcpy(right, left, (s->down ? 1024 : 2048) * sizeof(float));
 }
+
+void orc_sbr_set_downsampled(orc_sbr* s, int down) { s->down = down != 0; }
 
 /* derived tables of the current header (tests): k0 k2 kx M N_master N_high N_low N_Q noPatches */
 int orc_sbr_table_info(const jaad_sbr_header* h, int out_sf_index, int* info, int* f_master, int* f_table_lim)

@@ -44,6 +44,8 @@ def lib() -> C.CDLL:
         L.orc_qmf_analysis_frame.restype = None
         L.orc_qmf_synthesis_frame.argtypes = [C.c_void_p] * 4
         L.orc_qmf_synthesis_frame.restype = None
+        L.orc_qmf_synthesis32_frame.argtypes = [C.c_void_p] * 4
+        L.orc_qmf_synthesis32_frame.restype = None
         L.orc_sbr_table_info.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
         L.jaad_write_frame.argtypes = [C.c_int, C.c_int] + [C.c_void_p] * 6 + [C.c_int, C.c_void_p, C.c_size_t]
         L.jaad_write_frame.restype = C.c_long
@@ -121,6 +123,20 @@ class QmfSynthesis:
         X = np.ascontiguousarray(X, np.float32)
         out = np.empty(2048, np.float32)
         lib().orc_qmf_synthesis_frame(self.v.ctypes.data, self.idx.ctypes.data, X.ctypes.data, out.ctypes.data)
+        return out
+
+
+class QmfSynthesis32:
+    """SynthesisFilterbank32 state (v[1280] double ring + index): downsampled SBR."""
+
+    def __init__(self):
+        self.v = np.zeros(1280, np.float32)
+        self.idx = np.zeros(1, np.int32)
+
+    def frame(self, X: np.ndarray) -> np.ndarray:
+        X = np.ascontiguousarray(X, np.float32)
+        out = np.empty(1024, np.float32)
+        lib().orc_qmf_synthesis32_frame(self.v.ctypes.data, self.idx.ctypes.data, X.ctypes.data, out.ctypes.data)
         return out
 
 
@@ -209,7 +225,8 @@ class Streams:
 
 def decode_batch(cfg, batch, streams: Streams, flags: int = 0, threads: int = 1) -> np.ndarray:
     """Decode a jaadec_amd.native.Batch on the CPU restatement; returns uint8 [n_frames, bytes]."""
-    nb = (2048 if cfg.sbr else 1024) * 2 * (4 if flags & 2 else 2)
+    down = cfg.sbr and cfg.ext_sf_index == cfg.sf_index  # downsampled SBR: core-rate output
+    nb = (2048 if cfg.sbr and not down else 1024) * 2 * (4 if flags & 2 else 2)
     out = np.empty((batch.n_frames, nb), np.uint8)
     bs = batch.struct()
     if threads == 1:

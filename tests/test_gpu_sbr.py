@@ -137,3 +137,17 @@ def test_c4_single_frame_runs_and_empty_runs():
     for k in range(9):
         for r in range(4):
             assert np.array_equal(out[k][r], want[fb[r] + k])
+
+
+@pytest.mark.parametrize("cfgid,flags", [(4, N.PCM_BIG_ENDIAN), (4, N.PCM_FLOAT32), (5, N.PCM_LITTLE_ENDIAN),
+                                         (5, N.PCM_FLOAT32)])
+def test_downsampled_sbr(cfgid, flags):
+    """Downsampled SBR (a15': extension rate = core rate, SynthesisFilterbank32): 1024 samples per
+    frame at the core rate; GPU == the oracle's restatement bit for bit (both evaluate the 32-point
+    DCT-IV / DST-IV as the same double sums; to the reference itself +-1 LSB, see jaad_oracle_sbr.c)."""
+    p = N.synth_params(cfgid, n_streams=3, frames_per_stream=36)
+    b = N.synth_batch(p)
+    cfg = N.make_cfg(p.sf_index, p.channel_config, sbr=True, ps=p.sbr == 2, down=True)
+    got, want = _decode_both(p, b, flags, cfg)
+    assert got.shape == (b.n_frames, 4096 * (2 if flags & N.PCM_FLOAT32 else 1))
+    _assert_same(got, want, flags)

@@ -298,9 +298,9 @@ def test_implicit_sbr_probe_and_upgraded_config():
         P.pns_state = int(b.ics["pns_state"][0])
         got = P.parse(sbr_frames)
         _assert_sbr_equal(got.sbr, b.sbr, b.nch, up.ext_sf_index)
-    with pytest.raises(N.JaadError) as e:  # 64 kHz core: no doubled rate (downsampled SBR)
-        N.implicit_sbr_cfg(N.make_cfg(2, 2))
-    assert e.value.status == N.ERR_UNSUPPORTED
+    # 64 kHz core: no doubled rate, the SBR runs downsampled at the core rate
+    down = N.implicit_sbr_cfg(N.make_cfg(2, 2))
+    assert (down.sbr, down.ext_sf_index) == (1, 2) and N.sbr_downsampled(down)
     # explicit AOT 5 mono: PS stays enabled, as psEnabled is by default
     cfg = N.asc_parse(bytes([0x2B, 0x09, 0x88, 0x00]))
     assert (cfg.sbr, cfg.ps, cfg.channel_config) == (1, 1, 1)
