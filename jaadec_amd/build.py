@@ -51,7 +51,7 @@ def build_gpu(force: bool = False, out: Path | None = None, defines: list[str] |
     """Build the product library (or, with `defines`, an experimental variant at `out`)."""
     out = out or LIB
     srcs = [CSRC / "jaad_lc.hip", CSRC / "jaad_sbr.hip", CSRC / "jaad_ps.hip", CSRC / "jaad_capi.cpp", CSRC / "jaad_sbr_host.cpp",
-            CSRC / "jaad_parse.cpp", CSRC / "jaad_parse_sbr.cpp"]
+            CSRC / "jaad_parse.cpp", CSRC / "jaad_parse_sbr.cpp", CSRC / "jaad_mp4.cpp"]
     deps = srcs + _deps("jaadec_amd/csrc/*.h", "jaadec_amd/csrc/tables/*.inc", "include/*.h")
     if force or defines or extra or _stale(out, deps):
         tmp = out.with_suffix(".so.tmp")

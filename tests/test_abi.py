@@ -25,6 +25,16 @@ def test_library_exports_every_header_symbol():
         assert hasattr(lib, name), name
 
 
+@pytest.mark.parametrize("header", ["jaad_parse.h", "jaad_mp4.h"])
+def test_library_exports_the_front_end_headers(header):
+    """The host front end (bitstream parser, MP4 feeder) lives in the same library."""
+    lib = N.lib()
+    declared = header_functions(ROOT / "include" / header)
+    assert declared
+    for name in declared:
+        assert hasattr(lib, name), name
+
+
 def test_exported_dynamic_symbols_with_nm():
     out = subprocess.run(["nm", "-D", "--defined-only", str(N.LIB_PATH)], capture_output=True, text=True).stdout
     syms = {line.split()[-1] for line in out.splitlines() if line.strip()}
@@ -51,6 +61,10 @@ def test_config_queries_mirror_decoderconfig():
     assert L.jaad_cfg_channel_count(C.byref(cfg)) == 2  # mono -> stereo while sbrEnabled
     assert L.jaad_frame_pcm_bytes(C.byref(cfg), N.PCM_BIG_ENDIAN) == 4096
     assert L.jaad_frame_pcm_bytes(C.byref(cfg), N.PCM_FLOAT32) == 8192
+    up = N.make_cfg(sf_index=6, channel_config=2, sbr=True)
+    down = N.make_cfg(sf_index=6, channel_config=2, sbr=True, down=True)
+    assert L.jaad_cfg_sample_length(C.byref(up)) == 2048   # upsampling SBR doubles the length
+    assert L.jaad_cfg_sample_length(C.byref(down)) == 1024  # downsampled SBR keeps the core rate
 
 
 @pytest.mark.parametrize("fields,status", [
