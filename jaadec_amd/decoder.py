@@ -17,13 +17,26 @@ Errors surface as ``AACException`` (the JNI glue maps every nonzero jaad_status 
 """
 from __future__ import annotations
 
+import logging
+from collections import namedtuple
+
 import numpy as np
 
 from . import native as N
 
+LOGGER = logging.getLogger("jaad.aac.Decoder")
+
 
 class AACException(RuntimeError):
     """A/AACException.java"""
+
+
+class EOSException(AACException):
+    """A/EOSException.java: the frame ended inside a syntax element."""
+
+
+# javax.sound.sampled.AudioFormat fields the reference sets (A/Decoder.java:123-147)
+AudioFormat = namedtuple("AudioFormat", "encoding sample_rate bits channels frame_size frame_rate big_endian")
 
 
 # A/SampleFrequency.java:15-26
@@ -185,7 +198,7 @@ class Decoder:
         try:
             return self._parser.parse(frames, self.slot)
         except N.JaadError as e:
-            raise AACException(str(e)) from e
+            raise (EOSException if e.status == N.ERR_EOS else AACException)(str(e)) from e
 
     def decodeFrames(self, batch, buffers: list[SampleBuffer]) -> None:  # noqa: N802
         """Decode consecutive frames of this stream -- a list of raw_data_blocks or a parsed
@@ -210,9 +223,36 @@ class Decoder:
             buf.setBigEndian(want)  # no-op unless this buffer asked for the other byte order
         self.frames += batch.n_frames
 
-    def decodeFrame(self, frame, buffer: SampleBuffer) -> None:  # noqa: N802
-        """A/Decoder.java:89-101 for one frame (raw_data_block bytes or a parsed Batch)."""
+    def decode0(self, frame, buffer: SampleBuffer) -> None:
+        """A/Decoder.java:103-121: one frame; an EOSException propagates."""
         self.decodeFrames([frame] if isinstance(frame, (bytes, bytearray, memoryview)) else frame, [buffer])
+
+    def decodeFrame(self, frame, buffer: SampleBuffer) -> None:  # noqa: N802
+        """A/Decoder.java:89-101 for one frame (raw_data_block bytes or a parsed Batch): a frame that
+        ends early is logged and dropped -- the buffer keeps the previous frame's PCM -- and still
+        counts as a frame.  (The parser is atomic: unlike the JVM, nothing of its state moved.)"""
+        try:
+            self.decode0(frame, buffer)
+        except EOSException as e:
+            LOGGER.warning("unexpected end of frame: %s", e)
+            self.frames += 1
+
+    def getAudioFormat(self) -> AudioFormat:  # noqa: N802
+        """A/Decoder.java:123-134: 16-bit signed little-endian; a mono core below 24 kHz is assumed
+        to carry SBR/PS (rate doubled), whatever the configuration says."""
+        freq = self.config.getSampleFrequency()
+        if self.config.channel_config == 1 and freq < 24000:
+            freq *= 2
+        ch = self.config.getChannelCount()
+        return AudioFormat("PCM_SIGNED", freq, 16, ch, 2 * ch, freq, False)
+
+    def getAudioFormatFloat(self) -> AudioFormat:  # noqa: N802
+        """A/Decoder.java:136-147"""
+        freq = self.config.getSampleFrequency()
+        if self.config.channel_config == 1 and freq < 24000:
+            freq *= 2
+        ch = self.config.getChannelCount()
+        return AudioFormat("PCM_FLOAT", freq, 32, ch, 4 * ch, freq, False)
 
     def close(self) -> None:
         if self._own:

@@ -134,3 +134,29 @@ def test_decode_raw_frames_from_adts_matches_oracle():
         dec.decodeFrame(demux.readNextFrame(), buf)
         assert buf.getData() == want[i].tobytes()
     dec.close()
+
+
+@pytest.mark.gpu
+def test_truncated_frame_is_dropped_and_the_buffer_keeps_the_last_pcm():
+    """A/Decoder.java:89-101: decodeFrame swallows an EOSException (warning), the Receiver is not
+    called, the frame still counts; decode0 lets it propagate."""
+    from jaadec_amd.decoder import EOSException
+    from oracle import oracle as O
+    p = N.synth_params(2, n_streams=1, frames_per_stream=4)
+    b = N.synth_batch(p)
+    frames = O.write_frames(b, p.sf_index)
+    want = O.decode_batch(N.make_cfg(), b, O.Streams(1), N.PCM_BIG_ENDIAN)
+    dec = Decoder.create(DecoderConfig.decode(bytes([0x11, 0x90])))
+    buf = SampleBuffer()
+    dec.decodeFrame(frames[0], buf)
+    assert buf.getData() == want[0].tobytes()
+    dec.decodeFrame(frames[1][:len(frames[1]) // 2], buf)
+    assert buf.getData() == want[0].tobytes() and dec.frames == 2
+    with pytest.raises(EOSException):
+        dec.decode0(frames[1][:10], buf)
+    # the dropped frame changed nothing: frame 1 decodes as if it came right after frame 0
+    dec.decodeFrame(frames[1], buf)
+    assert buf.getData() == want[1].tobytes()
+    fmt = dec.getAudioFormat()
+    assert (fmt.sample_rate, fmt.bits, fmt.channels, fmt.big_endian) == (48000, 16, 2, False)
+    dec.close()
