@@ -274,6 +274,140 @@ __device__ __forceinline__ void imdct_long_n(float* const (&bufs)[N], const LdsT
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// Packed-FP32 form of the long IMDCT (CDNA v_pk_mul_f32 / v_pk_add_f32: two binary32 results
+// per lane per instruction, each rounded exactly as the scalar operation).  A complex value is
+// one register pair (re, im).  Every Java expression keeps its operands and rounding: a - b is
+// evaluated as a + (-b) (identical in IEEE 754, signed zeros included), products keep their
+// factors, sums their two operands (addition is commutative).  The half-swaps and negations
+// the complex arithmetic needs are VOP3P op_sel / neg modifiers, written as inline asm because
+// the compiler does not fold a partial negation.
+// ------------------------------------------------------------------------------------------
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+// (x.y * -w.y, x.x * w.y)
+__device__ __forceinline__ f2 pk_mul_swap_nlo(f2 x, f2 w)
+{
+    f2 r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,1] op_sel_hi:[0,1] neg_lo:[0,1]" : "=v"(r) : "v"(x), "v"(w));
+    return r;
+}
+// z = x * w (complex): (x.x*w.x - x.y*w.y, x.x*w.y + x.y*w.x), each product rounded, then one sum
+__device__ __forceinline__ f2 cmul(f2 x, f2 w) { return x * w.xx + pk_mul_swap_nlo(x, w); }
+// (c.x - d.y, c.y + d.x)
+__device__ __forceinline__ f2 pk_rot_p(f2 c, f2 d)
+{
+    f2 r;
+    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(c), "v"(d));
+    return r;
+}
+// (c.x + d.y, c.y - d.x)
+__device__ __forceinline__ f2 pk_rot_m(f2 c, f2 d)
+{
+    f2 r;
+    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(c), "v"(d));
+    return r;
+}
+// FFT.java:113-130: z = (r1*wr - i1*wi, r1*wi + i1*wr); b = a - z; a = a + z
+__device__ __forceinline__ void bfly_pk(f2& a, f2& b, f2 w)
+{
+    const f2 z = cmul(b, w);
+    b = a - z;
+    a = a + z;
+}
+// FFT.java:69-108 (inverse)
+__device__ __forceinline__ void radix4_pk(f2& c0, f2& c1, f2& c2, f2& c3)
+{
+    const f2 a = c0 + c1, b = c2 + c3, c = c0 - c1, d = c2 - c3;
+    c0 = a + b;
+    c2 = a - b;
+    c1 = pk_rot_p(c, d);
+    c3 = pk_rot_m(c, d);
+}
+__device__ __forceinline__ f2 ld2(const float (&p)[2]) { return *reinterpret_cast<const f2*>(p); }
+
+__device__ __forceinline__ void fft_pass1_pk(f2 (&c)[8], const float (*w)[2])
+{
+    radix4_pk(c[BR3[0]], c[BR3[1]], c[BR3[2]], c[BR3[3]]);
+    radix4_pk(c[BR3[4]], c[BR3[5]], c[BR3[6]], c[BR3[7]]);
+#pragma unroll
+    for (int k = 0; k < 4; k++) bfly_pk(c[BR3[k]], c[BR3[k + 4]], ld2(w[k]));
+}
+template <typename TW>
+__device__ __forceinline__ void fft_3stages_pk(f2 (&c)[8], TW tw)
+{
+    {
+        const f2 w = tw(0);
+#pragma unroll
+        for (int s = 0; s < 8; s += 2) bfly_pk(c[s], c[s + 1], w);
+    }
+#pragma unroll
+    for (int e = 0; e < 2; e++) {
+        const f2 w = tw(1 + e);
+        bfly_pk(c[e], c[e + 2], w);
+        bfly_pk(c[4 + e], c[6 + e], w);
+    }
+#pragma unroll
+    for (int s = 0; s < 4; s++) bfly_pk(c[s], c[s + 4], tw(3 + s));
+}
+
+// imdct_long_n in packed form: c[n][s] = (re, im) of element u + 64 s after the post-twiddle
+template <int N>
+__device__ __forceinline__ void imdct_long_pk(float* const (&bufs)[N], const LdsTables& T, int u, f2 (&c)[N][8])
+{
+#pragma unroll
+    for (int n = 0; n < N; n++)
+#pragma unroll
+        for (int s = 0; s < 8; s++) {
+            const int k = u + 64 * s;
+            // MDCT.java:39-42: re = in1*c - in0*sn, im = in0*c + in1*sn = cmul((in1, in0), (c, sn))
+            const f2 x = {bufs[n][eo_idx(1023 - 2 * k)], bufs[n][eo_idx(2 * k)]};
+            c[n][s] = cmul(x, ld2(T.mdct_l[k]));
+        }
+    wave_sync();
+    const int t = (int)(__builtin_bitreverse32((uint32_t)u) >> 26);
+    const int x1 = xs_l(8 * t);
+#pragma unroll
+    for (int n = 0; n < N; n++) {
+        fft_pass1_pk(c[n], T.tw1);
+        f2* X = reinterpret_cast<f2*>(bufs[n]);
+#pragma unroll
+        for (int r = 0; r < 8; r++) X[x1 + r] = c[n][BR3[r]];
+    }
+    wave_sync();
+    const int a = u >> 3, b = u & 7;
+    const int x2 = xs_l(64 * a + b);
+#pragma unroll
+    for (int n = 0; n < N; n++) {
+        const f2* X = reinterpret_cast<const f2*>(bufs[n]);
+#pragma unroll
+        for (int s = 0; s < 8; s++) c[n][s] = X[x2 + xs_l(8 * s)];
+    }
+#pragma unroll
+    for (int n = 0; n < N; n++) {
+        fft_3stages_pk(c[n], [&](int j) { return ld2(T.tw2[j][b]); });
+        f2* X = reinterpret_cast<f2*>(bufs[n]);
+#pragma unroll
+        for (int s = 0; s < 8; s++) X[x2 + xs_l(8 * s)] = c[n][s];
+    }
+    wave_sync();
+    const int x3 = xs_l(u);
+#pragma unroll
+    for (int n = 0; n < N; n++) {
+        const f2* X = reinterpret_cast<const f2*>(bufs[n]);
+#pragma unroll
+        for (int s = 0; s < 8; s++) c[n][s] = X[x3 + xs_l(64 * s)];
+    }
+    wave_sync();
+#pragma unroll
+    for (int n = 0; n < N; n++) {
+        fft_3stages_pk(c[n], [&](int j) { return ld2(T.tw3[j][u]); });
+        // MDCT.java:48-53: re = t0*c - t1*sn, im = t1*c + t0*sn = cmul((t0, t1), (c, sn))
+#pragma unroll
+        for (int s = 0; s < 8; s++) c[n][s] = cmul(c[n][s], ld2(T.mdct_l[u + 64 * s]));
+    }
+}
+
 __device__ __forceinline__ void imdct_long(float* buf, const LdsTables& T, int u, float (&re)[8], float (&im)[8])
 {
     float* const bufs[1] = {buf};
@@ -346,6 +480,53 @@ __device__ __forceinline__ void ola_long(const LdsTables& T, int, const FrameCtx
     else if (fc.seq == JAAD_LONG_START_SEQUENCE) ola_long_t<JAAD_LONG_START_SEQUENCE>(T, fc, re, im, ov, out);
     else ola_long_t<JAAD_LONG_STOP_SEQUENCE>(T, fc, re, im, ov, out);
 }
+
+// ONLY_LONG window + overlap-add in packed form (slot pair (2s, 2s+1) of ola_long_t):
+//   out[o] = ov[o] + f_o * W[P_o],  new ov[o] = g * W[1023 - P_o]
+// with (f_0, f_1, g) = (-re, re, -im) for s < 4 and (im, -im, re) for s >= 4
+__device__ __forceinline__ void ola_only_long_pk(const LdsTables& T, const FrameCtx& fc, const f2 (&c)[8],
+                                                 float (&ov)[16], float (&out)[16])
+{
+    const int u = lane_id();
+    const f2* Wp = reinterpret_cast<const f2*>(&T.win_pair[fc.shape_prev][0][0][0]);
+    const f2* Wc = reinterpret_cast<const f2*>(&T.win_pair[fc.shape][0][0][0]);
+#pragma unroll
+    for (int s = 0; s < 8; s++) {
+        const f2 wp = Wp[64 * s + u], wc = Wc[64 * s + u];
+        f2 fw, nv;
+        if (s < 4) {
+            asm("v_pk_mul_f32 %0, %1, %2 op_sel:[0,0] op_sel_hi:[0,1] neg_lo:[1,0]" : "=v"(fw) : "v"(c[s]), "v"(wp));
+            asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,1] op_sel_hi:[1,0] neg_lo:[1,0] neg_hi:[1,0]"
+                : "=v"(nv) : "v"(c[s]), "v"(wc));
+        } else {
+            asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,0] op_sel_hi:[1,1] neg_hi:[1,0]" : "=v"(fw) : "v"(c[s]), "v"(wp));
+            asm("v_pk_mul_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[0,0]" : "=v"(nv) : "v"(c[s]), "v"(wc));
+        }
+        const f2 o = f2{ov[2 * s], ov[2 * s + 1]} + fw;
+        out[2 * s] = o.x;
+        out[2 * s + 1] = o.y;
+        ov[2 * s] = nv.x;
+        ov[2 * s + 1] = nv.y;
+    }
+}
+
+__device__ __forceinline__ void ola_long_pk(const LdsTables& T, const FrameCtx& fc, const f2 (&c)[8], float (&ov)[16],
+                                            float (&out)[16])
+{
+    if (fc.seq == JAAD_ONLY_LONG_SEQUENCE) {
+        ola_only_long_pk(T, fc, c, ov, out);
+        return;
+    }
+    float re[8], im[8];
+#pragma unroll
+    for (int s = 0; s < 8; s++) {
+        re[s] = c[s].x;
+        im[s] = c[s].y;
+    }
+    if (fc.seq == JAAD_LONG_START_SEQUENCE) ola_long_t<JAAD_LONG_START_SEQUENCE>(T, fc, re, im, ov, out);
+    else ola_long_t<JAAD_LONG_STOP_SEQUENCE>(T, fc, re, im, ov, out);
+}
+
 
 // ------------------------------------------------------------------------------------------
 // EIGHT_SHORT_SEQUENCE: 8 x MDCT(256) (64-point IFFTs), FilterBank.java:71-101.
@@ -1038,10 +1219,17 @@ __global__ __launch_bounds__(64 * waves_per_wg<kTnsSpec>()) void lc_decode_kerne
                     }
                 }
                 float* const bufs[2] = {W.buf, W.rsp};
+#ifdef JAAD_LC_SCALAR
                 float re[2][8], im[2][8];
                 imdct_long_n<2>(bufs, T, lane_id(), re, im);
                 ola_long(T, u, FrameCtx{iL.seq, iL.shape, iL.shape_prev}, re[0], im[0], ovL, outL);
                 ola_long(T, u, FrameCtx{iR.seq, iR.shape, iR.shape_prev}, re[1], im[1], ovR, outR);
+#else
+                f2 cx[2][8];
+                imdct_long_pk<2>(bufs, T, lane_id(), cx);
+                ola_long_pk(T, FrameCtx{iL.seq, iL.shape, iL.shape_prev}, cx[0], ovL, outL);
+                ola_long_pk(T, FrameCtx{iR.seq, iR.shape, iR.shape_prev}, cx[1], ovR, outR);
+#endif
                 wave_sync();
             } else {
                 synth_channel<kTnsSpec>(A, T, W, W.buf, iL, cf0, ovL, outL);

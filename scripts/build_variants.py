@@ -7,9 +7,8 @@ sys.path.insert(0, str(ROOT))
 from jaadec_amd import build as B  # noqa: E402
 
 VARIANTS = {
-    "a_base": ([], []),
-    "b_dual": (["JAAD_LC_DUAL"], []),
-    "c_dual_w10": (["JAAD_LC_DUAL", "JAAD_LC_WAVES=10"], []),
+    "p_scalar": (["JAAD_LC_SCALAR"], []),
+    "q_pk": ([], []),
 }
 
 if __name__ == "__main__":

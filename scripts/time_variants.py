@@ -32,7 +32,8 @@ print("%%.4f" %% (ev[0].elapsed_time(ev[1]) / 20))
 def main():
     libs = sorted((ROOT / ".tmp/exp").glob("lib_*.so"))
     cfgid = sys.argv[1] if len(sys.argv) > 1 else "2"
-    for lib in libs:
+    rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 1
+    for lib in [l for _ in range(rounds) for l in libs]:  # alternate: clock drift hits all alike
         env = dict(os.environ, JAAD_LIB=str(lib))
         r = subprocess.run([sys.executable, "-c", CHILD, cfgid], env=env, capture_output=True, text=True, timeout=300)
         out = r.stdout.strip().splitlines()
