@@ -831,6 +831,19 @@ __global__ __launch_bounds__(256) void sbr_synthesis_kernel(SbrArgs A)
         for (int n = 0; n < 32; n++) cm[n] = A.dct32[(half * 32 + e) * 32 + n];
     }
     float* xin = xin_s[wave];
+    // This lane's two DCT inputs of a slot, gathered straight from the row of X (64 float2, band
+    // order) instead of exchanged through cross-lane permutes:
+    //   64 bands: half 0 (in_real1[e], in_imag1[e]) = (Re X[2e], Re X[63-2e]),
+    //             half 1 (in_real2[e], in_imag2[e]) = (Im X[63-2e], Im X[2e])  (SynthesisFilterbank64.java:25-42)
+    //   32 bands: (Re X[e], Im X[e]) in both halves
+    const int band_a = kDown ? e : (half ? 63 - 2 * e : 2 * e);
+    const int band_b = kDown ? e : (half ? 2 * e : 63 - 2 * e);
+    const int ia = kDown ? 2 * e : 2 * band_a + half, ib = kDown ? 2 * e + 1 : 2 * band_b + half;
+    auto fetch = [&](const float2* row, int klim, float& a, float& b) {
+        const float* r = reinterpret_cast<const float*>(row);
+        a = band_a < klim ? r[ia] : 0.0f;
+        b = band_b < klim ? r[ib] : 0.0f;
+    };
 
     auto store_pcm = [&](float out, size_t n, bool dup) {
         if (A.out_mode & JAAD_PCM_FLOAT32) {
@@ -847,8 +860,7 @@ __global__ __launch_bounds__(256) void sbr_synthesis_kernel(SbrArgs A)
     };
 
     // downsampled slot (:50-92): pre-twiddle, DCT-IV / DST-IV, v block of 64, 32 windowed outputs
-    auto slot32 = [&](float Xr, float Xi, bool emit, size_t n0, bool dup) {
-        const float xr = shfl(Xr, e), xi = shfl(Xi, e);  // X[l][e]
+    auto slot32 = [&](float xr, float xi, bool emit, size_t n0, bool dup) {
         float x1 = (xr * tw_c) - (xi * tw_s);
         float x2 = (xi * tw_c) + (xr * tw_s);
         x1 *= scale;
@@ -885,13 +897,9 @@ __global__ __launch_bounds__(256) void sbr_synthesis_kernel(SbrArgs A)
     };
 
     // one slot: DCT-IV pair -> v block (:99-129); emit: window (:134-146) + PCM
-    auto slot64 = [&](float Xr, float Xi, bool emit, size_t n0, bool dup) {
-        // DCT inputs: d = 0: real parts (in_real1[e] = X[2e], in_imag1[e] = X[63-2e]);
-        //             d = 1: imag parts (in_real2[e] = X[63-2e], in_imag2[e] = X[2e])
-        const float ar = shfl(Xr, 2 * e), br = shfl(Xr, 63 - 2 * e);
-        const float ai = shfl(Xi, 2 * e), bi = shfl(Xi, 63 - 2 * e);
-        const float in_r = scale * (half ? bi : ar);
-        const float in_i = scale * (half ? ai : br);
+    auto slot64 = [&](float a, float b, bool emit, size_t n0, bool dup) {
+        const float in_r = scale * a;  // (fetch) d = 0: in_real1[e] / d = 1: in_real2[e]
+        const float in_i = scale * b;  //            in_imag1[e] /        in_imag2[e]
         float orr, oi;
         dct4(K, e, E, in_r, in_i, orr, oi);
         const float Ap = shfl(orr, u ^ 32);
@@ -942,8 +950,9 @@ __global__ __launch_bounds__(256) void sbr_synthesis_kernel(SbrArgs A)
         const float2* xp = back == 0 ? reinterpret_cast<const float2*>(&A.state[(size_t)R0.slot * 2 + c].xsyn[0][0][0])
                                      : reinterpret_cast<const float2*>(prev) + 23 * 64;
         for (int l = 0; l < 9; l++) {
-            const float2 v = xp[l * 64 + u];
-            slot(v.x, v.y, false, 0);
+            float a, b;
+            fetch(xp + l * 64, 64, a, b);
+            slot(a, b, false, 0);
         }
     }
     for (int j = 0; j < (int)ck.n; j++) {
@@ -957,8 +966,9 @@ __global__ __launch_bounds__(256) void sbr_synthesis_kernel(SbrArgs A)
             if (c == 1 && !ps_on) continue;
             const float2* xq = reinterpret_cast<const float2*>(A.xps + ((size_t)f * 2 + c) * 4096);
             for (int l = 0; l < 32; l++) {
-                const float2 v = xq[l * 64 + u];
-                slot(v.x, v.y, true, (size_t)f * spf + sps * l, !ps_on);
+                float a, b;
+                fetch(xq + l * 64, 64, a, b);
+                slot(a, b, true, (size_t)f * spf + sps * l, !ps_on);
             }
             continue;
         }
@@ -969,14 +979,10 @@ __global__ __launch_bounds__(256) void sbr_synthesis_kernel(SbrArgs A)
                                    : reinterpret_cast<const float2*>(A.xcarry + (cf - nch) * 768);
         const int kprev = R.kx_prev + R.M_prev;
         for (int l = 0; l < 32; l++) {
-            float2 v;
-            if (l < t0) {
-                v = xc[l * 64 + u];
-                if (u >= kprev) v = make_float2(0.0f, 0.0f);
-            } else {
-                v = xs[l * 64 + u];
-            }
-            slot(v.x, v.y, true, (size_t)f * spf + sps * l);
+            float a, b;
+            if (l < t0) fetch(xc + l * 64, kprev, a, b);
+            else fetch(xs + l * 64, 64, a, b);
+            slot(a, b, true, (size_t)f * spf + sps * l);
         }
     }
 }
