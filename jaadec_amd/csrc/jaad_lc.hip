@@ -983,7 +983,7 @@ __global__ __launch_bounds__(64 * waves_per_wg<kTnsSpec>()) void lc_decode_kerne
     constexpr bool big_endian = !(kOut & JAAD_PCM_LITTLE_ENDIAN);
     constexpr bool planar = kOut == (int)kOutPlanarF32;
     constexpr bool out_f32 = (kOut & JAAD_PCM_FLOAT32) != 0 && !planar;
-    constexpr bool out_i16 = !planar && !out_f32;
+    [[maybe_unused]] constexpr bool out_i16 = !planar && !out_f32;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     // channel count is a template parameter: a run-time flag would leave the register allocator
     // with paths where the right channel's values live across frames

@@ -223,7 +223,10 @@ int read_ics(BitReader& br, const Cfg& C, bool common_window, IcsInfo& I, int pr
             }
         }
     }
-    // ---- pulse data: parsed, never applied (:17, :148-170)
+    // ---- pulse data (:17, :148-170): parsed and, as in the reference, not applied -- except in
+    // spec mode (cfg.tns_mode == JAAD_TNS_SPEC, the "spec tools" switch of SURVEY 8(f)-4), where
+    // ISO/IEC 14496-3 4.6.3.3 adds the pulses to the quantised values below
+    int pulse_n = 0, pulse_off[4] = {0, 0, 0, 0}, pulse_amp[4] = {0, 0, 0, 0};
     if (br.left() < 1) return JAAD_ERR_EOS;
     if (br.read(1)) {
         if (is_short) return JAAD_ERR_BITSTREAM;  // "pulse data not allowed for short frames"
@@ -235,9 +238,11 @@ int read_ics(BitReader& br, const Cfg& C, bool common_window, IcsInfo& I, int pr
         for (int i = 0; i < count; i++) {
             if (br.left() < 9) return JAAD_ERR_EOS;
             offs += (int)br.read(5);
-            br.skip(4);  // amplitude
+            pulse_amp[i] = (int)br.read(4);
+            pulse_off[i] = offs;
             if (i > 0 && offs > 1023) return JAAD_ERR_BITSTREAM;
         }
+        pulse_n = count;
     }
     // ---- TNS data (TNS.decode, A/tools/TNS.java:35-61)
     jaad_tns tns;
@@ -338,6 +343,14 @@ int read_ics(BitReader& br, const Cfg& C, bool common_window, IcsInfo& I, int pr
         group_off += gl << 7;
     }
     if (br.overrun()) return JAAD_ERR_EOS;
+    if (C.cfg.tns_mode == JAAD_TNS_SPEC)  // spec-mode pulse tool (4.6.3.3, long windows only)
+        for (int i = 0; i < pulse_n; i++) {
+            const int k = pulse_off[i];
+            if (k > 1023) return JAAD_ERR_BITSTREAM;  // the first offset is not range-checked above
+            const int v = q[k] > 0 ? q[k] + pulse_amp[i] : q[k] - pulse_amp[i];
+            if (v > 8190 || v < -8190) return JAAD_ERR_BITSTREAM;  // beyond IQ_TABLE
+            q[k] = (int16_t)v;
+        }
 
     // ---- records
     std::memcpy(o.q, q, sizeof q);

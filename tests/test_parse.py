@@ -202,3 +202,21 @@ def test_bitstream_fixtures_on_the_gpu(name):
     with N.Context(cfg, 1) as ctx:
         got = ctx.decode(b, N.PCM_BIG_ENDIAN)
     assert got.tobytes() == z["pcm"].tobytes()
+
+
+def test_pulse_data_is_applied_only_in_spec_mode():
+    """The reference parses pulse_data and never applies it (A/syntax/ICStream.java:148-170);
+    with cfg.tns_mode = JAAD_TNS_SPEC (spec tools) the parser adds the pulses to the quantised
+    values as ISO/IEC 14496-3 4.6.3.3 does: q[k] += amp if q[k] > 0 else q[k] -= amp.
+    The test writer puts 2 pulses at swb 0: offset 3 (amp 5) and 3 + 7 = 10 (amp 2)."""
+    p = N.synth_params(2, n_streams=1, frames_per_stream=4)
+    b = N.synth_batch(p)
+    frames = O.write_frames(b, p.sf_index, extras=2)
+    compat = N.Parser(N.cfg_for(p)).parse(frames)
+    assert np.array_equal(compat.q, b.q)
+    spec = N.Parser(N.cfg_for(p, tns_mode=N.TNS_SPEC)).parse(frames)
+    want = b.q.astype(np.int32).copy()
+    for row in want:
+        for k, amp in ((3, 5), (10, 2)):
+            row[k] = row[k] + amp if row[k] > 0 else row[k] - amp
+    assert np.array_equal(spec.q.astype(np.int32), want)
