@@ -362,6 +362,29 @@ __global__ __launch_bounds__(256) void sbr_hf_kernel(SbrArgs A)
             xi[r] = u < 32 ? v.y : 0.0f;
         }
     }
+    // Parameter lookups issued now, while the Xlow rows are in flight: the generation's source band
+    // and chirp factor, and calculate_gain's per-band inputs of every envelope (noise band ->
+    // Q_div / Q_div2, resolution band -> E_orig).  Each is a two-level table walk in global memory;
+    // fetched inside the envelope loop they were two dependent round trips per envelope.
+    const int p_src = T.src_p[u];
+    float bw_k, pEo[5], pQd[5], pQd2[5];
+    {
+        const int gk = T.g_of_k[u];
+        bw_k = R.bw[gk < 5 ? gk : 0];
+        const int mi = (u - kx >= 0 && u - kx < M) ? u - kx : 0;
+        const int nb = T.noise_map[s_lim][mi];
+        const int rm0 = T.res_map[s_lim][0][mi], rm1 = T.res_map[s_lim][1][mi];
+        int eo = (int)R.e_off;
+#pragma unroll
+        for (int l = 0; l < 5; l++) {
+            const bool on = l < L_E;
+            const int fl = on ? R.f[l] : 0, tnb = on ? R.tnb[l] : 0;
+            pEo[l] = on ? A.epool[eo + (fl ? rm1 : rm0)] : 0.0f;
+            pQd[l] = R.q_div[tnb][nb];
+            pQd2[l] = R.q_div2[tnb][nb];
+            eo += on ? (fl ? T.n_hi : T.n_lo) : 0;
+        }
+    }
     float gr[5] = {0, 0, 0, 0, 0}, qr[5] = {0, 0, 0, 0, 0};
     int gidx = R.gq0;
     if (kPhase == 2 && !(R.flags & kSbrReset)) {
@@ -417,10 +440,10 @@ __global__ __launch_bounds__(256) void sbr_hf_kernel(SbrArgs A)
         if (((a0r * a0r) + (a0i * a0i) >= 16.0f) || ((a1r * a1r) + (a1i * a1i) >= 16.0f)) a0r = a0i = a1r = a1i = 0.0f;
     }
     {
-        const int p = T.src_p[u];
+        const int p = p_src;
         const bool gen = p != 0xFF;
         const int ps = gen ? p : u;
-        const float bw = R.bw[T.g_of_k[u] < 5 ? T.g_of_k[u] : 0];
+        const float bw = bw_k;
         const float bw2 = bw * bw;
         const float A0r = shfl(a0r, ps) * bw, A1r = shfl(a1r, ps) * bw2;
         const float A0i = shfl(a0i, ps) * bw, A1i = shfl(a1i, ps) * bw2;
@@ -534,7 +557,6 @@ __global__ __launch_bounds__(256) void sbr_hf_kernel(SbrArgs A)
     {
         const int NL = T.N_L[s_lim];
         const float EPS = 1e-12f;
-        int eo = (int)R.e_off;
         // limiter band of band m (lane); bands outside every limiter band keep G = Q = S = 0
         int kbm = 0;
         for (int kb = 1; kb < NL; kb++)
@@ -545,17 +567,16 @@ __global__ __launch_bounds__(256) void sbr_hf_kernel(SbrArgs A)
         const int ml1 = lim_lane ? T.lim[s_lim][kb] : 0, ml2 = lim_lane ? T.lim[s_lim][kb + 1] : 0;
         int wmax = 0;
         for (int j = 0; j < NL; j++) wmax = max(wmax, (int)T.lim[s_lim][j + 1] - (int)T.lim[s_lim][j]);
-        for (int l = 0; l < L_E; l++) {
-            const int fl = R.f[l];
-            const int tnb = R.tnb[l];
+#pragma unroll
+        for (int l = 0; l < 5; l++) {
+            if (l >= L_E) break;
             const bool delta1 = !((R.no_noise >> l) & 1);
             const uint64_t smask = R.s_index[l], mmask = R.s_mapped[l];
             const bool sidx = band && ((smask >> m) & 1);
             float Eom = 0.0f, Ec = 0.0f, Q_M = 0.0f, S_M = 0.0f, G = 0.0f;
             if (band) {  // (1)
-                const int nb = T.noise_map[s_lim][m];
-                const float Qd = R.q_div[tnb][nb], Qd2 = R.q_div2[tnb][nb];
-                Eom = A.epool[eo + T.res_map[s_lim][fl][m]];
+                const float Qd = pQd[l], Qd2 = pQd2[l];
+                Eom = pEo[l];
                 Ec = L.ecurr[l][m];
                 const bool smap = (mmask >> m) & 1;
                 G = __fdiv_rn(Eom, 1.0f + Ec);
@@ -565,7 +586,6 @@ __global__ __launch_bounds__(256) void sbr_hf_kernel(SbrArgs A)
                 Q_M = Eom * Qd2;
                 S_M = sidx ? Eom * Qd : 0.0f;
             }
-            eo += fl ? T.n_hi : T.n_lo;
             wave_sync();
             if (lim_lane) {  // (2)
                 float acc1 = 0.0f, acc2 = 0.0f;
