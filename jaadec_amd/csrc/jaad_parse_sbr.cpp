@@ -290,19 +290,19 @@ int read_envelope(BitReader& br, ChWork& w, const SbrParseState& S, bool coupled
         if (w.df_env[env] == 0) {
             const int bits = coupled ? (amp_res ? 5 : 6) : (amp_res ? 6 : 7);
             if (br.left() < bits) return JAAD_ERR_EOS;
-            w.E[0][env] = (int)br.read(bits) << delta;
+            w.E[0][env] = (int)br.read(bits) * (1 << delta);  // Java << on an int (negative deltas too)
             for (int band = 1; band < nb; band++) {
                 int v;
                 const int st = tree_decode(br, fh, fn, 64, v);
                 if (st) return st;
-                w.E[band][env] = v << delta;
+                w.E[band][env] = v * (1 << delta);  // Java << on an int (negative deltas too)
             }
         } else {
             for (int band = 0; band < nb; band++) {
                 int v;
                 const int st = tree_decode(br, th, tn, 64, v);
                 if (st) return st;
-                w.E[band][env] = v << delta;
+                w.E[band][env] = v * (1 << delta);  // Java << on an int (negative deltas too)
             }
         }
     }
@@ -345,19 +345,19 @@ int read_noise(BitReader& br, ChWork& w, const SbrParseState& S, bool coupled)
     for (int noise = 0; noise < w.L_Q; noise++) {
         if (w.df_noise[noise] == 0) {
             if (br.left() < 5) return JAAD_ERR_EOS;
-            w.Q[0][noise] = (int)br.read(5) << delta;
+            w.Q[0][noise] = (int)br.read(5) * (1 << delta);  // Java << on an int (negative deltas too)
             for (int band = 1; band < S.N_Q; band++) {
                 int v;
                 const int st = tree_decode(br, fh, fn, 64, v);
                 if (st) return st;
-                w.Q[band][noise] = v << delta;
+                w.Q[band][noise] = v * (1 << delta);  // Java << on an int (negative deltas too)
             }
         } else {
             for (int band = 0; band < S.N_Q; band++) {
                 int v;
                 const int st = tree_decode(br, th, tn, 64, v);
                 if (st) return st;
-                w.Q[band][noise] = v << delta;
+                w.Q[band][noise] = v * (1 << delta);  // Java << on an int (negative deltas too)
             }
         }
     }
@@ -412,8 +412,9 @@ PsKind icc_kind(int id)
 {
     return PsKind{kIccNrPar[id], id % 3 == 0 ? 2 : 0, 34, 0, 7, false, JAAD_PS_F_HUFF_ICC, 14, JAAD_PS_T_HUFF_ICC, 14};
 }
-PsKind pd_kind(int id, bool opd)
+PsKind pd_kind(int id, bool opd)  // id < 0 (null mode): a placeholder, never read or decoded with
 {
+    id = id < 0 ? 0 : id;
     return PsKind{kPdNrPar[id], 1, 17, 0, 7, true, opd ? JAAD_PS_F_HUFF_OPD : JAAD_PS_F_HUFF_IPD, 7,
                   opd ? JAAD_PS_T_HUFF_OPD : JAAD_PS_T_HUFF_IPD, 7};
 }
