@@ -193,6 +193,7 @@ struct jaad_ctx {
     // ---- SBR (cfg.sbr) ----
     std::unique_ptr<SbrHost> sbr_host;
     std::vector<SbrHostSlot> sbr_slots;          // parameter-side state per slot (host)
+    std::vector<uint32_t> sbr_depth;             // HF fix pass of each channel-frame (scratch)
     SbrChState* d_sbr_state = nullptr;           // [slot][2], rewritten at the end of each call
     float* d_sbr_const = nullptr;                // qmf_c[640] | dct4 tab[192] w_re[16] w_im[16] | noise[1024] |
                                                  // tw32[64] | dct32 double[2][32][32]
@@ -493,7 +494,8 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
     const size_t o_last = al(o_chunks + ctx->sbr_chunks.size() * sizeof(SbrChunk));
     const size_t o_runs = al(o_last + ctx->sbr_last.size() * sizeof(uint32_t));
     const size_t o_pslist = al(o_runs + ctx->ps_runs.size() * sizeof(uint32_t));
-    const size_t n1 = al(o_pslist + (ps ? nf * sizeof(uint32_t) : 0));
+    const size_t o_fix = al(o_pslist + (ps ? nf * sizeof(uint32_t) : 0));
+    const size_t n1 = al(o_fix + ncf * sizeof(uint32_t));
 
     // JAAD_TRACE_HOST=1: per-call host timings of this stage on stderr (tuning aid)
     static const bool trace = std::getenv("JAAD_TRACE_HOST") != nullptr;
@@ -618,12 +620,41 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
         }
     }
     if (!tabs.empty()) std::memcpy(h2 + o_tabs, tabs.data(), tabs.size() * sizeof(SbrTab));
+
+    // HF fix passes: a kSbrDep channel-frame needs frame f-1's final carry rows, so it is
+    // recomputed in pass d = its link count down a chain of such frames (with G/Q smoothing a
+    // frame whose predecessor was recomputed is recomputed too: its ring came from that frame)
+    std::vector<uint32_t> fix_counts;
+    {
+        uint32_t* fix_h = reinterpret_cast<uint32_t*>(h1 + o_fix);
+        std::vector<uint32_t>& depth = ctx->sbr_depth;
+        depth.assign(ncf, 0);
+        uint32_t max_d = 0;
+        for (uint32_t r = 0; r < b->n_runs; r++)
+            for (uint32_t f = b->frame_begin[r] + 1; f < b->frame_begin[r + 1]; f++)
+                for (int c = 0; c < nch; c++) {
+                    const size_t cf = (size_t)f * nch + c;
+                    const uint8_t fl = recs[cf].flags;
+                    const uint32_t dp = depth[cf - nch];
+                    if ((fl & kSbrDep) || ((fl & kSbrSmooth) && !(fl & kSbrReset) && dp > 0)) {
+                        depth[cf] = dp + 1;
+                        max_d = std::max(max_d, dp + 1);
+                    }
+                }
+        fix_counts.assign(max_d, 0);
+        for (size_t cf = 0; cf < ncf; cf++)
+            if (depth[cf]) fix_counts[depth[cf] - 1]++;
+        std::vector<uint32_t> pos(max_d + 1, 0);
+        for (uint32_t d = 0; d < max_d; d++) pos[d + 1] = pos[d] + fix_counts[d];
+        for (size_t cf = 0; cf < ncf; cf++)
+            if (depth[cf]) fix_h[pos[depth[cf] - 1]++] = (uint32_t)cf;
+    }
     const auto t_packed = clk::now();
 
     // device side: intermediates (stream-ordered) and this set's record copy (copy stream)
     HIPCHK(ctx->d_xlow.ensure(ncf * 2048 * sizeof(float) + 256));
     HIPCHK(ctx->d_xsyn.ensure(ncf * 4096 * sizeof(float) + 256));
-    HIPCHK(ctx->d_xcarry.ensure(ncf * 768 * sizeof(float) + 256));
+    HIPCHK(ctx->d_xcarry.ensure(ncf * kSbrCarryFloats * sizeof(float) + 256));
     HIPCHK(ctx->d_gq.ensure(ncf * 640 * sizeof(float) + 256));
     if (ps) {
         HIPCHK(ctx->d_xps.ensure(nf * 8192 * sizeof(float) + 256));
@@ -688,7 +719,8 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
         a.ps_list = reinterpret_cast<const uint32_t*>(d1 + o_pslist);
         a.n_runs = (uint32_t)(ctx->ps_runs.size() / 2);
     }
-    HIPCHK(launch_sbr(a, stream));
+    HIPCHK(launch_sbr(a, stream, reinterpret_cast<const uint32_t*>(d1 + o_fix), fix_counts.data(),
+                      (int)fix_counts.size()));
     HIPCHK(hipEventRecord(S.used, stream));
     S.live = true;
     if (trace) {

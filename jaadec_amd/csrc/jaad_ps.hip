@@ -119,19 +119,19 @@ __device__ __forceinline__ void filter2(const float2 b[13], const float* c, floa
 }
 
 // X_left row l < 38 of frame f for QMF band u: Xsbr rows l + 2 as SBR1.processPS assembles them
-// (A/sbr/SBR1.java:102-120): rows l < t_E[0] carried from frame f-1 with kx_prev + M_prev,
-// rows 32..37 = Xsbr rows 34..39 for bands < 5
+// (A/sbr/SBR1.java:102-120): rows l < t_E[0] carried from frame f-1 (its carry rows l + 2) with
+// kx_prev + M_prev bands, rows 32..37 = Xsbr rows 34..39 (carry rows 2..7) for bands < 5
 __device__ __forceinline__ const float2* x_carry_prev(const SbrArgs& A, const SbrRec& R, uint32_t f)
 {
     return R.first ? reinterpret_cast<const float2*>(&A.state[(size_t)R.slot * 2].xcarry[0][0][0])
-                   : reinterpret_cast<const float2*>(A.xcarry + (size_t)(f - 1) * 768);
+                   : reinterpret_cast<const float2*>(A.xcarry + (size_t)(f - 1) * kSbrCarryFloats);
 }
 
 // Filterbank.buffer after frame f, element i of band b: work[32 + i] = X_left[26 + i][b] (b < 3)
 __device__ __forceinline__ float2 hyb_history_after(const SbrArgs& A, uint32_t f, int b, int i)
 {
     return i < 6 ? reinterpret_cast<const float2*>(A.xsyn + (size_t)f * 4096)[(26 + i) * 64 + b]
-                 : reinterpret_cast<const float2*>(A.xcarry + (size_t)f * 768)[(i - 6) * 64 + b];
+                 : reinterpret_cast<const float2*>(A.xcarry + (size_t)f * kSbrCarryFloats)[(i - 4) * 64 + b];
 }
 
 struct AnaLds {
@@ -149,21 +149,24 @@ __global__ __launch_bounds__(256) void ps_analysis_kernel(SbrArgs A)
     const SbrRec& R = A.recs[f];
     const PsConst& K = *A.psc;
     {
-        const int t0 = R.t_E[0], kprev = R.kx_prev + R.M_prev;
+        const int t0 = R.t_E[0], kprev = R.kx_prev + R.M_prev, kcur = sbr_kcur(A, R);
         const float2* xs = reinterpret_cast<const float2*>(A.xsyn + (size_t)f * 4096);
         const float2* xc = x_carry_prev(A, R, f);
-        const float2* xn = reinterpret_cast<const float2*>(A.xcarry + (size_t)f * 768);
+        const float2* xn = reinterpret_cast<const float2*>(A.xcarry + (size_t)f * kSbrCarryFloats);
         float2* xo = reinterpret_cast<float2*>(A.xps + (size_t)f * 8192);
         for (int l = 0; l < 32; l++) {
-            float2 v;
-            if (l < t0) v = u < kprev ? xc[l * 64 + u] : make_float2(0.0f, 0.0f);
-            else v = xs[l * 64 + u];
+            float2 v = make_float2(0.0f, 0.0f);
+            if (l < t0) {
+                if (u < kprev) v = xc[(l + 2) * 64 + u];
+            } else if (u < kcur) {
+                v = xs[l * 64 + u];  // the stored bands (sbr_kcur)
+            }
             L.xl[l][u] = v;
             xo[l * 64 + u] = v;
         }
         // a frame without PS data only hands its X (qmfs0 input) to the synthesis
         if (!(R.flags & kSbrPsOn)) return;
-        for (int l = 32; l < 38; l++) L.xl[l][u] = u < 5 ? xn[(l - 32) * 64 + u] : make_float2(0.0f, 0.0f);
+        for (int l = 32; l < 38; l++) L.xl[l][u] = u < 5 ? xn[(l - 30) * 64 + u] : make_float2(0.0f, 0.0f);
         if (u < 36) {
             // Filterbank.buffer as the previous PS frame left it (frames without PS data do not
             // run the hybrid analysis)

@@ -44,6 +44,7 @@ enum : uint8_t {
     kSbrInterpol = 4,    // bs_interpol_freq
     kSbrProcess = 8,     // a header has been seen (else analysis only, kx = 32)
     kSbrPsOn = 16,       // PS config: this frame carries PS data (SBR1.isPSUsed, A/sbr/SBR1.java:136)
+    kSbrDep = 32,        // reads the high band of frame f-1's Xsbr rows 32..39: an HF fix pass
 };
 
 // One channel-frame.  224 bytes.
@@ -74,11 +75,12 @@ static_assert(sizeof(SbrRec) == 224, "SbrRec layout");
 // call for the first frame of a run, rewritten by the last kernel of the call (sbr_state_kernel).
 struct SbrChState {
     float tail[288];            // last 288 core samples of the previous frame (analysis ring)
-    float xlow[8][32][2];       // analysis slots 24..31 of the previous frame (Xsbr rows 0..7, k < 32)
+    float xcarry[8][64][2];     // Xsbr rows 32..39 of the previous frame after HF adjustment
+                                // (sbr_save_matrix: rows 0..7 of the next frame, every band)
     float xsyn[9][64][2];       // synthesis input rows 23..31 of the previous frame (v history)
-    float xcarry[6][64][2];     // Xsbr rows 34..39 of the previous frame after HF adjustment
     float gq[2][5][64];         // G/Q smoothing ring after the previous frame [ring position][m]
 };
+constexpr int kSbrCarryFloats = 8 * 64 * 2;  // per channel-frame in SbrArgs::xcarry
 
 // Frame-parallel pipeline (one launch each, stream-ordered):
 //   sbr_analysis_kernel  [ch-frame]  core time samples -> X_low  (AnalysisFilterbank)
@@ -130,12 +132,14 @@ struct SbrArgs {
     const SbrTab* tabs;
     float* xlow;                // [ch-frame][32 slots][32 bands][2]
     float* xsyn;                // [ch-frame][32 slots][64 bands][2]
-    float* xcarry;              // [ch-frame][6][64][2]
+    float* xcarry;              // [ch-frame][8][64][2]: Xsbr rows 32..39 after HF adjustment
     float* gq;                  // [ch-frame][2][5][64] ring after the frame (smoothing / state)
     const SbrChunk* chunks;     // synthesis chunks
     const uint32_t* last_cf;    // ch-frame index of the last frame of each (run, channel)
     SbrChState* state;          // [slot][2]
     void* pcm;
+    const uint32_t* fix;        // HF fix pass: the channel-frames it recomputes (kSbrDep chains)
+    uint32_t n_fix;
     const float* noise;         // NOISE_TABLE [512][2]
     const float* qmf_c;         // [640]
     const float* dct;           // dct4_64_tab [192] + w_re [16] + w_im [16]
@@ -164,7 +168,19 @@ struct SbrArgs {
     uint32_t n_runs;
 };
 
-hipError_t launch_sbr(const SbrArgs& a, hipStream_t stream);
+// Bands of a channel-frame's synthesis input X (xsyn) and carry rows (xcarry) that sbr_hf_kernel
+// stores: kx + M (rows l < t_E[0] of X: kx_prev + M_prev).  X is zero above them
+// (A/sbr/Channel.java:619-645), so the stores stop there and every reader masks by the writer's
+// value.  (The analysis likewise stores X_low bands < kx only.)
+__device__ __forceinline__ int sbr_kcur(const SbrArgs& A, const SbrRec& R)
+{
+    const SbrTab& T = A.tabs[R.table];
+    return T.kx + T.M;
+}
+
+// fix_dev: channel-frames of the HF fix passes, pass after pass (fix_counts[p] in pass p)
+hipError_t launch_sbr(const SbrArgs& a, hipStream_t stream, const uint32_t* fix_dev = nullptr,
+                      const uint32_t* fix_counts = nullptr, int n_fix_passes = 0);
 hipError_t launch_ps(const SbrArgs& a, hipStream_t stream);  // jaad_ps.hip, called by launch_sbr
 
 // ---------------------------------------------------------------------------------------------
@@ -178,6 +194,7 @@ struct SbrHostCh {
     int prevEnvIsShort;
     int index_noise_prev, psi_is_prev;
     int gq_index;
+    int last_prev;  // t_E[L_E] of the previous frame (its HF adjusted rows up to last_prev + 1)
 };
 
 struct SbrHostSlot {
@@ -194,6 +211,8 @@ struct SbrFbt {
     int f_master[65], f_table_res[2][65], f_table_noise[65], f_table_lim[4][65], N_L[4];
     int table_map_k_to_g[64];
     int noPatches, patchNoSubbands[64], patchStartSubband[64];
+    int max_src;   // highest HF generation source band (-1: none)
+    int gen_cnt;   // bands the patches generate (< M when patch_construction dropped one)
     // band counters of calculate_gain per limiter setting s, resolution f, band m
     int res_map[4][2][64], noise_map[4][64], hi_map[4][64];
     uint8_t visited[4][64];

@@ -316,6 +316,12 @@ int SbrHost::table_for(const jaad_sbr_header& h)
                                       : master_fs(t, t.k0, t.k2, h.freq_scale);
     if (!ok || !derived_tables(t, h.xover_band, h.noise_bands)) return -1;
     patches(t, sfi);
+    t.max_src = -1;
+    t.gen_cnt = 0;
+    for (int i = 0; i < t.noPatches; i++) {
+        t.gen_cnt += t.patchNoSubbands[i];
+        if (t.patchNoSubbands[i] > 0) t.max_src = std::max(t.max_src, t.patchStartSubband[i] + t.patchNoSubbands[i] - 1);
+    }
     limiter_tables(t);
     band_maps(t);
 
@@ -496,6 +502,17 @@ int SbrHost::frame(SbrHostSlot& st, const jaad_sbr_frame& fr, int nch, bool firs
         ch.add_harmonic_prev = harm & ((1ull << 49) - 1);
         ch.add_harmonic_flag_prev = in.add_harmonic_flag;
         ch.prevEnvIsShort = (l_A == L_E) ? 0 : -1;
+
+        // kSbrDep: the frame reads the high band frame f-1 left in Xsbr rows 32..39 (its rows
+        // 0..7 here, SBR.sbr_save_matrix A/sbr/SBR.java:286-300), which the frame-parallel HF
+        // pass does not have (sbr_hf_kernel): a source band at or above kx_prev (auto_correlation
+        // and the generation read rows 0..39 of it, A/sbr/HFGeneration.java:100-159,56-85), or,
+        // when frame f-1 adjusted rows 34.. (its last border past slot 32), rows 2..7 of bands
+        // [kx_prev, kx) going out as X (kx raised, Channel.java:619-645) or of a band no patch
+        // generates (patch_construction dropped its last patch) entering estimate_current_envelope
+        if (!first && (t.max_src >= st.kx_prev || (ch.last_prev > 32 && (t.kx > st.kx_prev || t.gen_cnt < t.M))))
+            r.flags |= kSbrDep;
+        ch.last_prev = in.t_E[L_E];
     }
     st.kx_prev = t.kx;
     st.M_prev = t.M;

@@ -1296,7 +1296,8 @@ void orc_sbr_process(orc_sbr* s, float* left, float* right, int nch)
 
 void orc_sbr_set_downsampled(orc_sbr* s, int down) { s->down = down != 0; }
 
-/* derived tables of the current header (tests): k0 k2 kx M N_master N_high N_low N_Q noPatches */
+/* derived tables of the current header (tests): k0 k2 kx M N_master N_high N_low N_Q noPatches N_L
+   gen_cnt max_src */
 int orc_sbr_table_info(const jaad_sbr_header* h, int out_sf_index, int* info, int* f_master, int* f_table_lim)
 {
     orc_sbr* s = (orc_sbr*)calloc(1, sizeof(orc_sbr));
@@ -1317,6 +1318,13 @@ int orc_sbr_table_info(const jaad_sbr_header* h, int out_sf_index, int* info, in
         info[7] = s->N_Q;
         info[8] = s->noPatches;
         info[9] = s->N_L[h->limiter_bands];
+        info[10] = 0;  /* bands the patches generate, highest source band */
+        info[11] = -1;
+        for (int i = 0; i < s->noPatches; i++) {
+            info[10] += s->patchNoSubbands[i];
+            if (s->patchNoSubbands[i] > 0 && s->patchStartSubband[i] + s->patchNoSubbands[i] - 1 > info[11])
+                info[11] = s->patchStartSubband[i] + s->patchNoSubbands[i] - 1;
+        }
         if (f_master) memcpy(f_master, s->f_master, sizeof s->f_master);
         if (f_table_lim) memcpy(f_table_lim, s->f_table_lim[h->limiter_bands], sizeof s->f_table_lim[0]);
     }

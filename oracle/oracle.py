@@ -143,13 +143,13 @@ class QmfSynthesis32:
 def sbr_table_info(hdr, out_sf_index: int):
     """(info dict, f_master, f_table_lim) of FBT for a header (numpy record of SBR_HEADER_DTYPE)."""
     h = np.ascontiguousarray(np.array(hdr))
-    info = np.zeros(10, np.int32)
+    info = np.zeros(12, np.int32)
     fm = np.zeros(64, np.int32)
     lim = np.zeros(64, np.int32)
     rc = lib().orc_sbr_table_info(h.ctypes.data, out_sf_index, info.ctypes.data, fm.ctypes.data, lim.ctypes.data)
     if rc:
         raise RuntimeError(f"orc_sbr_table_info failed: {rc}")
-    keys = ["k0", "k2", "kx", "M", "N_master", "N_high", "N_low", "N_Q", "noPatches", "N_L"]
+    keys = ["k0", "k2", "kx", "M", "N_master", "N_high", "N_low", "N_Q", "noPatches", "N_L", "gen_cnt", "max_src"]
     return dict(zip(keys, map(int, info))), fm, lim
 
 

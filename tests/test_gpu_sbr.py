@@ -122,6 +122,65 @@ def test_c4_continuation_and_state_roundtrip():
     assert np.array_equal(g2b, want[fb[1] + 13:fb[2]])
 
 
+def _header_changes(s, fps):
+    """Mid-stream SBR header changes that move kx and M: xover_band 2 from frame 12 of each
+    stream, start_freq 7 (k0 up) from frame 24.  Both shrink the band count, so the envelope data
+    drawn for the first header stays valid."""
+    f = np.arange(len(s)) % fps
+    s["hdr"]["xover_band"][f >= 12] = 2
+    s["hdr"]["start_freq"][f >= 24] = 7
+
+
+@pytest.mark.parametrize("cfgid", [4, 5])
+def test_header_change_moves_kx_across_calls(cfgid):
+    """kx / M change inside a run and at a call boundary: the analysis stores X_low bands < kx and
+    the HF kernel X bands < kx + M only, so every reader masks by the writer's values (frame f-1's
+    kx_prev / M_prev, the slot state)."""
+    fps = 36
+    p = N.synth_params(cfgid, n_streams=3, frames_per_stream=fps)
+    rng = np.random.default_rng(11)
+    b = _edit(N.synth_batch(p), lambda s: (_header_changes(s, fps), _var_grids(s, rng)))
+    cfg = N.cfg_for(p)
+    want = O.decode_batch(cfg, b, O.Streams(3), N.PCM_FLOAT32, threads=8)
+    first, second = b.split_frames(23)
+    with N.Context(cfg, 3) as ctx:
+        g1 = ctx.decode(first, N.PCM_FLOAT32)
+        g2 = ctx.decode(second, N.PCM_FLOAT32)
+    fb = b.frame_begin
+    for r in range(3):
+        _assert_same(g1[23 * r:23 * (r + 1)], want[fb[r]:fb[r] + 23], N.PCM_FLOAT32)
+        _assert_same(g2[13 * r:13 * (r + 1)], want[fb[r] + 23:fb[r + 1]], N.PCM_FLOAT32)
+
+
+@pytest.mark.parametrize("cfgid", [4, 5])
+def test_dropped_patch_with_trailing_borders(cfgid):
+    """A header whose patch_construction drops bands (start_freq 0, stop_freq 7, freq_scale 0 at
+    48 kHz: kx 7, M 31, the patches generate 21 bands) with envelopes ending past slot 32: the
+    bands without patch carry frame f-1's adjusted rows into the envelope estimate, chains of
+    kSbrDep frames run through the HF fix passes."""
+    fps = 36
+    p = N.synth_params(cfgid, n_streams=3, frames_per_stream=fps)
+    rng = np.random.default_rng(5)
+
+    def edit(s):
+        s["hdr"]["start_freq"], s["hdr"]["stop_freq"], s["hdr"]["freq_scale"] = 0, 7, 0
+        _var_grids(s, rng)
+
+    b = _edit(N.synth_batch(p), edit)
+    info = O.sbr_table_info(b.sbr["hdr"][0], 3)[0]
+    assert info["gen_cnt"] < info["M"], info
+    cfg = N.cfg_for(p)
+    want = O.decode_batch(cfg, b, O.Streams(3), N.PCM_FLOAT32, threads=8)
+    first, second = b.split_frames(17)
+    with N.Context(cfg, 3) as ctx:
+        g1 = ctx.decode(first, N.PCM_FLOAT32)
+        g2 = ctx.decode(second, N.PCM_FLOAT32)
+    fb = b.frame_begin
+    for r in range(3):
+        _assert_same(g1[17 * r:17 * (r + 1)], want[fb[r]:fb[r] + 17], N.PCM_FLOAT32)
+        _assert_same(g2[19 * r:19 * (r + 1)], want[fb[r] + 17:fb[r + 1]], N.PCM_FLOAT32)
+
+
 def test_c4_single_frame_runs_and_empty_runs():
     p = N.synth_params(4, n_streams=4, frames_per_stream=9)
     b = N.synth_batch(p)
