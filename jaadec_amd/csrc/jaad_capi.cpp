@@ -534,7 +534,7 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
     char* h2 = static_cast<char*>(S.h2.p);
     std::vector<int> rcs(nt, 0), bad(nt, -1);
     std::vector<uint32_t> used(nt, 0);
-    std::vector<char> smooth(nt, 0);
+    std::vector<char> smooth(nt, 0), deps(nt, 0);
     // a failed call must leave every slot's host SBR state as it found it (the device state and
     // the core overlap are untouched then): each run's slot is saved before its first frame
     std::vector<SbrHostSlot> saved(b->n_runs);
@@ -544,7 +544,7 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
         float* region = reinterpret_cast<float*>(h2) + rbase[t];
         uint32_t epos = 0;
         uint32_t last_ps = UINT32_MAX;
-        bool sm = false;
+        bool sm = false, dp = false;
         for (uint32_t r = rr[t]; r < rr[t + 1] && !rcs[t]; r++) {
             SbrHostSlot& hs = ctx->sbr_slots[b->stream_slot[r]];
             saved[r] = hs;
@@ -587,15 +587,17 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
                     }
                 }
                 sm |= (rec[0].flags & kSbrSmooth) != 0;
+                for (int c = 0; c < nch; c++) dp |= (rec[c].flags & kSbrDep) != 0;
             }
         }
         used[t] = epos;
         smooth[t] = sm;
+        deps[t] = dp;
     };
     if (nt > 1) ctx->workers->run(work);
     else work(0);
     const auto t_built = clk::now();
-    bool smoothing = false;
+    bool smoothing = false, any_dep = false;
     for (int t = 0; t < nt; t++) {
         if (rcs[t]) {
             // restore every run any worker started (a worker stops at its first bad frame)
@@ -605,6 +607,7 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
             return rcs[t];
         }
         smoothing |= smooth[t] != 0;
+        any_dep |= deps[t] != 0;
     }
     if (ps) {  // per run: (offset, count) of its PS frames in ps_list
         uint32_t np = 0, ri = 0;
@@ -625,7 +628,7 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
     // recomputed in pass d = its link count down a chain of such frames (with G/Q smoothing a
     // frame whose predecessor was recomputed is recomputed too: its ring came from that frame)
     std::vector<uint32_t> fix_counts;
-    {
+    if (any_dep) {
         uint32_t* fix_h = reinterpret_cast<uint32_t*>(h1 + o_fix);
         std::vector<uint32_t>& depth = ctx->sbr_depth;
         depth.assign(ncf, 0);

@@ -149,18 +149,15 @@ __global__ __launch_bounds__(256) void ps_analysis_kernel(SbrArgs A)
     const SbrRec& R = A.recs[f];
     const PsConst& K = *A.psc;
     {
-        const int t0 = R.t_E[0], kprev = R.kx_prev + R.M_prev, kcur = sbr_kcur(A, R);
+        const int t0 = R.t_E[0], kprev = R.kx_prev + R.M_prev;
         const float2* xs = reinterpret_cast<const float2*>(A.xsyn + (size_t)f * 4096);
         const float2* xc = x_carry_prev(A, R, f);
         const float2* xn = reinterpret_cast<const float2*>(A.xcarry + (size_t)f * kSbrCarryFloats);
         float2* xo = reinterpret_cast<float2*>(A.xps + (size_t)f * 8192);
         for (int l = 0; l < 32; l++) {
-            float2 v = make_float2(0.0f, 0.0f);
-            if (l < t0) {
-                if (u < kprev) v = xc[(l + 2) * 64 + u];
-            } else if (u < kcur) {
-                v = xs[l * 64 + u];  // the stored bands (sbr_kcur)
-            }
+            float2 v;
+            if (l < t0) v = u < kprev ? xc[(l + 2) * 64 + u] : make_float2(0.0f, 0.0f);
+            else v = xs[l * 64 + u];
             L.xl[l][u] = v;
             xo[l * 64 + u] = v;
         }

@@ -168,16 +168,6 @@ struct SbrArgs {
     uint32_t n_runs;
 };
 
-// Bands of a channel-frame's synthesis input X (xsyn) and carry rows (xcarry) that sbr_hf_kernel
-// stores: kx + M (rows l < t_E[0] of X: kx_prev + M_prev).  X is zero above them
-// (A/sbr/Channel.java:619-645), so the stores stop there and every reader masks by the writer's
-// value.  (The analysis likewise stores X_low bands < kx only.)
-__device__ __forceinline__ int sbr_kcur(const SbrArgs& A, const SbrRec& R)
-{
-    const SbrTab& T = A.tabs[R.table];
-    return T.kx + T.M;
-}
-
 // fix_dev: channel-frames of the HF fix passes, pass after pass (fix_counts[p] in pass p)
 hipError_t launch_sbr(const SbrArgs& a, hipStream_t stream, const uint32_t* fix_dev = nullptr,
                       const uint32_t* fix_counts = nullptr, int n_fix_passes = 0);

@@ -302,13 +302,17 @@ __global__ __launch_bounds__(256) void sbr_analysis_kernel(SbrArgs A)
         const int k = e;
         const int srcl = hb + bitrev5((k & 1) ? 31 - (k >> 1) : (k >> 1));
         const float vr = shfl(orr, srcl), vi = shfl(oi, srcl);
-        // bands >= kx are zero (:59-70) and are not stored: readers mask them by the kx of the
-        // frame that wrote the row (HBM traffic: kx of 32 bands per slot)
+        float re = 0.0f, im = 0.0f;
         if (k < kx) {
-            const float re = (k & 1) ? -2.0f * vi : 2.0f * vr;
-            const float im = (k & 1) ? -2.0f * vr : 2.0f * vi;
-            reinterpret_cast<float2*>(out)[(2 * p + half) * 32 + k] = make_float2(re, im);
+            if (k & 1) {
+                re = -2.0f * vi;
+                im = -2.0f * vr;
+            } else {
+                re = 2.0f * vr;
+                im = 2.0f * vi;
+            }
         }
+        reinterpret_cast<float2*>(out)[(2 * p + half) * 32 + k] = make_float2(re, im);
     }
 }
 
@@ -349,8 +353,9 @@ __global__ __launch_bounds__(256) void sbr_hf_kernel(SbrArgs A)
     // zero above) -- exact unless the frame reads the high band (source band >= kx_prev, kx above
     // kx_prev or a band without patch with rows 2..7 carried: kSbrDep, jaad_sbr_host.cpp); those
     // frames run again in fix passes (kPhase 3) that read frame f-1's finished carry rows.  The
-    // first frame of a run reads the slot state's carry rows (whole, exact).  Rows 8..39 = this
-    // frame's analysis slots 0..31, stored for bands < kx (zero above).
+    // first frame of a run reads the slot state's carry rows (exact).  Rows 8..39 = this frame's
+    // analysis slots 0..31 (zero from kx up).  The loads wait for nothing but the record's first
+    // flag: masks that need the band tables would put two more dependent round trips first.
     float xr[40], xi[40];
     {
         const float2* cur = reinterpret_cast<const float2*>(A.xlow + (size_t)cf * 2048);
@@ -358,21 +363,20 @@ __global__ __launch_bounds__(256) void sbr_hf_kernel(SbrArgs A)
         const float2* prv = R.first ? reinterpret_cast<const float2*>(&A.state[(size_t)R.slot * 2 + c].xcarry[0][0][0])
                           : carry   ? reinterpret_cast<const float2*>(A.xcarry + (size_t)(cf - A.nch) * kSbrCarryFloats)
                                     : reinterpret_cast<const float2*>(A.xlow + (size_t)(cf - A.nch) * 2048) + 24 * 32;
-        const int kp = R.first ? 64 : carry ? R.kx_prev + R.M_prev : R.kx_prev;
-        const int stride = carry ? 64 : 32;
+        const int kp = carry ? 64 : 32;  // carry rows: every band (zero from kx + M up)
+        const int k = u < kp ? u : kp - 1;
 #pragma unroll
         for (int r = 0; r < 8; r++) {
-            float2 v = make_float2(0.0f, 0.0f);
-            if (u < kp) v = prv[r * stride + u];
-            xr[r] = v.x;
-            xi[r] = v.y;
+            const float2 v = prv[r * kp + k];
+            xr[r] = u < kp ? v.x : 0.0f;
+            xi[r] = u < kp ? v.y : 0.0f;
         }
+        const int k32 = u < 32 ? u : 31;
 #pragma unroll
         for (int r = 8; r < 40; r++) {
-            float2 v = make_float2(0.0f, 0.0f);
-            if (u < kx) v = cur[(r - 8) * 32 + u];
-            xr[r] = v.x;
-            xi[r] = v.y;
+            const float2 v = cur[(r - 8) * 32 + k32];
+            xr[r] = u < 32 ? v.x : 0.0f;
+            xi[r] = u < 32 ? v.y : 0.0f;
         }
     }
     // Parameter lookups issued now, while the Xlow rows are in flight: the generation's source band
@@ -674,12 +678,8 @@ __global__ __launch_bounds__(256) void sbr_hf_kernel(SbrArgs A)
     }
 #endif
 
-    // last frame of its run in this call: its ring, carry rows and synthesis rows go to the slot
-    // state (sbr_state_kernel); otherwise the next frame of the run is record cf + nch
-    const bool last_of_run = cf + A.nch >= A.n_cf || A.recs[cf + A.nch].first;
-    // G/Q ring after this frame: the last 5 assembled rows (rows >= 26 always, see the host check).
-    // Read by the next frame only with smoothing (the second launch), else only by the state
-    if (A.smoothing || last_of_run) {
+    // G/Q ring after this frame: the last 5 assembled rows (rows >= 26 always, see the host check)
+    {
         float* ring = A.gq + (size_t)cf * 640;
         const int rows = last - first;
         for (int j = 0; j < 5; j++) {
@@ -815,19 +815,19 @@ __global__ __launch_bounds__(256) void sbr_hf_kernel(SbrArgs A)
     // rows l < t_E[0] take kx_prev/M_prev and the carried rows, patched in by the synthesis kernel
     {
         // rows l < t_E[0] are Xsbr rows 2..7 as frame f-1 left them: its carry rows 2..7, which
-        // the synthesis / PS analysis read (a later launch) with kx_prev + M_prev bands.  X is zero
-        // above kx + M, which is not stored: readers mask by the writer's limit (sbr_kcur)
+        // the synthesis / PS analysis read (a later launch) with kx_prev + M_prev bands
         float2* xs = reinterpret_cast<float2*>(A.xsyn + (size_t)cf * 4096);
         const int kcur = kx + M;
 #pragma unroll
-        for (int l = 0; l < 32; l++)
-            if (l >= first && u < kcur) xs[l * 64 + u] = make_float2(xr[l + 2], xi[l + 2]);
-        // Xsbr rows 32..39 (the next frame's rows 0..7, the PS look-ahead rows, the slot state)
-        if (u < kcur) {
-            float2* xc = reinterpret_cast<float2*>(A.xcarry + (size_t)cf * kSbrCarryFloats);
-#pragma unroll
-            for (int j = 0; j < 8; j++) xc[j * 64 + u] = make_float2(xr[32 + j], xi[32 + j]);
+        for (int l = 0; l < 32; l++) {
+            const bool keep = u < kcur;
+            xs[l * 64 + u] = make_float2(keep ? xr[l + 2] : 0.0f, keep ? xi[l + 2] : 0.0f);
         }
+        // Xsbr rows 32..39, every band (zero from kx + M up): the next frame's rows 0..7, the PS
+        // look-ahead rows, the slot state
+        float2* xc = reinterpret_cast<float2*>(A.xcarry + (size_t)cf * kSbrCarryFloats);
+#pragma unroll
+        for (int j = 0; j < 8; j++) xc[j * 64 + u] = make_float2(xr[32 + j], xi[32 + j]);
     }
 }
 
@@ -990,11 +990,9 @@ __global__ __launch_bounds__(256) void sbr_synthesis_kernel(SbrArgs A)
         const float* prev = ps ? A.xps + ((size_t)(ck.frame0 - back) * 2 + c) * 4096 : A.xsyn + (cf0 - nch) * 4096;
         const float2* xp = back == 0 ? reinterpret_cast<const float2*>(&A.state[(size_t)R0.slot * 2 + c].xsyn[0][0][0])
                                      : reinterpret_cast<const float2*>(prev) + 23 * 64;
-        // xps and the slot state hold whole rows; xsyn rows of frame f-1 its kx + M bands
-        const int klim = (back == 0 || ps) ? 64 : R0.kx_prev + R0.M_prev;
         for (int l = 0; l < 9; l++) {
             float a, b;
-            fetch(xp + l * 64, klim, a, b);
+            fetch(xp + l * 64, 64, a, b);
             slot(a, b, false, 0);
         }
     }
@@ -1021,11 +1019,11 @@ __global__ __launch_bounds__(256) void sbr_synthesis_kernel(SbrArgs A)
         const int t0 = R.t_E[0];
         const float2* xc = R.first ? reinterpret_cast<const float2*>(&A.state[(size_t)R.slot * 2 + c].xcarry[0][0][0])
                                    : reinterpret_cast<const float2*>(A.xcarry + (cf - nch) * kSbrCarryFloats);
-        const int kprev = R.kx_prev + R.M_prev, kcur = sbr_kcur(A, R);
+        const int kprev = R.kx_prev + R.M_prev;
         for (int l = 0; l < 32; l++) {
             float a, b;
             if (l < t0) fetch(xc + (l + 2) * 64, kprev, a, b);
-            else fetch(xs + l * 64, kcur, a, b);
+            else fetch(xs + l * 64, 64, a, b);
             slot(a, b, true, (size_t)f * spf + sps * l);
         }
     }
@@ -1045,8 +1043,6 @@ __global__ __launch_bounds__(256) void sbr_state_kernel(SbrArgs A)
     SbrChState& S = A.state[(size_t)R.slot * 2 + c];
     const float* t = A.time + (size_t)cf * 1024 + 736;
     for (int k = u; k < 288; k += 64) S.tail[k] = t[k];
-    // the HF kernel stores bands < kx + M of X and of the carry rows: the state rows are made whole
-    const int kcur = sbr_kcur(A, R);
     if (A.ps) {  // synthesis history of both output channels comes from xps
         for (int oc = 0; oc < 2; oc++) {
             // the right channel's synthesis (qmfs1) last ran on the run's last PS frame
@@ -1061,10 +1057,10 @@ __global__ __launch_bounds__(256) void sbr_state_kernel(SbrArgs A)
         }
     } else {
         const float* xs = A.xsyn + (size_t)cf * 4096 + 23 * 128;
-        for (int k = u; k < 9 * 128; k += 64) (&S.xsyn[0][0][0])[k] = ((k >> 1) & 63) < kcur ? xs[k] : 0.0f;
+        for (int k = u; k < 9 * 128; k += 64) (&S.xsyn[0][0][0])[k] = xs[k];
     }
     const float* xc = A.xcarry + (size_t)cf * kSbrCarryFloats;
-    for (int k = u; k < kSbrCarryFloats; k += 64) (&S.xcarry[0][0][0])[k] = ((k >> 1) & 63) < kcur ? xc[k] : 0.0f;
+    for (int k = u; k < kSbrCarryFloats; k += 64) (&S.xcarry[0][0][0])[k] = xc[k];
     const float* g = A.gq + (size_t)cf * 640;
     for (int k = u; k < 640; k += 64) (&S.gq[0][0][0])[k] = g[k];
 }
