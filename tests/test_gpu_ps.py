@@ -183,3 +183,12 @@ def test_c5_rejects_what_the_gpu_path_does_not_decode(name, fn, status):
         with pytest.raises(N.JaadError) as e:
             ctx.decode(b, N.PCM_BIG_ENDIAN)
     assert e.value.status == status
+
+
+@pytest.mark.slow
+def test_c5_full_shard_bitexact():
+    """One GPU's share of the 262 144-frame C5 job (32 768 frames = 256 streams x 128, the bench's
+    per-GPU workload) against the restatement."""
+    p = N.synth_params(5, n_streams=256, frames_per_stream=128)
+    got, want = _decode_both(p, N.synth_batch(p), N.PCM_BIG_ENDIAN)
+    _assert_same(got, want, N.PCM_BIG_ENDIAN)

@@ -133,9 +133,10 @@ def _header_changes(s, fps):
 
 @pytest.mark.parametrize("cfgid", [4, 5])
 def test_header_change_moves_kx_across_calls(cfgid):
-    """kx / M change inside a run and at a call boundary: the analysis stores X_low bands < kx and
-    the HF kernel X bands < kx + M only, so every reader masks by the writer's values (frame f-1's
-    kx_prev / M_prev, the slot state)."""
+    """kx / M change inside a run and at a call boundary.  Where kx rises after a frame whose last
+    envelope ended past slot 32, rows 2..7 of bands [kx_prev, kx) are frame f-1's adjusted high
+    band (sbr_save_matrix): those frames (kSbrDep) run again in an HF fix pass on frame f-1's
+    final carry rows; the call boundary hands them over through the slot state."""
     fps = 36
     p = N.synth_params(cfgid, n_streams=3, frames_per_stream=fps)
     rng = np.random.default_rng(11)
@@ -210,3 +211,12 @@ def test_downsampled_sbr(cfgid, flags):
     got, want = _decode_both(p, b, flags, cfg)
     assert got.shape == (b.n_frames, 4096 * (2 if flags & N.PCM_FLOAT32 else 1))
     _assert_same(got, want, flags)
+
+
+@pytest.mark.slow
+def test_c4_full_batch_bitexact():
+    """The whole 32 768-frame C4 batch (the bench workload, 128 streams x 256) against the restatement."""
+    p = N.synth_params(4)
+    assert p.n_streams * p.frames_per_stream == 32768
+    got, want = _decode_both(p, N.synth_batch(p), N.PCM_BIG_ENDIAN)
+    _assert_same(got, want, N.PCM_BIG_ENDIAN)
