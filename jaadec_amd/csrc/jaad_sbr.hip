@@ -28,7 +28,10 @@ struct HfLds {
     float gq_eo[64];                        // per-envelope E_orig of band m
     float den_s[64], den_e[64], den_q[64];  // per-band terms of the limiter band's den sum
     float lim_gmax[64], lim_acc1[64], lim_boost[64];  // per limiter band
+    SbrRec rec;                             // the channel-frame's record and its band tables,
+    SbrTab tab;                             // copied once (see sbr_hf_kernel)
 };
+static_assert(sizeof(SbrRec) % 4 == 0 && sizeof(SbrTab) % 4 == 0, "record copies are dword-wise");
 
 // Math.round + short clamp (S/SampleBuffer.java:190-205)
 __device__ __forceinline__ int java_round16(float s)
@@ -338,8 +341,22 @@ __global__ __launch_bounds__(256) void sbr_hf_kernel(SbrArgs A)
     HfLds& L = Ls[wave];
     const int u = lane_id();
     const int c = (int)(cf % (uint32_t)A.nch);
-    const SbrRec& R = A.recs[cf];
-    const SbrTab& T = A.tabs[R.table];
+    // The record and its band tables are read field by field all through the kernel: byte loads
+    // at wave-uniform addresses, many inside the envelope and limiter-band loops, each a global
+    // round trip the wave waits on.  One coalesced copy into the wave's LDS first; every field
+    // read after it is an LDS round trip.
+    {
+        const int table = A.recs[cf].table;  // issued beside the record copy
+        const uint32_t* rs = reinterpret_cast<const uint32_t*>(A.recs + cf);
+        uint32_t* rd = reinterpret_cast<uint32_t*>(&L.rec);
+        if (u < (int)(sizeof(SbrRec) / 4)) rd[u] = rs[u];
+        const uint32_t* ts = reinterpret_cast<const uint32_t*>(A.tabs + table);
+        uint32_t* td = reinterpret_cast<uint32_t*>(&L.tab);
+        for (int i = u; i < (int)(sizeof(SbrTab) / 4); i += 64) td[i] = ts[i];
+        wave_sync();
+    }
+    const SbrRec& R = L.rec;
+    const SbrTab& T = L.tab;
     const int kx = T.kx, M = T.M, L_E = R.L_E;
     const int first = R.t_E[0], last = R.t_E[L_E];
     const int s_lim = R.lim_bands;
