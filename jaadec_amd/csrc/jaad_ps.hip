@@ -566,12 +566,11 @@ __global__ __launch_bounds__(256) void ps_decor_kernel(SbrArgs A)
 // ---------------------------------------------------------------------------------------------
 // Walk the 32 slots of a frame for one (sub)band of group gr (inputs already in registers): H
 // advances by its delta every slot and restarts at each envelope border, as the Java interpolates.
+// hbf: the frame's H start/delta rows (in LDS); bw: border_position[0..5] as bytes
 template <typename Store>
-__device__ __forceinline__ void mix_band(const SbrArgs& A, const jaad_ps_frame& P, uint32_t f, int gr, bool rot,
-                                         const float2 (&l)[32], const float2 (&r0)[32], const float (&G)[32],
-                                         Store&& store)
+__device__ __forceinline__ void mix_band(const float* hbf, uint64_t bw, int gr, bool rot, const float2 (&l)[32],
+                                         const float2 (&r0)[32], const float (&G)[32], Store&& store)
 {
-    const float* hbf = A.hb + (size_t)f * (5 * 22 * 16);
     float H[8], D[8];
     int env = 0, next = 0;
 #pragma unroll
@@ -584,7 +583,7 @@ __device__ __forceinline__ void mix_band(const SbrArgs& A, const jaad_ps_frame& 
                 D[k] = hv[8 + k];
             }
             env++;
-            next = P.border[env];
+            next = (int)((bw >> (8 * env)) & 255u);
         }
 #pragma unroll
         for (int k = 0; k < 4; k++) H[k] += D[k];
@@ -605,8 +604,13 @@ __device__ __forceinline__ void mix_band(const SbrArgs& A, const jaad_ps_frame& 
     }
 }
 
+static_assert(offsetof(jaad_ps_frame, num_env) == 2 && offsetof(jaad_ps_frame, nr_ipdopd_par) == 3 &&
+                  offsetof(jaad_ps_frame, border) == 4 && sizeof(jaad_ps_frame) % 4 == 0,
+              "ps_mix_kernel reads the frame header as three dwords");
+
 struct MixLds {
     float2 ml[32][12], mr[32][12];
+    float4 hb[5 * 22 * 16 / 4];  // the frame's H start/delta rows (ps_decor_kernel's hb)
 };
 
 __global__ __launch_bounds__(256) void ps_mix_kernel(SbrArgs A)
@@ -617,8 +621,21 @@ __global__ __launch_bounds__(256) void ps_mix_kernel(SbrArgs A)
     if (f >= A.n_cf) return;
     if (!(A.recs[f].flags & kSbrPsOn)) return;  // X_left stays as the analysis wrote it
     MixLds& L = lds_s[wave];
-    const jaad_ps_frame& P = A.psf[f];
-    const int nr = P.nr_ipdopd_par;
+    // frame parameters and H rows read once (the slot walks below would otherwise wait on a
+    // global round trip at every envelope border): the first 12 bytes of jaad_ps_frame are
+    // (iid_mode, icc_mode, num_env, nr_ipdopd_par, border[6], reserved[2])
+    const uint32_t* ph = reinterpret_cast<const uint32_t*>(A.psf + f);
+    const uint32_t w0 = __builtin_amdgcn_readfirstlane(ph[0]);
+    const uint64_t bw = (uint64_t)__builtin_amdgcn_readfirstlane(ph[1]) |
+                        ((uint64_t)__builtin_amdgcn_readfirstlane(ph[2]) << 32);
+    const int nr = (int)(w0 >> 24), num_env = (int)((w0 >> 16) & 255u);
+    {
+        const float4* src = reinterpret_cast<const float4*>(A.hb + (size_t)f * (5 * 22 * 16));
+        const int n4 = (num_env < 5 ? num_env : 5) * (22 * 16 / 4);
+        for (int i = u; i < n4; i += 64) L.hb[i] = src[i];
+        wave_sync();
+    }
+    const float* hbf = reinterpret_cast<const float*>(L.hb);
     const float* pg = A.pg + (size_t)f * 640;
     float2* xl = reinterpret_cast<float2*>(A.xps + (size_t)f * 8192);
     float2* xr = xl + 2048;
@@ -640,7 +657,7 @@ __global__ __launch_bounds__(256) void ps_mix_kernel(SbrArgs A)
                 r[n] = xr[n * 64 + u];
                 G[n] = pg[n * 20 + bk];
             }
-            mix_band(A, P, f, gr, bk < nr, l, r, G,
+            mix_band(hbf, bw, gr, bk < nr, l, r, G,
                      [&](int n, float2 a, float2 b) { xl[n * 64 + u] = a; xr[n * 64 + u] = b; });
         }
         if (u < 10) {
@@ -651,7 +668,7 @@ __global__ __launch_bounds__(256) void ps_mix_kernel(SbrArgs A)
                 r[n] = hr[n * 12 + sb];
                 G[n] = pg[n * 20 + bk];
             }
-            mix_band(A, P, f, u, bk < nr, l, r, G,
+            mix_band(hbf, bw, u, bk < nr, l, r, G,
                      [&](int n, float2 a, float2 b) { L.ml[n][sb] = a; L.mr[n][sb] = b; });
         } else if (u < 12) {  // sub-bands 4, 5: zero after grouping, never decorrelated or mixed
             const int sb = u - 6;
