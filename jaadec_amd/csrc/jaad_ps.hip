@@ -265,10 +265,37 @@ __device__ __forceinline__ float magnitude_c(float re, float im)
 // over every envelope of every frame of the run.  The shared phase_hist counter flips once per
 // (group, envelope) with bk < nr_ipdopd_par; those groups are always 0 .. nr + 1, so the
 // counter at (gr, env) is phase_hist(frame start) + gr * num_env + env.
-__device__ void ps_param_scan(const SbrArgs& A, const uint32_t* fl, uint32_t nfr, PsState& S, bool fresh, int u)
+// The walk is sequential over the run's frames and each (envelope, group) step reads the frame
+// record and then table entries it indexes: the record of frame j+1 is fetched into registers
+// while frame j is scanned and parked in LDS (pbuf, double-buffered) at its end; K is the
+// block's LDS copy of PsConst.
+constexpr int kPsFrameDw = (int)(sizeof(jaad_ps_frame) / 4);
+constexpr int kPsFrameDwPerLane = (kPsFrameDw + 19) / 20;
+static_assert(sizeof(jaad_ps_frame) % 4 == 0, "PS records are copied dword-wise");
+
+__device__ void ps_param_scan(const SbrArgs& A, const PsConst& K, const uint32_t* fl, uint32_t nfr, PsState& S,
+                              bool fresh, int u, uint32_t (*pbuf)[kPsFrameDw])
 {
     if (u >= 20) return;
-    const PsConst& K = *A.psc;
+    uint32_t pre[kPsFrameDwPerLane];
+    auto fetch = [&](uint32_t f) {
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(A.psf + f);
+#pragma unroll
+        for (int i = 0; i < kPsFrameDwPerLane; i++) {
+            const int d = u + 20 * i;
+            pre[i] = d < kPsFrameDw ? src[d] : 0u;
+        }
+    };
+    auto park = [&](uint32_t* dst) {
+#pragma unroll
+        for (int i = 0; i < kPsFrameDwPerLane; i++) {
+            const int d = u + 20 * i;
+            if (d < kPsFrameDw) dst[d] = pre[i];
+        }
+    };
+    fetch(fl[0]);
+    park(pbuf[0]);
+    wave_sync();
     const int bk = u;
     const int grs[2] = {bk == 0 ? 1 : (bk == 1 ? 0 : bk + 2), bk == 0 ? 2 : (bk == 1 ? 3 : -1)};
     float hp[2][8];
@@ -285,9 +312,11 @@ __device__ void ps_param_scan(const SbrArgs& A, const uint32_t* fl, uint32_t nfr
             opd[ph][c] = fresh ? 0.0f : S.opd_prev[bk][ph][c];
         }
     int phase = fresh ? 0 : S.phase_hist;
+    uint32_t f = fl[0], f_next = nfr > 1 ? fl[1] : 0u;
     for (uint32_t j = 0; j < nfr; j++) {
-        const uint32_t f = fl[j];
-        const jaad_ps_frame& P = A.psf[f];
+        if (j + 1 < nfr) fetch(f_next);  // lands during this frame's scan
+        const uint32_t f_after = j + 2 < nfr ? fl[j + 2] : 0u;
+        const jaad_ps_frame& P = *reinterpret_cast<const jaad_ps_frame*>(pbuf[j & 1]);
         const int E = P.num_env, nr = P.nr_ipdopd_par;
         const bool elig = bk < nr;
         float* hbf = A.hb + (size_t)f * (5 * 22 * 16);
@@ -364,6 +393,13 @@ __device__ void ps_param_scan(const SbrArgs& A, const uint32_t* fl, uint32_t nfr
             }
         }
         if (nr) phase = (phase + (nr + 2) * E) & 1;
+        if (j + 1 < nfr) {
+            wave_sync();  // every lane is done with buffer (j + 1) & 1's previous frame
+            park(pbuf[(j + 1) & 1]);
+            wave_sync();
+        }
+        f = f_next;
+        f_next = f_after;
     }
     for (int g = 0; g < 2; g++)
         if (grs[g] >= 0)
@@ -446,8 +482,17 @@ __global__ __launch_bounds__(256) void ps_decor_kernel(SbrArgs A)
     const uint32_t nfr = A.runs[2 * run + 1];
     if (nfr == 0) return;
     const int wave = threadIdx.x >> 6, u = lane_id();
+    // PsConst in LDS: the parameter scan indexes its tables at every (frame, envelope, group)
+    __shared__ PsConst Ks;
+    __shared__ uint32_t pbuf[2][kPsFrameDw];
+    {
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(A.psc);
+        uint32_t* dst = reinterpret_cast<uint32_t*>(&Ks);
+        for (int i = threadIdx.x; i < (int)(sizeof(PsConst) / 4); i += 256) dst[i] = src[i];
+    }
+    __syncthreads();
     PsState& S = A.pss[A.recs[fl[0]].slot];
-    const PsConst& K = *A.psc;
+    const PsConst& K = Ks;
     const bool fresh = S.init == 0;
 
     if (wave == 0) {
@@ -527,7 +572,7 @@ __global__ __launch_bounds__(256) void ps_decor_kernel(SbrArgs A)
 #pragma unroll
         for (int k = 0; k < 14; k++) S.aph[k][u] = ap[k];
     } else if (wave == 3) {
-        ps_param_scan(A, fl, nfr, S, fresh, u);
+        ps_param_scan(A, K, fl, nfr, S, fresh, u, pbuf);
     } else {
         // ---- transient detector (lane = parameter band), PSImpl.java:238-270 ----
         if (u >= 20) return;

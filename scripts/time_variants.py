@@ -10,7 +10,8 @@ import sys, time, numpy as np, torch
 sys.path.insert(0, "%s")
 from jaadec_amd import native as N
 cfgid = int(sys.argv[1]) if len(sys.argv) > 1 else 2
-p = N.synth_params(cfgid); b = N.synth_batch(p); cfg = N.cfg_for(p)
+ns = int(sys.argv[2]) if len(sys.argv) > 2 else 0  # streams (0: the config's default)
+p = N.synth_params(cfgid, n_streams=ns) if ns else N.synth_params(cfgid); b = N.synth_batch(p); cfg = N.cfg_for(p)
 dev = torch.device("cuda", 0)
 t = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1)).to(dev)
 d = {"q": t(b.q), "sf": t(b.sf), "cb": t(b.cb), "ics": t(b.ics)}
@@ -33,9 +34,11 @@ def main():
     libs = sorted((ROOT / ".tmp/exp").glob("lib_*.so"))
     cfgid = sys.argv[1] if len(sys.argv) > 1 else "2"
     rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 1
+    streams = sys.argv[3] if len(sys.argv) > 3 else "0"
     for lib in [l for _ in range(rounds) for l in libs]:  # alternate: clock drift hits all alike
         env = dict(os.environ, JAAD_LIB=str(lib))
-        r = subprocess.run([sys.executable, "-c", CHILD, cfgid], env=env, capture_output=True, text=True, timeout=300)
+        r = subprocess.run([sys.executable, "-c", CHILD, cfgid, streams], env=env, capture_output=True, text=True,
+                           timeout=300)
         out = r.stdout.strip().splitlines()
         print(f"{lib.stem:28s} {out[-1] if out else 'ERR ' + r.stderr[-300:]} ms", flush=True)
 
