@@ -324,7 +324,7 @@ __global__ __launch_bounds__(256) void sbr_analysis_kernel(SbrArgs A)
 // phase 0: full; phase 1: gains and G/Q ring only; phase 2: full, ring from frame f-1
 // ---------------------------------------------------------------------------------------------
 template <int kPhase>
-__global__ __launch_bounds__(256) void sbr_hf_kernel(SbrArgs A)
+__global__ __launch_bounds__(256, 3) void sbr_hf_kernel(SbrArgs A)
 {
     __shared__ HfLds Ls[kWavesPerBlock];
     __shared__ float2 noise_s[512];  // NoiseTable.NOISE_TABLE (A/sbr/NoiseTable.java:6), read per slot
