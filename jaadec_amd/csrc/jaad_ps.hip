@@ -494,6 +494,9 @@ __global__ __launch_bounds__(256) void ps_decor_kernel(SbrArgs A)
     PsState& S = A.pss[A.recs[fl[0]].slot];
     const PsConst& K = Ks;
     const bool fresh = S.init == 0;
+#ifdef JAAD_DECOR_ONLY  // timing probe: one of the four recurrences alone (output invalid)
+    if (wave != JAAD_DECOR_ONLY) return;
+#endif
 
     if (wave == 0) {
         // ---- QMF bands (lane = sb): all-pass below 23, 14-slot delay to 34, 1-slot above ----
