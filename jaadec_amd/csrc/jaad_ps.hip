@@ -154,16 +154,26 @@ __global__ __launch_bounds__(256) void ps_analysis_kernel(SbrArgs A)
         const float2* xc = x_carry_prev(A, R, f);
         const float2* xn = reinterpret_cast<const float2*>(A.xcarry + (size_t)f * kSbrCarryFloats);
         float2* xo = reinterpret_cast<float2*>(A.xps + (size_t)f * 8192);
+        // every row load is issued before the first store: xo might alias the sources as far as
+        // the compiler knows, so a load-store-load loop waits out one global round trip per row
+        const bool ps_on = (R.flags & kSbrPsOn) != 0;
+        float2 v[38];
+#pragma unroll
+        for (int l = 0; l < 38; l++) {
+            const float2* src = l >= 32 ? xn + (l - 30) * 64 : l < t0 ? xc + (l + 2) * 64 : xs + l * 64;
+            const bool ok = l >= 32 ? u < 5 && ps_on : l < t0 ? u < kprev : true;
+            const float2 t = src[ok ? u : 0];
+            v[l] = ok ? t : make_float2(0.0f, 0.0f);
+        }
+#pragma unroll
         for (int l = 0; l < 32; l++) {
-            float2 v;
-            if (l < t0) v = u < kprev ? xc[(l + 2) * 64 + u] : make_float2(0.0f, 0.0f);
-            else v = xs[l * 64 + u];
-            L.xl[l][u] = v;
-            xo[l * 64 + u] = v;
+            L.xl[l][u] = v[l];
+            xo[l * 64 + u] = v[l];
         }
         // a frame without PS data only hands its X (qmfs0 input) to the synthesis
-        if (!(R.flags & kSbrPsOn)) return;
-        for (int l = 32; l < 38; l++) L.xl[l][u] = u < 5 ? xn[(l - 30) * 64 + u] : make_float2(0.0f, 0.0f);
+        if (!ps_on) return;
+#pragma unroll
+        for (int l = 32; l < 38; l++) L.xl[l][u] = v[l];
         if (u < 36) {
             // Filterbank.buffer as the previous PS frame left it (frames without PS data do not
             // run the hybrid analysis)
