@@ -153,18 +153,20 @@ def test_header_change_moves_kx_across_calls(cfgid):
         _assert_same(g2[13 * r:13 * (r + 1)], want[fb[r] + 23:fb[r + 1]], N.PCM_FLOAT32)
 
 
-@pytest.mark.parametrize("cfgid", [4, 5])
-def test_dropped_patch_with_trailing_borders(cfgid):
+@pytest.mark.parametrize("cfgid,smoothing", [(4, 1), (5, 1), (4, 0)])
+def test_dropped_patch_with_trailing_borders(cfgid, smoothing):
     """A header whose patch_construction drops bands (start_freq 0, stop_freq 7, freq_scale 0 at
     48 kHz: kx 7, M 31, the patches generate 21 bands) with envelopes ending past slot 32: the
     bands without patch carry frame f-1's adjusted rows into the envelope estimate, chains of
-    kSbrDep frames run through the HF fix passes."""
+    kSbrDep frames run through the HF fix passes.  With G/Q smoothing (bs_smoothing_mode 0) the
+    frame after a recomputed one is recomputed too (its smoothing ring came from that frame)."""
     fps = 36
     p = N.synth_params(cfgid, n_streams=3, frames_per_stream=fps)
     rng = np.random.default_rng(5)
 
     def edit(s):
         s["hdr"]["start_freq"], s["hdr"]["stop_freq"], s["hdr"]["freq_scale"] = 0, 7, 0
+        s["hdr"]["smoothing_mode"] = smoothing
         _var_grids(s, rng)
 
     b = _edit(N.synth_batch(p), edit)
