@@ -259,7 +259,9 @@ int jaad_decode_batch_device(jaad_ctx* ctx, const jaad_batch* batch, void* pcm_d
                              uint32_t flags, void* hip_stream);
 int jaad_wait(jaad_ctx* ctx);
 
-/* Per-slot persistent DSP state (seek/resume, A/syntax/ICStream.java:47,56 overlap, ...).   */
+/* Per-slot persistent DSP state (seek/resume, A/syntax/ICStream.java:47,56 overlap, ...).
+ * The blob is opaque and specific to the library build that wrote it (its layout follows the
+ * kernels' state records): resume within one deployment, do not persist it across upgrades. */
 size_t jaad_state_bytes(const jaad_ctx* ctx);
 int jaad_state_export(jaad_ctx* ctx, uint32_t slot, void* buf, size_t bytes);
 int jaad_state_import(jaad_ctx* ctx, uint32_t slot, const void* buf, size_t bytes);
