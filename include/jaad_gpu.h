@@ -181,11 +181,29 @@ typedef struct jaad_ps_frame {
     uint8_t pad[6];
 } jaad_ps_frame;                   /* 528 bytes */
 
+/* jaad_sbr_frame.status */
+enum {
+    /* sbr_data decoded (SBR.decode sets valid, A/sbr/SBR.java:179-184).  Before the stream's first
+       SBR header the reference marks the element valid too and runs the QMF banks on the low band
+       only (Channel.process_channel with hdr == null, A/sbr/Channel.java:589-617): the library
+       does the same for such frames (header_present = 0 and no header seen yet on the slot).  */
+    JAAD_SBR_OK = 0,
+    /* the element has no usable SBR data this frame: no SBR payload followed it, or sbr_data
+       failed (a grid whose borders do not fit, A/sbr/Channel.java:418-432).  The reference then
+       skips SBR entirely -- its state stays as the last processed frame left it -- and outputs
+       the core upsampled by sample repetition (SBR.upsample, A/sbr/SBR.java:302-309, which never
+       writes index 1; A/syntax/CPE.java:196-204, SCE.java:123-132).  With a downsampled-SBR
+       configuration (output rate = core rate) the core is output as it is.                     */
+    JAAD_SBR_UPSAMPLE = 1
+};
+
 typedef struct jaad_sbr_frame {
     uint8_t header_present;        /* bs_header_flag: hdr below is this frame's sbr_header           */
     uint8_t coupling;              /* bs_coupling (CPE only)                                         */
     uint8_t ps_present;            /* PS data decoded for this frame (SBR1.isPSUsed, A/sbr/SBR1.java:136) */
-    uint8_t reserved;
+    uint8_t status;                /* JAAD_SBR_OK / JAAD_SBR_UPSAMPLE (the rest of the record is then
+                                      ignored except header_present/hdr, which must not change the
+                                      slot's tables: the reference would lose that reset)         */
     jaad_sbr_header hdr;
     jaad_sbr_channel ch[2];        /* ch[1] unused for an SCE                                        */
     jaad_ps_frame ps;              /* valid when ps_present                                          */

@@ -39,7 +39,12 @@ extern "C" {
  * 29 (PS) with an LC core; frameLengthFlag = 1 (960-sample frames) is rejected as the
  * reference rejects it (JAAD_ERR_UNSUPPORTED).  A mono AOT 5 stream gets ps = 1: the reference
  * has PS enabled by default (A/DecoderConfig.java:36, A/sbr/SBR1.java:62-73), so PS data it
- * meets is applied, and frames without it duplicate the SBR channel as ps = 0 would. */
+ * meets is applied, and frames without it duplicate the SBR channel as ps = 0 would.  An AOT 2
+ * config with the backward-compatible sync extension (0x2B7, sbrPresent, extension rate;
+ * readSyncExtension A/DecoderConfig.java:260-291) is explicit SBR as well.  Without it the
+ * output rate is the core rate (A/DecoderConfig.java:180): SBR found later in the frames
+ * (implicit signalling) runs downsampled for such a decoder, unlike one created from an ADTS
+ * header (AudioDecoderInfo), whose output rate is doubled (DecoderConfig.setSBRPresent :124-135). */
 int jaad_asc_parse(const uint8_t* asc, size_t bytes, jaad_stream_cfg* cfg);
 
 /* ADTS fixed + variable header (S/adts/ADTSFrame.java:48-111) */

@@ -35,6 +35,10 @@ typedef struct jaad_synth_params {
     uint8_t sbr;              /* 1: also emit SBR records (jaad_synth_sbr), C4; 2: SBR + PS, C5 */
     uint8_t sbr_level;        /* centre of the envelope-scalefactor walk, 3 dB units        */
     uint32_t pns_state0;      /* static ICStream.randomState before the first ch-frame       */
+    uint8_t coupling_percent; /* SBR CPE: % of frames with bs_coupling (balance-coded channel 1) */
+    uint8_t upsample_percent; /* SBR: % of frames without usable SBR data (JAAD_SBR_UPSAMPLE)   */
+    uint8_t nohdr_frames;     /* SBR: leading frames of each stream before its first SBR header */
+    uint8_t reserved;
 } jaad_synth_params;
 
 /* defaults for a BASELINE.json config id (1..5: C1 mono 44.1k, C2, C3, C4 HE-AAC v1, C5 HE-AAC v2) */
@@ -52,8 +56,11 @@ int jaad_synth_generate(const jaad_synth_params* p, int16_t* q, uint8_t* sf, uin
 /* SBR records (one jaad_sbr_frame per frame, stream-major like jaad_synth_generate) for the C4
  * workload: header every frame with the Header.java defaults, start_freq 5,
  * stop_freq 9, xover 0; FIXFIX grids with 1 or 2 envelopes; envelope/noise scalefactors as
- * bounded random walks; invf_mode uniform; sinusoids rare; no coupling.  Every band of E[][64]
- * and Q[][8] is filled (the decoder reads only n[f] / N_Q of them). */
+ * bounded random walks; invf_mode uniform; sinusoids rare.  coupling_percent of the CPE frames
+ * are coupled (channel 1 carries the coupled grid and even balance values 0..24, as
+ * SBR2.sbr_data leaves them), upsample_percent of the frames are JAAD_SBR_UPSAMPLE and the first
+ * nohdr_frames frames of a stream carry no header (none seen yet).  Every band of E[][64] and
+ * Q[][8] is filled (the decoder reads only n[f] / N_Q of them). */
 int jaad_synth_sbr(const jaad_synth_params* p, jaad_sbr_frame* out, int threads);
 
 #ifdef __cplusplus

@@ -204,6 +204,7 @@ struct jaad_ctx {
     std::unique_ptr<WorkerPool> workers;
     std::vector<SbrChunk> sbr_chunks;
     std::vector<uint32_t> sbr_last;
+    std::vector<uint32_t> sbr_rbegin, sbr_fmap, sbr_ups;  // record plan of the call (launch_sbr_stage)
     float* sbr_dbg = nullptr;
     // ---- PS (cfg.ps) ----
     PsState* d_ps_state = nullptr;               // [slot]
@@ -225,11 +226,16 @@ void build_lds_tables(int sf_index, LdsTables* t, GlobalTables* gt)
     std::memcpy(t->win_short[0], JAAD_SINE_128, sizeof(t->win_short[0]));
     std::memcpy(t->win_short[1], JAAD_KBD_128, sizeof(t->win_short[1]));
     std::memcpy(t->mdct_l, JAAD_MDCT_TABLE_2048, sizeof(t->mdct_l));
+    for (int s = 0; s < 8; s++)
+        for (int u = 0; u < 64; u++) {
+            t->mdct_post[s][u][0] = JAAD_MDCT_TABLE_2048[lane_pos_host(u) + 64 * s][0];
+            t->mdct_post[s][u][1] = JAAD_MDCT_TABLE_2048[lane_pos_host(u) + 64 * s][1];
+        }
     // 512-point IFFT twiddles roots[k*m] (FFT.java:116-120, inverse column 1) pre-arranged per
-    // register pass: pass 1 (i = 4, m = 64); pass 2 lane b = u&7: slot 0 -> stage 8 (m = 32, k = b),
-    // slots 1,2 -> stage 16 (m = 16, k = b + 8e), slots 3..6 -> stage 32 (m = 8, k = b + 8s);
-    // pass 3 lane u: slot 0 -> stage 64 (m = 4, k = u), 1,2 -> stage 128 (m = 2, k = u + 64e),
-    // 3..6 -> stage 256 (m = 1, k = u + 64s)
+    // register pass: pass 1 (i = 4, m = 64); pass 2 by b = position mod 8: slot 0 -> stage 8
+    // (m = 32, k = b), slots 1,2 -> stage 16 (m = 16, k = b + 8e), slots 3..6 -> stage 32 (m = 8,
+    // k = b + 8s); pass 3 by lane u, position p = lane_pos(u): slot 0 -> stage 64 (m = 4, k = p),
+    // 1,2 -> stage 128 (m = 2, k = p + 64e), 3..6 -> stage 256 (m = 1, k = p + 64s)
     auto root = [](int idx, float* d) {
         d[0] = JAAD_FFT_TABLE_512[idx][0];
         d[1] = JAAD_FFT_TABLE_512[idx][1];
@@ -240,19 +246,20 @@ void build_lds_tables(int sf_index, LdsTables* t, GlobalTables* gt)
         for (int e = 0; e < 2; e++) root(16 * (b + 8 * e), t->tw2[1 + e][b]);
         for (int s = 0; s < 4; s++) root(8 * (b + 8 * s), t->tw2[3 + s][b]);
     }
-    for (int u = 0; u < 64; u++) {  // pass 3: j = 0 -> 4u, j = 1,2 -> 2(u + 64e), j = 3..6 -> u + 64s
-        root(4 * u, t->tw3[0][u]);
-        for (int e = 0; e < 2; e++) root(2 * (u + 64 * e), t->tw3[1 + e][u]);
-        for (int s = 0; s < 4; s++) root(u + 64 * s, t->tw3[3 + s][u]);
+    for (int u = 0; u < 64; u++) {  // pass 3: j = 0 -> 4p, j = 1,2 -> 2(p + 64e), j = 3..6 -> p + 64s
+        const int p = lane_pos_host(u);
+        root(4 * p, t->tw3[0][u]);
+        for (int e = 0; e < 2; e++) root(2 * (p + 64 * e), t->tw3[1 + e][u]);
+        for (int s = 0; s < 4; s++) root(p + 64 * s, t->tw3[3 + s][u]);
     }
     std::memcpy(t->mdct_s, JAAD_MDCT_TABLE_128, sizeof(t->mdct_s));
     for (int k = 0; k < 32; k++) {
         t->roots_s[k][0] = JAAD_FFT_TABLE_64[k][0];
         t->roots_s[k][1] = JAAD_FFT_TABLE_64[k][1];
     }
-    for (int i = 0; i < 256; i++) {
-        t->sf_gain[i] = JAAD_SCALEFACTOR_TABLE[100 + i];
-        const int q = i - 128;  // float of (q>0 ? IQ[q] : -IQ[-q]): q = 0 gives -0.0
+    for (int i = 0; i < 256; i++) t->sf_gain[i] = JAAD_SCALEFACTOR_TABLE[100 + i];
+    for (int i = 0; i < 2 * kIqHead; i++) {
+        const int q = i - kIqHead;  // float of (q>0 ? IQ[q] : -IQ[-q]): q = 0 gives -0.0
         t->iq_signed[i] = q > 0 ? JAAD_IQ_TABLE[q] : -JAAD_IQ_TABLE[-q];
     }
     std::memcpy(gt->tns_coef[0], JAAD_TNS_COEF_0_3, sizeof(JAAD_TNS_COEF_0_3));
@@ -468,34 +475,61 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
     const int nch = ctx->nch;
     const bool ps = ctx->cfg.ps != 0;
     const int och = ps ? 2 : nch;  // channels of the QMF synthesis
-    const size_t nf = b->n_frames, ncf = nf * nch;
+    const size_t nf = b->n_frames;
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
 
-    // chunk plan (depends on the runs only)
+    // The SBR stages run on the frames whose SBR data is usable, compacted per run ("records"):
+    // a JAAD_SBR_UPSAMPLE frame skips SBR in the reference (A/syntax/CPE.java:196-204,
+    // SCE.java:123-132), so the record before and after it are consecutive as far as the SBR
+    // state goes.  Its PCM is the upsampled core (sbr_upsample_kernel).
+    std::vector<uint32_t>& rbeg = ctx->sbr_rbegin;  // [run + 1] first record of each run
+    std::vector<uint32_t>& fmap = ctx->sbr_fmap;    // record -> batch frame
+    std::vector<uint32_t>& ups = ctx->sbr_ups;      // upsampled batch frames
+    rbeg.assign(b->n_runs + 1, 0);
+    fmap.clear();
+    ups.clear();
+    for (uint32_t r = 0; r < b->n_runs; r++) {
+        rbeg[r] = (uint32_t)fmap.size();
+        for (uint32_t f = b->frame_begin[r]; f < b->frame_begin[r + 1]; f++) {
+            if (b->sbr[f].status == JAAD_SBR_UPSAMPLE) ups.push_back(f);
+            else if (b->sbr[f].status == JAAD_SBR_OK) fmap.push_back(f);
+            else {
+                ctx->err = "SBR status of frame " + std::to_string(f);
+                return JAAD_ERR_INVALID_ARG;
+            }
+        }
+    }
+    rbeg[b->n_runs] = (uint32_t)fmap.size();
+    const size_t nr = fmap.size(), ncf = nr * nch;  // records, record ch-frames
+    const bool identity = ups.empty();
+
+    // chunk plan (records of each run)
     ctx->sbr_chunks.clear();
     ctx->sbr_last.clear();
     ctx->ps_runs.clear();
     for (uint32_t r = 0; r < b->n_runs; r++) {
-        const uint32_t f0 = b->frame_begin[r], f1 = b->frame_begin[r + 1];
-        if (f1 == f0) continue;  // empty run: the slot state stays as it is
+        const uint32_t i0 = rbeg[r], i1 = rbeg[r + 1];
+        if (i1 == i0) continue;  // no SBR frame in this call: the slot's SBR state stays as it is
         for (int c = 0; c < och; c++)
-            for (uint32_t f = f0; f < f1; f += kSbrSynFrames) {
-                const uint32_t n = f1 - f < (uint32_t)kSbrSynFrames ? f1 - f : (uint32_t)kSbrSynFrames;
-                ctx->sbr_chunks.push_back(SbrChunk{f, (uint16_t)n, (uint8_t)c, 0});
+            for (uint32_t i = i0; i < i1; i += kSbrSynFrames) {
+                const uint32_t n = i1 - i < (uint32_t)kSbrSynFrames ? i1 - i : (uint32_t)kSbrSynFrames;
+                ctx->sbr_chunks.push_back(SbrChunk{i, (uint16_t)n, (uint8_t)c, 0});
             }
-        for (int c = 0; c < nch; c++) ctx->sbr_last.push_back((f1 - 1) * nch + c);
+        for (int c = 0; c < nch; c++) ctx->sbr_last.push_back((i1 - 1) * nch + c);
         if (ps) {
-            ctx->ps_runs.push_back(f0);
-            ctx->ps_runs.push_back(f1 - f0);
+            ctx->ps_runs.push_back(i0);
+            ctx->ps_runs.push_back(i1 - i0);
         }
     }
     const size_t o_recs = 0, o_psf = al(ncf * sizeof(SbrRec));
-    const size_t o_chunks = al(o_psf + (ps ? nf * sizeof(jaad_ps_frame) : 0));
+    const size_t o_chunks = al(o_psf + (ps ? nr * sizeof(jaad_ps_frame) : 0));
     const size_t o_last = al(o_chunks + ctx->sbr_chunks.size() * sizeof(SbrChunk));
     const size_t o_runs = al(o_last + ctx->sbr_last.size() * sizeof(uint32_t));
     const size_t o_pslist = al(o_runs + ctx->ps_runs.size() * sizeof(uint32_t));
-    const size_t o_fix = al(o_pslist + (ps ? nf * sizeof(uint32_t) : 0));
-    const size_t n1 = al(o_fix + ncf * sizeof(uint32_t));
+    const size_t o_fix = al(o_pslist + (ps ? nr * sizeof(uint32_t) : 0));
+    const size_t o_fmap = al(o_fix + ncf * sizeof(uint32_t));
+    const size_t o_ups = al(o_fmap + (identity ? 0 : nr * sizeof(uint32_t)));
+    const size_t n1 = al(o_ups + ups.size() * sizeof(uint32_t));
 
     // JAAD_TRACE_HOST=1: per-call host timings of this stage on stderr (tuning aid)
     static const bool trace = std::getenv("JAAD_TRACE_HOST") != nullptr;
@@ -513,6 +547,8 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
         std::memcpy(h1 + o_chunks, ctx->sbr_chunks.data(), ctx->sbr_chunks.size() * sizeof(SbrChunk));
     if (!ctx->sbr_last.empty())
         std::memcpy(h1 + o_last, ctx->sbr_last.data(), ctx->sbr_last.size() * sizeof(uint32_t));
+    if (!identity) std::memcpy(h1 + o_fmap, fmap.data(), nr * sizeof(uint32_t));
+    if (!ups.empty()) std::memcpy(h1 + o_ups, ups.data(), ups.size() * sizeof(uint32_t));
     uint32_t* ps_runs_h = reinterpret_cast<uint32_t*>(h1 + o_runs);
     uint32_t* ps_list_h = reinterpret_cast<uint32_t*>(h1 + o_pslist);
 
@@ -525,8 +561,7 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
     for (int t = 0; t <= nt; t++) rr[t] = (uint32_t)((uint64_t)b->n_runs * t / nt);
     std::vector<size_t> rbase(nt + 1, 0);  // region offsets in floats
     for (int t = 0; t < nt; t++)
-        rbase[t + 1] = rbase[t] + ((size_t)(b->frame_begin[rr[t + 1]] - b->frame_begin[rr[t]]) * nch *
-                                       SbrHost::kMaxEorig + 63) / 64 * 64;
+        rbase[t + 1] = rbase[t] + ((size_t)(rbeg[rr[t + 1]] - rbeg[rr[t]]) * nch * SbrHost::kMaxEorig + 63) / 64 * 64;
     const auto& tabs = ctx->sbr_host->tabs();
     const size_t o_tabs = al(rbase[nt] * sizeof(float) + sizeof(float));
     const size_t n2 = o_tabs + SbrHost::kMaxTables * sizeof(SbrTab);
@@ -550,44 +585,57 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
             saved[r] = hs;
             saved_ok[r] = 1;
             const uint32_t fe = b->frame_begin[r + 1];
+            uint32_t i = rbeg[r];  // record of frame f
             for (uint32_t f = b->frame_begin[r]; f < fe; f++) {
                 if (f + 2 < fe)  // the records are large and sparse-read: pull frame f+2 in early
                     for (size_t o = 0; o < sizeof(jaad_sbr_frame); o += 64)
                         __builtin_prefetch(reinterpret_cast<const char*>(&b->sbr[f + 2]) + o);
+                const jaad_sbr_frame& F = b->sbr[f];
+                if (F.status == JAAD_SBR_UPSAMPLE) {
+                    // the reference would still take this frame's header: a table reset it then
+                    // never applies (the next frame's reset flag is read afresh, A/sbr/SBR.java:168)
+                    if (F.header_present && (!hs.have_hdr || SbrHost::header_changes(hs.hdr, F.hdr))) {
+                        rcs[t] = JAAD_ERR_UNSUPPORTED;
+                        bad[t] = (int)f;
+                        break;
+                    }
+                    continue;
+                }
                 if (ps) {
-                    if (!ps_frame_ok(b->sbr[f])) {
+                    if (!ps_frame_ok(F)) {
                         rcs[t] = JAAD_ERR_BITSTREAM;
                         bad[t] = (int)f;
                         break;
                     }
-                    if (b->sbr[f].ps_present) psf[f] = b->sbr[f].ps;
+                    if (F.ps_present) psf[i] = F.ps;
                 }
-                SbrRec* rec = &recs[(size_t)f * nch];
-                int rc = ctx->sbr_host->frame(hs, b->sbr[f], nch, f == b->frame_begin[r], b->stream_slot[r], rec,
-                                              region, epos, (uint32_t)rbase[t]);
+                SbrRec* rec = &recs[(size_t)i * nch];
+                int rc = ctx->sbr_host->frame(hs, F, nch, i == rbeg[r], b->stream_slot[r], rec, region, epos,
+                                              (uint32_t)rbase[t]);
                 if (rc) {
                     rcs[t] = rc;
                     bad[t] = (int)f;
                     break;
                 }
-                if (ps) {  // PS frames of the run (the PS kernels walk only these)
-                    if (f == b->frame_begin[r]) last_ps = UINT32_MAX;
+                if (ps) {  // PS records of the run (the PS kernels walk only these)
+                    if (i == rbeg[r]) last_ps = UINT32_MAX;
                     rec->ps_back = 0;
                     if (last_ps != UINT32_MAX) {
-                        if (f - last_ps > 0xffffu) {
-                            rcs[t] = JAAD_ERR_UNSUPPORTED;  // > 65535 frames without PS data in one call
+                        if (i - last_ps > 0xffffu) {
+                            rcs[t] = JAAD_ERR_UNSUPPORTED;  // > 65535 records without PS data in one call
                             bad[t] = (int)f;
                             break;
                         }
-                        rec->ps_back = (uint16_t)(f - last_ps);
+                        rec->ps_back = (uint16_t)(i - last_ps);
                     }
-                    if (b->sbr[f].ps_present) {
+                    if (F.ps_present) {
                         rec->flags |= kSbrPsOn;
-                        last_ps = f;
+                        last_ps = i;
                     }
                 }
                 sm |= (rec[0].flags & kSbrSmooth) != 0;
                 for (int c = 0; c < nch; c++) dp |= (rec[c].flags & kSbrDep) != 0;
+                i++;
             }
         }
         used[t] = epos;
@@ -609,14 +657,14 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
         smoothing |= smooth[t] != 0;
         any_dep |= deps[t] != 0;
     }
-    if (ps) {  // per run: (offset, count) of its PS frames in ps_list
+    if (ps) {  // per run: (offset, count) of its PS records in ps_list
         uint32_t np = 0, ri = 0;
         for (uint32_t r = 0; r < b->n_runs; r++) {
-            const uint32_t f0 = b->frame_begin[r], f1 = b->frame_begin[r + 1];
-            if (f1 == f0) continue;
+            const uint32_t i0 = rbeg[r], i1 = rbeg[r + 1];
+            if (i1 == i0) continue;
             const uint32_t off = np;
-            for (uint32_t f = f0; f < f1; f++)
-                if (b->sbr[f].ps_present) ps_list_h[np++] = f;
+            for (uint32_t i = i0; i < i1; i++)
+                if (recs[i].flags & kSbrPsOn) ps_list_h[np++] = i;
             ps_runs_h[2 * ri] = off;
             ps_runs_h[2 * ri + 1] = np - off;
             ri++;
@@ -634,9 +682,9 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
         depth.assign(ncf, 0);
         uint32_t max_d = 0;
         for (uint32_t r = 0; r < b->n_runs; r++)
-            for (uint32_t f = b->frame_begin[r] + 1; f < b->frame_begin[r + 1]; f++)
+            for (uint32_t i = rbeg[r] + 1; i < rbeg[r + 1]; i++)
                 for (int c = 0; c < nch; c++) {
-                    const size_t cf = (size_t)f * nch + c;
+                    const size_t cf = (size_t)i * nch + c;
                     const uint8_t fl = recs[cf].flags;
                     const uint32_t dp = depth[cf - nch];
                     if ((fl & kSbrDep) || ((fl & kSbrSmooth) && !(fl & kSbrReset) && dp > 0)) {
@@ -660,11 +708,11 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
     HIPCHK(ctx->d_xcarry.ensure(ncf * kSbrCarryFloats * sizeof(float) + 256));
     HIPCHK(ctx->d_gq.ensure(ncf * 640 * sizeof(float) + 256));
     if (ps) {
-        HIPCHK(ctx->d_xps.ensure(nf * 8192 * sizeof(float) + 256));
-        HIPCHK(ctx->d_xhl.ensure(nf * 768 * sizeof(float) + 256));
-        HIPCHK(ctx->d_xhr.ensure(nf * 768 * sizeof(float) + 256));
-        HIPCHK(ctx->d_pg.ensure(nf * 640 * sizeof(float) + 256));
-        HIPCHK(ctx->d_hb.ensure(nf * 5 * 22 * 16 * sizeof(float) + 256));
+        HIPCHK(ctx->d_xps.ensure(nr * 8192 * sizeof(float) + 256));
+        HIPCHK(ctx->d_xhl.ensure(nr * 768 * sizeof(float) + 256));
+        HIPCHK(ctx->d_xhr.ensure(nr * 768 * sizeof(float) + 256));
+        HIPCHK(ctx->d_pg.ensure(nr * 640 * sizeof(float) + 256));
+        HIPCHK(ctx->d_hb.ensure(nr * 5 * 22 * 16 * sizeof(float) + 256));
     }
     HIPCHK(S.d1.ensure(n1 + 256));
     HIPCHK(S.d2.ensure(n2 + 256));
@@ -684,6 +732,9 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
 
     SbrArgs a{};
     a.time = static_cast<const float*>(ctx->d_time.p);
+    a.fmap = identity ? nullptr : reinterpret_cast<const uint32_t*>(d1 + o_fmap);
+    a.ups = reinterpret_cast<const uint32_t*>(d1 + o_ups);
+    a.n_ups = (uint32_t)ups.size();
     a.recs = reinterpret_cast<const SbrRec*>(d1 + o_recs);
     a.epool = reinterpret_cast<const float*>(d2);
     a.tabs = reinterpret_cast<const SbrTab*>(d2 + o_tabs);

@@ -7,6 +7,8 @@
 namespace jaad {
 
 constexpr int kMinChunkFrames = 8;  // shortest chunk the planner makes (one re-decoded prefix frame per chunk)
+// |q| < kIqHead is inverse-quantised from an LDS copy of IQ_TABLE, larger values from global memory
+constexpr int kIqHead = 1024;
 
 // One unit of work = up to N consecutive frames of one run.  A chunk that does not start its
 // run first re-decodes the frame before it to rebuild the IMDCT overlap (the overlap written by
@@ -25,8 +27,9 @@ enum : uint32_t { kChunkPrefix = 1u << 16, kChunkLoadState = 1u << 17, kChunkSto
 // csrc/tables/jaad_tables.inc), pre-permuted so that every lane-parallel read is
 // bank-conflict free.  Built by the host (build_lds_tables), copied verbatim by the prologue.
 struct alignas(16) LdsTables {
-    float win_pair[2][8][64][2];  // long window [shape][s][lane u][h] = W[long_pos(u,2s+h)] (SINE/KBD_1024)
-    float mdct_l[512][2];       // MDCT_TABLE_2048 (A/filterbank/MDCTTables.java:5), k order
+    float win_pair[2][8][64][2];  // long window [shape][s][lane u][h] = W[long_pos(lane_pos(u),2s+h)] (SINE/KBD_1024)
+    float mdct_l[512][2];       // MDCT_TABLE_2048 (A/filterbank/MDCTTables.java:5), k order (pre-twiddle)
+    float mdct_post[8][64][2];  // the same table for the post-twiddle: [s][lane u] = entry lane_pos(u) + 64 s
     float tw3[7][64][2];        // 512-pt IFFT pass-3 twiddles [j][lane] (FFT_TABLE_512, A/filterbank/FFTTables.java:5)
     float tw2[7][8][2];         // 512-pt IFFT pass-2 twiddles [j][lane&7]
     float tw1[4][2];            // 512-pt IFFT pass-1 (i = 4) twiddles
@@ -34,7 +37,7 @@ struct alignas(16) LdsTables {
     float mdct_s[64][2];        // MDCT_TABLE_128 (:519)
     float roots_s[32][2];       // FFT_TABLE_64[k], k < 32 (:519)
     float sf_gain[256];         // SCALEFACTOR_TABLE[100+i] (A/syntax/ScaleFactorTable.java)
-    float iq_signed[256];       // q = i-128: q>0 ? IQ_TABLE[q] : -IQ_TABLE[-q] (A/syntax/ICStream.java:266)
+    float iq_signed[2 * kIqHead]; // q = i-kIqHead: q>0 ? IQ_TABLE[q] : -IQ_TABLE[-q] (A/syntax/ICStream.java:266)
     uint8_t quad2band_l[256];   // long window: scalefactor band of bins 4i..4i+3 (255 = none)
     uint8_t quad2band_s[32];    // short window
     int32_t nswb_l, nswb_s, tns_max_l, tns_max_s;
@@ -70,10 +73,21 @@ struct KernelArgs {
     int dbg_frame;
 };
 
+// IFFT output position (mod 64) that lane u holds after the register transposes of the long
+// IMDCT (jaad_lc.hip, imdct_long_pk): (u >> 3) + 8 * bitrev3(u & 7).  JAAD_LC_LDSX (the LDS
+// transpose variant kept for A/B timing) leaves the lanes in natural order.
+inline int lane_pos_host(int u)
+{
+#ifdef JAAD_LC_LDSX
+    return u;
+#else
+    return (u >> 3) | ((((u & 1) << 2) | (u & 2) | ((u >> 2) & 1)) << 3);
+#endif
+}
 // position (0..1023) of lane u's IMDCT output slot o = 2s+h (see jaad_lc.hip, long_pos)
 inline int long_pos_host(int u, int o)
 {
-    int s = o >> 1, h = o & 1, k = u + 64 * s;
+    int s = o >> 1, h = o & 1, k = lane_pos_host(u) + 64 * s;
     if (s < 4) return h ? 512 + 2 * k : 511 - 2 * k;
     return h ? 1535 - 2 * k : 2 * k - 512;
 }

@@ -19,32 +19,36 @@
 // frame to rebuild it.  Frame f+1's inputs are loaded while frame f's two IMDCTs run.
 //
 // The 512-point complex IFFT of a frame is 8 complex values per lane in three register passes
-// (bit-reversed radix-4 + one radix-2 stage, then 3 + 3 radix-2 stages) with two padded LDS
-// transposes.  Butterflies, twiddles (the reference's float32 recurrence tables) and
-// evaluation order are those of the Java code and the file is compiled with
-// -ffp-contract=off, so the results are bit-exact.
+// (bit-reversed radix-4 + one radix-2 stage, then 3 + 3 radix-2 stages).  Between the passes
+// the lanes trade register bits for lane bits with v_permlane32_swap / v_permlane16_swap and
+// DPP moves (no LDS round trip; JAAD_LC_LDSX builds the earlier padded-LDS transposes for A/B
+// timing).  Butterflies, twiddles (the reference's float32 recurrence tables) and evaluation
+// order are those of the Java code and the file is compiled with -ffp-contract=off, so the
+// results are bit-exact.
 #include <hip/hip_runtime.h>
 
 #include "jaad_lc.h"
-
-// The two channels of a CPE run their long-window IMDCTs in lockstep (JAAD_LC_NODUAL: one after
-// the other, the right spectrum parked in LDS meanwhile)
-#ifndef JAAD_LC_NODUAL
-#define JAAD_LC_DUAL 1
-#endif
 
 namespace jaad {
 
 __device__ __forceinline__ int lane_id()
 {
-#ifndef JAAD_HOISTABLE_LANE
+    // opaque to the optimiser: index math derived from it is recomputed where used instead of
+    // being hoisted into registers that live across the frame loop
     int v;
     asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(v));
-#else
-    int v = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-#endif
     __builtin_assume(v >= 0 && v < 64);
     return v;
+}
+
+// IFFT output position (mod 64) held by lane u after the register transposes (lane_pos_host)
+__device__ __forceinline__ int lane_pos(int u)
+{
+#ifdef JAAD_LC_LDSX
+    return u;
+#else
+    return (u >> 3) | ((int)(__builtin_bitreverse32((uint32_t)u) >> 29) << 3);
+#endif
 }
 
 __device__ __forceinline__ void wave_sync()
@@ -152,7 +156,7 @@ __device__ __forceinline__ void fft_3stages(float (&re)[8], float (&im)[8], TW t
 // position of IMDCT output slot o = 2s+h for lane u (MDCT.java:56-80 reorder)
 __device__ __forceinline__ int long_pos(int u, int o)
 {
-    int s = o >> 1, h = o & 1, k = u + 64 * s;
+    int s = o >> 1, h = o & 1, k = lane_pos(u) + 64 * s;
     if (s < 4) return h ? 512 + 2 * k : 511 - 2 * k;
     return h ? 1535 - 2 * k : 2 * k - 512;
 }
@@ -185,93 +189,6 @@ __device__ __forceinline__ Ics ics_from_lanes(uint32_t side, int base, const Lds
     const int groups = r.seq == JAAD_EIGHT_SHORT_SEQUENCE ? 8 - __builtin_popcount(r.grouping & 0x7f) : 1;
     r.nbands = groups * r.max_sfb;
     return r;
-}
-
-// ------------------------------------------------------------------------------------------
-// IMDCT N = 2048 (MDCT.process): lane u holds k = u + 64 s.  Reads the spectrum from buf.
-// ------------------------------------------------------------------------------------------
-// N channel transforms in lockstep (N = 2: the two channels of a CPE share every LDS round
-// trip and give the scheduler two independent dependency chains)
-template <int N>
-__device__ __forceinline__ void imdct_long_n(float* const (&bufs)[N], const LdsTables& T, int u, float (&re)[N][8],
-                                             float (&im)[N][8])
-{
-#pragma unroll
-    for (int n = 0; n < N; n++)
-#pragma unroll
-        for (int s = 0; s < 8; s++) {
-            int k = u + 64 * s;
-            float in0 = bufs[n][eo_idx(2 * k)];
-            float in1 = bufs[n][eo_idx(1023 - 2 * k)];
-            float c = T.mdct_l[k][0], sn = T.mdct_l[k][1];
-            im[n][s] = (in0 * c) + (in1 * sn);  // MDCT.java:39-42
-            re[n][s] = (in1 * c) - (in0 * sn);
-        }
-    wave_sync();
-    // pass 1: this lane is bit-reversed row t = bitrev6(u): rev[8t+r] = buf[u + 64*bitrev3(r)]
-    const int t = (int)(__builtin_bitreverse32((uint32_t)u) >> 26);
-    const int x1 = xs_l(8 * t);
-#pragma unroll
-    for (int n = 0; n < N; n++) {
-        fft_pass1(re[n], im[n], T.tw1, 1);
-        float2* X = reinterpret_cast<float2*>(bufs[n]);
-#pragma unroll
-        for (int r = 0; r < 8; r++) X[x1 + r] = make_float2(re[n][BR3[r]], im[n][BR3[r]]);
-    }
-    wave_sync();
-    // pass 2: elements 64a + b + 8s, stages i = 8, 16, 32
-    const int a = u >> 3, b = u & 7;
-    const int x2 = xs_l(64 * a + b);
-#pragma unroll
-    for (int n = 0; n < N; n++) {
-        const float2* X = reinterpret_cast<const float2*>(bufs[n]);
-#pragma unroll
-        for (int s = 0; s < 8; s++) {
-            float2 v = X[x2 + xs_l(8 * s)];
-            re[n][s] = v.x;
-            im[n][s] = v.y;
-        }
-    }
-#pragma unroll
-    for (int n = 0; n < N; n++) {
-        fft_3stages(re[n], im[n], [&](int j, float& wr, float& wi) {
-            wr = T.tw2[j][b][0];
-            wi = T.tw2[j][b][1];
-        });
-        float2* X = reinterpret_cast<float2*>(bufs[n]);
-#pragma unroll
-        for (int s = 0; s < 8; s++) X[x2 + xs_l(8 * s)] = make_float2(re[n][s], im[n][s]);
-    }
-    wave_sync();
-    // pass 3: elements u + 64 s, stages i = 64, 128, 256
-    const int x3 = xs_l(u);
-#pragma unroll
-    for (int n = 0; n < N; n++) {
-        const float2* X = reinterpret_cast<const float2*>(bufs[n]);
-#pragma unroll
-        for (int s = 0; s < 8; s++) {
-            float2 v = X[x3 + xs_l(64 * s)];
-            re[n][s] = v.x;
-            im[n][s] = v.y;
-        }
-    }
-    wave_sync();
-#pragma unroll
-    for (int n = 0; n < N; n++) {
-        // stages 64 (m = 4, k = u), 128 (m = 2, k = u + 64e), 256 (m = 1, k = u + 64s)
-        fft_3stages(re[n], im[n], [&](int j, float& wr, float& wi) {
-            wr = T.tw3[j][u][0];
-            wi = T.tw3[j][u][1];
-        });
-#pragma unroll
-        for (int s = 0; s < 8; s++) {  // MDCT.java:48-53
-            int k = u + 64 * s;
-            float c = T.mdct_l[k][0], sn = T.mdct_l[k][1];
-            float t0 = re[n][s], t1 = im[n][s];
-            im[n][s] = (t1 * c) + (t0 * sn);
-            re[n][s] = (t0 * c) - (t1 * sn);
-        }
-    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -351,7 +268,60 @@ __device__ __forceinline__ void fft_3stages_pk(f2 (&c)[8], TW tw)
     for (int s = 0; s < 4; s++) bfly_pk(c[s], c[s + 4], tw(3 + s));
 }
 
-// imdct_long_n in packed form: c[n][s] = (re, im) of element u + 64 s after the post-twiddle
+
+// Register transposes between the IFFT passes.  A pair of registers (a: register bit i clear,
+// b: set) trades register bit i for lane bit L: the element at (register bit, lane bit L) =
+// (x, y) moves to (y, x), every other lane bit unchanged.
+template <int L>
+__device__ __forceinline__ void xch(float& a, float& b, int u)
+{
+    const int ia = __float_as_int(a), ib = __float_as_int(b);
+    if constexpr (L == 5 || L == 4) {  // swap a's upper half-lanes with b's lower ones
+        const auto r = L == 5 ? __builtin_amdgcn_permlane32_swap(ia, ib, false, false)
+                              : __builtin_amdgcn_permlane16_swap(ia, ib, false, false);
+        a = __int_as_float(r[0]);
+        b = __int_as_float(r[1]);
+    } else if constexpr (L == 3) {  // row_ror:8 = lane ^ 8; bank mask = the lanes written
+        a = __int_as_float(__builtin_amdgcn_update_dpp(ia, ib, 0x128, 0xF, 0xC, false));
+        b = __int_as_float(__builtin_amdgcn_update_dpp(ib, ia, 0x128, 0xF, 0x3, false));
+    } else if constexpr (L == 2) {  // row_ror:n reads lane (l - n) mod 16: 4 -> lane - 4 for lanes 4..7, 12 -> lane + 4 for 0..3
+        a = __int_as_float(__builtin_amdgcn_update_dpp(ia, ib, 0x124, 0xF, 0xA, false));
+        b = __int_as_float(__builtin_amdgcn_update_dpp(ib, ia, 0x12C, 0xF, 0x5, false));
+    } else {  // quad_perm lane ^ 2 / lane ^ 1, then a per-lane select
+        constexpr int kCtl = L == 1 ? 0x4E : 0xB1;
+        const int pb = __builtin_amdgcn_mov_dpp(ib, kCtl, 0xF, 0xF, true);
+        const int pa = __builtin_amdgcn_mov_dpp(ia, kCtl, 0xF, 0xF, true);
+        const bool hi = (u >> L) & 1;
+        a = __int_as_float(hi ? pb : ia);
+        b = __int_as_float(hi ? ib : pa);
+    }
+}
+// register bit I <-> lane bit L for all four register pairs, both floats of each complex value
+template <int I, int L>
+__device__ __forceinline__ void xch_bit(f2 (&c)[8], int u)
+{
+#pragma unroll
+    for (int s = 0; s < 8; s++) {
+        if ((s >> I) & 1) continue;
+        float ax = c[s].x, ay = c[s].y, bx = c[s | (1 << I)].x, by = c[s | (1 << I)].y;
+        xch<L>(ax, bx, u);
+        xch<L>(ay, by, u);
+        c[s] = f2{ax, ay};
+        c[s | (1 << I)] = f2{bx, by};
+    }
+}
+
+// IMDCT N = 2048 (MDCT.process, A/filterbank/MDCT.java:36-81) of N channels in lockstep (N = 2:
+// the two channels of a CPE share the table reads and give the scheduler two independent
+// dependency chains).  Reads the spectrum (E/O layout) from bufs[n]; on return c[n][s] = (re, im)
+// of IFFT position lane_pos(u) + 64 s after the post-twiddle.
+//
+// Element e (0..511) of the bit-reversed IFFT array: pass 1 works on e bits 0-2, pass 2 on bits
+// 3-5, pass 3 on bits 6-8 (FFT.java:69-134), each as three in-register stages.  Lane u starts
+// with k = u + 64 s (e = bitrev9(k): e bits 3-8 = bitrev6(u), register s holds e bits 2,1,0 in
+// its bits 0,1,2).  The first exchange trades register bits 0,1,2 for lane bits 5,4,3 (e bits
+// 3,4,5 into registers; lane bits 3-5 then hold e bits 0-2), the second register bits 0,1,2 for
+// lane bits 2,1,0 (e bits 6,7,8 into registers), leaving lane u with positions lane_pos(u) + 64 s.
 template <int N>
 __device__ __forceinline__ void imdct_long_pk(float* const (&bufs)[N], const LdsTables& T, int u, f2 (&c)[N][8])
 {
@@ -364,6 +334,7 @@ __device__ __forceinline__ void imdct_long_pk(float* const (&bufs)[N], const Lds
             const f2 x = {bufs[n][eo_idx(1023 - 2 * k)], bufs[n][eo_idx(2 * k)]};
             c[n][s] = cmul(x, ld2(T.mdct_l[k]));
         }
+#ifdef JAAD_LC_LDSX
     wave_sync();
     const int t = (int)(__builtin_bitreverse32((uint32_t)u) >> 26);
     const int x1 = xs_l(8 * t);
@@ -399,24 +370,34 @@ __device__ __forceinline__ void imdct_long_pk(float* const (&bufs)[N], const Lds
         for (int s = 0; s < 8; s++) c[n][s] = X[x3 + xs_l(64 * s)];
     }
     wave_sync();
+#else
+    // pass 1: register s holds e bits (s2, s1, s0) = e bits 0, 1, 2 (fft_pass1_pk's BR3 order)
+#pragma unroll
+    for (int n = 0; n < N; n++) fft_pass1_pk(c[n], T.tw1);
+#pragma unroll
+    for (int n = 0; n < N; n++) {
+        xch_bit<0, 5>(c[n], u);  // e bit 3 (lane bit 5) <-> e bit 2
+        xch_bit<1, 4>(c[n], u);  // e bit 4 (lane bit 4) <-> e bit 1
+        xch_bit<2, 3>(c[n], u);  // e bit 5 (lane bit 3) <-> e bit 0
+    }
+    // pass 2: register bits 0,1,2 = e bits 3,4,5; e mod 8 = u >> 3
+    const int b = u >> 3;
+#pragma unroll
+    for (int n = 0; n < N; n++) fft_3stages_pk(c[n], [&](int j) { return ld2(T.tw2[j][b]); });
+#pragma unroll
+    for (int n = 0; n < N; n++) {
+        xch_bit<0, 2>(c[n], u);  // e bit 6 (lane bit 2) <-> e bit 3
+        xch_bit<1, 1>(c[n], u);  // e bit 7 (lane bit 1) <-> e bit 4
+        xch_bit<2, 0>(c[n], u);  // e bit 8 (lane bit 0) <-> e bit 5
+    }
+#endif
+    // pass 3: register bits 0,1,2 = e bits 6,7,8, e mod 64 = lane_pos(u)
 #pragma unroll
     for (int n = 0; n < N; n++) {
         fft_3stages_pk(c[n], [&](int j) { return ld2(T.tw3[j][u]); });
         // MDCT.java:48-53: re = t0*c - t1*sn, im = t1*c + t0*sn = cmul((t0, t1), (c, sn))
 #pragma unroll
-        for (int s = 0; s < 8; s++) c[n][s] = cmul(c[n][s], ld2(T.mdct_l[u + 64 * s]));
-    }
-}
-
-__device__ __forceinline__ void imdct_long(float* buf, const LdsTables& T, int u, float (&re)[8], float (&im)[8])
-{
-    float* const bufs[1] = {buf};
-    float r1[1][8], i1[1][8];
-    imdct_long_n<1>(bufs, T, u, r1, i1);
-#pragma unroll
-    for (int s = 0; s < 8; s++) {
-        re[s] = r1[0][s];
-        im[s] = i1[0][s];
+        for (int s = 0; s < 8; s++) c[n][s] = cmul(c[n][s], ld2(T.mdct_post[s][u]));
     }
 }
 
@@ -471,14 +452,6 @@ __device__ __forceinline__ void ola_long_t(const LdsTables& T, const FrameCtx& f
             ov[o] = n_v;
         }
     }
-}
-
-__device__ __forceinline__ void ola_long(const LdsTables& T, int, const FrameCtx& fc, const float (&re)[8],
-                                         const float (&im)[8], float (&ov)[16], float (&out)[16])
-{
-    if (fc.seq == JAAD_ONLY_LONG_SEQUENCE) ola_long_t<JAAD_ONLY_LONG_SEQUENCE>(T, fc, re, im, ov, out);
-    else if (fc.seq == JAAD_LONG_START_SEQUENCE) ola_long_t<JAAD_LONG_START_SEQUENCE>(T, fc, re, im, ov, out);
-    else ola_long_t<JAAD_LONG_STOP_SEQUENCE>(T, fc, re, im, ov, out);
 }
 
 // ONLY_LONG window + overlap-add in packed form (slot pair (2s, 2s+1) of ola_long_t):
@@ -743,15 +716,34 @@ __device__ __forceinline__ uint32_t round_pk16(float a, float b)
     return w;
 }
 
+// s_waitcnt vmcnt(0) that the compiler's wait insertion sees (an asm statement it would not).
+// vmcnt counts loads and stores together, and the compiler cannot rely on a load completing
+// before a younger store (it then waits for vmcnt(0)); so the prefetched loads of frame f+1 are
+// drained explicitly BEFORE frame f's PCM stores are issued.  Otherwise the first use of frame
+// f+1's inputs at the top of the loop waits for frame f's stores to reach memory.
+__device__ __forceinline__ void vmem_drain() { __builtin_amdgcn_s_waitcnt(0x0F70); }  // vmcnt(0) expcnt(7) lgkmcnt(15)
+
+// PCM stores of one frame through a buffer resource covering exactly that frame: a prefix frame
+// (re-decoded only to rebuild the overlap) stores to offset >= num_records, which the hardware
+// drops.  So every frame issues the same stores: the compiler then knows that the next frame's
+// prefetched loads have exactly those stores younger than them and waits with vmcnt(N) at the
+// top of the frame loop instead of vmcnt(0) -- which would wait for the previous frame's stores
+// to reach memory (a wave would stall once per frame for the whole store round trip).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t frame_rsrc(void* base, int bytes)
+{
+    return __builtin_amdgcn_make_buffer_rsrc(base, (short)0, bytes, 0x00020000);  // gfx9 raw buffer
+}
+__device__ __forceinline__ void store16(v4u v, __amdgpu_buffer_rsrc_t r, int off, bool nt)
+{
+    if (nt) __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 2);  // aux 2: nt
+    else __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 0);
+}
+
 // per-wave LDS area: 8.5 KiB (16 waves + the 20 KiB table image fill a CU's 160 KiB)
 //   buf  band records [0,512) + raw sf/cb rows [512,640) -> spectrum (E/O) -> IFFT transposes ->
 //        OLA scratch -> PCM staging
 //   rsp  the right channel's spectrum while the left one is transformed (PNS: raw row copy)
-#ifdef JAAD_LC_DUAL
-constexpr int kRspFloats = kWaveBuf;  // second channel buffer (spectrum + transposes)
-#else
-constexpr int kRspFloats = 1024;
-#endif
+constexpr int kRspFloats = kWaveBuf;  // second channel buffer (spectrum + PCM staging)
 template <bool kTns>
 struct alignas(16) WaveLds {
     float buf[kWaveBuf];
@@ -764,11 +756,7 @@ struct alignas(16) WaveLds<true> {
     float tns[192];  // spec-TNS LPC scratch (8 filters x 24)
 };
 #ifndef JAAD_LC_WAVES
-#ifdef JAAD_LC_DUAL
 #define JAAD_LC_WAVES 12
-#else
-#define JAAD_LC_WAVES 16
-#endif
 #endif
 template <bool kTns>
 constexpr int waves_per_wg()
@@ -854,11 +842,7 @@ __device__ __forceinline__ void prefetch(const KernelArgs& A, int f, bool stereo
 #pragma unroll
     for (int c = 0; c < 2; c++) {
         if (c == 1 && !stereo) break;
-#ifdef JAAD_ABL_NO_LOADS
-        const size_t cf = (size_t)(f & 7) * nch + c;  // ablation: inputs stay cache resident
-#else
         const size_t cf = (size_t)f * nch + c;
-#endif
         const v4i* q = reinterpret_cast<const v4i*>(A.q + cf * 1024);
         pf.q[c][0] = __builtin_nontemporal_load(q + u);
         pf.q[c][1] = __builtin_nontemporal_load(q + 64 + u);
@@ -882,13 +866,9 @@ __device__ __forceinline__ void iq_channel(const LdsTables& T, const float* iq_g
 #pragma unroll
     for (int e = 0; e < 16; e++) {
         const int qq = reinterpret_cast<const int16_t*>(&q[e >> 3])[e & 7];
-        const int qc = qq < -128 ? -128 : (qq > 127 ? 127 : qq);
+        const int qc = qq < -kIqHead ? -kIqHead : (qq > kIqHead - 1 ? kIqHead - 1 : qq);
         esc |= qc != qq;
-#ifdef JAAD_ABL_NO_IQ
-        v[e] = (float)qc;
-#else
-        v[e] = T.iq_signed[qc + 128];
-#endif
+        v[e] = T.iq_signed[qc + kIqHead];
     }
     __builtin_amdgcn_sched_group_barrier(0x0100, 16, 0);  // the 16 DS reads first
     __builtin_amdgcn_sched_group_barrier(0x0002, 64, 0);  // then the VALU
@@ -897,7 +877,9 @@ __device__ __forceinline__ void iq_channel(const LdsTables& T, const float* iq_g
         const float gn = g[e >> 2];
         x[e] = gn != 0.0f ? v[e] * gn : 0.0f;
     }
-    if (__builtin_expect(__ballot(esc) != 0, 0)) {  // escape values beyond the LDS head of IQ_TABLE
+    // escape values beyond the LDS head of IQ_TABLE (|q| >= 1024: rare in real streams and absent
+    // from the synthetic ones); global loads, which also wait for the previous frame's PCM stores
+    if (__builtin_expect(__ballot(esc) != 0, 0)) {
         // uniform branch; every lane loads and selects (no exec-masked partial register writes)
 #pragma unroll
         for (int e = 0; e < 16; e++) {
@@ -905,7 +887,7 @@ __device__ __forceinline__ void iq_channel(const LdsTables& T, const float* iq_g
             const int aq = qq < 0 ? -qq : qq;
             const float gn = g[e >> 2];
             const float m = iq_global[aq > 8190 ? 8190 : aq] * gn;
-            const bool big = (qq > 127 || qq < -128) && gn != 0.0f;
+            const bool big = (qq > kIqHead - 1 || qq < -kIqHead) && gn != 0.0f;
             x[e] = big ? (qq > 0 ? m : -m) : x[e];
         }
     }
@@ -921,21 +903,15 @@ __device__ __forceinline__ void synth_channel(const KernelArgs& A, const LdsTabl
     if constexpr (kTnsSpec)
         if (A.tns_mode == JAAD_TNS_SPEC && (ic.flags & JAAD_ICS_TNS) && A.tns) tns_spec(buf, W.tns, T, *A.gtab, u, ic, A.tns + cf);
     const FrameCtx fc{ic.seq, ic.shape, ic.shape_prev};
-    float re[8], im[8];
     if (fc.seq == JAAD_EIGHT_SHORT_SEQUENCE) {
+        float re[8], im[8];
         imdct_short(buf, T, u, re, im);
         ola_short(buf, T, u, fc, re, im, ov, out);
     } else {
-#ifdef JAAD_ABL_NO_IMDCT
-#pragma unroll
-        for (int o = 0; o < 16; o++) {
-            out[o] = buf[o * 64 + u] + ov[o];
-            ov[o] = out[o] * 0.5f;
-        }
-#else
-        imdct_long(buf, T, u, re, im);
-        ola_long(T, u, fc, re, im, ov, out);
-#endif
+        float* const bufs[1] = {buf};
+        f2 cx[1][8];
+        imdct_long_pk<1>(bufs, T, u, cx);
+        ola_long_pk(T, fc, cx[0], ov, out);
     }
     wave_sync();
 }
@@ -1033,9 +1009,9 @@ __global__ __launch_bounds__(64 * waves_per_wg<kTnsSpec>()) void lc_decode_kerne
         }
         Prefetch pf;
         if (my_n > 0) prefetch(A, f_first, stereo, lane_id(), pf);
+        vmem_drain();  // (see vmem_drain) the loop head then finds no load pending on any path
 
         for (int it = 0; it < my_n; it++) {
-#ifndef JAAD_LC_NOPRIO
             // Issue arbitration between the waves of a SIMD favours the oldest wave, so the
             // waves of a SIMD would finish one after another and the last ones run with their
             // latency exposed.  A wave's priority drops as it advances through its chunk: the
@@ -1048,7 +1024,6 @@ __global__ __launch_bounds__(64 * waves_per_wg<kTnsSpec>()) void lc_decode_kerne
                 else if (q4 == 2) __builtin_amdgcn_s_setprio(1);
                 else __builtin_amdgcn_s_setprio(0);
             }
-#endif
 #ifdef JAAD_WAVETIME
             wt_frames++;
 #endif
@@ -1057,9 +1032,6 @@ __global__ __launch_bounds__(64 * waves_per_wg<kTnsSpec>()) void lc_decode_kerne
             const bool emit = f >= (int)cd.frame0;
             const size_t cf0 = (size_t)f * nch;
             const Prefetch cur = pf;
-#ifdef JAAD_EARLY_PREFETCH
-            if (it + 1 < my_n) prefetch(A, f + 1, stereo, u, pf);
-#endif
 
             // ---------------- side info ----------------
             const Ics iL = ics_from_lanes(cur.side, 0, T);
@@ -1148,9 +1120,9 @@ __global__ __launch_bounds__(64 * waves_per_wg<kTnsSpec>()) void lc_decode_kerne
             if (stereo) iq_channel(T, A.iq_table, cur.q[1], gR, xR);
             // the inputs are consumed: frame f+1's loads fly while this frame's IMDCTs run
             STAMP(12);
-#ifndef JAAD_EARLY_PREFETCH
-            if (it + 1 < my_n) prefetch(A, f + 1, stereo, u, pf);
-#endif
+            // issued on every iteration (the last one reloads its own frame) so that the VMEM
+            // pattern of the loop body is the same on every path: see the PCM stores below
+            prefetch(A, it + 1 < my_n ? f + 1 : f, stereo, u, pf);
 
             if ((iL.flags | (stereo ? iR.flags : 0)) & JAAD_ICS_HAS_PNS) {  // rare: lane 0 replays the LCG
                 // the spectrum overwrites the raw rows: pns_fill reads a copy in rsp
@@ -1202,7 +1174,6 @@ __global__ __launch_bounds__(64 * waves_per_wg<kTnsSpec>()) void lc_decode_kerne
             }
 
             STAMP(3);
-#ifdef JAAD_LC_DUAL
             // both spectra to LDS (E/O layout): left in buf, right in rsp
             wave_sync();
             store_spec(W.buf, u, xL);
@@ -1219,42 +1190,38 @@ __global__ __launch_bounds__(64 * waves_per_wg<kTnsSpec>()) void lc_decode_kerne
                     }
                 }
                 float* const bufs[2] = {W.buf, W.rsp};
-#ifdef JAAD_LC_SCALAR
-                float re[2][8], im[2][8];
-                imdct_long_n<2>(bufs, T, lane_id(), re, im);
-                ola_long(T, u, FrameCtx{iL.seq, iL.shape, iL.shape_prev}, re[0], im[0], ovL, outL);
-                ola_long(T, u, FrameCtx{iR.seq, iR.shape, iR.shape_prev}, re[1], im[1], ovR, outR);
-#else
                 f2 cx[2][8];
                 imdct_long_pk<2>(bufs, T, lane_id(), cx);
                 ola_long_pk(T, FrameCtx{iL.seq, iL.shape, iL.shape_prev}, cx[0], ovL, outL);
                 ola_long_pk(T, FrameCtx{iR.seq, iR.shape, iR.shape_prev}, cx[1], ovR, outR);
-#endif
                 wave_sync();
             } else {
                 synth_channel<kTnsSpec>(A, T, W, W.buf, iL, cf0, ovL, outL);
                 if (stereo) synth_channel<kTnsSpec>(A, T, W, W.rsp, iR, cf0 + 1, ovR, outR);
             }
             STAMP(8);
+            // frame f+1's inputs (loaded since the IQ, a whole IMDCT ago) are in registers before
+            // this frame's PCM stores are issued
+            vmem_drain();
+            STAMP(9);
             {
                 const int u2 = lane_id();
                 if constexpr (planar) {
-                    if (emit) {
 #pragma unroll
-                        for (int o = 0; o < 16; o++) {
-                            W.buf[long_pos(u2, o)] = outL[o];
-                            if (stereo) W.rsp[long_pos(u2, o)] = outR[o];
-                        }
-                        wave_sync();
-#pragma unroll
-                        for (int c = 0; c < nch; c++) {
-                            float* dst = reinterpret_cast<float*>(A.pcm) + (cf0 + c) * 1024;
-                            const float* srcb = c ? W.rsp : W.buf;
-#pragma unroll
-                            for (int jj = 0; jj < 4; jj++)
-                                *reinterpret_cast<float4*>(dst + 4 * u2 + 256 * jj) = *reinterpret_cast<const float4*>(srcb + 4 * u2 + 256 * jj);
-                        }
+                    for (int o = 0; o < 16; o++) {
+                        W.buf[long_pos(u2, o)] = outL[o];
+                        if (stereo) W.rsp[long_pos(u2, o)] = outR[o];
                     }
+                    wave_sync();
+#pragma unroll
+                    for (int c = 0; c < nch; c++) {
+                        const __amdgpu_buffer_rsrc_t dst = frame_rsrc(reinterpret_cast<float*>(A.pcm) + (cf0 + c) * 1024, 4096);
+                        const float* srcb = c ? W.rsp : W.buf;
+#pragma unroll
+                        for (int jj = 0; jj < 4; jj++)
+                            store16(*reinterpret_cast<const v4u*>(srcb + 4 * u2 + 256 * jj), dst, emit ? 16 * u2 + 1024 * jj : 4096, false);
+                    }
+                    wave_sync();
                 } else if constexpr (out_f32) {  // tolerance/debug format: strided stores
                     if (emit) {
                         float2* dst = reinterpret_cast<float2*>(reinterpret_cast<uint8_t*>(A.pcm) + (size_t)f * 8192);
@@ -1275,122 +1242,13 @@ __global__ __launch_bounds__(64 * waves_per_wg<kTnsSpec>()) void lc_decode_kerne
                         stage[long_pos(u2, 2 * m + 1)] = __builtin_amdgcn_perm(pr, pl, sel1);
                     }
                     wave_sync();
-                    if (emit) {
-                        uint8_t* dst = reinterpret_cast<uint8_t*>(A.pcm) + (size_t)f * 4096;
-#pragma unroll
-                        for (int jj = 0; jj < 4; jj++)
-                            __builtin_nontemporal_store(*reinterpret_cast<const v4u*>(stage + 4 * u2 + 256 * jj),
-                                                        reinterpret_cast<v4u*>(dst + 16 * u2 + 1024 * jj));
-                    }
-                    wave_sync();
-                }
-            }
-#else
-            // left spectrum -> buf (E/O layout); right spectrum parked in rsp (lane-linear)
-            wave_sync();
-            store_spec(W.buf, u, xL);
-            if (stereo) {
-#pragma unroll
-                for (int k = 0; k < 4; k++)
-                    *reinterpret_cast<float4*>(W.rsp + 4 * u + 256 * k) = make_float4(xR[4 * k], xR[4 * k + 1], xR[4 * k + 2], xR[4 * k + 3]);
-            }
-            wave_sync();
-
-            STAMP(4);
-            // ---------------- per channel: IMDCT, window/OLA, PCM ----------------
-            // int16 PCM is staged in rsp as the frame's interleaved SampleBuffer image (word P =
-            // sample P of L and R); channel c's samples wait in pk until rsp is free.
-            uint16_t* stage16 = reinterpret_cast<uint16_t*>(W.rsp);
-            uint32_t pk[8];
-            // PCM values are computed and staged for every frame (emit only gates the HBM stores):
-            // a staging step guarded by its own run-time test would keep pk live across frames
-            auto channel = [&](const int c, float (&ov)[16]) {
-                const Ics& ic = c ? iR : iL;
-                if (c == 1) {
-                    const int u2 = lane_id();
-                    float x[16];
-#pragma unroll
-                    for (int k = 0; k < 4; k++) {
-                        const float4 v = *reinterpret_cast<const float4*>(W.rsp + 4 * u2 + 256 * k);
-                        x[4 * k] = v.x;
-                        x[4 * k + 1] = v.y;
-                        x[4 * k + 2] = v.z;
-                        x[4 * k + 3] = v.w;
-                    }
-                    store_spec(W.buf, u2, x);
-                    if constexpr (out_i16) {
-                        wave_sync();
-#pragma unroll
-                        for (int o = 0; o < 16; o++) stage16[2 * long_pos(u2, o)] = (uint16_t)(pk[o >> 1] >> (16 * (o & 1)));
-                    }
-                    wave_sync();
-                }
-                STAMP(c ? 7 : 5);
-                float out[16];
-                synth_channel<kTnsSpec>(A, T, W, W.buf, ic, cf0 + c, ov, out);
-                STAMP(c ? 8 : 6);
-                const int u2 = lane_id();
-                if constexpr (planar) {
-                    if (emit) {
-                        float* dst = reinterpret_cast<float*>(A.pcm) + (cf0 + c) * 1024;
-#pragma unroll
-                        for (int o = 0; o < 16; o++) W.buf[long_pos(u2, o)] = out[o];
-                        wave_sync();
-#pragma unroll
-                        for (int jj = 0; jj < 4; jj++)
-                            *reinterpret_cast<float4*>(dst + 4 * u2 + 256 * jj) = *reinterpret_cast<const float4*>(W.buf + 4 * u2 + 256 * jj);
-                    }
-                } else if constexpr (out_f32) {  // tolerance/debug format: strided stores
-                    if (emit) {
-                        float* dst = reinterpret_cast<float*>(reinterpret_cast<uint8_t*>(A.pcm) + (size_t)f * 8192);
-#pragma unroll
-                        for (int o = 0; o < 16; o++) {
-                            const int P = long_pos(u2, o);
-                            dst[2 * P + c] = out[o];
-                            if (!stereo) dst[2 * P + 1] = out[o];
-                        }
-                    }
-                } else {
-                    // big endian swaps the two bytes of every sample
-                    const uint32_t sel = big_endian ? 0x02030001u : 0x03020100u;
-#pragma unroll
-                    for (int m = 0; m < 8; m++) pk[m] = __builtin_amdgcn_perm(0u, round_pk16(out[2 * m], out[2 * m + 1]), sel);
-                }
-            };
-            channel(0, ovL);
-            if (stereo) channel(1, ovR);
-            STAMP(9);
-            if constexpr (out_i16) {
-                const int u2 = lane_id();
-                wave_sync();
-#pragma unroll
-                for (int o = 0; o < 16; o++) {
-                    const uint16_t v = (uint16_t)(pk[o >> 1] >> (16 * (o & 1)));
-                    const int P = long_pos(u2, o);
-                    if (stereo) {
-                        stage16[2 * P + 1] = v;
-                    } else {
-                        stage16[2 * P] = v;
-                        stage16[2 * P + 1] = v;
-                    }
-                }
-                wave_sync();
-                if (emit) {
-                    uint8_t* dst = reinterpret_cast<uint8_t*>(A.pcm) + (size_t)f * 4096;
+                    const __amdgpu_buffer_rsrc_t dst = frame_rsrc(reinterpret_cast<uint8_t*>(A.pcm) + (size_t)f * 4096, 4096);
 #pragma unroll
                     for (int jj = 0; jj < 4; jj++)
-#ifdef JAAD_ABL_NO_STORE
-                        if (A.n_chunks == 0)
-#endif
-#ifdef JAAD_TEMPORAL_STORE
-                        *reinterpret_cast<v4u*>(dst + 16 * u2 + 1024 * jj) = *reinterpret_cast<const v4u*>(W.rsp + 4 * u2 + 256 * jj);
-#else
-                        __builtin_nontemporal_store(*reinterpret_cast<const v4u*>(W.rsp + 4 * u2 + 256 * jj),
-                                                    reinterpret_cast<v4u*>(dst + 16 * u2 + 1024 * jj));
-#endif
+                        store16(*reinterpret_cast<const v4u*>(stage + 4 * u2 + 256 * jj), dst, emit ? 16 * u2 + 1024 * jj : 4096, true);
+                    wave_sync();
                 }
             }
-#endif
             STAMP(10);
         }
         STAMP(11);

@@ -476,8 +476,26 @@ int jaad_asc_parse(const uint8_t* asc, size_t bytes, jaad_stream_cfg* cfg)
         if (br.read(1)) br.skip(1);                   // extensionFlag -> extensionFlag3
         if (br.overrun()) return JAAD_ERR_EOS;
         if (chc == 0) return JAAD_ERR_UNSUPPORTED;    // PCE channel layouts: not a 1/2-channel config
-        // sync extension (readSyncExtension, :255-285) is read only when sbrEnabled: the
-        // implicit/backward-compatible signalling keeps the core rate
+        // readSyncExtension (A/DecoderConfig.java:238, 260-291; sbrEnabled is always on): a
+        // backward-compatible 0x2B7 extension can signal SBR (and PS, 0x548) with its output
+        // rate.  Without it the output rate stays the core rate (:180): SBR met later in the
+        // frames (implicit signalling) then runs downsampled (the facade's implicit_sbr_cfg).
+        if (!br.overrun() && br.left() > 10 && br.read(11) == 0x2B7) {
+            const int ext = (int)br.read(5);
+            if (ext == 5 || ext == 22) {  // AAC_SBR, ER_BSAC
+                if (br.read(1)) {         // sbrPresent
+                    const int esf = rate();
+                    if (ext == 5) {
+                        cfg->sbr = 1;
+                        cfg->ext_sf_index = (uint8_t)esf;
+                        cfg->ps = chc == 1;  // psPresent (0x548) or not: PS data is applied when present
+                    } else {
+                        return JAAD_ERR_UNSUPPORTED;  // BSAC
+                    }
+                }
+                if (ext == 5 && br.left() > 12 && br.read(11) == 0x548) br.skip(1);  // psPresent
+            }
+        }
     }
     if (br.overrun()) return JAAD_ERR_EOS;
     if (aot != 2) return JAAD_ERR_UNSUPPORTED;

@@ -91,6 +91,10 @@ int sbr_log2(int v)
 
 // Channel.sbr_grid + envelope_time_border_vector + noise_floor_time_border_vector (:324-583);
 // numTimeSlots 16, rate 2, tHFAdj 2, tHFGen 8 (1024-sample frames)
+// Channel.sbr_grid returning 1 (A/sbr/Channel.java:418-432): the grid's borders do not fit.  The
+// reference then marks the frame's SBR data invalid (SBR.decode, A/sbr/SBR.java:179-182).
+constexpr int kGridInvalid = 1;
+
 int read_grid(BitReader& br, ChWork& w)
 {
     const int NTS = 16, RATE = 2;
@@ -166,7 +170,7 @@ int read_grid(BitReader& br, ChWork& w)
     }
     (void)n_rel_lead;
     (void)n_rel_trail;
-    if (w.L_E <= 0) return JAAD_ERR_UNSUPPORTED;
+    if (w.L_E <= 0) return kGridInvalid;
     w.L_Q = w.L_E > 1 ? 2 : 1;
     // envelope_time_border_vector (:455-542)
     // eTmp persists in the reference; t_E is a full copy of it, so entries past L_E are stale
@@ -189,7 +193,7 @@ int read_grid(BitReader& br, ChWork& w)
         if (w.L_E > 1) {
             int i = w.L_E, border = abs_trail;
             for (int l = 0; l < w.L_E - 1; l++) {
-                if (border < rel[l]) return JAAD_ERR_UNSUPPORTED;
+                if (border < rel[l]) return kGridInvalid;
                 border -= rel[l];
                 e[--i] = RATE * border;
             }
@@ -200,7 +204,7 @@ int read_grid(BitReader& br, ChWork& w)
             int i = 1, border = abs_lead;
             for (int l = 0; l < w.L_E - 1; l++) {
                 border += rel[l];
-                if (RATE * border + 2 > 2 * NTS + 8) return JAAD_ERR_UNSUPPORTED;
+                if (RATE * border + 2 > 2 * NTS + 8) return kGridInvalid;
                 e[i++] = RATE * border;
             }
         }
@@ -210,14 +214,14 @@ int read_grid(BitReader& br, ChWork& w)
             int i = 1, border = abs_lead;
             for (int l = 0; l < nrel0; l++) {
                 border += rel0[l];
-                if (RATE * border + 2 > 2 * NTS + 8) return JAAD_ERR_UNSUPPORTED;
+                if (RATE * border + 2 > 2 * NTS + 8) return kGridInvalid;
                 e[i++] = RATE * border;
             }
         }
         if (nrel1) {
             int i = w.L_E, border = abs_trail;
             for (int l = 0; l < nrel1; l++) {
-                if (border < rel1[l]) return JAAD_ERR_UNSUPPORTED;
+                if (border < rel1[l]) return kGridInvalid;
                 border -= rel1[l];
                 e[--i] = RATE * border;
             }
@@ -625,7 +629,7 @@ void to_record(const ChWork& w, const SbrParseState& S, jaad_sbr_channel& c)
     c.L_Q = (uint8_t)w.L_Q;
     c.bs_pointer = (uint8_t)w.bs_pointer;
     for (int i = 0; i <= w.L_E; i++) c.t_E[i] = (uint8_t)w.t_E[i];
-    for (int i = 0; i < 3; i++) c.t_Q[i] = (uint8_t)w.t_Q[i];
+    for (int i = 0; i <= w.L_Q && i < 3; i++) c.t_Q[i] = (uint8_t)w.t_Q[i];  // past L_Q: stale (Channel.couple)
     for (int i = 0; i < w.L_E; i++) c.f[i] = (uint8_t)w.f[i];
     for (int i = 0; i < S.N_Q; i++) c.invf_mode[i] = (uint8_t)w.invf[i];
     c.add_harmonic_flag = (uint8_t)w.add_harmonic_flag;
@@ -685,19 +689,44 @@ int parse_sbr(BitReader& br, const Cfg& C, bool crc, ParseState& st, jaad_sbr_fr
         S.have_hdr = true;
         rec.header_present = 1;
     }
-    if (!S.have_hdr) return JAAD_ERR_UNSUPPORTED;  // no SBR header yet: the reference skips the data
+    // no SBR header yet: SBR.decode skips sbr_data and marks the data valid (A/sbr/SBR.java:179-184);
+    // the DSP stage then runs the QMF banks on the low band (the record stays header-less)
+    if (!S.have_hdr) return JAAD_OK;
     rec.hdr = S.hdr;
     if (S.N_Q > 5 || S.n[0] > 49 || S.n[1] > 49 || S.N_high > 64) return JAAD_ERR_BITSTREAM;
     ChWork* w = S.ch;
     int rc;
-    // a grid whose borders do not fit (read_grid -> UNSUPPORTED) makes the reference mark the SBR
-    // data invalid and upsample the core for this frame (A/sbr/Channel.java:418-432,
-    // A/syntax/SCE.java:123-132); the DSP path has no record for that
+    // a grid whose borders do not fit makes sbr_data return early: the reference restores the
+    // grid fields of the channels it had read (frame class, L_E, L_Q; channel 0's borders too,
+    // A/sbr/Channel.java:427-432, A/sbr/SBR2.java:89-103), marks the SBR data invalid and upsamples
+    // the core for this frame (JAAD_SBR_UPSAMPLE); nothing after the grid is read
+    struct Grid {  // what sbr_grid writes
+        int frame_class, L_E, L_Q, bs_pointer, t_E[6], t_Q[3], f[6];
+    } saved[2];
+    for (int c = 0; c < 2; c++) {
+        Grid& g = saved[c];
+        g.frame_class = w[c].frame_class, g.L_E = w[c].L_E, g.L_Q = w[c].L_Q, g.bs_pointer = w[c].bs_pointer;
+        std::memcpy(g.t_E, w[c].t_E, sizeof g.t_E);
+        std::memcpy(g.t_Q, w[c].t_Q, sizeof g.t_Q);
+        std::memcpy(g.f, w[c].f, sizeof g.f);
+    }
     auto grid = [&](ChWork& c) { return read_grid(br, c); };
+    auto invalid = [&]() {
+        for (int c = 0; c < 2; c++) {
+            const Grid& g = saved[c];
+            w[c].frame_class = g.frame_class, w[c].L_E = g.L_E, w[c].L_Q = g.L_Q, w[c].bs_pointer = g.bs_pointer;
+            std::memcpy(w[c].t_E, g.t_E, sizeof g.t_E);
+            std::memcpy(w[c].t_Q, g.t_Q, sizeof g.t_Q);
+            std::memcpy(w[c].f, g.f, sizeof g.f);
+        }
+        rec.status = JAAD_SBR_UPSAMPLE;
+        return JAAD_OK;
+    };
     if (C.nch == 1) {  // SBR1.sbr_data (A/sbr/SBR1.java:34-60)
         if (br.left() < 1) return JAAD_ERR_EOS;
         if (br.read(1)) br.skip(4);
-        if ((rc = grid(w[0])) || (rc = read_dtdf(br, w[0])) || (rc = read_invf(br, w[0], S.N_Q)) ||
+        if ((rc = grid(w[0])) == kGridInvalid) return invalid();
+        if (rc || (rc = read_dtdf(br, w[0])) || (rc = read_invf(br, w[0], S.N_Q)) ||
             (rc = read_envelope(br, w[0], S, false)) || (rc = read_noise(br, w[0], S, false)) ||
             (rc = read_harmonics(br, w[0], S.N_high)))
             return rc;
@@ -708,15 +737,16 @@ int parse_sbr(BitReader& br, const Cfg& C, bool crc, ParseState& st, jaad_sbr_fr
         rec.coupling = coupling;
         if (coupling) {
             // ch1.sbr_dtdf runs with ch1's L_E / L_Q of the previous frame, before couple()
-            if ((rc = grid(w[0])) || (rc = read_dtdf(br, w[0])) || (rc = read_dtdf(br, w[1])) ||
-                (rc = read_invf(br, w[0], S.N_Q)))
+            if ((rc = grid(w[0])) == kGridInvalid) return invalid();
+            if (rc || (rc = read_dtdf(br, w[0])) || (rc = read_dtdf(br, w[1])) || (rc = read_invf(br, w[0], S.N_Q)))
                 return rc;
             couple(w[1], w[0], S.N_Q);
             if ((rc = read_envelope(br, w[0], S, false)) || (rc = read_noise(br, w[0], S, false)) ||
                 (rc = read_envelope(br, w[1], S, true)) || (rc = read_noise(br, w[1], S, true)))
                 return rc;
         } else {
-            if ((rc = grid(w[0])) || (rc = grid(w[1])) || (rc = read_dtdf(br, w[0])) || (rc = read_dtdf(br, w[1])) ||
+            if ((rc = grid(w[0])) == kGridInvalid || (!rc && (rc = grid(w[1])) == kGridInvalid)) return invalid();
+            if (rc || (rc = read_dtdf(br, w[0])) || (rc = read_dtdf(br, w[1])) ||
                 (rc = read_invf(br, w[0], S.N_Q)) || (rc = read_invf(br, w[1], S.N_Q)) ||
                 (rc = read_envelope(br, w[0], S, false)) || (rc = read_envelope(br, w[1], S, false)) ||
                 (rc = read_noise(br, w[0], S, false)) || (rc = read_noise(br, w[1], S, false)))
@@ -754,11 +784,14 @@ int parse_sbr(BitReader& br, const Cfg& C, bool crc, ParseState& st, jaad_sbr_fr
     return JAAD_OK;
 }
 
-int sbr_missing(const Cfg&, ParseState&, jaad_sbr_frame&)
+int sbr_missing(const Cfg&, ParseState&, jaad_sbr_frame& rec)
 {
-    // a frame of an SBR stream without SBR payload: the reference decodes the core and
-    // upsamples it (A/sbr/SBR.java:302-309); the DSP path has no record for that
-    return JAAD_ERR_UNSUPPORTED;
+    // a frame of an SBR stream without SBR payload after its channel element: ChannelElement.decode
+    // invalidated the element's SBR (A/syntax/ChannelElement.java:56-59) and nothing revalidated
+    // it, so the reference upsamples the core (A/syntax/CPE.java:201-204, SCE.java:129-131)
+    std::memset(&rec, 0, sizeof rec);
+    rec.status = JAAD_SBR_UPSAMPLE;
+    return JAAD_OK;
 }
 
 }  // namespace parse

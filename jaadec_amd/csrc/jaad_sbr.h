@@ -47,19 +47,23 @@ enum : uint8_t {
     kSbrDep = 32,        // reads the high band of frame f-1's Xsbr rows 32..39: an HF fix pass
 };
 
-// One channel-frame.  224 bytes.
+// One channel-frame.  232 bytes.  The SBR stages run on the call's SBR-processed frames only,
+// compacted (frames whose SBR data is unusable are upsampled instead and leave the SBR state
+// alone, JAAD_SBR_UPSAMPLE): "the previous frame" of a record is the previous record of its run.
 struct SbrRec {
-    uint8_t L_E, table, lim_bands, flags;
+    uint8_t L_E, lim_bands, flags;
     uint8_t no_noise;           // bit l: l == l_A || l == prevEnvIsShort  (delta = 0, no noise)
-    uint8_t kx_prev, M_prev, sine0;
+    uint16_t table;             // index into the context's SbrTab list (0: no header yet)
+    uint8_t kx_prev, M_prev;
     uint16_t noise0;
     int8_t l_A;
-    uint8_t first;              // first frame of its run: previous-frame data comes from the slot state
+    uint8_t first;              // first record of its run: previous-frame data comes from the slot state
     uint8_t t_E[6];
     uint8_t f[6];
     uint8_t tnb[5];             // current_t_noise_band of envelope l
     uint8_t gq0;                // GQ_ringbuf_index when the frame's first row is assembled
-    uint16_t ps_back;           // PS config: frames back to the previous PS frame of the run in this
+    uint8_t sine0, pad0;
+    uint16_t ps_back;           // PS config: records back to the previous PS record of the run in this
                                 // call (0: none, the PS state of the slot holds it)
     float lim_gain;             // limGain[bs_limiter_gains]
     uint32_t e_off;             // E_orig[l][band] at epool[e_off + sum_{l'<l} n[f[l']] + band]
@@ -69,7 +73,7 @@ struct SbrRec {
     uint64_t s_index[5];        // bit m: S_index_mapped == 1
     uint64_t s_mapped[5];       // bit m: S_mapped == 1
 };
-static_assert(sizeof(SbrRec) == 224, "SbrRec layout");
+static_assert(sizeof(SbrRec) == 232 && sizeof(SbrRec) <= 256, "SbrRec layout (copied by one wave, a dword per lane)");
 
 // Per (slot, channel) state carried between calls, in global memory.  Read by the kernels of a
 // call for the first frame of a run, rewritten by the last kernel of the call (sbr_state_kernel).
@@ -126,8 +130,12 @@ struct PsState {
 };
 
 struct SbrArgs {
-    const float* time;          // [ch-frame][1024] core output (lc kernel, planar f32)
-    const SbrRec* recs;         // [ch-frame]
+    const float* time;          // [batch ch-frame][1024] core output (lc kernel, planar f32)
+    const uint32_t* fmap;       // record frame -> batch frame (null: the same); the SBR stages index
+                                // records, the core input and the PCM output batch frames
+    const uint32_t* ups;        // batch frames output by upsampling the core (JAAD_SBR_UPSAMPLE)
+    uint32_t n_ups;
+    const SbrRec* recs;         // [record ch-frame]
     const float* epool;
     const SbrTab* tabs;
     float* xlow;                // [ch-frame][32 slots][32 bands][2]
@@ -214,13 +222,11 @@ bool sbr_tables_for_parse(int out_sf, const jaad_sbr_header& h, SbrFbt& t);
 class SbrHost {
 public:
     static constexpr size_t kMaxTables = 1024;  // distinct SBR headers per context
-    explicit SbrHost(int out_sf_index) : out_sf_(out_sf_index)
-    {
-        tabs_.reserve(kMaxTables);
-        fbt_.reserve(kMaxTables);
-        keys_.reserve(kMaxTables);
-    }
+    static constexpr int kNoHeaderTable = 0;    // kx 32, M 0: the QMF banks on the low band only
+    explicit SbrHost(int out_sf_index);
     static void reset_slot(SbrHostSlot& s);
+    // Header.differs (A/sbr/Header.java:70-78): would this header reset the tables
+    static bool header_changes(const jaad_sbr_header& a, const jaad_sbr_header& b);
     // Build the records of one frame of one stream (both channels) in stream order.
     // Returns 0 or a jaad_status; writes the E_orig values at epool[epos..] (epos advances; the
     // record's e_off is e_base + epos) -- room for kMaxEorig floats per channel is the caller's.

@@ -239,6 +239,13 @@ __device__ __forceinline__ void dct4(const DctConst& K, int e, int E, float xr, 
 
 constexpr int kWavesPerBlock = 4;
 
+// batch frame / batch ch-frame of a record (frame) / record ch-frame (SbrArgs::fmap)
+__device__ __forceinline__ size_t batch_frame(const SbrArgs& A, size_t rf) { return A.fmap ? (size_t)A.fmap[rf] : rf; }
+__device__ __forceinline__ size_t batch_cf(const SbrArgs& A, size_t rcf)
+{
+    return A.fmap ? (size_t)A.fmap[rcf / (uint32_t)A.nch] * A.nch + rcf % (uint32_t)A.nch : rcf;
+}
+
 // ---------------------------------------------------------------------------------------------
 // AnalysisFilterbank.sbr_qmf_analysis_32 (A/sbr/AnalysisFilterbank.java:9-73)
 // ---------------------------------------------------------------------------------------------
@@ -255,9 +262,9 @@ __global__ __launch_bounds__(256) void sbr_analysis_kernel(SbrArgs A)
     const int c = (int)(cf % (uint32_t)A.nch);
     const SbrRec& R = A.recs[cf];
     const int kx = (R.flags & kSbrProcess) ? A.tabs[R.table].kx : 32;
-    const float* cur = A.time + (size_t)cf * 1024;
-    // samples before the frame: previous frame of the run, or the slot state (first frame)
-    const float* prev = R.first ? A.state[(size_t)R.slot * 2 + c].tail : A.time + (size_t)(cf - A.nch) * 1024 + 736;
+    const float* cur = A.time + batch_cf(A, cf) * 1024;
+    // samples before the frame: previous record of the run, or the slot state (first record)
+    const float* prev = R.first ? A.state[(size_t)R.slot * 2 + c].tail : A.time + batch_cf(A, cf - A.nch) * 1024 + 736;
     const int E = bitrev5(e);
     const DctConst K = load_dct_const(A.dct, e, E);
     float ca[5], cb[5];
@@ -1026,7 +1033,7 @@ __global__ __launch_bounds__(256) void sbr_synthesis_kernel(SbrArgs A)
             for (int l = 0; l < 32; l++) {
                 float a, b;
                 fetch(xq + l * 64, 64, a, b);
-                slot(a, b, true, (size_t)f * spf + sps * l, !ps_on);
+                slot(a, b, true, batch_frame(A, f) * spf + sps * l, !ps_on);
             }
             continue;
         }
@@ -1041,7 +1048,7 @@ __global__ __launch_bounds__(256) void sbr_synthesis_kernel(SbrArgs A)
             float a, b;
             if (l < t0) fetch(xc + (l + 2) * 64, kprev, a, b);
             else fetch(xs + l * 64, 64, a, b);
-            slot(a, b, true, (size_t)f * spf + sps * l);
+            slot(a, b, true, batch_frame(A, f) * spf + sps * l);
         }
     }
 }
@@ -1058,7 +1065,7 @@ __global__ __launch_bounds__(256) void sbr_state_kernel(SbrArgs A)
     const int c = (int)(cf % (uint32_t)A.nch);
     const SbrRec& R = A.recs[cf];
     SbrChState& S = A.state[(size_t)R.slot * 2 + c];
-    const float* t = A.time + (size_t)cf * 1024 + 736;
+    const float* t = A.time + batch_cf(A, cf) * 1024 + 736;
     for (int k = u; k < 288; k += 64) S.tail[k] = t[k];
     if (A.ps) {  // synthesis history of both output channels comes from xps
         for (int oc = 0; oc < 2; oc++) {
@@ -1082,11 +1089,43 @@ __global__ __launch_bounds__(256) void sbr_state_kernel(SbrArgs A)
     for (int k = u; k < 640; k += 64) (&S.gq[0][0][0])[k] = g[k];
 }
 
+// ---------------------------------------------------------------------------------------------
+// JAAD_SBR_UPSAMPLE frames: SBR.upsample (A/sbr/SBR.java:302-309) of the core output -- data[2i] =
+// data[2i+1] = core[i] for i = len/2-1 .. 1, data[0] and data[1] keep core[0] and core[1] -- then
+// SampleBuffer.accept; one channel (SCE, PS) is accepted once and duplicated to stereo
+// (A/syntax/SyntacticElements.java:243-245).  Downsampled SBR (frame length = sample length):
+// the core as it is (A/syntax/CPE.java:201).  One block per frame.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void sbr_upsample_kernel(SbrArgs A)
+{
+    const size_t f = A.ups[blockIdx.x];
+    const int nch = A.nch;
+    const float* c0 = A.time + (size_t)f * nch * 1024;
+    const float* c1 = nch == 2 ? c0 + 1024 : c0;
+    const int spf = A.down ? 1024 : 2048;
+    for (int n = threadIdx.x; n < spf; n += blockDim.x) {
+        const int k = A.down ? n : (n == 1 ? 1 : n >> 1);
+        const float l = c0[k], r = c1[k];
+        const size_t o = (size_t)f * spf + n;
+        if (A.out_mode & JAAD_PCM_FLOAT32) {
+            reinterpret_cast<float2*>(A.pcm)[o] = make_float2(l, r);
+        } else {
+            uint32_t sl = (uint32_t)(uint16_t)(int16_t)java_round16(l), sr = (uint32_t)(uint16_t)(int16_t)java_round16(r);
+            if (!(A.out_mode & JAAD_PCM_LITTLE_ENDIAN)) {
+                sl = ((sl & 0xFF) << 8) | (sl >> 8);
+                sr = ((sr & 0xFF) << 8) | (sr >> 8);
+            }
+            reinterpret_cast<uint32_t*>(A.pcm)[o] = sl | (sr << 16);
+        }
+    }
+}
+
 }  // namespace
 
 hipError_t launch_sbr(const SbrArgs& a, hipStream_t stream, const uint32_t* fix_dev, const uint32_t* fix_counts,
                       int n_fix_passes)
 {
+    if (a.n_ups) hipLaunchKernelGGL(sbr_upsample_kernel, dim3(a.n_ups), dim3(256), 0, stream, a);
     const dim3 blk(256);
     if (a.n_cf) {
         const dim3 g((a.n_cf + kWavesPerBlock - 1) / kWavesPerBlock);

@@ -266,6 +266,33 @@ bool header_differs(const jaad_sbr_header& a, const jaad_sbr_header& b)  // Head
 
 }  // namespace
 
+SbrHost::SbrHost(int out_sf_index) : out_sf_(out_sf_index)
+{
+    tabs_.reserve(kMaxTables);
+    fbt_.reserve(kMaxTables);
+    keys_.reserve(kMaxTables);
+    // table 0: before the first SBR header (Channel.process_channel with sbr.hdr == null,
+    // A/sbr/Channel.java:589-617) the analysis keeps 32 bands and nothing is generated or
+    // adjusted: kx = 32, M = 0, no patch, no limiter band.  Its key never matches a header
+    // (start_freq is a 4-bit field).
+    auto t = std::make_unique<SbrFbt>();
+    std::memset(t.get(), 0, sizeof(SbrFbt));
+    t->kx = 32;
+    t->max_src = -1;
+    SbrTab g;
+    std::memset(&g, 0, sizeof g);
+    g.kx = 32;
+    std::memset(g.src_p, 0xFF, sizeof g.src_p);
+    jaad_sbr_header key;
+    std::memset(&key, 0, sizeof key);
+    key.start_freq = 0xFF;
+    keys_.push_back(key);
+    fbt_.push_back(std::move(t));
+    tabs_.push_back(g);
+}
+
+bool SbrHost::header_changes(const jaad_sbr_header& a, const jaad_sbr_header& b) { return header_differs(a, b); }
+
 void SbrHost::reset_slot(SbrHostSlot& s)
 {
     std::memset(&s, 0, sizeof s);
@@ -369,8 +396,26 @@ int SbrHost::frame(SbrHostSlot& st, const jaad_sbr_frame& fr, int nch, bool firs
             if (st.table < 0) return JAAD_ERR_BITSTREAM;
         }
     }
-    if (!st.have_hdr) return JAAD_ERR_UNSUPPORTED;  // frames before the first SBR header
-    if (nch == 2 && fr.coupling) return JAAD_ERR_UNSUPPORTED;
+    if (!st.have_hdr) {
+        // no SBR header yet: SBR.decode marks the data valid without reading it and
+        // process_channel only analyses and resynthesises the low band (A/sbr/SBR.java:179-184,
+        // A/sbr/Channel.java:589-617); nothing of the parameter state moves (sbr_save_prev_data
+        // runs only with a header, A/sbr/SBR2.java:150-153)
+        for (int c = 0; c < nch; c++) {
+            SbrRec& r = rec[c];
+            std::memset(&r, 0, sizeof r);
+            r.L_E = 1;
+            r.t_E[1] = 32;  // one envelope over the frame: the HF stage copies rows 2..33
+            r.table = kNoHeaderTable;
+            r.first = first ? 1 : 0;
+            r.slot = slot;
+            r.kx_prev = (uint8_t)st.kx_prev;
+            r.M_prev = (uint8_t)st.M_prev;
+            r.e_off = e_base + epos;
+        }
+        return JAAD_OK;
+    }
+    const bool coupled = nch == 2 && fr.coupling;
     const SbrFbt& t = *fbt_[st.table];
     const jaad_sbr_header& h = st.hdr;
     const int s_lim = h.limiter_bands & 3;
@@ -388,7 +433,7 @@ int SbrHost::frame(SbrHostSlot& st, const jaad_sbr_frame& fr, int nch, bool firs
         for (int l = 0; l < L_E; l++)
             if (in.f[l] > 1) return JAAD_ERR_BITSTREAM;
         r.L_E = (uint8_t)L_E;
-        r.table = (uint8_t)st.table;
+        r.table = (uint16_t)st.table;
         r.lim_bands = (uint8_t)s_lim;
         r.flags = (uint8_t)((reset ? kSbrReset : 0) | (h.smoothing_mode ? 0 : kSbrSmooth) |
                             (h.interpol_freq ? kSbrInterpol : 0) | kSbrProcess);
@@ -428,33 +473,72 @@ int SbrHost::frame(SbrHostSlot& st, const jaad_sbr_frame& fr, int nch, bool firs
             ch.invf_prev[i] = in.invf_mode[i];
         }
 
-        // dequantisation (NoiseEnvelope.dequantChannel, no coupling)
-        const bool amp_res = !(L_E == 1 && in.frame_class == FIXFIX) && h.amp_res;
-        const int amp = amp_res ? 0 : 1;
+        // dequantisation: NoiseEnvelope.dequantChannel, or unmap for a coupled pair
+        // (A/sbr/NoiseEnvelope.java:250-281, :299-344; SBR2.sbr_data :125-129)
+        auto amp_of = [&](const jaad_sbr_channel& x) {  // Channel.sbr_envelope (A/sbr/Channel.java:130-133)
+            return (!(x.L_E == 1 && x.frame_class == FIXFIX) && h.amp_res) ? 0 : 1;
+        };
         r.e_off = e_base + epos;
-        for (int l = 0; l < L_E; l++) {
-            const int nb = t.n[in.f[l]];
-            const int16_t* Er = in.E[l];
-            float* out = epool + epos;
-            for (int k = 0; k < nb; k++) {
-                const int E = Er[k];
-                const int e = E >> amp;
-                float v = 0.0f;
-                if (e >= 0 && e < 64) {
-                    v = JAAD_SBR_E_DEQ[e];
-                    if (amp != 0 && (E & 1) != 0) v = v * 1.414213562f;
+        if (!coupled) {
+            const int amp = amp_of(in);
+            for (int l = 0; l < L_E; l++) {
+                const int nb = t.n[in.f[l]];
+                const int16_t* Er = in.E[l];
+                float* out = epool + epos;
+                for (int k = 0; k < nb; k++) {
+                    const int E = Er[k];
+                    const int e = E >> amp;
+                    float v = 0.0f;
+                    if (e >= 0 && e < 64) {
+                        v = JAAD_SBR_E_DEQ[e];
+                        if (amp != 0 && (E & 1) != 0) v = v * 1.414213562f;
+                    }
+                    out[k] = v;
                 }
-                out[k] = v;
+                epos += (uint32_t)nb;
             }
-            epos += (uint32_t)nb;
+            for (int l = 0; l < L_Q; l++)
+                for (int k = 0; k < t.N_Q; k++) {
+                    const int q = in.Q[l][k];
+                    const bool ok = q >= 0 && q <= 30;
+                    r.q_div[l][k] = ok ? JAAD_SBR_Q_DIV[q] : 0.0f;
+                    r.q_div2[l][k] = ok ? JAAD_SBR_Q_DIV2[q] : 0.0f;
+                }
+        } else {
+            // both channels from channel 0's level and channel 1's balance, over channel 0's
+            // envelopes (channel 1's grid is a copy of it, Channel.couple)
+            const jaad_sbr_channel& c0 = fr.ch[0];
+            const jaad_sbr_channel& c1 = fr.ch[1];
+            const int amp0 = amp_of(c0), amp1 = amp_of(c1);
+            for (int l = 0; l < c0.L_E; l++) {
+                const int nb = t.n[c0.f[l]];
+                float* out = epool + epos;
+                for (int k = 0; k < nb; k++) {
+                    const int ch0E = c0.E[l][k];
+                    const int exp0 = (ch0E >> amp0) + 1;
+                    const int exp1 = c1.E[l][k] >> amp1;
+                    float v = 0.0f;
+                    if (!(exp0 < 0 || exp0 >= 64 || exp1 < 0 || exp1 > 24)) {
+                        float tmp = JAAD_SBR_E_DEQ[exp0];
+                        // tmp *= 1.414213562: a double literal, so the product is rounded once
+                        // from double (unlike dequantChannel's float constant)
+                        if (amp0 != 0 && (ch0E & 1) != 0) tmp = (float)((double)tmp * 1.414213562);
+                        v = tmp * JAAD_SBR_E_PAN[c == 0 ? exp1 : 24 - exp1];
+                    }
+                    out[k] = v;
+                }
+                epos += (uint32_t)nb;
+            }
+            const float(*qd)[13] = c == 0 ? JAAD_SBR_Q_DIV_LEFT : JAAD_SBR_Q_DIV_RIGHT;
+            const float(*qd2)[13] = c == 0 ? JAAD_SBR_Q_DIV2_LEFT : JAAD_SBR_Q_DIV2_RIGHT;
+            for (int l = 0; l < c0.L_Q; l++)
+                for (int k = 0; k < t.N_Q; k++) {
+                    const int q0 = c0.Q[l][k], q1 = c1.Q[l][k];
+                    const bool ok = !((q0 < 0 || q0 > 30) || (q1 < 0 || q1 > 24));
+                    r.q_div[l][k] = ok ? qd[q0][q1 >> 1] : 0.0f;
+                    r.q_div2[l][k] = ok ? qd2[q0][q1 >> 1] : 0.0f;
+                }
         }
-        for (int l = 0; l < L_Q; l++)
-            for (int k = 0; k < t.N_Q; k++) {
-                const int q = in.Q[l][k];
-                const bool ok = q >= 0 && q <= 30;
-                r.q_div[l][k] = ok ? JAAD_SBR_Q_DIV[q] : 0.0f;
-                r.q_div2[l][k] = ok ? JAAD_SBR_Q_DIV2[q] : 0.0f;
-            }
 
         // sinusoids: bs_add_harmonic cleared, then N_high flags (SBR2.java:63-72, SBR.java:249-254)
         const uint64_t hmask = t.N_high >= 64 ? ~0ull : ((1ull << t.N_high) - 1);

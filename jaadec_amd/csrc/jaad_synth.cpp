@@ -203,14 +203,57 @@ void gen_sbr_stream(const jaad_synth_params& P, jaad_sbr_frame* out, uint32_t s)
         for (int k = 0; k < 64; k++) lvl[c][k] = P.sbr_level - (int)r.below(5);
         for (int k = 0; k < 5; k++) qv[c][k] = 8 + (int)r.below(16);
     }
+    int bal[64], qbal[5];  // coupled channel 1: balance walks (even values 0..24)
+    for (int k = 0; k < 64; k++) bal[k] = 2 * (int)r.below(13);
+    for (int k = 0; k < 5; k++) qbal[k] = 2 * (int)r.below(13);
     for (uint32_t fi = 0; fi < P.frames_per_stream; fi++) {
         jaad_sbr_frame& F = out[(size_t)s * P.frames_per_stream + fi];
         std::memset(&F, 0, sizeof F);
-        F.header_present = 1;
-        F.coupling = 0;
         // Header.java defaults (A/sbr/Header.java:12-22,44-60) with start 5 / stop 9 / xover 0
         F.hdr = jaad_sbr_header{1, 5, 9, 0, 2, 1, 2, 2, 2, 1, 1, 0};
+        if (fi < P.nohdr_frames) continue;  // before the first header: no SBR data is read
+        F.header_present = 1;
+        // drawn first so that the other fields do not depend on the options (the default stream
+        // is the same with and without them)
+        const bool ups = P.upsample_percent && r.percent(P.upsample_percent);
+        const bool coupled = nch == 2 && P.coupling_percent && r.percent(P.coupling_percent);
+        if (ups) {  // the element's SBR data is missing or unusable this frame
+            F.status = JAAD_SBR_UPSAMPLE;
+            F.header_present = 0;
+            continue;
+        }
+        F.coupling = coupled ? 1 : 0;
         for (int c = 0; c < nch; c++) {
+            if (c == 1 && coupled) {  // Channel.couple (A/sbr/Channel.java:103-122), balance data
+                jaad_sbr_channel& C1 = F.ch[1];
+                const jaad_sbr_channel& C0 = F.ch[0];
+                C1.frame_class = C0.frame_class;
+                C1.L_E = C0.L_E;
+                C1.L_Q = C0.L_Q;
+                C1.bs_pointer = C0.bs_pointer;
+                std::memcpy(C1.t_E, C0.t_E, sizeof C1.t_E);
+                std::memcpy(C1.t_Q, C0.t_Q, sizeof C1.t_Q);
+                std::memcpy(C1.f, C0.f, sizeof C1.f);
+                std::memcpy(C1.invf_mode, C0.invf_mode, sizeof C1.invf_mode);
+                const bool amp_res = !(C0.L_E == 1);
+                for (int l = 0; l < C1.L_E; l++)
+                    for (int k = 0; k < 64; k++) {  // E << delta: even, pan 0..24 (x2 at 1.5 dB)
+                        bal[k] += 2 * ((int)r.below(3) - 1);
+                        bal[k] = bal[k] < 0 ? 0 : (bal[k] > 24 ? 24 : bal[k]);
+                        C1.E[l][k] = (int16_t)(amp_res ? bal[k] : 2 * bal[k]);
+                    }
+                for (int l = 0; l < C1.L_Q; l++)
+                    for (int k = 0; k < 5; k++) {
+                        qbal[k] += 2 * ((int)r.below(3) - 1);
+                        qbal[k] = qbal[k] < 0 ? 0 : (qbal[k] > 24 ? 24 : qbal[k]);
+                        C1.Q[l][k] = (int16_t)qbal[k];
+                    }
+                C1.add_harmonic_flag = (uint8_t)r.percent(30);
+                if (C1.add_harmonic_flag)
+                    for (int k = 0; k < 64; k++)
+                        if (r.percent(5)) C1.add_harmonic |= 1ull << k;
+                continue;
+            }
             jaad_sbr_channel& C = F.ch[c];
             const int L_E = 1 + (int)r.below(2);  // FIXFIX: bs_num_env = 1 << (0|1)
             const int fres = (int)r.below(2);

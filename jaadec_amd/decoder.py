@@ -48,10 +48,13 @@ class DecoderConfig:
     explicit SBR (AOT 5) or SBR + PS (AOT 29)."""
 
     def __init__(self, profile: int = 2, sf_index: int = 3, channel_config: int = 2, tns_mode: int = N.TNS_COMPAT,
-                 sbr: bool = False, ps: bool = False, ext_sf_index: int | None = None):
+                 sbr: bool = False, ps: bool = False, ext_sf_index: int | None = None, from_asc: bool = False):
         self.profile, self.sf_index, self.channel_config, self.tns_mode = profile, sf_index, channel_config, tns_mode
         self.sbr, self.ps = bool(sbr), bool(ps)
         self.ext_sf_index = (sf_index - 3) if ext_sf_index is None and sbr else (ext_sf_index or 0)
+        # decoded from an AudioSpecificConfig: outputFrequency is set to the core rate there
+        # (A/DecoderConfig.java:180), so implicit SBR does not double it (setSBRPresent :124-135)
+        self.from_asc = bool(from_asc)
 
     @classmethod
     def decode(cls, asc: bytes) -> "DecoderConfig":
@@ -69,7 +72,8 @@ class DecoderConfig:
             if aot == 2 and len(asc) > 1 and (asc[1] >> 2) & 1:
                 raise AACException("config uses 960-sample frames, not yet supported") from e  # :206-207
             raise AACException(f"unsupported configuration ({e})") from e
-        return cls(c.profile, c.sf_index, c.channel_config, N.TNS_COMPAT, bool(c.sbr), bool(c.ps), c.ext_sf_index)
+        return cls(c.profile, c.sf_index, c.channel_config, N.TNS_COMPAT, bool(c.sbr), bool(c.ps), c.ext_sf_index,
+                   from_asc=True)
 
     def getChannelCount(self) -> int:  # noqa: N802  (Java name)
         return 2  # mono -> stereo while sbrEnabled (A/DecoderConfig.java:108-115)
@@ -174,20 +178,21 @@ class Decoder:
 
     def _implicit_sbr(self, first: bytes) -> None:
         """A core configuration whose first frame carries SBR data is upgraded as the reference
-        upgrades its DecoderConfig (A/syntax/ChannelElement.java:63-74, SBR.java:100): doubled
-        output rate, stereo output, PS applied if present."""
+        upgrades its DecoderConfig (A/syntax/ChannelElement.java:63-74, SBR.java:100): stereo
+        output, PS applied if present; the output rate doubled for an ADTS-created decoder, kept
+        (downsampled SBR) for one created from an AudioSpecificConfig (native.implicit_sbr_cfg)."""
         c = self.config
         try:
             if c.sbr or not N.probe_sbr(c.cfg(), first):
                 return
-            up = N.implicit_sbr_cfg(c.cfg())
+            up = N.implicit_sbr_cfg(c.cfg(), from_asc=c.from_asc)
         except N.JaadError as e:
             raise AACException(str(e)) from e
         if not self._own:
             raise AACException("implicit SBR in a stream decoded on a shared core-only context")
         self._ctx.close()
         self.config = DecoderConfig(c.profile, c.sf_index, c.channel_config, c.tns_mode, True, bool(up.ps),
-                                    up.ext_sf_index)
+                                    up.ext_sf_index, from_asc=c.from_asc)
         self._ctx = N.Context(self.config.cfg(), 1)
 
     def _parse(self, frames: list) -> N.Batch:

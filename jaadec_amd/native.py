@@ -48,7 +48,8 @@ PS_FRAME_DTYPE = np.dtype([("iid_mode", "u1"), ("icc_mode", "u1"), ("num_env", "
                            ("border", "u1", (6,)), ("reserved", "u1", (2,)), ("iid", "i1", (5, 34)),
                            ("icc", "i1", (5, 34)), ("ipd", "i1", (5, 17)), ("opd", "i1", (5, 17)),
                            ("pad", "u1", (6,))])
-SBR_FRAME_DTYPE = np.dtype([("header_present", "u1"), ("coupling", "u1"), ("ps_present", "u1"), ("reserved", "u1"),
+SBR_OK, SBR_UPSAMPLE = 0, 1  # jaad_sbr_frame.status
+SBR_FRAME_DTYPE = np.dtype([("header_present", "u1"), ("coupling", "u1"), ("ps_present", "u1"), ("status", "u1"),
                             ("hdr", SBR_HEADER_DTYPE), ("ch", SBR_CHANNEL_DTYPE, (2,)), ("ps", PS_FRAME_DTYPE)])
 assert SBR_CHANNEL_DTYPE.itemsize == 712 and PS_FRAME_DTYPE.itemsize == 528 and SBR_FRAME_DTYPE.itemsize == 1968
 
@@ -71,7 +72,8 @@ class SynthParams(C.Structure):
                 ("tns_percent", C.c_uint8), ("pns_percent", C.c_uint8), ("is_percent", C.c_uint8),
                 ("ms_mode", C.c_uint8), ("global_gain", C.c_uint8), ("escape_permille", C.c_uint8),
                 ("common_window", C.c_uint8), ("sbr", C.c_uint8), ("sbr_level", C.c_uint8),
-                ("pns_state0", C.c_uint32)]
+                ("pns_state0", C.c_uint32), ("coupling_percent", C.c_uint8), ("upsample_percent", C.c_uint8),
+                ("nohdr_frames", C.c_uint8), ("reserved", C.c_uint8)]
 
 
 # every symbol include/jaad_gpu.h declares (checked by tests/test_abi.py)
@@ -409,14 +411,16 @@ def probe_sbr(cfg: StreamCfg, frame: bytes) -> bool:
     return bool(found.value & 1)
 
 
-def implicit_sbr_cfg(cfg: StreamCfg) -> StreamCfg:
+def implicit_sbr_cfg(cfg: StreamCfg, from_asc: bool = False) -> StreamCfg:
     """The configuration the reference switches to when it meets SBR data in a core stream
-    (DecoderConfig.setSBRPresent, A/DecoderConfig.java:124-135): doubled output rate; a mono
-    core decodes to stereo (SCE.isStereo) with PS applied when present (psEnabled)."""
-    # no doubled rate above 48 kHz: SampleFrequency.duplicated() is SF_NONE, the SBR runs
-    # downsampled (A/DecoderConfig.java:124-135, A/sbr/SBR.java:100)
+    (DecoderConfig.setSBRPresent, A/DecoderConfig.java:124-135): a mono core decodes to stereo
+    (SCE.isStereo) with PS applied when present (psEnabled).  The output rate is doubled for a
+    decoder created from an ADTS header (AudioDecoderInfo: outputFrequency unset) unless
+    SampleFrequency.duplicated() is SF_NONE (above 48 kHz); a decoder created from an
+    AudioSpecificConfig already has outputFrequency = the core rate (A/DecoderConfig.java:180),
+    so its SBR runs downsampled at the core rate (A/sbr/SBR.java:100)."""
     return make_cfg(cfg.sf_index, cfg.channel_config, cfg.tns_mode, sbr=True, ps=cfg.channel_config == 1,
-                    down=cfg.sf_index < 3)
+                    down=from_asc or cfg.sf_index < 3)
 
 
 class Parser:

@@ -482,6 +482,24 @@ static int decode_frame(const jaad_stream_cfg* cfg, orc_stream* st, const jaad_b
         orc_filterbank(info->window_sequence, info->window_shape, info->window_shape_prev, iq[c], data[c],
                        st->overlap[c]);
     }
+    if (cfg->sbr && b->sbr[f].status == JAAD_SBR_UPSAMPLE) {
+        /* SBR invalid (ChannelElement.isSBRPresent false, A/syntax/ChannelElement.java:76-78):
+         * CPE.process / SCE.process upsample the core instead (A/syntax/CPE.java:201-204,
+         * A/syntax/SCE.java:129-131) when the buffer is longer than a frame; the SBR object is
+         * not touched.  SBR.upsample (A/sbr/SBR.java:302-309) runs i = len/2-1 down to 1, so
+         * data[0] and data[1] keep the core's first two samples. */
+        if (frame_samples(cfg) != 1024)
+            for (int c = 0; c < nch; c++)
+                for (int i = 1024 - 1; i > 0; --i) {
+                    const float v = data[c][i];
+                    data[c][2 * i] = v;
+                    data[c][2 * i + 1] = v;
+                }
+        /* one channel accepted for an SCE: SyntacticElements.process duplicates it */
+        const float* chans[2] = {data[0], nch == 2 ? data[1] : data[0]};
+        orc_pcm_pack(chans, 2, frame_samples(cfg), flags, pcm);
+        return JAAD_OK;
+    }
     if (cfg->sbr) {
         /* CPE.process / SCE.process -> SBR.process (A/syntax/CPE.java:195-204, SCE.java:122-133) */
         if (!st->sbr) {

@@ -87,6 +87,10 @@ typedef struct {
     int tables_gen; /* bumped on each table reset */
     int prev_gen[2], have_prev[2];
     int E_prev[2][64], Q_prev[2][64], f_prev[2];
+    /* what the reader's Channel keeps between frames: L_E / L_Q (a coupled channel 1 reads its
+     * dtdf bits with the previous frame's counts, A/sbr/SBR2.java:48-50) and bs_df_env /
+     * bs_df_noise (entries past those counts stay as an earlier frame left them) */
+    int L_E_last[2], L_Q_last[2], df_env[2][9], df_noise[2][3];
     int ps_have_hdr, ps_iid_mode, ps_icc_mode;
     int ps_first_iid[34], ps_first_icc[34];
 } jaad_sbr_wstate;
@@ -250,6 +254,109 @@ static int put_noise(Sw* w, jaad_sbr_wstate* s, int ch, const jaad_sbr_channel* 
     return 0;
 }
 
+/* can envelope l (noise envelope l) of an uncoupled channel be time-delta coded: every delta in
+ * the time tree (T_HUFFMAN_ENV_*, T_HUFFMAN_NOISE_3_0DB) */
+static int env_time_ok(const jaad_sbr_wstate* s, int ch, const jaad_sbr_channel* c, int l)
+{
+    const int amp_res = (c->L_E == 1 && c->frame_class == 0) ? 0 : s->hdr.amp_res;
+    const int(*th)[2] = amp_res ? JAAD_SBR_T_HUFFMAN_ENV_3_0DB : JAAD_SBR_T_HUFFMAN_ENV_1_5DB;
+    const int tn = amp_res ? NN(JAAD_SBR_T_HUFFMAN_ENV_3_0DB) : NN(JAAD_SBR_T_HUFFMAN_ENV_1_5DB);
+    uint32_t code;
+    int len;
+    for (int k = 0; k < s->n[c->f[l] & 1]; k++)
+        if (tree_find(th, tn, 0, c->E[l][k] - env_prev_value(s, ch, c, l, k) - 64, 0, 0, &code, &len)) return 0;
+    return 1;
+}
+static int noise_time_ok(const jaad_sbr_wstate* s, int ch, const jaad_sbr_channel* c, int l)
+{
+    uint32_t code;
+    int len;
+    for (int k = 0; k < s->N_Q; k++) {
+        const int p = l == 0 ? s->Q_prev[ch][k] : c->Q[l - 1][k];
+        if (tree_find(JAAD_SBR_T_HUFFMAN_NOISE_3_0DB, NN(JAAD_SBR_T_HUFFMAN_NOISE_3_0DB), 0, c->Q[l][k] - p - 64, 0, 0,
+                      &code, &len))
+            return 0;
+    }
+    return 1;
+}
+
+/* coded value of band k of envelope l of a coupled channel 1 (sbr_envelope with coupled = true:
+ * BAL tables, values transmitted >> 1, A/sbr/Channel.java:125-198); -1 when not codable */
+static int bal_env_ok(const jaad_sbr_wstate* s, int ch, const jaad_sbr_channel* c, int l, int df)
+{
+    const int amp_res = (c->L_E == 1 && c->frame_class == 0) ? 0 : s->hdr.amp_res;
+    const int nb = s->n[c->f[l] & 1], range = amp_res ? 12 : 24;
+    for (int k = 0; k < nb; k++) {
+        const int v = c->E[l][k];
+        const int base = df ? env_prev_value(s, ch, c, l, k) : (k ? c->E[l][k - 1] : 0);
+        const int d = v - base;
+        if (v < 0 || (d & 1)) return 0;
+        if (!df && k == 0) {
+            if ((v >> 1) >= (1 << (amp_res ? 5 : 6))) return 0;
+        } else if (d / 2 < -range || d / 2 > range) {
+            return 0;
+        }
+    }
+    return 1;
+}
+static int put_bal_envelope(Sw* w, jaad_sbr_wstate* s, int ch, const jaad_sbr_channel* c, const int* df)
+{
+    const int amp_res = (c->L_E == 1 && c->frame_class == 0) ? 0 : s->hdr.amp_res;
+    const int(*th)[2] = amp_res ? JAAD_SBR_T_HUFFMAN_ENV_BAL_3_0DB : JAAD_SBR_T_HUFFMAN_ENV_BAL_1_5DB;
+    const int(*fh)[2] = amp_res ? JAAD_SBR_F_HUFFMAN_ENV_BAL_3_0DB : JAAD_SBR_F_HUFFMAN_ENV_BAL_1_5DB;
+    const int tn = amp_res ? NN(JAAD_SBR_T_HUFFMAN_ENV_BAL_3_0DB) : NN(JAAD_SBR_T_HUFFMAN_ENV_BAL_1_5DB);
+    const int fn = amp_res ? NN(JAAD_SBR_F_HUFFMAN_ENV_BAL_3_0DB) : NN(JAAD_SBR_F_HUFFMAN_ENV_BAL_1_5DB);
+    for (int l = 0; l < c->L_E; l++) {
+        if (!bal_env_ok(s, ch, c, l, df[l])) return FAIL;
+        const int nb = s->n[c->f[l] & 1];
+        if (!df[l]) {
+            sput(w, (uint32_t)(c->E[l][0] >> 1), amp_res ? 5 : 6);
+            for (int k = 1; k < nb; k++)
+                if (put_tree(w, fh, fn, 64, (c->E[l][k] - c->E[l][k - 1]) / 2)) return FAIL;
+        } else {
+            for (int k = 0; k < nb; k++)
+                if (put_tree(w, th, tn, 64, (c->E[l][k] - env_prev_value(s, ch, c, l, k)) / 2)) return FAIL;
+        }
+    }
+    return 0;
+}
+static int bal_noise_ok(const jaad_sbr_wstate* s, int ch, const jaad_sbr_channel* c, int l, int df)
+{
+    for (int k = 0; k < s->N_Q; k++) {
+        const int v = c->Q[l][k];
+        const int base = df ? (l == 0 ? s->Q_prev[ch][k] : c->Q[l - 1][k]) : (k ? c->Q[l][k - 1] : 0);
+        const int d = v - base;
+        if (v < 0 || (d & 1)) return 0;
+        if (!df && k == 0) {
+            if ((v >> 1) > 31) return 0;
+        } else if (d / 2 < -12 || d / 2 > 12) {
+            return 0;
+        }
+    }
+    return 1;
+}
+static int put_bal_noise(Sw* w, jaad_sbr_wstate* s, int ch, const jaad_sbr_channel* c, const int* df)
+{
+    for (int l = 0; l < c->L_Q; l++) {
+        if (!bal_noise_ok(s, ch, c, l, df[l])) return FAIL;
+        if (!df[l]) {
+            sput(w, (uint32_t)(c->Q[l][0] >> 1), 5);
+            for (int k = 1; k < s->N_Q; k++)
+                if (put_tree(w, JAAD_SBR_F_HUFFMAN_ENV_BAL_3_0DB, NN(JAAD_SBR_F_HUFFMAN_ENV_BAL_3_0DB), 64,
+                             (c->Q[l][k] - c->Q[l][k - 1]) / 2))
+                    return FAIL;
+        } else {
+            for (int k = 0; k < s->N_Q; k++) {
+                const int p = l == 0 ? s->Q_prev[ch][k] : c->Q[l - 1][k];
+                if (put_tree(w, JAAD_SBR_T_HUFFMAN_NOISE_BAL_3_0DB, NN(JAAD_SBR_T_HUFFMAN_NOISE_BAL_3_0DB), 64,
+                             (c->Q[l][k] - p) / 2))
+                    return FAIL;
+            }
+        }
+    }
+    return 0;
+}
+
 /* ps_data for records with IID / ICC enabled, fixed borders and no IPD/OPD extension */
 static int put_ps(Sw* w, jaad_sbr_wstate* s, const jaad_ps_frame* p)
 {
@@ -318,10 +425,69 @@ static int put_ps(Sw* w, jaad_sbr_wstate* s, const jaad_ps_frame* p)
     return 0;
 }
 
+/* the FIL element (SyntacticElements.decodeFIL, A/syntax/SyntacticElements.java:169-203) around an
+ * extension payload of `bits` bits in buf: count bytes (escape: count = 15 + esc - 1), payload
+ * padded to whole bytes */
+static long emit_fil(Sw* outw, const uint8_t* buf, size_t bits)
+{
+    const int count = (int)((bits + 7) / 8);
+    if (count > 15 + 255 - 1) return FAIL;
+    sput(outw, 6, 3);
+    if (count >= 15) {
+        sput(outw, 15, 4);
+        sput(outw, (uint32_t)(count - 14), 8);
+    } else {
+        sput(outw, (uint32_t)count, 4);
+    }
+    for (int i = 0; i < count; i++) sput(outw, buf[i], 8);
+    return outw->overflow ? -1 : (long)outw->pos;
+}
+
+/* a grid whose borders do not fit: VARFIX, lead border 3, relative borders 8, 8, 8 -> the third
+ * border 27 puts 2 * 27 + tHFAdj past numTimeSlotsRate + tHFGen (A/sbr/Channel.java:497-503) */
+static void put_bad_grid(Sw* w, jaad_sbr_wstate* s)
+{
+    sput(w, 2, 2);          /* VARFIX */
+    sput(w, 3, 2);          /* bs_abs_bord */
+    sput(w, 3, 2);          /* bs_num_env - 1 */
+    for (int r = 0; r < 3; r++) sput(w, 3, 2); /* rel = 2 * 3 + 2 */
+    sput(w, rnd(s, 5), 3);  /* bs_pointer (sbr_log2(5) = 3 bits) */
+    for (int e = 0; e < 4; e++) sput(w, rnd(s, 2), 1);
+    for (int i = 0; i < 16; i++) sput(w, rnd(s, 2), 1); /* whatever followed: never read */
+}
+
+/* bs_df_env / bs_df_noise of one channel: the reader reads n_env / n_noise flags (the channel's
+ * L_E / L_Q when it reads them) and keeps older entries; an envelope past them takes the entry an
+ * earlier frame left */
+static void choose_df(jaad_sbr_wstate* s, int ch, const jaad_sbr_channel* C, int n_env, int n_noise, int bal,
+                      int* dfe, int* dfq)
+{
+    const int prev_ok = s->have_prev[ch] && s->prev_gen[ch] == s->tables_gen;
+    for (int l = 0; l < C->L_E; l++) {
+        if (l >= n_env) {
+            dfe[l] = s->df_env[ch][l];
+            continue;
+        }
+        dfe[l] = (l > 0 || prev_ok) ? (int)rnd(s, 2) : 0;
+        if (dfe[l] && !(bal ? bal_env_ok(s, ch, C, l, 1) : env_time_ok(s, ch, C, l))) dfe[l] = 0;
+    }
+    for (int l = 0; l < C->L_Q; l++) {
+        if (l >= n_noise) {
+            dfq[l] = s->df_noise[ch][l];
+            continue;
+        }
+        dfq[l] = (l > 0 || prev_ok) ? (int)rnd(s, 2) : 0;
+        if (dfq[l] && !(bal ? bal_noise_ok(s, ch, C, l, 1) : noise_time_ok(s, ch, C, l))) dfq[l] = 0;
+    }
+}
+
 /*
  * The FIL element carrying `rec` for the channel element just written (nch 1: SCE, 2: CPE),
- * MSB-first into out[cap].  Returns its length in bits, or -1 when the record is not
- * representable by this writer.
+ * MSB-first into out[cap].  Returns its length in bits (0: no FIL element, for a frame whose SBR
+ * payload is missing), or -1 when the record is not representable by this writer.
+ *   status JAAD_SBR_UPSAMPLE: no payload, or a payload whose grid does not fit (sbr_data fails);
+ *   no header seen yet: a payload of bs_header_flag = 0 only (the reader skips sbr_data);
+ *   coupling: SBR2.sbr_data's coupled branch (A/sbr/SBR2.java:44-72), channel 1 balance coded.
  */
 long jaad_sbr_fil_bits(void* state, int nch, const jaad_sbr_frame* rec, uint8_t* out, size_t cap)
 {
@@ -332,11 +498,38 @@ long jaad_sbr_fil_bits(void* state, int nch, const jaad_sbr_frame* rec, uint8_t*
     uint8_t buf[1024];
     memset(buf, 0, sizeof buf);
     Sw w = {buf, sizeof buf, 0, 0};
+    if (rec->status == JAAD_SBR_UPSAMPLE) {
+        if (rec->header_present) return FAIL;
+        if (!s->have_hdr || rnd(s, 2)) return 0; /* no SBR payload after the element */
+    }
     const int crc = (int)rnd(s, 4) == 0;
     sput(&w, crc ? 14 : 13, 4);
     if (crc) sput(&w, rnd(s, 1024), 10);
+    if (rec->status == JAAD_SBR_UPSAMPLE) { /* a header-less payload whose grid fails */
+        sput(&w, 0, 1);
+        if (nch == 1) {
+            sput(&w, 0, 1);
+            put_bad_grid(&w, s);
+        } else {
+            sput(&w, 0, 1);
+            const int coupled = (int)rnd(s, 2);
+            sput(&w, (uint32_t)coupled, 1);
+            if (!coupled && rnd(s, 2)) { /* channel 0's grid fits, channel 1's does not */
+                sput(&w, 0, 2);
+                sput(&w, rnd(s, 3), 2);
+                sput(&w, rnd(s, 2), 1);
+            }
+            put_bad_grid(&w, s);
+        }
+        if (w.overflow) return FAIL;
+        return emit_fil(outw, buf, w.pos);
+    }
+    if (!rec->header_present && !s->have_hdr) { /* before the first header: nothing is read */
+        sput(&w, 0, 1);
+        for (int i = 0; i < 8; i++) sput(&w, rnd(s, 2), 1);
+        return emit_fil(outw, buf, w.pos);
+    }
     /* header */
-    if (!rec->header_present && !s->have_hdr) return FAIL;
     sput(&w, rec->header_present, 1);
     if (rec->header_present) {
         put_header(&w, s, &rec->hdr);
@@ -355,35 +548,62 @@ long jaad_sbr_fil_bits(void* state, int nch, const jaad_sbr_frame* rec, uint8_t*
     } else if (memcmp(&rec->hdr, &s->hdr, sizeof rec->hdr)) {
         return FAIL; /* a header-less frame carries the current header */
     }
-    if (rec->coupling) return FAIL;
-    int dfe[2][5], dfq[2][2];
-    for (int c = 0; c < nch; c++) {
-        const jaad_sbr_channel* C = &rec->ch[c];
-        const int prev_ok = s->have_prev[c] && s->prev_gen[c] == s->tables_gen;
-        for (int l = 0; l < C->L_E; l++) dfe[c][l] = (l > 0 || prev_ok) ? (int)rnd(s, 2) : 0;
-        for (int l = 0; l < C->L_Q; l++) dfq[c][l] = (l > 0 || prev_ok) ? (int)rnd(s, 2) : 0;
-    }
-    if (nch == 1) {
+    const int coupled = nch == 2 && rec->coupling;
+    int dfe[2][9], dfq[2][3];
+    if (coupled) {
+        const jaad_sbr_channel *C0 = &rec->ch[0], *C1 = &rec->ch[1];
+        if (C1->frame_class != C0->frame_class || C1->L_E != C0->L_E || C1->L_Q != C0->L_Q ||
+            C1->bs_pointer != C0->bs_pointer || memcmp(C1->t_E, C0->t_E, C0->L_E + 1) ||
+            memcmp(C1->f, C0->f, C0->L_E) || memcmp(C1->t_Q, C0->t_Q, C0->L_Q + 1) ||
+            memcmp(C1->invf_mode, C0->invf_mode, (size_t)s->N_Q))
+            return FAIL; /* not what Channel.couple leaves */
+        choose_df(s, 0, C0, C0->L_E, C0->L_Q, 0, dfe[0], dfq[0]);
+        /* channel 1 reads its flags before couple(): with the previous frame's L_E / L_Q */
+        choose_df(s, 1, C1, s->L_E_last[1], s->L_Q_last[1], 1, dfe[1], dfq[1]);
         sput(&w, 0, 1); /* bs_data_extra */
-    } else {
-        sput(&w, 1, 1); /* bs_data_extra: 8 reserved bits */
-        sput(&w, 0x5A, 8);
-        sput(&w, 0, 1); /* bs_coupling */
-    }
-    for (int c = 0; c < nch; c++)
-        if (put_grid(&w, &rec->ch[c])) return FAIL;
-    for (int c = 0; c < nch; c++) {
-        for (int l = 0; l < rec->ch[c].L_E; l++) sput(&w, (uint32_t)dfe[c][l], 1);
-        for (int l = 0; l < rec->ch[c].L_Q; l++) sput(&w, (uint32_t)dfq[c][l], 1);
-    }
-    for (int c = 0; c < nch; c++)
-        for (int k = 0; k < s->N_Q; k++) sput(&w, rec->ch[c].invf_mode[k] & 3, 2);
-    if (nch == 1) {
-        if (put_envelope(&w, s, 0, &rec->ch[0], dfe[0]) || put_noise(&w, s, 0, &rec->ch[0], dfq[0])) return FAIL;
-    } else {
-        if (put_envelope(&w, s, 0, &rec->ch[0], dfe[0]) || put_envelope(&w, s, 1, &rec->ch[1], dfe[1]) ||
-            put_noise(&w, s, 0, &rec->ch[0], dfq[0]) || put_noise(&w, s, 1, &rec->ch[1], dfq[1]))
+        sput(&w, 1, 1); /* bs_coupling */
+        if (put_grid(&w, C0)) return FAIL;
+        for (int l = 0; l < C0->L_E; l++) sput(&w, (uint32_t)dfe[0][l], 1);
+        for (int l = 0; l < C0->L_Q; l++) sput(&w, (uint32_t)dfq[0][l], 1);
+        for (int l = 0; l < s->L_E_last[1]; l++) sput(&w, (uint32_t)(l < C1->L_E ? dfe[1][l] : s->df_env[1][l]), 1);
+        for (int l = 0; l < s->L_Q_last[1]; l++) sput(&w, (uint32_t)(l < C1->L_Q ? dfq[1][l] : s->df_noise[1][l]), 1);
+        for (int k = 0; k < s->N_Q; k++) sput(&w, C0->invf_mode[k] & 3, 2);
+        if (put_envelope(&w, s, 0, C0, dfe[0]) || put_noise(&w, s, 0, C0, dfq[0]) ||
+            put_bal_envelope(&w, s, 1, C1, dfe[1]) || put_bal_noise(&w, s, 1, C1, dfq[1]))
             return FAIL;
+        /* flags the reader now holds */
+        for (int l = 0; l < C0->L_E; l++) s->df_env[0][l] = dfe[0][l];
+        for (int l = 0; l < C0->L_Q; l++) s->df_noise[0][l] = dfq[0][l];
+        for (int l = 0; l < s->L_E_last[1] && l < C1->L_E; l++) s->df_env[1][l] = dfe[1][l];
+        for (int l = 0; l < s->L_Q_last[1] && l < C1->L_Q; l++) s->df_noise[1][l] = dfq[1][l];
+    } else {
+        for (int c = 0; c < nch; c++) choose_df(s, c, &rec->ch[c], rec->ch[c].L_E, rec->ch[c].L_Q, 0, dfe[c], dfq[c]);
+        if (nch == 1) {
+            sput(&w, 0, 1); /* bs_data_extra */
+        } else {
+            sput(&w, 1, 1); /* bs_data_extra: 8 reserved bits */
+            sput(&w, 0x5A, 8);
+            sput(&w, 0, 1); /* bs_coupling */
+        }
+        for (int c = 0; c < nch; c++)
+            if (put_grid(&w, &rec->ch[c])) return FAIL;
+        for (int c = 0; c < nch; c++) {
+            for (int l = 0; l < rec->ch[c].L_E; l++) sput(&w, (uint32_t)dfe[c][l], 1);
+            for (int l = 0; l < rec->ch[c].L_Q; l++) sput(&w, (uint32_t)dfq[c][l], 1);
+        }
+        for (int c = 0; c < nch; c++)
+            for (int k = 0; k < s->N_Q; k++) sput(&w, rec->ch[c].invf_mode[k] & 3, 2);
+        if (nch == 1) {
+            if (put_envelope(&w, s, 0, &rec->ch[0], dfe[0]) || put_noise(&w, s, 0, &rec->ch[0], dfq[0])) return FAIL;
+        } else {
+            if (put_envelope(&w, s, 0, &rec->ch[0], dfe[0]) || put_envelope(&w, s, 1, &rec->ch[1], dfe[1]) ||
+                put_noise(&w, s, 0, &rec->ch[0], dfq[0]) || put_noise(&w, s, 1, &rec->ch[1], dfq[1]))
+                return FAIL;
+        }
+        for (int c = 0; c < nch; c++) {
+            for (int l = 0; l < rec->ch[c].L_E; l++) s->df_env[c][l] = dfe[c][l];
+            for (int l = 0; l < rec->ch[c].L_Q; l++) s->df_noise[c][l] = dfq[c][l];
+        }
     }
     for (int c = 0; c < nch; c++) {
         const jaad_sbr_channel* C = &rec->ch[c];
@@ -411,9 +631,7 @@ long jaad_sbr_fil_bits(void* state, int nch, const jaad_sbr_frame* rec, uint8_t*
         sput(&w, 0, 1);
     }
     if (w.overflow) return FAIL;
-    /* FIL: count bytes (escape: count = 15 + esc - 1), payload padded to whole bytes */
-    const int count = (int)((w.pos + 7) / 8);
-    if (count > 15 + 255 - 1) return FAIL;
+    if ((w.pos + 7) / 8 > 15 + 255 - 1) return FAIL;
     /* state the next frame's delta coding starts from (sbr_save_prev_data) */
     for (int c = 0; c < nch; c++) {
         const jaad_sbr_channel* C = &rec->ch[c];
@@ -424,14 +642,8 @@ long jaad_sbr_fil_bits(void* state, int nch, const jaad_sbr_frame* rec, uint8_t*
         }
         s->have_prev[c] = 1;
         s->prev_gen[c] = s->tables_gen;
+        s->L_E_last[c] = C->L_E;
+        s->L_Q_last[c] = C->L_Q;
     }
-    sput(outw, 6, 3);
-    if (count >= 15) {
-        sput(outw, 15, 4);
-        sput(outw, (uint32_t)(count - 14), 8);
-    } else {
-        sput(outw, (uint32_t)count, 4);
-    }
-    for (int i = 0; i < count; i++) sput(outw, buf[i], 8);
-    return outw->overflow ? -1 : (long)outw->pos;
+    return emit_fil(outw, buf, w.pos);
 }

@@ -7,15 +7,16 @@ sys.path.insert(0, str(ROOT))
 from jaadec_amd import build as B  # noqa: E402
 
 VARIANTS = {
-    "p_scalar": (["JAAD_LC_SCALAR"], []),
-    "q_pk": ([], []),
+    "b_ldsx": (["JAAD_LC_LDSX"], []),
+    "c_regx": ([], []),
+    "s_stamps": (["JAAD_STAMPS"], []),
 }
 
 if __name__ == "__main__":
     out = ROOT / ".tmp" / "exp"
     out.mkdir(parents=True, exist_ok=True)
     for f in out.glob("lib_*.so"):
-        f.unlink()
+        if f.stem[4:] in VARIANTS: f.unlink()
     only = set(sys.argv[1:])
     from concurrent.futures import ThreadPoolExecutor
     todo = [(n, d) for n, d in VARIANTS.items() if not only or n in only]

@@ -30,9 +30,9 @@ for _ in range(3):
 torch.cuda.synchronize()
 S = dbg.cpu().numpy().view(np.uint32).reshape(nw, 16).astype(np.int64)
 S = S[S.sum(1) > 0]
-names = ["top: wait inputs, side info", "band records", "IQ (+prefetch issue)", "PNS/MS/IS", "store L, park R",
-         "c0 pre", "L synth (IMDCT+OLA)", "L PCM, unpark R, stage L", "R synth (IMDCT+OLA)", "R PCM",
-         "stage R + stores", "chunk tail", "IQ R (13->12)", "IQ L (14->13)", "rec reads (1->14)"]
+names = ["top: loop head, side info", "band records", "prefetch issue (+PNS)", "M/S, I/S", "spectra to LDS",
+         "-", "-", "-", "IMDCT + OLA (both channels)", "drain next frame's loads",
+         "PCM stage + stores", "chunk tail", "IQ R", "IQ L", "band record reads"]
 med = np.median(S, axis=0)
 tot = med[:15].sum()
 for k in range(15):

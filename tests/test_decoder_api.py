@@ -160,3 +160,59 @@ def test_truncated_frame_is_dropped_and_the_buffer_keeps_the_last_pcm():
     fmt = dec.getAudioFormat()
     assert (fmt.sample_rate, fmt.bits, fmt.channels, fmt.big_endian) == (48000, 16, 2, False)
     dec.close()
+
+
+def _asc(bits: str) -> bytes:
+    bits += "0" * (-len(bits) % 8)
+    return int(bits, 2).to_bytes(len(bits) // 8, "big")
+
+
+def test_sync_extension_signals_sbr_and_asc_keeps_the_core_rate():
+    """readSyncExtension (A/DecoderConfig.java:260-291): an AOT 2 config carrying 0x2B7 + AAC_SBR
+    + sbrPresent is explicit SBR at the signalled rate (0x548: psPresent).  Without it the config
+    keeps outputFrequency = the core rate (:180): implicit SBR found later runs downsampled for an
+    ASC-created decoder, doubled for an ADTS-created one (AudioDecoderInfo, setSBRPresent :124-135)."""
+    core = f"{2:05b}{6:04b}{2:04b}000"                     # LC, 24 kHz, stereo, GASpecificConfig
+    c = DecoderConfig.decode(_asc(core + f"{0x2B7:011b}{5:05b}1{3:04b}"))
+    assert (c.sbr, c.ext_sf_index, c.getSampleLength(), c.getOutputFrequency()) == (True, 3, 2048, 48000)
+    c = DecoderConfig.decode(_asc(f"{2:05b}{6:04b}{1:04b}000" + f"{0x2B7:011b}{5:05b}1{3:04b}{0x548:011b}1"))
+    assert (c.sbr, c.ps, c.channel_config, c.ext_sf_index) == (True, True, 1, 3)
+    c = DecoderConfig.decode(_asc(core + f"{0x2B7:011b}{5:05b}0"))  # sbrPresent = 0
+    assert (c.sbr, c.from_asc, c.getSampleLength()) == (False, True, 1024)
+    plain = DecoderConfig.decode(_asc(core))
+    assert not plain.sbr and plain.from_asc
+    up_asc = N.implicit_sbr_cfg(plain.cfg(), from_asc=True)
+    up_adts = N.implicit_sbr_cfg(plain.cfg())
+    assert (up_asc.ext_sf_index, up_adts.ext_sf_index) == (6, 3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("via", ["asc", "adts"])
+def test_implicit_sbr_rate_follows_the_creation_path(via):
+    """Main.decodeMP4 (S/Main.java:62, Decoder.create(DSI)) vs Main.decodeAAC (:84, ADTS header):
+    the same AOT 2 frames with SBR in FIL elements decode to 1024 core-rate samples through an
+    ASC-created decoder (SynthesisFilterbank32) and to 2048 doubled-rate samples through an
+    ADTS-created one, each equal to the restatement."""
+    from jaadec_amd.decoder import ADTSDemultiplexer
+    from oracle import oracle as O
+    p = N.synth_params(4, n_streams=1, frames_per_stream=10)
+    b = N.synth_batch(p)
+    frames = O.write_frames(b, p.sf_index, sbr_writer=O.SbrWriter(p.sf_index - 3, 5))
+    if via == "asc":
+        dec = Decoder.create(_asc(f"{2:05b}{p.sf_index:04b}{2:04b}000"))
+        cfg = N.make_cfg(p.sf_index, 2, sbr=True, down=True)
+        frames_in = frames
+    else:
+        demux = ADTSDemultiplexer(O.adts_wrap(frames, p.sf_index, 2))
+        dec = Decoder.create(demux.getDecoderInfo())
+        cfg = N.cfg_for(p)
+        frames_in = [demux.readNextFrame() for _ in range(10)]
+    want = O.decode_batch(cfg, b, O.Streams(1), N.PCM_BIG_ENDIAN)
+    for i in range(10):
+        buf = SampleBuffer()
+        dec.decodeFrame(frames_in[i], buf)
+        assert buf.getData() == want[i].tobytes(), i
+    c = dec.getConfig()
+    assert c.getSampleLength() == (1024 if via == "asc" else 2048)
+    assert buf.getSampleRate() == (24000 if via == "asc" else 48000)
+    dec.close()

@@ -222,3 +222,99 @@ def test_c4_full_batch_bitexact():
     assert p.n_streams * p.frames_per_stream == 32768
     got, want = _decode_both(p, N.synth_batch(p), N.PCM_BIG_ENDIAN)
     _assert_same(got, want, N.PCM_BIG_ENDIAN)
+
+
+def _recouple(s):
+    """Coupled frames: channel 1 carries channel 0's grid (Channel.couple, A/sbr/Channel.java:103-122)."""
+    for f in np.flatnonzero(s["coupling"]):
+        c0, c1 = s[f]["ch"][0], s[f]["ch"][1]
+        for k in ("frame_class", "L_E", "L_Q", "bs_pointer", "t_E", "t_Q", "f", "invf_mode"):
+            c1[k] = c0[k]
+        r = s[f]
+        r["ch"][1] = c1
+        s[f] = r
+
+
+@pytest.mark.parametrize("name,fn", [
+    ("plain", None),
+    ("amp_res0_var_grids", lambda s, rng: (s["hdr"].__setitem__("amp_res", 0), _var_grids(s, rng), _recouple(s))),
+    ("smoothing_limiter3", lambda s, rng: (s["hdr"].__setitem__("smoothing_mode", 0),
+                                           s["hdr"].__setitem__("limiter_bands", 3))),
+])
+def test_c4_coupled_stereo(name, fn):
+    """Coupled stereo SBR (bs_coupling, the usual coding of low-rate HE-AAC v1): both channels'
+    envelopes and noise floors come from channel 0's level and channel 1's balance
+    (NoiseEnvelope.unmap incl. its double-precision sqrt(2) step and the Q_div left / right tables,
+    A/sbr/NoiseEnvelope.java:192-240, 299-344), split over two calls."""
+    p = N.synth_params(4, n_streams=3, frames_per_stream=36, coupling_percent=60)
+    b = N.synth_batch(p)
+    if fn is not None:
+        rng = np.random.default_rng(3)
+        b = _edit(b, lambda s: fn(s, rng))
+    assert b.sbr["coupling"].sum() > 20
+    cfg = N.cfg_for(p)
+    want = O.decode_batch(cfg, b, O.Streams(3), N.PCM_FLOAT32, threads=8)
+    first, second = b.split_frames(15)
+    with N.Context(cfg, 3) as ctx:
+        g1 = ctx.decode(first, N.PCM_FLOAT32)
+        g2 = ctx.decode(second, N.PCM_FLOAT32)
+    fb = b.frame_begin
+    for r in range(3):
+        _assert_same(g1[15 * r:15 * (r + 1)], want[fb[r]:fb[r] + 15], N.PCM_FLOAT32)
+        _assert_same(g2[21 * r:21 * (r + 1)], want[fb[r] + 15:fb[r + 1]], N.PCM_FLOAT32)
+
+
+@pytest.mark.parametrize("cfgid,flags,down", [(4, N.PCM_BIG_ENDIAN, False), (4, N.PCM_FLOAT32, False),
+                                              (5, N.PCM_LITTLE_ENDIAN, False), (5, N.PCM_FLOAT32, False),
+                                              (4, N.PCM_FLOAT32, True)])
+def test_sbr_fallback_frames(cfgid, flags, down):
+    """Frames before the stream's first SBR header (QMF banks on the low band only,
+    Channel.process_channel with hdr == null, A/sbr/Channel.java:589-617) and frames without
+    usable SBR data (JAAD_SBR_UPSAMPLE: SBR.upsample of the core, A/sbr/SBR.java:302-309, the SBR
+    state untouched -- the next SBR frame continues from the last processed one), with calls that
+    cut through them: byte-exact against the restatement."""
+    p = N.synth_params(cfgid, n_streams=3, frames_per_stream=40, upsample_percent=20, nohdr_frames=5,
+                       coupling_percent=30 if cfgid == 4 else 0)
+    b = N.synth_batch(p)
+    st = b.sbr["status"].reshape(3, 40)
+    assert (st == N.SBR_UPSAMPLE).any(axis=1).all()
+    cfg = N.make_cfg(p.sf_index, p.channel_config, sbr=True, ps=p.sbr == 2, down=down)
+    want = O.decode_batch(cfg, b, O.Streams(3), flags, threads=8)
+    cuts = [0, 3, 7, 19, 20, 40]
+    rest = b
+    out = []
+    with N.Context(cfg, 3) as ctx:
+        for k in range(1, len(cuts)):
+            part, rest = rest.split_frames(cuts[k] - cuts[k - 1])
+            out.append(ctx.decode(part, flags))
+    fb = b.frame_begin
+    for k in range(1, len(cuts)):
+        n = cuts[k] - cuts[k - 1]
+        for r in range(3):
+            _assert_same(out[k - 1][n * r:n * (r + 1)], want[fb[r] + cuts[k - 1]:fb[r] + cuts[k]], flags)
+
+
+def test_upsample_only_call_and_state():
+    """A call whose every frame upsamples: no SBR stage runs and the slot's SBR state stays for the
+    next call's SBR frames."""
+    p = N.synth_params(4, n_streams=2, frames_per_stream=12)
+    b = N.synth_batch(p)
+    s = b.sbr.copy()
+    for r in range(2):
+        s[12 * r + 4:12 * r + 7]["status"] = N.SBR_UPSAMPLE
+        s[12 * r + 4:12 * r + 7]["header_present"] = 0
+    b = N.Batch(b.q, b.sf, b.cb, b.ics, b.ms_used, b.tns, b.stream_slot, b.frame_begin, b.nch, s)
+    cfg = N.cfg_for(p)
+    want = O.decode_batch(cfg, b, O.Streams(2), N.PCM_BIG_ENDIAN)
+    a, rest = b.split_frames(4)
+    mid, c = rest.split_frames(3)
+    with N.Context(cfg, 2) as ctx:
+        g = [ctx.decode(x, N.PCM_BIG_ENDIAN) for x in (a, mid, c)]
+    fb = b.frame_begin
+    for r in range(2):
+        assert np.array_equal(g[0][4 * r:4 * (r + 1)], want[fb[r]:fb[r] + 4])
+        assert np.array_equal(g[1][3 * r:3 * (r + 1)], want[fb[r] + 4:fb[r] + 7])
+        assert np.array_equal(g[2][5 * r:5 * (r + 1)], want[fb[r] + 7:fb[r + 1]])
+    # the upsampled frames repeat the core sample pairs (index 1 keeps core sample 1)
+    L = g[1].view(">i2").reshape(-1, 2048, 2)[..., 0].astype(np.int32)
+    assert np.array_equal(L[:, 2::2], L[:, 3::2])
