@@ -3,17 +3,27 @@
 
 One "step" = one pass of the hot path (jaad_decode_batch_device: IQ + M/S + IMDCT + window/OLA +
 PCM packing) over one 65 536-frame batch (256 streams x 256 frames, AAC-LC 48 kHz stereo, long
-windows) with inputs already resident in HBM.  Multi-GPU: one process per GPU, each rank decodes
-its own 65 536-frame shard of independent streams (weak scaling, no collectives on the data
-path; the only collectives are the barrier and the max-over-ranks timing reduction).
+windows) with inputs already resident in HBM.
+
+Multi-GPU: one process per GPU.  The job is ONE global batch of N x (per-GPU streams) independent
+streams; rank r decodes its shard_runs() slice of it (jaadec_amd/shard.py), generated on the rank
+itself (the synthetic generator seeds every stream by its global index, so a rank's slice equals
+the same streams of the whole batch).  Weak scaling, no collectives on the data path: the only
+collectives are the barrier around the timed region and the max-over-ranks time reduction.
 
     python bench.py [--gpus N --steps K --warmup W] [--config 2|3|4|5] [--no-cpu]
+
+`--gpus N` with N > 1 and no torch.distributed environment launches N ranks itself
+(torch.distributed.run, before this process touches the GPU) and exits with their status; under
+a launcher, WORLD_SIZE must equal --gpus.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -38,123 +48,225 @@ WORKLOADS = {
     5: "C5: HE-AAC v2, 24 kHz mono core + SBR + PS to 48 kHz stereo; 32768 frames per GPU (256 streams x 128), "
        "the 8-GPU job is the 262144-frame batch",
 }
-SHARD_OVERRIDES = {5: {"n_streams": 256}}  # C5 is quoted for 8 GPUs: each rank decodes 1/8 of it
+PER_GPU_STREAMS = {5: 256}  # C5 is quoted for 8 GPUs: each rank decodes 1/8 of the 2048-stream job
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", type=int, default=2, choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the host-buffer (PCIe-inclusive) leg")
     ap.add_argument("--cpu-streams", type=int, default=256, help="streams in the CPU baseline sample")
-    return ap.parse_args()
+    # diagnostics / CPU tests only: a smaller job than the config's (the line's config says so)
+    ap.add_argument("--streams-per-gpu", type=int, default=0)
+    ap.add_argument("--frames-per-stream", type=int, default=0)
+    return ap.parse_args(argv)
 
 
-def main():
-    args = parse()
-    import torch
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args, argv) -> int:
+    """Run this script as args.gpus ranks (one per GPU) and return their exit status.  The parent
+    never touches the GPU: it only starts the launcher as a child process."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", str(Path(__file__).resolve())] + list(argv)
+    return subprocess.run(cmd, env=dict(os.environ)).returncode
+
+
+def shard_params(N, config: int, world: int, rank: int, streams_per_gpu: int = 0, frames_per_stream: int = 0):
+    """Synthetic-generator parameters of rank `rank`'s slice of the global job (world x the per-GPU
+    stream count), the slice being shard_runs() of the global batch."""
+    from jaadec_amd.shard import shard_runs
+
+    over = {}
+    if frames_per_stream:
+        over["frames_per_stream"] = frames_per_stream
+    g = N.synth_params(config, **over)
+    per_gpu = streams_per_gpu or PER_GPU_STREAMS.get(config, g.n_streams)
+    n_global = per_gpu * world
+    fps = g.frames_per_stream
+    begin = np.arange(n_global + 1, dtype=np.uint64) * fps  # stream-major, one run per stream
+    runs = shard_runs(begin, world, rank)
+    p = N.synth_params(config, n_streams=len(runs), first_stream=runs.start if len(runs) else 0, **over)
+    return p, n_global
+
+
+class HipEngine:
+    """The product path on one GPU: the batch resident in HBM, jaad_decode_batch_device on a
+    non-default stream, HIP events around every timed step."""
+
+    def __init__(self, cfg, batch, flags: int, device: int, n_slots: int):
+        import torch
+
+        from jaadec_amd import native as N
+
+        self.torch, self.N = torch, N
+        self.dev = torch.device("cuda", device)
+        torch.cuda.set_device(self.dev)
+        self.batch, self.flags = batch, flags
+        self.pcm_bytes = batch.n_frames * N.pcm_frame_bytes(flags, bool(cfg.sbr), N.sbr_downsampled(cfg))
+
+        def to_dev(a):
+            if a is None:
+                return None
+            return torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1)).to(self.dev)
+
+        self.bufs = {k: to_dev(getattr(batch, k)) for k in ("q", "sf", "cb", "ics", "ms_used", "tns")}
+        self.ptr = {k: (v.data_ptr() if v is not None else None) for k, v in self.bufs.items()}
+        self.pcm_dev = torch.empty(self.pcm_bytes, dtype=torch.uint8, device=self.dev)
+        self.ctx = N.Context(cfg, n_slots, device=device)
+        # a real (non-null) stream: the kernels and the timing events must share it
+        self.stream = torch.cuda.Stream(self.dev)
+        torch.cuda.set_stream(self.stream)
+        self.ev = []
+
+    def step(self, timed: bool = False):
+        s = self.stream
+        if timed:
+            a, b = self.torch.cuda.Event(enable_timing=True), self.torch.cuda.Event(enable_timing=True)
+            a.record(s)
+        self.ctx.decode_device(self.ptr, self.batch, self.pcm_dev.data_ptr(), self.pcm_bytes, self.flags,
+                               s.cuda_stream)
+        if timed:
+            b.record(s)
+            self.ev.append((a, b))
+
+    def sync(self):
+        self.torch.cuda.synchronize(self.dev)
+
+    def kernel_ms(self) -> float:
+        return float(np.mean([a.elapsed_time(b) for a, b in self.ev])) if self.ev else float("nan")
+
+    def pcm(self) -> np.ndarray:
+        return self.pcm_dev.cpu().numpy().reshape(self.batch.n_frames, -1)
+
+    def decode_host(self) -> dict:
+        """The drop-in entry (host buffers in, host PCM out): frames/s with the caller's buffers
+        page-locked once (jaad_host_register, as a JNI caller pins its direct buffers) and with
+        plain pageable buffers (staged).  Best of 3 calls each."""
+        b = self.batch
+        out = np.empty((b.n_frames, self.pcm_bytes // max(b.n_frames, 1)), np.uint8)
+        arrays = [b.q, b.sf, b.cb, b.ics, b.ms_used, b.tns, out]
+
+        def best():
+            ts = []
+            for _ in range(3):
+                t1 = time.perf_counter()
+                self.ctx.decode(b, self.flags, out=out)
+                ts.append(time.perf_counter() - t1)
+            return b.n_frames / min(ts)
+
+        pageable = best()
+        self.ctx.register(*arrays)
+        try:
+            registered = best()
+        finally:
+            self.ctx.unregister(*arrays)
+        return {"registered": registered, "pageable": pageable}
+
+    def close(self):
+        self.ctx.close()
+
+
+def run(args, engine_cls=HipEngine, backend: str = "nccl"):
+    """One rank of the benchmark; returns the JSON line on rank 0 (None elsewhere) and this
+    rank's PCM after the timed steps."""
     import torch.distributed as dist
 
     from jaadec_amd import native as N
+    from jaadec_amd.shard import reduce_max_time
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local if world > 1 else 0)
-    torch.cuda.set_device(dev)
+    if world > 1 and not dist.is_initialized():
+        if backend == "nccl":
+            import torch
 
-    # ---- this rank's shard: its own 256 independent streams (seeded by rank)
-    p = N.synth_params(args.config, **SHARD_OVERRIDES.get(args.config, {}))
-    p.seed = p.seed + 0x1000 * rank
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
+
+    # ---- this rank's slice of the global job
+    p, n_global_streams = shard_params(N, args.config, world, rank, args.streams_per_gpu, args.frames_per_stream)
     batch = N.synth_batch(p)
     cfg = N.cfg_for(p)
     sbr = bool(p.sbr)
     n_frames = batch.n_frames
     flags = N.PCM_BIG_ENDIAN
-    pcm_bytes = n_frames * N.pcm_frame_bytes(flags, sbr)
-    ALGO_BYTES_PER_FRAME = ALGO_BYTES[args.config]
-
-    def to_dev(a):
-        if a is None:
-            return None
-        t = torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1)).to(dev)
-        return t
-
-    dq, dsf, dcb, dics, dms = (to_dev(batch.q), to_dev(batch.sf), to_dev(batch.cb), to_dev(batch.ics),
-                               to_dev(batch.ms_used))
-    dtns = to_dev(batch.tns)
-    dptr = {"q": dq.data_ptr(), "sf": dsf.data_ptr(), "cb": dcb.data_ptr(), "ics": dics.data_ptr(),
-            "ms_used": dms.data_ptr() if dms is not None else None, "tns": dtns.data_ptr() if dtns is not None else None}
-    pcm = torch.empty(pcm_bytes, dtype=torch.uint8, device=dev)
-    ctx = N.Context(cfg, int(batch.stream_slot.max()) + 1, device=dev.index)
-    # a real (non-null) stream: the kernels and the timing events must share it
-    stream = torch.cuda.Stream(dev)
-    torch.cuda.set_stream(stream)
-    sptr = stream.cuda_stream
+    eng = engine_cls(cfg, batch, flags, local, int(batch.stream_slot.max()) + 1 if n_frames else 1)
 
     # ---- parity sample: the first call decodes every stream from a fresh state
-    ctx.decode_device(dptr, batch, pcm.data_ptr(), pcm_bytes, flags, sptr)
-    torch.cuda.synchronize(dev)
+    eng.step()
+    eng.sync()
     parity = None
-    if rank == 0:
+    if rank == 0 and n_frames:
         from oracle import oracle as O
-        sub = batch.select_runs([0, len(batch.stream_slot) - 1])
-        want = O.decode_batch(cfg, sub, O.Streams(ctx.n_slots), flags, threads=2)
-        got_all = pcm.cpu().numpy().reshape(n_frames, -1)
+        sub = batch.select_runs(sorted({0, len(batch.stream_slot) - 1}))
+        want = O.decode_batch(cfg, sub, O.Streams(int(batch.stream_slot.max()) + 1), flags, threads=2)
+        got_all = eng.pcm()
         fb = batch.frame_begin
-        got = np.concatenate([got_all[fb[0]:fb[1]], got_all[fb[-2]:fb[-1]]])
+        runs = sorted({0, len(batch.stream_slot) - 1})
+        got = np.concatenate([got_all[fb[r]:fb[r + 1]] for r in runs])
         d = np.abs(got.view(">i2").astype(np.int32) - want.view(">i2").astype(np.int32))
         parity = {"frames_checked": int(want.shape[0]), "max_abs_lsb": int(d.max()),
                   "samples_off_by_1": int((d == 1).sum())}
 
     for _ in range(max(0, args.warmup - 1)):
-        ctx.decode_device(dptr, batch, pcm.data_ptr(), pcm_bytes, flags, sptr)
-    torch.cuda.synchronize(dev)
+        eng.step()
+    eng.sync()
 
     # ---- timed region: exactly K steps between barrier + synchronize
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize(dev)
+    eng.sync()
     t0 = time.perf_counter()
-    for k in range(args.steps):
-        ev[k][0].record(stream)
-        ctx.decode_device(dptr, batch, pcm.data_ptr(), pcm_bytes, flags, sptr)
-        ev[k][1].record(stream)
-    torch.cuda.synchronize(dev)
+    for _ in range(args.steps):
+        eng.step(timed=True)
+    eng.sync()
     if world > 1:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    elapsed = reduce_max_time(time.perf_counter() - t0)
+    kern_ms = eng.kernel_ms()
+    frames_all = n_frames
     if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
+        import torch
+
+        t = torch.tensor([n_frames], dtype=torch.int64)
+        if backend == "nccl":
+            t = t.to(eng.dev)
+        dist.all_reduce(t)
+        frames_all = int(t.item())
+    pcm = eng.pcm()
 
     # ---- PCIe-inclusive rate (host buffers in, host PCM out), reported beside, never as value
-    e2e_fps = None
-    if rank == 0:
-        t1 = time.perf_counter()
-        ctx.decode(batch, flags)
-        e2e_fps = n_frames / (time.perf_counter() - t1)
+    e2e = None
+    if rank == 0 and not args.no_e2e:
+        e2e = eng.decode_host()
 
     cpu = None
     if rank == 0 and not args.no_cpu:
         from oracle import oracle as O
         ns = min(args.cpu_streams if not sbr else min(args.cpu_streams, 16), len(batch.stream_slot))
         sub = batch.select_runs(range(ns))
+        nsl = int(batch.stream_slot.max()) + 1
         t1 = time.perf_counter()
-        O.decode_batch(cfg, sub, O.Streams(ctx.n_slots), flags, threads=1)
+        O.decode_batch(cfg, sub, O.Streams(nsl), flags, threads=1)
         dt1 = time.perf_counter() - t1
         ncores = os.cpu_count() or 1
         thr = min(ncores, 64)
         t1 = time.perf_counter()
-        O.decode_batch(cfg, sub, O.Streams(ctx.n_slots), flags, threads=thr)
+        O.decode_batch(cfg, sub, O.Streams(nsl), flags, threads=thr)
         dtn = time.perf_counter() - t1
         cpu = {"value": round(sub.n_frames / dt1, 1), "unit": "frames/s", "cores": 1, "kind": "port",
                "sample": f"{sub.n_frames} frames ({ns} streams x {p.frames_per_stream}) of the same workload, "
@@ -171,30 +283,51 @@ def main():
         traffic = prof.get("hbm_traffic_bytes_per_launch")
         traffic_src = f"profiles/{prof.get('tag')}.json ({prof.get('hbm_traffic_note')})" if traffic else None
 
+    line = None
     if rank == 0:
         steps = args.steps
-        total_frames = n_frames * world * steps
-        value = total_frames / elapsed
-        achieved = ALGO_BYTES_PER_FRAME * n_frames / (kern_ms * 1e-3) / 1e9
+        value = frames_all * steps / elapsed
+        achieved = ALGO_BYTES[args.config] * n_frames / (kern_ms * 1e-3) / 1e9
+        workload = WORKLOADS[args.config]
+        if args.streams_per_gpu or args.frames_per_stream:
+            workload += f" [reduced: {n_global_streams} streams x {p.frames_per_stream} frames]"
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "frames/s", "n_gpus": world, "steps": steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / steps * 1e3, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-            "config": {"workload": WORKLOADS[args.config], "frames_per_gpu": n_frames,
+            "config": {"workload": workload, "frames_per_gpu": n_frames, "frames_per_job": frames_all,
+                       "streams_per_job": n_global_streams,
                        "parallelism": f"stream-sharded x{world} (no collectives)", "pcm": "int16 big-endian",
                        "samples_per_frame": 2048 if sbr else 1024},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "traffic_source": traffic_src,
-                         "algorithmic_bytes_per_launch": ALGO_BYTES_PER_FRAME * n_frames,
+                         "algorithmic_bytes_per_launch": ALGO_BYTES[args.config] * n_frames,
                          "kernel_ms": round(kern_ms, 4)},
             "cpu_baseline": cpu,
             "parity_sample": parity,
-            "e2e_pcie_frames_per_s": round(e2e_fps, 1) if e2e_fps else None,
+            "e2e_pcie_frames_per_s": round(e2e["registered"], 1) if e2e else None,
+            "e2e_pcie_pageable_frames_per_s": round(e2e["pageable"], 1) if e2e else None,
         }
+    eng.close()
+    return line, pcm
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(args, argv))
+    if int(env_world or 1) != args.gpus:
+        print(f"bench.py: WORLD_SIZE={env_world} but --gpus {args.gpus}", file=sys.stderr)
+        sys.exit(2)
+    line, _ = run(args)
+    if line is not None:
         print(json.dumps(line), flush=True)
-    ctx.close()
-    if world > 1:
+    import torch.distributed as dist
+
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

@@ -259,9 +259,22 @@ void jaad_ctx_destroy(jaad_ctx* ctx);
 int jaad_ctx_core_channels(const jaad_ctx* ctx);
 
 /* Synchronous host-buffer entry: copies the batch to the device, runs the DSP, copies
- * n_frames * jaad_frame_pcm_bytes(flags) bytes of PCM back to pcm_out (frame-major).       */
+ * n_frames * jaad_frame_pcm_bytes(flags) bytes of PCM back to pcm_out (frame-major).
+ * Replaces the per-frame Decoder.decodeFrame(byte[], SampleBuffer) (A/Decoder.java:131-150)
+ * for a batch of already parsed frames.  The side info is range-checked first
+ * (JAAD_ERR_BITSTREAM, every slot's state left as before the call).  An AAC-LC batch of
+ * >= 8192 frames is cut into run-aligned pieces whose copies and kernels overlap; caller
+ * buffers registered with jaad_host_register are copied by DMA directly, others through
+ * page-locked staging.                                                                      */
 int jaad_decode_batch(jaad_ctx* ctx, const jaad_batch* batch, void* pcm_out, size_t pcm_bytes,
                       uint32_t flags);
+
+/* Page-lock [p, p + bytes) (hipHostRegister) for the context's host-buffer entry: batch arrays
+ * and PCM buffers that lie inside a registered range skip the staging copy.  Register buffers
+ * that are reused call after call (a JNI caller: its direct ByteBuffers, once per stream);
+ * unregister before freeing them.  jaad_ctx_destroy unregisters what is left.               */
+int jaad_host_register(jaad_ctx* ctx, void* p, size_t bytes);
+int jaad_host_unregister(jaad_ctx* ctx, void* p);
 
 /* Device-resident entry: all [dev] arrays and pcm_dev are device pointers; work is queued on
  * `hip_stream` (a hipStream_t, NULL = the context's stream) and the call returns without

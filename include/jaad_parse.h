@@ -70,6 +70,12 @@ typedef struct jaad_parser jaad_parser;
 
 int jaad_parser_create(const jaad_stream_cfg* cfg, jaad_parser** out);
 void jaad_parser_destroy(jaad_parser* p);
+/* Snapshot / rollback of a parser's whole state (window shapes, PNS LCG, SBR/PS history): a
+ * host that parses a batch ahead of its decode copies the state first and restores it when the
+ * decode is rejected, so the parser never runs ahead of the DSP state.  `dst` of copy must have
+ * been created for the same configuration. */
+int jaad_parser_clone(const jaad_parser* src, jaad_parser** out);
+int jaad_parser_copy(jaad_parser* dst, const jaad_parser* src);
 /* the static ICStream.randomState (PNS) the next ch-frame starts from; 0x1F2E3D4C initially */
 uint32_t jaad_parser_pns_state(const jaad_parser* p);
 void jaad_parser_set_pns_state(jaad_parser* p, uint32_t state);

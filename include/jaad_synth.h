@@ -39,6 +39,10 @@ typedef struct jaad_synth_params {
     uint8_t upsample_percent; /* SBR: % of frames without usable SBR data (JAAD_SBR_UPSAMPLE)   */
     uint8_t nohdr_frames;     /* SBR: leading frames of each stream before its first SBR header */
     uint8_t reserved;
+    uint32_t first_stream;    /* global index of the first stream generated: the streams
+                               * [first_stream, first_stream + n_streams) of a larger job (one
+                               * rank's shard); 0 with pns_percent > 0 (the PNS LCG runs over the
+                               * whole job in parse order) */
 } jaad_synth_params;
 
 /* defaults for a BASELINE.json config id (1..5: C1 mono 44.1k, C2, C3, C4 HE-AAC v1, C5 HE-AAC v2) */

@@ -10,6 +10,7 @@
 #include <vector>
 
 #include <algorithm>
+#include <atomic>
 #include <memory>
 #include <chrono>
 #include <condition_variable>
@@ -144,6 +145,12 @@ private:
     bool stop_ = false;
 };
 
+// jaad_decode_batch pipeline: a batch is cut into up to kMaxPieces run-aligned pieces whose
+// H2D copy, kernels and D2H copy overlap on three streams; pageable caller memory goes through
+// kStageSlots page-locked staging slots per direction.
+constexpr int kMaxPieces = 8, kStageSlots = 2;
+constexpr uint32_t kMinPieceFrames = 4096;
+
 // One call's SBR/PS parameter records: built on the host straight into page-locked staging,
 // copied on the context's copy stream while the previous call's kernels run.  Two sets
 // alternate between calls; `copied` guards the staging, `used` the device copy.
@@ -211,6 +218,13 @@ struct jaad_ctx {
     PsConst* d_ps_const = nullptr;
     DevBuf d_xps, d_xhl, d_xhr, d_pg, d_hb;
     std::vector<uint32_t> ps_runs;
+    // ---- host-buffer entry (jaad_decode_batch), set up on its first call ----
+    hipStream_t h2d = nullptr, d2h = nullptr;      // copy streams beside `stream`
+    hipEvent_t ev_in[kMaxPieces] = {}, ev_k[kMaxPieces] = {}, ev_out[kMaxPieces] = {};
+    PinnedBuf stage_in[kStageSlots], stage_out[kStageSlots];
+    std::unique_ptr<WorkerPool> io;                // validation / staging copies
+    std::vector<std::pair<uintptr_t, size_t>> pinned;  // jaad_host_register ranges
+    uint32_t plan_L = 0;                           // chunk length of the cached plan
 };
 
 namespace jaad {
@@ -321,25 +335,28 @@ int validate_cfg(const jaad_stream_cfg* cfg)
 // table is built in locals and committed (cache key, slot_used, device copy) only once it is
 // complete, so a rejected batch leaves the previous plan intact.  The upload is queued on the
 // call's stream (ordered after the previous call by launch()) from page-locked staging.
-int plan(jaad_ctx* ctx, const jaad_batch* b, hipStream_t stream)
+// `size_frames` (0: the batch's) is the frame count one launch covers: the host-buffer entry
+// launches the kernel once per piece of the batch, so its chunks are sized for a piece.
+int plan(jaad_ctx* ctx, const jaad_batch* b, hipStream_t stream, uint32_t size_frames = 0)
 {
     if (!b->stream_slot || !b->frame_begin) return JAAD_ERR_INVALID_ARG;
     if (b->frame_begin[0] != 0 || b->frame_begin[b->n_runs] != b->n_frames) return JAAD_ERR_INVALID_ARG;
-    bool same = ctx->plan_valid && ctx->plan_slots.size() == b->n_runs &&
-                std::memcmp(ctx->plan_slots.data(), b->stream_slot, b->n_runs * sizeof(uint32_t)) == 0 &&
-                std::memcmp(ctx->plan_begin.data(), b->frame_begin, (b->n_runs + 1) * sizeof(uint32_t)) == 0;
-    if (same) return JAAD_OK;
-    std::vector<ChunkDesc> chunks;
-    std::vector<uint8_t> used(ctx->n_slots, 0);
     // One wave decodes one chunk; a chunk that does not start its run re-decodes one frame.
     // Chunk length L is chosen so that the chunks fill the device's resident waves about once
     // (balanced, no tail round), but never shorter than kMinChunkFrames (prefix overhead).
     uint32_t L = ctx->chunk_frames;
     if (!L) {
         const uint64_t cap = ctx->lc_waves ? ctx->lc_waves : 4096;
-        L = (uint32_t)std::max<uint64_t>(kMinChunkFrames, (b->n_frames + cap - 1) / cap);
+        const uint64_t n = size_frames ? size_frames : b->n_frames;
+        L = (uint32_t)std::max<uint64_t>(kMinChunkFrames, (n + cap - 1) / cap);
     }
     L = std::min<uint32_t>(L, 0xffff);
+    bool same = ctx->plan_valid && ctx->plan_L == L && ctx->plan_slots.size() == b->n_runs &&
+                std::memcmp(ctx->plan_slots.data(), b->stream_slot, b->n_runs * sizeof(uint32_t)) == 0 &&
+                std::memcmp(ctx->plan_begin.data(), b->frame_begin, (b->n_runs + 1) * sizeof(uint32_t)) == 0;
+    if (same) return JAAD_OK;
+    std::vector<ChunkDesc> chunks;
+    std::vector<uint8_t> used(ctx->n_slots, 0);
     for (uint32_t r = 0; r < b->n_runs; r++) {
         uint32_t f0 = b->frame_begin[r], f1 = b->frame_begin[r + 1];
         uint32_t slot = b->stream_slot[r];
@@ -376,6 +393,7 @@ int plan(jaad_ctx* ctx, const jaad_batch* b, hipStream_t stream)
     ctx->slot_used.swap(used);
     ctx->plan_slots.assign(b->stream_slot, b->stream_slot + b->n_runs);
     ctx->plan_begin.assign(b->frame_begin, b->frame_begin + b->n_runs + 1);
+    ctx->plan_L = L;
     ctx->plan_valid = true;
     return JAAD_OK;
 }
@@ -527,7 +545,8 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
     const size_t o_runs = al(o_last + ctx->sbr_last.size() * sizeof(uint32_t));
     const size_t o_pslist = al(o_runs + ctx->ps_runs.size() * sizeof(uint32_t));
     const size_t o_fix = al(o_pslist + (ps ? nr * sizeof(uint32_t) : 0));
-    const size_t o_fmap = al(o_fix + ncf * sizeof(uint32_t));
+    const size_t o_chains = al(o_fix + ncf * sizeof(uint32_t));
+    const size_t o_fmap = al(o_chains + (size_t)b->n_runs * nch * 2 * sizeof(uint32_t));
     const size_t o_ups = al(o_fmap + (identity ? 0 : nr * sizeof(uint32_t)));
     const size_t n1 = al(o_ups + ups.size() * sizeof(uint32_t));
 
@@ -675,9 +694,14 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
     // HF fix passes: a kSbrDep channel-frame needs frame f-1's final carry rows, so it is
     // recomputed in pass d = its link count down a chain of such frames (with G/Q smoothing a
     // frame whose predecessor was recomputed is recomputed too: its ring came from that frame)
+    // Chains longer than kSbrFixPasses (bs_smoothing_mode 0 after a kSbrDep frame can run to the
+    // end of the run) are not walked one launch per link: their frames past that depth go to one
+    // sequential walker launch, a wave per (run, channel) stepping frame by frame.
     std::vector<uint32_t> fix_counts;
+    uint32_t n_chains = 0;
     if (any_dep) {
         uint32_t* fix_h = reinterpret_cast<uint32_t*>(h1 + o_fix);
+        uint32_t* chains_h = reinterpret_cast<uint32_t*>(h1 + o_chains);
         std::vector<uint32_t>& depth = ctx->sbr_depth;
         depth.assign(ncf, 0);
         uint32_t max_d = 0;
@@ -692,13 +716,30 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
                         max_d = std::max(max_d, dp + 1);
                     }
                 }
-        fix_counts.assign(max_d, 0);
+        const uint32_t np = std::min<uint32_t>(max_d, kSbrFixPasses);
+        fix_counts.assign(np, 0);
         for (size_t cf = 0; cf < ncf; cf++)
-            if (depth[cf]) fix_counts[depth[cf] - 1]++;
-        std::vector<uint32_t> pos(max_d + 1, 0);
-        for (uint32_t d = 0; d < max_d; d++) pos[d + 1] = pos[d] + fix_counts[d];
+            if (depth[cf] && depth[cf] <= np) fix_counts[depth[cf] - 1]++;
+        std::vector<uint32_t> pos(np + 1, 0);
+        for (uint32_t d = 0; d < np; d++) pos[d + 1] = pos[d] + fix_counts[d];
         for (size_t cf = 0; cf < ncf; cf++)
-            if (depth[cf]) fix_h[pos[depth[cf] - 1]++] = (uint32_t)cf;
+            if (depth[cf] && depth[cf] <= np) fix_h[pos[depth[cf] - 1]++] = (uint32_t)cf;
+        if (max_d > np) {  // the walker's lists follow the passes' (frame order per run and channel)
+            uint32_t at = pos[np];
+            for (uint32_t r = 0; r < b->n_runs; r++)
+                for (int c = 0; c < nch; c++) {
+                    const uint32_t o = at;
+                    for (uint32_t i = rbeg[r]; i < rbeg[r + 1]; i++) {
+                        const size_t cf = (size_t)i * nch + c;
+                        if (depth[cf] > np) fix_h[at++] = (uint32_t)cf;
+                    }
+                    if (at > o) {
+                        chains_h[2 * n_chains] = o - pos[np];
+                        chains_h[2 * n_chains + 1] = at - o;
+                        n_chains++;
+                    }
+                }
+        }
     }
     const auto t_packed = clk::now();
 
@@ -773,6 +814,8 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
         a.ps_list = reinterpret_cast<const uint32_t*>(d1 + o_pslist);
         a.n_runs = (uint32_t)(ctx->ps_runs.size() / 2);
     }
+    a.chains = reinterpret_cast<const uint32_t*>(d1 + o_chains);
+    a.n_chains = n_chains;
     HIPCHK(launch_sbr(a, stream, reinterpret_cast<const uint32_t*>(d1 + o_fix), fix_counts.data(),
                       (int)fix_counts.size()));
     HIPCHK(hipEventRecord(S.used, stream));
@@ -1038,6 +1081,18 @@ void jaad_ctx_destroy(jaad_ctx* ctx)
         if (r.used) (void)hipEventDestroy(r.used);
     }
     if (ctx->cstream) (void)hipStreamDestroy(ctx->cstream);
+    for (hipStream_t st : {ctx->h2d, ctx->d2h})
+        if (st) {
+            (void)hipStreamSynchronize(st);
+            (void)hipStreamDestroy(st);
+        }
+    for (int i = 0; i < kMaxPieces; i++)
+        for (hipEvent_t ev : {ctx->ev_in[i], ctx->ev_k[i], ctx->ev_out[i]})
+            if (ev) (void)hipEventDestroy(ev);
+    for (auto& st : ctx->stage_in) st.release();
+    for (auto& st : ctx->stage_out) st.release();
+    for (const auto& r : ctx->pinned) (void)hipHostUnregister(reinterpret_cast<void*>(r.first));
+    ctx->io.reset();
     ctx->d_chunks.release();
     ctx->h_chunks.release();
     if (ctx->done) (void)hipEventDestroy(ctx->done);
@@ -1059,37 +1114,99 @@ static int check_batch(const jaad_ctx* ctx, const jaad_batch* b, size_t pcm_byte
     return JAAD_OK;
 }
 
-// host-side range checks the Java parser would have raised as AACException
-static int validate_side_info(const jaad_ctx* ctx, const jaad_batch* b)
+// host-side range checks the Java parser would have raised as AACException, over ch-frames
+// [c0, c1) (ics/TNS records; |q| separately, fused with its copy)
+static bool side_info_ok(const jaad_ctx* ctx, const jaad_batch* b, size_t c0, size_t c1)
 {
-    const int nch = ctx->nch;
     const int nl = JAAD_SWB_LONG_WINDOW_COUNT[ctx->cfg.sf_index], ns = JAAD_SWB_SHORT_WINDOW_COUNT[ctx->cfg.sf_index];
-    for (size_t i = 0; i < (size_t)b->n_frames * nch; i++) {
+    for (size_t i = c0; i < c1; i++) {
         const jaad_ics_info& ic = b->ics[i];
-        if (ic.window_sequence > 3 || ic.window_shape > 1 || ic.window_shape_prev > 1) return JAAD_ERR_BITSTREAM;
-        int lim = ic.window_sequence == JAAD_EIGHT_SHORT_SEQUENCE ? ns : nl;
-        if (ic.max_sfb > lim) return JAAD_ERR_BITSTREAM;  // ICStream.java:137-138 / IndexOutOfBounds
-        const int16_t* q = b->q + i * 1024;
-        for (int k = 0; k < 1024; k++)
-            if (q[k] > 8190 || q[k] < -8190) return JAAD_ERR_BITSTREAM;  // IQ_TABLE has 8191 entries
+        if (ic.window_sequence > 3 || ic.window_shape > 1 || ic.window_shape_prev > 1) return false;
+        const int lim = ic.window_sequence == JAAD_EIGHT_SHORT_SEQUENCE ? ns : nl;
+        if (ic.max_sfb > lim) return false;  // ICStream.java:137-138 / IndexOutOfBounds
         if (b->tns && (ic.flags & JAAD_ICS_TNS)) {
             const jaad_tns& t = b->tns[i];
-            if (t.n_filters > 8) return JAAD_ERR_BITSTREAM;
+            if (t.n_filters > 8) return false;
             for (int f = 0; f < t.n_filters; f++)
-                if (t.filt[f].order > 20 || t.filt[f].window > 7) return JAAD_ERR_BITSTREAM;  // TNS.java:56-57
+                if (t.filt[f].order > 20 || t.filt[f].window > 7) return false;  // TNS.java:56-57
         }
     }
+    return true;
+}
+
+// |q| <= 8190 (IQ_TABLE has 8191 entries) over n values, copying them to dst on the way (dst may
+// be null: check only).  Branch-free inner loop: the compiler vectorises the max.
+static bool q_ok_copy(const int16_t* src, int16_t* dst, size_t n)
+{
+    constexpr size_t B = 4096;
+    for (size_t o = 0; o < n; o += B) {
+        const size_t m = std::min(B, n - o);
+        int bad = 0;
+        for (size_t k = 0; k < m; k++) bad |= (src[o + k] > 8190) | (src[o + k] < -8190);
+        if (bad) return false;
+        if (dst) std::memcpy(dst + o, src + o, m * sizeof(int16_t));
+    }
+    return true;
+}
+
+// is [p, p + n) inside a range registered with jaad_host_register?
+static bool is_pinned(const jaad_ctx* ctx, const void* p, size_t n)
+{
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    for (const auto& r : ctx->pinned)
+        if (a >= r.first && a + n <= r.first + r.second) return true;
+    return false;
+}
+
+static int io_setup(jaad_ctx* ctx)
+{
+    if (ctx->h2d) return JAAD_OK;
+    HIPCHK(hipStreamCreateWithFlags(&ctx->h2d, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&ctx->d2h, hipStreamNonBlocking));
+    for (int i = 0; i < kMaxPieces; i++) {
+        HIPCHK(hipEventCreateWithFlags(&ctx->ev_in[i], hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&ctx->ev_k[i], hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&ctx->ev_out[i], hipEventDisableTiming));
+    }
+    const unsigned hw = std::thread::hardware_concurrency();
+    ctx->io.reset(new (std::nothrow) WorkerPool((int)std::min(16u, hw ? hw : 1u)));
+    if (!ctx->io) return JAAD_ERR_NOMEM;
     return JAAD_OK;
 }
 
-int jaad_decode_batch(jaad_ctx* ctx, const jaad_batch* b, void* pcm_out, size_t pcm_bytes, uint32_t flags)
+// Pieces of the batch: run-aligned, balanced by frames (run r goes to the piece whose frame
+// interval holds its first frame), as many as kMaxPieces with >= kMinPieceFrames each.
+static std::vector<uint32_t> cut_pieces(const jaad_batch* b)
 {
-    int rc = check_batch(ctx, b, pcm_bytes, flags);
-    if (rc) return rc;
-    if (!pcm_out && b->n_frames) return JAAD_ERR_INVALID_ARG;
-    if ((rc = validate_side_info(ctx, b))) return rc;
-    HIPCHK(hipSetDevice(ctx->device));
+    const uint32_t nf = b->n_frames;
+    uint32_t P = std::min<uint32_t>(kMaxPieces, std::max<uint32_t>(1, nf / kMinPieceFrames));
+    P = std::max<uint32_t>(1, std::min<uint32_t>(P, b->n_runs));
+    std::vector<uint32_t> run0{0};  // first run of each piece, then n_runs
+    for (uint32_t r = 0; r < b->n_runs; r++) {
+        const uint32_t piece = (uint32_t)std::min<uint64_t>((uint64_t)b->frame_begin[r] * P / std::max(nf, 1u), P - 1);
+        while (run0.size() <= piece) run0.push_back(r);
+    }
+    while (run0.size() <= P) run0.push_back(b->n_runs);
+    run0.back() = b->n_runs;
+    // drop empty pieces
+    std::vector<uint32_t> out{0};
+    for (size_t i = 1; i < run0.size(); i++)
+        if (b->frame_begin[run0[i]] > b->frame_begin[out.back()] || i + 1 == run0.size()) out.push_back(run0[i]);
+    out.back() = b->n_runs;
+    return out;
+}
+
+// The whole SBR path and the fallback: validate, copy in, launch, copy out, one after the other.
+static int decode_batch_serial(jaad_ctx* ctx, const jaad_batch* b, void* pcm_out, uint32_t flags)
+{
     const size_t nf = b->n_frames, ncf = nf * ctx->nch;
+    std::atomic<bool> bad{false};
+    const int W = ctx->io->size();
+    ctx->io->run([&](int t) {
+        const size_t c0 = ncf * t / W, c1 = ncf * (t + 1) / W;
+        if (!side_info_ok(ctx, b, c0, c1) || !q_ok_copy(b->q + c0 * 1024, nullptr, (c1 - c0) * 1024)) bad = true;
+    });
+    if (bad) return JAAD_ERR_BITSTREAM;
     // one staging allocation, 256-B aligned sub-buffers
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     size_t o_q = 0, o_sf = al(o_q + ncf * 2048), o_cb = al(o_sf + ncf * 128), o_ics = al(o_cb + ncf * 128);
@@ -1115,9 +1232,209 @@ int jaad_decode_batch(jaad_ctx* ctx, const jaad_batch* b, void* pcm_out, size_t 
     db.ics = reinterpret_cast<const jaad_ics_info*>(base + o_ics);
     db.ms_used = b->ms_used ? reinterpret_cast<const uint64_t*>(base + o_ms) : nullptr;
     db.tns = b->tns ? reinterpret_cast<const jaad_tns*>(base + o_tns) : nullptr;
-    if ((rc = launch(ctx, &db, ctx->d_pcm.p, flags, s))) return rc;
+    int rc = launch(ctx, &db, ctx->d_pcm.p, flags, s);
+    if (rc) return rc;
     if (nf) HIPCHK(hipMemcpyAsync(pcm_out, ctx->d_pcm.p, pbytes, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
+    return JAAD_OK;
+}
+
+// AAC-LC: the pieces pipeline.  Every piece's kernels read the call's input state buffer and
+// write the output one (pieces touch disjoint slots), so the state flips once, at the end, and a
+// piece that fails validation leaves every slot's state as it was before the call.
+static int decode_batch_pieces(jaad_ctx* ctx, const jaad_batch* b, void* pcm_out, uint32_t flags,
+                               const std::vector<uint32_t>& run0)
+{
+    const int nch = ctx->nch;
+    const size_t nf = b->n_frames, ncf = nf * nch;
+    const int P = (int)run0.size() - 1;
+    const size_t fbytes = pcm_bytes_per_frame(ctx, flags);
+    // device image of the whole batch (the chunk table addresses frames batch-wide)
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const size_t o_q = 0, o_sf = al(o_q + ncf * 2048), o_cb = al(o_sf + ncf * 128), o_ics = al(o_cb + ncf * 128);
+    const size_t o_ms = al(o_ics + ncf * sizeof(jaad_ics_info)), o_tns = al(o_ms + nf * 16);
+    const size_t total = al(o_tns + (b->tns ? ncf * sizeof(jaad_tns) : 0));
+    HIPCHK(ctx->d_batch.ensure(total + 256));
+    HIPCHK(ctx->d_pcm.ensure(fbytes * nf + 256));
+    char* base = static_cast<char*>(ctx->d_batch.p);
+    char* dpcm = static_cast<char*>(ctx->d_pcm.p);
+    jaad_batch db = *b;
+    db.q = reinterpret_cast<const int16_t*>(base + o_q);
+    db.sf = reinterpret_cast<const uint8_t*>(base + o_sf);
+    db.cb = reinterpret_cast<const uint8_t*>(base + o_cb);
+    db.ics = reinterpret_cast<const jaad_ics_info*>(base + o_ics);
+    db.ms_used = b->ms_used ? reinterpret_cast<const uint64_t*>(base + o_ms) : nullptr;
+    db.tns = b->tns ? reinterpret_cast<const jaad_tns*>(base + o_tns) : nullptr;
+
+    // piece frame ranges and the largest piece (chunk sizing, staging)
+    std::vector<size_t> F(P + 1);
+    size_t maxf = 0;
+    for (int i = 0; i <= P; i++) F[i] = b->frame_begin[run0[i]];
+    for (int i = 0; i < P; i++) maxf = std::max(maxf, F[i + 1] - F[i]);
+    hipStream_t s = ctx->stream;
+    if (ctx->done_live && ctx->last_stream != s) HIPCHK(hipStreamWaitEvent(s, ctx->done, 0));
+    int rc = plan(ctx, &db, s, (uint32_t)maxf);
+    if (rc) return rc;
+    // chunk range of each piece (chunks are in run order, frames ascending)
+    std::vector<uint32_t> C(P + 1);
+    for (int i = 0; i <= P; i++) {
+        if (i == P) {
+            C[i] = (uint32_t)ctx->chunks.size();
+            break;
+        }
+        C[i] = (uint32_t)(std::lower_bound(ctx->chunks.begin(), ctx->chunks.end(), (uint32_t)F[i],
+                                           [](const ChunkDesc& c, uint32_t f) { return c.frame0 < f; }) -
+                          ctx->chunks.begin());
+    }
+    KernelArgs a{};
+    a.q = db.q;
+    a.sf = db.sf;
+    a.cb = db.cb;
+    a.ics = db.ics;
+    a.ms_used = db.ms_used;
+    a.tns = db.tns;
+    a.iq_table = ctx->d_iq;
+    a.tables = ctx->d_tables;
+    a.gtab = ctx->d_gtab;
+    a.state_in = ctx->d_state[ctx->parity];
+    a.state_out = ctx->d_state[ctx->parity ^ 1];
+    a.pcm = dpcm;
+    a.nch = (uint32_t)nch;
+    a.out_mode = flags;
+    a.tns_mode = ctx->cfg.tns_mode;
+    a.dbg = ctx->dbg;
+    a.dbg_frame = ctx->dbg_frame;
+    const bool tns_spec = ctx->cfg.tns_mode == JAAD_TNS_SPEC && db.tns != nullptr;
+    if ((rc = carry_untouched(ctx, a.state_out, a.state_in, 2048, s))) return rc;
+
+    // caller arrays: DMA straight from registered memory, else through the staging slots
+    const bool pin_q = is_pinned(ctx, b->q, ncf * 2048), pin_out = is_pinned(ctx, pcm_out, fbytes * nf);
+    const bool pin_rest = is_pinned(ctx, b->sf, ncf * 128) && is_pinned(ctx, b->cb, ncf * 128) &&
+                          is_pinned(ctx, b->ics, ncf * sizeof(jaad_ics_info)) &&
+                          (!b->ms_used || is_pinned(ctx, b->ms_used, nf * 16)) &&
+                          (!b->tns || is_pinned(ctx, b->tns, ncf * sizeof(jaad_tns)));
+    const size_t mc = maxf * nch;
+    const size_t s_q = 0, s_sf = al(s_q + (pin_q ? 0 : mc * 2048)), s_cb = al(s_sf + (pin_rest ? 0 : mc * 128));
+    const size_t s_ics = al(s_cb + (pin_rest ? 0 : mc * 128)), s_ms = al(s_ics + (pin_rest ? 0 : mc * sizeof(jaad_ics_info)));
+    const size_t s_tns = al(s_ms + (pin_rest || !b->ms_used ? 0 : maxf * 16));
+    const size_t s_total = al(s_tns + (pin_rest || !b->tns ? 0 : mc * sizeof(jaad_tns)));
+    if (s_total)
+        for (auto& st : ctx->stage_in) HIPCHK(st.ensure(s_total));
+    if (!pin_out)
+        for (auto& st : ctx->stage_out) HIPCHK(st.ensure(maxf * fbytes));
+
+    WorkerPool& io = *ctx->io;
+    const int W = io.size();
+    std::atomic<bool> bad{false};
+    int queued = 0;  // pieces whose copies/kernels are queued
+    auto copy_out = [&](int i) -> int {  // staging -> caller PCM of piece i
+        HIPCHK(hipEventSynchronize(ctx->ev_out[i]));
+        const char* src = static_cast<const char*>(ctx->stage_out[i % kStageSlots].p);
+        char* dst = static_cast<char*>(pcm_out) + F[i] * fbytes;
+        const size_t n = (F[i + 1] - F[i]) * fbytes;
+        io.run([&](int t) { std::memcpy(dst + n * t / W, src + n * t / W, n * (t + 1) / W - n * t / W); });
+        return JAAD_OK;
+    };
+    for (int i = 0; i < P && !bad; i++) {
+        const size_t f0 = F[i], nfi = F[i + 1] - f0, c0 = f0 * nch, nci = nfi * nch;
+        char* st = static_cast<char*>(ctx->stage_in[i % kStageSlots].p);
+        if (i >= kStageSlots && s_total) HIPCHK(hipEventSynchronize(ctx->ev_in[i - kStageSlots]));
+        // validate (and stage) the piece on the workers
+        io.run([&](int t) {
+            const size_t a0 = nci * t / W, a1 = nci * (t + 1) / W;
+            if (!side_info_ok(ctx, b, c0 + a0, c0 + a1) ||
+                !q_ok_copy(b->q + (c0 + a0) * 1024, pin_q ? nullptr : reinterpret_cast<int16_t*>(st + s_q) + a0 * 1024,
+                           (a1 - a0) * 1024))
+                bad = true;
+            if (!pin_rest) {
+                std::memcpy(st + s_sf + a0 * 128, b->sf + (c0 + a0) * 128, (a1 - a0) * 128);
+                std::memcpy(st + s_cb + a0 * 128, b->cb + (c0 + a0) * 128, (a1 - a0) * 128);
+                std::memcpy(st + s_ics + a0 * sizeof(jaad_ics_info), b->ics + c0 + a0, (a1 - a0) * sizeof(jaad_ics_info));
+                if (b->tns)
+                    std::memcpy(st + s_tns + a0 * sizeof(jaad_tns), b->tns + c0 + a0, (a1 - a0) * sizeof(jaad_tns));
+                if (b->ms_used && t == 0) std::memcpy(st + s_ms, b->ms_used + f0 * 2, nfi * 16);
+            }
+        });
+        if (bad) break;
+        hipStream_t h = ctx->h2d;
+        HIPCHK(hipMemcpyAsync(base + o_q + c0 * 2048, pin_q ? (const void*)(b->q + c0 * 1024) : st + s_q, nci * 2048,
+                              hipMemcpyHostToDevice, h));
+        const char* src_sf = pin_rest ? (const char*)(b->sf + c0 * 128) : st + s_sf;
+        const char* src_cb = pin_rest ? (const char*)(b->cb + c0 * 128) : st + s_cb;
+        const char* src_ics = pin_rest ? (const char*)(b->ics + c0) : st + s_ics;
+        HIPCHK(hipMemcpyAsync(base + o_sf + c0 * 128, src_sf, nci * 128, hipMemcpyHostToDevice, h));
+        HIPCHK(hipMemcpyAsync(base + o_cb + c0 * 128, src_cb, nci * 128, hipMemcpyHostToDevice, h));
+        HIPCHK(hipMemcpyAsync(base + o_ics + c0 * sizeof(jaad_ics_info), src_ics, nci * sizeof(jaad_ics_info),
+                              hipMemcpyHostToDevice, h));
+        if (b->ms_used)
+            HIPCHK(hipMemcpyAsync(base + o_ms + f0 * 16, pin_rest ? (const char*)(b->ms_used + f0 * 2) : st + s_ms, nfi * 16,
+                                  hipMemcpyHostToDevice, h));
+        if (b->tns)
+            HIPCHK(hipMemcpyAsync(base + o_tns + c0 * sizeof(jaad_tns), pin_rest ? (const char*)(b->tns + c0) : st + s_tns,
+                                  nci * sizeof(jaad_tns), hipMemcpyHostToDevice, h));
+        HIPCHK(hipEventRecord(ctx->ev_in[i], h));
+        HIPCHK(hipStreamWaitEvent(s, ctx->ev_in[i], 0));
+        a.chunks = static_cast<const ChunkDesc*>(ctx->d_chunks.p) + C[i];
+        a.n_chunks = C[i + 1] - C[i];
+        if (a.n_chunks) HIPCHK(launch_lc(a, s, tns_spec));
+        HIPCHK(hipEventRecord(ctx->ev_k[i], s));
+        HIPCHK(hipStreamWaitEvent(ctx->d2h, ctx->ev_k[i], 0));
+        void* dst = pin_out ? static_cast<char*>(pcm_out) + f0 * fbytes : ctx->stage_out[i % kStageSlots].p;
+        if (i >= kStageSlots && !pin_out && (rc = copy_out(i - kStageSlots))) return rc;
+        HIPCHK(hipMemcpyAsync(dst, dpcm + f0 * fbytes, nfi * fbytes, hipMemcpyDeviceToHost, ctx->d2h));
+        HIPCHK(hipEventRecord(ctx->ev_out[i], ctx->d2h));
+        queued = i + 1;
+    }
+    if (!pin_out)
+        for (int i = std::max(0, queued - kStageSlots); i < queued; i++)
+            if ((rc = copy_out(i))) return rc;
+    HIPCHK(hipStreamSynchronize(ctx->d2h));
+    HIPCHK(hipStreamSynchronize(s));
+    HIPCHK(hipEventRecord(ctx->done, s));
+    ctx->done_live = true;
+    ctx->last_stream = s;
+    if (bad) return JAAD_ERR_BITSTREAM;  // state not flipped: every slot as before the call
+    ctx->parity ^= 1;
+    return JAAD_OK;
+}
+
+int jaad_decode_batch(jaad_ctx* ctx, const jaad_batch* b, void* pcm_out, size_t pcm_bytes, uint32_t flags)
+{
+    int rc = check_batch(ctx, b, pcm_bytes, flags);
+    if (rc) return rc;
+    if (!pcm_out && b->n_frames) return JAAD_ERR_INVALID_ARG;
+    HIPCHK(hipSetDevice(ctx->device));
+    if ((rc = io_setup(ctx))) return rc;
+    if (ctx->cfg.sbr || b->n_frames < 2 * kMinPieceFrames || !b->stream_slot || !b->frame_begin)
+        return decode_batch_serial(ctx, b, pcm_out, flags);
+    // the run layout is checked by plan(); pieces need it sane before cutting
+    if (b->frame_begin[0] != 0 || b->frame_begin[b->n_runs] != b->n_frames) return JAAD_ERR_INVALID_ARG;
+    for (uint32_t r = 0; r < b->n_runs; r++)
+        if (b->frame_begin[r + 1] < b->frame_begin[r]) return JAAD_ERR_INVALID_ARG;
+    const std::vector<uint32_t> run0 = cut_pieces(b);
+    if (run0.size() <= 2) return decode_batch_serial(ctx, b, pcm_out, flags);
+    return decode_batch_pieces(ctx, b, pcm_out, flags, run0);
+}
+
+int jaad_host_register(jaad_ctx* ctx, void* p, size_t bytes)
+{
+    if (!ctx || !p || !bytes) return JAAD_ERR_INVALID_ARG;
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(hipHostRegister(p, bytes, hipHostRegisterDefault));
+    ctx->pinned.emplace_back(reinterpret_cast<uintptr_t>(p), bytes);
+    return JAAD_OK;
+}
+
+int jaad_host_unregister(jaad_ctx* ctx, void* p)
+{
+    if (!ctx || !p) return JAAD_ERR_INVALID_ARG;
+    auto it = std::find_if(ctx->pinned.begin(), ctx->pinned.end(),
+                           [&](const std::pair<uintptr_t, size_t>& r) { return r.first == reinterpret_cast<uintptr_t>(p); });
+    if (it == ctx->pinned.end()) return JAAD_ERR_INVALID_ARG;
+    HIPCHK(hipSetDevice(ctx->device));
+    if (ctx->done_live) HIPCHK(hipEventSynchronize(ctx->done));
+    ctx->pinned.erase(it);
+    HIPCHK(hipHostUnregister(p));
     return JAAD_OK;
 }
 

@@ -74,15 +74,10 @@ struct KernelArgs {
 };
 
 // IFFT output position (mod 64) that lane u holds after the register transposes of the long
-// IMDCT (jaad_lc.hip, imdct_long_pk): (u >> 3) + 8 * bitrev3(u & 7).  JAAD_LC_LDSX (the LDS
-// transpose variant kept for A/B timing) leaves the lanes in natural order.
+// IMDCT (jaad_lc.hip, imdct_long_pk): (u >> 3) + 8 * bitrev3(u & 7).
 inline int lane_pos_host(int u)
 {
-#ifdef JAAD_LC_LDSX
-    return u;
-#else
     return (u >> 3) | ((((u & 1) << 2) | (u & 2) | ((u >> 2) & 1)) << 3);
-#endif
 }
 // position (0..1023) of lane u's IMDCT output slot o = 2s+h (see jaad_lc.hip, long_pos)
 inline int long_pos_host(int u, int o)

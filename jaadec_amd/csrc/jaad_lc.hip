@@ -21,8 +21,7 @@
 // The 512-point complex IFFT of a frame is 8 complex values per lane in three register passes
 // (bit-reversed radix-4 + one radix-2 stage, then 3 + 3 radix-2 stages).  Between the passes
 // the lanes trade register bits for lane bits with v_permlane32_swap / v_permlane16_swap and
-// DPP moves (no LDS round trip; JAAD_LC_LDSX builds the earlier padded-LDS transposes for A/B
-// timing).  Butterflies, twiddles (the reference's float32 recurrence tables) and evaluation
+// DPP moves (no LDS round trip).  Butterflies, twiddles (the reference's float32 recurrence tables) and evaluation
 // order are those of the Java code and the file is compiled with -ffp-contract=off, so the
 // results are bit-exact.
 #include <hip/hip_runtime.h>
@@ -44,11 +43,7 @@ __device__ __forceinline__ int lane_id()
 // IFFT output position (mod 64) held by lane u after the register transposes (lane_pos_host)
 __device__ __forceinline__ int lane_pos(int u)
 {
-#ifdef JAAD_LC_LDSX
-    return u;
-#else
     return (u >> 3) | ((int)(__builtin_bitreverse32((uint32_t)u) >> 29) << 3);
-#endif
 }
 
 __device__ __forceinline__ void wave_sync()
@@ -334,43 +329,6 @@ __device__ __forceinline__ void imdct_long_pk(float* const (&bufs)[N], const Lds
             const f2 x = {bufs[n][eo_idx(1023 - 2 * k)], bufs[n][eo_idx(2 * k)]};
             c[n][s] = cmul(x, ld2(T.mdct_l[k]));
         }
-#ifdef JAAD_LC_LDSX
-    wave_sync();
-    const int t = (int)(__builtin_bitreverse32((uint32_t)u) >> 26);
-    const int x1 = xs_l(8 * t);
-#pragma unroll
-    for (int n = 0; n < N; n++) {
-        fft_pass1_pk(c[n], T.tw1);
-        f2* X = reinterpret_cast<f2*>(bufs[n]);
-#pragma unroll
-        for (int r = 0; r < 8; r++) X[x1 + r] = c[n][BR3[r]];
-    }
-    wave_sync();
-    const int a = u >> 3, b = u & 7;
-    const int x2 = xs_l(64 * a + b);
-#pragma unroll
-    for (int n = 0; n < N; n++) {
-        const f2* X = reinterpret_cast<const f2*>(bufs[n]);
-#pragma unroll
-        for (int s = 0; s < 8; s++) c[n][s] = X[x2 + xs_l(8 * s)];
-    }
-#pragma unroll
-    for (int n = 0; n < N; n++) {
-        fft_3stages_pk(c[n], [&](int j) { return ld2(T.tw2[j][b]); });
-        f2* X = reinterpret_cast<f2*>(bufs[n]);
-#pragma unroll
-        for (int s = 0; s < 8; s++) X[x2 + xs_l(8 * s)] = c[n][s];
-    }
-    wave_sync();
-    const int x3 = xs_l(u);
-#pragma unroll
-    for (int n = 0; n < N; n++) {
-        const f2* X = reinterpret_cast<const f2*>(bufs[n]);
-#pragma unroll
-        for (int s = 0; s < 8; s++) c[n][s] = X[x3 + xs_l(64 * s)];
-    }
-    wave_sync();
-#else
     // pass 1: register s holds e bits (s2, s1, s0) = e bits 0, 1, 2 (fft_pass1_pk's BR3 order)
 #pragma unroll
     for (int n = 0; n < N; n++) fft_pass1_pk(c[n], T.tw1);
@@ -390,7 +348,6 @@ __device__ __forceinline__ void imdct_long_pk(float* const (&bufs)[N], const Lds
         xch_bit<1, 1>(c[n], u);  // e bit 7 (lane bit 1) <-> e bit 4
         xch_bit<2, 0>(c[n], u);  // e bit 8 (lane bit 0) <-> e bit 5
     }
-#endif
     // pass 3: register bits 0,1,2 = e bits 6,7,8, e mod 64 = lane_pos(u)
 #pragma unroll
     for (int n = 0; n < N; n++) {

@@ -162,7 +162,7 @@ int parse_esds(Span esds, std::vector<uint8_t>& dsi)
     return e.bad ? JAAD_ERR_EOS : JAAD_OK;
 }
 
-int parse_trak(Span trak, std::vector<Track>& tracks)
+int parse_trak(Span trak, std::vector<Track>& tracks, size_t file_bytes)
 {
     std::vector<Box> tk, md, mi, st, sd;
     int rc;
@@ -249,6 +249,13 @@ int parse_trak(Span trak, std::vector<Track>& tracks)
         const uint64_t count = z.u(4);
         if (z.bad) return JAAD_ERR_EOS;
         if (count > (1u << 28)) return JAAD_ERR_BITSTREAM;
+        // every sample is bytes of this file: a count the file cannot hold is corrupt (and would
+        // size the tables below from a ~100-byte file)
+        if (stsz && fixed) {
+            if (count > file_bytes / fixed) return JAAD_ERR_BITSTREAM;
+        } else if (count > z.left() * (field == 4 ? 2 : 1)) {
+            return JAAD_ERR_EOS;
+        }
         sizes.resize((size_t)count);
         if (stsz && fixed) {
             std::fill(sizes.begin(), sizes.end(), fixed);
@@ -338,10 +345,23 @@ struct jaad_mp4 {
 
 extern "C" {
 
+static int mp4_open(const uint8_t* file, size_t bytes, jaad_mp4** out);
+
 int jaad_mp4_open(const uint8_t* file, size_t bytes, jaad_mp4** out)
 {
     if (!out || (!file && bytes)) return JAAD_ERR_INVALID_ARG;
     *out = nullptr;
+    try {  // no C++ exception may cross the C ABI (a JVM / Python host would abort)
+        return mp4_open(file, bytes, out);
+    } catch (const std::bad_alloc&) {
+        return JAAD_ERR_NOMEM;
+    } catch (...) {
+        return JAAD_ERR_BITSTREAM;
+    }
+}
+
+static int mp4_open(const uint8_t* file, size_t bytes, jaad_mp4** out)
+{
     std::vector<Box> top, moov;
     int rc = children(Span{file, bytes}, top, true);
     if (rc) return rc;
@@ -353,7 +373,7 @@ int jaad_mp4_open(const uint8_t* file, size_t bytes, jaad_mp4** out)
     if (!m) return JAAD_ERR_NOMEM;
     for (const Box& b : moov) {
         if (b.type != fourcc("trak")) continue;
-        if ((rc = parse_trak(b.body, m->tracks))) {
+        if ((rc = parse_trak(b.body, m->tracks, bytes))) {
             delete m;
             return rc;
         }

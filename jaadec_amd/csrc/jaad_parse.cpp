@@ -568,6 +568,21 @@ int jaad_parser_create(const jaad_stream_cfg* cfg, jaad_parser** out)
 
 void jaad_parser_destroy(jaad_parser* p) { delete p; }
 
+int jaad_parser_clone(const jaad_parser* src, jaad_parser** out)
+{
+    if (!src || !out) return JAAD_ERR_INVALID_ARG;
+    *out = new (std::nothrow) jaad_parser(*src);
+    return *out ? JAAD_OK : JAAD_ERR_NOMEM;
+}
+
+int jaad_parser_copy(jaad_parser* dst, const jaad_parser* src)
+{
+    if (!dst || !src) return JAAD_ERR_INVALID_ARG;
+    if (std::memcmp(&dst->C.cfg, &src->C.cfg, sizeof(jaad_stream_cfg)) != 0) return JAAD_ERR_INVALID_ARG;
+    *dst = *src;
+    return JAAD_OK;
+}
+
 uint32_t jaad_parser_pns_state(const jaad_parser* p) { return p ? p->st.pns : 0u; }
 void jaad_parser_set_pns_state(jaad_parser* p, uint32_t s)
 {

@@ -504,9 +504,6 @@ __global__ __launch_bounds__(256) void ps_decor_kernel(SbrArgs A)
     PsState& S = A.pss[A.recs[fl[0]].slot];
     const PsConst& K = Ks;
     const bool fresh = S.init == 0;
-#ifdef JAAD_DECOR_ONLY  // timing probe: one of the four recurrences alone (output invalid)
-    if (wave != JAAD_DECOR_ONLY) return;
-#endif
 
     if (wave == 0) {
         // ---- QMF bands (lane = sb): all-pass below 23, 14-slot delay to 34, 1-slot above ----
@@ -684,8 +681,8 @@ __global__ __launch_bounds__(256) void ps_mix_kernel(SbrArgs A)
     // (iid_mode, icc_mode, num_env, nr_ipdopd_par, border[6], reserved[2])
     const uint32_t* ph = reinterpret_cast<const uint32_t*>(A.psf + f);
     const uint32_t w0 = __builtin_amdgcn_readfirstlane(ph[0]);
-    const uint64_t bw = (uint64_t)__builtin_amdgcn_readfirstlane(ph[1]) |
-                        ((uint64_t)__builtin_amdgcn_readfirstlane(ph[2]) << 32);
+    const uint64_t bw = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(ph[1]) |
+                        ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(ph[2]) << 32);
     const int nr = (int)(w0 >> 24), num_env = (int)((w0 >> 16) & 255u);
     {
         const float4* src = reinterpret_cast<const float4*>(A.hb + (size_t)f * (5 * 22 * 16));

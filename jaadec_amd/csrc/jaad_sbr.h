@@ -148,6 +148,9 @@ struct SbrArgs {
     void* pcm;
     const uint32_t* fix;        // HF fix pass: the channel-frames it recomputes (kSbrDep chains)
     uint32_t n_fix;
+    const uint32_t* chains;     // HF chain walker: (offset, count) per chain into the walker's part of
+                                // `fix` (after the passes' lists), frames in order
+    uint32_t n_chains;
     const float* noise;         // NOISE_TABLE [512][2]
     const float* qmf_c;         // [640]
     const float* dct;           // dct4_64_tab [192] + w_re [16] + w_im [16]
@@ -176,7 +179,10 @@ struct SbrArgs {
     uint32_t n_runs;
 };
 
-// fix_dev: channel-frames of the HF fix passes, pass after pass (fix_counts[p] in pass p)
+// HF fix passes launched one per chain link at most; deeper links go to the chain walker
+constexpr uint32_t kSbrFixPasses = 8;
+// fix_dev: channel-frames of the HF fix passes, pass after pass (fix_counts[p] in pass p), then
+// the chain walker's lists (a.chains, relative to the end of the passes' lists)
 hipError_t launch_sbr(const SbrArgs& a, hipStream_t stream, const uint32_t* fix_dev = nullptr,
                       const uint32_t* fix_counts = nullptr, int n_fix_passes = 0);
 hipError_t launch_ps(const SbrArgs& a, hipStream_t stream);  // jaad_ps.hip, called by launch_sbr

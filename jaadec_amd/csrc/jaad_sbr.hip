@@ -239,6 +239,11 @@ __device__ __forceinline__ void dct4(const DctConst& K, int e, int E, float xr, 
 
 constexpr int kWavesPerBlock = 4;
 
+using gfloat = const __attribute__((address_space(1))) float;  // global memory (never flat)
+
+// s_waitcnt vmcnt(0) the compiler's wait insertion sees (see the synthesis kernel)
+__device__ __forceinline__ void vmem_drain() { __builtin_amdgcn_s_waitcnt(0x0F70); }  // vmcnt(0) expcnt(7) lgkmcnt(15)
+
 // batch frame / batch ch-frame of a record (frame) / record ch-frame (SbrArgs::fmap)
 __device__ __forceinline__ size_t batch_frame(const SbrArgs& A, size_t rf) { return A.fmap ? (size_t)A.fmap[rf] : rf; }
 __device__ __forceinline__ size_t batch_cf(const SbrArgs& A, size_t rcf)
@@ -330,9 +335,12 @@ __global__ __launch_bounds__(256) void sbr_analysis_kernel(SbrArgs A)
 // Channel.process_channel HF part: HFGeneration + HFAdjustment (A/sbr/Channel.java:596-604)
 // phase 0: full; phase 1: gains and G/Q ring only; phase 2: full, ring from frame f-1
 // ---------------------------------------------------------------------------------------------
+// phase 3: fix pass over the listed channel-frames; phase 4: chain walker, one wave per chain
+// stepping its frames in order (each one a phase-3 frame reading the frame before it)
 template <int kPhase>
 __global__ __launch_bounds__(256, 3) void sbr_hf_kernel(SbrArgs A)
 {
+    constexpr int P = kPhase == 4 ? 3 : kPhase;  // the body's phase
     __shared__ HfLds Ls[kWavesPerBlock];
     __shared__ float2 noise_s[512];  // NoiseTable.NOISE_TABLE (A/sbr/NoiseTable.java:6), read per slot
     for (int i = threadIdx.x; i < 512; i += blockDim.x)
@@ -340,12 +348,19 @@ __global__ __launch_bounds__(256, 3) void sbr_hf_kernel(SbrArgs A)
     __syncthreads();
     const int wave = threadIdx.x >> 6;
     uint32_t cf = blockIdx.x * kWavesPerBlock + wave;
+    uint32_t n_iter = 1, o = 0;
+    if constexpr (kPhase == 4) {
+        if (cf >= A.n_chains) return;
+        o = A.chains[2 * cf];
+        n_iter = A.chains[2 * cf + 1];
+    }
     if constexpr (kPhase == 3) {  // fix pass: the listed channel-frames only
         if (cf >= A.n_fix) return;
         cf = A.fix[cf];
     }
-    if (cf >= A.n_cf) return;
+    if (kPhase != 4 && cf >= A.n_cf) return;
     HfLds& L = Ls[wave];
+    auto frame = [&](const uint32_t cf) {
     const int u = lane_id();
     const int c = (int)(cf % (uint32_t)A.nch);
     // The record and its band tables are read field by field all through the kernel: byte loads
@@ -383,7 +398,7 @@ __global__ __launch_bounds__(256, 3) void sbr_hf_kernel(SbrArgs A)
     float xr[40], xi[40];
     {
         const float2* cur = reinterpret_cast<const float2*>(A.xlow + (size_t)cf * 2048);
-        const bool carry = R.first || kPhase == 3;
+        const bool carry = R.first || P == 3;
         const float2* prv = R.first ? reinterpret_cast<const float2*>(&A.state[(size_t)R.slot * 2 + c].xcarry[0][0][0])
                           : carry   ? reinterpret_cast<const float2*>(A.xcarry + (size_t)(cf - A.nch) * kSbrCarryFloats)
                                     : reinterpret_cast<const float2*>(A.xlow + (size_t)(cf - A.nch) * 2048) + 24 * 32;
@@ -428,7 +443,7 @@ __global__ __launch_bounds__(256, 3) void sbr_hf_kernel(SbrArgs A)
     }
     float gr[5] = {0, 0, 0, 0, 0}, qr[5] = {0, 0, 0, 0, 0};
     int gidx = R.gq0;
-    if ((kPhase == 2 || (kPhase == 3 && A.smoothing)) && !(R.flags & kSbrReset)) {
+    if ((P == 2 || (P == 3 && A.smoothing)) && !(R.flags & kSbrReset)) {
         const float* ring = R.first ? &A.state[(size_t)R.slot * 2 + c].gq[0][0][0] : A.gq + (size_t)(cf - A.nch) * 640;
         const int mm = u - kx >= 0 && u - kx < 64 ? u - kx : 0;
 #pragma unroll
@@ -445,7 +460,6 @@ __global__ __launch_bounds__(256, 3) void sbr_hf_kernel(SbrArgs A)
 
     // ---------- HF generation (A/sbr/HFGeneration.java:17-98, 100-196) ----------
     float a0r = 0, a0i = 0, a1r = 0, a1i = 0;
-#ifndef JAAD_HF_SKIP_GEN
     {
         float r01r = 0, r01i = 0, r02r = 0, r02i = 0, r11r = 0;
         float t1r, t1i, t2r = xr[0], t2i = xi[0], t3r = xr[1], t3i = xi[1];
@@ -517,17 +531,12 @@ __global__ __launch_bounds__(256, 3) void sbr_hf_kernel(SbrArgs A)
             if ((r & 7) == 7) __builtin_amdgcn_sched_barrier(0);
         }
     }
-#endif
 
     // ---------- HF adjustment (A/sbr/HFAdjustment.java) ----------
     const int m = u - kx;
     const bool band = m >= 0 && m < M;
     // estimate_current_envelope (:82-138)
-#ifdef JAAD_HF_SKIP_EST
-    if (false) {
-#else
     if (R.flags & kSbrInterpol) {
-#endif
         float acc[5] = {0, 0, 0, 0, 0};
 #pragma unroll
         for (int r = 2; r < 40; r++) {
@@ -586,7 +595,6 @@ __global__ __launch_bounds__(256, 3) void sbr_hf_kernel(SbrArgs A)
     }
     wave_sync();
 
-#ifndef JAAD_HF_SKIP_GAIN
     // calculate_gain (:240-415), per envelope, with every per-band step lane-parallel:
     //   (1) lane m: E_orig, E_curr, Q_M, S_M and the unlimited G;
     //   (2) lane kb (limiter band): acc1, acc2 as the Java's ordered sums over its bands -> G_max;
@@ -700,7 +708,6 @@ __global__ __launch_bounds__(256, 3) void sbr_hf_kernel(SbrArgs A)
             wave_sync();
         }
     }
-#endif
 
     // G/Q ring after this frame: the last 5 assembled rows (rows >= 26 always, see the host check)
     {
@@ -716,10 +723,9 @@ __global__ __launch_bounds__(256, 3) void sbr_hf_kernel(SbrArgs A)
             ring[320 + pos * 64 + u] = u < M ? L.ql[l][u] : 0.0f;
         }
     }
-    if (kPhase == 1) return;
+    if (P == 1) return;
 
     // hf_assembly (:140-238): lane k = m + kx
-#ifndef JAAD_HF_SKIP_ASM
     {
         const int mi = band ? m : 0;
         const bool smooth = (R.flags & kSbrSmooth) != 0;
@@ -831,7 +837,6 @@ __global__ __launch_bounds__(256, 3) void sbr_hf_kernel(SbrArgs A)
         }
         }
     }
-#endif
 
 
     // ---------- outputs ----------
@@ -853,6 +858,18 @@ __global__ __launch_bounds__(256, 3) void sbr_hf_kernel(SbrArgs A)
 #pragma unroll
         for (int j = 0; j < 8; j++) xc[j * 64 + u] = make_float2(xr[32 + j], xi[32 + j]);
     }
+    };
+    if constexpr (kPhase == 4) {
+        for (uint32_t it = 0; it < n_iter; it++) {
+            if (it) {
+                __threadfence();  // the previous frame's carry rows and G/Q ring, before this frame reads them
+                wave_sync();
+            }
+            frame(A.fix[o + it]);
+        }
+    } else {
+        frame(cf);
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -867,7 +884,7 @@ __global__ __launch_bounds__(256) void sbr_synthesis_kernel(SbrArgs A)
 {
     __shared__ float vring_s[kWavesPerBlock][10][128];
     __shared__ float xin_s[kWavesPerBlock][64];
-    const int wave = threadIdx.x >> 6;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t ci = blockIdx.x * kWavesPerBlock + wave;
     if (ci >= A.n_chunks) return;
     float(*vring)[128] = vring_s[wave];
@@ -904,28 +921,20 @@ __global__ __launch_bounds__(256) void sbr_synthesis_kernel(SbrArgs A)
     const int band_a = kDown ? e : (half ? 63 - 2 * e : 2 * e);
     const int band_b = kDown ? e : (half ? 2 * e : 63 - 2 * e);
     const int ia = kDown ? 2 * e : 2 * band_a + half, ib = kDown ? 2 * e + 1 : 2 * band_b + half;
-    auto fetch = [&](const float2* row, int klim, float& a, float& b) {
-        const float* r = reinterpret_cast<const float*>(row);
-        a = band_a < klim ? r[ia] : 0.0f;
-        b = band_b < klim ? r[ib] : 0.0f;
+    // Rows hold 64 bands in memory; bands >= klim read as zero.  The mask is applied where the
+    // slot consumes the values (a select next to the load would wait for it).
+    auto fetch = [&](const gfloat* r, float& a, float& b) {
+        a = r[ia];
+        b = r[ib];
     };
-
-    auto store_pcm = [&](float out, size_t n, bool dup) {
-        if (A.out_mode & JAAD_PCM_FLOAT32) {
-            float* o = reinterpret_cast<float*>(A.pcm) + 2 * n;
-            if ((nch == 2 || ps) && !dup) o[c] = out;
-            else o[0] = o[1] = out;
-        } else {
-            uint32_t s16 = (uint32_t)(uint16_t)(int16_t)java_round16(out);
-            if (!(A.out_mode & JAAD_PCM_LITTLE_ENDIAN)) s16 = ((s16 & 0xFF) << 8) | (s16 >> 8);
-            uint16_t* o = reinterpret_cast<uint16_t*>(A.pcm) + 2 * n;
-            if ((nch == 2 || ps) && !dup) o[c] = (uint16_t)s16;
-            else o[0] = o[1] = (uint16_t)s16;
-        }
+    auto mask = [&](int klim, float& a, float& b) {
+        a = band_a < klim ? a : 0.0f;
+        b = band_b < klim ? b : 0.0f;
     };
 
     // downsampled slot (:50-92): pre-twiddle, DCT-IV / DST-IV, v block of 64, 32 windowed outputs
-    auto slot32 = [&](float xr, float xi, bool emit, size_t n0, bool dup) {
+    // (lanes of half 0 return sample e of the slot in `res`)
+    auto slot32 = [&](float xr, float xi, bool emit, float& res) {
         float x1 = (xr * tw_c) - (xi * tw_s);
         float x2 = (xi * tw_c) + (xr * tw_s);
         x1 *= scale;
@@ -952,17 +961,16 @@ __global__ __launch_bounds__(256) void sbr_synthesis_kernel(SbrArgs A)
             const float* v7 = vring[(vpos + 3) % 10];
             const float* v8 = vring[(vpos + 2) % 10];
             const float* v9 = vring[(vpos + 1) % 10];
-            const float out = (v0[e] * cw[0]) + (v1[32 + e] * cw[1]) + (v2[e] * cw[2]) + (v3[32 + e] * cw[3]) +
-                              (v4[e] * cw[4]) + (v5[32 + e] * cw[5]) + (v6[e] * cw[6]) + (v7[32 + e] * cw[7]) +
-                              (v8[e] * cw[8]) + (v9[32 + e] * cw[9]);
-            store_pcm(out, n0 + e, dup);
+            res = (v0[e] * cw[0]) + (v1[32 + e] * cw[1]) + (v2[e] * cw[2]) + (v3[32 + e] * cw[3]) +
+                  (v4[e] * cw[4]) + (v5[32 + e] * cw[5]) + (v6[e] * cw[6]) + (v7[32 + e] * cw[7]) +
+                  (v8[e] * cw[8]) + (v9[32 + e] * cw[9]);
         }
         wave_sync();
         vpos = vpos == 9 ? 0 : vpos + 1;
     };
 
-    // one slot: DCT-IV pair -> v block (:99-129); emit: window (:134-146) + PCM
-    auto slot64 = [&](float a, float b, bool emit, size_t n0, bool dup) {
+    // one slot: DCT-IV pair -> v block (:99-129); emit: window (:134-146), sample u in `res`
+    auto slot64 = [&](float a, float b, bool emit, float& res) {
         const float in_r = scale * a;  // (fetch) d = 0: in_real1[e] / d = 1: in_real2[e]
         const float in_i = scale * b;  //            in_imag1[e] /        in_imag2[e]
         float orr, oi;
@@ -990,66 +998,181 @@ __global__ __launch_bounds__(256) void sbr_synthesis_kernel(SbrArgs A)
             const float* v7 = vring[(vpos + 3) % 10];
             const float* v8 = vring[(vpos + 2) % 10];
             const float* v9 = vring[(vpos + 1) % 10];
-            const float out = (v0[u] * cw[0]) + (v1[64 + u] * cw[1]) + (v2[u] * cw[2]) + (v3[64 + u] * cw[3]) +
-                              (v4[u] * cw[4]) + (v5[64 + u] * cw[5]) + (v6[u] * cw[6]) + (v7[64 + u] * cw[7]) +
-                              (v8[u] * cw[8]) + (v9[64 + u] * cw[9]);
-            store_pcm(out, n0 + u, dup);
+            res = (v0[u] * cw[0]) + (v1[64 + u] * cw[1]) + (v2[u] * cw[2]) + (v3[64 + u] * cw[3]) +
+                  (v4[u] * cw[4]) + (v5[64 + u] * cw[5]) + (v6[u] * cw[6]) + (v7[64 + u] * cw[7]) +
+                  (v8[u] * cw[8]) + (v9[64 + u] * cw[9]);
         }
         wave_sync();
         vpos = vpos == 9 ? 0 : vpos + 1;
     };
 
     const size_t spf = kDown ? 1024 : 2048, sps = kDown ? 32 : 64;  // output samples per frame / slot
-    auto slot = [&](float Xr, float Xi, bool emit, size_t n0, bool dup = false) {
-        if constexpr (kDown) slot32(Xr, Xi, emit, n0, dup);
-        else slot64(Xr, Xi, emit, n0, dup);
+    auto slot = [&](float Xr, float Xi, bool emit, float& res) {
+        if constexpr (kDown) slot32(Xr, Xi, emit, res);
+        else slot64(Xr, Xi, emit, res);
     };
 
-    // v history: slots 23..31 of the frame before the chunk
-    {
-        const size_t cf0 = (size_t)ck.frame0 * nch + rc;
-        const SbrRec& R0 = A.recs[cf0];
-        // PS right channel (qmfs1): history of the previous frame that carried PS data
-        const uint32_t back = (ps && c == 1) ? R0.ps_back : (R0.first ? 0u : 1u);
-        const float* prev = ps ? A.xps + ((size_t)(ck.frame0 - back) * 2 + c) * 4096 : A.xsyn + (cf0 - nch) * 4096;
-        const float2* xp = back == 0 ? reinterpret_cast<const float2*>(&A.state[(size_t)R0.slot * 2 + c].xsyn[0][0][0])
-                                     : reinterpret_cast<const float2*>(prev) + 23 * 64;
-        for (int l = 0; l < 9; l++) {
-            float a, b;
-            fetch(xp + l * 64, 64, a, b);
-            slot(a, b, false, 0);
-        }
-    }
-    for (int j = 0; j < (int)ck.n; j++) {
-        const uint32_t f = ck.frame0 + j;
-        const size_t cf = (size_t)f * nch + rc;
-        const SbrRec& R = A.recs[cf];
+    // The chunk's slots (9 history slots, then 32 per frame) run as a software pipeline of 4-slot
+    // groups: the rows of group g+1 are loaded while group g computes, and group g's PCM is
+    // stored after an explicit vmcnt(0) (vmem_drain): vmcnt counts loads and stores in issue order,
+    // so a store issued before the next group's loads would otherwise make every row load wait for
+    // the previous slot's PCM to reach memory (one global round trip per slot).
+    // Where the rows of one frame of the sequence come from.  All fields are wave-uniform.
+    struct Src {
+        const gfloat* xs;  // rows l >= t0 (64 bands, 128 floats a row)
+        const gfloat* xc;  // rows l < t0: the carried Xsbr rows 2..7, kprev bands
+        int t0, kprev, rows;
+        size_t n0;         // first output sample (emitting frames)
+        bool emit, dup;
+    };
+    auto uni = [](uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane(x); };  // (int -> uint32, no sign extension)
+    auto uptr = [&](const float* p) {
+        const uint64_t v = reinterpret_cast<uint64_t>(p);
+        return (const gfloat*)(((uint64_t)uni((uint32_t)(v >> 32)) << 32) | uni((uint32_t)v));
+    };
+    // the record fields the synthesis needs (dwords 0..3 and the slot), loaded one frame ahead
+    struct RecW { uint32_t w0, w1, w2, w3, slot; };
+    static_assert(offsetof(SbrRec, flags) == 2 && offsetof(SbrRec, kx_prev) == 6 && offsetof(SbrRec, M_prev) == 7 &&
+                      offsetof(SbrRec, first) == 11 && offsetof(SbrRec, t_E) == 12 && offsetof(SbrRec, slot) == 64,
+                  "SbrRec field offsets used by the synthesis");
+    auto rec_load = [&](int j, RecW& W) {
+        if (j >= (int)ck.n) return;
+        const uint32_t* r = reinterpret_cast<const uint32_t*>(A.recs + (size_t)(ck.frame0 + j) * nch + rc);
+        W.w0 = r[0];
+        W.w1 = r[1];
+        W.w2 = r[2];
+        W.w3 = r[3];
+        W.slot = r[16];
+    };
+    // frame j >= 0 of the chunk from its record fields
+    auto frame_src = [&](int j, const RecW& W) {
+        Src S{};
+        const uint32_t f = ck.frame0 + (uint32_t)j;
+        const uint32_t cf = f * nch + rc;
+        const uint32_t flags = uni(W.w0 >> 16) & 0xFF, first = uni(W.w2 >> 24) & 0xFF;
+        S.rows = 32;
+        S.emit = true;
+        S.n0 = batch_frame(A, f) * spf;
         if (ps) {
             // a frame without PS data: SBR1.process synthesises X with qmfs0 and copies the left
             // channel to the right one (A/sbr/SBR1.java:75-81); qmfs1 does not run
-            const bool ps_on = (R.flags & kSbrPsOn) != 0;
-            if (c == 1 && !ps_on) continue;
-            const float2* xq = reinterpret_cast<const float2*>(A.xps + ((size_t)f * 2 + c) * 4096);
-            for (int l = 0; l < 32; l++) {
-                float a, b;
-                fetch(xq + l * 64, 64, a, b);
-                slot(a, b, true, batch_frame(A, f) * spf + sps * l, !ps_on);
-            }
-            continue;
+            const bool ps_on = (flags & kSbrPsOn) != 0;
+            if (c == 1 && !ps_on) S.rows = 0;
+            S.dup = !ps_on;
+            S.xs = uptr(A.xps + ((size_t)f * 2 + c) * 4096);
+            return S;
         }
-        const float2* xs = reinterpret_cast<const float2*>(A.xsyn + cf * 4096);
+        S.xs = uptr(A.xsyn + (size_t)cf * 4096);
         // rows l < t_E[0]: Xsbr rows 2..7 carried from frame f-1 (its carry rows 2..7 = rows
         // 34..39), kx_prev + M_prev bands
-        const int t0 = R.t_E[0];
-        const float2* xc = R.first ? reinterpret_cast<const float2*>(&A.state[(size_t)R.slot * 2 + c].xcarry[0][0][0])
-                                   : reinterpret_cast<const float2*>(A.xcarry + (cf - nch) * kSbrCarryFloats);
-        const int kprev = R.kx_prev + R.M_prev;
-        for (int l = 0; l < 32; l++) {
-            float a, b;
-            if (l < t0) fetch(xc + (l + 2) * 64, kprev, a, b);
-            else fetch(xs + l * 64, 64, a, b);
-            slot(a, b, true, batch_frame(A, f) * spf + sps * l);
+        S.t0 = (int)(uni(W.w3) & 0xFF);
+        S.xc = first ? uptr(&A.state[(size_t)uni(W.slot) * 2 + c].xcarry[0][0][0])
+                     : uptr(A.xcarry + (size_t)(cf - nch) * kSbrCarryFloats);
+        S.kprev = (int)((uni(W.w1) >> 16) & 0xFF) + (int)(uni(W.w1) >> 24);
+        return S;
+    };
+    // frame -1: the v history (slots 23..31 of the frame before the chunk)
+    auto history_src = [&]() {
+        Src S{};
+        const uint32_t cf0 = uni(ck.frame0 * nch + rc);
+        const SbrRec& R0 = A.recs[cf0];
+        // PS right channel (qmfs1): history of the previous frame that carried PS data
+        const uint32_t back = uni((ps && c == 1) ? R0.ps_back : (R0.first ? 0u : 1u));
+        if (back == 0) S.xs = uptr(&A.state[(size_t)uni(R0.slot) * 2 + c].xsyn[0][0][0]);
+        else if (ps) S.xs = uptr(A.xps + ((size_t)(ck.frame0 - back) * 2 + c) * 4096) + 23 * 128;
+        else S.xs = uptr(A.xsyn + (size_t)(cf0 - nch) * 4096) + 23 * 128;
+        S.rows = 9;
+        return S;
+    };
+    auto load_group = [&](const Src& S, int l0, float (&ga)[4], float (&gb)[4], int (&kl)[4]) {
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int l = min(l0 + i, S.rows - 1);  // (rows past the frame's last are not used)
+            const bool carry = l < S.t0;
+            kl[i] = carry ? S.kprev : 64;
+            fetch(carry ? S.xc + (l + 2) * 128 : S.xs + l * 128, ga[i], gb[i]);
         }
+    };
+    const bool f32 = (A.out_mode & JAAD_PCM_FLOAT32) != 0;
+    const bool swap = !(A.out_mode & JAAD_PCM_LITTLE_ENDIAN);
+    auto store_group = [&](const Src& S, int l0, const float (&res)[4]) {
+        if (!S.emit || (kDown && half)) return;
+        const int k = kDown ? e : u;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int l = l0 + i;
+            if (l >= S.rows) break;
+            const size_t n = S.n0 + sps * l + k;
+            const bool one = (nch == 2 || ps) && !S.dup;  // this channel's half of the word
+            if (f32) {
+                float* o = reinterpret_cast<float*>(A.pcm) + 2 * n;
+                if (one) o[c] = res[i];
+                else *reinterpret_cast<float2*>(o) = make_float2(res[i], res[i]);
+            } else {
+                uint32_t s16 = (uint32_t)(uint16_t)(int16_t)java_round16(res[i]);
+                if (swap) s16 = ((s16 & 0xFF) << 8) | (s16 >> 8);
+                if (one) reinterpret_cast<uint16_t*>(A.pcm)[2 * n + c] = (uint16_t)s16;
+                else reinterpret_cast<uint32_t*>(A.pcm)[n] = s16 | (s16 << 16);
+            }
+        }
+    };
+
+    Src S = history_src();
+    RecW W{};                    // record fields of frame j + 1
+    rec_load(0, W);
+    float ga[4] = {0, 0, 0, 0}, gb[4] = {0, 0, 0, 0};
+    int kl[4] = {64, 64, 64, 64};
+    load_group(S, 0, ga, gb, kl);
+    vmem_drain();
+    bool have = true;            // ga/gb hold the rows of the group about to run
+    for (int j = -1;;) {
+        for (int l0 = 0; l0 < S.rows; l0 += 4) {
+            if (!have) {         // first group after a frame without rows
+                load_group(S, l0, ga, gb, kl);
+                vmem_drain();
+            }
+            have = false;
+            float na[4] = {0, 0, 0, 0}, nb[4] = {0, 0, 0, 0};
+            int nk[4] = {64, 64, 64, 64};
+            // the next group: later rows of this frame or the first rows of the next one (only
+            // scalar selects branch; the loads themselves are unconditional, a reload of the
+            // current rows when there is nothing to fetch)
+            Src Sn = S;
+            int ln = l0 + 4;
+            if (ln >= S.rows) {
+                have = false;
+                if (j + 1 < (int)ck.n) {
+                    const Src F = frame_src(j + 1, W);
+                    if (F.rows) {
+                        Sn = F;
+                        ln = 0;
+                        have = true;
+                    }
+                }
+                if (!have) ln = l0;
+            } else {
+                have = true;
+            }
+            load_group(Sn, ln, na, nb, nk);
+            float res[4] = {0, 0, 0, 0};
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                if (l0 + i >= S.rows) break;
+                mask(kl[i], ga[i], gb[i]);
+                slot(ga[i], gb[i], S.emit, res[i]);
+            }
+            vmem_drain();
+            store_group(S, l0, res);
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                ga[i] = na[i];
+                gb[i] = nb[i];
+                kl[i] = nk[i];
+            }
+        }
+        if (++j >= (int)ck.n) break;
+        S = frame_src(j, W);
+        rec_load(j + 1, W);
     }
 }
 
@@ -1147,6 +1270,9 @@ hipError_t launch_sbr(const SbrArgs& a, hipStream_t stream, const uint32_t* fix_
                                    stream, fa);
             fa.fix += fix_counts[p];
         }
+        if (a.n_chains)  // links past kSbrFixPasses: fa.fix now points at the walker's lists
+            hipLaunchKernelGGL(sbr_hf_kernel<4>, dim3((a.n_chains + kWavesPerBlock - 1) / kWavesPerBlock), blk, 0,
+                               stream, fa);
     }
     if (a.ps) {
         const hipError_t e = launch_ps(a, stream);

@@ -47,7 +47,7 @@ void gen_stream(const Gen& G, uint32_t s)
 {
     const jaad_synth_params& P = *G.p;
     const int nch = P.channel_config == 2 ? 2 : 1;
-    SplitMix64 r{P.seed ^ (0xA5A5A5A5ull + (uint64_t)s * 0x9E3779B97F4A7C15ull)};
+    SplitMix64 r{P.seed ^ (0xA5A5A5A5ull + (uint64_t)(P.first_stream + s) * 0x9E3779B97F4A7C15ull)};
     for (int i = 0; i < 4; i++) r.next();
     const short* offL = JAAD_SWB_OFFSET_LONG_WINDOW[P.sf_index];
     const short* offS = JAAD_SWB_OFFSET_SHORT_WINDOW[P.sf_index];
@@ -192,7 +192,7 @@ void gen_stream(const Gen& G, uint32_t s)
 void gen_sbr_stream(const jaad_synth_params& P, jaad_sbr_frame* out, uint32_t s)
 {
     const int nch = P.channel_config == 2 ? 2 : 1;
-    SplitMix64 r{P.seed ^ (0x5B5B5B5Bull + (uint64_t)s * 0xD1B54A32D192ED03ull)};
+    SplitMix64 r{P.seed ^ (0x5B5B5B5Bull + (uint64_t)(P.first_stream + s) * 0xD1B54A32D192ED03ull)};
     for (int i = 0; i < 4; i++) r.next();
     int lvl[2][64], qv[2][5], iid[34], icc[34];
     for (int b = 0; b < 34; b++) {
@@ -376,6 +376,7 @@ int jaad_synth_generate(const jaad_synth_params* p, int16_t* q, uint8_t* sf, uin
     if (!p || !q || !sf || !cb || !ics || !stream_slot || !frame_begin) return JAAD_ERR_INVALID_ARG;
     if (p->sf_index > 11 || (p->channel_config != 1 && p->channel_config != 2)) return JAAD_ERR_INVALID_ARG;
     if (p->channel_config == 2 && !ms_used) return JAAD_ERR_INVALID_ARG;
+    if (p->first_stream && p->pns_percent) return JAAD_ERR_INVALID_ARG;
     Gen G{p, q, sf, cb, ics, ms_used, tns};
     const uint32_t ns = p->n_streams;
     if (threads <= 0) threads = (int)std::thread::hardware_concurrency();

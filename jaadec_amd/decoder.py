@@ -27,6 +27,8 @@ from . import native as N
 LOGGER = logging.getLogger("jaad.aac.Decoder")
 
 
+_FRESH = object()  # decodeFrames: the batch created the stream's parser
+
 class AACException(RuntimeError):
     """A/AACException.java"""
 
@@ -208,9 +210,18 @@ class Decoder:
     def decodeFrames(self, batch, buffers: list[SampleBuffer]) -> None:  # noqa: N802
         """Decode consecutive frames of this stream -- a list of raw_data_blocks or a parsed
         ``native.Batch`` -- buffer i receives frame i's PCM."""
+        snap = None
         if isinstance(batch, (list, tuple)):
-            batch = self._parse(list(batch))
+            # the parser commits frame by frame: roll it back if this batch is not decoded, so
+            # it never runs ahead of the DSP state (a failed parse restores nothing else)
+            snap = self._parser.snapshot() if self._parser is not None else _FRESH
+            try:
+                batch = self._parse(list(batch))
+            except AACException:
+                self._rollback(snap)
+                raise
         if len(buffers) != batch.n_frames:
+            self._rollback(snap)
             raise AACException("one SampleBuffer per frame expected")
         b = N.Batch(batch.q, batch.sf, batch.cb, batch.ics, batch.ms_used, batch.tns,
                     np.array([self.slot], np.uint32), np.array([0, batch.n_frames], np.uint32), batch.nch,
@@ -219,7 +230,10 @@ class Decoder:
         try:
             pcm = self._ctx.decode(b, flags)
         except N.JaadError as e:
+            self._rollback(snap)
             raise AACException(str(e)) from e
+        if snap is not None and snap is not _FRESH:
+            snap.close()
         rate = self.config.getOutputFrequency()
         for i, buf in enumerate(buffers):
             want = buf.big_endian
@@ -227,6 +241,17 @@ class Decoder:
             buf.big_endian = flags == N.PCM_BIG_ENDIAN
             buf.setBigEndian(want)  # no-op unless this buffer asked for the other byte order
         self.frames += batch.n_frames
+
+    def _rollback(self, snap) -> None:
+        if snap is None:  # a pre-parsed batch: no parser state was touched
+            return
+        if snap is _FRESH:  # the parser was created by this batch: start over at the next one
+            if self._parser is not None:
+                self._parser.close()
+                self._parser = None
+            return
+        self._parser.restore(snap)
+        snap.close()
 
     def decode0(self, frame, buffer: SampleBuffer) -> None:
         """A/Decoder.java:103-121: one frame; an EOSException propagates."""

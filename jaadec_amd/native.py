@@ -73,15 +73,17 @@ class SynthParams(C.Structure):
                 ("ms_mode", C.c_uint8), ("global_gain", C.c_uint8), ("escape_permille", C.c_uint8),
                 ("common_window", C.c_uint8), ("sbr", C.c_uint8), ("sbr_level", C.c_uint8),
                 ("pns_state0", C.c_uint32), ("coupling_percent", C.c_uint8), ("upsample_percent", C.c_uint8),
-                ("nohdr_frames", C.c_uint8), ("reserved", C.c_uint8)]
+                ("nohdr_frames", C.c_uint8), ("reserved", C.c_uint8), ("first_stream", C.c_uint32)]
 
 
 # every symbol include/jaad_gpu.h declares (checked by tests/test_abi.py)
 EXPORTS = ["jaad_cfg_sample_length", "jaad_cfg_channel_count", "jaad_frame_pcm_bytes", "jaad_ctx_create",
            "jaad_ctx_destroy", "jaad_ctx_core_channels", "jaad_decode_batch", "jaad_decode_batch_device", "jaad_wait", "jaad_state_bytes",
-           "jaad_state_export", "jaad_state_import", "jaad_state_reset", "jaad_strerror", "jaad_last_error"]
+           "jaad_state_export", "jaad_state_import", "jaad_state_reset", "jaad_strerror", "jaad_last_error",
+           "jaad_host_register", "jaad_host_unregister"]
 # every symbol include/jaad_parse.h declares
 PARSE_EXPORTS = ["jaad_asc_parse", "jaad_adts_find", "jaad_adts_cfg", "jaad_parser_create", "jaad_parser_destroy",
+                 "jaad_parser_clone", "jaad_parser_copy",
                  "jaad_parser_pns_state", "jaad_parser_set_pns_state", "jaad_parse_frame", "jaad_probe_sbr"]
 
 
@@ -127,6 +129,8 @@ def lib() -> C.CDLL:
         L.jaad_decode_batch_device.argtypes = [C.c_void_p, C.POINTER(BatchStruct), C.c_void_p, C.c_size_t,
                                                C.c_uint32, C.c_void_p]
         L.jaad_wait.argtypes = [C.c_void_p]
+        L.jaad_host_register.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
+        L.jaad_host_unregister.argtypes = [C.c_void_p, C.c_void_p]
         L.jaad_state_bytes.argtypes = [C.c_void_p]
         L.jaad_state_bytes.restype = C.c_size_t
         L.jaad_state_export.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_size_t]
@@ -137,10 +141,12 @@ def lib() -> C.CDLL:
         L.jaad_last_error.argtypes = [C.c_void_p]
         L.jaad_last_error.restype = C.c_char_p
         L.jaad_asc_parse.argtypes = [C.c_char_p, C.c_size_t, C.POINTER(StreamCfg)]
-        L.jaad_adts_find.argtypes = [C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t), C.POINTER(AdtsHeader)]
+        L.jaad_adts_find.argtypes = [C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t), C.POINTER(AdtsHeader)]
         L.jaad_adts_cfg.argtypes = [C.POINTER(AdtsHeader), C.POINTER(StreamCfg)]
         L.jaad_parser_create.argtypes = [C.POINTER(StreamCfg), C.POINTER(C.c_void_p)]
         L.jaad_parser_destroy.argtypes = [C.c_void_p]
+        L.jaad_parser_clone.argtypes = [C.c_void_p, C.POINTER(C.c_void_p)]
+        L.jaad_parser_copy.argtypes = [C.c_void_p, C.c_void_p]
         L.jaad_parser_destroy.restype = None
         L.jaad_parser_pns_state.argtypes = [C.c_void_p]
         L.jaad_parser_pns_state.restype = C.c_uint32
@@ -332,13 +338,31 @@ class Context:
             detail = lib().jaad_last_error(self.h).decode()
             raise JaadError(rc, f"{what} {detail}".strip())
 
-    def decode(self, batch: Batch, flags: int = PCM_BIG_ENDIAN) -> np.ndarray:
-        """Host-buffer batch decode -> PCM bytes (uint8 [n_frames, frame_bytes])."""
+    def decode(self, batch: Batch, flags: int = PCM_BIG_ENDIAN, out: np.ndarray | None = None) -> np.ndarray:
+        """Host-buffer batch decode -> PCM bytes (uint8 [n_frames, frame_bytes]), into `out` when
+        given (e.g. a buffer registered with register())."""
         nb = pcm_frame_bytes(flags, bool(self.cfg.sbr), sbr_downsampled(self.cfg))
-        out = np.empty((batch.n_frames, nb), np.uint8)
+        if out is None:
+            out = np.empty((batch.n_frames, nb), np.uint8)
+        assert out.flags["C_CONTIGUOUS"] and out.nbytes >= batch.n_frames * nb
         bs = batch.struct()
         self._check(lib().jaad_decode_batch(self.h, C.byref(bs), _ptr(out), out.nbytes, flags), "jaad_decode_batch")
         return out
+
+    def wait(self) -> None:
+        """Wait for every call queued on the context (jaad_wait)."""
+        self._check(lib().jaad_wait(self.h), "jaad_wait")
+
+    def register(self, *arrays: np.ndarray) -> None:
+        """Page-lock host arrays reused across decode() calls (jaad_host_register)."""
+        for a in arrays:
+            if a is not None and a.nbytes:
+                self._check(lib().jaad_host_register(self.h, _ptr(a), a.nbytes), "jaad_host_register")
+
+    def unregister(self, *arrays: np.ndarray) -> None:
+        for a in arrays:
+            if a is not None and a.nbytes:
+                self._check(lib().jaad_host_unregister(self.h, _ptr(a)), "jaad_host_unregister")
 
     def decode_device(self, dev: dict, batch: Batch, pcm_dev_ptr: int, pcm_bytes: int, flags: int = 0,
                       stream_ptr: int | None = None) -> None:
@@ -380,8 +404,10 @@ def adts_frames(data: bytes):
     pos = 0
     h = AdtsHeader()
     off = C.c_size_t()
+    data = bytes(data)
+    base = C.cast(C.c_char_p(data), C.c_void_p).value  # one buffer, searched at an offset (no copies)
     while pos < len(data):
-        rc = lib().jaad_adts_find(data[pos:], len(data) - pos, C.byref(off), C.byref(h))
+        rc = lib().jaad_adts_find(C.c_void_p(base + pos), len(data) - pos, C.byref(off), C.byref(h))
         if rc == ERR_EOS:
             return
         if rc:
@@ -441,6 +467,22 @@ class Parser:
             self.h = None
 
     __del__ = close
+
+    def snapshot(self) -> "Parser":
+        """A copy of the whole parser state (jaad_parser_clone)."""
+        h = C.c_void_p()
+        rc = lib().jaad_parser_clone(self.h, C.byref(h))
+        if rc:
+            raise JaadError(rc, "jaad_parser_clone")
+        s = Parser.__new__(Parser)
+        s.cfg, s.nch, s.h = self.cfg, self.nch, h
+        return s
+
+    def restore(self, snap: "Parser") -> None:
+        """Roll the state back to a snapshot (jaad_parser_copy)."""
+        rc = lib().jaad_parser_copy(self.h, snap.h)
+        if rc:
+            raise JaadError(rc, "jaad_parser_copy")
 
     @property
     def pns_state(self) -> int:

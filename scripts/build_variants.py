@@ -7,8 +7,7 @@ sys.path.insert(0, str(ROOT))
 from jaadec_amd import build as B  # noqa: E402
 
 VARIANTS = {
-    "b_ldsx": (["JAAD_LC_LDSX"], []),
-    "c_regx": ([], []),
+    "c_head": ([], []),
     "s_stamps": (["JAAD_STAMPS"], []),
 }
 

@@ -162,6 +162,30 @@ def test_truncated_frame_is_dropped_and_the_buffer_keeps_the_last_pcm():
     dec.close()
 
 
+@pytest.mark.gpu
+def test_rejected_batch_rolls_the_parser_back():
+    """decodeFrames parses the whole list before the DSP runs: when the batch is then rejected,
+    the parser state (PNS LCG, window shapes) is rolled back, so the frames decode afterwards
+    exactly as if the failed call had never happened."""
+    from oracle import oracle as O
+    p = N.synth_params(3, n_streams=1, frames_per_stream=8, pns_percent=10)
+    b = N.synth_batch(p)
+    frames = O.write_frames(b, p.sf_index)
+    want = O.decode_batch(N.make_cfg(), b, O.Streams(1), N.PCM_BIG_ENDIAN)
+    dec = Decoder.create(bytes([0x11, 0x90]))
+    dec._parse([])
+    dec._parser.pns_state = int(b.ics["pns_state"][0])
+    bufs = [SampleBuffer() for _ in range(3)]
+    dec.decodeFrames(frames[:3], bufs)
+    with pytest.raises(AACException):
+        dec.decodeFrames(frames[3:6], bufs[:2])  # parsed, then rejected (buffer count)
+    bufs = [SampleBuffer() for _ in range(5)]
+    dec.decodeFrames(frames[3:], bufs)
+    for i, buf in enumerate(bufs):
+        assert buf.getData() == want[3 + i].tobytes(), i
+    dec.close()
+
+
 def _asc(bits: str) -> bytes:
     bits += "0" * (-len(bits) % 8)
     return int(bits, 2).to_bytes(len(bits) // 8, "big")
@@ -197,7 +221,10 @@ def test_implicit_sbr_rate_follows_the_creation_path(via):
     from oracle import oracle as O
     p = N.synth_params(4, n_streams=1, frames_per_stream=10)
     b = N.synth_batch(p)
-    frames = O.write_frames(b, p.sf_index, sbr_writer=O.SbrWriter(p.sf_index - 3, 5))
+    # the SBR frequency tables follow the SBR output rate (SBR.sample_rate = outputFrequency,
+    # A/sbr/SBR.java:102): the core rate through the ASC, twice it through ADTS
+    out_sf = p.sf_index if via == "asc" else p.sf_index - 3
+    frames = O.write_frames(b, p.sf_index, sbr_writer=O.SbrWriter(out_sf, 5))
     if via == "asc":
         dec = Decoder.create(_asc(f"{2:05b}{p.sf_index:04b}{2:04b}000"))
         cfg = N.make_cfg(p.sf_index, 2, sbr=True, down=True)

@@ -1,0 +1,110 @@
+"""The host-buffer entry (jaad_decode_batch): the pieces pipeline for large AAC-LC batches, with
+pageable and registered (jaad_host_register) caller buffers, against the device-resident entry
+and the C restatement; validation failures leave every slot's state untouched."""
+import numpy as np
+import pytest
+import torch
+
+from jaadec_amd import native as N
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _device_decode(cfg, b, n_slots, flags):
+    dev = torch.device("cuda", 0)
+    t = lambda a: None if a is None else torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1)).to(dev)
+    d = {k: t(getattr(b, k)) for k in ("q", "sf", "cb", "ics", "ms_used", "tns")}
+    ptr = {k: (v.data_ptr() if v is not None else None) for k, v in d.items()}
+    nb = N.pcm_frame_bytes(flags)
+    pcm = torch.empty(b.n_frames * nb, dtype=torch.uint8, device=dev)
+    with N.Context(cfg, n_slots) as ctx:
+        ctx.decode_device(ptr, b, pcm.data_ptr(), pcm.numel(), flags)
+        ctx.wait()
+    return pcm.cpu().numpy().reshape(b.n_frames, nb)
+
+
+def _ragged(b, lens):
+    """Runs of the given lengths (prefixes of b's runs)."""
+    fb = b.frame_begin
+    frames = np.concatenate([np.arange(fb[r], fb[r] + L) for r, L in enumerate(lens)])
+    cfr = (frames[:, None] * b.nch + np.arange(b.nch)).reshape(-1)
+    begin = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint32)
+    return N.Batch(b.q[cfr].copy(), b.sf[cfr].copy(), b.cb[cfr].copy(), b.ics[cfr].copy(),
+                   None if b.ms_used is None else b.ms_used[frames].copy(),
+                   None if b.tns is None else b.tns[cfr].copy(), b.stream_slot[:len(lens)].copy(), begin, b.nch)
+
+
+@pytest.mark.parametrize("flags", [N.PCM_BIG_ENDIAN, N.PCM_FLOAT32])
+def test_pieces_pipeline_matches_device_entry_and_oracle(flags):
+    p = N.synth_params(3, n_streams=24, frames_per_stream=700)  # 16 800 frames: 4 pieces
+    b = N.synth_batch(p)
+    cfg = N.make_cfg()
+    with N.Context(cfg, 24) as ctx:
+        got = ctx.decode(b, flags)
+    want_dev = _device_decode(cfg, b, 24, flags)
+    assert (got == want_dev).all()
+    sub = b.select_runs([0, 11, 23])
+    want = O.decode_batch(cfg, sub, O.Streams(24), flags, threads=8)
+    fb = b.frame_begin
+    g = np.concatenate([got[fb[r]:fb[r + 1]] for r in (0, 11, 23)])
+    assert (g == want).all()
+
+
+def test_registered_buffers_and_continuation():
+    p = N.synth_params(2, n_streams=12, frames_per_stream=1400)
+    b = N.synth_batch(p)
+    cfg = N.make_cfg()
+    first, second = b.split_frames(900)  # 10 800 frames, then 6 000 frames: both piecewise
+    want = np.concatenate(
+        [_device_decode(cfg, b, 12, N.PCM_BIG_ENDIAN)[b.frame_begin[r]:b.frame_begin[r + 1]] for r in range(12)])
+    with N.Context(cfg, 12) as ctx:
+        out1 = np.empty((first.n_frames, 4096), np.uint8)
+        out2 = np.empty((second.n_frames, 4096), np.uint8)
+        arrays = [first.q, first.sf, first.cb, first.ics, first.ms_used, out1]
+        ctx.register(*arrays)
+        g1 = ctx.decode(first, out=out1)
+        g2 = ctx.decode(second, out=out2)  # pageable
+        ctx.unregister(*arrays)
+    got = np.empty_like(want)
+    i1 = i2 = 0
+    for r in range(12):
+        got[r * 1400:r * 1400 + 900] = g1[i1:i1 + 900]
+        got[r * 1400 + 900:(r + 1) * 1400] = g2[i2:i2 + 500]
+        i1 += 900
+        i2 += 500
+    assert (got == want).all()
+
+
+def test_ragged_runs_and_few_runs():
+    p = N.synth_params(2, n_streams=3, frames_per_stream=9000)
+    b = N.synth_batch(p)
+    cfg = N.make_cfg()
+    rag = _ragged(b, [9000, 17, 5000])  # 3 runs, pieces of unequal size
+    with N.Context(cfg, 3) as ctx:
+        got = ctx.decode(rag, N.PCM_FLOAT32)
+    assert (got == _device_decode(cfg, rag, 3, N.PCM_FLOAT32)).all()
+
+
+def test_bad_piece_leaves_state_untouched():
+    p = N.synth_params(2, n_streams=16, frames_per_stream=1024)
+    b = N.synth_batch(p)
+    cfg = N.make_cfg()
+    with N.Context(cfg, 16) as ctx:
+        half, rest = b.split_frames(512)
+        ctx.decode(half)
+        before = [ctx.state_export(s) for s in range(16)]
+        bad = rest.select_runs(range(16))
+        bad.q[-1, 5] = 9000  # |q| > 8190 in the last piece
+        with pytest.raises(N.JaadError) as e:
+            ctx.decode(bad)
+        assert e.value.status == N.ERR_BITSTREAM
+        assert all((ctx.state_export(s) == before[s]).all() for s in range(16))
+        # the good batch still continues every stream exactly
+        g2 = ctx.decode(rest)
+    want = _device_decode(cfg, b, 16, N.PCM_BIG_ENDIAN)
+    fb = b.frame_begin
+    i = 0
+    for r in range(16):
+        assert (g2[i:i + 512] == want[fb[r] + 512:fb[r + 1]]).all()
+        i += 512

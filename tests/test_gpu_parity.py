@@ -157,3 +157,15 @@ def test_c2_full_batch_bitexact():
     p = N.synth_params(2)
     _, got, want = _run_both(p, N.make_cfg(), N.PCM_BIG_ENDIAN, threads=16)
     _assert_pcm_equal(got, want)
+
+
+@pytest.mark.slow
+def test_c3_full_batch_bitexact():
+    """The whole 65 536-frame C3 batch (LONG/START/SHORT/STOP + TNS data, compat mode) in float32
+    output (samples before Math.round) against the restatement."""
+    p = N.synth_params(3)
+    b, got, want = _run_both(p, N.make_cfg(), N.PCM_FLOAT32, threads=16)
+    seqs = np.bincount(b.ics["window_sequence"], minlength=4)
+    assert (seqs > 0).all(), seqs
+    assert b.tns is not None and (b.tns["n_filters"] > 0).mean() > 0.3  # TNS data in ~50 % of ch-frames
+    _assert_pcm_equal(got, want, N.PCM_FLOAT32)

@@ -184,6 +184,24 @@ def test_dropped_patch_with_trailing_borders(cfgid, smoothing):
         _assert_same(g2[19 * r:19 * (r + 1)], want[fb[r] + 17:fb[r + 1]], N.PCM_FLOAT32)
 
 
+def test_long_dependent_chain_uses_the_chain_walker():
+    """With G/Q smoothing a kSbrDep frame makes every later frame of the run depend on the one
+    before it: chains far longer than kSbrFixPasses (8) links.  The links past 8 run in the
+    sequential chain walker (one wave per run and channel) instead of one launch per link."""
+    fps = 120
+    p = N.synth_params(4, n_streams=2, frames_per_stream=fps)
+    rng = np.random.default_rng(9)
+
+    def edit(s):
+        s["hdr"]["start_freq"], s["hdr"]["stop_freq"], s["hdr"]["freq_scale"] = 0, 7, 0
+        s["hdr"]["smoothing_mode"] = 0
+        _var_grids(s, rng)
+
+    b = _edit(N.synth_batch(p), edit)
+    got, want = _decode_both(p, b, N.PCM_FLOAT32)
+    _assert_same(got, want, N.PCM_FLOAT32)
+
+
 def test_c4_single_frame_runs_and_empty_runs():
     p = N.synth_params(4, n_streams=4, frames_per_stream=9)
     b = N.synth_batch(p)

@@ -94,6 +94,39 @@ def test_mp4_errors():
         t.readNextFrame()
 
 
+def test_mp4_huge_sample_count_is_rejected():
+    """A fixed-size stsz claiming 2^28 samples in a ~1 KB file is corrupt: rejected before any
+    table is sized from it (no allocation from the claimed count)."""
+    _, _, frames = _lc_stream(4)
+    data = bytearray(W.write_mp4(frames, bytes([0x11, 0x90]), 48000, 2))
+    i = data.find(b"stsz")
+    assert i > 0
+    # version/flags(4) | sample_size(4) | sample_count(4): make it fixed-size with 2^28 samples
+    data[i + 8:i + 12] = (64).to_bytes(4, "big")
+    data[i + 12:i + 16] = (1 << 28).to_bytes(4, "big")
+    with pytest.raises(N.JaadError) as e:
+        M.MP4Container(bytes(data))
+    assert e.value.status == N.ERR_BITSTREAM
+    # per-sample sizes: a count beyond the box's bytes ends the box early
+    data[i + 8:i + 12] = (0).to_bytes(4, "big")
+    data[i + 12:i + 16] = (1 << 27).to_bytes(4, "big")
+    with pytest.raises(N.JaadError) as e:
+        M.MP4Container(bytes(data))
+    assert e.value.status == N.ERR_EOS
+
+
+def test_adts_split_is_linear():
+    """adts_frames searches one buffer at an offset (no per-frame copy of the rest of the file)."""
+    import time
+    _, _, frames = _lc_stream(6)
+    one = O.adts_wrap(frames, 3, 2)
+    t0 = time.perf_counter()
+    n = sum(1 for _ in N.adts_frames(one * 2000))  # 12 000 frames, ~6 MB
+    dt = time.perf_counter() - t0
+    assert n == 12000
+    assert dt < 5.0, dt
+
+
 def test_mp4_exports():
     L = N.lib()
     for name in M.MP4_EXPORTS:

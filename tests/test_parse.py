@@ -220,3 +220,24 @@ def test_pulse_data_is_applied_only_in_spec_mode():
         for k, amp in ((3, 5), (10, 2)):
             row[k] = row[k] + amp if row[k] > 0 else row[k] - amp
     assert np.array_equal(spec.q.astype(np.int32), want)
+
+
+def test_parser_snapshot_and_restore():
+    """jaad_parser_clone / jaad_parser_copy: a batch parsed after a restore is byte-identical to
+    the first parse (window shapes, PNS LCG and SBR history all rolled back)."""
+    p = N.synth_params(4, n_streams=1, frames_per_stream=8)
+    b = N.synth_batch(p)
+    cfg = N.cfg_for(p)
+    frames = O.write_frames(b, p.sf_index, sbr_writer=O.SbrWriter(cfg.ext_sf_index, 3))
+    P = N.Parser(cfg)
+    P.parse(frames[:3])
+    snap = P.snapshot()
+    first = P.parse(frames[3:])
+    P.restore(snap)
+    again = P.parse(frames[3:])
+    for k in ("q", "sf", "cb", "ics", "ms_used", "sbr"):
+        assert getattr(first, k).tobytes() == getattr(again, k).tobytes(), k
+    other = N.Parser(N.make_cfg(3, 2))
+    with pytest.raises(N.JaadError):
+        other.restore(snap)  # a snapshot of another configuration
+    snap.close()
