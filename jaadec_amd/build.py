@@ -106,11 +106,25 @@ def build_jni(force: bool = False) -> Path | None:
     return out
 
 
+def build_jni_mock(force: bool = False) -> Path:
+    """TEST INFRASTRUCTURE: the JNI glue (jaad_jni.c) compiled against tests/jni_mock/jni.h and a
+    mock JNIEnv, so tests/test_jni_glue.py runs its argument checks without a JDK."""
+    mock = ROOT / "tests" / "jni_mock"
+    out = mock / "libjaadjni_mock.so"
+    srcs = [CSRC / "jaad_jni.c", mock / "jni_mock.c"]
+    if force or _stale(out, srcs + [mock / "jni.h", LIB]):
+        _run(["gcc", "-O2", "-std=c11", "-fPIC", "-shared", "-Wall", "-I", str(mock), "-I", str(ROOT / "include"),
+              "-o", str(out)] + [str(x) for x in srcs] + ["-L", str(PKG), "-ljaadgpu", f"-Wl,-rpath,{PKG}",
+                                                          "-Wl,-rpath,$ORIGIN/../../jaadec_amd"])
+    return out
+
+
 def build_all(force: bool = False) -> None:
     build_oracle(force)
     build_synth(force)
     build_gpu(force)
     build_jni(force)
+    build_jni_mock(force)
 
 
 if __name__ == "__main__":

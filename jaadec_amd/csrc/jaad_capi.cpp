@@ -29,10 +29,8 @@ using namespace jaad;
 
 namespace {
 
-// offsets (in floats) into the SBR constant buffer, after qmf_c | dct4 | noise
+// offset (in floats) into the SBR constant buffer of qmf32_pre_twiddle, after qmf_c | dct4 | noise
 constexpr size_t kSbrConstTw32 = 640 + 224 + 1024;
-constexpr size_t kSbrConstDct32 = kSbrConstTw32 + 64;  // 8-byte aligned: double table
-static_assert(kSbrConstDct32 % 2 == 0, "double table alignment");
 
 // SampleFrequency maxTNS_SFB {long, short} (A/SampleFrequency.java:15-26)
 const unsigned char kMaxTnsSfb[12][2] = {{31, 9}, {31, 9}, {34, 10}, {40, 14}, {42, 14}, {51, 14},
@@ -203,7 +201,7 @@ struct jaad_ctx {
     std::vector<uint32_t> sbr_depth;             // HF fix pass of each channel-frame (scratch)
     SbrChState* d_sbr_state = nullptr;           // [slot][2], rewritten at the end of each call
     float* d_sbr_const = nullptr;                // qmf_c[640] | dct4 tab[192] w_re[16] w_im[16] | noise[1024] |
-                                                 // tw32[64] | dct32 double[2][32][32]
+                                                 // qmf32_pre_twiddle[32][2]
     DevBuf d_time, d_xlow, d_xsyn, d_xcarry, d_gq;
     hipStream_t cstream = nullptr;               // record uploads
     RecSet rsets[2];
@@ -792,7 +790,6 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
     a.noise = ctx->d_sbr_const + 640 + 224;
     a.down = sbr_downsampled(ctx->cfg) ? 1 : 0;
     a.tw32 = ctx->d_sbr_const + kSbrConstTw32;
-    a.dct32 = reinterpret_cast<const double*>(ctx->d_sbr_const + kSbrConstDct32);
     a.n_cf = (uint32_t)ncf;
     a.n_chunks = (uint32_t)ctx->sbr_chunks.size();
     a.n_last = (uint32_t)ctx->sbr_last.size();
@@ -1012,25 +1009,14 @@ int jaad_ctx_create(const jaad_stream_cfg* cfg, uint32_t n_slots, int device, ja
         const size_t sb = (size_t)n_slots * 2 * sizeof(SbrChState);
         if ((e = hipMalloc(&ctx->d_sbr_state, sb)) != hipSuccess) return bail(e, "hipMalloc sbr state");
         if ((e = hipMemset(ctx->d_sbr_state, 0, sb)) != hipSuccess) return bail(e, "hipMemset sbr state");
-        std::vector<float> k(kSbrConstDct32 + 2 * 2 * 32 * 32);
+        std::vector<float> k(kSbrConstTw32 + 64);
         std::memcpy(k.data(), JAAD_QMF_C, sizeof(JAAD_QMF_C));
         std::memcpy(k.data() + 640, JAAD_DCT4_64_TAB, sizeof(JAAD_DCT4_64_TAB));
         std::memcpy(k.data() + 640 + 192, JAAD_DCT_W_RE, sizeof(JAAD_DCT_W_RE));
         std::memcpy(k.data() + 640 + 208, JAAD_DCT_W_IM, sizeof(JAAD_DCT_W_IM));
         std::memcpy(k.data() + 640 + 224, JAAD_SBR_NOISE_TABLE, sizeof(JAAD_SBR_NOISE_TABLE));
-        // downsampled synthesis: qmf32_pre_twiddle (A/sbr/SynthesisFilterbank32.java:5-38) as
-        // (float) cos / -sin of pi(2k+1)/256, and the 32-point DCT-IV / DST-IV rows in double
-        for (int q = 0; q < 32; q++) {
-            k[kSbrConstTw32 + 2 * q] = (float)std::cos(M_PI * (2 * q + 1) / 256.0);
-            k[kSbrConstTw32 + 2 * q + 1] = -(float)std::sin(M_PI * (2 * q + 1) / 256.0);
-        }
-        double* d32 = reinterpret_cast<double*>(k.data() + kSbrConstDct32);
-        for (int h = 0; h < 2; h++)
-            for (int r = 0; r < 32; r++)
-                for (int n = 0; n < 32; n++) {
-                    const double ph = M_PI / 128.0 * (double)((2 * n + 1) * (2 * r + 1));
-                    d32[(h * 32 + r) * 32 + n] = h ? std::sin(ph) : std::cos(ph);
-                }
+        // downsampled synthesis: qmf32_pre_twiddle (A/sbr/SynthesisFilterbank32.java:5-38) verbatim
+        std::memcpy(k.data() + kSbrConstTw32, JAAD_QMF32_PRE_TWIDDLE, sizeof(JAAD_QMF32_PRE_TWIDDLE));
         if ((e = hipMalloc(&ctx->d_sbr_const, k.size() * sizeof(float))) != hipSuccess) return bail(e, "hipMalloc sbr const");
         if ((e = hipMemcpy(ctx->d_sbr_const, k.data(), k.size() * sizeof(float), hipMemcpyHostToDevice)) != hipSuccess)
             return bail(e, "hipMemcpy sbr const");

@@ -106,3 +106,25 @@ JNIEXPORT void JNICALL Java_net_sourceforge_jaad_aac_gpu_GpuDSP_nativeReset(JNIE
     int rc = jaad_state_reset(ctx, (uint32_t)slot);
     if (rc) throw_aac(env, ctx, rc);
 }
+
+/* static native void nativeRegister(long h, ByteBuffer buf) / nativeUnregister(long h, ByteBuffer buf):
+ * page-lock a direct buffer the stream reuses call after call (jaad_host_register), so
+ * nativeDecode copies it by DMA without staging; unregister before the buffer is released. */
+JNIEXPORT void JNICALL Java_net_sourceforge_jaad_aac_gpu_GpuDSP_nativeRegister(JNIEnv* env, jclass cls, jlong h,
+                                                                             jobject buf) {
+    (void)cls;
+    jaad_ctx* ctx = (jaad_ctx*)(intptr_t)h;
+    const jlong cap = buf ? (*env)->GetDirectBufferCapacity(env, buf) : -1;
+    void* p = buf ? (*env)->GetDirectBufferAddress(env, buf) : NULL;
+    const int rc = (!ctx || !p || cap <= 0) ? JAAD_ERR_INVALID_ARG : jaad_host_register(ctx, p, (size_t)cap);
+    if (rc) throw_aac(env, ctx, rc);
+}
+
+JNIEXPORT void JNICALL Java_net_sourceforge_jaad_aac_gpu_GpuDSP_nativeUnregister(JNIEnv* env, jclass cls, jlong h,
+                                                                               jobject buf) {
+    (void)cls;
+    jaad_ctx* ctx = (jaad_ctx*)(intptr_t)h;
+    void* p = buf ? (*env)->GetDirectBufferAddress(env, buf) : NULL;
+    const int rc = (!ctx || !p) ? JAAD_ERR_INVALID_ARG : jaad_host_unregister(ctx, p);
+    if (rc) throw_aac(env, ctx, rc);
+}

@@ -156,8 +156,7 @@ struct SbrArgs {
     const float* dct;           // dct4_64_tab [192] + w_re [16] + w_im [16]
     // downsampled SBR (extension rate = core rate): 32-band synthesis, 1024 samples per frame
     int down;
-    const float* tw32;          // qmf32_pre_twiddle [32][2] (cos, -sin of pi(2k+1)/256)
-    const double* dct32;        // [2][32][32]: cos / sin (pi(2n+1)(2k+1)/128), row k
+    const float* tw32;          // qmf32_pre_twiddle [32][2] (A/sbr/SynthesisFilterbank32.java:5-38)
     uint32_t n_cf, n_chunks, n_last;
     int nch;
     uint32_t out_mode;          // JAAD_PCM_*

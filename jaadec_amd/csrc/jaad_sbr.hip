@@ -16,7 +16,11 @@
 // radix-2 DIF stages exchange partners with v_permlane16_swap (xor 16) and DPP (xor 8..1).
 #include <hip/hip_runtime.h>
 
+#include <utility>
+
 #include "jaad_sbr.h"
+#define JAAD_DCT32_TABLE static constexpr
+#include "tables/jaad_sbr_dct32.inc"
 #include "jaad_wave.h"
 
 namespace jaad {
@@ -873,6 +877,125 @@ __global__ __launch_bounds__(256, 3) void sbr_hf_kernel(SbrArgs A)
 }
 
 // ---------------------------------------------------------------------------------------------
+// synthesis: where the rows of one frame of a chunk's sequence come from (all wave-uniform)
+// ---------------------------------------------------------------------------------------------
+struct SynSrc {
+    const gfloat* xs;  // rows l >= t0 (64 bands, 128 floats a row)
+    const gfloat* xc;  // rows l < t0: the carried Xsbr rows 2..7, kprev bands
+    int t0, kprev, rows;
+    size_t n0;         // first output sample (emitting frames)
+    bool emit, dup;
+};
+// the record fields the synthesis needs (dwords 0..3 and the slot), loaded one frame ahead
+struct SynRec {
+    uint32_t w0, w1, w2, w3, slot;
+};
+
+// SynthesisFilterbank32's DCT4_32 / DST4_32 (A/sbr/SynthesisFilterbank32.java:95-940): the
+// reference's straight-line binary32 programs (tables/jaad_sbr_dct32.inc), unrolled at compile
+// time over a register file r[] (in place on r[0..31], temporaries above), same ops, same order.
+template <int kKind, int kD, int kA, int kB>
+__device__ __forceinline__ void dct32_op(float* r, float k)
+{
+    if constexpr (kKind == 0) r[kD] = r[kA] - r[kB];
+    else if constexpr (kKind == 1) r[kD] = r[kA] + r[kB];
+    else r[kD] = k * r[kA];
+}
+template <size_t... I>
+__device__ __forceinline__ void dct4_32(float* r, std::index_sequence<I...>)
+{
+    (dct32_op<JAAD_SBR_DCT4_32_OPS[I][0], JAAD_SBR_DCT4_32_OPS[I][1], JAAD_SBR_DCT4_32_OPS[I][2],
+              JAAD_SBR_DCT4_32_OPS[I][3]>(r, JAAD_SBR_DCT4_32_K[I]),
+     ...);
+}
+template <size_t... I>
+__device__ __forceinline__ void dst4_32(float* r, std::index_sequence<I...>)
+{
+    (dct32_op<JAAD_SBR_DST4_32_OPS[I][0], JAAD_SBR_DST4_32_OPS[I][1], JAAD_SBR_DST4_32_OPS[I][2],
+              JAAD_SBR_DST4_32_OPS[I][3]>(r, JAAD_SBR_DST4_32_K[I]),
+     ...);
+}
+
+// Downsampled synthesis (SynthesisFilterbank32.synthesis, A/sbr/SynthesisFilterbank32.java:44-93),
+// a frame at a time: lane (half, l) pre-twiddles row l of the frame and runs DCT4_32 (half 0, x1)
+// or DST4_32 (half 1, x2) on it -- the 32 slots of a frame in parallel --, the v blocks go to an
+// LDS ring of 41 (9 history + 32), then the 10-tap window makes 2 slots' 32 samples per pass.
+constexpr int kRing32 = 41;
+template <class HistSrc, class FrameSrc, class RecLoad, class StorePcm>
+__device__ __forceinline__ void synthesis32(const SbrArgs& A, const SbrChunk& ck, int wave, HistSrc history_src,
+                                            FrameSrc frame_src, RecLoad rec_load, const float (&cw)[10],
+                                            StorePcm store_pcm)
+{
+    __shared__ float ring_s[kWavesPerBlock][kRing32][64];
+    __shared__ float tr_s[kWavesPerBlock][2][32][33];  // DCT / DST outputs [half][slot][n] (+1 pad)
+    float(*ring)[64] = ring_s[wave];
+    float(*tr)[32][33] = tr_s[wave];
+    const int u = lane_id();
+    const int l = u & 31, half = u >> 5;
+    const float scale = 1.f / 64.f;
+    // v blocks of the frame's rows -> ring[(base + l) % kRing32]
+    auto transform = [&](const SynSrc& S, int base) {
+        if (l < S.rows) {
+            const bool carry = l < S.t0;
+            const gfloat* row = carry ? S.xc + (l + 2) * 128 : S.xs + l * 128;
+            const int klim = carry ? S.kprev : 64;
+            float r[JAAD_SBR_DCT4_32_NREG > JAAD_SBR_DST4_32_NREG ? JAAD_SBR_DCT4_32_NREG : JAAD_SBR_DST4_32_NREG];
+#pragma unroll
+            for (int k = 0; k < 32; k++) {
+                const float re = k < klim ? row[2 * k] : 0.0f, im = k < klim ? row[2 * k + 1] : 0.0f;
+                const float t0 = A.tw32[2 * k], t1 = A.tw32[2 * k + 1];  // qmf32_pre_twiddle[k]
+                float x1 = (re * t0) - (im * t1);
+                float x2 = (im * t0) + (re * t1);
+                x1 *= scale;
+                x2 *= scale;
+                r[k] = half ? x2 : x1;
+            }
+            if (half) dst4_32(r, std::make_index_sequence<JAAD_SBR_DST4_32_NOPS>{});
+            else dct4_32(r, std::make_index_sequence<JAAD_SBR_DCT4_32_NOPS>{});
+#pragma unroll
+            for (int n = 0; n < 32; n++) tr[half][l][n] = r[n];
+        }
+        wave_sync();
+        if (l < S.rows) {
+            float* vb = ring[(base + l) % kRing32];
+#pragma unroll
+            for (int n = 0; n < 32; n++) {
+                const float c1 = tr[0][l][n], s2 = tr[1][l][n];
+                if (!half) vb[n] = -c1 + s2;       // v[n] = -x1[n] + x2[n]
+                else vb[63 - n] = c1 + s2;         // v[63 - n] = x1[n] + x2[n]
+            }
+        }
+        wave_sync();
+    };
+    // the 10-tap window (:73-86) of slot s (block b = its ring block), sample l
+    auto window = [&](int b) {
+        float acc = 0.0f;
+#pragma unroll
+        for (int t = 0; t < 10; t++) {
+            const float* vt = ring[(b - t + kRing32) % kRing32];
+            const float p = vt[(t & 1) * 32 + l] * cw[t];
+            acc = t == 0 ? p : acc + p;
+        }
+        return acc;
+    };
+    SynSrc S = history_src();
+    SynRec W{};
+    rec_load(0, W);
+    transform(S, 0);
+    int base = S.rows;  // ring block of the next frame's slot 0
+    for (uint32_t j = 0; j < ck.n; j++) {
+        S = frame_src((int)j, W);
+        rec_load((int)j + 1, W);
+        if (!S.rows) continue;
+        transform(S, base);
+        if (S.emit)
+            for (int s = half; s < S.rows; s += 2) store_pcm(S, S.n0 + 32 * s + l, window(base + s));
+        base = (base + S.rows) % kRing32;
+        wave_sync();
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
 // SynthesisFilterbank64.synthesis (A/sbr/SynthesisFilterbank64.java:9-79) + SampleBuffer PCM
 // ---------------------------------------------------------------------------------------------
 // kDown: SynthesisFilterbank32 (downsampled SBR, A/sbr/SynthesisFilterbank32.java:44-93), bands
@@ -882,8 +1005,7 @@ __global__ __launch_bounds__(256, 3) void sbr_hf_kernel(SbrArgs A)
 template <bool kDown>
 __global__ __launch_bounds__(256) void sbr_synthesis_kernel(SbrArgs A)
 {
-    __shared__ float vring_s[kWavesPerBlock][10][128];
-    __shared__ float xin_s[kWavesPerBlock][64];
+    __shared__ float vring_s[kWavesPerBlock][kDown ? 1 : 10][128];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t ci = blockIdx.x * kWavesPerBlock + wave;
     if (ci >= A.n_chunks) return;
@@ -902,25 +1024,13 @@ __global__ __launch_bounds__(256) void sbr_synthesis_kernel(SbrArgs A)
     for (int t = 0; t < 10; t++) cw[t] = kDown ? A.qmf_c[64 * t + 2 * e] : A.qmf_c[u + 64 * t];
     const float scale = 1.f / 64.f;
     int vpos = 0;
-    // downsampled: pre-twiddle of band e and lane (half, e)'s row of the DCT-IV (half 0) / DST-IV
-    // (half 1) matrix, output element e
-    float tw_c = 0.0f, tw_s = 0.0f;
-    double cm[kDown ? 32 : 1];
-    if constexpr (kDown) {
-        tw_c = A.tw32[2 * e];
-        tw_s = A.tw32[2 * e + 1];
-#pragma unroll
-        for (int n = 0; n < 32; n++) cm[n] = A.dct32[(half * 32 + e) * 32 + n];
-    }
-    float* xin = xin_s[wave];
     // This lane's two DCT inputs of a slot, gathered straight from the row of X (64 float2, band
     // order) instead of exchanged through cross-lane permutes:
     //   64 bands: half 0 (in_real1[e], in_imag1[e]) = (Re X[2e], Re X[63-2e]),
     //             half 1 (in_real2[e], in_imag2[e]) = (Im X[63-2e], Im X[2e])  (SynthesisFilterbank64.java:25-42)
-    //   32 bands: (Re X[e], Im X[e]) in both halves
-    const int band_a = kDown ? e : (half ? 63 - 2 * e : 2 * e);
-    const int band_b = kDown ? e : (half ? 2 * e : 63 - 2 * e);
-    const int ia = kDown ? 2 * e : 2 * band_a + half, ib = kDown ? 2 * e + 1 : 2 * band_b + half;
+    const int band_a = half ? 63 - 2 * e : 2 * e;
+    const int band_b = half ? 2 * e : 63 - 2 * e;
+    const int ia = 2 * band_a + half, ib = 2 * band_b + half;
     // Rows hold 64 bands in memory; bands >= klim read as zero.  The mask is applied where the
     // slot consumes the values (a select next to the load would wait for it).
     auto fetch = [&](const gfloat* r, float& a, float& b) {
@@ -930,43 +1040,6 @@ __global__ __launch_bounds__(256) void sbr_synthesis_kernel(SbrArgs A)
     auto mask = [&](int klim, float& a, float& b) {
         a = band_a < klim ? a : 0.0f;
         b = band_b < klim ? b : 0.0f;
-    };
-
-    // downsampled slot (:50-92): pre-twiddle, DCT-IV / DST-IV, v block of 64, 32 windowed outputs
-    // (lanes of half 0 return sample e of the slot in `res`)
-    auto slot32 = [&](float xr, float xi, bool emit, float& res) {
-        float x1 = (xr * tw_c) - (xi * tw_s);
-        float x2 = (xi * tw_c) + (xr * tw_s);
-        x1 *= scale;
-        x2 *= scale;
-        xin[u] = half ? x2 : x1;
-        wave_sync();
-        double acc = 0.0;
-#pragma unroll
-        for (int n = 0; n < 32; n++) acc = acc + ((double)xin[half * 32 + n] * cm[n]);
-        const float y = (float)acc;          // half 0: DCT-IV(x1)[e], half 1: DST-IV(x2)[e]
-        const float o = shfl(y, u ^ 32);     // the other transform's element e
-        float* vb = vring[vpos];
-        if (!half) vb[e] = -y + o;           // v[n] = -x1[n] + x2[n]
-        else vb[63 - e] = o + y;             // v[63 - n] = x1[n] + x2[n]
-        wave_sync();
-        if (emit && !half) {
-            const float* v0 = vring[vpos];
-            const float* v1 = vring[(vpos + 9) % 10];
-            const float* v2 = vring[(vpos + 8) % 10];
-            const float* v3 = vring[(vpos + 7) % 10];
-            const float* v4 = vring[(vpos + 6) % 10];
-            const float* v5 = vring[(vpos + 5) % 10];
-            const float* v6 = vring[(vpos + 4) % 10];
-            const float* v7 = vring[(vpos + 3) % 10];
-            const float* v8 = vring[(vpos + 2) % 10];
-            const float* v9 = vring[(vpos + 1) % 10];
-            res = (v0[e] * cw[0]) + (v1[32 + e] * cw[1]) + (v2[e] * cw[2]) + (v3[32 + e] * cw[3]) +
-                  (v4[e] * cw[4]) + (v5[32 + e] * cw[5]) + (v6[e] * cw[6]) + (v7[32 + e] * cw[7]) +
-                  (v8[e] * cw[8]) + (v9[32 + e] * cw[9]);
-        }
-        wave_sync();
-        vpos = vpos == 9 ? 0 : vpos + 1;
     };
 
     // one slot: DCT-IV pair -> v block (:99-129); emit: window (:134-146), sample u in `res`
@@ -1007,35 +1080,22 @@ __global__ __launch_bounds__(256) void sbr_synthesis_kernel(SbrArgs A)
     };
 
     const size_t spf = kDown ? 1024 : 2048, sps = kDown ? 32 : 64;  // output samples per frame / slot
-    auto slot = [&](float Xr, float Xi, bool emit, float& res) {
-        if constexpr (kDown) slot32(Xr, Xi, emit, res);
-        else slot64(Xr, Xi, emit, res);
-    };
+    auto slot = [&](float Xr, float Xi, bool emit, float& res) { slot64(Xr, Xi, emit, res); };
 
     // The chunk's slots (9 history slots, then 32 per frame) run as a software pipeline of 4-slot
     // groups: the rows of group g+1 are loaded while group g computes, and group g's PCM is
     // stored after an explicit vmcnt(0) (vmem_drain): vmcnt counts loads and stores in issue order,
     // so a store issued before the next group's loads would otherwise make every row load wait for
     // the previous slot's PCM to reach memory (one global round trip per slot).
-    // Where the rows of one frame of the sequence come from.  All fields are wave-uniform.
-    struct Src {
-        const gfloat* xs;  // rows l >= t0 (64 bands, 128 floats a row)
-        const gfloat* xc;  // rows l < t0: the carried Xsbr rows 2..7, kprev bands
-        int t0, kprev, rows;
-        size_t n0;         // first output sample (emitting frames)
-        bool emit, dup;
-    };
     auto uni = [](uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane(x); };  // (int -> uint32, no sign extension)
     auto uptr = [&](const float* p) {
         const uint64_t v = reinterpret_cast<uint64_t>(p);
         return (const gfloat*)(((uint64_t)uni((uint32_t)(v >> 32)) << 32) | uni((uint32_t)v));
     };
-    // the record fields the synthesis needs (dwords 0..3 and the slot), loaded one frame ahead
-    struct RecW { uint32_t w0, w1, w2, w3, slot; };
     static_assert(offsetof(SbrRec, flags) == 2 && offsetof(SbrRec, kx_prev) == 6 && offsetof(SbrRec, M_prev) == 7 &&
                       offsetof(SbrRec, first) == 11 && offsetof(SbrRec, t_E) == 12 && offsetof(SbrRec, slot) == 64,
                   "SbrRec field offsets used by the synthesis");
-    auto rec_load = [&](int j, RecW& W) {
+    auto rec_load = [&](int j, SynRec& W) {
         if (j >= (int)ck.n) return;
         const uint32_t* r = reinterpret_cast<const uint32_t*>(A.recs + (size_t)(ck.frame0 + j) * nch + rc);
         W.w0 = r[0];
@@ -1045,8 +1105,8 @@ __global__ __launch_bounds__(256) void sbr_synthesis_kernel(SbrArgs A)
         W.slot = r[16];
     };
     // frame j >= 0 of the chunk from its record fields
-    auto frame_src = [&](int j, const RecW& W) {
-        Src S{};
+    auto frame_src = [&](int j, const SynRec& W) {
+        SynSrc S{};
         const uint32_t f = ck.frame0 + (uint32_t)j;
         const uint32_t cf = f * nch + rc;
         const uint32_t flags = uni(W.w0 >> 16) & 0xFF, first = uni(W.w2 >> 24) & 0xFF;
@@ -1073,7 +1133,7 @@ __global__ __launch_bounds__(256) void sbr_synthesis_kernel(SbrArgs A)
     };
     // frame -1: the v history (slots 23..31 of the frame before the chunk)
     auto history_src = [&]() {
-        Src S{};
+        SynSrc S{};
         const uint32_t cf0 = uni(ck.frame0 * nch + rc);
         const SbrRec& R0 = A.recs[cf0];
         // PS right channel (qmfs1): history of the previous frame that carried PS data
@@ -1084,7 +1144,7 @@ __global__ __launch_bounds__(256) void sbr_synthesis_kernel(SbrArgs A)
         S.rows = 9;
         return S;
     };
-    auto load_group = [&](const Src& S, int l0, float (&ga)[4], float (&gb)[4], int (&kl)[4]) {
+    auto load_group = [&](const SynSrc& S, int l0, float (&ga)[4], float (&gb)[4], int (&kl)[4]) {
 #pragma unroll
         for (int i = 0; i < 4; i++) {
             const int l = min(l0 + i, S.rows - 1);  // (rows past the frame's last are not used)
@@ -1095,30 +1155,38 @@ __global__ __launch_bounds__(256) void sbr_synthesis_kernel(SbrArgs A)
     };
     const bool f32 = (A.out_mode & JAAD_PCM_FLOAT32) != 0;
     const bool swap = !(A.out_mode & JAAD_PCM_LITTLE_ENDIAN);
-    auto store_group = [&](const Src& S, int l0, const float (&res)[4]) {
-        if (!S.emit || (kDown && half)) return;
-        const int k = kDown ? e : u;
+    // PCM sample n (frame-major, 2 channels) of this channel; a frame without PS data or a mono
+    // core writes both channels (SampleBuffer duplicates an SCE, SBR1 copies L to R)
+    auto store_pcm = [&](const SynSrc& S, size_t n, float v) {
+        const bool one = (nch == 2 || ps) && !S.dup;  // this channel's half of the word
+        if (f32) {
+            float* o = reinterpret_cast<float*>(A.pcm) + 2 * n;
+            if (one) o[c] = v;
+            else *reinterpret_cast<float2*>(o) = make_float2(v, v);
+        } else {
+            uint32_t s16 = (uint32_t)(uint16_t)(int16_t)java_round16(v);
+            if (swap) s16 = ((s16 & 0xFF) << 8) | (s16 >> 8);
+            if (one) reinterpret_cast<uint16_t*>(A.pcm)[2 * n + c] = (uint16_t)s16;
+            else reinterpret_cast<uint32_t*>(A.pcm)[n] = s16 | (s16 << 16);
+        }
+    };
+    auto store_group = [&](const SynSrc& S, int l0, const float (&res)[4]) {
+        if (!S.emit) return;
 #pragma unroll
         for (int i = 0; i < 4; i++) {
             const int l = l0 + i;
             if (l >= S.rows) break;
-            const size_t n = S.n0 + sps * l + k;
-            const bool one = (nch == 2 || ps) && !S.dup;  // this channel's half of the word
-            if (f32) {
-                float* o = reinterpret_cast<float*>(A.pcm) + 2 * n;
-                if (one) o[c] = res[i];
-                else *reinterpret_cast<float2*>(o) = make_float2(res[i], res[i]);
-            } else {
-                uint32_t s16 = (uint32_t)(uint16_t)(int16_t)java_round16(res[i]);
-                if (swap) s16 = ((s16 & 0xFF) << 8) | (s16 >> 8);
-                if (one) reinterpret_cast<uint16_t*>(A.pcm)[2 * n + c] = (uint16_t)s16;
-                else reinterpret_cast<uint32_t*>(A.pcm)[n] = s16 | (s16 << 16);
-            }
+            store_pcm(S, S.n0 + sps * l + u, res[i]);
         }
     };
 
-    Src S = history_src();
-    RecW W{};                    // record fields of frame j + 1
+    if constexpr (kDown) {
+        synthesis32(A, ck, wave, history_src, frame_src, rec_load, cw, store_pcm);
+        return;
+    }
+
+    SynSrc S = history_src();
+    SynRec W{};                  // record fields of frame j + 1
     rec_load(0, W);
     float ga[4] = {0, 0, 0, 0}, gb[4] = {0, 0, 0, 0};
     int kl[4] = {64, 64, 64, 64};
@@ -1137,12 +1205,12 @@ __global__ __launch_bounds__(256) void sbr_synthesis_kernel(SbrArgs A)
             // the next group: later rows of this frame or the first rows of the next one (only
             // scalar selects branch; the loads themselves are unconditional, a reload of the
             // current rows when there is nothing to fetch)
-            Src Sn = S;
+            SynSrc Sn = S;
             int ln = l0 + 4;
             if (ln >= S.rows) {
                 have = false;
                 if (j + 1 < (int)ck.n) {
-                    const Src F = frame_src(j + 1, W);
+                    const SynSrc F = frame_src(j + 1, W);
                     if (F.rows) {
                         Sn = F;
                         ln = 0;

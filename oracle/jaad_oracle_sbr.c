@@ -16,6 +16,7 @@
 #include <string.h>
 
 #include "../jaadec_amd/csrc/tables/jaad_sbr_tables.inc"
+#include "../jaadec_amd/csrc/tables/jaad_sbr_dct32.inc"
 
 #ifndef M_PI
 #define M_PI 3.14159265358979323846
@@ -310,47 +311,39 @@ static void qmf_synthesis(float* v, int* v_index, float (*X)[64][2], float* outp
 /* ------------------------------------------------------------------------------------------ */
 /* SynthesisFilterbank32.synthesis (A/sbr/SynthesisFilterbank32.java:44-93): downsampled SBR    */
 /* ------------------------------------------------------------------------------------------ */
-/* PARITY UNPINNED in the transform: the reference's DCT4_32 / DST4_32 (:95-940) are machine-
- * generated fast factorisations of the 32-point DCT-IV y[k] = sum x[n] cos(pi(2n+1)(2k+1)/128) and
- * DST-IV (sin); their identity was read off their structure (the final rotations by (2k+1)pi/128
- * and the 1/(2 sin((2k+1)pi/128)) output scales), not executed.  Here both are evaluated as double
- * sums of the float inputs, rounded once to float; the pre-twiddle, scale, v ring and the
- * 10-tap window keep the reference's binary32 order.  Expected distance to the reference: a few
- * ulp in v, i.e. PCM within +-1 LSB (the metric's tolerance).  The structure (signs, twiddle,
- * ring taps) is pinned by the analysis -> synthesis reconstruction test (tests/test_sbr_oracle.py). */
-static void dct4_dst4_32(const float* x1, const float* x2, float* c1, float* s2)
+/* DCT4_32 / DST4_32 (:95-940): the reference's generated straight-line binary32 code, carried as
+ * op lists (tables/jaad_sbr_dct32.inc, extracted by tools/extract_tables.py) and executed here in
+ * order, in place on the 32-float array as the reference calls them (DCT4_32(x1, x1)). */
+static void run_dct32(const unsigned short (*ops)[4], const float* K, int nops, float* x)
 {
-    for (int k = 0; k < 32; k++) {
-        double a = 0.0, b = 0.0;
-        for (int n = 0; n < 32; n++) {
-            const double ph = M_PI / 128.0 * (double)((2 * n + 1) * (2 * k + 1));
-            a += (double)x1[n] * cos(ph);
-            b += (double)x2[n] * sin(ph);
-        }
-        c1[k] = (float)a;
-        s2[k] = (float)b;
+    float r[JAAD_SBR_DCT4_32_NREG > JAAD_SBR_DST4_32_NREG ? JAAD_SBR_DCT4_32_NREG : JAAD_SBR_DST4_32_NREG];
+    memcpy(r, x, 32 * sizeof(float));
+    for (int i = 0; i < nops; i++) {
+        const unsigned short* o = ops[i];
+        r[o[1]] = o[0] == 0 ? r[o[2]] - r[o[3]] : o[0] == 1 ? r[o[2]] + r[o[3]] : K[i] * r[o[2]];
     }
+    memcpy(x, r, 32 * sizeof(float));
 }
 
 static void qmf_synthesis32(float* v, int* v_index, float (*X)[64][2], float* output)
 {
     const float scale = 1.f / 64.f;
-    float x1[32], x2[32], c1[32], s2[32];
+    float x1[32], x2[32];
     int out = 0;
     for (int l = 0; l < 32; l++) {
         for (int k = 0; k < 32; k++) {
-            /* qmf32_pre_twiddle[k] = (cos, -sin) of pi(2k+1)/256 as float */
-            const float tc = (float)cos(M_PI * (2 * k + 1) / 256.0), ts = -(float)sin(M_PI * (2 * k + 1) / 256.0);
+            const float tc = JAAD_QMF32_PRE_TWIDDLE[k][0], ts = JAAD_QMF32_PRE_TWIDDLE[k][1];
             x1[k] = (X[l][k][0] * tc) - (X[l][k][1] * ts);
             x2[k] = (X[l][k][1] * tc) + (X[l][k][0] * ts);
             x1[k] *= scale;
             x2[k] *= scale;
         }
-        dct4_dst4_32(x1, x2, c1, s2);
+        run_dct32(JAAD_SBR_DCT4_32_OPS, JAAD_SBR_DCT4_32_K, JAAD_SBR_DCT4_32_NOPS, x1);
+        run_dct32(JAAD_SBR_DST4_32_OPS, JAAD_SBR_DST4_32_K, JAAD_SBR_DST4_32_NOPS, x2);
         const int vi = *v_index;
         for (int n = 0; n < 32; n++) {
-            v[vi + n] = v[vi + 640 + n] = -c1[n] + s2[n];
-            v[vi + 63 - n] = v[vi + 640 + 63 - n] = c1[n] + s2[n];
+            v[vi + n] = v[vi + 640 + n] = -x1[n] + x2[n];
+            v[vi + 63 - n] = v[vi + 640 + 63 - n] = x1[n] + x2[n];
         }
         const float* w = v + vi;
         for (int k = 0; k < 32; k++) {

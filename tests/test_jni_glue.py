@@ -1,0 +1,155 @@
+"""The JNI glue (jaadec_amd/csrc/jaad_jni.c) compiled against a mock JNIEnv
+(tests/jni_mock/): its argument and capacity checks and its AACException mapping run here
+without a JDK; with a GPU the same entry points decode a batch through direct buffers."""
+import ctypes as C
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from jaadec_amd import native as N
+
+LIB = Path(__file__).resolve().parent / "jni_mock" / "libjaadjni_mock.so"
+PFX = "Java_net_sourceforge_jaad_aac_gpu_GpuDSP_"
+AAC_EXC = "net/sourceforge/jaad/aac/AACException"
+
+
+class Buf(C.Structure):
+    """A mock direct ByteBuffer: (address, capacity)."""
+    _fields_ = [("address", C.c_void_p), ("capacity", C.c_int64)]
+
+
+def _lib():
+    if not LIB.exists():
+        pytest.skip("libjaadjni_mock.so not built (python -m jaadec_amd.build)")
+    L = C.CDLL(str(LIB))
+    L.jni_mock_env.restype = C.c_void_p
+    L.jni_mock_take_exception.argtypes = [C.c_char_p, C.c_int, C.c_char_p, C.c_int]
+    create = getattr(L, PFX + "nativeCreate")
+    create.argtypes = [C.c_void_p, C.c_void_p] + [C.c_int32] * 7
+    create.restype = C.c_int64
+    getattr(L, PFX + "nativeDestroy").argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
+    decode = getattr(L, PFX + "nativeDecode")
+    decode.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_int32, C.c_int32] + [C.c_void_p] * 10 + [C.c_int32]
+    getattr(L, PFX + "nativeReset").argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32]
+    for name in ("nativeRegister", "nativeUnregister"):
+        getattr(L, PFX + name).argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p]
+    return L
+
+
+def _exception(L):
+    cls, msg = C.create_string_buffer(256), C.create_string_buffer(1024)
+    if not L.jni_mock_take_exception(cls, 256, msg, 1024):
+        return None
+    return cls.value.decode(), msg.value.decode()
+
+
+def _buf(a, keep):
+    if a is None:
+        return None
+    b = Buf(a.ctypes.data, a.nbytes)
+    keep.append(b)
+    return C.addressof(b)
+
+
+def test_exports():
+    L = _lib()
+    for name in ("nativeCreate", "nativeDestroy", "nativeDecode", "nativeReset", "nativeRegister",
+                 "nativeUnregister"):
+        assert hasattr(L, PFX + name)
+
+
+def test_invalid_handles_throw_aac_exception():
+    L = _lib()
+    env = L.jni_mock_env()
+    getattr(L, PFX + "nativeDecode")(env, None, 0, 1, 1, 2, *([None] * 10), 0)
+    cls, msg = _exception(L)
+    assert cls == AAC_EXC and N.strerror(N.ERR_INVALID_ARG) in msg
+    getattr(L, PFX + "nativeReset")(env, None, 0, 0)
+    cls, msg = _exception(L)
+    assert cls == AAC_EXC and N.strerror(N.ERR_INVALID_ARG) in msg
+    getattr(L, PFX + "nativeDestroy")(env, None, 0)  # a null handle is a no-op
+    assert _exception(L) is None
+    a = np.zeros(64, np.uint8)
+    b = Buf(a.ctypes.data, a.nbytes)
+    for name in ("nativeRegister", "nativeUnregister"):
+        getattr(L, PFX + name)(env, None, 0, C.addressof(b))
+        cls, msg = _exception(L)
+        assert cls == AAC_EXC and N.strerror(N.ERR_INVALID_ARG) in msg
+
+
+def test_create_without_gpu_throws_no_device():
+    import torch
+    if torch.cuda.device_count() > 0:
+        pytest.skip("a GPU is present")
+    L = _lib()
+    h = getattr(L, PFX + "nativeCreate")(L.jni_mock_env(), None, 3, 2, 0, 0, 0, 4, 0)
+    assert h == 0
+    cls, msg = _exception(L)
+    assert cls == AAC_EXC and N.strerror(N.ERR_NO_DEVICE) in msg
+
+
+@pytest.mark.gpu
+def test_decode_through_direct_buffers_and_capacity_checks():
+    L = _lib()
+    env = L.jni_mock_env()
+    p = N.synth_params(2, n_streams=3, frames_per_stream=20)
+    b = N.synth_batch(p)
+    with N.Context(N.make_cfg(), 3) as ctx:
+        want = ctx.decode(b, N.PCM_BIG_ENDIAN)
+    h = getattr(L, PFX + "nativeCreate")(env, None, 3, 2, 0, 0, 0, 3, 0)
+    assert h and _exception(L) is None
+    decode = getattr(L, PFX + "nativeDecode")
+    try:
+        out = np.zeros_like(want)
+        keep = []
+        args = [_buf(x, keep) for x in (b.stream_slot, b.frame_begin, b.q, b.sf, b.cb, b.ics, b.ms_used, b.tns, None,
+                                         out)]
+        decode(env, None, h, b.n_frames, len(b.stream_slot), 2, *args, N.PCM_BIG_ENDIAN)
+        assert _exception(L) is None
+        assert (out == want).all()
+        # the same buffers page-locked once (nativeRegister): DMA without staging, same PCM
+        reg = [a for a in (args[2], args[3], args[4], args[5], args[6], args[9])]
+        for r in reg:
+            getattr(L, PFX + "nativeRegister")(env, None, h, r)
+            assert _exception(L) is None
+        out[:] = 0
+        for slot in range(3):  # from fresh stream states again
+            getattr(L, PFX + "nativeReset")(env, None, h, slot)
+        decode(env, None, h, b.n_frames, len(b.stream_slot), 2, *args, N.PCM_BIG_ENDIAN)
+        assert _exception(L) is None
+        assert (out == want).all()
+        for r in reg:
+            getattr(L, PFX + "nativeUnregister")(env, None, h, r)
+            assert _exception(L) is None
+        # nch must be the context's channels per record
+        decode(env, None, h, b.n_frames, len(b.stream_slot), 1, *args, N.PCM_BIG_ENDIAN)
+        cls, msg = _exception(L)
+        assert cls == AAC_EXC and N.strerror(N.ERR_INVALID_ARG) in msg
+        # a q buffer one ch-frame short is refused before any copy
+        short = list(args)
+        qshort = Buf(b.q.ctypes.data, b.q.nbytes - 2048)
+        keep.append(qshort)
+        short[2] = C.addressof(qshort)
+        decode(env, None, h, b.n_frames, len(b.stream_slot), 2, *short, N.PCM_BIG_ENDIAN)
+        cls, msg = _exception(L)
+        assert cls == AAC_EXC and N.strerror(N.ERR_INVALID_ARG) in msg
+        # a PCM buffer too small for the batch
+        small = np.zeros(want.nbytes - 1, np.uint8)
+        args2 = list(args)
+        args2[9] = _buf(small, keep)
+        decode(env, None, h, b.n_frames, len(b.stream_slot), 2, *args2, N.PCM_BIG_ENDIAN)
+        cls, msg = _exception(L)
+        assert cls == AAC_EXC and N.strerror(N.ERR_INVALID_ARG) in msg
+        # a bitstream error (max_sfb beyond the swb count) maps to AACException too
+        bad = b.ics.copy()
+        bad["max_sfb"][0] = 60
+        args3 = list(args)
+        args3[5] = _buf(bad, keep)
+        decode(env, None, h, b.n_frames, len(b.stream_slot), 2, *args3, N.PCM_BIG_ENDIAN)
+        cls, msg = _exception(L)
+        assert cls == AAC_EXC and N.strerror(N.ERR_BITSTREAM) in msg
+        getattr(L, PFX + "nativeReset")(env, None, h, 1)
+        assert _exception(L) is None
+    finally:
+        getattr(L, PFX + "nativeDestroy")(env, None, h)

@@ -1,6 +1,8 @@
 """Pins the SBR restatement (oracle/jaad_oracle_sbr.c) against closed forms and the reference's
 own derived values (C4 header -> k0 13, k2 45, N_master 16, kx 13, M 32,
 N_high 16, N_low 8, N_Q 4)."""
+from pathlib import Path
+
 import numpy as np
 import pytest
 
@@ -96,9 +98,9 @@ def test_qmf_synthesis_matches_iso_closed_form():
 
 
 def test_downsampled_synthesis_reconstructs_the_analysed_signal():
-    """SynthesisFilterbank32 (downsampled SBR, a15'): the restatement's DCT-IV / DST-IV are not the
-    reference's generated code (parity unpinned there), so its structure -- pre-twiddle, signs,
-    v ring, the 10 taps of every other prototype coefficient -- is pinned by what any correct
+    """SynthesisFilterbank32 (downsampled SBR, a15'): the transforms are the reference's own
+    DCT4_32 / DST4_32 op lists (test below); the structure around them -- pre-twiddle, signs, v
+    ring, the 10 taps of every other prototype coefficient -- is pinned by what any correct
     32-band synthesis must do: analysis (kx = 32) followed by it reconstructs the input, delayed
     by 289 samples, to the QMF bank's aliasing level."""
     rng = np.random.default_rng(5)
@@ -110,6 +112,50 @@ def test_downsampled_synthesis_reconstructs_the_analysed_signal():
     assert np.abs(a - b).max() < 2e-3 * np.abs(b).max()
     # a sign error anywhere in the transform pair would not reconstruct
     assert np.abs(y[2000:5000] - b).max() > 0.5 * np.abs(b).max()
+
+
+def _dct32_program(name):
+    import re
+    src = (Path(__file__).resolve().parents[1] / "jaadec_amd/csrc/tables/jaad_sbr_dct32.inc").read_text()
+    body = re.search(name + r"_OPS\[\d+\]\[4\] = \{(.*?)\};", src, re.S).group(1)
+    ops = [tuple(map(int, t)) for t in re.findall(r"\{(\d+), (\d+), (\d+), (\d+)\}", body)]
+    ks = re.search(name + r"_K\[\d+\] = \{(.*?)\};", src, re.S).group(1)
+    ks = [float.fromhex(t.strip().rstrip("f")) if "p" in t else float(t.strip().rstrip("f"))
+          for t in ks.split(",") if t.strip()]
+    return ops, np.array(ks, np.float32)
+
+
+@pytest.mark.parametrize("name,fn", [("JAAD_SBR_DCT4_32", np.cos), ("JAAD_SBR_DST4_32", np.sin)])
+def test_dct32_programs_are_the_32_point_dct4_dst4(name, fn):
+    """The op lists extracted from SynthesisFilterbank32.DCT4_32 / DST4_32 (tools/extract_tables.py)
+    evaluate the 32-point DCT-IV / DST-IV y[k] = sum x[n] cos|sin(pi(2n+1)(2k+1)/128), in place
+    (outputs in registers 0..31), each register written once."""
+    ops, ks = _dct32_program(name)
+    dsts = [o[1] for o in ops]
+    assert len(set(d for d in dsts if d >= 32)) == sum(d >= 32 for d in dsts)  # temporaries: SSA
+    assert sorted(d for d in dsts if d < 32) == list(range(32))               # every output once
+    x = np.random.default_rng(3).standard_normal(32)
+    r = np.zeros(512)
+    r[:32] = x
+    for i, (kind, d, a, b) in enumerate(ops):
+        r[d] = r[a] - r[b] if kind == 0 else r[a] + r[b] if kind == 1 else float(ks[i]) * r[a]
+    n = np.arange(32)
+    want = fn(np.pi / 128 * np.outer(2 * n + 1, 2 * n + 1)) @ x
+    assert np.abs(r[:32] - want).max() < 1e-5 * np.abs(want).max()
+
+
+def test_qmf32_pre_twiddle_is_the_reference_table():
+    """qmf32_pre_twiddle (SynthesisFilterbank32.java:5-38) is carried verbatim; it is (cos, -sin) of
+    pi(2k+1)/256 to within an ulp."""
+    import re
+    src = (Path(__file__).resolve().parents[1] / "jaadec_amd/csrc/tables/jaad_sbr_tables.inc").read_text()
+    body = re.search(r"JAAD_QMF32_PRE_TWIDDLE\[32\]\[2\] = \{(.*?)\};", src, re.S).group(1)
+    t = np.array([float.fromhex(x.strip().rstrip("f")) for x in re.findall(r"-?0x[0-9a-fA-Fp+\-.]+f", body)],
+                 np.float32).reshape(32, 2)
+    ph = np.pi * (2 * np.arange(32) + 1) / 256
+    want = np.stack([np.cos(ph), -np.sin(ph)], 1).astype(np.float32)
+    d = np.abs(t.view(np.int32).astype(np.int64) - want.view(np.int32).astype(np.int64))
+    assert d.max() <= 1
 
 
 def test_dct4_kernel_is_a_linear_map_of_its_inputs():

@@ -67,7 +67,17 @@ SBR_TABLES = [
     ("sbr/FBT.java", "stopMinTable", "JAAD_SBR_STOP_MIN", "i32"),
     ("sbr/FBT.java", "STOP_OFFSET_TABLE", "JAAD_SBR_STOP_OFFSET", "i32_2d"),
     ("sbr/FBT.java", "limiterBandsCompare", "JAAD_SBR_LIMITER_COMPARE", "f32"),
+    ("sbr/SynthesisFilterbank32.java", "qmf32_pre_twiddle", "JAAD_QMF32_PRE_TWIDDLE", "f32x2"),
 ]
+
+# The downsampled synthesis's 32-point DCT-IV / DST-IV (A/sbr/SynthesisFilterbank32.java
+# DCT4_32 / DST4_32) are generated straight-line binary32 code.  They are carried as DATA too: an
+# op list per transform over one register file -- slots 0..31 = the in/out array (the reference
+# calls both in place: DCT4_32(x1, x1)), slot 32 + k = temporary f<k> -- each op
+# {kind, dst, a, b}: kind 0 = r[a] - r[b], 1 = r[a] + r[b], 2 = K * r[a] with K the op's constant.
+# The oracle interprets the list; the GPU kernel unrolls it at compile time.
+DCT32_OUT = OUT.with_name("jaad_sbr_dct32.inc")
+DCT32_PROGS = [("DCT4_32", "JAAD_SBR_DCT4_32"), ("DST4_32", "JAAD_SBR_DST4_32")]
 
 # PS (HE-AAC v2) tables -> jaad_ps_tables.inc (f32_flat: all numbers of a nested array, in order)
 PS_OUT = OUT.with_name("jaad_ps_tables.inc")
@@ -219,7 +229,79 @@ def main() -> int:
     emit(SBR_TABLES, SBR_OUT)
     emit(PS_TABLES, PS_OUT)
     emit(HUFF_TABLES, HUFF_OUT)
+    emit_dct32()
     return 0
+
+
+def _method_body(src: str, name: str) -> str:
+    m = re.search(r"\b" + name + r"\s*\(\s*float\[\]\s*y\s*,\s*float\[\]\s*x\s*\)\s*\{", src)
+    if not m:
+        raise KeyError(name)
+    depth, i = 0, m.end() - 1
+    for j in range(i, len(src)):
+        depth += src[j] == "{"
+        depth -= src[j] == "}"
+        if depth == 0:
+            return src[i + 1:j]
+    raise ValueError("unterminated " + name)
+
+
+def dct32_program(body: str):
+    """(ops, constants) of one straight-line transform: statements `dst = a-b | a+b | (c*a)`."""
+    def slot(tok: str) -> int:
+        tok = tok.strip()
+        m = re.fullmatch(r"([xy])\[(\d+)\]", tok)
+        if m:
+            return int(m.group(2))
+        m = re.fullmatch(r"f(\d+)", tok)
+        if m:
+            return 32 + int(m.group(1))
+        raise ValueError(tok)
+
+    ops, ks = [], []
+    for stmt in body.split(";"):
+        stmt = stmt.strip()
+        if not stmt or stmt.startswith("float"):
+            continue
+        dst, expr = (t.strip() for t in stmt.split("=", 1))
+        m = re.fullmatch(r"\(\s*(-?[0-9.]+f?)\s*\*\s*(\w+(?:\[\d+\])?)\s*\)", expr)
+        if m:
+            ops.append((2, slot(dst), slot(m.group(2)), 0))
+            ks.append(f32_from_decimal(m.group(1)))
+            continue
+        m = re.fullmatch(r"(\w+(?:\[\d+\])?)\s*([-+])\s*(\w+(?:\[\d+\])?)", expr)
+        if not m:
+            raise ValueError(stmt)
+        ops.append((0 if m.group(2) == "-" else 1, slot(dst), slot(m.group(1)), slot(m.group(3))))
+        ks.append(np.float32(0.0))
+    return ops, ks
+
+
+def emit_dct32() -> None:
+    src = strip_comments((REF / "sbr/SynthesisFilterbank32.java").read_text())
+    out = ["/* GENERATED by tools/extract_tables.py -- the downsampled SBR synthesis's 32-point",
+           " * DCT-IV / DST-IV (A/sbr/SynthesisFilterbank32.java DCT4_32, DST4_32) as op lists:",
+           " * {kind, dst, a, b} over registers 0..31 (in/out array) and 32+k (temporary f<k>);",
+           " * kind 0: r[a] - r[b], 1: r[a] + r[b], 2: K[i] * r[a].  Do not edit.",
+           " * A C++ includer may define JAAD_DCT32_TABLE as `static constexpr` (compile-time use). */",
+           "#pragma once", "#ifndef JAAD_DCT32_TABLE", "#define JAAD_DCT32_TABLE static const", "#endif", ""]
+    for jname, cname in DCT32_PROGS:
+        ops, ks = dct32_program(_method_body(src, jname))
+        nreg = 1 + max(max(o[1], o[2], o[3]) for o in ops)
+        out.append(f"#define {cname}_NOPS {len(ops)}")
+        out.append(f"#define {cname}_NREG {nreg}")
+        out.append(f"JAAD_DCT32_TABLE unsigned short {cname}_OPS[{len(ops)}][4] = {{")
+        for i in range(0, len(ops), 6):
+            out.append("  " + ", ".join("{%d, %d, %d, %d}" % o for o in ops[i:i + 6]) + ",")
+        out.append("};")
+        out.append(f"JAAD_DCT32_TABLE float {cname}_K[{len(ops)}] = {{")
+        for i in range(0, len(ks), 6):
+            out.append("  " + ", ".join(hexf(v) for v in ks[i:i + 6]) + ",")
+        out.append("};")
+        out.append(f"/* from sbr/SynthesisFilterbank32.java:{jname} */")
+        out.append("")
+    DCT32_OUT.write_text("\n".join(out) + "\n")
+    print("wrote", DCT32_OUT, len(out), "lines")
 
 
 def emit(tables, path: Path) -> None:
