@@ -147,6 +147,19 @@ private:
 // H2D copy, kernels and D2H copy overlap on three streams; pageable caller memory goes through
 // kStageSlots page-locked staging slots per direction.
 constexpr int kMaxPieces = 8, kStageSlots = 2;
+constexpr int kMaxElements = 8;
+
+// Channel elements of the AAC-LC channel configurations 3..7 (ISO/IEC 14496-3 Table 1.19: C, L/R,
+// surrounds, LFE), channels per element; returns the element count (0: not a multichannel config)
+int mc_elements(int channel_config, uint8_t* nch)
+{
+    static const uint8_t kLayouts[5][6] = {{1, 2}, {1, 2, 1}, {1, 2, 2}, {1, 2, 2, 1}, {1, 2, 2, 2, 1}};
+    static const int kCount[5] = {2, 3, 3, 4, 5};
+    if (channel_config < 3 || channel_config > 7) return 0;
+    const int k = channel_config - 3;
+    for (int i = 0; i < kCount[k]; i++) nch[i] = kLayouts[k][i];
+    return kCount[k];
+}
 constexpr uint32_t kMinPieceFrames = 4096;
 
 // One call's SBR/PS parameter records: built on the host straight into page-locked staging,
@@ -167,7 +180,12 @@ struct RecSet {
 struct jaad_ctx {
     jaad_stream_cfg cfg{};
     int device = 0;
-    int nch = 2;
+    int nch = 2;                 // channel-frame records per frame (a multichannel config: all channels)
+    // channel elements of a frame, in bitstream order (SyntacticElements.process,
+    // A/syntax/SyntacticElements.java:235-248): 1 = SCE/LFE, 2 = CPE; one element for channel
+    // configurations 1 and 2
+    int n_elem = 1, n_cpe = 0;
+    uint8_t elem_nch[kMaxElements] = {};
     uint32_t n_slots = 0;
     hipStream_t stream = nullptr;
     float* d_state[2] = {nullptr, nullptr};  // [slot][2][1024], double-buffered (see plan())
@@ -217,7 +235,7 @@ struct jaad_ctx {
     DevBuf d_xps, d_xhl, d_xhr, d_pg, d_hb;
     std::vector<uint32_t> ps_runs;
     // ---- host-buffer entry (jaad_decode_batch), set up on its first call ----
-    hipStream_t h2d = nullptr, d2h = nullptr;      // copy streams beside `stream`
+    hipStream_t h2d = nullptr, d2h = nullptr;      // copy streams beside `stream` (one DMA engine each)
     hipEvent_t ev_in[kMaxPieces] = {}, ev_k[kMaxPieces] = {}, ev_out[kMaxPieces] = {};
     PinnedBuf stage_in[kStageSlots], stage_out[kStageSlots];
     std::unique_ptr<WorkerPool> io;                // validation / staging copies
@@ -318,7 +336,9 @@ int validate_cfg(const jaad_stream_cfg* cfg)
     if (cfg->abi_version != JAAD_ABI_VERSION) return JAAD_ERR_ABI;
     if (cfg->profile != 2) return JAAD_ERR_UNSUPPORTED;  // Profile.AAC_LC (A/Profile.java)
     if (cfg->sf_index > 11) return JAAD_ERR_UNSUPPORTED;
-    if (cfg->channel_config != 1 && cfg->channel_config != 2) return JAAD_ERR_UNSUPPORTED;
+    if (cfg->channel_config < 1 || cfg->channel_config > 7) return JAAD_ERR_UNSUPPORTED;
+    // multichannel: AAC-LC elements only (SBR/PS of multichannel streams are not decoded here)
+    if (cfg->channel_config > 2 && (cfg->sbr || cfg->ps)) return JAAD_ERR_UNSUPPORTED;
     if (cfg->tns_mode > JAAD_TNS_SPEC) return JAAD_ERR_INVALID_ARG;
     if (cfg->sbr > 1 || cfg->ps > 1) return JAAD_ERR_UNSUPPORTED;
     if (cfg->ps && (!cfg->sbr || cfg->channel_config != 1)) return JAAD_ERR_UNSUPPORTED;
@@ -846,15 +866,49 @@ int launch_work(jaad_ctx* ctx, const jaad_batch* db, void* pcm, uint32_t flags, 
     a.state_in = ctx->d_state[ctx->parity];
     a.state_out = ctx->d_state[ctx->parity ^ 1];
     const bool sbr = ctx->cfg.sbr != 0;
-    if (sbr) HIPCHK(ctx->d_time.ensure((size_t)db->n_frames * ctx->nch * 1024 * sizeof(float) + 256));
+    if (sbr || ctx->n_elem > 1)
+        HIPCHK(ctx->d_time.ensure((size_t)db->n_frames * ctx->nch * 1024 * sizeof(float) + 256));
     a.pcm = sbr ? ctx->d_time.p : pcm;
     a.n_chunks = (uint32_t)ctx->chunks.size();
     a.nch = (uint32_t)ctx->nch;
+    a.cf_stride = (uint32_t)ctx->nch;
+    a.ms_stride = 1;
     a.out_mode = sbr ? kOutPlanarF32 : flags;
     a.tns_mode = ctx->cfg.tns_mode;
     a.dbg = ctx->dbg;
     a.dbg_frame = ctx->dbg_frame;
     if (a.n_chunks == 0) return JAAD_OK;
+    if (ctx->n_elem > 1) {
+        // Multichannel: each element decodes from its own channel-frame columns (stride = all
+        // channels) and its own state region into planar f32 columns; one pack pass then
+        // interleaves the channels in element order (SampleBuffer.accept, S/SampleBuffer.java:187-207)
+        const bool tns_spec = ctx->cfg.tns_mode == JAAD_TNS_SPEC && db->tns != nullptr;
+        int ch0 = 0, cpe = 0;
+        for (int k = 0; k < ctx->n_elem; k++) {
+            KernelArgs e = a;
+            const int n = ctx->elem_nch[k];
+            e.q = db->q + (size_t)ch0 * 1024;
+            e.sf = db->sf + (size_t)ch0 * 128;
+            e.cb = db->cb + (size_t)ch0 * 128;
+            e.ics = db->ics + ch0;
+            e.tns = db->tns ? db->tns + ch0 : nullptr;
+            e.ms_used = n == 2 && db->ms_used ? db->ms_used + 2 * cpe : nullptr;
+            e.ms_stride = (uint32_t)ctx->n_cpe;
+            e.nch = (uint32_t)n;
+            const size_t region = (size_t)k * ctx->n_slots * 2048;
+            e.state_in = a.state_in + region;
+            e.state_out = a.state_out + region;
+            e.pcm = static_cast<float*>(ctx->d_time.p) + (size_t)ch0 * 1024;
+            e.out_mode = kOutPlanarF32;
+            if ((rc = carry_untouched(ctx, e.state_out, e.state_in, 2048, stream))) return rc;
+            HIPCHK(launch_lc(e, stream, tns_spec));
+            ch0 += n;
+            cpe += n == 2;
+        }
+        HIPCHK(launch_pack(static_cast<const float*>(ctx->d_time.p), pcm, db->n_frames, ctx->nch, flags, stream));
+        ctx->parity ^= 1;
+        return JAAD_OK;
+    }
     rc = carry_untouched(ctx, a.state_out, a.state_in, 2048, stream);
     if (rc) return rc;
     const bool tns_spec = ctx->cfg.tns_mode == JAAD_TNS_SPEC && db->tns != nullptr;
@@ -889,8 +943,10 @@ int jaad_cfg_sample_length(const jaad_stream_cfg* cfg)
 
 int jaad_cfg_channel_count(const jaad_stream_cfg* cfg)
 {
-    (void)cfg;
-    return 2;  // mono is duplicated while sbrEnabled (A/DecoderConfig.java:108-115)
+    // mono is duplicated while sbrEnabled (A/DecoderConfig.java:108-115); configurations 3..7 carry
+    // 3, 4, 5, 6 (5.1) and 8 (7.1) channels (ChannelConfiguration, A/ChannelConfiguration.java)
+    if (cfg && cfg->channel_config >= 3 && cfg->channel_config <= 7) return cfg->channel_config == 7 ? 8 : cfg->channel_config;
+    return 2;
 }
 
 size_t jaad_frame_pcm_bytes(const jaad_stream_cfg* cfg, uint32_t flags)
@@ -950,6 +1006,17 @@ int jaad_ctx_create(const jaad_stream_cfg* cfg, uint32_t n_slots, int device, ja
     ctx->cfg = *cfg;
     ctx->device = device;
     ctx->nch = cfg->channel_config == 2 ? 2 : 1;
+    ctx->n_cpe = ctx->nch == 2;
+    ctx->elem_nch[0] = (uint8_t)ctx->nch;
+    if (const int ne = mc_elements(cfg->channel_config, ctx->elem_nch)) {
+        ctx->n_elem = ne;
+        ctx->nch = 0;
+        ctx->n_cpe = 0;
+        for (int k = 0; k < ne; k++) {
+            ctx->nch += ctx->elem_nch[k];
+            ctx->n_cpe += ctx->elem_nch[k] == 2;
+        }
+    }
     ctx->n_slots = n_slots;
     ctx->n_cu = prop.multiProcessorCount;
     ctx->slot_used.assign(n_slots, 0);
@@ -965,7 +1032,7 @@ int jaad_ctx_create(const jaad_stream_cfg* cfg, uint32_t n_slots, int device, ja
     if ((e = hipEventCreateWithFlags(&ctx->done, hipEventDisableTiming)) != hipSuccess) return bail(e, "hipEventCreate");
     if ((e = hipEventCreateWithFlags(&ctx->chunks_copied, hipEventDisableTiming)) != hipSuccess)
         return bail(e, "hipEventCreate");
-    size_t sbytes = (size_t)n_slots * 2048 * sizeof(float);
+    size_t sbytes = (size_t)ctx->n_elem * n_slots * 2048 * sizeof(float);  // [element][slot][2][1024]
     for (int i = 0; i < 2; i++) {
         if ((e = hipMalloc(&ctx->d_state[i], sbytes)) != hipSuccess) return bail(e, "hipMalloc state");
         if ((e = hipMemset(ctx->d_state[i], 0, sbytes)) != hipSuccess) return bail(e, "hipMemset state");
@@ -1093,7 +1160,7 @@ static int check_batch(const jaad_ctx* ctx, const jaad_batch* b, size_t pcm_byte
 {
     if (!ctx || !b) return JAAD_ERR_INVALID_ARG;
     if (b->n_frames && (!b->q || !b->sf || !b->cb || !b->ics)) return JAAD_ERR_INVALID_ARG;
-    if (ctx->nch == 2 && b->n_frames && !b->ms_used) return JAAD_ERR_INVALID_ARG;
+    if (ctx->n_cpe && b->n_frames && !b->ms_used) return JAAD_ERR_INVALID_ARG;
     if (ctx->cfg.sbr && b->n_frames && !b->sbr) return JAAD_ERR_INVALID_ARG;
     if (pcm_bytes < pcm_bytes_per_frame(ctx, flags) * b->n_frames) return JAAD_ERR_INVALID_ARG;
     if (flags & ~(uint32_t)(JAAD_PCM_LITTLE_ENDIAN | JAAD_PCM_FLOAT32)) return JAAD_ERR_INVALID_ARG;
@@ -1196,7 +1263,8 @@ static int decode_batch_serial(jaad_ctx* ctx, const jaad_batch* b, void* pcm_out
     // one staging allocation, 256-B aligned sub-buffers
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     size_t o_q = 0, o_sf = al(o_q + ncf * 2048), o_cb = al(o_sf + ncf * 128), o_ics = al(o_cb + ncf * 128);
-    size_t o_ms = al(o_ics + ncf * sizeof(jaad_ics_info)), o_tns = al(o_ms + nf * 16);
+    const size_t ms_bytes = nf * 16 * (size_t)std::max(ctx->n_cpe, 1);
+    size_t o_ms = al(o_ics + ncf * sizeof(jaad_ics_info)), o_tns = al(o_ms + ms_bytes);
     size_t total = al(o_tns + (b->tns ? ncf * sizeof(jaad_tns) : 0));
     HIPCHK(ctx->d_batch.ensure(total + 256));
     size_t pbytes = pcm_bytes_per_frame(ctx, flags) * nf;
@@ -1208,7 +1276,7 @@ static int decode_batch_serial(jaad_ctx* ctx, const jaad_batch* b, void* pcm_out
         HIPCHK(hipMemcpyAsync(base + o_sf, b->sf, ncf * 128, hipMemcpyHostToDevice, s));
         HIPCHK(hipMemcpyAsync(base + o_cb, b->cb, ncf * 128, hipMemcpyHostToDevice, s));
         HIPCHK(hipMemcpyAsync(base + o_ics, b->ics, ncf * sizeof(jaad_ics_info), hipMemcpyHostToDevice, s));
-        if (b->ms_used) HIPCHK(hipMemcpyAsync(base + o_ms, b->ms_used, nf * 16, hipMemcpyHostToDevice, s));
+        if (b->ms_used) HIPCHK(hipMemcpyAsync(base + o_ms, b->ms_used, ms_bytes, hipMemcpyHostToDevice, s));
         if (b->tns) HIPCHK(hipMemcpyAsync(base + o_tns, b->tns, ncf * sizeof(jaad_tns), hipMemcpyHostToDevice, s));
     }
     jaad_batch db = *b;
@@ -1286,6 +1354,8 @@ static int decode_batch_pieces(jaad_ctx* ctx, const jaad_batch* b, void* pcm_out
     a.state_out = ctx->d_state[ctx->parity ^ 1];
     a.pcm = dpcm;
     a.nch = (uint32_t)nch;
+    a.cf_stride = (uint32_t)nch;
+    a.ms_stride = 1;
     a.out_mode = flags;
     a.tns_mode = ctx->cfg.tns_mode;
     a.dbg = ctx->dbg;
@@ -1321,10 +1391,40 @@ static int decode_batch_pieces(jaad_ctx* ctx, const jaad_batch* b, void* pcm_out
         io.run([&](int t) { std::memcpy(dst + n * t / W, src + n * t / W, n * (t + 1) / W - n * t / W); });
         return JAAD_OK;
     };
+    // H2D of piece i on the one H2D copy stream (a second H2D stream shared a DMA engine with the
+    // D2H stream and serialised them: C2 e2e 9.4e6 -> 6.5e6 frames/s, profiles/round3_e2e_*)
+    auto h2d = [&](int i, const char* st) -> int {
+        const size_t f0 = F[i], nfi = F[i + 1] - f0, c0 = f0 * nch, nci = nfi * nch;
+        const char* src_q = pin_q ? (const char*)(b->q + c0 * 1024) : st + s_q;
+        hipStream_t h = ctx->h2d;
+        HIPCHK(hipMemcpyAsync(base + o_q + c0 * 2048, src_q, nci * 2048, hipMemcpyHostToDevice, h));
+        const char* src_sf = pin_rest ? (const char*)(b->sf + c0 * 128) : st + s_sf;
+        const char* src_cb = pin_rest ? (const char*)(b->cb + c0 * 128) : st + s_cb;
+        const char* src_ics = pin_rest ? (const char*)(b->ics + c0) : st + s_ics;
+        HIPCHK(hipMemcpyAsync(base + o_sf + c0 * 128, src_sf, nci * 128, hipMemcpyHostToDevice, h));
+        HIPCHK(hipMemcpyAsync(base + o_cb + c0 * 128, src_cb, nci * 128, hipMemcpyHostToDevice, h));
+        HIPCHK(hipMemcpyAsync(base + o_ics + c0 * sizeof(jaad_ics_info), src_ics, nci * sizeof(jaad_ics_info),
+                              hipMemcpyHostToDevice, h));
+        if (b->ms_used)
+            HIPCHK(hipMemcpyAsync(base + o_ms + f0 * 16, pin_rest ? (const char*)(b->ms_used + f0 * 2) : st + s_ms, nfi * 16,
+                                  hipMemcpyHostToDevice, h));
+        if (b->tns)
+            HIPCHK(hipMemcpyAsync(base + o_tns + c0 * sizeof(jaad_tns), pin_rest ? (const char*)(b->tns + c0) : st + s_tns,
+                                  nci * sizeof(jaad_tns), hipMemcpyHostToDevice, h));
+        HIPCHK(hipEventRecord(ctx->ev_in[i], h));
+        return JAAD_OK;
+    };
+    // every input pinned: a piece's copies are queued one piece ahead of its checks, which run while
+    // they fly (its kernel is queued once they passed).  Only one piece ahead: copies are served in
+    // submission order, so queueing every H2D first would hold the D2H copies back behind them.
+    const bool pinned_in = pin_q && pin_rest;
+    if (pinned_in && (rc = h2d(0, nullptr))) return rc;
     for (int i = 0; i < P && !bad; i++) {
+        if (pinned_in && i + 1 < P && (rc = h2d(i + 1, nullptr))) return rc;
         const size_t f0 = F[i], nfi = F[i + 1] - f0, c0 = f0 * nch, nci = nfi * nch;
         char* st = static_cast<char*>(ctx->stage_in[i % kStageSlots].p);
-        if (i >= kStageSlots && s_total) HIPCHK(hipEventSynchronize(ctx->ev_in[i - kStageSlots]));
+        if (i >= kStageSlots && s_total)  // the staging slot's previous piece has been copied
+            HIPCHK(hipEventSynchronize(ctx->ev_in[i - kStageSlots]));
         // validate (and stage) the piece on the workers
         io.run([&](int t) {
             const size_t a0 = nci * t / W, a1 = nci * (t + 1) / W;
@@ -1342,23 +1442,7 @@ static int decode_batch_pieces(jaad_ctx* ctx, const jaad_batch* b, void* pcm_out
             }
         });
         if (bad) break;
-        hipStream_t h = ctx->h2d;
-        HIPCHK(hipMemcpyAsync(base + o_q + c0 * 2048, pin_q ? (const void*)(b->q + c0 * 1024) : st + s_q, nci * 2048,
-                              hipMemcpyHostToDevice, h));
-        const char* src_sf = pin_rest ? (const char*)(b->sf + c0 * 128) : st + s_sf;
-        const char* src_cb = pin_rest ? (const char*)(b->cb + c0 * 128) : st + s_cb;
-        const char* src_ics = pin_rest ? (const char*)(b->ics + c0) : st + s_ics;
-        HIPCHK(hipMemcpyAsync(base + o_sf + c0 * 128, src_sf, nci * 128, hipMemcpyHostToDevice, h));
-        HIPCHK(hipMemcpyAsync(base + o_cb + c0 * 128, src_cb, nci * 128, hipMemcpyHostToDevice, h));
-        HIPCHK(hipMemcpyAsync(base + o_ics + c0 * sizeof(jaad_ics_info), src_ics, nci * sizeof(jaad_ics_info),
-                              hipMemcpyHostToDevice, h));
-        if (b->ms_used)
-            HIPCHK(hipMemcpyAsync(base + o_ms + f0 * 16, pin_rest ? (const char*)(b->ms_used + f0 * 2) : st + s_ms, nfi * 16,
-                                  hipMemcpyHostToDevice, h));
-        if (b->tns)
-            HIPCHK(hipMemcpyAsync(base + o_tns + c0 * sizeof(jaad_tns), pin_rest ? (const char*)(b->tns + c0) : st + s_tns,
-                                  nci * sizeof(jaad_tns), hipMemcpyHostToDevice, h));
-        HIPCHK(hipEventRecord(ctx->ev_in[i], h));
+        if (!pinned_in && (rc = h2d(i, st))) return rc;
         HIPCHK(hipStreamWaitEvent(s, ctx->ev_in[i], 0));
         a.chunks = static_cast<const ChunkDesc*>(ctx->d_chunks.p) + C[i];
         a.n_chunks = C[i + 1] - C[i];
@@ -1375,6 +1459,7 @@ static int decode_batch_pieces(jaad_ctx* ctx, const jaad_batch* b, void* pcm_out
         for (int i = std::max(0, queued - kStageSlots); i < queued; i++)
             if ((rc = copy_out(i))) return rc;
     HIPCHK(hipStreamSynchronize(ctx->d2h));
+    HIPCHK(hipStreamSynchronize(ctx->h2d));
     HIPCHK(hipStreamSynchronize(s));
     HIPCHK(hipEventRecord(ctx->done, s));
     ctx->done_live = true;
@@ -1391,7 +1476,7 @@ int jaad_decode_batch(jaad_ctx* ctx, const jaad_batch* b, void* pcm_out, size_t 
     if (!pcm_out && b->n_frames) return JAAD_ERR_INVALID_ARG;
     HIPCHK(hipSetDevice(ctx->device));
     if ((rc = io_setup(ctx))) return rc;
-    if (ctx->cfg.sbr || b->n_frames < 2 * kMinPieceFrames || !b->stream_slot || !b->frame_begin)
+    if (ctx->cfg.sbr || ctx->n_elem > 1 || b->n_frames < 2 * kMinPieceFrames || !b->stream_slot || !b->frame_begin)
         return decode_batch_serial(ctx, b, pcm_out, flags);
     // the run layout is checked by plan(); pieces need it sane before cutting
     if (b->frame_begin[0] != 0 || b->frame_begin[b->n_runs] != b->n_frames) return JAAD_ERR_INVALID_ARG;
@@ -1448,7 +1533,7 @@ int jaad_ctx_core_channels(const jaad_ctx* ctx) { return ctx ? ctx->nch : JAAD_E
 size_t jaad_state_bytes(const jaad_ctx* ctx)
 {
     if (!ctx) return 0;
-    return 2048 * sizeof(float) + (ctx->cfg.sbr ? 2 * sizeof(SbrChState) + sizeof(SbrHostSlot) : 0) +
+    return (size_t)ctx->n_elem * 2048 * sizeof(float) + (ctx->cfg.sbr ? 2 * sizeof(SbrChState) + sizeof(SbrHostSlot) : 0) +
            (ctx->cfg.ps ? sizeof(PsState) : 0);
 }
 
@@ -1458,7 +1543,9 @@ int jaad_state_export(jaad_ctx* ctx, uint32_t slot, void* buf, size_t bytes)
     int rc = sync_ctx(ctx);
     if (rc) return rc;
     char* o = static_cast<char*>(buf);
-    HIPCHK(hipMemcpy(o, ctx->d_state[ctx->parity] + (size_t)slot * 2048, 2048 * sizeof(float), hipMemcpyDeviceToHost));
+    for (int k = 0; k < ctx->n_elem; k++)  // one overlap record per channel element
+        HIPCHK(hipMemcpy(o + (size_t)k * 2048 * sizeof(float), ctx->d_state[ctx->parity] + ((size_t)k * ctx->n_slots + slot) * 2048,
+                         2048 * sizeof(float), hipMemcpyDeviceToHost));
     if (ctx->cfg.sbr) {
         o += 2048 * sizeof(float);
         HIPCHK(hipMemcpy(o, ctx->d_sbr_state + (size_t)slot * 2, 2 * sizeof(SbrChState), hipMemcpyDeviceToHost));
@@ -1476,13 +1563,15 @@ int jaad_state_import(jaad_ctx* ctx, uint32_t slot, const void* buf, size_t byte
     int rc = sync_ctx(ctx);
     if (rc) return rc;
     const char* in = static_cast<const char*>(buf);
-    {  // the overlap must be finite (the LC kernel's PCM rounding relies on it, jaad_lc.hip round_pk16)
+    for (int k = 0; k < ctx->n_elem; k++) {  // the overlap must be finite (the LC kernel's PCM rounding relies on it, jaad_lc.hip round_pk16)
         float ov[2048];
-        std::memcpy(ov, in, sizeof ov);
+        std::memcpy(ov, in + (size_t)k * sizeof ov, sizeof ov);
         for (float v : ov)
             if (!std::isfinite(v)) return JAAD_ERR_INVALID_ARG;
     }
-    HIPCHK(hipMemcpy(ctx->d_state[ctx->parity] + (size_t)slot * 2048, in, 2048 * sizeof(float), hipMemcpyHostToDevice));
+    for (int k = 0; k < ctx->n_elem; k++)
+        HIPCHK(hipMemcpy(ctx->d_state[ctx->parity] + ((size_t)k * ctx->n_slots + slot) * 2048, in + (size_t)k * 2048 * sizeof(float),
+                         2048 * sizeof(float), hipMemcpyHostToDevice));
     if (ctx->cfg.sbr) {
         in += 2048 * sizeof(float);
         SbrHostSlot hs;
@@ -1505,7 +1594,8 @@ int jaad_state_reset(jaad_ctx* ctx, uint32_t slot)
     if (!ctx || slot >= ctx->n_slots) return JAAD_ERR_INVALID_ARG;
     int rc = sync_ctx(ctx);
     if (rc) return rc;
-    HIPCHK(hipMemset(ctx->d_state[ctx->parity] + (size_t)slot * 2048, 0, 2048 * sizeof(float)));
+    for (int k = 0; k < ctx->n_elem; k++)
+        HIPCHK(hipMemset(ctx->d_state[ctx->parity] + ((size_t)k * ctx->n_slots + slot) * 2048, 0, 2048 * sizeof(float)));
     if (ctx->cfg.sbr) {
         HIPCHK(hipMemset(ctx->d_sbr_state + (size_t)slot * 2, 0, 2 * sizeof(SbrChState)));
         SbrHost::reset_slot(ctx->sbr_slots[slot]);

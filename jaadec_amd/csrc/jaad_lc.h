@@ -67,6 +67,10 @@ struct KernelArgs {
     void* pcm;                  // frame-major output
     uint32_t n_chunks;
     uint32_t nch;               // 1 (SCE) or 2 (CPE)
+    uint32_t cf_stride;         // channel-frame records per frame in q/sf/cb/ics/tns (nch; a
+                                // multichannel batch: all its channels, the pointers offset to
+                                // this element's first channel)
+    uint32_t ms_stride;         // ms_used pairs per frame (1; multichannel: the CPE count)
     uint32_t out_mode;          // JAAD_PCM_* flags, or kOutPlanarF32 (SBR input: float [ch-frame][1024])
     uint32_t tns_mode;          // JAAD_TNS_*
     float* dbg;                 // internal: stage dump of frame dbg_frame of chunk 0 (or null)
@@ -98,6 +102,10 @@ constexpr uint32_t kOutPlanarF32 = 4;  // internal output mode: core time sample
 
 // one wave per chunk (grid derived from a.n_chunks)
 hipError_t launch_lc(const KernelArgs& a, hipStream_t stream, bool tns_spec);
+// SampleBuffer.accept for a multichannel frame: planar f32 [frame][n_ch][1024] -> n_ch
+// interleaved samples per instant (int16 BE/LE after Math.round + clamp, or f32; JAAD_PCM_*)
+hipError_t launch_pack(const float* planar, void* pcm, uint32_t n_frames, int n_ch, uint32_t flags,
+                       hipStream_t stream);
 // LC kernel waves that can be resident on one CU (occupancy query; 0 on failure)
 int lc_resident_waves_per_cu(bool tns_spec);
 }

@@ -799,15 +799,15 @@ __device__ __forceinline__ void prefetch(const KernelArgs& A, int f, bool stereo
 #pragma unroll
     for (int c = 0; c < 2; c++) {
         if (c == 1 && !stereo) break;
-        const size_t cf = (size_t)f * nch + c;
+        const size_t cf = (size_t)f * A.cf_stride + c;
         const v4i* q = reinterpret_cast<const v4i*>(A.q + cf * 1024);
         pf.q[c][0] = __builtin_nontemporal_load(q + u);
         pf.q[c][1] = __builtin_nontemporal_load(q + 64 + u);
         const uint32_t* row = reinterpret_cast<const uint32_t*>(u < 32 ? A.sf + cf * 128 : A.cb + cf * 128);
         pf.sfcb[c] = row[u & 31];
     }
-    const uint32_t* side = u < 8 ? reinterpret_cast<const uint32_t*>(A.ics + (size_t)f * nch) + (u < 4 * nch ? u : 0)
-                                 : (A.ms_used ? reinterpret_cast<const uint32_t*>(A.ms_used + (size_t)f * 2) + (u & 3)
+    const uint32_t* side = u < 8 ? reinterpret_cast<const uint32_t*>(A.ics + (size_t)f * A.cf_stride) + (u < 4 * nch ? u : 0)
+                                 : (A.ms_used ? reinterpret_cast<const uint32_t*>(A.ms_used + (size_t)f * 2 * A.ms_stride) + (u & 3)
                                               : reinterpret_cast<const uint32_t*>(A.ics));
     pf.side = *side;
 }
@@ -987,7 +987,7 @@ __global__ __launch_bounds__(64 * waves_per_wg<kTnsSpec>()) void lc_decode_kerne
             const int u = lane_id();
             const int f = f_first + it;
             const bool emit = f >= (int)cd.frame0;
-            const size_t cf0 = (size_t)f * nch;
+            const size_t cf0 = (size_t)f * A.cf_stride;
             const Prefetch cur = pf;
 
             // ---------------- side info ----------------
@@ -1259,6 +1259,38 @@ static hipError_t launch_lc_ch(const KernelArgs& a, hipStream_t stream, bool tns
         else JAAD_LAUNCH(false, JAAD_PCM_BIG_ENDIAN);
     }
 #undef JAAD_LAUNCH
+    return hipGetLastError();
+}
+
+namespace {
+// one thread per (frame, sample instant): its n_ch planar samples -> n_ch interleaved outputs
+__global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ planar, void* __restrict__ pcm,
+                                                   uint32_t n_frames, int n_ch, uint32_t flags)
+{
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;  // frame * 1024 + sample
+    if (i >= (size_t)n_frames * 1024) return;
+    const size_t f = i >> 10, n = i & 1023;
+    const float* src = planar + f * (size_t)n_ch * 1024 + n;
+    if (flags & JAAD_PCM_FLOAT32) {
+        float* o = reinterpret_cast<float*>(pcm) + i * n_ch;
+        for (int c = 0; c < n_ch; c++) o[c] = src[(size_t)c * 1024];
+        return;
+    }
+    uint16_t* o = reinterpret_cast<uint16_t*>(pcm) + i * n_ch;
+    for (int c = 0; c < n_ch; c++) {
+        uint32_t s16 = round_pk16(src[(size_t)c * 1024], 0.0f) & 0xFFFFu;  // Math.round + clamp (as the LC PCM stage)
+        if (!(flags & JAAD_PCM_LITTLE_ENDIAN)) s16 = ((s16 & 0xFF) << 8) | (s16 >> 8);
+        o[c] = (uint16_t)s16;
+    }
+}
+}  // namespace
+
+hipError_t launch_pack(const float* planar, void* pcm, uint32_t n_frames, int n_ch, uint32_t flags, hipStream_t stream)
+{
+    const size_t n = (size_t)n_frames * 1024;
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(pack_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, planar, pcm, n_frames, n_ch,
+                       flags);
     return hipGetLastError();
 }
 

@@ -475,7 +475,7 @@ int jaad_asc_parse(const uint8_t* asc, size_t bytes, jaad_stream_cfg* cfg)
         if (br.read(1)) br.skip(14);                  // dependsOnCoreCoder -> coreCoderDelay
         if (br.read(1)) br.skip(1);                   // extensionFlag -> extensionFlag3
         if (br.overrun()) return JAAD_ERR_EOS;
-        if (chc == 0) return JAAD_ERR_UNSUPPORTED;    // PCE channel layouts: not a 1/2-channel config
+        if (chc == 0) return JAAD_ERR_UNSUPPORTED;    // PCE channel layouts: no fixed element list
         // readSyncExtension (A/DecoderConfig.java:238, 260-291; sbrEnabled is always on): a
         // backward-compatible 0x2B7 extension can signal SBR (and PS, 0x548) with its output
         // rate.  Without it the output rate stays the core rate (:180): SBR met later in the
@@ -500,7 +500,8 @@ int jaad_asc_parse(const uint8_t* asc, size_t bytes, jaad_stream_cfg* cfg)
     if (br.overrun()) return JAAD_ERR_EOS;
     if (aot != 2) return JAAD_ERR_UNSUPPORTED;
     if (sfi > 11 || (cfg->sbr && cfg->ext_sf_index > 11)) return JAAD_ERR_UNSUPPORTED;
-    if (chc != 1 && chc != 2) return JAAD_ERR_UNSUPPORTED;
+    if (chc < 1 || chc > 7) return JAAD_ERR_UNSUPPORTED;
+    if (chc > 2 && cfg->sbr) return JAAD_ERR_UNSUPPORTED;  // multichannel HE-AAC: not decoded here
     cfg->profile = 2;
     cfg->sf_index = (uint8_t)sfi;
     cfg->channel_config = (uint8_t)chc;
@@ -534,7 +535,7 @@ int jaad_adts_find(const uint8_t* buf, size_t bytes, size_t* offset, jaad_adts_h
 int jaad_adts_cfg(const jaad_adts_header* h, jaad_stream_cfg* cfg)
 {
     if (!h || !cfg) return JAAD_ERR_INVALID_ARG;
-    if (h->profile != 2 || h->sf_index > 11 || (h->channel_config != 1 && h->channel_config != 2))
+    if (h->profile != 2 || h->sf_index > 11 || h->channel_config < 1 || h->channel_config > 7)
         return JAAD_ERR_UNSUPPORTED;
     std::memset(cfg, 0, sizeof *cfg);
     cfg->abi_version = JAAD_ABI_VERSION;
@@ -550,12 +551,27 @@ int jaad_parser_create(const jaad_stream_cfg* cfg, jaad_parser** out)
     if (!cfg || !out) return JAAD_ERR_INVALID_ARG;
     *out = nullptr;
     if (cfg->abi_version != JAAD_ABI_VERSION) return JAAD_ERR_ABI;
-    if (cfg->profile != 2 || (cfg->channel_config != 1 && cfg->channel_config != 2)) return JAAD_ERR_UNSUPPORTED;
+    if (cfg->profile != 2 || cfg->channel_config < 1 || cfg->channel_config > 7) return JAAD_ERR_UNSUPPORTED;
     if (cfg->ps && (!cfg->sbr || cfg->channel_config != 1)) return JAAD_ERR_UNSUPPORTED;
+    if (cfg->channel_config > 2 && cfg->sbr) return JAAD_ERR_UNSUPPORTED;  // multichannel: AAC-LC elements only
     jaad_parser* p = new (std::nothrow) jaad_parser;
     if (!p) return JAAD_ERR_NOMEM;
     p->C.cfg = *cfg;
     p->C.nch = cfg->channel_config == 2 ? 2 : 1;
+    p->C.elem_nch[0] = (uint8_t)p->C.nch;
+    {  // ISO/IEC 14496-3 Table 1.19 channel elements of configurations 3..7
+        static const uint8_t kLayouts[5][6] = {{1, 2}, {1, 2, 1}, {1, 2, 2}, {1, 2, 2, 1}, {1, 2, 2, 2, 1}};
+        static const int kCount[5] = {2, 3, 3, 4, 5};
+        if (cfg->channel_config > 2) {
+            const int k = cfg->channel_config - 3;
+            p->C.n_elem = kCount[k];
+            p->C.nch = 0;
+            for (int i = 0; i < kCount[k]; i++) {
+                p->C.elem_nch[i] = kLayouts[k][i];
+                p->C.nch += kLayouts[k][i];
+            }
+        }
+    }
     const int st = sf_counts(cfg->sf_index, p->C);
     if (st) {
         delete p;
@@ -598,11 +614,14 @@ int parse_frame(jaad_parser* p, const uint8_t* data, size_t bytes, jaad_frame_ou
 {
     if (!p || !out || (!data && bytes) || !out->q || !out->sf || !out->cb || !out->ics) return JAAD_ERR_INVALID_ARG;
     const Cfg& C = p->C;
-    if (C.nch == 2 && !out->ms_used) return JAAD_ERR_INVALID_ARG;
+    int n_cpe = 0;
+    for (int k = 0; k < C.n_elem; k++) n_cpe += C.elem_nch[k] == 2;
+    if (n_cpe && !out->ms_used) return JAAD_ERR_INVALID_ARG;
     if (C.cfg.sbr && !out->sbr) return JAAD_ERR_INVALID_ARG;
     BitReader br(data, bytes);
     ParseState ns = p->st;  // committed only when the whole frame parsed
     bool have_channels = false;
+    int elem = 0, ch0 = 0, cpe = 0;  // channel elements parsed so far, their channels, CPEs
     int sbr_seen = 0;
     if (C.cfg.sbr) std::memset(out->sbr, 0, sizeof *out->sbr);
     for (;;) {
@@ -648,16 +667,19 @@ int parse_frame(jaad_parser* p, const uint8_t* data, size_t bytes, jaad_frame_ou
             if (st) return st;
             continue;
         }
-        if (id == 2 || id == 3) return JAAD_ERR_UNSUPPORTED;  // CCE, LFE: multichannel layouts
-        // SCE (0) / CPE (1): exactly the one channel element of a mono / stereo configuration
-        if (have_channels || (id == 1) != (C.nch == 2)) return JAAD_ERR_UNSUPPORTED;
+        if (id == 2) return JAAD_ERR_UNSUPPORTED;  // CCE (coupling channels are not decoded here)
+        // SCE (0) / LFE (3) / CPE (1): the configuration's channel elements in their ISO order (one
+        // SCE or CPE for mono / stereo); LFE decodes as an SCE (A/syntax/LFE.java)
+        if (elem >= C.n_elem || (id == 1) != (C.elem_nch[elem] == 2) || (id == 3 && C.n_elem == 1))
+            return JAAD_ERR_UNSUPPORTED;
         have_channels = true;
-        if (id == 0) {
+        if (id == 0 || id == 3) {
             IcsInfo I;
-            ChOut o{out->q, out->sf, out->cb, out->ics, out->tns};
-            const int st = read_ics(br, C, false, I, ns.shape[0], ns.pns, o);
+            ChOut o{out->q + (size_t)ch0 * 1024, out->sf + ch0 * 128, out->cb + ch0 * 128, out->ics + ch0,
+                    out->tns ? out->tns + ch0 : nullptr};
+            const int st = read_ics(br, C, false, I, ns.shape[ch0], ns.pns, o);
             if (st) return st;
-            ns.shape[0] = I.shape;
+            ns.shape[ch0] = I.shape;
         } else {
             // CPE.decode (A/syntax/CPE.java:85-123)
             if (br.left() < 1) return JAAD_ERR_EOS;
@@ -683,20 +705,26 @@ int parse_frame(jaad_parser* p, const uint8_t* data, size_t bytes, jaad_frame_ou
                 }
                 ms_present = mask != 0;
             }
-            ChOut oL{out->q, out->sf, out->cb, out->ics, out->tns};
-            ChOut oR{out->q + 1024, out->sf + 128, out->cb + 128, out->ics + 1, out->tns ? out->tns + 1 : nullptr};
-            int st = read_ics(br, C, common, IL, ns.shape[0], ns.pns, oL);
+            ChOut oL{out->q + (size_t)ch0 * 1024, out->sf + ch0 * 128, out->cb + ch0 * 128, out->ics + ch0,
+                     out->tns ? out->tns + ch0 : nullptr};
+            ChOut oR{out->q + (size_t)(ch0 + 1) * 1024, out->sf + (ch0 + 1) * 128, out->cb + (ch0 + 1) * 128,
+                     out->ics + ch0 + 1, out->tns ? out->tns + ch0 + 1 : nullptr};
+            int st = read_ics(br, C, common, IL, ns.shape[ch0], ns.pns, oL);
             if (st) return st;
-            st = read_ics(br, C, common, IR, ns.shape[1], ns.pns, oR);
+            st = read_ics(br, C, common, IR, ns.shape[ch0 + 1], ns.pns, oR);
             if (st) return st;
-            ns.shape[0] = IL.shape;
-            ns.shape[1] = IR.shape;
-            if (ms_present) out->ics[0].flags |= JAAD_ICS_MS_PRESENT;
-            out->ms_used[0] = ms[0];
-            out->ms_used[1] = ms[1];
+            ns.shape[ch0] = IL.shape;
+            ns.shape[ch0 + 1] = IR.shape;
+            if (ms_present) out->ics[ch0].flags |= JAAD_ICS_MS_PRESENT;
+            out->ms_used[2 * cpe] = ms[0];
+            out->ms_used[2 * cpe + 1] = ms[1];
+            cpe++;
         }
+        ch0 += C.elem_nch[elem];
+        elem++;
     }
     if (!have_channels) return JAAD_ERR_BITSTREAM;  // a frame without audio: nothing to decode
+    if (elem != C.n_elem) return JAAD_ERR_UNSUPPORTED;  // a frame without all the configuration's elements
     if (C.cfg.sbr && !sbr_seen) {
         const int st = sbr_missing(C, ns, *out->sbr);
         if (st) return st;
@@ -723,11 +751,11 @@ int jaad_probe_sbr(const jaad_stream_cfg* cfg, const uint8_t* data, size_t bytes
     jaad_parser* p = nullptr;
     int st = jaad_parser_create(&core, &p);
     if (st) return st;
-    std::vector<int16_t> q(2048);
-    std::vector<uint8_t> sf(256), cb(256);
-    jaad_ics_info ics[2];
-    jaad_tns tns[2];
-    uint64_t ms[2];
+    std::vector<int16_t> q(8 * 1024);  // up to 8 channels (configuration 7)
+    std::vector<uint8_t> sf(8 * 128), cb(8 * 128);
+    jaad_ics_info ics[8];
+    jaad_tns tns[8];
+    uint64_t ms[8];
     jaad_frame_out o{q.data(), sf.data(), cb.data(), ics, ms, tns, nullptr};
     st = parse_frame(p, data, bytes, &o, found);
     jaad_parser_destroy(p);

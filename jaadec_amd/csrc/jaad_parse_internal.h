@@ -59,8 +59,12 @@ private:
 
 struct Cfg {
     jaad_stream_cfg cfg;
-    int nch = 1;            // channels per ch-frame record (1 SCE, 2 CPE)
+    int nch = 1;            // channel-frame records per frame (1 SCE, 2 CPE, 3..8 multichannel)
     int sf_index = 0, nswb_l = 0, nswb_s = 0;
+    // the frame's channel elements in bitstream order (1 = SCE/LFE, 2 = CPE): one for
+    // configurations 1 / 2, the ISO layout for 3..7 (jaad_capi.cpp mc_elements)
+    int n_elem = 1;
+    uint8_t elem_nch[8] = {1};
 };
 
 // SBR / PS bitstream state that persists between frames (jaad_parse_sbr.cpp): what the
@@ -97,7 +101,7 @@ struct SbrParseState {
 
 struct ParseState {
     uint32_t pns = 0x1F2E3D4Cu;  // static ICStream.randomState (A/syntax/ICStream.java:26)
-    int shape[2] = {0, 0};       // ICSInfo.windowShape[CURRENT] of the previous frame
+    int shape[8] = {0};          // ICSInfo.windowShape[CURRENT] of the previous frame, per channel
     SbrParseState sbr;
 };
 

@@ -78,7 +78,11 @@ class DecoderConfig:
                    from_asc=True)
 
     def getChannelCount(self) -> int:  # noqa: N802  (Java name)
-        return 2  # mono -> stereo while sbrEnabled (A/DecoderConfig.java:108-115)
+        # mono -> stereo while sbrEnabled (A/DecoderConfig.java:108-115); otherwise the
+        # configuration's speakers (ChannelConfiguration.forInt: 7 -> 7.1, 8 channels)
+        if self.channel_config in N.MC_ELEMENTS:
+            return 8 if self.channel_config == 7 else self.channel_config
+        return 2
 
     def getSampleLength(self) -> int:  # noqa: N802
         # A/DecoderConfig.java:83-86: doubled only by upsampling SBR (not downsampled SBR)
@@ -145,10 +149,10 @@ class SampleBuffer:
     def getBitrate(self) -> float:  # noqa: N802
         return self.bitrate
 
-    def _set(self, pcm: bytes, rate: int, sample_length: int = 1024) -> None:
-        self.data, self.sample_rate, self.channels, self.bits_per_sample = pcm, rate, 2, 16
+    def _set(self, pcm: bytes, rate: int, sample_length: int = 1024, channels: int = 2) -> None:
+        self.data, self.sample_rate, self.channels, self.bits_per_sample = pcm, rate, channels, 16
         self.length = sample_length / rate
-        self.bitrate = sample_length * 16 * 2 / len(pcm)
+        self.bitrate = sample_length * 16 * channels / len(pcm)
 
 
 class Decoder:
@@ -237,7 +241,7 @@ class Decoder:
         rate = self.config.getOutputFrequency()
         for i, buf in enumerate(buffers):
             want = buf.big_endian
-            buf._set(pcm[i].tobytes(), rate, self.config.getSampleLength())
+            buf._set(pcm[i].tobytes(), rate, self.config.getSampleLength(), self.config.getChannelCount())
             buf.big_endian = flags == N.PCM_BIG_ENDIAN
             buf.setBigEndian(want)  # no-op unless this buffer asked for the other byte order
         self.frames += batch.n_frames

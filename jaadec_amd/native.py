@@ -304,6 +304,48 @@ def cfg_for(p: SynthParams, tns_mode: int = TNS_COMPAT) -> StreamCfg:
     return make_cfg(p.sf_index, p.channel_config, tns_mode, bool(p.sbr), p.sbr == 2)
 
 
+# channel elements of the AAC-LC multichannel configurations (0 SCE, 1 CPE, 3 LFE; ISO/IEC 14496-3
+# Table 1.19), in bitstream order
+MC_ELEMENTS = {3: (0, 1), 4: (0, 1, 0), 5: (0, 1, 1), 6: (0, 1, 1, 3), 7: (0, 1, 1, 1, 3)}
+
+
+def core_channels(cfg) -> int:
+    """Channel-frame records per frame of a configuration (jaad_ctx_core_channels)."""
+    cc = cfg.channel_config
+    if cc in MC_ELEMENTS:
+        return sum(2 if e == 1 else 1 for e in MC_ELEMENTS[cc])
+    return 2 if cc == 2 else 1
+
+
+def n_cpe(cfg) -> int:
+    cc = cfg.channel_config
+    return sum(e == 1 for e in MC_ELEMENTS[cc]) if cc in MC_ELEMENTS else int(cc == 2)
+
+
+def mc_batch(elements: list, ids) -> "Batch":
+    """One multichannel batch (all channels' records per frame, element order) from per-element
+    batches of the same runs (SCE/LFE: 1 channel, CPE: 2 with ms_used)."""
+    nf = elements[0].n_frames
+    nch = sum(e.nch for e in elements)
+    cols = lambda name, w: np.concatenate([getattr(e, name).reshape(nf, e.nch, *w) for e in elements], 1)
+    q = np.ascontiguousarray(cols("q", (1024,)).reshape(nf * nch, 1024))
+    sf = np.ascontiguousarray(cols("sf", (128,)).reshape(nf * nch, 128))
+    cb = np.ascontiguousarray(cols("cb", (128,)).reshape(nf * nch, 128))
+    ics = np.ascontiguousarray(cols("ics", ()).reshape(nf * nch))
+    cpes = [e for e, i in zip(elements, ids) if i == 1]
+    ms = np.ascontiguousarray(np.concatenate([e.ms_used for e in cpes], 1)) if cpes else None
+    tns = None
+    if any(e.tns is not None for e in elements):
+        tns = np.zeros((nf, nch), TNS_DTYPE)
+        c = 0
+        for e in elements:
+            if e.tns is not None:
+                tns[:, c:c + e.nch] = e.tns.reshape(nf, e.nch)
+            c += e.nch
+        tns = tns.reshape(nf * nch)
+    return Batch(q, sf, cb, ics, ms, tns, elements[0].stream_slot.copy(), elements[0].frame_begin.copy(), nch)
+
+
 def pcm_frame_bytes(flags: int, sbr: bool = False, down: bool = False) -> int:
     return (2048 if sbr and not down else 1024) * 2 * (4 if flags & PCM_FLOAT32 else 2)
 
@@ -341,7 +383,7 @@ class Context:
     def decode(self, batch: Batch, flags: int = PCM_BIG_ENDIAN, out: np.ndarray | None = None) -> np.ndarray:
         """Host-buffer batch decode -> PCM bytes (uint8 [n_frames, frame_bytes]), into `out` when
         given (e.g. a buffer registered with register())."""
-        nb = pcm_frame_bytes(flags, bool(self.cfg.sbr), sbr_downsampled(self.cfg))
+        nb = lib().jaad_frame_pcm_bytes(C.byref(self.cfg), flags)
         if out is None:
             out = np.empty((batch.n_frames, nb), np.uint8)
         assert out.flags["C_CONTIGUOUS"] and out.nbytes >= batch.n_frames * nb
@@ -454,7 +496,7 @@ class Parser:
 
     def __init__(self, cfg: StreamCfg):
         self.cfg = cfg
-        self.nch = 2 if cfg.channel_config == 2 else 1
+        self.nch = core_channels(cfg)
         h = C.c_void_p()
         rc = lib().jaad_parser_create(C.byref(cfg), C.byref(h))
         if rc:
@@ -494,12 +536,12 @@ class Parser:
 
     def parse(self, frames: list, slot: int = 0) -> Batch:
         """raw_data_blocks (bytes) of this stream -> one-run Batch in the jaad_gpu.h layout."""
-        nf, nch = len(frames), self.nch
+        nf, nch, ncpe = len(frames), self.nch, n_cpe(self.cfg)
         q = np.zeros((nf * nch, 1024), np.int16)
         sf = np.zeros((nf * nch, 128), np.uint8)
         cb = np.zeros((nf * nch, 128), np.uint8)
         ics = np.zeros(nf * nch, ICS_DTYPE)
-        ms = np.zeros((nf, 2), np.uint64) if nch == 2 else None
+        ms = np.zeros((nf, 2 * ncpe), np.uint64) if ncpe else None
         tns = np.zeros(nf * nch, TNS_DTYPE)
         sbr = np.zeros(nf, SBR_FRAME_DTYPE) if self.cfg.sbr else None
         for i, fr in enumerate(frames):

@@ -260,6 +260,62 @@ static int put_ics(Bw* w, int sf_index, int common, const int16_t* q, const uint
 
 long jaad_sbr_fil_bits(void* state, int nch, const jaad_sbr_frame* rec, uint8_t* out, size_t cap);
 
+/* one channel element: id 0 SCE / 3 LFE (one ICS) or 1 CPE (A/syntax/CPE.java:85-123), instance tag */
+static int put_element(Bw* w, int sf_index, int id, int tag, const int16_t* q, const uint8_t* sf, const uint8_t* cb,
+                       const jaad_ics_info* ics, const uint64_t* ms_used, const jaad_tns* tns, int extras)
+{
+    put(w, (uint32_t)id, 3);
+    put(w, (uint32_t)tag, 4);
+    if (id != 1) return put_ics(w, sf_index, 0, q, sf, cb, ics, tns, extras & 2);
+    const int common = (ics[0].flags & JAAD_ICS_COMMON_WINDOW) != 0;
+    put(w, (uint32_t)common, 1);
+    if (common) {
+        Info I;
+        info_of(&ics[0], &I);
+        put_ics_info(w, &I);
+        const int nb = I.ngroups * I.max_sfb;
+        if (ics[0].flags & JAAD_ICS_MS_PRESENT) {
+            int all = 1;
+            for (int i = 0; i < nb; i++) all &= (int)((ms_used[i >> 6] >> (i & 63)) & 1);
+            if (all && nb) {
+                put(w, 2, 2);
+            } else {
+                put(w, 1, 2);
+                for (int i = 0; i < nb; i++) put(w, (uint32_t)((ms_used[i >> 6] >> (i & 63)) & 1), 1);
+            }
+        } else {
+            put(w, 0, 2);
+        }
+    }
+    if (put_ics(w, sf_index, common, q, sf, cb, &ics[0], tns, extras & 2)) return -1;
+    return put_ics(w, sf_index, common, q + 1024, sf + 128, cb + 128, &ics[1], tns ? tns + 1 : NULL, extras & 2);
+}
+
+/*
+ * One raw_data_block of a multichannel frame: the elements ids[0..n_elem) (0 SCE, 1 CPE, 3 LFE)
+ * in order over the frame's channel records (q/sf/cb/ics/tns: all channels, element k starting
+ * at the channels before it; ms_used: one pair per CPE), then END.
+ */
+long jaad_write_frame_mc(int sf_index, int n_elem, const int* ids, const int16_t* q, const uint8_t* sf,
+                         const uint8_t* cb, const jaad_ics_info* ics, const uint64_t* ms_used, const jaad_tns* tns,
+                         uint8_t* out, size_t cap)
+{
+    Bw w = {out, cap, 0, 0};
+    memset(out, 0, cap);
+    int ch = 0, cpe = 0, tags[8] = {0};
+    for (int k = 0; k < n_elem; k++) {
+        const int id = ids[k];
+        if (put_element(&w, sf_index, id, tags[id]++, q + (size_t)ch * 1024, sf + ch * 128, cb + ch * 128, ics + ch,
+                        id == 1 ? ms_used + 2 * cpe : NULL, tns ? tns + ch : NULL, 0))
+            return -1;
+        ch += id == 1 ? 2 : 1;
+        cpe += id == 1;
+    }
+    put(&w, 7, 3); /* END */
+    align(&w);
+    return w.overflow ? -1 : (long)(w.pos / 8);
+}
+
 /*
  * One raw_data_block of the frame's records (nch = 1: SCE, 2: CPE), optionally wrapped in
  * extra DSE / FIL(fill) elements (extras bit 0) and carrying pulse data (bit 1); with `sbr`
@@ -281,37 +337,7 @@ long jaad_write_frame_sbr(int sf_index, int nch, const int16_t* q, const uint8_t
         align(&w);
         put(&w, 0xABCDEF, 24);
     }
-    if (nch == 1) {
-        put(&w, 0, 3);
-        put(&w, 0, 4);
-        if (put_ics(&w, sf_index, 0, q, sf, cb, ics, tns, extras & 2)) return -1;
-    } else {
-        put(&w, 1, 3);
-        put(&w, 0, 4);
-        const int common = (ics[0].flags & JAAD_ICS_COMMON_WINDOW) != 0;
-        put(&w, (uint32_t)common, 1);
-        if (common) {
-            Info I;
-            info_of(&ics[0], &I);
-            put_ics_info(&w, &I);
-            const int nb = I.ngroups * I.max_sfb;
-            if (ics[0].flags & JAAD_ICS_MS_PRESENT) {
-                int all = 1;
-                for (int i = 0; i < nb; i++) all &= (int)((ms_used[i >> 6] >> (i & 63)) & 1);
-                if (all && nb) {
-                    put(&w, 2, 2);
-                } else {
-                    put(&w, 1, 2);
-                    for (int i = 0; i < nb; i++) put(&w, (uint32_t)((ms_used[i >> 6] >> (i & 63)) & 1), 1);
-                }
-            } else {
-                put(&w, 0, 2);
-            }
-        }
-        if (put_ics(&w, sf_index, common, q, sf, cb, &ics[0], tns, extras & 2)) return -1;
-        if (put_ics(&w, sf_index, common, q + 1024, sf + 128, cb + 128, &ics[1], tns ? tns + 1 : NULL, extras & 2))
-            return -1;
-    }
+    if (put_element(&w, sf_index, nch == 1 ? 0 : 1, 0, q, sf, cb, ics, ms_used, tns, extras)) return -1;
     if (sbr) {
         uint8_t fil[512];
         const long nbits = jaad_sbr_fil_bits(sbr_state, nch, sbr, fil, sizeof fil);

@@ -57,6 +57,8 @@ def lib() -> C.CDLL:
         L.jaad_sbr_wstate_init.restype = None
         L.orc_sbr_res_tables.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
         L.jaad_write_adts_header.argtypes = [C.c_int, C.c_int, C.c_size_t, C.c_void_p]
+        L.jaad_write_frame_mc.argtypes = [C.c_int, C.c_int, C.c_void_p] + [C.c_void_p] * 6 + [C.c_void_p, C.c_size_t]
+        L.jaad_write_frame_mc.restype = C.c_long
         _lib = L
     return _lib
 
@@ -199,6 +201,58 @@ def write_frames(batch, sf_index: int, frames=None, extras: int = 0, sbr_writer:
             raise ValueError(f"frame {f} cannot be written")
         out.append(buf[:n].tobytes())
     return out
+
+
+def write_frames_mc(batch, sf_index: int, ids) -> list:
+    """TEST WRITER: raw_data_blocks of a multichannel batch (native.mc_batch layout): the elements
+    `ids` (0 SCE, 1 CPE, 3 LFE) in order, then END (jaad_write_frame_mc)."""
+    nch = batch.nch
+    ids_a = (C.c_int * len(ids))(*ids)
+    buf = np.zeros(65536, np.uint8)
+    out = []
+    for f in range(batch.n_frames):
+        cf = f * nch
+        q = np.ascontiguousarray(batch.q[cf:cf + nch])
+        sf = np.ascontiguousarray(batch.sf[cf:cf + nch])
+        cb = np.ascontiguousarray(batch.cb[cf:cf + nch])
+        ics = np.ascontiguousarray(batch.ics[cf:cf + nch])
+        ms = np.ascontiguousarray(batch.ms_used[f]) if batch.ms_used is not None else np.zeros(2, np.uint64)
+        tns = np.ascontiguousarray(batch.tns[cf:cf + nch]) if batch.tns is not None else None
+        n = lib().jaad_write_frame_mc(sf_index, len(ids), ids_a, q.ctypes.data, sf.ctypes.data, cb.ctypes.data,
+                                      ics.ctypes.data, ms.ctypes.data, tns.ctypes.data if tns is not None else None,
+                                      buf.ctypes.data, buf.nbytes)
+        if n < 0:
+            raise ValueError(f"frame {f} cannot be written")
+        out.append(buf[:n].tobytes())
+    return out
+
+
+def decode_batch_mc(sf_index: int, batch, ids, flags: int = 0, threads: int = 1, tns_mode: int = 0) -> np.ndarray:
+    """TEST ORACLE for a multichannel batch, from fresh stream states: every element decoded on its
+    own (SCE/LFE as a mono, CPE as a stereo stream: SyntacticElements.process runs them in turn)
+    and the channels interleaved in element order (SampleBuffer.accept); uint8 [n_frames, bytes]."""
+    import jaadec_amd.native as N
+
+    nf, nch = batch.n_frames, batch.nch
+    fb = 4 if flags & 2 else 2
+    planes = []
+    c, cpe = 0, 0
+    for i in ids:
+        k = 2 if i == 1 else 1
+        cfr = (np.arange(nf)[:, None] * nch + c + np.arange(k)[None, :]).reshape(-1)
+        el = N.Batch(np.ascontiguousarray(batch.q[cfr]), np.ascontiguousarray(batch.sf[cfr]),
+                     np.ascontiguousarray(batch.cb[cfr]), np.ascontiguousarray(batch.ics[cfr]),
+                     np.ascontiguousarray(batch.ms_used[:, 2 * cpe:2 * cpe + 2]) if k == 2 else None,
+                     np.ascontiguousarray(batch.tns[cfr]) if batch.tns is not None else None,
+                     batch.stream_slot.copy(), batch.frame_begin.copy(), k)
+        cfg = N.make_cfg(sf_index, 2 if k == 2 else 1, tns_mode)
+        pcm = decode_batch(cfg, el, Streams(int(batch.stream_slot.max()) + 1), flags, threads)
+        dt = np.uint32 if fb == 4 else np.uint16
+        frames = pcm.view(dt).reshape(nf, 1024, 2)
+        planes += [frames[:, :, j] for j in range(k)]
+        c += k
+        cpe += k == 2
+    return np.ascontiguousarray(np.stack(planes, 2)).view(np.uint8).reshape(nf, -1)
 
 
 def adts_wrap(payloads: list, sf_index: int, channel_config: int) -> bytes:

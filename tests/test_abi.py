@@ -65,13 +65,18 @@ def test_config_queries_mirror_decoderconfig():
     down = N.make_cfg(sf_index=6, channel_config=2, sbr=True, down=True)
     assert L.jaad_cfg_sample_length(C.byref(up)) == 2048   # upsampling SBR doubles the length
     assert L.jaad_cfg_sample_length(C.byref(down)) == 1024  # downsampled SBR keeps the core rate
+    for cc, n in ((3, 3), (4, 4), (5, 5), (6, 6), (7, 8)):  # ChannelConfiguration: 5.1 = 6, 7.1 = 8
+        mc = N.make_cfg(channel_config=cc)
+        assert L.jaad_cfg_channel_count(C.byref(mc)) == n
+        assert L.jaad_frame_pcm_bytes(C.byref(mc), N.PCM_BIG_ENDIAN) == 1024 * n * 2
 
 
 @pytest.mark.parametrize("fields,status", [
     ({"abi_version": 99}, N.ERR_ABI),
     ({"profile": 1}, N.ERR_UNSUPPORTED),      # AAC Main: ICPrediction is out of scope
     ({"sf_index": 12}, N.ERR_UNSUPPORTED),
-    ({"channel_config": 6}, N.ERR_UNSUPPORTED),
+    ({"channel_config": 8}, N.ERR_UNSUPPORTED),               # no configuration 8
+    ({"channel_config": 6, "sbr": 1, "ext_sf_index": 0}, N.ERR_UNSUPPORTED),  # multichannel: AAC-LC only
     ({"sbr": 1, "ext_sf_index": 1}, N.ERR_UNSUPPORTED),    # SBR output rate must be 2x the core rate
     ({"sbr": 1, "sf_index": 1, "ext_sf_index": 0}, N.ERR_UNSUPPORTED),
     ({"ps": 1, "sbr": 1, "channel_config": 2}, N.ERR_UNSUPPORTED),  # PS needs an SCE core
