@@ -238,6 +238,8 @@ struct jaad_ctx {
     hipStream_t h2d = nullptr, d2h = nullptr;      // copy streams beside `stream` (one DMA engine each)
     hipEvent_t ev_in[kMaxPieces] = {}, ev_k[kMaxPieces] = {}, ev_out[kMaxPieces] = {};
     PinnedBuf stage_in[kStageSlots], stage_out[kStageSlots];
+    DevBuf d_flag;                                 // |q| check result of a host-buffer call (device)
+    PinnedBuf h_flag;
     std::unique_ptr<WorkerPool> io;                // validation / staging copies
     std::vector<std::pair<uintptr_t, size_t>> pinned;  // jaad_host_register ranges
     uint32_t plan_L = 0;                           // chunk length of the cached plan
@@ -1144,6 +1146,8 @@ void jaad_ctx_destroy(jaad_ctx* ctx)
             if (ev) (void)hipEventDestroy(ev);
     for (auto& st : ctx->stage_in) st.release();
     for (auto& st : ctx->stage_out) st.release();
+    ctx->d_flag.release();
+    ctx->h_flag.release();
     for (const auto& r : ctx->pinned) (void)hipHostUnregister(reinterpret_cast<void*>(r.first));
     ctx->io.reset();
     ctx->d_chunks.release();
@@ -1379,6 +1383,14 @@ static int decode_batch_pieces(jaad_ctx* ctx, const jaad_batch* b, void* pcm_out
     if (!pin_out)
         for (auto& st : ctx->stage_out) HIPCHK(st.ensure(maxf * fbytes));
 
+    // |q| <= 8190 is checked on the device, piece by piece, before the piece's kernel (the host never
+    // reads q: a registered q goes straight from the caller's memory to HBM); the LC kernel clamps
+    // |q| anyway, so a bad piece decodes garbage but touches nothing outside its buffers, and the
+    // flag read at the end turns the call into JAAD_ERR_BITSTREAM with the state not flipped
+    HIPCHK(ctx->d_flag.ensure(256));
+    HIPCHK(ctx->h_flag.ensure(16));
+    int* const dflag = static_cast<int*>(ctx->d_flag.p);
+    HIPCHK(hipMemsetAsync(dflag, 0, sizeof(int), s));
     WorkerPool& io = *ctx->io;
     const int W = io.size();
     std::atomic<bool> bad{false};
@@ -1425,13 +1437,13 @@ static int decode_batch_pieces(jaad_ctx* ctx, const jaad_batch* b, void* pcm_out
         char* st = static_cast<char*>(ctx->stage_in[i % kStageSlots].p);
         if (i >= kStageSlots && s_total)  // the staging slot's previous piece has been copied
             HIPCHK(hipEventSynchronize(ctx->ev_in[i - kStageSlots]));
-        // validate (and stage) the piece on the workers
+        // check the side info (and stage the piece) on the workers
         io.run([&](int t) {
             const size_t a0 = nci * t / W, a1 = nci * (t + 1) / W;
-            if (!side_info_ok(ctx, b, c0 + a0, c0 + a1) ||
-                !q_ok_copy(b->q + (c0 + a0) * 1024, pin_q ? nullptr : reinterpret_cast<int16_t*>(st + s_q) + a0 * 1024,
-                           (a1 - a0) * 1024))
-                bad = true;
+            if (!side_info_ok(ctx, b, c0 + a0, c0 + a1)) bad = true;
+            if (!pin_q)
+                std::memcpy(reinterpret_cast<int16_t*>(st + s_q) + a0 * 1024, b->q + (c0 + a0) * 1024,
+                            (a1 - a0) * 1024 * sizeof(int16_t));
             if (!pin_rest) {
                 std::memcpy(st + s_sf + a0 * 128, b->sf + (c0 + a0) * 128, (a1 - a0) * 128);
                 std::memcpy(st + s_cb + a0 * 128, b->cb + (c0 + a0) * 128, (a1 - a0) * 128);
@@ -1444,6 +1456,7 @@ static int decode_batch_pieces(jaad_ctx* ctx, const jaad_batch* b, void* pcm_out
         if (bad) break;
         if (!pinned_in && (rc = h2d(i, st))) return rc;
         HIPCHK(hipStreamWaitEvent(s, ctx->ev_in[i], 0));
+        HIPCHK(launch_check_q(db.q + c0 * 1024, nci * 1024, dflag, s));
         a.chunks = static_cast<const ChunkDesc*>(ctx->d_chunks.p) + C[i];
         a.n_chunks = C[i + 1] - C[i];
         if (a.n_chunks) HIPCHK(launch_lc(a, s, tns_spec));
@@ -1458,13 +1471,15 @@ static int decode_batch_pieces(jaad_ctx* ctx, const jaad_batch* b, void* pcm_out
     if (!pin_out)
         for (int i = std::max(0, queued - kStageSlots); i < queued; i++)
             if ((rc = copy_out(i))) return rc;
+    int* const hflag = static_cast<int*>(ctx->h_flag.p);
+    HIPCHK(hipMemcpyAsync(hflag, dflag, sizeof(int), hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(ctx->d2h));
     HIPCHK(hipStreamSynchronize(ctx->h2d));
     HIPCHK(hipStreamSynchronize(s));
     HIPCHK(hipEventRecord(ctx->done, s));
     ctx->done_live = true;
     ctx->last_stream = s;
-    if (bad) return JAAD_ERR_BITSTREAM;  // state not flipped: every slot as before the call
+    if (bad || *hflag) return JAAD_ERR_BITSTREAM;  // state not flipped: every slot as before the call
     ctx->parity ^= 1;
     return JAAD_OK;
 }

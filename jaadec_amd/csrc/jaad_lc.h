@@ -102,6 +102,9 @@ constexpr uint32_t kOutPlanarF32 = 4;  // internal output mode: core time sample
 
 // one wave per chunk (grid derived from a.n_chunks)
 hipError_t launch_lc(const KernelArgs& a, hipStream_t stream, bool tns_spec);
+// |q| <= 8190 over n int16 values (IQ_TABLE has 8191 entries; the reference's array index would
+// throw): any value beyond sets *flag to 1 (plain stores; *flag is cleared by the caller)
+hipError_t launch_check_q(const int16_t* q, size_t n, int* flag, hipStream_t stream);
 // SampleBuffer.accept for a multichannel frame: planar f32 [frame][n_ch][1024] -> n_ch
 // interleaved samples per instant (int16 BE/LE after Math.round + clamp, or f32; JAAD_PCM_*)
 hipError_t launch_pack(const float* planar, void* pcm, uint32_t n_frames, int n_ch, uint32_t flags,

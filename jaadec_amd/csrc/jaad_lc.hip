@@ -26,6 +26,8 @@
 // results are bit-exact.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "jaad_lc.h"
 
 namespace jaad {
@@ -1284,6 +1286,32 @@ __global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ pla
     }
 }
 }  // namespace
+
+namespace {
+// 16 bytes (8 values) per thread and step, grid-stride over the range
+__global__ __launch_bounds__(256) void check_q_kernel(const v4i* __restrict__ q, size_t n16, int* __restrict__ flag)
+{
+    int bad = 0;
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += (size_t)gridDim.x * 256) {
+        const v4i w = __builtin_nontemporal_load(q + i);
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int lo = (int)(int16_t)(w[k] & 0xFFFF), hi = w[k] >> 16;
+            bad |= (lo > 8190) | (lo < -8190) | (hi > 8190) | (hi < -8190);
+        }
+    }
+    if (bad) *flag = 1;
+}
+}  // namespace
+
+hipError_t launch_check_q(const int16_t* q, size_t n, int* flag, hipStream_t stream)
+{
+    const size_t n16 = n / 8;  // q rows are 1024 values: whole 16-byte words
+    if (!n16) return hipSuccess;
+    const unsigned blocks = (unsigned)std::min<size_t>((n16 + 255) / 256, 2048);
+    hipLaunchKernelGGL(check_q_kernel, dim3(blocks), dim3(256), 0, stream, reinterpret_cast<const v4i*>(q), n16, flag);
+    return hipGetLastError();
+}
 
 hipError_t launch_pack(const float* planar, void* pcm, uint32_t n_frames, int n_ch, uint32_t flags, hipStream_t stream)
 {

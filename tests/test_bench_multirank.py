@@ -141,3 +141,43 @@ def test_gloo_world2_bench_line_and_pcm_match_world1(monkeypatch):
     line1, pcm1 = bench.run(args, engine_cls=OracleEngine, backend="gloo")
     assert line1["n_gpus"] == 1
     assert b"".join(got) == pcm1.tobytes()
+
+
+def _gpu_worker(rank, world, port, q):
+    # both ranks on the one GPU of the box (LOCAL_RANK 0), gloo for the barrier / reductions
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
+                      LOCAL_RANK="0")
+    import torch.distributed as dist
+
+    try:
+        line, pcm = bench.run(bench.parse(SMALL + ["--gpus", str(world)]), backend="gloo")
+        got = [None] * world
+        dist.all_gather_object(got, pcm.tobytes())
+        if rank == 0:
+            q.put((line, got))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_gpu_world2_bench_path_on_the_hip_engine(monkeypatch):
+    """bench.run() on two ranks with the product engine (HipEngine: jaad_decode_batch_device on the
+    GPU): the ranks' PCM concatenates to the world-1 PCM of the same global job."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gpu_worker, args=(r, world, port, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    line, got = q.get(timeout=300)
+    for pr in procs:
+        pr.join(timeout=120)
+        assert pr.exitcode == 0
+    assert line["n_gpus"] == 2 and line["parity_sample"]["max_abs_lsb"] == 0
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        monkeypatch.delenv(k, raising=False)
+    args = bench.parse(["--config", "2", "--steps", "2", "--warmup", "2", "--no-cpu", "--no-e2e",
+                        "--streams-per-gpu", "6", "--frames-per-stream", "6"])
+    _, pcm1 = bench.run(args)
+    assert b"".join(got) == pcm1.tobytes()
