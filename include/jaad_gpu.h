@@ -272,9 +272,16 @@ int jaad_decode_batch(jaad_ctx* ctx, const jaad_batch* batch, void* pcm_out, siz
 /* Page-lock [p, p + bytes) (hipHostRegister) for the context's host-buffer entry: batch arrays
  * and PCM buffers that lie inside a registered range skip the staging copy.  Register buffers
  * that are reused call after call (a JNI caller: its direct ByteBuffers, once per stream);
- * unregister before freeing them.  jaad_ctx_destroy unregisters what is left.               */
+ * unregister before freeing them.  jaad_ctx_destroy unregisters what is left.  Memory that is
+ * page-locked already (hipHostMalloc) is accepted and only recorded.                         */
 int jaad_host_register(jaad_ctx* ctx, void* p, size_t bytes);
 int jaad_host_unregister(jaad_ctx* ctx, void* p);
+/* Page-locked host memory owned by the context (hipHostMalloc), counted as registered: batch
+ * arrays and PCM buffers placed in it are copied by DMA directly.  A JNI caller wraps it in a
+ * direct ByteBuffer.  jaad_host_free releases it (after the context's work
+ * that may read it); jaad_ctx_destroy frees what is left.                                    */
+int jaad_host_alloc(jaad_ctx* ctx, size_t bytes, void** p);
+int jaad_host_free(jaad_ctx* ctx, void* p);
 
 /* Device-resident entry: all [dev] arrays and pcm_dev are device pointers; work is queued on
  * `hip_stream` (a hipStream_t, NULL = the context's stream) and the call returns without

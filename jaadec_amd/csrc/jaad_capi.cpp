@@ -146,7 +146,14 @@ private:
 // jaad_decode_batch pipeline: a batch is cut into up to kMaxPieces run-aligned pieces whose
 // H2D copy, kernels and D2H copy overlap on three streams; pageable caller memory goes through
 // kStageSlots page-locked staging slots per direction.
-constexpr int kMaxPieces = 8, kStageSlots = 2;
+#ifndef JAAD_MAX_PIECES
+#define JAAD_MAX_PIECES 8
+#endif
+#ifndef JAAD_MIN_PIECE_FRAMES
+#define JAAD_MIN_PIECE_FRAMES 4096
+#endif
+constexpr int kMaxPieces = JAAD_MAX_PIECES, kStageSlots = 2;
+enum : int { kPinRegistered = 0, kPinForeign = 1, kPinOwned = 2 };
 constexpr int kMaxElements = 8;
 
 // Channel elements of the AAC-LC channel configurations 3..7 (ISO/IEC 14496-3 Table 1.19: C, L/R,
@@ -160,7 +167,7 @@ int mc_elements(int channel_config, uint8_t* nch)
     for (int i = 0; i < kCount[k]; i++) nch[i] = kLayouts[k][i];
     return kCount[k];
 }
-constexpr uint32_t kMinPieceFrames = 4096;
+constexpr uint32_t kMinPieceFrames = JAAD_MIN_PIECE_FRAMES;
 
 // One call's SBR/PS parameter records: built on the host straight into page-locked staging,
 // copied on the context's copy stream while the previous call's kernels run.  Two sets
@@ -241,7 +248,12 @@ struct jaad_ctx {
     DevBuf d_flag;                                 // |q| check result of a host-buffer call (device)
     PinnedBuf h_flag;
     std::unique_ptr<WorkerPool> io;                // validation / staging copies
-    std::vector<std::pair<uintptr_t, size_t>> pinned;  // jaad_host_register ranges
+    struct PinRange {
+        uintptr_t p;
+        size_t n;
+        int kind;  // kPinRegistered (hipHostRegister'd here), kPinForeign (already page-locked), kPinOwned (jaad_host_alloc)
+    };
+    std::vector<PinRange> pinned;  // jaad_host_register / jaad_host_alloc ranges
     uint32_t plan_L = 0;                           // chunk length of the cached plan
 };
 
@@ -1148,7 +1160,10 @@ void jaad_ctx_destroy(jaad_ctx* ctx)
     for (auto& st : ctx->stage_out) st.release();
     ctx->d_flag.release();
     ctx->h_flag.release();
-    for (const auto& r : ctx->pinned) (void)hipHostUnregister(reinterpret_cast<void*>(r.first));
+    for (const auto& r : ctx->pinned) {
+        if (r.kind == kPinRegistered) (void)hipHostUnregister(reinterpret_cast<void*>(r.p));
+        if (r.kind == kPinOwned) (void)hipHostFree(reinterpret_cast<void*>(r.p));
+    }
     ctx->io.reset();
     ctx->d_chunks.release();
     ctx->h_chunks.release();
@@ -1211,7 +1226,7 @@ static bool is_pinned(const jaad_ctx* ctx, const void* p, size_t n)
 {
     const uintptr_t a = reinterpret_cast<uintptr_t>(p);
     for (const auto& r : ctx->pinned)
-        if (a >= r.first && a + n <= r.first + r.second) return true;
+        if (a >= r.p && a + n <= r.p + r.n) return true;
     return false;
 }
 
@@ -1300,6 +1315,12 @@ static int decode_batch_serial(jaad_ctx* ctx, const jaad_batch* b, void* pcm_out
 // AAC-LC: the pieces pipeline.  Every piece's kernels read the call's input state buffer and
 // write the output one (pieces touch disjoint slots), so the state flips once, at the end, and a
 // piece that fails validation leaves every slot's state as it was before the call.
+//
+// Per piece two H2D copies: its q (straight from registered caller memory, else from staging) and
+// one block with its side info, which the workers pack into staging while they check it (sf, cb,
+// ics, ms_used, tns of the piece back to back; four small copies per piece cost ~0.5 ms of DMA
+// set-up per C2 batch).  The piece's kernel gets pointers into its block, offset by the piece's
+// first channel-frame so that the batch-wide indices land in it.
 static int decode_batch_pieces(jaad_ctx* ctx, const jaad_batch* b, void* pcm_out, uint32_t flags,
                                const std::vector<uint32_t>& run0)
 {
@@ -1307,32 +1328,45 @@ static int decode_batch_pieces(jaad_ctx* ctx, const jaad_batch* b, void* pcm_out
     const size_t nf = b->n_frames, ncf = nf * nch;
     const int P = (int)run0.size() - 1;
     const size_t fbytes = pcm_bytes_per_frame(ctx, flags);
-    // device image of the whole batch (the chunk table addresses frames batch-wide)
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-    const size_t o_q = 0, o_sf = al(o_q + ncf * 2048), o_cb = al(o_sf + ncf * 128), o_ics = al(o_cb + ncf * 128);
-    const size_t o_ms = al(o_ics + ncf * sizeof(jaad_ics_info)), o_tns = al(o_ms + nf * 16);
-    const size_t total = al(o_tns + (b->tns ? ncf * sizeof(jaad_tns) : 0));
-    HIPCHK(ctx->d_batch.ensure(total + 256));
-    HIPCHK(ctx->d_pcm.ensure(fbytes * nf + 256));
-    char* base = static_cast<char*>(ctx->d_batch.p);
-    char* dpcm = static_cast<char*>(ctx->d_pcm.p);
-    jaad_batch db = *b;
-    db.q = reinterpret_cast<const int16_t*>(base + o_q);
-    db.sf = reinterpret_cast<const uint8_t*>(base + o_sf);
-    db.cb = reinterpret_cast<const uint8_t*>(base + o_cb);
-    db.ics = reinterpret_cast<const jaad_ics_info*>(base + o_ics);
-    db.ms_used = b->ms_used ? reinterpret_cast<const uint64_t*>(base + o_ms) : nullptr;
-    db.tns = b->tns ? reinterpret_cast<const jaad_tns*>(base + o_tns) : nullptr;
 
     // piece frame ranges and the largest piece (chunk sizing, staging)
     std::vector<size_t> F(P + 1);
     size_t maxf = 0;
     for (int i = 0; i <= P; i++) F[i] = b->frame_begin[run0[i]];
     for (int i = 0; i < P; i++) maxf = std::max(maxf, F[i + 1] - F[i]);
+    // side block of a piece of nfi frames: [sf][cb][ics][ms_used][tns], 256-B aligned parts
+    struct SideLayout {
+        size_t sf, cb, ics, ms, tns, bytes;
+    };
+    auto side_layout = [&](size_t nfi) {
+        const size_t nci = nfi * nch;
+        SideLayout L;
+        L.sf = 0;
+        L.cb = al(nci * 128);
+        L.ics = L.cb + al(nci * 128);
+        L.ms = L.ics + al(nci * sizeof(jaad_ics_info));
+        L.tns = L.ms + (b->ms_used ? al(nfi * 16) : 0);
+        L.bytes = L.tns + (b->tns ? al(nci * sizeof(jaad_tns)) : 0);
+        return L;
+    };
+    // device image: q batch-wide (the check kernel reads it), then the pieces' side blocks
+    std::vector<size_t> SB(P + 1);
+    SB[0] = al(ncf * 2048);
+    for (int i = 0; i < P; i++) SB[i + 1] = SB[i] + side_layout(F[i + 1] - F[i]).bytes;
+    HIPCHK(ctx->d_batch.ensure(SB[P] + 256));
+    HIPCHK(ctx->d_pcm.ensure(fbytes * nf + 256));
+    char* base = static_cast<char*>(ctx->d_batch.p);
+    char* dpcm = static_cast<char*>(ctx->d_pcm.p);
+    const int16_t* dq = reinterpret_cast<const int16_t*>(base);
+
     hipStream_t s = ctx->stream;
     if (ctx->done_live && ctx->last_stream != s) HIPCHK(hipStreamWaitEvent(s, ctx->done, 0));
-    int rc = plan(ctx, &db, s, (uint32_t)maxf);
-    if (rc) return rc;
+    {   // the planner reads only the run layout and the frame count
+        jaad_batch db = *b;
+        int rc = plan(ctx, &db, s, (uint32_t)maxf);
+        if (rc) return rc;
+    }
     // chunk range of each piece (chunks are in run order, frames ascending)
     std::vector<uint32_t> C(P + 1);
     for (int i = 0; i <= P; i++) {
@@ -1345,12 +1379,7 @@ static int decode_batch_pieces(jaad_ctx* ctx, const jaad_batch* b, void* pcm_out
                           ctx->chunks.begin());
     }
     KernelArgs a{};
-    a.q = db.q;
-    a.sf = db.sf;
-    a.cb = db.cb;
-    a.ics = db.ics;
-    a.ms_used = db.ms_used;
-    a.tns = db.tns;
+    a.q = dq;
     a.iq_table = ctx->d_iq;
     a.tables = ctx->d_tables;
     a.gtab = ctx->d_gtab;
@@ -1364,22 +1393,14 @@ static int decode_batch_pieces(jaad_ctx* ctx, const jaad_batch* b, void* pcm_out
     a.tns_mode = ctx->cfg.tns_mode;
     a.dbg = ctx->dbg;
     a.dbg_frame = ctx->dbg_frame;
-    const bool tns_spec = ctx->cfg.tns_mode == JAAD_TNS_SPEC && db.tns != nullptr;
+    const bool tns_spec = ctx->cfg.tns_mode == JAAD_TNS_SPEC && b->tns != nullptr;
+    int rc;
     if ((rc = carry_untouched(ctx, a.state_out, a.state_in, 2048, s))) return rc;
 
-    // caller arrays: DMA straight from registered memory, else through the staging slots
+    // q and PCM: DMA straight from / to registered memory, else through the staging slots
     const bool pin_q = is_pinned(ctx, b->q, ncf * 2048), pin_out = is_pinned(ctx, pcm_out, fbytes * nf);
-    const bool pin_rest = is_pinned(ctx, b->sf, ncf * 128) && is_pinned(ctx, b->cb, ncf * 128) &&
-                          is_pinned(ctx, b->ics, ncf * sizeof(jaad_ics_info)) &&
-                          (!b->ms_used || is_pinned(ctx, b->ms_used, nf * 16)) &&
-                          (!b->tns || is_pinned(ctx, b->tns, ncf * sizeof(jaad_tns)));
-    const size_t mc = maxf * nch;
-    const size_t s_q = 0, s_sf = al(s_q + (pin_q ? 0 : mc * 2048)), s_cb = al(s_sf + (pin_rest ? 0 : mc * 128));
-    const size_t s_ics = al(s_cb + (pin_rest ? 0 : mc * 128)), s_ms = al(s_ics + (pin_rest ? 0 : mc * sizeof(jaad_ics_info)));
-    const size_t s_tns = al(s_ms + (pin_rest || !b->ms_used ? 0 : maxf * 16));
-    const size_t s_total = al(s_tns + (pin_rest || !b->tns ? 0 : mc * sizeof(jaad_tns)));
-    if (s_total)
-        for (auto& st : ctx->stage_in) HIPCHK(st.ensure(s_total));
+    const size_t s_side = pin_q ? 0 : al(maxf * nch * 2048);
+    for (auto& st : ctx->stage_in) HIPCHK(st.ensure(s_side + side_layout(maxf).bytes));
     if (!pin_out)
         for (auto& st : ctx->stage_out) HIPCHK(st.ensure(maxf * fbytes));
 
@@ -1394,7 +1415,7 @@ static int decode_batch_pieces(jaad_ctx* ctx, const jaad_batch* b, void* pcm_out
     WorkerPool& io = *ctx->io;
     const int W = io.size();
     std::atomic<bool> bad{false};
-    int queued = 0;  // pieces whose copies/kernels are queued
+    int queued = 0;  // pieces whose kernels and D2H copies are queued
     auto copy_out = [&](int i) -> int {  // staging -> caller PCM of piece i
         HIPCHK(hipEventSynchronize(ctx->ev_out[i]));
         const char* src = static_cast<const char*>(ctx->stage_out[i % kStageSlots].p);
@@ -1403,60 +1424,54 @@ static int decode_batch_pieces(jaad_ctx* ctx, const jaad_batch* b, void* pcm_out
         io.run([&](int t) { std::memcpy(dst + n * t / W, src + n * t / W, n * (t + 1) / W - n * t / W); });
         return JAAD_OK;
     };
-    // H2D of piece i on the one H2D copy stream (a second H2D stream shared a DMA engine with the
-    // D2H stream and serialised them: C2 e2e 9.4e6 -> 6.5e6 frames/s, profiles/round3_e2e_*)
-    auto h2d = [&](int i, const char* st) -> int {
+    // piece i: check its side info and pack it (and q, unless registered) into staging slot i % 2,
+    // then queue its two H2D copies on the one H2D copy stream (a second H2D stream shared a DMA
+    // engine with the D2H stream and serialised them: C2 e2e 9.4e6 -> 6.5e6 frames/s,
+    // profiles/round3_e2e_*); ev_in[i] marks both done
+    auto stage_piece = [&](int i) -> int {
         const size_t f0 = F[i], nfi = F[i + 1] - f0, c0 = f0 * nch, nci = nfi * nch;
-        const char* src_q = pin_q ? (const char*)(b->q + c0 * 1024) : st + s_q;
-        hipStream_t h = ctx->h2d;
-        HIPCHK(hipMemcpyAsync(base + o_q + c0 * 2048, src_q, nci * 2048, hipMemcpyHostToDevice, h));
-        const char* src_sf = pin_rest ? (const char*)(b->sf + c0 * 128) : st + s_sf;
-        const char* src_cb = pin_rest ? (const char*)(b->cb + c0 * 128) : st + s_cb;
-        const char* src_ics = pin_rest ? (const char*)(b->ics + c0) : st + s_ics;
-        HIPCHK(hipMemcpyAsync(base + o_sf + c0 * 128, src_sf, nci * 128, hipMemcpyHostToDevice, h));
-        HIPCHK(hipMemcpyAsync(base + o_cb + c0 * 128, src_cb, nci * 128, hipMemcpyHostToDevice, h));
-        HIPCHK(hipMemcpyAsync(base + o_ics + c0 * sizeof(jaad_ics_info), src_ics, nci * sizeof(jaad_ics_info),
-                              hipMemcpyHostToDevice, h));
-        if (b->ms_used)
-            HIPCHK(hipMemcpyAsync(base + o_ms + f0 * 16, pin_rest ? (const char*)(b->ms_used + f0 * 2) : st + s_ms, nfi * 16,
-                                  hipMemcpyHostToDevice, h));
-        if (b->tns)
-            HIPCHK(hipMemcpyAsync(base + o_tns + c0 * sizeof(jaad_tns), pin_rest ? (const char*)(b->tns + c0) : st + s_tns,
-                                  nci * sizeof(jaad_tns), hipMemcpyHostToDevice, h));
-        HIPCHK(hipEventRecord(ctx->ev_in[i], h));
-        return JAAD_OK;
-    };
-    // every input pinned: a piece's copies are queued one piece ahead of its checks, which run while
-    // they fly (its kernel is queued once they passed).  Only one piece ahead: copies are served in
-    // submission order, so queueing every H2D first would hold the D2H copies back behind them.
-    const bool pinned_in = pin_q && pin_rest;
-    if (pinned_in && (rc = h2d(0, nullptr))) return rc;
-    for (int i = 0; i < P && !bad; i++) {
-        if (pinned_in && i + 1 < P && (rc = h2d(i + 1, nullptr))) return rc;
-        const size_t f0 = F[i], nfi = F[i + 1] - f0, c0 = f0 * nch, nci = nfi * nch;
-        char* st = static_cast<char*>(ctx->stage_in[i % kStageSlots].p);
-        if (i >= kStageSlots && s_total)  // the staging slot's previous piece has been copied
+        const SideLayout L = side_layout(nfi);
+        if (i >= kStageSlots)  // the slot's previous piece has been copied
             HIPCHK(hipEventSynchronize(ctx->ev_in[i - kStageSlots]));
-        // check the side info (and stage the piece) on the workers
+        char* st = static_cast<char*>(ctx->stage_in[i % kStageSlots].p);
+        char* sd = st + s_side;
         io.run([&](int t) {
             const size_t a0 = nci * t / W, a1 = nci * (t + 1) / W;
             if (!side_info_ok(ctx, b, c0 + a0, c0 + a1)) bad = true;
             if (!pin_q)
-                std::memcpy(reinterpret_cast<int16_t*>(st + s_q) + a0 * 1024, b->q + (c0 + a0) * 1024,
+                std::memcpy(reinterpret_cast<int16_t*>(st) + a0 * 1024, b->q + (c0 + a0) * 1024,
                             (a1 - a0) * 1024 * sizeof(int16_t));
-            if (!pin_rest) {
-                std::memcpy(st + s_sf + a0 * 128, b->sf + (c0 + a0) * 128, (a1 - a0) * 128);
-                std::memcpy(st + s_cb + a0 * 128, b->cb + (c0 + a0) * 128, (a1 - a0) * 128);
-                std::memcpy(st + s_ics + a0 * sizeof(jaad_ics_info), b->ics + c0 + a0, (a1 - a0) * sizeof(jaad_ics_info));
-                if (b->tns)
-                    std::memcpy(st + s_tns + a0 * sizeof(jaad_tns), b->tns + c0 + a0, (a1 - a0) * sizeof(jaad_tns));
-                if (b->ms_used && t == 0) std::memcpy(st + s_ms, b->ms_used + f0 * 2, nfi * 16);
-            }
+            std::memcpy(sd + L.sf + a0 * 128, b->sf + (c0 + a0) * 128, (a1 - a0) * 128);
+            std::memcpy(sd + L.cb + a0 * 128, b->cb + (c0 + a0) * 128, (a1 - a0) * 128);
+            std::memcpy(sd + L.ics + a0 * sizeof(jaad_ics_info), b->ics + c0 + a0, (a1 - a0) * sizeof(jaad_ics_info));
+            if (b->tns) std::memcpy(sd + L.tns + a0 * sizeof(jaad_tns), b->tns + c0 + a0, (a1 - a0) * sizeof(jaad_tns));
+            if (b->ms_used && t == 0) std::memcpy(sd + L.ms, b->ms_used + f0 * 2, nfi * 16);
         });
+        if (bad) return JAAD_OK;
+        hipStream_t h = ctx->h2d;
+        HIPCHK(hipMemcpyAsync(base + c0 * 2048, pin_q ? (const void*)(b->q + c0 * 1024) : (const void*)st, nci * 2048,
+                              hipMemcpyHostToDevice, h));
+        HIPCHK(hipMemcpyAsync(base + SB[i], sd, L.bytes, hipMemcpyHostToDevice, h));
+        HIPCHK(hipEventRecord(ctx->ev_in[i], h));
+        return JAAD_OK;
+    };
+    // piece i+1 is checked, packed and its copies queued before piece i's kernel: the host work of
+    // one piece overlaps the copies of the previous one, and copies stay one piece ahead (copies
+    // are served in submission order, so queueing every H2D first would hold the D2H copies back)
+    if ((rc = stage_piece(0))) return rc;
+    for (int i = 0; i < P && !bad; i++) {
+        if (i + 1 < P && (rc = stage_piece(i + 1))) return rc;
         if (bad) break;
-        if (!pinned_in && (rc = h2d(i, st))) return rc;
+        const size_t f0 = F[i], nfi = F[i + 1] - f0, c0 = f0 * nch, nci = nfi * nch;
+        const SideLayout L = side_layout(nfi);
+        char* sd = base + SB[i];
+        a.sf = reinterpret_cast<const uint8_t*>(sd + L.sf) - c0 * 128;
+        a.cb = reinterpret_cast<const uint8_t*>(sd + L.cb) - c0 * 128;
+        a.ics = reinterpret_cast<const jaad_ics_info*>(sd + L.ics) - c0;
+        a.ms_used = b->ms_used ? reinterpret_cast<const uint64_t*>(sd + L.ms) - f0 * 2 : nullptr;
+        a.tns = b->tns ? reinterpret_cast<const jaad_tns*>(sd + L.tns) - c0 : nullptr;
         HIPCHK(hipStreamWaitEvent(s, ctx->ev_in[i], 0));
-        HIPCHK(launch_check_q(db.q + c0 * 1024, nci * 1024, dflag, s));
+        HIPCHK(launch_check_q(dq + c0 * 1024, nci * 1024, dflag, s));
         a.chunks = static_cast<const ChunkDesc*>(ctx->d_chunks.p) + C[i];
         a.n_chunks = C[i + 1] - C[i];
         if (a.n_chunks) HIPCHK(launch_lc(a, s, tns_spec));
@@ -1506,21 +1521,61 @@ int jaad_host_register(jaad_ctx* ctx, void* p, size_t bytes)
 {
     if (!ctx || !p || !bytes) return JAAD_ERR_INVALID_ARG;
     HIPCHK(hipSetDevice(ctx->device));
+    // memory that is page-locked already (hipHostMalloc, another registration) is recorded as is
+    hipPointerAttribute_t at{};
+    if (hipPointerGetAttributes(&at, p) == hipSuccess && at.type == hipMemoryTypeHost) {
+        ctx->pinned.push_back({reinterpret_cast<uintptr_t>(p), bytes, kPinForeign});
+        return JAAD_OK;
+    }
+    (void)hipGetLastError();  // pageable memory: the query's error is expected
     HIPCHK(hipHostRegister(p, bytes, hipHostRegisterDefault));
-    ctx->pinned.emplace_back(reinterpret_cast<uintptr_t>(p), bytes);
+    ctx->pinned.push_back({reinterpret_cast<uintptr_t>(p), bytes, kPinRegistered});
     return JAAD_OK;
+}
+
+static std::vector<jaad_ctx::PinRange>::iterator find_pin(jaad_ctx* ctx, void* p)
+{
+    return std::find_if(ctx->pinned.begin(), ctx->pinned.end(),
+                        [&](const jaad_ctx::PinRange& r) { return r.p == reinterpret_cast<uintptr_t>(p); });
 }
 
 int jaad_host_unregister(jaad_ctx* ctx, void* p)
 {
     if (!ctx || !p) return JAAD_ERR_INVALID_ARG;
-    auto it = std::find_if(ctx->pinned.begin(), ctx->pinned.end(),
-                           [&](const std::pair<uintptr_t, size_t>& r) { return r.first == reinterpret_cast<uintptr_t>(p); });
-    if (it == ctx->pinned.end()) return JAAD_ERR_INVALID_ARG;
+    auto it = find_pin(ctx, p);
+    if (it == ctx->pinned.end() || it->kind == kPinOwned) return JAAD_ERR_INVALID_ARG;
+    HIPCHK(hipSetDevice(ctx->device));
+    if (ctx->done_live) HIPCHK(hipEventSynchronize(ctx->done));
+    const int kind = it->kind;
+    ctx->pinned.erase(it);
+    if (kind == kPinRegistered) HIPCHK(hipHostUnregister(p));
+    return JAAD_OK;
+}
+
+int jaad_host_alloc(jaad_ctx* ctx, size_t bytes, void** p)
+{
+    if (!ctx || !bytes || !p) return JAAD_ERR_INVALID_ARG;
+    *p = nullptr;
+    HIPCHK(hipSetDevice(ctx->device));
+    void* q = nullptr;
+    if (hipHostMalloc(&q, bytes, hipHostMallocDefault) != hipSuccess || !q) {
+        (void)hipGetLastError();
+        return JAAD_ERR_NOMEM;
+    }
+    ctx->pinned.push_back({reinterpret_cast<uintptr_t>(q), bytes, kPinOwned});
+    *p = q;
+    return JAAD_OK;
+}
+
+int jaad_host_free(jaad_ctx* ctx, void* p)
+{
+    if (!ctx || !p) return JAAD_ERR_INVALID_ARG;
+    auto it = find_pin(ctx, p);
+    if (it == ctx->pinned.end() || it->kind != kPinOwned) return JAAD_ERR_INVALID_ARG;
     HIPCHK(hipSetDevice(ctx->device));
     if (ctx->done_live) HIPCHK(hipEventSynchronize(ctx->done));
     ctx->pinned.erase(it);
-    HIPCHK(hipHostUnregister(p));
+    HIPCHK(hipHostFree(p));
     return JAAD_OK;
 }
 

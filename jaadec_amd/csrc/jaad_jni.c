@@ -128,3 +128,32 @@ JNIEXPORT void JNICALL Java_net_sourceforge_jaad_aac_gpu_GpuDSP_nativeUnregister
     const int rc = (!ctx || !p) ? JAAD_ERR_INVALID_ARG : jaad_host_unregister(ctx, p);
     if (rc) throw_aac(env, ctx, rc);
 }
+
+/* static native ByteBuffer nativeAllocDirect(long h, long bytes) / nativeFreeDirect(long h, ByteBuffer buf):
+ * a direct buffer over page-locked memory the context owns (jaad_host_alloc): a stream that
+ * keeps its q/side-info/PCM arrays in such buffers gets DMA without staging and without
+ * registering pageable memory.  Free it (nativeFreeDirect) before dropping the buffer;
+ * nativeDestroy frees what is left. */
+JNIEXPORT jobject JNICALL Java_net_sourceforge_jaad_aac_gpu_GpuDSP_nativeAllocDirect(JNIEnv* env, jclass cls, jlong h,
+                                                                                   jlong bytes) {
+    (void)cls;
+    jaad_ctx* ctx = (jaad_ctx*)(intptr_t)h;
+    void* p = NULL;
+    const int rc = (!ctx || bytes <= 0) ? JAAD_ERR_INVALID_ARG : jaad_host_alloc(ctx, (size_t)bytes, &p);
+    if (rc) {
+        throw_aac(env, ctx, rc);
+        return NULL;
+    }
+    jobject buf = (*env)->NewDirectByteBuffer(env, p, bytes);
+    if (!buf) (void)jaad_host_free(ctx, p);  /* the JVM has an OutOfMemoryError pending */
+    return buf;
+}
+
+JNIEXPORT void JNICALL Java_net_sourceforge_jaad_aac_gpu_GpuDSP_nativeFreeDirect(JNIEnv* env, jclass cls, jlong h,
+                                                                               jobject buf) {
+    (void)cls;
+    jaad_ctx* ctx = (jaad_ctx*)(intptr_t)h;
+    void* p = buf ? (*env)->GetDirectBufferAddress(env, buf) : NULL;
+    const int rc = (!ctx || !p) ? JAAD_ERR_INVALID_ARG : jaad_host_free(ctx, p);
+    if (rc) throw_aac(env, ctx, rc);
+}

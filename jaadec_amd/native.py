@@ -80,7 +80,7 @@ class SynthParams(C.Structure):
 EXPORTS = ["jaad_cfg_sample_length", "jaad_cfg_channel_count", "jaad_frame_pcm_bytes", "jaad_ctx_create",
            "jaad_ctx_destroy", "jaad_ctx_core_channels", "jaad_decode_batch", "jaad_decode_batch_device", "jaad_wait", "jaad_state_bytes",
            "jaad_state_export", "jaad_state_import", "jaad_state_reset", "jaad_strerror", "jaad_last_error",
-           "jaad_host_register", "jaad_host_unregister"]
+           "jaad_host_register", "jaad_host_unregister", "jaad_host_alloc", "jaad_host_free"]
 # every symbol include/jaad_parse.h declares
 PARSE_EXPORTS = ["jaad_asc_parse", "jaad_adts_find", "jaad_adts_cfg", "jaad_parser_create", "jaad_parser_destroy",
                  "jaad_parser_clone", "jaad_parser_copy",
@@ -131,6 +131,8 @@ def lib() -> C.CDLL:
         L.jaad_wait.argtypes = [C.c_void_p]
         L.jaad_host_register.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
         L.jaad_host_unregister.argtypes = [C.c_void_p, C.c_void_p]
+        L.jaad_host_alloc.argtypes = [C.c_void_p, C.c_size_t, C.POINTER(C.c_void_p)]
+        L.jaad_host_free.argtypes = [C.c_void_p, C.c_void_p]
         L.jaad_state_bytes.argtypes = [C.c_void_p]
         L.jaad_state_bytes.restype = C.c_size_t
         L.jaad_state_export.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_size_t]
@@ -405,6 +407,32 @@ class Context:
         for a in arrays:
             if a is not None and a.nbytes:
                 self._check(lib().jaad_host_unregister(self.h, _ptr(a)), "jaad_host_unregister")
+
+    def host_array(self, shape, dtype=np.uint8) -> np.ndarray:
+        """A numpy array in page-locked memory owned by the context (jaad_host_alloc): batch arrays
+        and PCM buffers placed in it are copied by DMA directly.  Valid until free_host() or close()."""
+        dt = np.dtype(dtype)
+        n = max(int(np.prod(shape)) * dt.itemsize, 1)
+        p = C.c_void_p()
+        self._check(lib().jaad_host_alloc(self.h, n, C.byref(p)), "jaad_host_alloc")
+        buf = (C.c_uint8 * n).from_address(p.value)
+        return np.frombuffer(buf, np.uint8, int(np.prod(shape)) * dt.itemsize).view(dt).reshape(shape)
+
+    def free_host(self, *arrays: np.ndarray) -> None:
+        for a in arrays:
+            if a is not None:
+                self._check(lib().jaad_host_free(self.h, _ptr(a)), "jaad_host_free")
+
+    def host_batch(self, b: "Batch") -> "Batch":
+        """A copy of b whose arrays live in host_array() memory (free with free_host(*arrays))."""
+        def cp(a):
+            if a is None:
+                return None
+            h = self.host_array(a.shape, a.dtype)
+            h[...] = a
+            return h
+        return Batch(cp(b.q), cp(b.sf), cp(b.cb), cp(b.ics), cp(b.ms_used), cp(b.tns), b.stream_slot, b.frame_begin,
+                     b.nch, b.sbr)
 
     def decode_device(self, dev: dict, batch: Batch, pcm_dev_ptr: int, pcm_bytes: int, flags: int = 0,
                       stream_ptr: int | None = None) -> None:

@@ -27,7 +27,8 @@ ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
 ev[0].record(s)
 for _ in range(20): ctx.decode_device(ptr, b, pcm.data_ptr(), pcm.numel(), 0, s.cuda_stream)
 ev[1].record(s); torch.cuda.synchronize()
-print("%%.4f" %% (ev[0].elapsed_time(ev[1]) / 20))
+import hashlib
+print("%%.4f %%s" %% (ev[0].elapsed_time(ev[1]) / 20, hashlib.blake2b(pcm.cpu().numpy().tobytes(), digest_size=6).hexdigest()))
 ''' % ROOT
 
 def main():

@@ -18,6 +18,7 @@ struct JNINativeInterface_ {
     jint (*ThrowNew)(JNIEnv* env, jclass cls, const char* msg);
     void* (*GetDirectBufferAddress)(JNIEnv* env, jobject buf);
     jlong (*GetDirectBufferCapacity)(JNIEnv* env, jobject buf);
+    jobject (*NewDirectByteBuffer)(JNIEnv* env, void* address, jlong capacity);
 };
 
 #define JNIEXPORT __attribute__((visibility("default")))

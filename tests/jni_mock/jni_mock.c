@@ -25,7 +25,19 @@ static jint throw_new(JNIEnv* env, jclass cls, const char* msg)
 static void* buf_address(JNIEnv* env, jobject b) { (void)env; return b ? ((jni_mock_buffer*)b)->address : 0; }
 static jlong buf_capacity(JNIEnv* env, jobject b) { (void)env; return b ? ((jni_mock_buffer*)b)->capacity : -1; }
 
-static const struct JNINativeInterface_ g_table = {find_class, throw_new, buf_address, buf_capacity};
+/* buffers made by NewDirectByteBuffer: a small pool the test reads back with jni_mock_buffer_at */
+static jni_mock_buffer g_made[16];
+static int g_n_made;
+static jobject new_direct(JNIEnv* env, void* address, jlong capacity)
+{
+    (void)env;
+    if (g_n_made >= 16) return 0;
+    g_made[g_n_made].address = address;
+    g_made[g_n_made].capacity = capacity;
+    return &g_made[g_n_made++];
+}
+
+static const struct JNINativeInterface_ g_table = {find_class, throw_new, buf_address, buf_capacity, new_direct};
 static JNIEnv g_env = &g_table;
 
 JNIEXPORT JNIEnv* jni_mock_env(void) { return &g_env; }

@@ -108,3 +108,33 @@ def test_bad_piece_leaves_state_untouched():
     for r in range(16):
         assert (g2[i:i + 512] == want[fb[r] + 512:fb[r + 1]]).all()
         i += 512
+
+
+def test_host_alloc_buffers_and_foreign_pinned_memory():
+    """Batch and PCM in jaad_host_alloc memory (DMA straight from it), then the same batch in
+    memory page-locked by someone else (torch's pinned allocator) passed to jaad_host_register,
+    which records it without registering it again; both equal the device entry."""
+    p = N.synth_params(2, n_streams=10, frames_per_stream=1000)
+    b = N.synth_batch(p)
+    cfg = N.make_cfg()
+    want = _device_decode(cfg, b, 10, N.PCM_BIG_ENDIAN)
+    with N.Context(cfg, 10) as ctx:
+        hb = ctx.host_batch(b)
+        out = ctx.host_array((b.n_frames, 4096))
+        ctx.decode(hb, out=out)
+        assert (out == want).all()
+        ctx.free_host(hb.q, hb.sf, hb.cb, hb.ics, hb.ms_used, out)
+        with pytest.raises(N.JaadError):
+            ctx.free_host(hb.q)  # freed already
+    with N.Context(cfg, 10) as ctx:
+        def pin(a):
+            raw = np.ascontiguousarray(a).reshape(-1).view(np.uint8)
+            return torch.from_numpy(raw).pin_memory().numpy().view(a.dtype).reshape(a.shape)
+        tb = N.Batch(pin(b.q), pin(b.sf), pin(b.cb), pin(b.ics), pin(b.ms_used), None, b.stream_slot, b.frame_begin,
+                     b.nch)
+        out2 = torch.empty(b.n_frames * 4096, dtype=torch.uint8).pin_memory().numpy().reshape(b.n_frames, 4096)
+        arrays = [tb.q, tb.sf, tb.cb, tb.ics, tb.ms_used, out2]
+        ctx.register(*arrays)
+        ctx.decode(tb, out=out2)
+        ctx.unregister(*arrays)
+    assert (out2 == want).all()

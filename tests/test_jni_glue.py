@@ -32,8 +32,11 @@ def _lib():
     decode = getattr(L, PFX + "nativeDecode")
     decode.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_int32, C.c_int32] + [C.c_void_p] * 10 + [C.c_int32]
     getattr(L, PFX + "nativeReset").argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32]
-    for name in ("nativeRegister", "nativeUnregister"):
+    for name in ("nativeRegister", "nativeUnregister", "nativeFreeDirect"):
         getattr(L, PFX + name).argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p]
+    alloc = getattr(L, PFX + "nativeAllocDirect")
+    alloc.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int64]
+    alloc.restype = C.c_void_p
     return L
 
 
@@ -55,7 +58,7 @@ def _buf(a, keep):
 def test_exports():
     L = _lib()
     for name in ("nativeCreate", "nativeDestroy", "nativeDecode", "nativeReset", "nativeRegister",
-                 "nativeUnregister"):
+                 "nativeUnregister", "nativeAllocDirect", "nativeFreeDirect"):
         assert hasattr(L, PFX + name)
 
 
@@ -72,10 +75,13 @@ def test_invalid_handles_throw_aac_exception():
     assert _exception(L) is None
     a = np.zeros(64, np.uint8)
     b = Buf(a.ctypes.data, a.nbytes)
-    for name in ("nativeRegister", "nativeUnregister"):
+    for name in ("nativeRegister", "nativeUnregister", "nativeFreeDirect"):
         getattr(L, PFX + name)(env, None, 0, C.addressof(b))
         cls, msg = _exception(L)
         assert cls == AAC_EXC and N.strerror(N.ERR_INVALID_ARG) in msg
+    assert getattr(L, PFX + "nativeAllocDirect")(env, None, 0, 4096) is None
+    cls, msg = _exception(L)
+    assert cls == AAC_EXC and N.strerror(N.ERR_INVALID_ARG) in msg
 
 
 def test_create_without_gpu_throws_no_device():
@@ -151,5 +157,23 @@ def test_decode_through_direct_buffers_and_capacity_checks():
         assert cls == AAC_EXC and N.strerror(N.ERR_BITSTREAM) in msg
         getattr(L, PFX + "nativeReset")(env, None, h, 1)
         assert _exception(L) is None
+        # PCM into a direct buffer over context-owned page-locked memory (nativeAllocDirect)
+        db = getattr(L, PFX + "nativeAllocDirect")(env, None, h, want.nbytes)
+        assert db and _exception(L) is None
+        mb = Buf.from_address(db)
+        assert mb.capacity == want.nbytes
+        args4 = list(args)
+        args4[9] = db
+        for slot in range(3):
+            getattr(L, PFX + "nativeReset")(env, None, h, slot)
+        decode(env, None, h, b.n_frames, len(b.stream_slot), 2, *args4, N.PCM_BIG_ENDIAN)
+        assert _exception(L) is None
+        got = np.ctypeslib.as_array((C.c_uint8 * want.nbytes).from_address(mb.address)).reshape(want.shape)
+        assert (got == want).all()
+        getattr(L, PFX + "nativeFreeDirect")(env, None, h, db)
+        assert _exception(L) is None
+        getattr(L, PFX + "nativeFreeDirect")(env, None, h, db)  # freed already
+        cls, msg = _exception(L)
+        assert cls == AAC_EXC and N.strerror(N.ERR_INVALID_ARG) in msg
     finally:
         getattr(L, PFX + "nativeDestroy")(env, None, h)
