@@ -210,6 +210,30 @@ typedef struct jaad_sbr_frame {
 } jaad_sbr_frame;                  /* 1968 bytes */
 
 /*
+ * Dependent coupling (coupling_channel_element, A/syntax/CCE.java).  A CCE's ICStream is carried
+ * as a record in jaad_batch.cce_q/cce_sf/cce_cb/cce_ics (the same layouts as the channel records;
+ * its spectrum is ICStream.decodeSpectralData's, PNS from cce_ics.pns_state).  Each application
+ * of CCE.applyDependentCoupling (:188-215) to a target channel, as
+ * ChannelElement.processDependentCoupling (A/syntax/ChannelElement.java:105-130) makes them, is one
+ * term: target[k] += gain[idx] * cce_spectrum[k] over the CCE's bands idx = g*max_sfb+sfb whose
+ * sfbCB != ZERO_HCB (all windows of the group).  Terms of a frame are listed in the reference's
+ * order (CCEs in bitstream order, then coupled targets in order).  The reference applies them
+ * after M/S and I/S in two passes, every point-0 (BEFORE_TNS) term, TNS, then every point-1
+ * (AFTER_TNS) term; the library does the same.  The reference's TNS is a no-op, so only the order
+ * of the additions tells the points apart in JAAD_TNS_COMPAT mode (JAAD_TNS_SPEC batches with
+ * terms are refused).  Independent switching
+ * CCEs (ind_sw_cce_flag) never apply in the reference (couplingPoint becomes 3, matching neither
+ * BEFORE_TNS, AFTER_TNS nor AFTER_IMDCT: CCE.java:113-129), so they produce no terms.
+ */
+typedef struct jaad_cce_term {
+    uint32_t frame;    /* batch frame (terms sorted by frame)                                  */
+    uint8_t channel;   /* target channel within the frame (0 .. channels-1)                      */
+    uint8_t point;     /* 0 BEFORE_TNS, 1 AFTER_TNS                                               */
+    uint16_t cce;      /* CCE record (index into cce_q / cce_sf / cce_cb / cce_ics)               */
+    float gain[120];   /* CCE.gain[index][idx] for idx < groups * max_sfb of the CCE's ICS       */
+} jaad_cce_term;       /* 488 bytes */
+
+/*
  * A batch: n_frames frames (raw_data_blocks) of one channel configuration.  Frames are grouped
  * in runs: run r holds consecutive-in-time frames [frame_begin[r], frame_begin[r+1]) of the
  * stream whose persistent DSP state (IMDCT overlap, ...) lives in context slot stream_slot[r].
@@ -237,6 +261,15 @@ typedef struct jaad_batch {
     const uint64_t* ms_used;      /* [dev] [frame][2] bit idx = g*max_sfb+sfb (CPE only, else NULL) */
     const jaad_tns* tns;          /* [dev] [ch-frame] or NULL when no ch-frame sets JAAD_ICS_TNS    */
     const jaad_sbr_frame* sbr;    /* host [frame] when cfg.sbr, else NULL                            */
+    /* dependent coupling (jaad_cce_term above); all zero / NULL for a batch without CCEs.  AAC-LC
+       configurations in JAAD_TNS_COMPAT mode only (JAAD_ERR_UNSUPPORTED otherwise). */
+    uint32_t n_cce;               /* CCE records                                                    */
+    uint32_t n_cce_terms;
+    const int16_t* cce_q;         /* [dev] [n_cce][1024]                                            */
+    const uint8_t* cce_sf;        /* [dev] [n_cce][128]                                             */
+    const uint8_t* cce_cb;        /* [dev] [n_cce][128]                                             */
+    const jaad_ics_info* cce_ics; /* [dev] [n_cce]                                                  */
+    const jaad_cce_term* cce_terms; /* host [n_cce_terms]                                           */
 } jaad_batch;
 
 typedef struct jaad_ctx jaad_ctx;
@@ -263,7 +296,7 @@ int jaad_ctx_core_channels(const jaad_ctx* ctx);
  * Replaces the per-frame Decoder.decodeFrame(byte[], SampleBuffer) (A/Decoder.java:131-150)
  * for a batch of already parsed frames.  The side info is range-checked first
  * (JAAD_ERR_BITSTREAM, every slot's state left as before the call).  An AAC-LC batch of
- * >= 8192 frames is cut into run-aligned pieces whose copies and kernels overlap; caller
+ * >= 4096 frames is cut into run-aligned pieces whose copies and kernels overlap; caller
  * buffers registered with jaad_host_register are copied by DMA directly, others through
  * page-locked staging.                                                                      */
 int jaad_decode_batch(jaad_ctx* ctx, const jaad_batch* batch, void* pcm_out, size_t pcm_bytes,

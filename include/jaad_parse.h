@@ -91,6 +91,17 @@ typedef struct jaad_frame_out {
     uint64_t* ms_used;     /* [2], CPE only */
     jaad_tns* tns;         /* [nch] or NULL */
     jaad_sbr_frame* sbr;   /* [1] when cfg.sbr */
+    /* coupling channel elements (CCE.decode, A/syntax/CCE.java:112-175): NULL cce_q makes a frame
+       with a CCE JAAD_ERR_UNSUPPORTED.  Records go to cce_q/sf/cb/ics (up to cce_cap), the terms
+       the frame's CCEs apply (jaad_gpu.h jaad_cce_term; frame 0, cce relative to this frame's
+       records, in the reference's order) to cce_terms (up to term_cap). */
+    int16_t* cce_q;        /* [cce_cap][1024] */
+    uint8_t* cce_sf;       /* [cce_cap][128]  */
+    uint8_t* cce_cb;       /* [cce_cap][128]  */
+    jaad_ics_info* cce_ics; /* [cce_cap]      */
+    jaad_cce_term* cce_terms; /* [term_cap]   */
+    uint32_t cce_cap, term_cap;
+    uint32_t n_cce, n_cce_terms; /* out */
 } jaad_frame_out;
 
 /* Parse one raw_data_block (SyntacticElements.decode) into *out.  On error nothing of the

@@ -147,10 +147,10 @@ private:
 // H2D copy, kernels and D2H copy overlap on three streams; pageable caller memory goes through
 // kStageSlots page-locked staging slots per direction.
 #ifndef JAAD_MAX_PIECES
-#define JAAD_MAX_PIECES 8
+#define JAAD_MAX_PIECES 12
 #endif
 #ifndef JAAD_MIN_PIECE_FRAMES
-#define JAAD_MIN_PIECE_FRAMES 4096
+#define JAAD_MIN_PIECE_FRAMES 2048
 #endif
 constexpr int kMaxPieces = JAAD_MAX_PIECES, kStageSlots = 2;
 enum : int { kPinRegistered = 0, kPinForeign = 1, kPinOwned = 2 };
@@ -247,6 +247,8 @@ struct jaad_ctx {
     PinnedBuf stage_in[kStageSlots], stage_out[kStageSlots];
     DevBuf d_flag;                                 // |q| check result of a host-buffer call (device)
     PinnedBuf h_flag;
+    DevBuf d_cce;                                  // coupling: term offsets / meta / gains, then addends
+    PinnedBuf h_cce;                               // their host image
     std::unique_ptr<WorkerPool> io;                // validation / staging copies
     struct PinRange {
         uintptr_t p;
@@ -862,6 +864,61 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
     return JAAD_OK;
 }
 
+// Dependent coupling of a batch (jaad_gpu.h jaad_cce_term): the terms' frame ranges, targets and
+// band gains go to the device with one copy, cce_term_kernel turns each term into its addend, and
+// the LC kernel (mode 2) adds a frame's addends to its target channels after M/S and I/S.
+int setup_coupling(jaad_ctx* ctx, const jaad_batch* db, KernelArgs& a, hipStream_t stream)
+{
+    const uint32_t nt = db->n_cce_terms, nf = db->n_frames;
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const size_t o_off = 0, o_meta = al(4 * ((size_t)nf + 1)), o_gain = al(o_meta + 4 * (size_t)nt);
+    const size_t o_spec = al(o_gain + 480 * (size_t)nt), total = o_spec + 4096 * (size_t)nt;
+    HIPCHK(ctx->d_cce.ensure(total + 256));
+    if (ctx->done_live) HIPCHK(hipEventSynchronize(ctx->done));  // the previous call's copy of the image is done
+    HIPCHK(ctx->h_cce.ensure(o_spec));
+    char* h = static_cast<char*>(ctx->h_cce.p);
+    uint32_t* off = reinterpret_cast<uint32_t*>(h + o_off);
+    uint32_t* meta = reinterpret_cast<uint32_t*>(h + o_meta);
+    float* gain = reinterpret_cast<float*>(h + o_gain);
+    // a frame's terms in application order: every BEFORE_TNS term, then every AFTER_TNS term (the
+    // two processDependentCoupling passes, A/syntax/CPE.java:172-179), each pass in list order
+    uint32_t t = 0, o = 0;
+    for (uint32_t f = 0; f <= nf; f++) {  // terms are sorted by frame (check_batch)
+        off[f] = o;
+        uint32_t e = t;
+        while (f < nf && e < nt && db->cce_terms[e].frame == f) e++;
+        for (uint32_t point = 0; point < 2; point++)
+            for (uint32_t i = t; i < e; i++) {
+                const jaad_cce_term& T = db->cce_terms[i];
+                if (T.point != point) continue;
+                meta[o] = (uint32_t)T.cce | ((uint32_t)T.channel << 16);
+                std::memcpy(gain + (size_t)o * 120, T.gain, 480);
+                o++;
+            }
+        t = e;
+    }
+    char* d = static_cast<char*>(ctx->d_cce.p);
+    HIPCHK(hipMemcpyAsync(d, h, o_spec, hipMemcpyHostToDevice, stream));
+    CceArgs c{};
+    c.q = db->cce_q;
+    c.sf = db->cce_sf;
+    c.cb = db->cce_cb;
+    c.ics = db->cce_ics;
+    c.meta = reinterpret_cast<const uint32_t*>(d + o_meta);
+    c.gain = reinterpret_cast<const float*>(d + o_gain);
+    c.spec = reinterpret_cast<float*>(d + o_spec);
+    c.iq_table = ctx->d_iq;
+    c.tables = ctx->d_tables;
+    c.gtab = ctx->d_gtab;
+    c.n_terms = nt;
+    HIPCHK(launch_cce_terms(c, stream));
+    a.cce_off = reinterpret_cast<const uint32_t*>(d + o_off);
+    a.cce_meta = c.meta;
+    a.cce_spec = c.spec;
+    a.ch0 = 0;
+    return JAAD_OK;
+}
+
 int launch_work(jaad_ctx* ctx, const jaad_batch* db, void* pcm, uint32_t flags, hipStream_t stream)
 {
     int rc = plan(ctx, db, stream);
@@ -892,6 +949,7 @@ int launch_work(jaad_ctx* ctx, const jaad_batch* db, void* pcm, uint32_t flags, 
     a.dbg = ctx->dbg;
     a.dbg_frame = ctx->dbg_frame;
     if (a.n_chunks == 0) return JAAD_OK;
+    if (db->n_cce_terms && (rc = setup_coupling(ctx, db, a, stream))) return rc;
     if (ctx->n_elem > 1) {
         // Multichannel: each element decodes from its own channel-frame columns (stride = all
         // channels) and its own state region into planar f32 columns; one pack pass then
@@ -914,6 +972,7 @@ int launch_work(jaad_ctx* ctx, const jaad_batch* db, void* pcm, uint32_t flags, 
             e.state_out = a.state_out + region;
             e.pcm = static_cast<float*>(ctx->d_time.p) + (size_t)ch0 * 1024;
             e.out_mode = kOutPlanarF32;
+            e.ch0 = (uint32_t)ch0;
             if ((rc = carry_untouched(ctx, e.state_out, e.state_in, 2048, stream))) return rc;
             HIPCHK(launch_lc(e, stream, tns_spec));
             ch0 += n;
@@ -1160,6 +1219,8 @@ void jaad_ctx_destroy(jaad_ctx* ctx)
     for (auto& st : ctx->stage_out) st.release();
     ctx->d_flag.release();
     ctx->h_flag.release();
+    ctx->d_cce.release();
+    ctx->h_cce.release();
     for (const auto& r : ctx->pinned) {
         if (r.kind == kPinRegistered) (void)hipHostUnregister(reinterpret_cast<void*>(r.p));
         if (r.kind == kPinOwned) (void)hipHostFree(reinterpret_cast<void*>(r.p));
@@ -1183,6 +1244,15 @@ static int check_batch(const jaad_ctx* ctx, const jaad_batch* b, size_t pcm_byte
     if (ctx->cfg.sbr && b->n_frames && !b->sbr) return JAAD_ERR_INVALID_ARG;
     if (pcm_bytes < pcm_bytes_per_frame(ctx, flags) * b->n_frames) return JAAD_ERR_INVALID_ARG;
     if (flags & ~(uint32_t)(JAAD_PCM_LITTLE_ENDIAN | JAAD_PCM_FLOAT32)) return JAAD_ERR_INVALID_ARG;
+    if (b->n_cce_terms) {  // dependent coupling: AAC-LC in TNS compat mode (jaad_gpu.h)
+        if (ctx->cfg.sbr || ctx->cfg.tns_mode != JAAD_TNS_COMPAT) return JAAD_ERR_UNSUPPORTED;
+        if (!b->cce_terms || !b->n_cce || !b->cce_q || !b->cce_sf || !b->cce_cb || !b->cce_ics) return JAAD_ERR_INVALID_ARG;
+        for (uint32_t t = 0; t < b->n_cce_terms; t++) {
+            const jaad_cce_term& T = b->cce_terms[t];
+            if (T.frame >= b->n_frames || (t && T.frame < b->cce_terms[t - 1].frame)) return JAAD_ERR_INVALID_ARG;
+            if (T.channel >= ctx->nch || T.point > 1 || T.cce >= b->n_cce) return JAAD_ERR_INVALID_ARG;
+        }
+    }
     return JAAD_OK;
 }
 
@@ -1279,12 +1349,22 @@ static int decode_batch_serial(jaad_ctx* ctx, const jaad_batch* b, void* pcm_out
         if (!side_info_ok(ctx, b, c0, c1) || !q_ok_copy(b->q + c0 * 1024, nullptr, (c1 - c0) * 1024)) bad = true;
     });
     if (bad) return JAAD_ERR_BITSTREAM;
+    if (b->n_cce_terms) {  // the CCE records get the channel records' checks
+        jaad_batch cb = *b;
+        cb.ics = b->cce_ics;
+        cb.tns = nullptr;
+        if (!side_info_ok(ctx, &cb, 0, b->n_cce) || !q_ok_copy(b->cce_q, nullptr, (size_t)b->n_cce * 1024))
+            return JAAD_ERR_BITSTREAM;
+    }
     // one staging allocation, 256-B aligned sub-buffers
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     size_t o_q = 0, o_sf = al(o_q + ncf * 2048), o_cb = al(o_sf + ncf * 128), o_ics = al(o_cb + ncf * 128);
     const size_t ms_bytes = nf * 16 * (size_t)std::max(ctx->n_cpe, 1);
     size_t o_ms = al(o_ics + ncf * sizeof(jaad_ics_info)), o_tns = al(o_ms + ms_bytes);
-    size_t total = al(o_tns + (b->tns ? ncf * sizeof(jaad_tns) : 0));
+    const size_t nce = b->n_cce_terms ? b->n_cce : 0;  // CCE records (coupling batches)
+    size_t o_cq = al(o_tns + (b->tns ? ncf * sizeof(jaad_tns) : 0)), o_csf = al(o_cq + nce * 2048);
+    size_t o_ccb = al(o_csf + nce * 128), o_cics = al(o_ccb + nce * 128);
+    size_t total = al(o_cics + nce * sizeof(jaad_ics_info));
     HIPCHK(ctx->d_batch.ensure(total + 256));
     size_t pbytes = pcm_bytes_per_frame(ctx, flags) * nf;
     HIPCHK(ctx->d_pcm.ensure(pbytes + 256));
@@ -1297,6 +1377,12 @@ static int decode_batch_serial(jaad_ctx* ctx, const jaad_batch* b, void* pcm_out
         HIPCHK(hipMemcpyAsync(base + o_ics, b->ics, ncf * sizeof(jaad_ics_info), hipMemcpyHostToDevice, s));
         if (b->ms_used) HIPCHK(hipMemcpyAsync(base + o_ms, b->ms_used, ms_bytes, hipMemcpyHostToDevice, s));
         if (b->tns) HIPCHK(hipMemcpyAsync(base + o_tns, b->tns, ncf * sizeof(jaad_tns), hipMemcpyHostToDevice, s));
+        if (nce) {
+            HIPCHK(hipMemcpyAsync(base + o_cq, b->cce_q, nce * 2048, hipMemcpyHostToDevice, s));
+            HIPCHK(hipMemcpyAsync(base + o_csf, b->cce_sf, nce * 128, hipMemcpyHostToDevice, s));
+            HIPCHK(hipMemcpyAsync(base + o_ccb, b->cce_cb, nce * 128, hipMemcpyHostToDevice, s));
+            HIPCHK(hipMemcpyAsync(base + o_cics, b->cce_ics, nce * sizeof(jaad_ics_info), hipMemcpyHostToDevice, s));
+        }
     }
     jaad_batch db = *b;
     db.q = reinterpret_cast<const int16_t*>(base + o_q);
@@ -1305,6 +1391,12 @@ static int decode_batch_serial(jaad_ctx* ctx, const jaad_batch* b, void* pcm_out
     db.ics = reinterpret_cast<const jaad_ics_info*>(base + o_ics);
     db.ms_used = b->ms_used ? reinterpret_cast<const uint64_t*>(base + o_ms) : nullptr;
     db.tns = b->tns ? reinterpret_cast<const jaad_tns*>(base + o_tns) : nullptr;
+    if (nce) {
+        db.cce_q = reinterpret_cast<const int16_t*>(base + o_cq);
+        db.cce_sf = reinterpret_cast<const uint8_t*>(base + o_csf);
+        db.cce_cb = reinterpret_cast<const uint8_t*>(base + o_ccb);
+        db.cce_ics = reinterpret_cast<const jaad_ics_info*>(base + o_cics);
+    }
     int rc = launch(ctx, &db, ctx->d_pcm.p, flags, s);
     if (rc) return rc;
     if (nf) HIPCHK(hipMemcpyAsync(pcm_out, ctx->d_pcm.p, pbytes, hipMemcpyDeviceToHost, s));
@@ -1506,7 +1598,8 @@ int jaad_decode_batch(jaad_ctx* ctx, const jaad_batch* b, void* pcm_out, size_t 
     if (!pcm_out && b->n_frames) return JAAD_ERR_INVALID_ARG;
     HIPCHK(hipSetDevice(ctx->device));
     if ((rc = io_setup(ctx))) return rc;
-    if (ctx->cfg.sbr || ctx->n_elem > 1 || b->n_frames < 2 * kMinPieceFrames || !b->stream_slot || !b->frame_begin)
+    if (ctx->cfg.sbr || ctx->n_elem > 1 || b->n_cce_terms || b->n_frames < 2 * kMinPieceFrames || !b->stream_slot ||
+        !b->frame_begin)
         return decode_batch_serial(ctx, b, pcm_out, flags);
     // the run layout is checked by plan(); pieces need it sane before cutting
     if (b->frame_begin[0] != 0 || b->frame_begin[b->n_runs] != b->n_frames) return JAAD_ERR_INVALID_ARG;

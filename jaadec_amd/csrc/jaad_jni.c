@@ -59,18 +59,16 @@ JNIEXPORT void JNICALL Java_net_sourceforge_jaad_aac_gpu_GpuDSP_nativeDestroy(JN
     jaad_ctx_destroy((jaad_ctx*)(intptr_t)h);
 }
 
-/* static native void nativeDecode(long h, int nFrames, int nRuns, int nch, ByteBuffer streamSlot,
- *     ByteBuffer frameBegin, ByteBuffer q, ByteBuffer sf, ByteBuffer cb, ByteBuffer ics,
- *     ByteBuffer msUsed, ByteBuffer tns, ByteBuffer sbr, ByteBuffer pcm, int flags);
- * nch: channels per ch-frame record (1 SCE core, 2 CPE core); must equal the context's
- * (jaad_ctx_core_channels), since every buffer capacity below is checked against it.
- * sbr: one jaad_sbr_frame (1968 B, sizeof(jaad_sbr_frame)) per frame for SBR/PS streams, else null */
-JNIEXPORT void JNICALL Java_net_sourceforge_jaad_aac_gpu_GpuDSP_nativeDecode(
-    JNIEnv* env, jclass cls, jlong h, jint n_frames, jint n_runs, jint nch, jobject stream_slot, jobject frame_begin,
-    jobject q, jobject sf, jobject cb, jobject ics, jobject ms_used, jobject tns, jobject sbr, jobject pcm, jint flags) {
-    (void)cls;
-    jaad_ctx* ctx = (jaad_ctx*)(intptr_t)h;
-    if (!ctx || n_frames < 0 || n_runs < 0 || nch != jaad_ctx_core_channels(ctx)) {
+/* ms_used pairs per frame: one per CPE of the configuration (core channels 2: 1; 3, 4: 1; 5, 6: 2;
+ * 8: 3; mono: none) */
+static int cpe_count(int nch) { return nch == 1 ? 0 : nch <= 4 ? 1 : nch <= 6 ? 2 : 3; }
+
+/* the batch of a decode call; with n_terms > 0 the coupling records and terms too */
+static void decode_common(JNIEnv* env, jaad_ctx* ctx, jint n_frames, jint n_runs, jint nch, jobject stream_slot,
+                          jobject frame_begin, jobject q, jobject sf, jobject cb, jobject ics, jobject ms_used,
+                          jobject tns, jobject sbr, jobject pcm, jint flags, jint n_cce, jint n_terms, jobject cce_q,
+                          jobject cce_sf, jobject cce_cb, jobject cce_ics, jobject cce_terms) {
+    if (!ctx || n_frames < 0 || n_runs < 0 || n_cce < 0 || n_terms < 0 || nch != jaad_ctx_core_channels(ctx)) {
         throw_aac(env, ctx, JAAD_ERR_INVALID_ARG);
         return;
     }
@@ -85,18 +83,57 @@ JNIEXPORT void JNICALL Java_net_sourceforge_jaad_aac_gpu_GpuDSP_nativeDecode(
     b.sf = (const uint8_t*)addr(env, sf, 128LL * ncf);
     b.cb = (const uint8_t*)addr(env, cb, 128LL * ncf);
     b.ics = (const jaad_ics_info*)addr(env, ics, (jlong)sizeof(jaad_ics_info) * ncf);
-    b.ms_used = (const uint64_t*)addr(env, ms_used, 16LL * n_frames);
+    b.ms_used = (const uint64_t*)addr(env, ms_used, 16LL * n_frames * (cpe_count(nch) ? cpe_count(nch) : 1));
     b.tns = (const jaad_tns*)addr(env, tns, (jlong)sizeof(jaad_tns) * ncf);
     b.sbr = (const jaad_sbr_frame*)addr(env, sbr, (jlong)sizeof(jaad_sbr_frame) * n_frames);
+    if (n_terms) {
+        b.n_cce = (uint32_t)n_cce;
+        b.n_cce_terms = (uint32_t)n_terms;
+        b.cce_q = (const int16_t*)addr(env, cce_q, 2048LL * n_cce);
+        b.cce_sf = (const uint8_t*)addr(env, cce_sf, 128LL * n_cce);
+        b.cce_cb = (const uint8_t*)addr(env, cce_cb, 128LL * n_cce);
+        b.cce_ics = (const jaad_ics_info*)addr(env, cce_ics, (jlong)sizeof(jaad_ics_info) * n_cce);
+        b.cce_terms = (const jaad_cce_term*)addr(env, cce_terms, (jlong)sizeof(jaad_cce_term) * n_terms);
+    }
     jlong pcm_cap = pcm ? (*env)->GetDirectBufferCapacity(env, pcm) : -1;
     void* out = pcm ? (*env)->GetDirectBufferAddress(env, pcm) : NULL;
-    if (!ctx || !b.stream_slot || !b.frame_begin || !b.q || !b.sf || !b.cb || !b.ics || !out || pcm_cap < 0 ||
-        (ms_used && !b.ms_used) || (tns && !b.tns) || (sbr && !b.sbr)) {
+    if (!b.stream_slot || !b.frame_begin || !b.q || !b.sf || !b.cb || !b.ics || !out || pcm_cap < 0 ||
+        (ms_used && !b.ms_used) || (tns && !b.tns) || (sbr && !b.sbr) ||
+        (n_terms && (!b.cce_q || !b.cce_sf || !b.cce_cb || !b.cce_ics || !b.cce_terms))) {
         throw_aac(env, ctx, JAAD_ERR_INVALID_ARG);
         return;
     }
     int rc = jaad_decode_batch(ctx, &b, out, (size_t)pcm_cap, (uint32_t)flags);
     if (rc) throw_aac(env, ctx, rc);
+}
+
+/* static native void nativeDecode(long h, int nFrames, int nRuns, int nch, ByteBuffer streamSlot,
+ *     ByteBuffer frameBegin, ByteBuffer q, ByteBuffer sf, ByteBuffer cb, ByteBuffer ics,
+ *     ByteBuffer msUsed, ByteBuffer tns, ByteBuffer sbr, ByteBuffer pcm, int flags);
+ * nch: channels per frame (1 SCE core, 2 CPE core, 3..8 multichannel); must equal the context's
+ * (jaad_ctx_core_channels), since every buffer capacity below is checked against it.
+ * sbr: one jaad_sbr_frame (1968 B, sizeof(jaad_sbr_frame)) per frame for SBR/PS streams, else null */
+JNIEXPORT void JNICALL Java_net_sourceforge_jaad_aac_gpu_GpuDSP_nativeDecode(
+    JNIEnv* env, jclass cls, jlong h, jint n_frames, jint n_runs, jint nch, jobject stream_slot, jobject frame_begin,
+    jobject q, jobject sf, jobject cb, jobject ics, jobject ms_used, jobject tns, jobject sbr, jobject pcm, jint flags) {
+    (void)cls;
+    decode_common(env, (jaad_ctx*)(intptr_t)h, n_frames, n_runs, nch, stream_slot, frame_begin, q, sf, cb, ics, ms_used,
+                  tns, sbr, pcm, flags, 0, 0, NULL, NULL, NULL, NULL, NULL);
+}
+
+/* static native void nativeDecodeCoupled(long h, int nFrames, int nRuns, int nch, ByteBuffer streamSlot,
+ *     ByteBuffer frameBegin, ByteBuffer q, ByteBuffer sf, ByteBuffer cb, ByteBuffer ics,
+ *     ByteBuffer msUsed, ByteBuffer tns, ByteBuffer pcm, int flags, int nCce, int nTerms,
+ *     ByteBuffer cceQ, ByteBuffer cceSf, ByteBuffer cceCb, ByteBuffer cceIcs, ByteBuffer cceTerms);
+ * an AAC-LC batch with coupling channel elements: nCce CCE ICStream records and nTerms
+ * jaad_cce_term (488 B) in the reference's order (jaad_gpu.h) */
+JNIEXPORT void JNICALL Java_net_sourceforge_jaad_aac_gpu_GpuDSP_nativeDecodeCoupled(
+    JNIEnv* env, jclass cls, jlong h, jint n_frames, jint n_runs, jint nch, jobject stream_slot, jobject frame_begin,
+    jobject q, jobject sf, jobject cb, jobject ics, jobject ms_used, jobject tns, jobject pcm, jint flags, jint n_cce,
+    jint n_terms, jobject cce_q, jobject cce_sf, jobject cce_cb, jobject cce_ics, jobject cce_terms) {
+    (void)cls;
+    decode_common(env, (jaad_ctx*)(intptr_t)h, n_frames, n_runs, nch, stream_slot, frame_begin, q, sf, cb, ics, ms_used,
+                  tns, NULL, pcm, flags, n_cce, n_terms, cce_q, cce_sf, cce_cb, cce_ics, cce_terms);
 }
 
 JNIEXPORT void JNICALL Java_net_sourceforge_jaad_aac_gpu_GpuDSP_nativeReset(JNIEnv* env, jclass cls, jlong h,

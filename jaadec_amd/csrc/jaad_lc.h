@@ -75,6 +75,28 @@ struct KernelArgs {
     uint32_t tns_mode;          // JAAD_TNS_*
     float* dbg;                 // internal: stage dump of frame dbg_frame of chunk 0 (or null)
     int dbg_frame;
+    // dependent coupling (CCE terms, jaad_gpu.h jaad_cce_term): null cce_off = none.  Frame f's
+    // terms are [cce_off[f], cce_off[f+1]); term t targets frame channel cce_meta[t] >> 16 and adds
+    // cce_spec[t][0..1023] (cce_term_kernel); ch0 = this launch's first channel of the frame
+    const uint32_t* cce_off;
+    const uint32_t* cce_meta;
+    const float* cce_spec;
+    uint32_t ch0;
+};
+
+// inputs of cce_term_kernel: one wave per term
+struct CceArgs {
+    const int16_t* q;           // CCE records (jaad_batch.cce_*)
+    const uint8_t* sf;
+    const uint8_t* cb;
+    const jaad_ics_info* ics;
+    const uint32_t* meta;       // [term]: CCE record (bits 0..15) | target channel << 16
+    const float* gain;          // [term][120]
+    float* spec;                // out: [term][1024] addend, -0.0 where the reference adds nothing
+    const float* iq_table;
+    const LdsTables* tables;
+    const GlobalTables* gtab;
+    uint32_t n_terms;
 };
 
 // IFFT output position (mod 64) that lane u holds after the register transposes of the long
@@ -102,6 +124,8 @@ constexpr uint32_t kOutPlanarF32 = 4;  // internal output mode: core time sample
 
 // one wave per chunk (grid derived from a.n_chunks)
 hipError_t launch_lc(const KernelArgs& a, hipStream_t stream, bool tns_spec);
+// the addends of a batch's coupling terms (CCE spectrum x band gain)
+hipError_t launch_cce_terms(const CceArgs& a, hipStream_t stream);
 // |q| <= 8190 over n int16 values (IQ_TABLE has 8191 entries; the reference's array index would
 // throw): any value beyond sets *flag to 1 (plain stores; *flag is cleared by the caller)
 hipError_t launch_check_q(const int16_t* q, size_t n, int* flag, hipStream_t stream);

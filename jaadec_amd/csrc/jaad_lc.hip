@@ -285,6 +285,31 @@ __device__ __forceinline__ void xch(float& a, float& b, int u)
         a = __int_as_float(__builtin_amdgcn_update_dpp(ia, ib, 0x124, 0xF, 0xA, false));
         b = __int_as_float(__builtin_amdgcn_update_dpp(ib, ia, 0x12C, 0xF, 0x5, false));
     } else {  // quad_perm lane ^ 2 / lane ^ 1, then a per-lane select
+#ifdef JAAD_XCH_CNDDPP
+        // one v_cndmask_b32 with the swizzle on its DPP source per output (dst = vcc ? src1 : src0):
+        // a' = hi ? swz(b) : a, b' = hi ? b : swz(a); hi = lanes with bit L set
+        (void)u;
+        constexpr uint32_t kHi = L == 1 ? 0xCCCCCCCCu : 0xAAAAAAAAu;
+        int ra, rb;
+        if constexpr (L == 1) {
+            asm("s_mov_b32 vcc_lo, %3\n\ts_mov_b32 vcc_hi, %3\n\ts_nop 1\n\t"
+                "v_cndmask_b32_dpp %0, %1, %2, vcc quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf"
+                : "=&v"(ra) : "v"(ib), "v"(ia), "i"(~kHi) : "vcc");
+            asm("s_mov_b32 vcc_lo, %3\n\ts_mov_b32 vcc_hi, %3\n\ts_nop 1\n\t"
+                "v_cndmask_b32_dpp %0, %1, %2, vcc quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf"
+                : "=&v"(rb) : "v"(ia), "v"(ib), "i"(kHi) : "vcc");
+        } else {
+            asm("s_mov_b32 vcc_lo, %3\n\ts_mov_b32 vcc_hi, %3\n\ts_nop 1\n\t"
+                "v_cndmask_b32_dpp %0, %1, %2, vcc quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf"
+                : "=&v"(ra) : "v"(ib), "v"(ia), "i"(~kHi) : "vcc");
+            asm("s_mov_b32 vcc_lo, %3\n\ts_mov_b32 vcc_hi, %3\n\ts_nop 1\n\t"
+                "v_cndmask_b32_dpp %0, %1, %2, vcc quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf"
+                : "=&v"(rb) : "v"(ia), "v"(ib), "i"(kHi) : "vcc");
+        }
+        a = __int_as_float(ra);
+        b = __int_as_float(rb);
+        return;
+#endif
         constexpr int kCtl = L == 1 ? 0x4E : 0xB1;
         const int pb = __builtin_amdgcn_mov_dpp(ib, kCtl, 0xF, 0xF, true);
         const int pa = __builtin_amdgcn_mov_dpp(ia, kCtl, 0xF, 0xF, true);
@@ -732,6 +757,11 @@ struct alignas(16) BandRec {
     float gl, ms, gr, is;
 };
 constexpr int kNoBand = 127;  // a record index that is always all-zero (bands < 8*15 = 120)
+#ifdef JAAD_IQ_SELECT
+constexpr float kZeroBandGain = 0.0f;
+#else
+constexpr float kZeroBandGain = -0.0f;  // gain of bands that are not spectral (see iq_channel)
+#endif
 
 // record index of the bin quad starting at position p (4-aligned); long windows use the
 // lane's precomputed band byte
@@ -834,7 +864,11 @@ __device__ __forceinline__ void iq_channel(const LdsTables& T, const float* iq_g
 #pragma unroll
     for (int e = 0; e < 16; e++) {
         const float gn = g[e >> 2];
+#ifdef JAAD_IQ_SELECT
         x[e] = gn != 0.0f ? v[e] * gn : 0.0f;
+#else
+        x[e] = v[e] * gn;  // gn = -0.0 for a non-spectral band (kZeroBandGain): -0.0 * -0.0 = +0.0
+#endif
     }
     // escape values beyond the LDS head of IQ_TABLE (|q| >= 1024: rare in real streams and absent
     // from the synthetic ones); global loads, which also wait for the previous frame's PCM stores
@@ -891,9 +925,12 @@ __device__ __forceinline__ void synth_channel(const KernelArgs& A, const LdsTabl
     } while (0)
 #endif
 
-template <bool kTnsSpec, int kOut, bool kStereo>
-__global__ __launch_bounds__(64 * waves_per_wg<kTnsSpec>()) void lc_decode_kernel(KernelArgs A)
+// kMode: 0 = TNS compat (the reference), 1 = spec TNS, 2 = TNS compat with dependent coupling
+template <int kMode, int kOut, bool kStereo>
+__global__ __launch_bounds__(64 * waves_per_wg<kMode == 1>()) void lc_decode_kernel(KernelArgs A)
 {
+    constexpr bool kTnsSpec = kMode == 1;
+    [[maybe_unused]] constexpr bool kCouple = kMode == 2;
     constexpr int kW = waves_per_wg<kTnsSpec>();
     constexpr int kThreads = 64 * kW;
     // one LDS object with the tables first: every table access is a 16-bit immediate offset
@@ -1029,12 +1066,14 @@ __global__ __launch_bounds__(64 * waves_per_wg<kTnsSpec>()) void lc_decode_kerne
                     const bool inL = b < iL.nbands, inR = b < iR.nbands;
                     const bool msbit = (msb >> e) & 1u;
                     const float gvL = T.sf_gain[sfL];
-                    br[e].gl = (inL && cbL != JAAD_ZERO_HCB && cbL < JAAD_NOISE_HCB) ? gvL : 0.0f;
+                    // non-spectral bands get -0.0: q is 0 there and iq_signed[0] = -0.0, so the
+                    // product is the reference's +0.0 (ICStream.java:236-239) without a select
+                    br[e].gl = (inL && cbL != JAAD_ZERO_HCB && cbL < JAAD_NOISE_HCB) ? gvL : kZeroBandGain;
                     br[e].ms = (ms_on && inL && msbit && cbL < JAAD_NOISE_HCB && cbR < JAAD_NOISE_HCB) ? 1.0f : 0.0f;
                     float gr = 0.0f, is = 0.0f;
                     if (stereo) {
                         const float gvR = T.sf_gain[sfR];
-                        gr = (inR && cbR != JAAD_ZERO_HCB && cbR < JAAD_NOISE_HCB) ? gvR : 0.0f;
+                        gr = (inR && cbR != JAAD_ZERO_HCB && cbR < JAAD_NOISE_HCB) ? gvR : kZeroBandGain;
                         if (is_on && inR && (cbR == JAAD_INTENSITY_HCB || cbR == JAAD_INTENSITY_HCB2)) {
                             float cs = cbR == JAAD_INTENSITY_HCB ? 1.0f : -1.0f;
                             if ((iL.flags & JAAD_ICS_MS_PRESENT) && msbit) cs = -cs;
@@ -1127,6 +1166,40 @@ __global__ __launch_bounds__(64 * waves_per_wg<kTnsSpec>()) void lc_decode_kerne
                         for (int i = 0; i < 4; i++) {
                             const int e = 8 * (qd >> 1) + 4 * (qd & 1) + i;
                             xR[e] = xL[e] * isq[qd];
+                        }
+                    }
+                }
+            }
+
+            if constexpr (kCouple) {
+                // dependent coupling after M/S and I/S (CPE.java:172-179, SCE.java:100-108): the
+                // frame's terms in order, each adding its addend (CCE.applyDependentCoupling,
+                // A/syntax/CCE.java:188-215, precomputed by cce_term_kernel; -0.0 adds nothing)
+                const uint32_t t0 = A.cce_off[f], t1 = A.cce_off[f + 1];
+                for (uint32_t t = t0; t < t1; t++) {
+                    const int ch = (int)(A.cce_meta[t] >> 16) - (int)A.ch0;
+                    if (ch < 0 || ch >= nch) continue;
+                    const float4* sp = reinterpret_cast<const float4*>(A.cce_spec + (size_t)t * 1024);
+                    float v[16];
+#pragma unroll
+                    for (int h = 0; h < 2; h++) {
+                        const float4 a = sp[(512 * h + 8 * u) / 4], c = sp[(512 * h + 8 * u) / 4 + 1];
+                        v[8 * h + 0] = a.x;
+                        v[8 * h + 1] = a.y;
+                        v[8 * h + 2] = a.z;
+                        v[8 * h + 3] = a.w;
+                        v[8 * h + 4] = c.x;
+                        v[8 * h + 5] = c.y;
+                        v[8 * h + 6] = c.z;
+                        v[8 * h + 7] = c.w;
+                    }
+                    if (ch == 0) {
+#pragma unroll
+                        for (int e = 0; e < 16; e++) xL[e] += v[e];
+                    } else {
+                        if constexpr (stereo) {
+#pragma unroll
+                            for (int e = 0; e < 16; e++) xR[e] += v[e];
                         }
                     }
                 }
@@ -1241,26 +1314,26 @@ __global__ __launch_bounds__(64 * waves_per_wg<kTnsSpec>()) void lc_decode_kerne
 #endif
 }
 
+template <int kMode, bool kStereo>
+static void launch_lc_mode(const KernelArgs& a, hipStream_t stream)
+{
+    constexpr int W = waves_per_wg<kMode == 1>();
+#define JAAD_LAUNCH(O) \
+    hipLaunchKernelGGL((lc_decode_kernel<kMode, O, kStereo>), dim3((a.n_chunks + W - 1) / W), dim3(64 * W), 0, stream, a)
+    const int o = (a.out_mode == kOutPlanarF32) ? 4 : (a.out_mode & JAAD_PCM_FLOAT32) ? 2 : (a.out_mode & JAAD_PCM_LITTLE_ENDIAN) ? 1 : 0;
+    if (o == 4) JAAD_LAUNCH(kOutPlanarF32);
+    else if (o == 2) JAAD_LAUNCH(JAAD_PCM_FLOAT32);
+    else if (o == 1) JAAD_LAUNCH(JAAD_PCM_LITTLE_ENDIAN);
+    else JAAD_LAUNCH(JAAD_PCM_BIG_ENDIAN);
+#undef JAAD_LAUNCH
+}
+
 template <bool kStereo>
 static hipError_t launch_lc_ch(const KernelArgs& a, hipStream_t stream, bool tns_spec)
 {
-#define JAAD_LAUNCH(T, O)                                                                                           \
-    hipLaunchKernelGGL((lc_decode_kernel<T, O, kStereo>), dim3((a.n_chunks + waves_per_wg<T>() - 1) / waves_per_wg<T>()), \
-                       dim3(64 * waves_per_wg<T>()), 0, stream, a)
-    const int o = (a.out_mode == kOutPlanarF32) ? 4 : (a.out_mode & JAAD_PCM_FLOAT32) ? 2 : (a.out_mode & JAAD_PCM_LITTLE_ENDIAN) ? 1 : 0;
-    if (o == 4) {
-        if (tns_spec) JAAD_LAUNCH(true, kOutPlanarF32);
-        else JAAD_LAUNCH(false, kOutPlanarF32);
-    } else if (tns_spec) {
-        if (o == 2) JAAD_LAUNCH(true, JAAD_PCM_FLOAT32);
-        else if (o == 1) JAAD_LAUNCH(true, JAAD_PCM_LITTLE_ENDIAN);
-        else JAAD_LAUNCH(true, JAAD_PCM_BIG_ENDIAN);
-    } else {
-        if (o == 2) JAAD_LAUNCH(false, JAAD_PCM_FLOAT32);
-        else if (o == 1) JAAD_LAUNCH(false, JAAD_PCM_LITTLE_ENDIAN);
-        else JAAD_LAUNCH(false, JAAD_PCM_BIG_ENDIAN);
-    }
-#undef JAAD_LAUNCH
+    if (a.cce_off) launch_lc_mode<2, kStereo>(a, stream);  // coupling: TNS compat only (jaad_gpu.h)
+    else if (tns_spec) launch_lc_mode<1, kStereo>(a, stream);
+    else launch_lc_mode<0, kStereo>(a, stream);
     return hipGetLastError();
 }
 
@@ -1304,6 +1377,85 @@ __global__ __launch_bounds__(256) void check_q_kernel(const v4i* __restrict__ q,
 }
 }  // namespace
 
+namespace {
+// The addend of one coupling term: the CCE's ICStream spectrum as decodeSpectralData leaves it
+// (A/syntax/ICStream.java:222-272: IQ x scalefactor gain, noise bands from the static LCG at the
+// record's pns_state, ZERO / intensity bands 0) times the term's gain of the band, over the bins of
+// the CCE's bands whose sfbCB != ZERO_HCB (CCE.applyDependentCoupling, A/syntax/CCE.java:188-215:
+// data[k] += x * iqData[k]); every other bin -0.0, which leaves the target as it is.
+__global__ __launch_bounds__(64) void cce_term_kernel(CceArgs A)
+{
+    __shared__ float buf[kWaveBuf];
+    __shared__ uint32_t raw[64];
+    const uint32_t t = blockIdx.x;
+    if (t >= A.n_terms) return;
+    const int u = lane_id();
+    const LdsTables& T = *A.tables;
+    const uint32_t rec = A.meta[t] & 0xFFFFu;
+    const jaad_ics_info ic = A.ics[rec];
+    Ics info;
+    info.seq = ic.window_sequence & 3;
+    info.shape = ic.window_shape & 1;
+    info.shape_prev = ic.window_shape_prev & 1;
+    const int lim = info.seq == JAAD_EIGHT_SHORT_SEQUENCE ? T.nswb_s : T.nswb_l;
+    info.max_sfb = min((int)ic.max_sfb, lim);
+    info.grouping = ic.grouping;
+    info.flags = ic.flags;
+    info.pns = ic.pns_state;
+    const int groups = info.seq == JAAD_EIGHT_SHORT_SEQUENCE ? 8 - __builtin_popcount(info.grouping & 0x7f) : 1;
+    info.nbands = groups * info.max_sfb;
+    raw[u] = reinterpret_cast<const uint32_t*>(u < 32 ? A.sf + (size_t)rec * 128 : A.cb + (size_t)rec * 128)[u & 31];
+    wave_sync();
+    const uint8_t* sfr = reinterpret_cast<const uint8_t*>(raw);
+    const uint8_t* cbr = sfr + 128;
+    const int16_t* q = A.q + (size_t)rec * 1024;
+    const float* gain = A.gain + (size_t)t * 120;
+    float x[16], g[16];
+    bool touched[16];
+#pragma unroll
+    for (int e = 0; e < 16; e++) {
+        const int p = 512 * (e >> 3) + 8 * u + (e & 7);
+        int band = kNoBand;
+        if (info.seq == JAAD_EIGHT_SHORT_SEQUENCE) {
+            band = band_short(T, info, p & ~3);
+        } else {
+            const int b = T.quad2band_l[p >> 2];
+            band = b < info.max_sfb ? b : kNoBand;
+        }
+        x[e] = 0.0f;
+        g[e] = 0.0f;
+        touched[e] = false;
+        if (band == kNoBand) continue;
+        const int c = cbr[band];
+        touched[e] = c != JAAD_ZERO_HCB;
+        g[e] = gain[band];
+        if (c != JAAD_ZERO_HCB && c < JAAD_NOISE_HCB) {
+            const int v = q[p];
+            const int a = min(v < 0 ? -v : v, 8190);
+            const float iq = v > 0 ? A.iq_table[a] : -A.iq_table[a];
+            x[e] = iq * T.sf_gain[sfr[band]];
+        }
+    }
+    if (info.flags & JAAD_ICS_HAS_PNS) {
+        wave_sync();
+        store_spec(buf, u, x);
+        wave_sync();
+        pns_fill(buf, raw, T, *A.gtab, u, info);
+        load_spec(buf, u, x);
+    }
+    float* out = A.spec + (size_t)t * 1024;
+#pragma unroll
+    for (int e = 0; e < 16; e++) out[512 * (e >> 3) + 8 * u + (e & 7)] = touched[e] ? g[e] * x[e] : -0.0f;
+}
+}  // namespace
+
+hipError_t launch_cce_terms(const CceArgs& a, hipStream_t stream)
+{
+    if (!a.n_terms) return hipSuccess;
+    hipLaunchKernelGGL(cce_term_kernel, dim3(a.n_terms), dim3(64), 0, stream, a);
+    return hipGetLastError();
+}
+
 hipError_t launch_check_q(const int16_t* q, size_t n, int* flag, hipStream_t stream)
 {
     const size_t n16 = n / 8;  // q rows are 1024 values: whole 16-byte words
@@ -1330,9 +1482,9 @@ hipError_t launch_lc(const KernelArgs& a, hipStream_t stream, bool tns_spec)
 int lc_resident_waves_per_cu(bool tns_spec)
 {
     int blocks = 0;
-    hipError_t e = tns_spec ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, lc_decode_kernel<true, JAAD_PCM_BIG_ENDIAN, true>,
+    hipError_t e = tns_spec ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, lc_decode_kernel<1, JAAD_PCM_BIG_ENDIAN, true>,
                                                                             64 * waves_per_wg<true>(), 0)
-                            : hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, lc_decode_kernel<false, JAAD_PCM_BIG_ENDIAN, true>,
+                            : hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, lc_decode_kernel<0, JAAD_PCM_BIG_ENDIAN, true>,
                                                                             64 * waves_per_wg<false>(), 0);
     if (e != hipSuccess) return 0;
     return blocks * (tns_spec ? waves_per_wg<true>() : waves_per_wg<false>());

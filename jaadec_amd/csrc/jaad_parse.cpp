@@ -7,6 +7,7 @@
 // as it was.  SBR/PS extension payloads go to jaad_parse_sbr.cpp.
 #include "../../include/jaad_parse.h"
 
+#include <cmath>
 #include <cstring>
 #include <mutex>
 #include <new>
@@ -608,6 +609,137 @@ void jaad_parser_set_pns_state(jaad_parser* p, uint32_t s)
 }  // extern "C"
 
 namespace {
+
+// coupling_channel_element as CCE.decode reads it (A/syntax/CCE.java:112-175)
+struct CceElem {
+    int point = 0;                 // couplingPoint: 0 BEFORE_TNS, 1 AFTER_TNS, 3 (ind_sw: never applied)
+    int count = 0;                 // coupledCount
+    bool pair[8] = {false};
+    int id[8] = {0}, chs[8] = {0};
+    int gain_count = 0;
+    float gain[16][120] = {{0.0f}};
+    int rec = 0;                   // record index in the frame's CCE output
+};
+struct ChElem {                    // a channel element of the frame: SCE / LFE / CPE
+    bool cpe;
+    int tag, ch0;
+};
+
+int read_cce(BitReader& br, const Cfg& C, ParseState& ns, ChOut& o, CceElem& E)
+{
+    static const float kScale[4] = {1.09050773266525765921f, 1.18920711500272106672f, 1.4142135623730950488016887f, 2.0f};
+    if (br.left() < 4) return JAAD_ERR_EOS;
+    E.point = 2 * (int)br.read(1);
+    E.count = (int)br.read(3);
+    E.gain_count = 0;
+    for (int i = 0; i <= E.count; i++) {
+        if (br.left() < 5) return JAAD_ERR_EOS;
+        E.gain_count++;
+        E.pair[i] = br.read(1) != 0;
+        E.id[i] = (int)br.read(4);
+        if (E.pair[i]) {
+            if (br.left() < 2) return JAAD_ERR_EOS;
+            E.chs[i] = (int)br.read(2);
+            if (E.chs[i] == 3) E.gain_count++;
+        } else {
+            E.chs[i] = 2;
+        }
+    }
+    if (br.left() < 4) return JAAD_ERR_EOS;
+    E.point += (int)br.read(1);
+    E.point |= E.point >> 1;
+    const bool sign = br.read(1) != 0;
+    const double scale = kScale[br.read(2)];
+    IcsInfo I;
+    int st = read_ics(br, C, false, I, 0, ns.pns, o);
+    if (st) return st;
+    const Books& B = books();
+    auto sfcode = [&](int& v) {  // Huffman.decodeScaleFactor
+        const int r = B.sf.decode(br);
+        if (r < 0) return r == -2 ? JAAD_ERR_EOS : JAAD_ERR_BITSTREAM;
+        v = JAAD_HCB_SF[r][2];
+        return JAAD_OK;
+    };
+    for (int i = 0; i < E.gain_count; i++) {
+        int cge = 1, xg = 0;
+        float gc = 1.0f;
+        if (i > 0) {
+            if (br.left() < 1 && E.point != 2) return JAAD_ERR_EOS;
+            cge = E.point == 2 ? 1 : (int)br.read(1);
+            if (cge) {
+                if ((st = sfcode(xg))) return st;
+                xg -= 60;
+            }
+            gc = (float)std::pow(scale, (double)-xg);
+        }
+        if (E.point == 2) {
+            E.gain[i][0] = gc;
+            continue;
+        }
+        for (int g = 0, idx = 0; g < I.ngroups; g++)
+            for (int sfb = 0; sfb < I.max_sfb; sfb++, idx++) {
+                if (o.cb[idx] == JAAD_ZERO_HCB) continue;
+                if (cge == 0) {
+                    int t;
+                    if ((st = sfcode(t))) return st;
+                    t -= 60;
+                    if (t != 0) {
+                        int sgn = 1;
+                        t = xg += t;
+                        if (!sign) {
+                            sgn -= 2 * (t & 1);
+                            t >>= 1;
+                        }
+                        gc = (float)(std::pow(scale, (double)-t) * sgn);
+                    }
+                }
+                E.gain[i][idx] = gc;
+            }
+    }
+    return br.overrun() ? JAAD_ERR_EOS : JAAD_OK;
+}
+
+// ChannelElement.processDependentCoupling (A/syntax/ChannelElement.java:105-130) for every channel
+// element of the frame, as terms in the reference's order per target channel
+int cce_terms(const CceElem* cces, int n_cce, const ChElem* els, int n_el, jaad_frame_out* out)
+{
+    uint32_t n = 0;
+    auto emit = [&](const CceElem& E, int ch, int index) {
+        if (n >= out->term_cap) return false;
+        jaad_cce_term& t = out->cce_terms[n++];
+        std::memset(&t, 0, sizeof t);
+        t.channel = (uint8_t)ch;
+        t.point = (uint8_t)E.point;
+        t.cce = (uint16_t)E.rec;
+        std::memcpy(t.gain, E.gain[index], sizeof t.gain);
+        return true;
+    };
+    for (int k = 0; k < n_cce; k++) {
+        const CceElem& E = cces[k];
+        if (E.point != 0 && E.point != 1) continue;  // ind_sw CCEs (point 3) match no coupling point
+        for (int e = 0; e < n_el; e++) {
+            int index = 0;
+            for (int c = 0; c <= E.count; c++) {
+                const int chs = E.chs[c];
+                if (E.pair[c] == els[e].cpe && E.id[c] == els[e].tag) {
+                    if (chs != 1) {
+                        if (!emit(E, els[e].ch0, index)) return JAAD_ERR_UNSUPPORTED;
+                        if (chs != 0) index++;
+                    }
+                    if (chs != 2) {
+                        if (!emit(E, els[e].ch0 + 1, index)) return JAAD_ERR_UNSUPPORTED;
+                        index++;
+                    }
+                } else {
+                    index += 1 + (chs == 3 ? 1 : 0);
+                }
+            }
+        }
+    }
+    out->n_cce_terms = n;
+    return JAAD_OK;
+}
+
 // probe != nullptr: stop at the first SBR extension payload after the channel element
 // (bit 0 of *probe) and commit nothing
 int parse_frame(jaad_parser* p, const uint8_t* data, size_t bytes, jaad_frame_out* out, uint32_t* probe)
@@ -624,6 +756,11 @@ int parse_frame(jaad_parser* p, const uint8_t* data, size_t bytes, jaad_frame_ou
     int elem = 0, ch0 = 0, cpe = 0;  // channel elements parsed so far, their channels, CPEs
     int sbr_seen = 0;
     if (C.cfg.sbr) std::memset(out->sbr, 0, sizeof *out->sbr);
+    ChElem els[8];
+    int n_els = 0;
+    std::vector<CceElem> cces;  // 7.7 KB each: only when the frame has CCEs
+    int n_cce = 0;
+    out->n_cce = out->n_cce_terms = 0;
     for (;;) {
         if (br.left() < 3) return JAAD_ERR_EOS;
         const int id = (int)br.read(3);
@@ -656,7 +793,7 @@ int parse_frame(jaad_parser* p, const uint8_t* data, size_t bytes, jaad_frame_ou
             continue;
         }
         if (br.left() < 4) return JAAD_ERR_EOS;
-        br.skip(4);  // element_instance_tag
+        const int tag = (int)br.read(4);  // element_instance_tag
         if (id == 4) {  // DSE
             const int st = skip_dse(br);
             if (st) return st;
@@ -667,12 +804,26 @@ int parse_frame(jaad_parser* p, const uint8_t* data, size_t bytes, jaad_frame_ou
             if (st) return st;
             continue;
         }
-        if (id == 2) return JAAD_ERR_UNSUPPORTED;  // CCE (coupling channels are not decoded here)
+        if (id == 2) {  // CCE: its ICStream as a record, its gains for the terms made at the end
+            if (!out->cce_q || !out->cce_sf || !out->cce_cb || !out->cce_ics || !out->cce_terms) return JAAD_ERR_UNSUPPORTED;
+            if ((uint32_t)n_cce >= out->cce_cap || n_cce >= 8) return JAAD_ERR_UNSUPPORTED;
+            if (C.cfg.sbr) return JAAD_ERR_UNSUPPORTED;  // coupling with SBR: not decoded here
+            cces.emplace_back();
+            CceElem& E = cces.back();
+            E.rec = n_cce;
+            ChOut o{out->cce_q + (size_t)n_cce * 1024, out->cce_sf + n_cce * 128, out->cce_cb + n_cce * 128,
+                    out->cce_ics + n_cce, nullptr};
+            const int st = read_cce(br, C, ns, o, E);
+            if (st) return st;
+            n_cce++;
+            continue;
+        }
         // SCE (0) / LFE (3) / CPE (1): the configuration's channel elements in their ISO order (one
         // SCE or CPE for mono / stereo); LFE decodes as an SCE (A/syntax/LFE.java)
         if (elem >= C.n_elem || (id == 1) != (C.elem_nch[elem] == 2) || (id == 3 && C.n_elem == 1))
             return JAAD_ERR_UNSUPPORTED;
         have_channels = true;
+        els[n_els++] = ChElem{id == 1, tag, ch0};
         if (id == 0 || id == 3) {
             IcsInfo I;
             ChOut o{out->q + (size_t)ch0 * 1024, out->sf + ch0 * 128, out->cb + ch0 * 128, out->ics + ch0,
@@ -729,6 +880,11 @@ int parse_frame(jaad_parser* p, const uint8_t* data, size_t bytes, jaad_frame_ou
         const int st = sbr_missing(C, ns, *out->sbr);
         if (st) return st;
     }
+    if (n_cce) {
+        const int st = cce_terms(cces.data(), n_cce, els, n_els, out);
+        if (st) return st;
+        out->n_cce = (uint32_t)n_cce;
+    }
     if (!probe) p->st = ns;
     return JAAD_OK;
 }
@@ -756,7 +912,12 @@ int jaad_probe_sbr(const jaad_stream_cfg* cfg, const uint8_t* data, size_t bytes
     jaad_ics_info ics[8];
     jaad_tns tns[8];
     uint64_t ms[8];
-    jaad_frame_out o{q.data(), sf.data(), cb.data(), ics, ms, tns, nullptr};
+    std::vector<int16_t> cq(8 * 1024);
+    std::vector<uint8_t> csf(8 * 128), ccb(8 * 128);
+    jaad_ics_info cics[8];
+    std::vector<jaad_cce_term> terms(128);
+    jaad_frame_out o{q.data(), sf.data(), cb.data(), ics, ms, tns, nullptr, cq.data(), csf.data(), ccb.data(), cics,
+                     terms.data(), 8, 128, 0, 0};
     st = parse_frame(p, data, bytes, &o, found);
     jaad_parser_destroy(p);
     return st;

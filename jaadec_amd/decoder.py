@@ -229,7 +229,7 @@ class Decoder:
             raise AACException("one SampleBuffer per frame expected")
         b = N.Batch(batch.q, batch.sf, batch.cb, batch.ics, batch.ms_used, batch.tns,
                     np.array([self.slot], np.uint32), np.array([0, batch.n_frames], np.uint32), batch.nch,
-                    batch.sbr)
+                    batch.sbr, batch.cce_q, batch.cce_sf, batch.cce_cb, batch.cce_ics, batch.cce_terms)
         flags = self._flags(buffers[0]) if buffers else 0
         try:
             pcm = self._ctx.decode(b, flags)

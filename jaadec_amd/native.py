@@ -52,6 +52,9 @@ SBR_OK, SBR_UPSAMPLE = 0, 1  # jaad_sbr_frame.status
 SBR_FRAME_DTYPE = np.dtype([("header_present", "u1"), ("coupling", "u1"), ("ps_present", "u1"), ("status", "u1"),
                             ("hdr", SBR_HEADER_DTYPE), ("ch", SBR_CHANNEL_DTYPE, (2,)), ("ps", PS_FRAME_DTYPE)])
 assert SBR_CHANNEL_DTYPE.itemsize == 712 and PS_FRAME_DTYPE.itemsize == 528 and SBR_FRAME_DTYPE.itemsize == 1968
+# jaad_cce_term (include/jaad_gpu.h): one dependent-coupling application
+CCE_TERM_DTYPE = np.dtype([("frame", "<u4"), ("channel", "u1"), ("point", "u1"), ("cce", "<u2"), ("gain", "<f4", (120,))])
+assert CCE_TERM_DTYPE.itemsize == 488
 
 
 class StreamCfg(C.Structure):
@@ -63,7 +66,9 @@ class StreamCfg(C.Structure):
 class BatchStruct(C.Structure):
     _fields_ = [("n_frames", C.c_uint32), ("n_runs", C.c_uint32), ("stream_slot", C.c_void_p),
                 ("frame_begin", C.c_void_p), ("q", C.c_void_p), ("sf", C.c_void_p), ("cb", C.c_void_p),
-                ("ics", C.c_void_p), ("ms_used", C.c_void_p), ("tns", C.c_void_p), ("sbr", C.c_void_p)]
+                ("ics", C.c_void_p), ("ms_used", C.c_void_p), ("tns", C.c_void_p), ("sbr", C.c_void_p),
+                ("n_cce", C.c_uint32), ("n_cce_terms", C.c_uint32), ("cce_q", C.c_void_p), ("cce_sf", C.c_void_p),
+                ("cce_cb", C.c_void_p), ("cce_ics", C.c_void_p), ("cce_terms", C.c_void_p)]
 
 
 class SynthParams(C.Structure):
@@ -95,7 +100,10 @@ class AdtsHeader(C.Structure):
 
 class FrameOut(C.Structure):
     _fields_ = [("q", C.c_void_p), ("sf", C.c_void_p), ("cb", C.c_void_p), ("ics", C.c_void_p),
-                ("ms_used", C.c_void_p), ("tns", C.c_void_p), ("sbr", C.c_void_p)]
+                ("ms_used", C.c_void_p), ("tns", C.c_void_p), ("sbr", C.c_void_p),
+                ("cce_q", C.c_void_p), ("cce_sf", C.c_void_p), ("cce_cb", C.c_void_p), ("cce_ics", C.c_void_p),
+                ("cce_terms", C.c_void_p), ("cce_cap", C.c_uint32), ("term_cap", C.c_uint32),
+                ("n_cce", C.c_uint32), ("n_cce_terms", C.c_uint32)]
 
 
 class JaadError(RuntimeError):
@@ -199,17 +207,42 @@ class Batch:
     frame_begin: np.ndarray  # uint32 [n_runs+1]
     nch: int
     sbr: np.ndarray | None = None  # SBR_FRAME_DTYPE [nf] (host) when the config has SBR
+    # dependent coupling (jaad_cce_term): CCE records and the terms applying them (None: no CCEs)
+    cce_q: np.ndarray | None = None     # int16 [n_cce, 1024]
+    cce_sf: np.ndarray | None = None    # uint8 [n_cce, 128]
+    cce_cb: np.ndarray | None = None    # uint8 [n_cce, 128]
+    cce_ics: np.ndarray | None = None   # ICS_DTYPE [n_cce]
+    cce_terms: np.ndarray | None = None  # CCE_TERM_DTYPE [n_terms], sorted by frame
 
     @property
     def n_frames(self) -> int:
         return int(self.frame_begin[-1])
 
+    @property
+    def n_cce(self) -> int:
+        return 0 if self.cce_ics is None else len(self.cce_ics)
+
     def struct(self) -> BatchStruct:
         for a in (self.q, self.sf, self.cb, self.ics, self.stream_slot, self.frame_begin):
             assert a.flags["C_CONTIGUOUS"]
+        nt = 0 if self.cce_terms is None else len(self.cce_terms)
         return BatchStruct(self.n_frames, len(self.stream_slot), _ptr(self.stream_slot), _ptr(self.frame_begin),
                            _ptr(self.q), _ptr(self.sf), _ptr(self.cb), _ptr(self.ics), _ptr(self.ms_used),
-                           _ptr(self.tns), _ptr(self.sbr))
+                           _ptr(self.tns), _ptr(self.sbr), self.n_cce, nt, _ptr(self.cce_q), _ptr(self.cce_sf),
+                           _ptr(self.cce_cb), _ptr(self.cce_ics), _ptr(self.cce_terms))
+
+    def _cce_for(self, frames: np.ndarray) -> dict:
+        """The coupling of the given (renumbered in order) frames: all CCE records kept, the terms
+        of those frames with their frame indices renumbered."""
+        if self.cce_terms is None:
+            return {}
+        pos = np.full(self.n_frames, -1, np.int64)
+        pos[frames] = np.arange(len(frames))
+        t = self.cce_terms[pos[self.cce_terms["frame"]] >= 0].copy()
+        t["frame"] = pos[t["frame"]]
+        t = t[np.argsort(t["frame"], kind="stable")]
+        return dict(cce_q=self.cce_q, cce_sf=self.cce_sf, cce_cb=self.cce_cb, cce_ics=self.cce_ics,
+                    cce_terms=np.ascontiguousarray(t))
 
     def select_runs(self, runs) -> "Batch":
         """Sub-batch made of the given runs (frames renumbered, slots kept)."""
@@ -225,7 +258,7 @@ class Batch:
                      None if self.ms_used is None else np.ascontiguousarray(self.ms_used[frames]),
                      None if self.tns is None else np.ascontiguousarray(self.tns[cfr]),
                      np.ascontiguousarray(self.stream_slot[runs]).astype(np.uint32), begin, self.nch,
-                     None if self.sbr is None else np.ascontiguousarray(self.sbr[frames]))
+                     None if self.sbr is None else np.ascontiguousarray(self.sbr[frames]), **self._cce_for(frames))
 
     def split_frames(self, cut: int) -> tuple["Batch", "Batch"]:
         """Split every run at its frame `cut` (for multi-call continuation tests)."""
@@ -249,7 +282,7 @@ class Batch:
                          None if self.ms_used is None else np.ascontiguousarray(self.ms_used[frames]),
                          None if self.tns is None else np.ascontiguousarray(self.tns[cfr]),
                          self.stream_slot.copy(), begin, self.nch,
-                         None if self.sbr is None else np.ascontiguousarray(self.sbr[frames]))
+                         None if self.sbr is None else np.ascontiguousarray(self.sbr[frames]), **self._cce_for(frames))
 
         return mk(a_frames, la), mk(b_frames, lb)
 
@@ -432,14 +465,16 @@ class Context:
             h[...] = a
             return h
         return Batch(cp(b.q), cp(b.sf), cp(b.cb), cp(b.ics), cp(b.ms_used), cp(b.tns), b.stream_slot, b.frame_begin,
-                     b.nch, b.sbr)
+                     b.nch, b.sbr, b.cce_q, b.cce_sf, b.cce_cb, b.cce_ics, b.cce_terms)
 
     def decode_device(self, dev: dict, batch: Batch, pcm_dev_ptr: int, pcm_bytes: int, flags: int = 0,
                       stream_ptr: int | None = None) -> None:
         """Device-resident decode: dev maps array names to device pointers (ints)."""
+        nt = 0 if batch.cce_terms is None else len(batch.cce_terms)
         bs = BatchStruct(batch.n_frames, len(batch.stream_slot), _ptr(batch.stream_slot), _ptr(batch.frame_begin),
                          dev["q"], dev["sf"], dev["cb"], dev["ics"], dev.get("ms_used"), dev.get("tns"),
-                         _ptr(batch.sbr))
+                         _ptr(batch.sbr), batch.n_cce, nt, dev.get("cce_q"), dev.get("cce_sf"), dev.get("cce_cb"),
+                         dev.get("cce_ics"), _ptr(batch.cce_terms))
         self._check(lib().jaad_decode_batch_device(self.h, C.byref(bs), pcm_dev_ptr, pcm_bytes, flags, stream_ptr),
                     "jaad_decode_batch_device")
 
@@ -572,15 +607,36 @@ class Parser:
         ms = np.zeros((nf, 2 * ncpe), np.uint64) if ncpe else None
         tns = np.zeros(nf * nch, TNS_DTYPE)
         sbr = np.zeros(nf, SBR_FRAME_DTYPE) if self.cfg.sbr else None
+        # coupling channel elements: up to 8 records and 64 terms per frame
+        cq = np.zeros((8, 1024), np.int16)
+        csf = np.zeros((8, 128), np.uint8)
+        ccb = np.zeros((8, 128), np.uint8)
+        cics = np.zeros(8, ICS_DTYPE)
+        cterms = np.zeros(64, CCE_TERM_DTYPE)
+        recs, terms = [], []
         for i, fr in enumerate(frames):
             o = FrameOut(q[i * nch:].ctypes.data, sf[i * nch:].ctypes.data, cb[i * nch:].ctypes.data,
                          ics[i * nch:].ctypes.data, ms[i:].ctypes.data if ms is not None else None,
-                         tns[i * nch:].ctypes.data, sbr[i:].ctypes.data if sbr is not None else None)
+                         tns[i * nch:].ctypes.data, sbr[i:].ctypes.data if sbr is not None else None,
+                         cq.ctypes.data, csf.ctypes.data, ccb.ctypes.data, cics.ctypes.data, cterms.ctypes.data,
+                         8, 64, 0, 0)
             rc = lib().jaad_parse_frame(self.h, bytes(fr), len(fr), C.byref(o))
             if rc:
                 raise JaadError(rc, f"jaad_parse_frame (frame {i})")
+            if o.n_cce:
+                t = cterms[:o.n_cce_terms].copy()
+                t["frame"] = i
+                t["cce"] += len(recs)
+                terms.append(t)
+                recs += [(cq[k].copy(), csf[k].copy(), ccb[k].copy(), cics[k].copy()) for k in range(o.n_cce)]
         if not (ics["flags"] & ICS_TNS).any():
             tns = None
         b = Batch(q, sf, cb, ics, ms, tns, np.array([slot], np.uint32), np.array([0, nf], np.uint32), nch)
         b.sbr = sbr
+        if recs:
+            b.cce_q = np.ascontiguousarray(np.stack([r[0] for r in recs]))
+            b.cce_sf = np.ascontiguousarray(np.stack([r[1] for r in recs]))
+            b.cce_cb = np.ascontiguousarray(np.stack([r[2] for r in recs]))
+            b.cce_ics = np.ascontiguousarray(np.array([r[3] for r in recs], ICS_DTYPE))
+            b.cce_terms = np.ascontiguousarray(np.concatenate(terms)) if terms else np.zeros(0, CCE_TERM_DTYPE)
         return b

@@ -451,6 +451,53 @@ void orc_streams_free(orc_stream* streams, int n)
 static int sbr_down(const jaad_stream_cfg* cfg) { return cfg->sbr && cfg->ext_sf_index == cfg->sf_index; }
 static int frame_samples(const jaad_stream_cfg* cfg) { return cfg->sbr && !sbr_down(cfg) ? 2048 : 1024; }
 
+/* ChannelElement.processDependentCoupling (A/syntax/ChannelElement.java:105-130) at `point` for
+ * the frame's channels: every term of frame f (jaad_gpu.h jaad_cce_term, in the reference's order)
+ * runs CCE.applyDependentCoupling (A/syntax/CCE.java:188-215) on its target's spectrum, with the
+ * CCE's ICStream spectrum from decodeSpectralData (its own LCG state: cce_ics.pns_state). */
+static int orc_couple(const jaad_stream_cfg* cfg, const jaad_batch* b, uint32_t f, int point, int nch,
+                      float (*spec)[1024])
+{
+    uint32_t lo = 0, hi = b->n_cce_terms;
+    while (lo < hi) { /* first term of frame f (terms are sorted by frame) */
+        const uint32_t m = (lo + hi) / 2;
+        if (b->cce_terms[m].frame < f) lo = m + 1;
+        else hi = m;
+    }
+    for (uint32_t t = lo; t < b->n_cce_terms && b->cce_terms[t].frame == f; t++) {
+        const jaad_cce_term* T = &b->cce_terms[t];
+        if (T->point != point) continue;
+        if (T->channel >= nch || T->cce >= b->n_cce) return JAAD_ERR_INVALID_ARG;
+        const jaad_ics_info* info = &b->cce_ics[T->cce];
+        const uint8_t* sfbCB = b->cce_cb + (size_t)T->cce * 128;
+        float iqData[1024];
+        uint32_t rs = info->pns_state;
+        int rc = orc_dequant(info, cfg->sf_index, b->cce_q + (size_t)T->cce * 1024, b->cce_sf + (size_t)T->cce * 128,
+                             sfbCB, &rs, iqData);
+        if (rc) return rc;
+        int glen[8], nswb;
+        const int windowGroupCount = group_lengths(info, glen);
+        const short* swbOffsets = swb_offsets(info, cfg->sf_index, &nswb);
+        const int maxSFB = info->max_sfb;
+        float* data = spec[T->channel];
+        int srcOff = 0, dstOff = 0, idx = 0;
+        for (int g = 0; g < windowGroupCount; g++) {
+            const int len = glen[g];
+            for (int sfb = 0; sfb < maxSFB; sfb++, idx++) {
+                if (sfbCB[idx] != JAAD_ZERO_HCB) {
+                    const float x = T->gain[idx];
+                    for (int group = 0; group < len; group++)
+                        for (int k = swbOffsets[sfb]; k < swbOffsets[sfb + 1]; k++)
+                            data[dstOff + group * 128 + k] += x * iqData[srcOff + group * 128 + k];
+                }
+            }
+            dstOff += len * 128;
+            srcOff += len * 128;
+        }
+    }
+    return JAAD_OK;
+}
+
 static int decode_frame(const jaad_stream_cfg* cfg, orc_stream* st, const jaad_batch* b, uint32_t f,
                         uint32_t* rand_state, unsigned char* pcm, uint32_t flags)
 {
@@ -474,11 +521,19 @@ static int decode_frame(const jaad_stream_cfg* cfg, orc_stream* st, const jaad_b
         static const uint64_t zero_ms[2] = {0, 0};
         orc_is(iL, &b->ics[cR], cfg->sf_index, b->cb + cR * 128, b->sf + cR * 128, ms ? ms : zero_ms, iq[0], iq[1]);
     }
+    /* CPE.process / SCE.process: dependent coupling before TNS, TNS, dependent coupling after
+       TNS (A/syntax/CPE.java:172-179, A/syntax/SCE.java:100-108) */
+    if (b->n_cce_terms && (rc = orc_couple(cfg, b, f, 0, nch, iq))) return rc;
     for (int c = 0; c < nch; c++) {
         size_t cf = (size_t)f * nch + c;
         const jaad_ics_info* info = &b->ics[cf];
         if (cfg->tns_mode == JAAD_TNS_SPEC && (info->flags & JAAD_ICS_TNS) && b->tns)
             orc_tns_spec(info, cfg->sf_index, &b->tns[cf], iq[c]);
+    }
+    if (b->n_cce_terms && (rc = orc_couple(cfg, b, f, 1, nch, iq))) return rc;
+    for (int c = 0; c < nch; c++) {
+        size_t cf = (size_t)f * nch + c;
+        const jaad_ics_info* info = &b->ics[cf];
         orc_filterbank(info->window_sequence, info->window_shape, info->window_shape_prev, iq[c], data[c],
                        st->overlap[c]);
     }

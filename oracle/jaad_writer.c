@@ -317,6 +317,90 @@ long jaad_write_frame_mc(int sf_index, int n_elem, const int* ids, const int16_t
 }
 
 /*
+ * coupling_channel_element (the syntax CCE.decode reads, A/syntax/CCE.java:112-175) of a test
+ * description: targets, coupling domain, gain sign/scale, the CCE's ICStream records and its gain
+ * element codes.  gain list i (i >= 1): cge[i] = common_gain_element_present; with it, code[i][0]
+ * is the common gain (-60..60); without it code[i][idx] is the per-band dpcm value for every band
+ * idx whose cb != ZERO_HCB.
+ */
+typedef struct jaad_cce_desc {
+    uint8_t ind_sw, count, domain, sign, scale;  /* count = num_coupled_elements (0..7)          */
+    uint8_t pair[8], id[8], chs[8];               /* chs[i] (cc_l/cc_r as 2 bits) when pair[i]  */
+    uint8_t pos;                                  /* written before channel element `pos`        */
+    uint8_t cge[16];
+    int8_t code[16][120];
+} jaad_cce_desc;
+
+static int put_cce(Bw* w, int sf_index, int tag, const jaad_cce_desc* d, const int16_t* q, const uint8_t* sf,
+                   const uint8_t* cb, const jaad_ics_info* ic)
+{
+    put(w, 2, 3);
+    put(w, (uint32_t)tag, 4);
+    put(w, d->ind_sw, 1);
+    put(w, d->count, 3);
+    int gain_count = 0;
+    for (int i = 0; i <= d->count; i++) {
+        gain_count++;
+        put(w, d->pair[i], 1);
+        put(w, d->id[i], 4);
+        if (d->pair[i]) {
+            put(w, d->chs[i], 2);
+            if (d->chs[i] == 3) gain_count++;
+        }
+    }
+    put(w, d->domain, 1);
+    put(w, d->sign, 1);
+    put(w, d->scale, 2);
+    if (put_ics(w, sf_index, 0, q, sf, cb, ic, NULL, 0)) return -1;
+    int point = 2 * d->ind_sw + d->domain;
+    point |= point >> 1;
+    Info I;
+    info_of(ic, &I);
+    for (int i = 1; i < gain_count; i++) {
+        const int cge = point == 2 ? 1 : d->cge[i];
+        if (point != 2) put(w, (uint32_t)cge, 1);
+        if (cge) {
+            if (put_sf_delta(w, d->code[i][0])) return -1;
+            continue;
+        }
+        for (int idx = 0; idx < I.ngroups * I.max_sfb; idx++)
+            if (cb[idx] != JAAD_ZERO_HCB && put_sf_delta(w, d->code[i][idx])) return -1;
+    }
+    return 0;
+}
+
+/*
+ * A raw_data_block of channel elements ids[0..n_elem) (as jaad_write_frame_mc) with n_cce coupling
+ * channel elements (records cq/csf/ccb/cics, descriptions d) inserted before their d[k].pos-th
+ * channel element (pos = n_elem: after the last), then END.
+ */
+long jaad_write_frame_cce(int sf_index, int n_elem, const int* ids, const int16_t* q, const uint8_t* sf,
+                          const uint8_t* cb, const jaad_ics_info* ics, const uint64_t* ms_used, int n_cce,
+                          const jaad_cce_desc* d, const int16_t* cq, const uint8_t* csf, const uint8_t* ccb,
+                          const jaad_ics_info* cics, uint8_t* out, size_t cap)
+{
+    Bw w = {out, cap, 0, 0};
+    memset(out, 0, cap);
+    int ch = 0, cpe = 0, tags[8] = {0};
+    for (int k = 0; k <= n_elem; k++) {
+        for (int j = 0; j < n_cce; j++)
+            if (d[j].pos == k &&
+                put_cce(&w, sf_index, j, &d[j], cq + (size_t)j * 1024, csf + j * 128, ccb + j * 128, cics + j))
+                return -1;
+        if (k == n_elem) break;
+        const int id = ids[k];
+        if (put_element(&w, sf_index, id, tags[id]++, q + (size_t)ch * 1024, sf + ch * 128, cb + ch * 128, ics + ch,
+                        id == 1 ? ms_used + 2 * cpe : NULL, NULL, 0))
+            return -1;
+        ch += id == 1 ? 2 : 1;
+        cpe += id == 1;
+    }
+    put(&w, 7, 3); /* END */
+    align(&w);
+    return w.overflow ? -1 : (long)(w.pos / 8);
+}
+
+/*
  * One raw_data_block of the frame's records (nch = 1: SCE, 2: CPE), optionally wrapped in
  * extra DSE / FIL(fill) elements (extras bit 0) and carrying pulse data (bit 1); with `sbr`
  * (and the stream's writer state, jaad_writer_sbr.c) the SBR record follows the channel

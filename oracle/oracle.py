@@ -58,6 +58,9 @@ def lib() -> C.CDLL:
         L.orc_sbr_res_tables.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
         L.jaad_write_adts_header.argtypes = [C.c_int, C.c_int, C.c_size_t, C.c_void_p]
         L.jaad_write_frame_mc.argtypes = [C.c_int, C.c_int, C.c_void_p] + [C.c_void_p] * 6 + [C.c_void_p, C.c_size_t]
+        L.jaad_write_frame_cce.restype = C.c_long
+        L.jaad_write_frame_cce.argtypes = ([C.c_int, C.c_int, C.c_void_p] + [C.c_void_p] * 5 + [C.c_int] +
+                                           [C.c_void_p] * 5 + [C.c_void_p, C.c_size_t])
         L.jaad_write_frame_mc.restype = C.c_long
         _lib = L
     return _lib
@@ -227,6 +230,46 @@ def write_frames_mc(batch, sf_index: int, ids) -> list:
     return out
 
 
+# jaad_cce_desc (oracle/jaad_writer.c): a coupling channel element to write
+CCE_DESC_DTYPE = np.dtype([("ind_sw", "u1"), ("count", "u1"), ("domain", "u1"), ("sign", "u1"), ("scale", "u1"),
+                           ("pair", "u1", (8,)), ("id", "u1", (8,)), ("chs", "u1", (8,)), ("pos", "u1"),
+                           ("cge", "u1", (16,)), ("code", "i1", (16, 120))])
+
+
+def write_frames_cce(batch, sf_index: int, ids, cces) -> list:
+    """TEST WRITER: raw_data_blocks of a (multichannel) batch with coupling channel elements:
+    cces[f] = list of (desc CCE_DESC_DTYPE scalar, q [1024], sf [128], cb [128], ics ICS_DTYPE scalar)
+    written before channel element desc["pos"] (jaad_write_frame_cce)."""
+    nch = batch.nch
+    ids_a = (C.c_int * len(ids))(*ids)
+    buf = np.zeros(1 << 17, np.uint8)
+    out = []
+    for f in range(batch.n_frames):
+        cf = f * nch
+        q = np.ascontiguousarray(batch.q[cf:cf + nch])
+        sf = np.ascontiguousarray(batch.sf[cf:cf + nch])
+        cb = np.ascontiguousarray(batch.cb[cf:cf + nch])
+        ics = np.ascontiguousarray(batch.ics[cf:cf + nch])
+        ms = np.ascontiguousarray(batch.ms_used[f]) if batch.ms_used is not None else np.zeros(16, np.uint64)
+        lst = cces[f] if f < len(cces) else []
+        n = len(lst)
+        d = np.zeros(max(n, 1), CCE_DESC_DTYPE)
+        cq = np.zeros((max(n, 1), 1024), np.int16)
+        csf = np.zeros((max(n, 1), 128), np.uint8)
+        ccb = np.zeros((max(n, 1), 128), np.uint8)
+        import jaadec_amd.native as N
+        cics = np.zeros(max(n, 1), N.ICS_DTYPE)
+        for k, (dk, qk, sfk, cbk, icsk) in enumerate(lst):
+            d[k], cq[k], csf[k], ccb[k], cics[k] = dk, qk, sfk, cbk, icsk
+        r = lib().jaad_write_frame_cce(sf_index, len(ids), ids_a, q.ctypes.data, sf.ctypes.data, cb.ctypes.data,
+                                       ics.ctypes.data, ms.ctypes.data, n, d.ctypes.data, cq.ctypes.data,
+                                       csf.ctypes.data, ccb.ctypes.data, cics.ctypes.data, buf.ctypes.data, buf.nbytes)
+        if r < 0:
+            raise ValueError(f"frame {f} cannot be written")
+        out.append(buf[:r].tobytes())
+    return out
+
+
 def decode_batch_mc(sf_index: int, batch, ids, flags: int = 0, threads: int = 1, tns_mode: int = 0) -> np.ndarray:
     """TEST ORACLE for a multichannel batch, from fresh stream states: every element decoded on its
     own (SCE/LFE as a mono, CPE as a stereo stream: SyntacticElements.process runs them in turn)
@@ -245,6 +288,11 @@ def decode_batch_mc(sf_index: int, batch, ids, flags: int = 0, threads: int = 1,
                      np.ascontiguousarray(batch.ms_used[:, 2 * cpe:2 * cpe + 2]) if k == 2 else None,
                      np.ascontiguousarray(batch.tns[cfr]) if batch.tns is not None else None,
                      batch.stream_slot.copy(), batch.frame_begin.copy(), k)
+        if batch.cce_terms is not None:  # the element's coupling terms, channels relative to it
+            t = batch.cce_terms[(batch.cce_terms["channel"] >= c) & (batch.cce_terms["channel"] < c + k)].copy()
+            t["channel"] -= c
+            el.cce_q, el.cce_sf, el.cce_cb, el.cce_ics = batch.cce_q, batch.cce_sf, batch.cce_cb, batch.cce_ics
+            el.cce_terms = np.ascontiguousarray(t)
         cfg = N.make_cfg(sf_index, 2 if k == 2 else 1, tns_mode)
         pcm = decode_batch(cfg, el, Streams(int(batch.stream_slot.max()) + 1), flags, threads)
         dt = np.uint32 if fb == 4 else np.uint16

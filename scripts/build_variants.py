@@ -7,10 +7,8 @@ sys.path.insert(0, str(ROOT))
 from jaadec_amd import build as B  # noqa: E402
 
 VARIANTS = {
-    "p08": ([], []),
-    "p12": (["JAAD_MAX_PIECES=12", "JAAD_MIN_PIECE_FRAMES=2048"], []),
-    "p16": (["JAAD_MAX_PIECES=16"], []),
-    "p24": (["JAAD_MAX_PIECES=24", "JAAD_MIN_PIECE_FRAMES=2048"], []),
+    "c_head": ([], []),
+    "s_stamps": (["JAAD_STAMPS"], []),
 }
 
 if __name__ == "__main__":

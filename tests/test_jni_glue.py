@@ -34,6 +34,9 @@ def _lib():
     getattr(L, PFX + "nativeReset").argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32]
     for name in ("nativeRegister", "nativeUnregister", "nativeFreeDirect"):
         getattr(L, PFX + name).argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p]
+    coupled = getattr(L, PFX + "nativeDecodeCoupled")
+    coupled.argtypes = ([C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_int32, C.c_int32] + [C.c_void_p] * 9 +
+                        [C.c_int32, C.c_int32, C.c_int32] + [C.c_void_p] * 5)
     alloc = getattr(L, PFX + "nativeAllocDirect")
     alloc.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int64]
     alloc.restype = C.c_void_p
@@ -58,7 +61,7 @@ def _buf(a, keep):
 def test_exports():
     L = _lib()
     for name in ("nativeCreate", "nativeDestroy", "nativeDecode", "nativeReset", "nativeRegister",
-                 "nativeUnregister", "nativeAllocDirect", "nativeFreeDirect"):
+                 "nativeUnregister", "nativeAllocDirect", "nativeFreeDirect", "nativeDecodeCoupled"):
         assert hasattr(L, PFX + name)
 
 
@@ -173,6 +176,38 @@ def test_decode_through_direct_buffers_and_capacity_checks():
         getattr(L, PFX + "nativeFreeDirect")(env, None, h, db)
         assert _exception(L) is None
         getattr(L, PFX + "nativeFreeDirect")(env, None, h, db)  # freed already
+        cls, msg = _exception(L)
+        assert cls == AAC_EXC and N.strerror(N.ERR_INVALID_ARG) in msg
+    finally:
+        getattr(L, PFX + "nativeDestroy")(env, None, h)
+
+
+@pytest.mark.gpu
+def test_coupled_decode_through_direct_buffers():
+    """nativeDecodeCoupled: a stereo batch with CCE records and terms equals the Python entry."""
+    from tests.test_cce import coupled_batch
+    L = _lib()
+    env = L.jni_mock_env()
+    b = coupled_batch(2, n_streams=2, fps=12, seed=4)
+    with N.Context(N.make_cfg(), 2) as ctx:
+        want = ctx.decode(b, N.PCM_BIG_ENDIAN)
+    h = getattr(L, PFX + "nativeCreate")(env, None, 3, 2, 0, 0, 0, 2, 0)
+    assert h and _exception(L) is None
+    try:
+        out = np.zeros_like(want)
+        keep = []
+        a = [_buf(x, keep) for x in (b.stream_slot, b.frame_begin, b.q, b.sf, b.cb, b.ics, b.ms_used, None, out)]
+        c = [_buf(x, keep) for x in (b.cce_q, b.cce_sf, b.cce_cb, b.cce_ics, b.cce_terms)]
+        getattr(L, PFX + "nativeDecodeCoupled")(env, None, h, b.n_frames, len(b.stream_slot), 2, *a, N.PCM_BIG_ENDIAN,
+                                               b.n_cce, len(b.cce_terms), *c)
+        assert _exception(L) is None
+        assert (out == want).all()
+        # a term buffer one term short is refused
+        short = Buf(b.cce_terms.ctypes.data, b.cce_terms.nbytes - 488)
+        keep.append(short)
+        c[4] = C.addressof(short)
+        getattr(L, PFX + "nativeDecodeCoupled")(env, None, h, b.n_frames, len(b.stream_slot), 2, *a, N.PCM_BIG_ENDIAN,
+                                               b.n_cce, len(b.cce_terms), *c)
         cls, msg = _exception(L)
         assert cls == AAC_EXC and N.strerror(N.ERR_INVALID_ARG) in msg
     finally:

@@ -100,10 +100,10 @@ def test_errors_leave_the_parser_state_untouched():
             assert e.value.status == N.ERR_EOS
             assert P.pns_state == st
             bad = bytearray(fr)
-            bad[0] = (bad[0] & 0x1F) | 0x40  # element id SCE -> CCE
+            bad[0] = (bad[0] & 0x1F) | 0x40  # element id SCE -> CCE: its bits do not parse as one
             with pytest.raises(N.JaadError) as e:
                 P.parse([bytes(bad)])
-            assert e.value.status == N.ERR_UNSUPPORTED
+            assert e.value.status in (N.ERR_BITSTREAM, N.ERR_EOS, N.ERR_UNSUPPORTED)
             assert P.pns_state == st
         out.append(P.parse([fr]))
     for i, g in enumerate(out):
@@ -120,12 +120,19 @@ def test_reserved_codebook_and_unsupported_elements():
     with pytest.raises(N.JaadError) as e:
         P.parse([raw])
     assert e.value.status == N.ERR_BITSTREAM
-    # a CPE in a mono configuration, a CCE, an LFE
-    for elem in ("001", "010", "011"):
+    # a CPE in a mono configuration, an LFE
+    for elem in ("001", "011"):
         raw = int((elem + "0000").ljust(64, "0"), 2).to_bytes(8, "big")
         with pytest.raises(N.JaadError) as e:
             P.parse([raw])
         assert e.value.status == N.ERR_UNSUPPORTED
+    # a CCE (one SCE target, an empty ICS) and END: coupling but no audio element
+    cce = "010" + "0000" + "0" + "000" + "0" + "0000" + "0" + "0" + "00"
+    ics = "00000000" + "0" + "00" + "0" + "000000" + "0" + "0" + "0" + "0"
+    raw = int((cce + ics + "111").ljust(64, "0"), 2).to_bytes(8, "big")
+    with pytest.raises(N.JaadError) as e:
+        P.parse([raw])
+    assert e.value.status == N.ERR_BITSTREAM
     # an empty raw_data_block (END only) carries no audio
     with pytest.raises(N.JaadError) as e:
         P.parse([bytes([0xE0])])
