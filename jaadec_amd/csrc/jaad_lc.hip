@@ -285,31 +285,6 @@ __device__ __forceinline__ void xch(float& a, float& b, int u)
         a = __int_as_float(__builtin_amdgcn_update_dpp(ia, ib, 0x124, 0xF, 0xA, false));
         b = __int_as_float(__builtin_amdgcn_update_dpp(ib, ia, 0x12C, 0xF, 0x5, false));
     } else {  // quad_perm lane ^ 2 / lane ^ 1, then a per-lane select
-#ifdef JAAD_XCH_CNDDPP
-        // one v_cndmask_b32 with the swizzle on its DPP source per output (dst = vcc ? src1 : src0):
-        // a' = hi ? swz(b) : a, b' = hi ? b : swz(a); hi = lanes with bit L set
-        (void)u;
-        constexpr uint32_t kHi = L == 1 ? 0xCCCCCCCCu : 0xAAAAAAAAu;
-        int ra, rb;
-        if constexpr (L == 1) {
-            asm("s_mov_b32 vcc_lo, %3\n\ts_mov_b32 vcc_hi, %3\n\ts_nop 1\n\t"
-                "v_cndmask_b32_dpp %0, %1, %2, vcc quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf"
-                : "=&v"(ra) : "v"(ib), "v"(ia), "i"(~kHi) : "vcc");
-            asm("s_mov_b32 vcc_lo, %3\n\ts_mov_b32 vcc_hi, %3\n\ts_nop 1\n\t"
-                "v_cndmask_b32_dpp %0, %1, %2, vcc quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf"
-                : "=&v"(rb) : "v"(ia), "v"(ib), "i"(kHi) : "vcc");
-        } else {
-            asm("s_mov_b32 vcc_lo, %3\n\ts_mov_b32 vcc_hi, %3\n\ts_nop 1\n\t"
-                "v_cndmask_b32_dpp %0, %1, %2, vcc quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf"
-                : "=&v"(ra) : "v"(ib), "v"(ia), "i"(~kHi) : "vcc");
-            asm("s_mov_b32 vcc_lo, %3\n\ts_mov_b32 vcc_hi, %3\n\ts_nop 1\n\t"
-                "v_cndmask_b32_dpp %0, %1, %2, vcc quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf"
-                : "=&v"(rb) : "v"(ia), "v"(ib), "i"(kHi) : "vcc");
-        }
-        a = __int_as_float(ra);
-        b = __int_as_float(rb);
-        return;
-#endif
         constexpr int kCtl = L == 1 ? 0x4E : 0xB1;
         const int pb = __builtin_amdgcn_mov_dpp(ib, kCtl, 0xF, 0xF, true);
         const int pa = __builtin_amdgcn_mov_dpp(ia, kCtl, 0xF, 0xF, true);
@@ -319,9 +294,63 @@ __device__ __forceinline__ void xch(float& a, float& b, int u)
     }
 }
 // register bit I <-> lane bit L for all four register pairs, both floats of each complex value
+// Lane bits 0..3 for two register pairs (p, p | 1<<I) and (r, r | 1<<I) at once: each output is
+// ONE v_cndmask_b32 whose src0 is the partner lane's value through a DPP swizzle
+// (dst = vcc ? src1 : swz(src0)): a' = bit clear ? a : swz(b), b' = bit set ? b : swz(a).
+// Swizzles: lane ^ 1, ^ 2 by quad_perm; ^ 8 by row_ror:8; ^ 4 by row_ror:4 (lanes with bit 2 set
+// read lane - 4) and row_ror:12 (bit 2 clear read lane + 4).  The two s_movs in front are the
+// 2 wait states a DPP read of a VGPR that a VALU instruction just wrote needs.
+template <int L>
+__device__ __forceinline__ void xch2(f2& a0, f2& b0, f2& a1, f2& b1)
+{
+    // lanes with bit L set (the pattern repeats per 32 lanes: vcc_lo = vcc_hi, literal operands,
+    // no SGPRs held across the exchanges)
+    constexpr uint32_t kHi = L == 0 ? 0xAAAAAAAAu : L == 1 ? 0xCCCCCCCCu : L == 2 ? 0xF0F0F0F0u : 0xFF00FF00u;
+    f2 na0, nb0, na1, nb1;
+#define JAAD_XCH_BODY(QA, QB)                                                                    \
+    asm("s_mov_b32 vcc_lo, %[lo]\n\t"                                                            \
+        "s_mov_b32 vcc_hi, %[lo]\n\t"                                                            \
+        "v_cndmask_b32_dpp %[na0x], %[b0x], %[a0x], vcc " QA " row_mask:0xf bank_mask:0xf\n\t"   \
+        "v_cndmask_b32_dpp %[na0y], %[b0y], %[a0y], vcc " QA " row_mask:0xf bank_mask:0xf\n\t"   \
+        "v_cndmask_b32_dpp %[na1x], %[b1x], %[a1x], vcc " QA " row_mask:0xf bank_mask:0xf\n\t"   \
+        "v_cndmask_b32_dpp %[na1y], %[b1y], %[a1y], vcc " QA " row_mask:0xf bank_mask:0xf\n\t"   \
+        "s_mov_b32 vcc_lo, %[hi]\n\t"                                                            \
+        "s_mov_b32 vcc_hi, %[hi]\n\t"                                                            \
+        "v_cndmask_b32_dpp %[nb0x], %[a0x], %[b0x], vcc " QB " row_mask:0xf bank_mask:0xf\n\t"   \
+        "v_cndmask_b32_dpp %[nb0y], %[a0y], %[b0y], vcc " QB " row_mask:0xf bank_mask:0xf\n\t"   \
+        "v_cndmask_b32_dpp %[nb1x], %[a1x], %[b1x], vcc " QB " row_mask:0xf bank_mask:0xf\n\t"   \
+        "v_cndmask_b32_dpp %[nb1y], %[a1y], %[b1y], vcc " QB " row_mask:0xf bank_mask:0xf"       \
+        : [na0x] "=&v"(na0.x), [na0y] "=&v"(na0.y), [na1x] "=&v"(na1.x), [na1y] "=&v"(na1.y),     \
+          [nb0x] "=&v"(nb0.x), [nb0y] "=&v"(nb0.y), [nb1x] "=&v"(nb1.x), [nb1y] "=&v"(nb1.y)      \
+        : [a0x] "v"(a0.x), [a0y] "v"(a0.y), [a1x] "v"(a1.x), [a1y] "v"(a1.y), [b0x] "v"(b0.x),    \
+          [b0y] "v"(b0.y), [b1x] "v"(b1.x), [b1y] "v"(b1.y), [lo] "i"(~kHi), [hi] "i"(kHi)        \
+        : "vcc")
+    if constexpr (L == 0) JAAD_XCH_BODY("quad_perm:[1,0,3,2]", "quad_perm:[1,0,3,2]");
+    else if constexpr (L == 1) JAAD_XCH_BODY("quad_perm:[2,3,0,1]", "quad_perm:[2,3,0,1]");
+    else if constexpr (L == 2) JAAD_XCH_BODY("row_ror:4", "row_ror:12");
+    else JAAD_XCH_BODY("row_ror:8", "row_ror:8");
+#undef JAAD_XCH_BODY
+    a0 = na0;
+    b0 = nb0;
+    a1 = na1;
+    b1 = nb1;
+}
+
+#ifndef JAAD_XCH_CND_MAX
+#define JAAD_XCH_CND_MAX 3
+#endif
 template <int I, int L>
 __device__ __forceinline__ void xch_bit(f2 (&c)[8], int u)
 {
+    if constexpr (L <= JAAD_XCH_CND_MAX) {
+        constexpr int m = 1 << I;
+        // k-th register index with bit I clear
+        auto clr = [](int k) { return ((k >> I) << (I + 1)) | (k & (m - 1)); };
+        xch2<L>(c[clr(0)], c[clr(0) | m], c[clr(1)], c[clr(1) | m]);
+        xch2<L>(c[clr(2)], c[clr(2) | m], c[clr(3)], c[clr(3) | m]);
+        (void)u;
+        return;
+    }
 #pragma unroll
     for (int s = 0; s < 8; s++) {
         if ((s >> I) & 1) continue;
@@ -757,11 +786,7 @@ struct alignas(16) BandRec {
     float gl, ms, gr, is;
 };
 constexpr int kNoBand = 127;  // a record index that is always all-zero (bands < 8*15 = 120)
-#ifdef JAAD_IQ_SELECT
-constexpr float kZeroBandGain = 0.0f;
-#else
 constexpr float kZeroBandGain = -0.0f;  // gain of bands that are not spectral (see iq_channel)
-#endif
 
 // record index of the bin quad starting at position p (4-aligned); long windows use the
 // lane's precomputed band byte
@@ -849,39 +874,54 @@ __device__ __forceinline__ void prefetch(const KernelArgs& A, int f, bool stereo
 __device__ __forceinline__ void iq_channel(const LdsTables& T, const float* iq_global, const v4i (&q)[2],
                                            const float (&g)[4], float (&x)[16])
 {
-    bool esc = false;
     // all 16 table reads are issued before the first is consumed (one LDS round trip, not 16)
     float v[16];
+    // two bins per dword: one packed 16-bit add biases both to table indices q + kIqHead, which
+    // lie in [0, 2 kIqHead) exactly when no escape is needed (bits 11..15 of each half clear);
+    // the halves become byte offsets by SDWA word selects.  Escaped bins read some LDS word (an
+    // LDS read never faults) that the escape pass below replaces.
+    typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+    static_assert(kIqHead == 1024, "escape mask assumes a 2048-entry head");
+    uint32_t t[8];
+#pragma unroll
+    for (int d = 0; d < 8; d++) {
+        const uint32_t w = reinterpret_cast<const uint32_t*>(&q[d >> 2])[d & 3];
+        t[d] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(us2, w) + (us2){kIqHead, kIqHead});
+    }
+    const bool esc = ((t[0] | t[1] | t[2] | t[3] | t[4] | t[5] | t[6] | t[7]) & 0xF800F800u) != 0u;
 #pragma unroll
     for (int e = 0; e < 16; e++) {
-        const int qq = reinterpret_cast<const int16_t*>(&q[e >> 3])[e & 7];
-        const int qc = qq < -kIqHead ? -kIqHead : (qq > kIqHead - 1 ? kIqHead - 1 : qq);
-        esc |= qc != qq;
-        v[e] = T.iq_signed[qc + kIqHead];
+        const uint32_t idx = (e & 1) ? (t[e >> 1] >> 16) : (t[e >> 1] & 0xFFFFu);
+        v[e] = T.iq_signed[idx];
     }
-    __builtin_amdgcn_sched_group_barrier(0x0100, 16, 0);  // the 16 DS reads first
+    // the 8 packed adds, then each table read right after its address (no SDWA-after-VALU nops)
+    __builtin_amdgcn_sched_group_barrier(0x0002, 8, 0);
+#pragma unroll
+    for (int e = 0; e < 16; e++) {
+        __builtin_amdgcn_sched_group_barrier(0x0002, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x0100, 1, 0);
+    }
     __builtin_amdgcn_sched_group_barrier(0x0002, 64, 0);  // then the VALU
 #pragma unroll
     for (int e = 0; e < 16; e++) {
         const float gn = g[e >> 2];
-#ifdef JAAD_IQ_SELECT
-        x[e] = gn != 0.0f ? v[e] * gn : 0.0f;
-#else
         x[e] = v[e] * gn;  // gn = -0.0 for a non-spectral band (kZeroBandGain): -0.0 * -0.0 = +0.0
-#endif
     }
     // escape values beyond the LDS head of IQ_TABLE (|q| >= 1024: rare in real streams and absent
     // from the synthetic ones); global loads, which also wait for the previous frame's PCM stores
     if (__builtin_expect(__ballot(esc) != 0, 0)) {
-        // uniform branch; every lane loads and selects (no exec-masked partial register writes)
+        // uniform branch; every lane recomputes its 16 bins: the head entry of the clamped index
+        // (an escaped bin of a non-spectral band gives +-0 as in the reference, not whatever the
+        // fast path read), the global table where the gain is nonzero
 #pragma unroll
         for (int e = 0; e < 16; e++) {
             const int qq = reinterpret_cast<const int16_t*>(&q[e >> 3])[e & 7];
+            const int qc = qq < -kIqHead ? -kIqHead : (qq > kIqHead - 1 ? kIqHead - 1 : qq);
             const int aq = qq < 0 ? -qq : qq;
             const float gn = g[e >> 2];
             const float m = iq_global[aq > 8190 ? 8190 : aq] * gn;
             const bool big = (qq > kIqHead - 1 || qq < -kIqHead) && gn != 0.0f;
-            x[e] = big ? (qq > 0 ? m : -m) : x[e];
+            x[e] = big ? (qq > 0 ? m : -m) : T.iq_signed[qc + kIqHead] * gn;
         }
     }
 }

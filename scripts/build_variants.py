@@ -9,6 +9,7 @@ from jaadec_amd import build as B  # noqa: E402
 VARIANTS = {
     "c_head": ([], []),
     "s_stamps": (["JAAD_STAMPS"], []),
+    "xcnd1": (["JAAD_XCH_CND_MAX=1"], []),
 }
 
 if __name__ == "__main__":

@@ -58,6 +58,25 @@ def test_c3_tns_spec_mode():
     _assert_pcm_equal(got, want, N.PCM_FLOAT32)
 
 
+@pytest.mark.parametrize("cfg_id", [2, 3])
+def test_escaped_values_beyond_the_lds_iq_head(cfg_id):
+    """|q| in [1024, 8191] (IQ_TABLE entries past the kernel's 2 x 1024-entry LDS head, read from
+    the global table; A/syntax/ICStream.java:258-271), scattered over every band -- spectral,
+    zero, noise and intensity bands and bins past max_sfb, where the reference never reads q."""
+    p = N.synth_params(cfg_id, n_streams=4, frames_per_stream=20, pns_percent=6, is_percent=10)
+    b = N.synth_batch(p)
+    rng = np.random.default_rng(11)
+    flat = b.q.reshape(-1)
+    pick = rng.choice(flat.size, flat.size // 200, replace=False)
+    mag = rng.integers(1024, 8192, pick.size)
+    flat[pick] = np.where(rng.integers(0, 2, pick.size) == 1, mag, -mag).astype(np.int16)
+    n_slots = int(b.stream_slot.max()) + 1
+    with N.Context(N.make_cfg(), n_slots) as ctx:
+        got = ctx.decode(b, N.PCM_FLOAT32)
+    want = O.decode_batch(N.make_cfg(), b, O.Streams(n_slots), N.PCM_FLOAT32)
+    _assert_pcm_equal(got, want, N.PCM_FLOAT32)
+
+
 def test_pns_and_intensity():
     p = N.synth_params(3, n_streams=5, frames_per_stream=20, pns_percent=8, is_percent=15)
     b, got, want = _run_both(p, N.make_cfg(), N.PCM_FLOAT32)
