@@ -46,19 +46,31 @@ def _deps(*globs: str) -> list[Path]:
     return out
 
 
+# per-source extra flags (the LC kernel: see DESIGN.md §4a, scheduler strategy)
+GPU_FILE_FLAGS: dict[str, list[str]] = {}
+
+
 def build_gpu(force: bool = False, out: Path | None = None, defines: list[str] | None = None,
               extra: list[str] | None = None) -> Path:
-    """Build the product library (or, with `defines`, an experimental variant at `out`)."""
+    """Build the product library (or, with `defines`, an experimental variant at `out`): every
+    source compiled on its own (in parallel, with its GPU_FILE_FLAGS), then linked."""
     out = out or LIB
     srcs = [CSRC / "jaad_lc.hip", CSRC / "jaad_sbr.hip", CSRC / "jaad_ps.hip", CSRC / "jaad_capi.cpp", CSRC / "jaad_sbr_host.cpp",
             CSRC / "jaad_parse.cpp", CSRC / "jaad_parse_sbr.cpp", CSRC / "jaad_mp4.cpp"]
     deps = srcs + _deps("jaadec_amd/csrc/*.h", "jaadec_amd/csrc/tables/*.inc", "include/*.h")
     if force or defines or extra or _stale(out, deps):
+        objdir = ROOT / "build" / "obj" / out.stem
+        objdir.mkdir(parents=True, exist_ok=True)
+        common = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
+                  "-fno-slp-vectorize", "-fno-gpu-rdc", "-Wall", "-Wno-unused-function", "-I", str(ROOT / "include")]
+        common += [f"-D{d}" for d in (defines or [])] + (extra or [])
+        objs = [objdir / (s.name + ".o") for s in srcs]
+        from concurrent.futures import ThreadPoolExecutor
+        with ThreadPoolExecutor(min(8, os.cpu_count() or 1)) as ex:
+            list(ex.map(lambda so: _run(common + GPU_FILE_FLAGS.get(so[0].name, []) + ["-c", "-o", str(so[1]), str(so[0])]),
+                        zip(srcs, objs)))
         tmp = out.with_suffix(".so.tmp")
-        _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-              "-ffp-contract=off", "-fno-slp-vectorize", "-fno-gpu-rdc", "-Wall", "-Wno-unused-function",
-              "-I", str(ROOT / "include"), "-o", str(tmp)] + [f"-D{d}" for d in (defines or [])]
-             + (extra or []) + [str(s) for s in srcs])
+        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fno-gpu-rdc", "-o", str(tmp)] + [str(o) for o in objs])
         tmp.replace(out)
     return out
 

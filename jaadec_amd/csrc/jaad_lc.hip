@@ -269,31 +269,18 @@ __device__ __forceinline__ void fft_3stages_pk(f2 (&c)[8], TW tw)
 // Register transposes between the IFFT passes.  A pair of registers (a: register bit i clear,
 // b: set) trades register bit i for lane bit L: the element at (register bit, lane bit L) =
 // (x, y) moves to (y, x), every other lane bit unchanged.
+// Lane bits 5 / 4: one v_permlane32_swap / v_permlane16_swap swaps a's upper half-lanes with
+// b's lower ones.
 template <int L>
-__device__ __forceinline__ void xch(float& a, float& b, int u)
+__device__ __forceinline__ void xch_hi(float& a, float& b)
 {
+    static_assert(L == 5 || L == 4, "lane bits 0..3 go through xch2");
     const int ia = __float_as_int(a), ib = __float_as_int(b);
-    if constexpr (L == 5 || L == 4) {  // swap a's upper half-lanes with b's lower ones
-        const auto r = L == 5 ? __builtin_amdgcn_permlane32_swap(ia, ib, false, false)
-                              : __builtin_amdgcn_permlane16_swap(ia, ib, false, false);
-        a = __int_as_float(r[0]);
-        b = __int_as_float(r[1]);
-    } else if constexpr (L == 3) {  // row_ror:8 = lane ^ 8; bank mask = the lanes written
-        a = __int_as_float(__builtin_amdgcn_update_dpp(ia, ib, 0x128, 0xF, 0xC, false));
-        b = __int_as_float(__builtin_amdgcn_update_dpp(ib, ia, 0x128, 0xF, 0x3, false));
-    } else if constexpr (L == 2) {  // row_ror:n reads lane (l - n) mod 16: 4 -> lane - 4 for lanes 4..7, 12 -> lane + 4 for 0..3
-        a = __int_as_float(__builtin_amdgcn_update_dpp(ia, ib, 0x124, 0xF, 0xA, false));
-        b = __int_as_float(__builtin_amdgcn_update_dpp(ib, ia, 0x12C, 0xF, 0x5, false));
-    } else {  // quad_perm lane ^ 2 / lane ^ 1, then a per-lane select
-        constexpr int kCtl = L == 1 ? 0x4E : 0xB1;
-        const int pb = __builtin_amdgcn_mov_dpp(ib, kCtl, 0xF, 0xF, true);
-        const int pa = __builtin_amdgcn_mov_dpp(ia, kCtl, 0xF, 0xF, true);
-        const bool hi = (u >> L) & 1;
-        a = __int_as_float(hi ? pb : ia);
-        b = __int_as_float(hi ? ib : pa);
-    }
+    const auto r = L == 5 ? __builtin_amdgcn_permlane32_swap(ia, ib, false, false)
+                          : __builtin_amdgcn_permlane16_swap(ia, ib, false, false);
+    a = __int_as_float(r[0]);
+    b = __int_as_float(r[1]);
 }
-// register bit I <-> lane bit L for all four register pairs, both floats of each complex value
 // Lane bits 0..3 for two register pairs (p, p | 1<<I) and (r, r | 1<<I) at once: each output is
 // ONE v_cndmask_b32 whose src0 is the partner lane's value through a DPP swizzle
 // (dst = vcc ? src1 : swz(src0)): a' = bit clear ? a : swz(b), b' = bit set ? b : swz(a).
@@ -336,30 +323,28 @@ __device__ __forceinline__ void xch2(f2& a0, f2& b0, f2& a1, f2& b1)
     b1 = nb1;
 }
 
-#ifndef JAAD_XCH_CND_MAX
-#define JAAD_XCH_CND_MAX 3
-#endif
+// register bit I <-> lane bit L for all four register pairs, both floats of each complex value
 template <int I, int L>
 __device__ __forceinline__ void xch_bit(f2 (&c)[8], int u)
 {
-    if constexpr (L <= JAAD_XCH_CND_MAX) {
+    if constexpr (L <= 3) {
         constexpr int m = 1 << I;
         // k-th register index with bit I clear
         auto clr = [](int k) { return ((k >> I) << (I + 1)) | (k & (m - 1)); };
         xch2<L>(c[clr(0)], c[clr(0) | m], c[clr(1)], c[clr(1) | m]);
         xch2<L>(c[clr(2)], c[clr(2) | m], c[clr(3)], c[clr(3) | m]);
-        (void)u;
-        return;
-    }
+    } else {
 #pragma unroll
-    for (int s = 0; s < 8; s++) {
-        if ((s >> I) & 1) continue;
-        float ax = c[s].x, ay = c[s].y, bx = c[s | (1 << I)].x, by = c[s | (1 << I)].y;
-        xch<L>(ax, bx, u);
-        xch<L>(ay, by, u);
-        c[s] = f2{ax, ay};
-        c[s | (1 << I)] = f2{bx, by};
+        for (int s = 0; s < 8; s++) {
+            if ((s >> I) & 1) continue;
+            float ax = c[s].x, ay = c[s].y, bx = c[s | (1 << I)].x, by = c[s | (1 << I)].y;
+            xch_hi<L>(ax, bx);
+            xch_hi<L>(ay, by);
+            c[s] = f2{ax, ay};
+            c[s | (1 << I)] = f2{bx, by};
+        }
     }
+    (void)u;
 }
 
 // IMDCT N = 2048 (MDCT.process, A/filterbank/MDCT.java:36-81) of N channels in lockstep (N = 2:

@@ -9,14 +9,14 @@ from jaadec_amd import build as B  # noqa: E402
 VARIANTS = {
     "c_head": ([], []),
     "s_stamps": (["JAAD_STAMPS"], []),
-    "xcnd1": (["JAAD_XCH_CND_MAX=1"], []),
+    "ilp": ([], ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]),
 }
 
 if __name__ == "__main__":
     out = ROOT / ".tmp" / "exp"
     out.mkdir(parents=True, exist_ok=True)
     for f in out.glob("lib_*.so"):
-        if f.stem[4:] in VARIANTS: f.unlink()
+        if f.stem[4:] in VARIANTS and (len(sys.argv) < 2 or f.stem[4:] in sys.argv[1:]): f.unlink()
     only = set(sys.argv[1:])
     from concurrent.futures import ThreadPoolExecutor
     todo = [(n, d) for n, d in VARIANTS.items() if not only or n in only]
