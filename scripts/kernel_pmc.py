@@ -12,7 +12,7 @@ def main(root: str):
     for f in sorted(Path(root).rglob("*counter_collection.csv")):
         with open(f) as fh:
             for r in csv.DictReader(fh):
-                name = r["Kernel_Name"].split("(")[0].replace("void jaad::", "").replace("(anonymous namespace)::", "")
+                name = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "").replace("jaad::", "")
                 acc[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
     for k, c in sorted(acc.items()):
         a = {n: sum(v) / len(v) for n, v in c.items()}
