@@ -9,7 +9,6 @@ from jaadec_amd import build as B  # noqa: E402
 VARIANTS = {
     "c_head": ([], []),
     "s_stamps": (["JAAD_STAMPS"], []),
-    "ilp": ([], ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]),
 }
 
 if __name__ == "__main__":
