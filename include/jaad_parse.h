@@ -44,7 +44,13 @@ extern "C" {
  * readSyncExtension A/DecoderConfig.java:260-291) is explicit SBR as well.  Without it the
  * output rate is the core rate (A/DecoderConfig.java:180): SBR found later in the frames
  * (implicit signalling) runs downsampled for such a decoder, unlike one created from an ADTS
- * header (AudioDecoderInfo), whose output rate is doubled (DecoderConfig.setSBRPresent :124-135). */
+ * header (AudioDecoderInfo), whose output rate is doubled (DecoderConfig.setSBRPresent :124-135).
+ * channelConfiguration 0 reads the program_config_element that follows (PCE.read/decode,
+ * A/syntax/PCE.java:47-52,133-188); its profile and sample rate replace the ASC's and its channel
+ * count selects the configuration (setAudioDecoderInfo, PCE.getChannelConfiguration :221-223).
+ * Accepted when the PCE's elements (front, side, back, LFE) carry the channel counts of that
+ * configuration's element list, which is the list the frames are parsed against;
+ * JAAD_ERR_UNSUPPORTED otherwise (e.g. two SCEs as "dual mono", a 7-channel count). */
 int jaad_asc_parse(const uint8_t* asc, size_t bytes, jaad_stream_cfg* cfg);
 
 /* ADTS fixed + variable header (S/adts/ADTSFrame.java:48-111) */

@@ -414,8 +414,7 @@ int skip_dse(BitReader& br)
 int skip_pce(BitReader& br)
 {
     if (br.left() < 2 + 4 + 4 + 4 + 4 + 2 + 3 + 4) return JAAD_ERR_EOS;
-    br.skip(2);
-    if (br.read(4) == 15) br.skip(24);  // SampleFrequency.decode: explicit frequency
+    br.skip(2 + 4);  // profile, SampleFrequency.decode (4 bits, A/SampleFrequency.java:112-115)
     const int nfront = (int)br.read(4), nside = (int)br.read(4), nback = (int)br.read(4);
     const int nlfe = (int)br.read(2), nassoc = (int)br.read(3), ncc = (int)br.read(4);
     if (br.read(1)) br.skip(4);
@@ -427,6 +426,58 @@ int skip_pce(BitReader& br)
     const int ncomment = (int)br.read(8);
     br.skip(8 * ncomment);
     return br.overrun() ? JAAD_ERR_EOS : JAAD_OK;
+}
+
+// program_config_element of an AudioSpecificConfig with channelConfiguration 0 (PCE.decode,
+// A/syntax/PCE.java:133-188).  The reference replaces the config's profile, sample rate and channel
+// configuration with the PCE's (DecoderConfig.setAudioDecoderInfo, A/DecoderConfig.java:60-65);
+// the configuration is the one of the PCE's channel count (PCE.getChannelConfiguration ->
+// ChannelConfiguration.forChannelCount, :221-223; 7 channels throw, 8 are 7.1), and the frames'
+// elements are then decoded in bitstream order whatever the configuration says
+// (SyntacticElements.decode, A/syntax/SyntacticElements.java:60-86).  This library decodes the
+// element list of channel configurations 1..7, so a PCE is accepted when its front, side, back
+// and LFE elements (the order they appear in) have exactly those channel counts.
+int read_pce_layout(BitReader& br, int& profile, int& sfi, int& chc)
+{
+    if (br.left() < 4 + 2 + 4) return JAAD_ERR_EOS;
+    br.skip(4);                     // element_instance_tag (PCE.read, :47-52)
+    profile = 1 + (int)br.read(2);  // Profile.forInt(1 + object_type)
+    sfi = (int)br.read(4);  // SampleFrequency.decode: 4 bits, no explicit frequency
+    if (br.left() < 4 + 4 + 4 + 2 + 3 + 4) return JAAD_ERR_EOS;
+    const int nfront = (int)br.read(4), nside = (int)br.read(4), nback = (int)br.read(4);
+    const int nlfe = (int)br.read(2), nassoc = (int)br.read(3), ncc = (int)br.read(4);
+    if (br.read(1)) br.skip(4);  // mono mixdown
+    if (br.read(1)) br.skip(4);  // stereo mixdown
+    if (br.read(1)) br.skip(3);  // matrix mixdown
+    uint8_t nch[8 + 3];
+    int n = 0, channels = nlfe;
+    for (int i = 0; i < nfront + nside + nback; i++) {
+        const int cpe = (int)br.read(1);
+        br.skip(4);  // element tag
+        if (n < 8) nch[n] = (uint8_t)(1 + cpe);
+        n++;
+        channels += 1 + cpe;
+    }
+    for (int i = 0; i < nlfe; i++) {
+        br.skip(4);
+        if (n < 8 + 3) nch[n] = 1;
+        n++;
+    }
+    br.skip(4 * nassoc + 5 * ncc);
+    br.byte_align();
+    if (br.left() < 8) return JAAD_ERR_EOS;
+    br.skip(8 * (int)br.read(8));  // comment field
+    if (br.overrun()) return JAAD_ERR_EOS;
+    if (channels == 7 || channels < 1 || channels > 8) return JAAD_ERR_UNSUPPORTED;  // forChannelCount(7) throws
+    chc = channels == 8 ? 7 : channels;
+    // the element list the parser and the device path decode for that configuration
+    static const uint8_t kList[8][5] = {{}, {1}, {2}, {1, 2}, {1, 2, 1}, {1, 2, 2}, {1, 2, 2, 1}, {1, 2, 2, 2, 1}};
+    static const int kN[8] = {0, 1, 1, 2, 3, 3, 4, 5};
+    if (n != kN[chc]) return JAAD_ERR_UNSUPPORTED;
+    for (int i = 0; i < n; i++)
+        if (nch[i] != kList[chc][i]) return JAAD_ERR_UNSUPPORTED;
+    if (chc == 1 && nlfe) return JAAD_ERR_UNSUPPORTED;  // a lone LFE: the mono path decodes an SCE
+    return JAAD_OK;
 }
 
 }  // namespace
@@ -465,7 +516,7 @@ int jaad_asc_parse(const uint8_t* asc, size_t bytes, jaad_stream_cfg* cfg)
     cfg->tns_mode = JAAD_TNS_COMPAT;
     int aot = profile();
     int sfi = rate();
-    const int chc = (int)br.read(4);
+    int chc = (int)br.read(4);
     if (aot == 5 || aot == 29) {  // AAC_SBR / AAC_PS: extension rate, core profile; no GASpecificConfig
         cfg->sbr = 1;
         cfg->ps = aot == 29 || chc == 1;  // mono: PS enabled by default (jaad_parse.h)
@@ -476,7 +527,12 @@ int jaad_asc_parse(const uint8_t* asc, size_t bytes, jaad_stream_cfg* cfg)
         if (br.read(1)) br.skip(14);                  // dependsOnCoreCoder -> coreCoderDelay
         if (br.read(1)) br.skip(1);                   // extensionFlag -> extensionFlag3
         if (br.overrun()) return JAAD_ERR_EOS;
-        if (chc == 0) return JAAD_ERR_UNSUPPORTED;    // PCE channel layouts: no fixed element list
+        if (chc == 0) {  // DecoderConfig.decode: PCE.read + setAudioDecoderInfo (A/DecoderConfig.java:231-235)
+            int pprof = 0;
+            const int st = read_pce_layout(br, pprof, sfi, chc);
+            if (st) return st;
+            aot = pprof;
+        }
         // readSyncExtension (A/DecoderConfig.java:238, 260-291; sbrEnabled is always on): a
         // backward-compatible 0x2B7 extension can signal SBR (and PS, 0x548) with its output
         // rate.  Without it the output rate stays the core rate (:180): SBR met later in the

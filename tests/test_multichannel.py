@@ -125,3 +125,65 @@ def test_gpu_bitstream_to_pcm_through_the_decoder_facade():
         assert buf.getChannels() == 6
     assert dec.getConfig().getChannelCount() == 6
     dec.close()
+
+
+def _pce_asc(sfi: int, front, side=(), back=(), n_lfe: int = 0, pce_sfi: int | None = None, aot: int = 2) -> bytes:
+    """An AudioSpecificConfig with channelConfiguration 0 and its program_config_element
+    (PCE.read / decode, A/syntax/PCE.java:47-52,133-188): element lists as is_cpe flags."""
+    bits = f"{aot:05b}{sfi:04b}{0:04b}000"                           # GASpecificConfig
+    bits += f"{0:04b}{1:02b}{(sfi if pce_sfi is None else pce_sfi):04b}"  # tag, LC, rate
+    bits += f"{len(front):04b}{len(side):04b}{len(back):04b}{n_lfe:02b}{0:03b}{0:04b}000"
+    for lst in (front, side, back):
+        for k, cpe in enumerate(lst):
+            bits += f"{int(cpe):01b}{k:04b}"
+    bits += "".join(f"{k:04b}" for k in range(n_lfe))
+    bits += "0" * (-len(bits) % 8) + f"{0:08b}"                      # byte_align, no comment
+    bits += "0" * (-len(bits) % 8)
+    return int(bits, 2).to_bytes(len(bits) // 8, "big")
+
+
+@pytest.mark.parametrize("layout, cc", [
+    (dict(front=[True]), 2),                                          # stereo
+    (dict(front=[False]), 1),                                         # mono
+    (dict(front=[False, True], back=[True], n_lfe=1), 6),             # 5.1
+    (dict(front=[False, True], side=[True], n_lfe=1), 6),             # 5.1, surrounds as side elements
+    (dict(front=[False, True], back=[False]), 4),                     # 4.0: C, L/R, back centre
+    (dict(front=[False, True], n_lfe=1), 4),                          # 3.1 counts 4 channels -> 4.0 list
+    (dict(front=[False, True, True], back=[True], n_lfe=1), 7),       # 8 channels -> 7.1
+])
+def test_asc_program_config_element_layouts(layout, cc):
+    """DecoderConfig.decode with channelConfiguration 0 (A/DecoderConfig.java:231-235): the PCE's
+    channel count picks the configuration (PCE.getChannelConfiguration -> forChannelCount)."""
+    cfg = N.asc_parse(_pce_asc(3, **layout))
+    assert (cfg.channel_config, cfg.sf_index, cfg.profile) == (cc, 3, 2)
+
+
+def test_asc_program_config_element_rate_and_refusals():
+    # setAudioDecoderInfo(pce): the PCE's sample rate replaces the ASC's
+    assert N.asc_parse(_pce_asc(4, front=[True], pce_sfi=3)).sf_index == 3
+    for layout in (dict(front=[False, False]),                        # dual mono: SCE SCE is not the CPE list
+                   dict(front=[True, False]),                         # CPE then SCE: not the 3.0 list
+                   dict(front=[False, True, True], back=[True]),      # 7 channels: forChannelCount throws
+                   dict(front=[], n_lfe=1)):                          # a lone LFE
+        with pytest.raises(N.JaadError) as e:
+            N.asc_parse(_pce_asc(3, **layout))
+        assert e.value.status == N.ERR_UNSUPPORTED, layout
+
+
+@pytest.mark.gpu
+def test_gpu_pce_config_decodes_like_the_standard_configuration():
+    """A 5.1 stream whose AudioSpecificConfig carries a PCE (as an MP4 DSI can) through
+    Decoder.create(asc) + decodeFrame: the PCM of channel configuration 6."""
+    from jaadec_amd.decoder import Decoder, SampleBuffer
+    b = mc_synth(6, n_streams=1, fps=6)
+    frames = O.write_frames_mc(b, 3, IDS[6])
+    dec = Decoder.create(_pce_asc(3, front=[False, True], back=[True], n_lfe=1))
+    assert dec.getConfig().getChannelCount() == 6
+    dec._parse([])
+    dec._parser.pns_state = int(b.ics["pns_state"][0])
+    want = O.decode_batch_mc(3, b, IDS[6], N.PCM_BIG_ENDIAN)
+    for i in range(6):
+        buf = SampleBuffer()
+        dec.decodeFrame(frames[i], buf)
+        assert buf.getData() == want[i].tobytes(), i
+    dec.close()
