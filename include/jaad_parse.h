@@ -69,7 +69,14 @@ typedef struct jaad_adts_header {
  * search window (ADTSDemultiplexer.MAXIMUM_FRAME_SIZE = 6144 bytes) and decode its header.
  * *offset = byte offset of the header.  JAAD_ERR_EOS when no complete header is found. */
 int jaad_adts_find(const uint8_t* buf, size_t bytes, size_t* offset, jaad_adts_header* h);
-/* stream configuration implied by an ADTS header (AAC LC only) */
+/* The stream configuration a raw_data_block's leading program_config_element declares (an ADTS
+ * stream with channel_configuration 0: the reference decodes the PCE as an element and applies it
+ * with DecoderConfig.setAudioDecoderInfo, A/syntax/SyntacticElements.java:153-156); the same layout
+ * rule as jaad_asc_parse.  JAAD_ERR_BITSTREAM when the frame does not start with a PCE. */
+int jaad_raw_pce_cfg(const uint8_t* raw, size_t bytes, jaad_stream_cfg* cfg);
+
+/* stream configuration implied by an ADTS header (AAC LC only); channel_configuration 0 gives
+ * channel_config 0, the layout then comes from the first frame (jaad_raw_pce_cfg) */
 int jaad_adts_cfg(const jaad_adts_header* h, jaad_stream_cfg* cfg);
 
 typedef struct jaad_parser jaad_parser;

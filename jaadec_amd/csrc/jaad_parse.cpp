@@ -589,11 +589,30 @@ int jaad_adts_find(const uint8_t* buf, size_t bytes, size_t* offset, jaad_adts_h
     return JAAD_ERR_EOS;
 }
 
+int jaad_raw_pce_cfg(const uint8_t* raw, size_t bytes, jaad_stream_cfg* cfg)
+{
+    if (!raw || !cfg) return JAAD_ERR_INVALID_ARG;
+    BitReader br(raw, bytes);
+    if (br.left() < 3) return JAAD_ERR_EOS;
+    if (br.read(3) != 5) return JAAD_ERR_BITSTREAM;  // the frame does not start with a PCE
+    int profile = 0, sfi = 0, chc = 0;
+    const int st = read_pce_layout(br, profile, sfi, chc);
+    if (st) return st;
+    if (profile != 2 || sfi > 11) return JAAD_ERR_UNSUPPORTED;
+    std::memset(cfg, 0, sizeof *cfg);
+    cfg->abi_version = JAAD_ABI_VERSION;
+    cfg->profile = 2;
+    cfg->sf_index = (uint8_t)sfi;
+    cfg->channel_config = (uint8_t)chc;
+    cfg->tns_mode = JAAD_TNS_COMPAT;
+    return JAAD_OK;
+}
+
 int jaad_adts_cfg(const jaad_adts_header* h, jaad_stream_cfg* cfg)
 {
     if (!h || !cfg) return JAAD_ERR_INVALID_ARG;
-    if (h->profile != 2 || h->sf_index > 11 || h->channel_config < 1 || h->channel_config > 7)
-        return JAAD_ERR_UNSUPPORTED;
+    // channel_config 0: the layout comes from the PCE the frames carry (jaad_raw_pce_cfg)
+    if (h->profile != 2 || h->sf_index > 11 || h->channel_config > 7) return JAAD_ERR_UNSUPPORTED;
     std::memset(cfg, 0, sizeof *cfg);
     cfg->abi_version = JAAD_ABI_VERSION;
     cfg->profile = 2;

@@ -82,6 +82,8 @@ class DecoderConfig:
         # configuration's speakers (ChannelConfiguration.forInt: 7 -> 7.1, 8 channels)
         if self.channel_config in N.MC_ELEMENTS:
             return 8 if self.channel_config == 7 else self.channel_config
+        if self.channel_config == 0:
+            return 0  # ChannelConfiguration.NONE until a PCE arrives
         return 2
 
     def getSampleLength(self) -> int:  # noqa: N802
@@ -162,7 +164,10 @@ class Decoder:
         if config.profile != 2:
             raise AACException(f"unsupported profile: {config.profile}")
         self.config = config
-        self._ctx = context or N.Context(config.cfg(), 1)
+        # channel_configuration 0 (an ADTS header's): the layout arrives with the first frame's
+        # PCE (SyntacticElements.decode -> setAudioDecoderInfo, A/syntax/SyntacticElements.java:
+        # 153-156), the context is opened then (_pce_layout)
+        self._ctx = context or (N.Context(config.cfg(), 1) if config.channel_config else None)
         self._own = context is None
         self.slot = slot
         self.frames = 0
@@ -201,8 +206,25 @@ class Decoder:
                                     up.ext_sf_index, from_asc=c.from_asc)
         self._ctx = N.Context(self.config.cfg(), 1)
 
+    def _pce_layout(self, first: bytes) -> None:
+        """Channel configuration 0: the configuration of the first frame's program_config_element
+        (its profile, rate and channel count, DecoderConfig.setAudioDecoderInfo :60-65)."""
+        if not self._own:
+            raise AACException("a PCE-defined layout needs its own context")
+        try:
+            c = N.raw_pce_cfg(first)
+            self.config = DecoderConfig(c.profile, c.sf_index, c.channel_config, self.config.tns_mode,
+                                        from_asc=self.config.from_asc)
+            self._ctx = N.Context(self.config.cfg(), 1)
+        except N.JaadError as e:
+            raise AACException(str(e)) from e
+
     def _parse(self, frames: list) -> N.Batch:
         if self._parser is None:
+            if self._ctx is None:
+                if not frames:
+                    raise AACException("channel configuration 0: the first frame must carry the PCE")
+                self._pce_layout(bytes(frames[0]))
             if frames and self.frames == 0:
                 self._implicit_sbr(bytes(frames[0]))
             self._parser = N.Parser(self.config.cfg())
@@ -289,7 +311,7 @@ class Decoder:
         return AudioFormat("PCM_FLOAT", freq, 32, ch, 4 * ch, freq, False)
 
     def close(self) -> None:
-        if self._own:
+        if self._own and self._ctx is not None:
             self._ctx.close()
         if self._parser is not None:
             self._parser.close()

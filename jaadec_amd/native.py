@@ -87,7 +87,7 @@ EXPORTS = ["jaad_cfg_sample_length", "jaad_cfg_channel_count", "jaad_frame_pcm_b
            "jaad_state_export", "jaad_state_import", "jaad_state_reset", "jaad_strerror", "jaad_last_error",
            "jaad_host_register", "jaad_host_unregister", "jaad_host_alloc", "jaad_host_free"]
 # every symbol include/jaad_parse.h declares
-PARSE_EXPORTS = ["jaad_asc_parse", "jaad_adts_find", "jaad_adts_cfg", "jaad_parser_create", "jaad_parser_destroy",
+PARSE_EXPORTS = ["jaad_asc_parse", "jaad_adts_find", "jaad_adts_cfg", "jaad_raw_pce_cfg", "jaad_parser_create", "jaad_parser_destroy",
                  "jaad_parser_clone", "jaad_parser_copy",
                  "jaad_parser_pns_state", "jaad_parser_set_pns_state", "jaad_parse_frame", "jaad_probe_sbr"]
 
@@ -153,6 +153,7 @@ def lib() -> C.CDLL:
         L.jaad_asc_parse.argtypes = [C.c_char_p, C.c_size_t, C.POINTER(StreamCfg)]
         L.jaad_adts_find.argtypes = [C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t), C.POINTER(AdtsHeader)]
         L.jaad_adts_cfg.argtypes = [C.POINTER(AdtsHeader), C.POINTER(StreamCfg)]
+        L.jaad_raw_pce_cfg.argtypes = [C.c_char_p, C.c_size_t, C.POINTER(StreamCfg)]
         L.jaad_parser_create.argtypes = [C.POINTER(StreamCfg), C.POINTER(C.c_void_p)]
         L.jaad_parser_destroy.argtypes = [C.c_void_p]
         L.jaad_parser_clone.argtypes = [C.c_void_p, C.POINTER(C.c_void_p)]
@@ -523,6 +524,15 @@ def adts_frames(data: bytes):
             return  # truncated last frame (EOF inside the payload)
         yield AdtsHeader.from_buffer_copy(h), data[start:end]
         pos = end
+
+
+def raw_pce_cfg(raw: bytes) -> StreamCfg:
+    """The configuration a raw_data_block's leading PCE declares (jaad_raw_pce_cfg)."""
+    cfg = StreamCfg()
+    rc = lib().jaad_raw_pce_cfg(bytes(raw), len(raw), C.byref(cfg))
+    if rc:
+        raise JaadError(rc, "jaad_raw_pce_cfg")
+    return cfg
 
 
 def adts_cfg(h: AdtsHeader) -> StreamCfg:
