@@ -58,5 +58,7 @@ def test_random_parity_soak():
         n += 1
         frames += b.n_frames
         per[cid] = per.get(cid, 0) + 1
+        if n % 25 == 0:  # progress (a silent GPU job looks hung)
+            print(f"soak: {n} batches, {frames} frames", flush=True)
     print(f"\nsoak: {n} random batches ({frames} frames, per config {dict(sorted(per.items()))}) byte-identical to the restatement")
     assert n > 0
