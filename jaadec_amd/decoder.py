@@ -246,6 +246,8 @@ class Decoder:
             except AACException:
                 self._rollback(snap)
                 raise
+        if self._ctx is None:  # channel configuration 0 and no raw frame (with its PCE) seen yet
+            raise AACException("channel configuration 0: decode the raw frames (the first carries the PCE)")
         if len(buffers) != batch.n_frames:
             self._rollback(snap)
             raise AACException("one SampleBuffer per frame expected")
