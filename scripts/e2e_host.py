@@ -30,9 +30,11 @@ with N.Context(cfg, int(b.stream_slot.max()) + 1) as ctx:
             t0 = time.perf_counter()
             ctx.decode(bb, N.PCM_BIG_ENDIAN, out=o)
             ts.append(time.perf_counter() - t0)
+        import hashlib
+        digest = hashlib.blake2b(np.asarray(o).tobytes(), digest_size=6).hexdigest()  # PCM of the last call
         if mode == "registered":
             ctx.unregister(*arrays)
         if mode == "hostalloc":
             ctx.free_host(bb.q, bb.sf, bb.cb, bb.ics, bb.ms_used, bb.tns, o)
         print(f"{mode:10s} best {b.n_frames / min(ts):.4g} frames/s  median {b.n_frames / np.median(ts):.4g}  "
-              f"({min(ts) * 1e3:.2f} ms per {b.n_frames} frames)", flush=True)
+              f"({min(ts) * 1e3:.2f} ms per {b.n_frames} frames)  pcm {digest}", flush=True)
