@@ -399,11 +399,16 @@ class Context:
         self.h = h
 
     def close(self):
-        if getattr(self, "h", None):
-            lib().jaad_ctx_destroy(self.h)
+        h = getattr(self, "h", None)
+        if h:
             self.h = None
+            lib().jaad_ctx_destroy(h)
 
-    __del__ = close
+    def __del__(self):
+        try:
+            self.close()
+        except TypeError:  # interpreter shutdown: this module's globals (lib) are already gone
+            pass
 
     def __enter__(self):
         return self
