@@ -183,8 +183,13 @@ class MP4Container:
         return self._movie
 
     def close(self) -> None:
-        if getattr(self, "_h", None):
-            _lib().jaad_mp4_close(self._h)
+        h = getattr(self, "_h", None)
+        if h:
             self._h = None
+            _lib().jaad_mp4_close(h)
 
-    __del__ = close
+    def __del__(self):
+        try:
+            self.close()
+        except TypeError:  # interpreter shutdown: the module's globals are already gone
+            pass

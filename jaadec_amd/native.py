@@ -582,11 +582,16 @@ class Parser:
         self.h = h
 
     def close(self):
-        if getattr(self, "h", None):
-            lib().jaad_parser_destroy(self.h)
+        h = getattr(self, "h", None)
+        if h:
             self.h = None
+            lib().jaad_parser_destroy(h)
 
-    __del__ = close
+    def __del__(self):
+        try:
+            self.close()
+        except TypeError:  # interpreter shutdown (see Context.__del__)
+            pass
 
     def snapshot(self) -> "Parser":
         """A copy of the whole parser state (jaad_parser_clone)."""
