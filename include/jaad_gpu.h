@@ -224,7 +224,13 @@ typedef struct jaad_sbr_frame {
  * terms are refused).  Independent switching
  * CCEs (ind_sw_cce_flag) never apply in the reference (couplingPoint becomes 3, matching neither
  * BEFORE_TNS, AFTER_TNS nor AFTER_IMDCT: CCE.java:113-129), so they produce no terms.
+ * Limits (JAAD_ERR_UNSUPPORTED): a gain that is not finite or whose magnitude exceeds
+ * JAAD_CCE_GAIN_MAX (the reference's (float)Math.pow(scale, -t) of a long gain walk, where its
+ * spectrum and IMDCT overflow to inf/NaN), and more than 65536 CCE records in one batch (the
+ * 16-bit jaad_cce_term.cce).
  */
+#define JAAD_CCE_GAIN_MAX 1.152921504606846976e18f /* 2^60 */
+#define JAAD_CCE_MAX_RECORDS 65536u
 typedef struct jaad_cce_term {
     uint32_t frame;    /* batch frame (terms sorted by frame)                                  */
     uint8_t channel;   /* target channel within the frame (0 .. channels-1)                      */

@@ -1247,10 +1247,14 @@ static int check_batch(const jaad_ctx* ctx, const jaad_batch* b, size_t pcm_byte
     if (b->n_cce_terms) {  // dependent coupling: AAC-LC in TNS compat mode (jaad_gpu.h)
         if (ctx->cfg.sbr || ctx->cfg.tns_mode != JAAD_TNS_COMPAT) return JAAD_ERR_UNSUPPORTED;
         if (!b->cce_terms || !b->n_cce || !b->cce_q || !b->cce_sf || !b->cce_cb || !b->cce_ics) return JAAD_ERR_INVALID_ARG;
+        if (b->n_cce > JAAD_CCE_MAX_RECORDS) return JAAD_ERR_UNSUPPORTED;  // jaad_cce_term.cce is 16-bit
         for (uint32_t t = 0; t < b->n_cce_terms; t++) {
             const jaad_cce_term& T = b->cce_terms[t];
             if (T.frame >= b->n_frames || (t && T.frame < b->cce_terms[t - 1].frame)) return JAAD_ERR_INVALID_ARG;
             if (T.channel >= ctx->nch || T.point > 1 || T.cce >= b->n_cce) return JAAD_ERR_INVALID_ARG;
+            // non-finite or overflowing gains would carry inf/NaN into the IMDCT and the state
+            for (float g : T.gain)
+                if (!(std::fabs(g) <= JAAD_CCE_GAIN_MAX)) return JAAD_ERR_UNSUPPORTED;
         }
     }
     return JAAD_OK;

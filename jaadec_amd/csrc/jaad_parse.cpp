@@ -700,6 +700,9 @@ struct ChElem {                    // a channel element of the frame: SCE / LFE 
     int tag, ch0;
 };
 
+// a gain the library applies (jaad_gpu.h JAAD_CCE_GAIN_MAX): finite and at most 2^60 in magnitude
+static bool cce_gain_ok(float g) { return std::fabs(g) <= JAAD_CCE_GAIN_MAX; }  // false for NaN, +-inf
+
 int read_cce(BitReader& br, const Cfg& C, ParseState& ns, ChOut& o, CceElem& E)
 {
     static const float kScale[4] = {1.09050773266525765921f, 1.18920711500272106672f, 1.4142135623730950488016887f, 2.0f};
@@ -748,6 +751,7 @@ int read_cce(BitReader& br, const Cfg& C, ParseState& ns, ChOut& o, CceElem& E)
             gc = (float)std::pow(scale, (double)-xg);
         }
         if (E.point == 2) {
+            if (!cce_gain_ok(gc)) return JAAD_ERR_UNSUPPORTED;
             E.gain[i][0] = gc;
             continue;
         }
@@ -768,6 +772,7 @@ int read_cce(BitReader& br, const Cfg& C, ParseState& ns, ChOut& o, CceElem& E)
                         gc = (float)(std::pow(scale, (double)-t) * sgn);
                     }
                 }
+                if (!cce_gain_ok(gc)) return JAAD_ERR_UNSUPPORTED;
                 E.gain[i][idx] = gc;
             }
     }

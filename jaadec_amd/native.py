@@ -21,6 +21,8 @@ ABI_VERSION = 3
 
 # status codes (jaad_status)
 OK, ERR_INVALID_ARG, ERR_NO_DEVICE, ERR_HIP, ERR_UNSUPPORTED, ERR_BITSTREAM, ERR_NOMEM, ERR_ABI, ERR_EOS = 0, -1, -2, -3, -4, -5, -6, -7, -8
+CCE_MAX_RECORDS = 65536  # jaad_gpu.h JAAD_CCE_MAX_RECORDS (16-bit jaad_cce_term.cce)
+CCE_GAIN_MAX = float(2 ** 60)  # jaad_gpu.h JAAD_CCE_GAIN_MAX
 
 ONLY_LONG_SEQUENCE, LONG_START_SEQUENCE, EIGHT_SHORT_SEQUENCE, LONG_STOP_SEQUENCE = 0, 1, 2, 3
 ZERO_HCB, NOISE_HCB, INTENSITY_HCB2, INTENSITY_HCB = 0, 13, 14, 15
@@ -644,6 +646,9 @@ class Parser:
             if rc:
                 raise JaadError(rc, f"jaad_parse_frame (frame {i})")
             if o.n_cce:
+                if len(recs) + o.n_cce > CCE_MAX_RECORDS:  # jaad_cce_term.cce is 16-bit (jaad_gpu.h)
+                    raise JaadError(ERR_UNSUPPORTED, f"more than {CCE_MAX_RECORDS} CCE records in one batch "
+                                                     f"(frame {i}): parse fewer frames per call")
                 t = cterms[:o.n_cce_terms].copy()
                 t["frame"] = i
                 t["cce"] += len(recs)

@@ -329,3 +329,85 @@ def test_gpu_bitstream_with_cce_through_the_decoder_facade(cc):
         dec.decodeFrame(demux.readNextFrame(), buf)
         assert buf.getData() == want[i].tobytes(), i
     dec.close()
+
+
+# ------------------------------------------------------------------------------------------------
+# limits (jaad_gpu.h JAAD_CCE_GAIN_MAX, JAAD_CCE_MAX_RECORDS)
+# ------------------------------------------------------------------------------------------------
+
+def big_gain_frames(total_code):
+    """One stereo frame with a CCE whose per-band gain walk (scale 2, sign coding off) reaches
+    xg = total_code: its last band's gain is 2^-total_code, as CCE.decode computes it."""
+    b, ids, elements, _ = coupled_frames(2, 1, seed=9)
+    q, sf, cb, ics = cce_records(1, 4, short=0)
+    d = rand_desc(np.random.default_rng(5), [(1, 0, 3)], cb[0], ics[0], pos=1)
+    d["sign"], d["scale"] = 1, 3
+    d["cge"][1] = 0
+    nb = nbands(ics[0])
+    coded = [i for i in range(nb) if cb[0][i] != 0]
+    assert len(coded) >= 3
+    codes = np.zeros(120, np.int32)
+    step = int(np.sign(total_code)) * 60
+    left = total_code
+    for i in coded:
+        c = max(-60, min(60, left)) if step > 0 else min(60, max(-60, left))
+        codes[i] = c
+        left -= c
+    assert left == 0
+    d["code"][1][:] = codes
+    return O.write_frames_cce(b, 3, ids, [[(d, q[0], sf[0], cb[0], ics[0])]])
+
+
+def test_cce_gain_beyond_the_bound_is_refused():
+    """a gain walk past 2^60 would carry inf/NaN into the spectrum, the IMDCT and the
+    overlap state: the parser refuses it (JAAD_ERR_UNSUPPORTED); one inside the bound parses."""
+    P = N.Parser(N.make_cfg(sf_index=3, channel_config=2))
+    got = P.parse(big_gain_frames(-60))  # gain 2^60: the bound itself
+    assert np.abs(got.cce_terms["gain"]).max() == np.float32(2.0 ** 60)
+    with pytest.raises(N.JaadError) as e:
+        N.Parser(N.make_cfg(sf_index=3, channel_config=2)).parse(big_gain_frames(-61))
+    assert e.value.status == N.ERR_UNSUPPORTED
+    with pytest.raises(N.JaadError) as e:
+        N.Parser(N.make_cfg(sf_index=3, channel_config=2)).parse(big_gain_frames(-180))  # 2^180: inf as a float
+    assert e.value.status == N.ERR_UNSUPPORTED
+
+
+def test_cce_record_count_limit_in_parse(monkeypatch):
+    """jaad_cce_term.cce is 16-bit; Parser.parse raises instead of wrapping the record
+    index (the limit lowered to 2 records so the test stays small)."""
+    b, ids, elements, per_frame = coupled_frames(2, 4, seed=2)
+    frames = O.write_frames_cce(b, 3, ids, per_frame)
+    monkeypatch.setattr(N, "CCE_MAX_RECORDS", 2)
+    P = N.Parser(N.make_cfg(sf_index=3, channel_config=2))
+    P.pns_state = int(b.ics["pns_state"][0])
+    with pytest.raises(N.JaadError) as e:
+        P.parse(frames)
+    assert e.value.status == N.ERR_UNSUPPORTED
+
+
+@pytest.mark.gpu
+def test_gpu_coupling_rejects_bad_gains_and_too_many_records():
+    b = coupled_batch(2, n_streams=2, fps=8, seed=3)
+    with N.Context(N.make_cfg(channel_config=2), 2) as ctx:
+        for bad in (np.inf, np.nan, 2.0 ** 61):
+            t = b.cce_terms.copy()
+            t["gain"][0][5] = bad
+            b2 = N.Batch(b.q, b.sf, b.cb, b.ics, b.ms_used, b.tns, b.stream_slot, b.frame_begin, b.nch, None,
+                         b.cce_q, b.cce_sf, b.cce_cb, b.cce_ics, t)
+            with pytest.raises(N.JaadError) as e:
+                ctx.decode(b2)
+            assert e.value.status == N.ERR_UNSUPPORTED, bad
+        # more records than the 16-bit index can address
+        n = N.CCE_MAX_RECORDS + 1
+        cq = np.zeros((n, 1024), np.int16)
+        csf = np.zeros((n, 128), np.uint8)
+        ccb = np.zeros((n, 128), np.uint8)
+        cics = np.zeros(n, N.ICS_DTYPE)
+        b3 = N.Batch(b.q, b.sf, b.cb, b.ics, b.ms_used, b.tns, b.stream_slot, b.frame_begin, b.nch, None,
+                     cq, csf, ccb, cics, b.cce_terms)
+        with pytest.raises(N.JaadError) as e:
+            ctx.decode(b3)
+        assert e.value.status == N.ERR_UNSUPPORTED
+        # the context still decodes a good batch afterwards
+        want = O.decode_batch(N.make_cfg(channel_config=2), b, O.Streams(2), N.PCM_BIG_ENDIAN)
+        assert (ctx.decode(b) == want).all()
