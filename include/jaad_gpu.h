@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define JAAD_ABI_VERSION 3u
+#define JAAD_ABI_VERSION 4u
 
 /* ---- status codes (JNI maps every nonzero code to AACException, A/AACException.java) ---- */
 typedef enum jaad_status {
@@ -276,7 +276,21 @@ typedef struct jaad_batch {
     const uint8_t* cce_cb;        /* [dev] [n_cce][128]                                             */
     const jaad_ics_info* cce_ics; /* [dev] [n_cce]                                                  */
     const jaad_cce_term* cce_terms; /* host [n_cce_terms]                                           */
+    /* per-frame status (ABI 4): host [n_frames] of JAAD_FRAME_*, or NULL = every frame decodes.  A
+       frame marked JAAD_FRAME_EOS is dropped as Decoder.decodeFrame drops a frame whose bitstream
+       ended early (it catches the EOSException and skips process() and buffer.accept,
+       A/Decoder.java:89-101): no DSP runs for it, its PCM slot in the output is left as it is, and
+       its stream's state is the one the previous decoded frame left, so the run's next frame
+       continues from there.  Its records are not read (they may be zero).  The other frames of the
+       batch decode as usual. */
+    const uint8_t* frame_status;
 } jaad_batch;
+
+/* jaad_batch.frame_status values */
+enum {
+    JAAD_FRAME_DECODE = 0,
+    JAAD_FRAME_EOS = 1     /* dropped: the parser hit the end of this frame's bitstream (EOSException) */
+};
 
 typedef struct jaad_ctx jaad_ctx;
 
@@ -298,10 +312,13 @@ void jaad_ctx_destroy(jaad_ctx* ctx);
 int jaad_ctx_core_channels(const jaad_ctx* ctx);
 
 /* Synchronous host-buffer entry: copies the batch to the device, runs the DSP, copies
- * n_frames * jaad_frame_pcm_bytes(flags) bytes of PCM back to pcm_out (frame-major).
+ * n_frames * jaad_frame_pcm_bytes(flags) bytes of PCM back to pcm_out (frame-major; the slots of
+ * frames marked JAAD_FRAME_EOS are not written).
  * Replaces the per-frame Decoder.decodeFrame(byte[], SampleBuffer) (A/Decoder.java:131-150)
  * for a batch of already parsed frames.  The side info is range-checked first
- * (JAAD_ERR_BITSTREAM, every slot's state left as before the call).  An AAC-LC batch of
+ * (JAAD_ERR_BITSTREAM, every slot's state left as before the call; with dropped frames the
+ * frames between them decode as consecutive sub-batches, all checked before the first runs,
+ * except for SBR record rejections, which stop at the failing sub-batch).  An AAC-LC batch of
  * >= 4096 frames is cut into run-aligned pieces whose copies and kernels overlap; caller
  * buffers registered with jaad_host_register are copied by DMA directly, others through
  * page-locked staging.                                                                      */

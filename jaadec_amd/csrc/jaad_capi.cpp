@@ -1595,11 +1595,122 @@ static int decode_batch_pieces(jaad_ctx* ctx, const jaad_batch* b, void* pcm_out
     return JAAD_OK;
 }
 
+// ---- dropped frames (jaad_batch.frame_status) ----
+// The frames between dropped ones decode as consecutive sub-batches: segment [s, e) of the batch
+// with the runs clipped to it (a run that has no frame there is left out: its slot keeps its state),
+// array pointers advanced to frame s and the coupling terms of those frames renumbered.  A run cut
+// by a dropped frame continues in the next segment from the state its previous frame left, which is
+// what the reference's next decodeFrame sees after it swallowed the EOSException.
+extern "C++" {
+namespace {
+struct Segments {
+    std::vector<uint32_t> slot, begin;
+    std::vector<jaad_cce_term> terms;
+};
+
+// -1: no frame is dropped; else the number of dropped frames (JAAD_ERR_INVALID_ARG for a bad value)
+int dropped_frames(const jaad_batch* b)
+{
+    if (!b->frame_status) return -1;
+    int n = 0;
+    for (uint32_t f = 0; f < b->n_frames; f++) {
+        if (b->frame_status[f] > JAAD_FRAME_EOS) return JAAD_ERR_INVALID_ARG;
+        n += b->frame_status[f] != JAAD_FRAME_DECODE;
+    }
+    return n ? n : -1;
+}
+
+// the sub-batch of frames [s, e) (none dropped); `seg` owns its run and term arrays
+jaad_batch segment(const jaad_ctx* ctx, const jaad_batch* b, uint32_t s, uint32_t e, Segments& seg)
+{
+    seg.slot.clear();
+    seg.begin.assign(1, 0);
+    for (uint32_t r = 0; r < b->n_runs; r++) {
+        const uint32_t lo = std::max(b->frame_begin[r], s), hi = std::min(b->frame_begin[r + 1], e);
+        if (hi <= lo) continue;
+        seg.slot.push_back(b->stream_slot[r]);
+        seg.begin.push_back(hi - s);
+    }
+    jaad_batch d = *b;
+    const size_t nch = (size_t)ctx->nch;
+    d.n_frames = e - s;
+    d.n_runs = (uint32_t)seg.slot.size();
+    d.stream_slot = seg.slot.data();
+    d.frame_begin = seg.begin.data();
+    d.q = b->q + (size_t)s * nch * 1024;
+    d.sf = b->sf + (size_t)s * nch * 128;
+    d.cb = b->cb + (size_t)s * nch * 128;
+    d.ics = b->ics + (size_t)s * nch;
+    d.ms_used = b->ms_used ? b->ms_used + (size_t)s * 2 * ctx->n_cpe : nullptr;
+    d.tns = b->tns ? b->tns + (size_t)s * nch : nullptr;
+    d.sbr = b->sbr ? b->sbr + s : nullptr;
+    d.frame_status = nullptr;
+    seg.terms.clear();
+    for (uint32_t t = 0; t < b->n_cce_terms; t++)
+        if (b->cce_terms[t].frame >= s && b->cce_terms[t].frame < e) {
+            seg.terms.push_back(b->cce_terms[t]);
+            seg.terms.back().frame -= s;
+        }
+    d.n_cce_terms = (uint32_t)seg.terms.size();
+    d.cce_terms = seg.terms.empty() ? nullptr : seg.terms.data();
+    return d;
+}
+
+// fn(sub-batch, first frame) for every maximal run of non-dropped frames, in order
+template <class F>
+int for_each_segment(const jaad_ctx* ctx, const jaad_batch* b, F&& fn)
+{
+    if (!b->stream_slot || !b->frame_begin) return JAAD_ERR_INVALID_ARG;
+    if (b->frame_begin[0] != 0 || b->frame_begin[b->n_runs] != b->n_frames) return JAAD_ERR_INVALID_ARG;
+    for (uint32_t r = 0; r < b->n_runs; r++)
+        if (b->frame_begin[r + 1] < b->frame_begin[r]) return JAAD_ERR_INVALID_ARG;
+    Segments seg;
+    for (uint32_t s = 0; s < b->n_frames;) {
+        if (b->frame_status[s] != JAAD_FRAME_DECODE) {
+            s++;
+            continue;
+        }
+        uint32_t e = s;
+        while (e < b->n_frames && b->frame_status[e] == JAAD_FRAME_DECODE) e++;
+        const jaad_batch d = segment(ctx, b, s, e, seg);
+        const int rc = fn(d, s);
+        if (rc) return rc;
+        s = e;
+    }
+    return JAAD_OK;
+}
+}  // namespace
+}  // extern "C++"
+
+static int decode_batch_whole(jaad_ctx* ctx, const jaad_batch* b, void* pcm_out, uint32_t flags);
+
 int jaad_decode_batch(jaad_ctx* ctx, const jaad_batch* b, void* pcm_out, size_t pcm_bytes, uint32_t flags)
 {
     int rc = check_batch(ctx, b, pcm_bytes, flags);
     if (rc) return rc;
     if (!pcm_out && b->n_frames) return JAAD_ERR_INVALID_ARG;
+    const int dropped = dropped_frames(b);
+    if (dropped < -1) return dropped;
+    if (dropped < 0) {
+        jaad_batch d = *b;
+        d.frame_status = nullptr;
+        return decode_batch_whole(ctx, &d, pcm_out, flags);
+    }
+    // every segment's side info first: a rejected batch leaves every slot's state as it was
+    rc = for_each_segment(ctx, b, [&](const jaad_batch& d, uint32_t) {
+        const size_t ncf = (size_t)d.n_frames * ctx->nch;
+        return side_info_ok(ctx, &d, 0, ncf) && q_ok_copy(d.q, nullptr, ncf * 1024) ? JAAD_OK : JAAD_ERR_BITSTREAM;
+    });
+    if (rc) return rc;
+    const size_t per = pcm_bytes_per_frame(ctx, flags);
+    return for_each_segment(ctx, b, [&](const jaad_batch& d, uint32_t s) {
+        return decode_batch_whole(ctx, &d, static_cast<uint8_t*>(pcm_out) + per * s, flags);
+    });
+}
+
+static int decode_batch_whole(jaad_ctx* ctx, const jaad_batch* b, void* pcm_out, uint32_t flags)
+{
+    int rc;
     HIPCHK(hipSetDevice(ctx->device));
     if ((rc = io_setup(ctx))) return rc;
     if (ctx->cfg.sbr || ctx->n_elem > 1 || b->n_cce_terms || b->n_frames < 2 * kMinPieceFrames || !b->stream_slot ||
@@ -1684,7 +1795,17 @@ int jaad_decode_batch_device(jaad_ctx* ctx, const jaad_batch* b, void* pcm_dev, 
     if (!pcm_dev && b->n_frames) return JAAD_ERR_INVALID_ARG;
     HIPCHK(hipSetDevice(ctx->device));
     hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : ctx->stream;
-    return launch(ctx, b, pcm_dev, flags, s);
+    const int dropped = dropped_frames(b);
+    if (dropped < -1) return dropped;
+    if (dropped < 0) {
+        jaad_batch d = *b;
+        d.frame_status = nullptr;
+        return launch(ctx, &d, pcm_dev, flags, s);
+    }
+    const size_t per = pcm_bytes_per_frame(ctx, flags);
+    return for_each_segment(ctx, b, [&](const jaad_batch& d, uint32_t f0) {
+        return launch(ctx, &d, static_cast<uint8_t*>(pcm_dev) + per * f0, flags, s);
+    });
 }
 
 int jaad_wait(jaad_ctx* ctx)

@@ -67,7 +67,7 @@ static int cpe_count(int nch) { return nch == 1 ? 0 : nch <= 4 ? 1 : nch <= 6 ? 
 static void decode_common(JNIEnv* env, jaad_ctx* ctx, jint n_frames, jint n_runs, jint nch, jobject stream_slot,
                           jobject frame_begin, jobject q, jobject sf, jobject cb, jobject ics, jobject ms_used,
                           jobject tns, jobject sbr, jobject pcm, jint flags, jint n_cce, jint n_terms, jobject cce_q,
-                          jobject cce_sf, jobject cce_cb, jobject cce_ics, jobject cce_terms) {
+                          jobject cce_sf, jobject cce_cb, jobject cce_ics, jobject cce_terms, jobject frame_status) {
     if (!ctx || n_frames < 0 || n_runs < 0 || n_cce < 0 || n_terms < 0 || nch != jaad_ctx_core_channels(ctx)) {
         throw_aac(env, ctx, JAAD_ERR_INVALID_ARG);
         return;
@@ -95,10 +95,11 @@ static void decode_common(JNIEnv* env, jaad_ctx* ctx, jint n_frames, jint n_runs
         b.cce_ics = (const jaad_ics_info*)addr(env, cce_ics, (jlong)sizeof(jaad_ics_info) * n_cce);
         b.cce_terms = (const jaad_cce_term*)addr(env, cce_terms, (jlong)sizeof(jaad_cce_term) * n_terms);
     }
+    b.frame_status = (const uint8_t*)addr(env, frame_status, (jlong)n_frames);
     jlong pcm_cap = pcm ? (*env)->GetDirectBufferCapacity(env, pcm) : -1;
     void* out = pcm ? (*env)->GetDirectBufferAddress(env, pcm) : NULL;
     if (!b.stream_slot || !b.frame_begin || !b.q || !b.sf || !b.cb || !b.ics || !out || pcm_cap < 0 ||
-        (ms_used && !b.ms_used) || (tns && !b.tns) || (sbr && !b.sbr) ||
+        (ms_used && !b.ms_used) || (tns && !b.tns) || (sbr && !b.sbr) || (frame_status && !b.frame_status) ||
         (n_terms && (!b.cce_q || !b.cce_sf || !b.cce_cb || !b.cce_ics || !b.cce_terms))) {
         throw_aac(env, ctx, JAAD_ERR_INVALID_ARG);
         return;
@@ -109,31 +110,81 @@ static void decode_common(JNIEnv* env, jaad_ctx* ctx, jint n_frames, jint n_runs
 
 /* static native void nativeDecode(long h, int nFrames, int nRuns, int nch, ByteBuffer streamSlot,
  *     ByteBuffer frameBegin, ByteBuffer q, ByteBuffer sf, ByteBuffer cb, ByteBuffer ics,
- *     ByteBuffer msUsed, ByteBuffer tns, ByteBuffer sbr, ByteBuffer pcm, int flags);
+ *     ByteBuffer msUsed, ByteBuffer tns, ByteBuffer sbr, ByteBuffer pcm, int flags,
+ *     ByteBuffer frameStatus);
  * nch: channels per frame (1 SCE core, 2 CPE core, 3..8 multichannel); must equal the context's
  * (jaad_ctx_core_channels), since every buffer capacity below is checked against it.
- * sbr: one jaad_sbr_frame (1968 B, sizeof(jaad_sbr_frame)) per frame for SBR/PS streams, else null */
+ * sbr: one jaad_sbr_frame (1968 B, sizeof(jaad_sbr_frame)) per frame for SBR/PS streams, else null.
+ * frameStatus: one byte per frame (JAAD_FRAME_EOS = 1 for a frame whose parse threw EOSException:
+ * dropped, its PCM slot left as it is) or null when every frame decodes. */
 JNIEXPORT void JNICALL Java_net_sourceforge_jaad_aac_gpu_GpuDSP_nativeDecode(
     JNIEnv* env, jclass cls, jlong h, jint n_frames, jint n_runs, jint nch, jobject stream_slot, jobject frame_begin,
-    jobject q, jobject sf, jobject cb, jobject ics, jobject ms_used, jobject tns, jobject sbr, jobject pcm, jint flags) {
+    jobject q, jobject sf, jobject cb, jobject ics, jobject ms_used, jobject tns, jobject sbr, jobject pcm, jint flags,
+    jobject frame_status) {
     (void)cls;
     decode_common(env, (jaad_ctx*)(intptr_t)h, n_frames, n_runs, nch, stream_slot, frame_begin, q, sf, cb, ics, ms_used,
-                  tns, sbr, pcm, flags, 0, 0, NULL, NULL, NULL, NULL, NULL);
+                  tns, sbr, pcm, flags, 0, 0, NULL, NULL, NULL, NULL, NULL, frame_status);
 }
 
 /* static native void nativeDecodeCoupled(long h, int nFrames, int nRuns, int nch, ByteBuffer streamSlot,
  *     ByteBuffer frameBegin, ByteBuffer q, ByteBuffer sf, ByteBuffer cb, ByteBuffer ics,
  *     ByteBuffer msUsed, ByteBuffer tns, ByteBuffer pcm, int flags, int nCce, int nTerms,
- *     ByteBuffer cceQ, ByteBuffer cceSf, ByteBuffer cceCb, ByteBuffer cceIcs, ByteBuffer cceTerms);
+ *     ByteBuffer cceQ, ByteBuffer cceSf, ByteBuffer cceCb, ByteBuffer cceIcs, ByteBuffer cceTerms,
+ *     ByteBuffer frameStatus);
  * an AAC-LC batch with coupling channel elements: nCce CCE ICStream records and nTerms
- * jaad_cce_term (488 B) in the reference's order (jaad_gpu.h) */
+ * jaad_cce_term (488 B) in the reference's order (jaad_gpu.h); frameStatus as nativeDecode's */
 JNIEXPORT void JNICALL Java_net_sourceforge_jaad_aac_gpu_GpuDSP_nativeDecodeCoupled(
     JNIEnv* env, jclass cls, jlong h, jint n_frames, jint n_runs, jint nch, jobject stream_slot, jobject frame_begin,
     jobject q, jobject sf, jobject cb, jobject ics, jobject ms_used, jobject tns, jobject pcm, jint flags, jint n_cce,
-    jint n_terms, jobject cce_q, jobject cce_sf, jobject cce_cb, jobject cce_ics, jobject cce_terms) {
+    jint n_terms, jobject cce_q, jobject cce_sf, jobject cce_cb, jobject cce_ics, jobject cce_terms,
+    jobject frame_status) {
     (void)cls;
     decode_common(env, (jaad_ctx*)(intptr_t)h, n_frames, n_runs, nch, stream_slot, frame_begin, q, sf, cb, ics, ms_used,
-                  tns, NULL, pcm, flags, n_cce, n_terms, cce_q, cce_sf, cce_cb, cce_ics, cce_terms);
+                  tns, NULL, pcm, flags, n_cce, n_terms, cce_q, cce_sf, cce_cb, cce_ics, cce_terms, frame_status);
+}
+
+/* static native int nativeStateBytes(long h): size of one slot's state blob (jaad_state_bytes).
+ * static native void nativeStateExport(long h, int slot, ByteBuffer buf) /
+ * nativeStateImport(long h, int slot, ByteBuffer buf): a stream's DSP state (IMDCT overlap,
+ * window shape, SBR/PS filterbank and envelope state) out to / back from a direct buffer of at
+ * least nativeStateBytes bytes -- seek/resume of one stream (jaad_state_export / import). */
+JNIEXPORT jint JNICALL Java_net_sourceforge_jaad_aac_gpu_GpuDSP_nativeStateBytes(JNIEnv* env, jclass cls, jlong h) {
+    (void)cls;
+    jaad_ctx* ctx = (jaad_ctx*)(intptr_t)h;
+    if (!ctx) {
+        throw_aac(env, ctx, JAAD_ERR_INVALID_ARG);
+        return 0;
+    }
+    return (jint)jaad_state_bytes(ctx);
+}
+
+static void state_io(JNIEnv* env, jlong h, jint slot, jobject buf, int do_export) {
+    jaad_ctx* ctx = (jaad_ctx*)(intptr_t)h;
+    const jlong cap = buf ? (*env)->GetDirectBufferCapacity(env, buf) : -1;
+    void* p = buf ? (*env)->GetDirectBufferAddress(env, buf) : NULL;
+    if (!ctx || !p || cap < 0 || slot < 0) {
+        throw_aac(env, ctx, JAAD_ERR_INVALID_ARG);
+        return;
+    }
+    const size_t n = jaad_state_bytes(ctx);
+    if ((size_t)cap < n) {
+        throw_aac(env, ctx, JAAD_ERR_INVALID_ARG);
+        return;
+    }
+    const int rc = do_export ? jaad_state_export(ctx, (uint32_t)slot, p, n) : jaad_state_import(ctx, (uint32_t)slot, p, n);
+    if (rc) throw_aac(env, ctx, rc);
+}
+
+JNIEXPORT void JNICALL Java_net_sourceforge_jaad_aac_gpu_GpuDSP_nativeStateExport(JNIEnv* env, jclass cls, jlong h,
+                                                                                jint slot, jobject buf) {
+    (void)cls;
+    state_io(env, h, slot, buf, 1);
+}
+
+JNIEXPORT void JNICALL Java_net_sourceforge_jaad_aac_gpu_GpuDSP_nativeStateImport(JNIEnv* env, jclass cls, jlong h,
+                                                                                jint slot, jobject buf) {
+    (void)cls;
+    state_io(env, h, slot, buf, 0);
 }
 
 JNIEXPORT void JNICALL Java_net_sourceforge_jaad_aac_gpu_GpuDSP_nativeReset(JNIEnv* env, jclass cls, jlong h,

@@ -281,46 +281,76 @@ __device__ __forceinline__ void xch_hi(float& a, float& b)
     a = __int_as_float(r[0]);
     b = __int_as_float(r[1]);
 }
-// Lane bits 0..3 for two register pairs (p, p | 1<<I) and (r, r | 1<<I) at once: each output is
-// ONE v_cndmask_b32 whose src0 is the partner lane's value through a DPP swizzle
-// (dst = vcc ? src1 : swz(src0)): a' = bit clear ? a : swz(b), b' = bit set ? b : swz(a).
+// Lane bits 0..3 for two register pairs (a0, b0) and (a1, b1) at once:
+//   a' = bit clear ? a : b(partner),  b' = bit set ? b : a(partner).
+// VOP2 v_cndmask_b32 (its lane mask is the implicit VCC operand, DPP forms included) issues at
+// ~13.9 SIMD cycles per wave-instruction at 3 waves/SIMD on gfx950, against 3.3 for a DPP move and
+// 3.6 for the VOP3 v_cndmask_b32_e64 with an SGPR-pair mask (tools/valu_rate.hip,
+// profiles/round4_valu_rate.txt), so no exchange selects through VCC:
+// * lane bits 2, 3: DPP moves under a bank mask (bank = lane bits 3..2 of the 16-lane row) write
+//   only the lanes of one half: b' <- a(partner) in the bit-clear banks, a' <- b(partner) in the
+//   bit-set banks, from a copy of b (the first move overwrites b);
+// * lane bits 0, 1 (below the bank granularity): both partners' values by full DPP moves, then one
+//   v_cndmask_b32_e64 per output with the constant lane mask in an SGPR pair.
 // Swizzles: lane ^ 1, ^ 2 by quad_perm; ^ 8 by row_ror:8; ^ 4 by row_ror:4 (lanes with bit 2 set
-// read lane - 4) and row_ror:12 (bit 2 clear read lane + 4).  The two s_movs in front are the
-// 2 wait states a DPP read of a VGPR that a VALU instruction just wrote needs.
+// read lane - 4) and row_ror:12 (bit 2 clear read lane + 4).  A DPP read of a VGPR that a VALU
+// instruction wrote needs 2 wait states: the copies (bits 2, 3) or an s_nop (bits 0, 1) give them.
 template <int L>
 __device__ __forceinline__ void xch2(f2& a0, f2& b0, f2& a1, f2& b1)
 {
-    // lanes with bit L set (the pattern repeats per 32 lanes: vcc_lo = vcc_hi, literal operands,
-    // no SGPRs held across the exchanges)
-    constexpr uint32_t kHi = L == 0 ? 0xAAAAAAAAu : L == 1 ? 0xCCCCCCCCu : L == 2 ? 0xF0F0F0F0u : 0xFF00FF00u;
-    f2 na0, nb0, na1, nb1;
-#define JAAD_XCH_BODY(QA, QB)                                                                    \
-    asm("s_mov_b32 vcc_lo, %[lo]\n\t"                                                            \
-        "s_mov_b32 vcc_hi, %[lo]\n\t"                                                            \
-        "v_cndmask_b32_dpp %[na0x], %[b0x], %[a0x], vcc " QA " row_mask:0xf bank_mask:0xf\n\t"   \
-        "v_cndmask_b32_dpp %[na0y], %[b0y], %[a0y], vcc " QA " row_mask:0xf bank_mask:0xf\n\t"   \
-        "v_cndmask_b32_dpp %[na1x], %[b1x], %[a1x], vcc " QA " row_mask:0xf bank_mask:0xf\n\t"   \
-        "v_cndmask_b32_dpp %[na1y], %[b1y], %[a1y], vcc " QA " row_mask:0xf bank_mask:0xf\n\t"   \
-        "s_mov_b32 vcc_lo, %[hi]\n\t"                                                            \
-        "s_mov_b32 vcc_hi, %[hi]\n\t"                                                            \
-        "v_cndmask_b32_dpp %[nb0x], %[a0x], %[b0x], vcc " QB " row_mask:0xf bank_mask:0xf\n\t"   \
-        "v_cndmask_b32_dpp %[nb0y], %[a0y], %[b0y], vcc " QB " row_mask:0xf bank_mask:0xf\n\t"   \
-        "v_cndmask_b32_dpp %[nb1x], %[a1x], %[b1x], vcc " QB " row_mask:0xf bank_mask:0xf\n\t"   \
-        "v_cndmask_b32_dpp %[nb1y], %[a1y], %[b1y], vcc " QB " row_mask:0xf bank_mask:0xf"       \
-        : [na0x] "=&v"(na0.x), [na0y] "=&v"(na0.y), [na1x] "=&v"(na1.x), [na1y] "=&v"(na1.y),     \
-          [nb0x] "=&v"(nb0.x), [nb0y] "=&v"(nb0.y), [nb1x] "=&v"(nb1.x), [nb1y] "=&v"(nb1.y)      \
-        : [a0x] "v"(a0.x), [a0y] "v"(a0.y), [a1x] "v"(a1.x), [a1y] "v"(a1.y), [b0x] "v"(b0.x),    \
-          [b0y] "v"(b0.y), [b1x] "v"(b1.x), [b1y] "v"(b1.y), [lo] "i"(~kHi), [hi] "i"(kHi)        \
-        : "vcc")
-    if constexpr (L == 0) JAAD_XCH_BODY("quad_perm:[1,0,3,2]", "quad_perm:[1,0,3,2]");
-    else if constexpr (L == 1) JAAD_XCH_BODY("quad_perm:[2,3,0,1]", "quad_perm:[2,3,0,1]");
-    else if constexpr (L == 2) JAAD_XCH_BODY("row_ror:4", "row_ror:12");
-    else JAAD_XCH_BODY("row_ror:8", "row_ror:8");
-#undef JAAD_XCH_BODY
-    a0 = na0;
-    b0 = nb0;
-    a1 = na1;
-    b1 = nb1;
+    if constexpr (L >= 2) {
+        float t0x, t0y, t1x, t1y;
+#define JAAD_XCH_BANK(RLO, BLO, RHI, BHI)                                                               \
+    asm("v_mov_b32 %[t0x], %[b0x]\n\t"                                                                  \
+        "v_mov_b32 %[t0y], %[b0y]\n\t"                                                                  \
+        "v_mov_b32 %[t1x], %[b1x]\n\t"                                                                  \
+        "v_mov_b32 %[t1y], %[b1y]\n\t"                                                                  \
+        "v_mov_b32_dpp %[b0x], %[a0x] " RLO " row_mask:0xf bank_mask:" BLO "\n\t"                       \
+        "v_mov_b32_dpp %[b0y], %[a0y] " RLO " row_mask:0xf bank_mask:" BLO "\n\t"                       \
+        "v_mov_b32_dpp %[b1x], %[a1x] " RLO " row_mask:0xf bank_mask:" BLO "\n\t"                       \
+        "v_mov_b32_dpp %[b1y], %[a1y] " RLO " row_mask:0xf bank_mask:" BLO "\n\t"                       \
+        "v_mov_b32_dpp %[a0x], %[t0x] " RHI " row_mask:0xf bank_mask:" BHI "\n\t"                       \
+        "v_mov_b32_dpp %[a0y], %[t0y] " RHI " row_mask:0xf bank_mask:" BHI "\n\t"                       \
+        "v_mov_b32_dpp %[a1x], %[t1x] " RHI " row_mask:0xf bank_mask:" BHI "\n\t"                       \
+        "v_mov_b32_dpp %[a1y], %[t1y] " RHI " row_mask:0xf bank_mask:" BHI                              \
+        : [a0x] "+v"(a0.x), [a0y] "+v"(a0.y), [a1x] "+v"(a1.x), [a1y] "+v"(a1.y), [b0x] "+v"(b0.x),     \
+          [b0y] "+v"(b0.y), [b1x] "+v"(b1.x), [b1y] "+v"(b1.y), [t0x] "=&v"(t0x), [t0y] "=&v"(t0y),     \
+          [t1x] "=&v"(t1x), [t1y] "=&v"(t1y))
+        // bit 2: clear = banks 0, 2 (0x5), set = banks 1, 3 (0xA); bit 3: clear = banks 0, 1 (0x3)
+        if constexpr (L == 2) JAAD_XCH_BANK("row_ror:12", "0x5", "row_ror:4", "0xa");
+        else JAAD_XCH_BANK("row_ror:8", "0x3", "row_ror:8", "0xc");
+#undef JAAD_XCH_BANK
+    } else {
+        // lanes with bit L set
+        constexpr uint64_t kHi = L == 0 ? 0xAAAAAAAAAAAAAAAAull : 0xCCCCCCCCCCCCCCCCull;
+        float u0x, u0y, u1x, u1y, w0x, w0y, w1x, w1y;
+#define JAAD_XCH_QUAD(QP)                                                                             \
+    asm("s_nop 1\n\t"                                                                                 \
+        "v_mov_b32_dpp %[u0x], %[a0x] " QP " row_mask:0xf bank_mask:0xf\n\t"                          \
+        "v_mov_b32_dpp %[u0y], %[a0y] " QP " row_mask:0xf bank_mask:0xf\n\t"                          \
+        "v_mov_b32_dpp %[u1x], %[a1x] " QP " row_mask:0xf bank_mask:0xf\n\t"                          \
+        "v_mov_b32_dpp %[u1y], %[a1y] " QP " row_mask:0xf bank_mask:0xf\n\t"                          \
+        "v_mov_b32_dpp %[w0x], %[b0x] " QP " row_mask:0xf bank_mask:0xf\n\t"                          \
+        "v_mov_b32_dpp %[w0y], %[b0y] " QP " row_mask:0xf bank_mask:0xf\n\t"                          \
+        "v_mov_b32_dpp %[w1x], %[b1x] " QP " row_mask:0xf bank_mask:0xf\n\t"                          \
+        "v_mov_b32_dpp %[w1y], %[b1y] " QP " row_mask:0xf bank_mask:0xf\n\t"                          \
+        "v_cndmask_b32_e64 %[a0x], %[a0x], %[w0x], %[hi]\n\t"                                         \
+        "v_cndmask_b32_e64 %[a0y], %[a0y], %[w0y], %[hi]\n\t"                                         \
+        "v_cndmask_b32_e64 %[a1x], %[a1x], %[w1x], %[hi]\n\t"                                         \
+        "v_cndmask_b32_e64 %[a1y], %[a1y], %[w1y], %[hi]\n\t"                                         \
+        "v_cndmask_b32_e64 %[b0x], %[u0x], %[b0x], %[hi]\n\t"                                         \
+        "v_cndmask_b32_e64 %[b0y], %[u0y], %[b0y], %[hi]\n\t"                                         \
+        "v_cndmask_b32_e64 %[b1x], %[u1x], %[b1x], %[hi]\n\t"                                         \
+        "v_cndmask_b32_e64 %[b1y], %[u1y], %[b1y], %[hi]"                                             \
+        : [a0x] "+v"(a0.x), [a0y] "+v"(a0.y), [a1x] "+v"(a1.x), [a1y] "+v"(a1.y), [b0x] "+v"(b0.x),   \
+          [b0y] "+v"(b0.y), [b1x] "+v"(b1.x), [b1y] "+v"(b1.y), [u0x] "=&v"(u0x), [u0y] "=&v"(u0y),   \
+          [u1x] "=&v"(u1x), [u1y] "=&v"(u1y), [w0x] "=&v"(w0x), [w0y] "=&v"(w0y), [w1x] "=&v"(w1x),   \
+          [w1y] "=&v"(w1y)                                                                            \
+        : [hi] "s"(kHi))
+        if constexpr (L == 0) JAAD_XCH_QUAD("quad_perm:[1,0,3,2]");
+        else JAAD_XCH_QUAD("quad_perm:[2,3,0,1]");
+#undef JAAD_XCH_QUAD
+    }
 }
 
 // register bit I <-> lane bit L for all four register pairs, both floats of each complex value
@@ -1263,6 +1293,10 @@ __global__ __launch_bounds__(64 * waves_per_wg<kMode == 1>()) void lc_decode_ker
             STAMP(9);
             {
                 const int u2 = lane_id();
+                // a prefix frame's stores land past the frame's 4096-byte range (dropped by the
+                // buffer resource); the offset is added as a wave-uniform value, not selected per
+                // lane (a VOP2 v_cndmask costs ~4 VALU issue slots on gfx950)
+                const int drop = emit ? 0 : 4096;
                 if constexpr (planar) {
 #pragma unroll
                     for (int o = 0; o < 16; o++) {
@@ -1276,7 +1310,7 @@ __global__ __launch_bounds__(64 * waves_per_wg<kMode == 1>()) void lc_decode_ker
                         const float* srcb = c ? W.rsp : W.buf;
 #pragma unroll
                         for (int jj = 0; jj < 4; jj++)
-                            store16(*reinterpret_cast<const v4u*>(srcb + 4 * u2 + 256 * jj), dst, emit ? 16 * u2 + 1024 * jj : 4096, false);
+                            store16(*reinterpret_cast<const v4u*>(srcb + 4 * u2 + 256 * jj), dst, 16 * u2 + 1024 * jj + drop, false);
                     }
                     wave_sync();
                 } else if constexpr (out_f32) {  // tolerance/debug format: strided stores
@@ -1302,7 +1336,7 @@ __global__ __launch_bounds__(64 * waves_per_wg<kMode == 1>()) void lc_decode_ker
                     const __amdgpu_buffer_rsrc_t dst = frame_rsrc(reinterpret_cast<uint8_t*>(A.pcm) + (size_t)f * 4096, 4096);
 #pragma unroll
                     for (int jj = 0; jj < 4; jj++)
-                        store16(*reinterpret_cast<const v4u*>(stage + 4 * u2 + 256 * jj), dst, emit ? 16 * u2 + 1024 * jj : 4096, true);
+                        store16(*reinterpret_cast<const v4u*>(stage + 4 * u2 + 256 * jj), dst, 16 * u2 + 1024 * jj + drop, true);
                     wave_sync();
                 }
             }

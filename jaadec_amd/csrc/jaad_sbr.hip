@@ -999,9 +999,10 @@ __device__ __forceinline__ void synthesis32(const SbrArgs& A, const SbrChunk& ck
 // SynthesisFilterbank64.synthesis (A/sbr/SynthesisFilterbank64.java:9-79) + SampleBuffer PCM
 // ---------------------------------------------------------------------------------------------
 // kDown: SynthesisFilterbank32 (downsampled SBR, A/sbr/SynthesisFilterbank32.java:44-93), bands
-// 0..31, 32 samples per slot.  Its DCT-IV / DST-IV are evaluated as double sums over host-built
-// double coefficients (the reference's generated DCT4_32 / DST4_32 are not restated, so this path
-// matches the oracle's restatement bit for bit and the reference within +-1 LSB; jaad_oracle_sbr.c).
+// 0..31, 32 samples per slot.  Its DCT-IV / DST-IV run the reference's own generated DCT4_32 /
+// DST4_32 op lists (tables/jaad_sbr_dct32.inc, unrolled at compile time above), and the
+// pre-twiddle is the reference's qmf32_pre_twiddle, so oracle, kernel and reference perform the
+// same binary32 operations in the same order.
 template <bool kDown>
 __global__ __launch_bounds__(256) void sbr_synthesis_kernel(SbrArgs A)
 {

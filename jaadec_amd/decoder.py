@@ -219,7 +219,7 @@ class Decoder:
         except N.JaadError as e:
             raise AACException(str(e)) from e
 
-    def _parse(self, frames: list) -> N.Batch:
+    def _parse(self, frames: list, drop_eos: bool = False) -> N.Batch:
         if self._parser is None:
             if self._ctx is None:
                 if not frames:
@@ -229,20 +229,26 @@ class Decoder:
                 self._implicit_sbr(bytes(frames[0]))
             self._parser = N.Parser(self.config.cfg())
         try:
-            return self._parser.parse(frames, self.slot)
+            return self._parser.parse(frames, self.slot, drop_eos=drop_eos)
         except N.JaadError as e:
             raise (EOSException if e.status == N.ERR_EOS else AACException)(str(e)) from e
 
-    def decodeFrames(self, batch, buffers: list[SampleBuffer]) -> None:  # noqa: N802
+    def decodeFrames(self, batch, buffers: list[SampleBuffer], _drop_eos: bool = True) -> None:  # noqa: N802
         """Decode consecutive frames of this stream -- a list of raw_data_blocks or a parsed
-        ``native.Batch`` -- buffer i receives frame i's PCM."""
+        ``native.Batch`` -- buffer i receives frame i's PCM.
+
+        Per frame as Decoder.decodeFrame (A/Decoder.java:89-101): a frame whose bitstream ends
+        early is logged and dropped -- its buffer is left as it is, the stream continues from the
+        previous frame's state -- and still counts as a frame; the rest of the batch decodes
+        (jaad_batch.frame_status).  Any other error rejects the whole batch (AACException) and
+        leaves the decoder as it was."""
         snap = None
         if isinstance(batch, (list, tuple)):
             # the parser commits frame by frame: roll it back if this batch is not decoded, so
             # it never runs ahead of the DSP state (a failed parse restores nothing else)
             snap = self._parser.snapshot() if self._parser is not None else _FRESH
             try:
-                batch = self._parse(list(batch))
+                batch = self._parse(list(batch), drop_eos=_drop_eos)
             except AACException:
                 self._rollback(snap)
                 raise
@@ -253,7 +259,8 @@ class Decoder:
             raise AACException("one SampleBuffer per frame expected")
         b = N.Batch(batch.q, batch.sf, batch.cb, batch.ics, batch.ms_used, batch.tns,
                     np.array([self.slot], np.uint32), np.array([0, batch.n_frames], np.uint32), batch.nch,
-                    batch.sbr, batch.cce_q, batch.cce_sf, batch.cce_cb, batch.cce_ics, batch.cce_terms)
+                    batch.sbr, batch.cce_q, batch.cce_sf, batch.cce_cb, batch.cce_ics, batch.cce_terms,
+                    batch.frame_status)
         flags = self._flags(buffers[0]) if buffers else 0
         try:
             pcm = self._ctx.decode(b, flags)
@@ -263,7 +270,11 @@ class Decoder:
         if snap is not None and snap is not _FRESH:
             snap.close()
         rate = self.config.getOutputFrequency()
+        st = b.frame_status
         for i, buf in enumerate(buffers):
+            if st is not None and st[i] != N.FRAME_DECODE:
+                LOGGER.warning("unexpected end of frame: frame %d dropped", self.frames + i)
+                continue  # the reference swallows the EOSException: this buffer keeps what it had
             want = buf.big_endian
             buf._set(pcm[i].tobytes(), rate, self.config.getSampleLength(), self.config.getChannelCount())
             buf.big_endian = flags == N.PCM_BIG_ENDIAN
@@ -283,7 +294,8 @@ class Decoder:
 
     def decode0(self, frame, buffer: SampleBuffer) -> None:
         """A/Decoder.java:103-121: one frame; an EOSException propagates."""
-        self.decodeFrames([frame] if isinstance(frame, (bytes, bytearray, memoryview)) else frame, [buffer])
+        self.decodeFrames([frame] if isinstance(frame, (bytes, bytearray, memoryview)) else frame, [buffer],
+                          _drop_eos=False)
 
     def decodeFrame(self, frame, buffer: SampleBuffer) -> None:  # noqa: N802
         """A/Decoder.java:89-101 for one frame (raw_data_block bytes or a parsed Batch): a frame that

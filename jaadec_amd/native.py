@@ -17,7 +17,7 @@ import os as _os
 LIB_PATH = Path(_os.environ["JAAD_LIB"]) if _os.environ.get("JAAD_LIB") else PKG / "libjaadgpu.so"
 SYNTH_PATH = PKG / "libjaadsynth.so"
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 # status codes (jaad_status)
 OK, ERR_INVALID_ARG, ERR_NO_DEVICE, ERR_HIP, ERR_UNSUPPORTED, ERR_BITSTREAM, ERR_NOMEM, ERR_ABI, ERR_EOS = 0, -1, -2, -3, -4, -5, -6, -7, -8
@@ -70,7 +70,11 @@ class BatchStruct(C.Structure):
                 ("frame_begin", C.c_void_p), ("q", C.c_void_p), ("sf", C.c_void_p), ("cb", C.c_void_p),
                 ("ics", C.c_void_p), ("ms_used", C.c_void_p), ("tns", C.c_void_p), ("sbr", C.c_void_p),
                 ("n_cce", C.c_uint32), ("n_cce_terms", C.c_uint32), ("cce_q", C.c_void_p), ("cce_sf", C.c_void_p),
-                ("cce_cb", C.c_void_p), ("cce_ics", C.c_void_p), ("cce_terms", C.c_void_p)]
+                ("cce_cb", C.c_void_p), ("cce_ics", C.c_void_p), ("cce_terms", C.c_void_p),
+                ("frame_status", C.c_void_p)]
+
+# jaad_batch.frame_status values (JAAD_FRAME_*)
+FRAME_DECODE, FRAME_EOS = 0, 1
 
 
 class SynthParams(C.Structure):
@@ -216,6 +220,9 @@ class Batch:
     cce_cb: np.ndarray | None = None    # uint8 [n_cce, 128]
     cce_ics: np.ndarray | None = None   # ICS_DTYPE [n_cce]
     cce_terms: np.ndarray | None = None  # CCE_TERM_DTYPE [n_terms], sorted by frame
+    # per-frame status (uint8 [nf] of FRAME_*; None: every frame decodes): FRAME_EOS frames are
+    # dropped as Decoder.decodeFrame drops them (A/Decoder.java:89-101), PCM slot untouched
+    frame_status: np.ndarray | None = None
 
     @property
     def n_frames(self) -> int:
@@ -232,7 +239,16 @@ class Batch:
         return BatchStruct(self.n_frames, len(self.stream_slot), _ptr(self.stream_slot), _ptr(self.frame_begin),
                            _ptr(self.q), _ptr(self.sf), _ptr(self.cb), _ptr(self.ics), _ptr(self.ms_used),
                            _ptr(self.tns), _ptr(self.sbr), self.n_cce, nt, _ptr(self.cce_q), _ptr(self.cce_sf),
-                           _ptr(self.cce_cb), _ptr(self.cce_ics), _ptr(self.cce_terms))
+                           _ptr(self.cce_cb), _ptr(self.cce_ics), _ptr(self.cce_terms), _ptr(self._status()))
+
+    def _status(self) -> np.ndarray | None:
+        if self.frame_status is None:
+            return None
+        st = np.ascontiguousarray(self.frame_status, np.uint8)
+        if st.shape != (self.n_frames,):
+            raise ValueError("frame_status: one uint8 per frame expected")
+        self.frame_status = st
+        return st
 
     def _cce_for(self, frames: np.ndarray) -> dict:
         """The coupling of the given (renumbered in order) frames: all CCE records kept, the terms
@@ -261,7 +277,8 @@ class Batch:
                      None if self.ms_used is None else np.ascontiguousarray(self.ms_used[frames]),
                      None if self.tns is None else np.ascontiguousarray(self.tns[cfr]),
                      np.ascontiguousarray(self.stream_slot[runs]).astype(np.uint32), begin, self.nch,
-                     None if self.sbr is None else np.ascontiguousarray(self.sbr[frames]), **self._cce_for(frames))
+                     None if self.sbr is None else np.ascontiguousarray(self.sbr[frames]), **self._cce_for(frames),
+                     frame_status=None if self.frame_status is None else np.ascontiguousarray(self.frame_status[frames]))
 
     def split_frames(self, cut: int) -> tuple["Batch", "Batch"]:
         """Split every run at its frame `cut` (for multi-call continuation tests)."""
@@ -285,7 +302,8 @@ class Batch:
                          None if self.ms_used is None else np.ascontiguousarray(self.ms_used[frames]),
                          None if self.tns is None else np.ascontiguousarray(self.tns[cfr]),
                          self.stream_slot.copy(), begin, self.nch,
-                         None if self.sbr is None else np.ascontiguousarray(self.sbr[frames]), **self._cce_for(frames))
+                         None if self.sbr is None else np.ascontiguousarray(self.sbr[frames]), **self._cce_for(frames),
+                         frame_status=None if self.frame_status is None else np.ascontiguousarray(self.frame_status[frames]))
 
         return mk(a_frames, la), mk(b_frames, lb)
 
@@ -425,10 +443,12 @@ class Context:
 
     def decode(self, batch: Batch, flags: int = PCM_BIG_ENDIAN, out: np.ndarray | None = None) -> np.ndarray:
         """Host-buffer batch decode -> PCM bytes (uint8 [n_frames, frame_bytes]), into `out` when
-        given (e.g. a buffer registered with register())."""
+        given (e.g. a buffer registered with register()).  The rows of dropped frames
+        (batch.frame_status) are left as they are: zero in a fresh output."""
         nb = lib().jaad_frame_pcm_bytes(C.byref(self.cfg), flags)
         if out is None:
-            out = np.empty((batch.n_frames, nb), np.uint8)
+            drops = batch.frame_status is not None and bool(np.any(batch.frame_status))
+            out = (np.zeros if drops else np.empty)((batch.n_frames, nb), np.uint8)
         assert out.flags["C_CONTIGUOUS"] and out.nbytes >= batch.n_frames * nb
         bs = batch.struct()
         self._check(lib().jaad_decode_batch(self.h, C.byref(bs), _ptr(out), out.nbytes, flags), "jaad_decode_batch")
@@ -482,7 +502,7 @@ class Context:
         bs = BatchStruct(batch.n_frames, len(batch.stream_slot), _ptr(batch.stream_slot), _ptr(batch.frame_begin),
                          dev["q"], dev["sf"], dev["cb"], dev["ics"], dev.get("ms_used"), dev.get("tns"),
                          _ptr(batch.sbr), batch.n_cce, nt, dev.get("cce_q"), dev.get("cce_sf"), dev.get("cce_cb"),
-                         dev.get("cce_ics"), _ptr(batch.cce_terms))
+                         dev.get("cce_ics"), _ptr(batch.cce_terms), _ptr(batch._status()))
         self._check(lib().jaad_decode_batch_device(self.h, C.byref(bs), pcm_dev_ptr, pcm_bytes, flags, stream_ptr),
                     "jaad_decode_batch_device")
 
@@ -619,9 +639,16 @@ class Parser:
     def pns_state(self, v: int) -> None:
         lib().jaad_parser_set_pns_state(self.h, v)
 
-    def parse(self, frames: list, slot: int = 0) -> Batch:
-        """raw_data_blocks (bytes) of this stream -> one-run Batch in the jaad_gpu.h layout."""
+    def parse(self, frames: list, slot: int = 0, drop_eos: bool = False) -> Batch:
+        """raw_data_blocks (bytes) of this stream -> one-run Batch in the jaad_gpu.h layout.
+
+        drop_eos: a frame whose bitstream ends early (JAAD_ERR_EOS) is marked FRAME_EOS in
+        batch.frame_status -- the decode then drops it as Decoder.decodeFrame drops a frame that
+        throws EOSException (A/Decoder.java:89-101) -- and parsing goes on with the next frame
+        (the parser is atomic: the failed frame left its state as it was).  Without it the
+        JaadError propagates."""
         nf, nch, ncpe = len(frames), self.nch, n_cpe(self.cfg)
+        status = None
         q = np.zeros((nf * nch, 1024), np.int16)
         sf = np.zeros((nf * nch, 128), np.uint8)
         cb = np.zeros((nf * nch, 128), np.uint8)
@@ -643,6 +670,17 @@ class Parser:
                          cq.ctypes.data, csf.ctypes.data, ccb.ctypes.data, cics.ctypes.data, cterms.ctypes.data,
                          8, 64, 0, 0)
             rc = lib().jaad_parse_frame(self.h, bytes(fr), len(fr), C.byref(o))
+            if rc == ERR_EOS and drop_eos:
+                if status is None:
+                    status = np.zeros(nf, np.uint8)
+                status[i] = FRAME_EOS
+                for a in (q, sf, cb, ics, tns):
+                    a[i * nch:(i + 1) * nch] = 0
+                if ms is not None:
+                    ms[i] = 0
+                if sbr is not None:
+                    sbr[i] = np.zeros((), SBR_FRAME_DTYPE)
+                continue
             if rc:
                 raise JaadError(rc, f"jaad_parse_frame (frame {i})")
             if o.n_cce:
@@ -658,6 +696,7 @@ class Parser:
             tns = None
         b = Batch(q, sf, cb, ics, ms, tns, np.array([slot], np.uint32), np.array([0, nf], np.uint32), nch)
         b.sbr = sbr
+        b.frame_status = status
         if recs:
             b.cce_q = np.ascontiguousarray(np.stack([r[0] for r in recs]))
             b.cce_sf = np.ascontiguousarray(np.stack([r[1] for r in recs]))

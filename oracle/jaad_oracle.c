@@ -596,6 +596,7 @@ int orc_decode_batch(const jaad_stream_cfg* cfg, orc_stream* streams, const jaad
     for (uint32_t r = 0; r < b->n_runs; r++) {
         orc_stream* st = &streams[b->stream_slot[r]];
         for (uint32_t f = b->frame_begin[r]; f < b->frame_begin[r + 1]; f++) {
+            if (b->frame_status && b->frame_status[f]) continue;  /* dropped (A/Decoder.java:96-100) */
             rc = decode_frame(cfg, st, b, f, &rs, (unsigned char*)pcm_out + per * f, flags);
             if (rc) return rc;
         }
@@ -621,7 +622,8 @@ static void* mt_worker(void* p)
     for (uint32_t r = j->r0; r < j->r1 && !j->rc; r++) {
         orc_stream* st = &j->streams[j->b->stream_slot[r]];
         for (uint32_t f = j->b->frame_begin[r]; f < j->b->frame_begin[r + 1] && !j->rc; f++)
-            j->rc = decode_frame(j->cfg, st, j->b, f, &rs, j->pcm + j->per * f, j->flags);
+            if (!j->b->frame_status || !j->b->frame_status[f])
+                j->rc = decode_frame(j->cfg, st, j->b, f, &rs, j->pcm + j->per * f, j->flags);
     }
     return NULL;
 }

@@ -288,6 +288,7 @@ def decode_batch_mc(sf_index: int, batch, ids, flags: int = 0, threads: int = 1,
                      np.ascontiguousarray(batch.ms_used[:, 2 * cpe:2 * cpe + 2]) if k == 2 else None,
                      np.ascontiguousarray(batch.tns[cfr]) if batch.tns is not None else None,
                      batch.stream_slot.copy(), batch.frame_begin.copy(), k)
+        el.frame_status = batch.frame_status
         if batch.cce_terms is not None:  # the element's coupling terms, channels relative to it
             t = batch.cce_terms[(batch.cce_terms["channel"] >= c) & (batch.cce_terms["channel"] < c + k)].copy()
             t["channel"] -= c
@@ -329,7 +330,8 @@ def decode_batch(cfg, batch, streams: Streams, flags: int = 0, threads: int = 1)
     """Decode a jaadec_amd.native.Batch on the CPU restatement; returns uint8 [n_frames, bytes]."""
     down = cfg.sbr and cfg.ext_sf_index == cfg.sf_index  # downsampled SBR: core-rate output
     nb = (2048 if cfg.sbr and not down else 1024) * 2 * (4 if flags & 2 else 2)
-    out = np.empty((batch.n_frames, nb), np.uint8)
+    drops = getattr(batch, "frame_status", None) is not None and bool(np.any(batch.frame_status))
+    out = (np.zeros if drops else np.empty)((batch.n_frames, nb), np.uint8)  # dropped frames: rows stay 0
     bs = batch.struct()
     if threads == 1:
         rc = lib().orc_decode_batch(C.addressof(cfg), streams.state.ctypes.data, C.addressof(bs), out.ctypes.data,

@@ -1,0 +1,303 @@
+"""Per-frame status in the batch ABI (jaad_batch.frame_status): a frame whose
+bitstream ended early is dropped as Decoder.decodeFrame drops it (A/Decoder.java:89-101: the
+EOSException is caught, process() and buffer.accept are skipped, the frame still counts) -- no DSP
+for it, its PCM slot untouched, its stream continuing from the previous frame's state -- while
+the rest of the batch decodes.
+
+CPU: Parser.parse(drop_eos=True) marks the truncated frame and parses the next ones as if it were
+absent; the restatement with a status array equals the restatement of the batch without those
+frames.  GPU: every path (AAC-LC stereo/mono, window switching, HE-AAC v1/v2, multichannel,
+coupling, host and device entry, the Decoder facade, the JNI glue) against the restatement."""
+import numpy as np
+import pytest
+
+from jaadec_amd import native as N
+from oracle import oracle as O
+
+
+def without_frames(b: N.Batch, drop) -> N.Batch:
+    """b with the given frames removed (runs shortened, slots kept): what the stream sees when the
+    dropped frames never happened."""
+    drop = set(int(f) for f in drop)
+    fb = b.frame_begin
+    keep, lens = [], []
+    for r in range(len(b.stream_slot)):
+        fr = [f for f in range(int(fb[r]), int(fb[r + 1])) if f not in drop]
+        keep += fr
+        lens.append(len(fr))
+    frames = np.array(keep, np.int64)
+    cfr = (frames[:, None] * b.nch + np.arange(b.nch)[None, :]).reshape(-1)
+    begin = np.zeros(len(lens) + 1, np.uint32)
+    begin[1:] = np.cumsum(lens)
+    return N.Batch(np.ascontiguousarray(b.q[cfr]), np.ascontiguousarray(b.sf[cfr]), np.ascontiguousarray(b.cb[cfr]),
+                   np.ascontiguousarray(b.ics[cfr]),
+                   None if b.ms_used is None else np.ascontiguousarray(b.ms_used[frames]),
+                   None if b.tns is None else np.ascontiguousarray(b.tns[cfr]),
+                   b.stream_slot.copy(), begin, b.nch,
+                   None if b.sbr is None else np.ascontiguousarray(b.sbr[frames]), **b._cce_for(frames))
+
+
+def drop_pattern(b: N.Batch) -> np.ndarray:
+    """Dropped frames at a run's first frame, in the middle, two in a row, and a run's last frame."""
+    fb = b.frame_begin
+    st = np.zeros(b.n_frames, np.uint8)
+    st[int(fb[0])] = N.FRAME_EOS
+    r = len(b.stream_slot) // 2
+    mid = (int(fb[r]) + int(fb[r + 1])) // 2
+    st[mid] = st[mid + 1] = N.FRAME_EOS
+    st[int(fb[-1]) - 1] = N.FRAME_EOS
+    st[int(fb[1]) + 5] = N.FRAME_EOS
+    return st
+
+
+def oracle_pcm(cfg, b, flags, threads=4):
+    nsl = int(b.stream_slot.max()) + 1
+    return O.decode_batch(cfg, b, O.Streams(nsl), flags, threads=threads)
+
+
+def test_oracle_status_equals_the_batch_without_the_frames():
+    p = N.synth_params(3, n_streams=3, frames_per_stream=16)
+    b = N.synth_batch(p)
+    cfg = N.cfg_for(p)
+    st = drop_pattern(b)
+    b.frame_status = st
+    got = oracle_pcm(cfg, b, N.PCM_BIG_ENDIAN)
+    assert not got[st == 1].any()  # dropped rows untouched (zero)
+    b.frame_status = None
+    want = oracle_pcm(cfg, without_frames(b, np.flatnonzero(st)), N.PCM_BIG_ENDIAN)
+    assert (got[st == 0] == want).all()
+
+
+def test_parser_marks_a_truncated_frame_and_goes_on():
+    p = N.synth_params(3, n_streams=1, frames_per_stream=10, pns_percent=10)
+    b = N.synth_batch(p)
+    frames = O.write_frames(b, p.sf_index)
+    k = 4
+    bad = list(frames)
+    bad[k] = frames[k][:len(frames[k]) // 3]
+    P = N.Parser(N.make_cfg(sf_index=p.sf_index))
+    P.pns_state = int(b.ics["pns_state"][0])
+    with pytest.raises(N.JaadError) as e:
+        P.parse(bad)
+    assert e.value.status == N.ERR_EOS
+    P = N.Parser(N.make_cfg(sf_index=p.sf_index))
+    P.pns_state = int(b.ics["pns_state"][0])
+    got = P.parse(bad, drop_eos=True)
+    assert got.frame_status is not None and np.flatnonzero(got.frame_status).tolist() == [k]
+    assert not got.q[2 * k:2 * k + 2].any() and not got.ics[2 * k:2 * k + 2]["max_sfb"].any()
+    # the frames after it parse exactly as frames after an absent frame: the PNS LCG did not move
+    Q = N.Parser(N.make_cfg(sf_index=p.sf_index))
+    Q.pns_state = int(b.ics["pns_state"][0])
+    ref = Q.parse(frames[:k] + frames[k + 1:])
+    keep = np.r_[0:2 * k, 2 * k + 2:2 * len(frames)]
+    for f in ("q", "sf", "cb"):
+        assert (getattr(got, f)[keep] == getattr(ref, f)).all(), f
+    assert (got.ics[keep]["pns_state"] == ref.ics["pns_state"]).all()
+
+
+# ------------------------------------------------------------------------------------------------
+# GPU
+# ------------------------------------------------------------------------------------------------
+
+def _gpu_vs_oracle(cfg, b, flags, decode_batch=None):
+    st = b.frame_status
+    want = (decode_batch or oracle_pcm)(cfg, b, flags)
+    nsl = int(b.stream_slot.max()) + 1
+    out = np.full(want.shape, 0xA5, np.uint8)  # sentinel: dropped rows must keep it
+    with N.Context(cfg, nsl) as ctx:
+        ctx.decode(b, flags, out=out)
+    assert (out[st == 1] == 0xA5).all(), "a dropped frame's PCM slot was written"
+    assert (out[st == 0] == want[st == 0]).all(), np.flatnonzero((out != want).any(1) & (st == 0))[:8]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("config,streams,fps", [(2, 6, 40), (3, 6, 40), (4, 4, 24), (5, 4, 24)])
+def test_gpu_dropped_frames_match_the_restatement(config, streams, fps):
+    p = N.synth_params(config, n_streams=streams, frames_per_stream=fps)
+    b = N.synth_batch(p)
+    b.frame_status = drop_pattern(b)
+    _gpu_vs_oracle(N.cfg_for(p), b, N.PCM_BIG_ENDIAN)
+
+
+@pytest.mark.gpu
+def test_gpu_dropped_frames_mono_and_float32():
+    p = N.synth_params(3, n_streams=3, frames_per_stream=30, channel_config=1)
+    b = N.synth_batch(p)
+    b.frame_status = drop_pattern(b)
+    _gpu_vs_oracle(N.cfg_for(p), b, N.PCM_FLOAT32)
+
+
+@pytest.mark.gpu
+def test_gpu_dropped_frames_multichannel_and_coupling():
+    from tests.test_cce import coupled_batch
+    from tests.test_multichannel import mc_synth
+    b = mc_synth(6, n_streams=3, fps=20, seed=4)
+    b.frame_status = drop_pattern(b)
+    cfg = N.make_cfg(channel_config=6)
+
+    def mc_oracle(cfg, b, flags):
+        return O.decode_batch_mc(3, b, N.MC_ELEMENTS[6], flags, threads=4)
+    _gpu_vs_oracle(cfg, b, N.PCM_BIG_ENDIAN, mc_oracle)
+    c = coupled_batch(2, n_streams=4, fps=20, seed=8)
+    c.frame_status = drop_pattern(c)
+    _gpu_vs_oracle(N.make_cfg(channel_config=2), c, N.PCM_BIG_ENDIAN)
+
+
+@pytest.mark.gpu
+def test_gpu_large_batch_dropped_frames_host_pieces():
+    """A batch big enough for the piece pipeline of the host entry (>= 8192 frames)."""
+    p = N.synth_params(2, n_streams=64, frames_per_stream=160)
+    b = N.synth_batch(p)
+    st = np.zeros(b.n_frames, np.uint8)
+    st[np.random.default_rng(3).choice(b.n_frames, 40, replace=False)] = N.FRAME_EOS
+    b.frame_status = st
+    cfg = N.cfg_for(p)
+    want = oracle_pcm(cfg, b, N.PCM_BIG_ENDIAN, threads=16)
+    out = np.full((b.n_frames, N.pcm_frame_bytes(0)), 0x5A, np.uint8)
+    with N.Context(cfg, 64) as ctx:
+        ctx.decode(b, N.PCM_BIG_ENDIAN, out=out)
+    assert (out[st == 1] == 0x5A).all()
+    assert (out[st == 0] == want[st == 0]).all()
+
+
+@pytest.mark.gpu
+def test_gpu_dropped_frames_device_entry_and_errors():
+    import torch
+    p = N.synth_params(2, n_streams=4, frames_per_stream=30)
+    b = N.synth_batch(p)
+    b.frame_status = drop_pattern(b)
+    cfg = N.cfg_for(p)
+    want = oracle_pcm(cfg, b, N.PCM_BIG_ENDIAN)
+    dev = torch.device("cuda", 0)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a).reshape(-1).view(np.uint8)).to(dev)
+    d = {k: t(getattr(b, k)) for k in ("q", "sf", "cb", "ics", "ms_used")}
+    ptr = {k: v.data_ptr() for k, v in d.items()}
+    nb = N.pcm_frame_bytes(0)
+    pcm = torch.full((b.n_frames * nb,), 0x33, dtype=torch.uint8, device=dev)
+    st = b.frame_status
+    with N.Context(cfg, 4) as ctx:
+        ctx.decode_device(ptr, b, pcm.data_ptr(), pcm.numel(), N.PCM_BIG_ENDIAN)
+        ctx.wait()
+        got = pcm.cpu().numpy().reshape(b.n_frames, nb)
+        assert (got[st == 1] == 0x33).all() and (got[st == 0] == want[st == 0]).all()
+        # every frame dropped: nothing written, no state moved
+        b2 = N.synth_batch(p)
+        b2.frame_status = np.ones(b2.n_frames, np.uint8)
+        out = np.full((b2.n_frames, nb), 7, np.uint8)
+        ctx.decode(b2, N.PCM_BIG_ENDIAN, out=out)
+        assert (out == 7).all()
+        # an unknown status value is refused
+        b2.frame_status = np.full(b2.n_frames, 2, np.uint8)
+        with pytest.raises(N.JaadError) as e:
+            ctx.decode(b2, N.PCM_BIG_ENDIAN)
+        assert e.value.status == N.ERR_INVALID_ARG
+        # a bad side-info record in a later segment: refused before anything decodes
+        b3 = N.synth_batch(p)
+        st3 = np.zeros(b3.n_frames, np.uint8)
+        st3[10] = N.FRAME_EOS
+        b3.frame_status = st3
+        b3.ics["max_sfb"][2 * 50] = 60
+        before = ctx.state_export(0)
+        with pytest.raises(N.JaadError) as e:
+            ctx.decode(b3, N.PCM_BIG_ENDIAN)
+        assert e.value.status == N.ERR_BITSTREAM
+        assert (ctx.state_export(0) == before).all()
+
+
+@pytest.mark.gpu
+def test_decode_frames_drops_a_truncated_frame_per_frame():
+    """frame k of a 40-frame decodeFrames batch is truncated; the other 39 equal the
+    per-frame decode with frame k dropped, and buffer k keeps what it held (here: frame k-1's PCM,
+    as a reused SampleBuffer would)."""
+    from jaadec_amd.decoder import Decoder, SampleBuffer
+    p = N.synth_params(3, n_streams=1, frames_per_stream=40, pns_percent=10)
+    b = N.synth_batch(p)
+    frames = O.write_frames(b, p.sf_index)
+    k = 17
+    bad = list(frames)
+    bad[k] = frames[k][:len(frames[k]) // 2]
+    st = np.zeros(40, np.uint8)
+    st[k] = N.FRAME_EOS
+    b.frame_status = st
+    want = oracle_pcm(N.make_cfg(sf_index=p.sf_index), b, N.PCM_BIG_ENDIAN)
+    dec = Decoder.create(bytes([0x11, 0x90]))
+    dec._parse([])
+    dec._parser.pns_state = int(b.ics["pns_state"][0])
+    bufs = [SampleBuffer() for _ in range(40)]
+    bufs[k]._set(want[k - 1].tobytes(), 48000)
+    dec.decodeFrames(bad, bufs)
+    assert dec.frames == 40
+    for i, buf in enumerate(bufs):
+        assert buf.getData() == (want[k - 1] if i == k else want[i]).tobytes(), i
+    # the stream goes on from frame k+1's state: frame k re-sent whole is the next frame
+    dec.close()
+
+
+@pytest.mark.gpu
+def test_jni_frame_status_and_state_export_import():
+    """nativeDecode's frameStatus buffer, and nativeStateExport/Import (seek/resume) through the
+    mock JNIEnv: a stream decoded in two calls with its state exported, the slot reset and the
+    state imported in between equals one call."""
+    import ctypes as C
+    from tests.test_jni_glue import AAC_EXC, PFX, _buf, _exception, _lib
+    L = _lib()
+    env = L.jni_mock_env()
+    p = N.synth_params(2, n_streams=2, frames_per_stream=24)
+    b = N.synth_batch(p)
+    st = drop_pattern(b)
+    b.frame_status = st
+    cfg = N.cfg_for(p)
+    want = oracle_pcm(cfg, b, N.PCM_BIG_ENDIAN)
+    h = getattr(L, PFX + "nativeCreate")(env, None, 3, 2, 0, 0, 0, 2, 0)
+    assert h and _exception(L) is None
+    decode = getattr(L, PFX + "nativeDecode")
+    try:
+        keep = []
+        out = np.zeros_like(want)
+        args = [_buf(x, keep) for x in (b.stream_slot, b.frame_begin, b.q, b.sf, b.cb, b.ics, b.ms_used, b.tns, None,
+                                         out)]
+        decode(env, None, h, b.n_frames, 2, 2, *args, N.PCM_BIG_ENDIAN, _buf(st, keep))
+        assert _exception(L) is None
+        assert (out[st == 0] == want[st == 0]).all() and not out[st == 1].any()
+        # a status buffer shorter than the batch is refused
+        short = st[:-1].copy()
+        decode(env, None, h, b.n_frames, 2, 2, *args, N.PCM_BIG_ENDIAN, _buf(short, keep))
+        cls, msg = _exception(L)
+        assert cls == AAC_EXC and N.strerror(N.ERR_INVALID_ARG) in msg
+        # seek/resume: frames [0, 12) of both streams, export, reset, import, frames [12, 24)
+        b.frame_status = None
+        full = oracle_pcm(cfg, b, N.PCM_BIG_ENDIAN)
+        a1, a2 = b.split_frames(12)
+        n = getattr(L, PFX + "nativeStateBytes")(env, None, h)
+        assert n > 0 and _exception(L) is None
+        for slot in range(2):
+            getattr(L, PFX + "nativeReset")(env, None, h, slot)
+        o1 = np.zeros((a1.n_frames, want.shape[1]), np.uint8)
+        decode(env, None, h, a1.n_frames, 2, 2, *[_buf(x, keep) for x in (a1.stream_slot, a1.frame_begin, a1.q, a1.sf,
+                                                                         a1.cb, a1.ics, a1.ms_used, a1.tns, None, o1)],
+               N.PCM_BIG_ENDIAN, None)
+        assert _exception(L) is None
+        blobs = [np.zeros(n, np.uint8) for _ in range(2)]
+        for slot in range(2):
+            getattr(L, PFX + "nativeStateExport")(env, None, h, slot, _buf(blobs[slot], keep))
+            assert _exception(L) is None
+            getattr(L, PFX + "nativeReset")(env, None, h, slot)
+        small = np.zeros(n - 1, np.uint8)
+        getattr(L, PFX + "nativeStateImport")(env, None, h, 0, _buf(small, keep))
+        cls, msg = _exception(L)
+        assert cls == AAC_EXC and N.strerror(N.ERR_INVALID_ARG) in msg
+        for slot in range(2):
+            getattr(L, PFX + "nativeStateImport")(env, None, h, slot, _buf(blobs[slot], keep))
+            assert _exception(L) is None
+        o2 = np.zeros((a2.n_frames, want.shape[1]), np.uint8)
+        decode(env, None, h, a2.n_frames, 2, 2, *[_buf(x, keep) for x in (a2.stream_slot, a2.frame_begin, a2.q, a2.sf,
+                                                                         a2.cb, a2.ics, a2.ms_used, a2.tns, None, o2)],
+               N.PCM_BIG_ENDIAN, None)
+        assert _exception(L) is None
+        fb = b.frame_begin
+        for r in range(2):
+            assert (o1[12 * r:12 * r + 12] == full[fb[r]:fb[r] + 12]).all()
+            assert (o2[12 * r:12 * r + 12] == full[fb[r] + 12:fb[r + 1]]).all()
+        del C
+    finally:
+        getattr(L, PFX + "nativeDestroy")(env, None, h)

@@ -30,13 +30,18 @@ def _lib():
     create.restype = C.c_int64
     getattr(L, PFX + "nativeDestroy").argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
     decode = getattr(L, PFX + "nativeDecode")
-    decode.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_int32, C.c_int32] + [C.c_void_p] * 10 + [C.c_int32]
+    decode.argtypes = ([C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_int32, C.c_int32] + [C.c_void_p] * 10 +
+                       [C.c_int32, C.c_void_p])
     getattr(L, PFX + "nativeReset").argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32]
     for name in ("nativeRegister", "nativeUnregister", "nativeFreeDirect"):
         getattr(L, PFX + name).argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p]
     coupled = getattr(L, PFX + "nativeDecodeCoupled")
     coupled.argtypes = ([C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_int32, C.c_int32] + [C.c_void_p] * 9 +
-                        [C.c_int32, C.c_int32, C.c_int32] + [C.c_void_p] * 5)
+                        [C.c_int32, C.c_int32, C.c_int32] + [C.c_void_p] * 6)
+    getattr(L, PFX + "nativeStateBytes").argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
+    getattr(L, PFX + "nativeStateBytes").restype = C.c_int32
+    for name in ("nativeStateExport", "nativeStateImport"):
+        getattr(L, PFX + name).argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_void_p]
     alloc = getattr(L, PFX + "nativeAllocDirect")
     alloc.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int64]
     alloc.restype = C.c_void_p
@@ -61,14 +66,15 @@ def _buf(a, keep):
 def test_exports():
     L = _lib()
     for name in ("nativeCreate", "nativeDestroy", "nativeDecode", "nativeReset", "nativeRegister",
-                 "nativeUnregister", "nativeAllocDirect", "nativeFreeDirect", "nativeDecodeCoupled"):
+                 "nativeUnregister", "nativeAllocDirect", "nativeFreeDirect", "nativeDecodeCoupled",
+                 "nativeStateBytes", "nativeStateExport", "nativeStateImport"):
         assert hasattr(L, PFX + name)
 
 
 def test_invalid_handles_throw_aac_exception():
     L = _lib()
     env = L.jni_mock_env()
-    getattr(L, PFX + "nativeDecode")(env, None, 0, 1, 1, 2, *([None] * 10), 0)
+    getattr(L, PFX + "nativeDecode")(env, None, 0, 1, 1, 2, *([None] * 10), 0, None)
     cls, msg = _exception(L)
     assert cls == AAC_EXC and N.strerror(N.ERR_INVALID_ARG) in msg
     getattr(L, PFX + "nativeReset")(env, None, 0, 0)
@@ -85,6 +91,13 @@ def test_invalid_handles_throw_aac_exception():
     assert getattr(L, PFX + "nativeAllocDirect")(env, None, 0, 4096) is None
     cls, msg = _exception(L)
     assert cls == AAC_EXC and N.strerror(N.ERR_INVALID_ARG) in msg
+    assert getattr(L, PFX + "nativeStateBytes")(env, None, 0) == 0
+    cls, msg = _exception(L)
+    assert cls == AAC_EXC and N.strerror(N.ERR_INVALID_ARG) in msg
+    for name in ("nativeStateExport", "nativeStateImport"):
+        getattr(L, PFX + name)(env, None, 0, 0, C.addressof(b))
+        cls, msg = _exception(L)
+        assert cls == AAC_EXC and N.strerror(N.ERR_INVALID_ARG) in msg
 
 
 def test_create_without_gpu_throws_no_device():
@@ -114,7 +127,7 @@ def test_decode_through_direct_buffers_and_capacity_checks():
         keep = []
         args = [_buf(x, keep) for x in (b.stream_slot, b.frame_begin, b.q, b.sf, b.cb, b.ics, b.ms_used, b.tns, None,
                                          out)]
-        decode(env, None, h, b.n_frames, len(b.stream_slot), 2, *args, N.PCM_BIG_ENDIAN)
+        decode(env, None, h, b.n_frames, len(b.stream_slot), 2, *args, N.PCM_BIG_ENDIAN, None)
         assert _exception(L) is None
         assert (out == want).all()
         # the same buffers page-locked once (nativeRegister): DMA without staging, same PCM
@@ -125,14 +138,14 @@ def test_decode_through_direct_buffers_and_capacity_checks():
         out[:] = 0
         for slot in range(3):  # from fresh stream states again
             getattr(L, PFX + "nativeReset")(env, None, h, slot)
-        decode(env, None, h, b.n_frames, len(b.stream_slot), 2, *args, N.PCM_BIG_ENDIAN)
+        decode(env, None, h, b.n_frames, len(b.stream_slot), 2, *args, N.PCM_BIG_ENDIAN, None)
         assert _exception(L) is None
         assert (out == want).all()
         for r in reg:
             getattr(L, PFX + "nativeUnregister")(env, None, h, r)
             assert _exception(L) is None
         # nch must be the context's channels per record
-        decode(env, None, h, b.n_frames, len(b.stream_slot), 1, *args, N.PCM_BIG_ENDIAN)
+        decode(env, None, h, b.n_frames, len(b.stream_slot), 1, *args, N.PCM_BIG_ENDIAN, None)
         cls, msg = _exception(L)
         assert cls == AAC_EXC and N.strerror(N.ERR_INVALID_ARG) in msg
         # a q buffer one ch-frame short is refused before any copy
@@ -140,14 +153,14 @@ def test_decode_through_direct_buffers_and_capacity_checks():
         qshort = Buf(b.q.ctypes.data, b.q.nbytes - 2048)
         keep.append(qshort)
         short[2] = C.addressof(qshort)
-        decode(env, None, h, b.n_frames, len(b.stream_slot), 2, *short, N.PCM_BIG_ENDIAN)
+        decode(env, None, h, b.n_frames, len(b.stream_slot), 2, *short, N.PCM_BIG_ENDIAN, None)
         cls, msg = _exception(L)
         assert cls == AAC_EXC and N.strerror(N.ERR_INVALID_ARG) in msg
         # a PCM buffer too small for the batch
         small = np.zeros(want.nbytes - 1, np.uint8)
         args2 = list(args)
         args2[9] = _buf(small, keep)
-        decode(env, None, h, b.n_frames, len(b.stream_slot), 2, *args2, N.PCM_BIG_ENDIAN)
+        decode(env, None, h, b.n_frames, len(b.stream_slot), 2, *args2, N.PCM_BIG_ENDIAN, None)
         cls, msg = _exception(L)
         assert cls == AAC_EXC and N.strerror(N.ERR_INVALID_ARG) in msg
         # a bitstream error (max_sfb beyond the swb count) maps to AACException too
@@ -155,7 +168,7 @@ def test_decode_through_direct_buffers_and_capacity_checks():
         bad["max_sfb"][0] = 60
         args3 = list(args)
         args3[5] = _buf(bad, keep)
-        decode(env, None, h, b.n_frames, len(b.stream_slot), 2, *args3, N.PCM_BIG_ENDIAN)
+        decode(env, None, h, b.n_frames, len(b.stream_slot), 2, *args3, N.PCM_BIG_ENDIAN, None)
         cls, msg = _exception(L)
         assert cls == AAC_EXC and N.strerror(N.ERR_BITSTREAM) in msg
         getattr(L, PFX + "nativeReset")(env, None, h, 1)
@@ -169,7 +182,7 @@ def test_decode_through_direct_buffers_and_capacity_checks():
         args4[9] = db
         for slot in range(3):
             getattr(L, PFX + "nativeReset")(env, None, h, slot)
-        decode(env, None, h, b.n_frames, len(b.stream_slot), 2, *args4, N.PCM_BIG_ENDIAN)
+        decode(env, None, h, b.n_frames, len(b.stream_slot), 2, *args4, N.PCM_BIG_ENDIAN, None)
         assert _exception(L) is None
         got = np.ctypeslib.as_array((C.c_uint8 * want.nbytes).from_address(mb.address)).reshape(want.shape)
         assert (got == want).all()
@@ -199,7 +212,7 @@ def test_coupled_decode_through_direct_buffers():
         a = [_buf(x, keep) for x in (b.stream_slot, b.frame_begin, b.q, b.sf, b.cb, b.ics, b.ms_used, None, out)]
         c = [_buf(x, keep) for x in (b.cce_q, b.cce_sf, b.cce_cb, b.cce_ics, b.cce_terms)]
         getattr(L, PFX + "nativeDecodeCoupled")(env, None, h, b.n_frames, len(b.stream_slot), 2, *a, N.PCM_BIG_ENDIAN,
-                                               b.n_cce, len(b.cce_terms), *c)
+                                               b.n_cce, len(b.cce_terms), *c, None)
         assert _exception(L) is None
         assert (out == want).all()
         # a term buffer one term short is refused
@@ -207,7 +220,7 @@ def test_coupled_decode_through_direct_buffers():
         keep.append(short)
         c[4] = C.addressof(short)
         getattr(L, PFX + "nativeDecodeCoupled")(env, None, h, b.n_frames, len(b.stream_slot), 2, *a, N.PCM_BIG_ENDIAN,
-                                               b.n_cce, len(b.cce_terms), *c)
+                                               b.n_cce, len(b.cce_terms), *c, None)
         cls, msg = _exception(L)
         assert cls == AAC_EXC and N.strerror(N.ERR_INVALID_ARG) in msg
     finally:
