@@ -103,7 +103,8 @@ typedef struct jaad_frame_out {
     jaad_ics_info* ics;    /* [nch]       */
     uint64_t* ms_used;     /* [2], CPE only */
     jaad_tns* tns;         /* [nch] or NULL */
-    jaad_sbr_frame* sbr;   /* [1] when cfg.sbr */
+    jaad_sbr_frame* sbr;   /* when cfg.sbr: [1], or one per channel element (in bitstream order,
+                              LFE included: always JAAD_SBR_UPSAMPLE) for configurations 3..7 */
     /* coupling channel elements (CCE.decode, A/syntax/CCE.java:112-175): NULL cce_q makes a frame
        with a CCE JAAD_ERR_UNSUPPORTED.  Records go to cce_q/sf/cb/ics (up to cce_cap), the terms
        the frame's CCEs apply (jaad_gpu.h jaad_cce_term; frame 0, cce relative to this frame's

@@ -167,6 +167,8 @@ int mc_elements(int channel_config, uint8_t* nch)
     for (int i = 0; i < kCount[k]; i++) nch[i] = kLayouts[k][i];
     return kCount[k];
 }
+// the LFE position of a multichannel layout: configurations 6 and 7 end with the LFE
+bool mc_is_lfe(int channel_config, int k, int n) { return (channel_config == 6 || channel_config == 7) && k == n - 1; }
 constexpr uint32_t kMinPieceFrames = JAAD_MIN_PIECE_FRAMES;
 
 // One call's SBR/PS parameter records: built on the host straight into page-locked staging,
@@ -257,6 +259,12 @@ struct jaad_ctx {
     };
     std::vector<PinRange> pinned;  // jaad_host_register / jaad_host_alloc ranges
     uint32_t plan_L = 0;                           // chunk length of the cached plan
+    // ---- multichannel HE-AAC (configurations 3..7 with cfg.sbr): every channel element runs as its
+    // own mono (SCE, LFE) or stereo (CPE) SBR context on the element's records, gathered from the
+    // batch; the elements' PCM is then interleaved (launch_mc_sbr) ----
+    std::vector<jaad_ctx*> children;
+    DevBuf d_mc;                                   // gathered element records + element PCM
+    std::vector<jaad_sbr_frame> h_mc_sbr;          // one element's SBR records of the call
 };
 
 namespace jaad {
@@ -353,8 +361,8 @@ int validate_cfg(const jaad_stream_cfg* cfg)
     if (cfg->profile != 2) return JAAD_ERR_UNSUPPORTED;  // Profile.AAC_LC (A/Profile.java)
     if (cfg->sf_index > 11) return JAAD_ERR_UNSUPPORTED;
     if (cfg->channel_config < 1 || cfg->channel_config > 7) return JAAD_ERR_UNSUPPORTED;
-    // multichannel: AAC-LC elements only (SBR/PS of multichannel streams are not decoded here)
-    if (cfg->channel_config > 2 && (cfg->sbr || cfg->ps)) return JAAD_ERR_UNSUPPORTED;
+    // multichannel: AAC-LC elements, or SBR per element (HE-AAC v1); PS only in a mono stream
+    if (cfg->channel_config > 2 && cfg->ps) return JAAD_ERR_UNSUPPORTED;
     if (cfg->tns_mode > JAAD_TNS_SPEC) return JAAD_ERR_INVALID_ARG;
     if (cfg->sbr > 1 || cfg->ps > 1) return JAAD_ERR_UNSUPPORTED;
     if (cfg->ps && (!cfg->sbr || cfg->channel_config != 1)) return JAAD_ERR_UNSUPPORTED;
@@ -919,8 +927,11 @@ int setup_coupling(jaad_ctx* ctx, const jaad_batch* db, KernelArgs& a, hipStream
     return JAAD_OK;
 }
 
+int launch_mc_sbr(jaad_ctx* ctx, const jaad_batch* db, void* pcm, uint32_t flags, hipStream_t stream);
+
 int launch_work(jaad_ctx* ctx, const jaad_batch* db, void* pcm, uint32_t flags, hipStream_t stream)
 {
+    if (!ctx->children.empty()) return launch_mc_sbr(ctx, db, pcm, flags, stream);
     int rc = plan(ctx, db, stream);
     if (rc) return rc;
     KernelArgs a{};
@@ -991,6 +1002,91 @@ int launch_work(jaad_ctx* ctx, const jaad_batch* db, void* pcm, uint32_t flags, 
     return JAAD_OK;
 }
 
+int launch(jaad_ctx* ctx, const jaad_batch* db, void* pcm, uint32_t flags, hipStream_t stream);
+
+// Multichannel HE-AAC.  Element k's records (its channel columns of q/sf/cb/ics/tns, its ms_used pair,
+// its SBR record of each frame) are gathered into contiguous arrays by strided device copies and
+// decoded by the element's own SBR context into [frame][sample][2] PCM (an SCE's SBR1 output is
+// dataL and its copy dataR, A/sbr/SBR1.java:75-81; a CPE's SBR2 gives L and R; the LFE's records are
+// all JAAD_SBR_UPSAMPLE, A/sbr/SBR.java:302-309).  One pass then interleaves the elements' channels
+// in element order, as SyntacticElements.process collects them (A/syntax/SyntacticElements.java:
+// 235-248): SCE 2, CPE 2, LFE 1 (its left).  Byte order / float32 are already the children's.
+int launch_mc_sbr(jaad_ctx* ctx, const jaad_batch* db, void* pcm, uint32_t flags, hipStream_t stream)
+{
+    const size_t nf = db->n_frames;
+    const int ne = ctx->n_elem, nch = ctx->nch;
+    if (!db->sbr) return JAAD_ERR_INVALID_ARG;
+    // element kinds of the layout: an SCE must carry SBR data in every frame (without it the
+    // reference's channel list shrinks, A/syntax/SCE.java:122-132), an LFE never does
+    for (size_t f = 0; f < nf; f++)
+        for (int k = 0; k < ne; k++) {
+            const jaad_sbr_frame& r = db->sbr[f * ne + k];
+            const bool lfe = mc_is_lfe(ctx->cfg.channel_config, k, ne);
+            if (lfe ? r.status != JAAD_SBR_UPSAMPLE : (ctx->elem_nch[k] == 1 && r.status == JAAD_SBR_UPSAMPLE))
+                return JAAD_ERR_UNSUPPORTED;
+        }
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const size_t S = (size_t)jaad_cfg_sample_length(&ctx->cfg), bps = (flags & JAAD_PCM_FLOAT32) ? 4 : 2;
+    const size_t pcm_k = al(nf * S * 2 * bps);  // one element's PCM
+    // per element: q | sf | cb | ics | ms | tns | pcm, each 256-B aligned (sized for a CPE)
+    const size_t o_sf = al(nf * 2 * 2048), o_cb = o_sf + al(nf * 2 * 128), o_ics = o_cb + al(nf * 2 * 128);
+    const size_t o_ms = o_ics + al(nf * 2 * sizeof(jaad_ics_info)), o_tns = o_ms + al(nf * 16);
+    const size_t o_pcm = o_tns + (db->tns ? al(nf * 2 * sizeof(jaad_tns)) : 0), per_el = o_pcm + pcm_k;
+    HIPCHK(ctx->d_mc.ensure(per_el * ne + 256));
+    char* base = static_cast<char*>(ctx->d_mc.p);
+    int ch0 = 0, cpe = 0;
+    for (int k = 0; k < ne; k++) {
+        const int n = ctx->elem_nch[k];
+        char* e = base + per_el * k;
+        if (nf) {
+            auto gather = [&](size_t off, const void* src, size_t per_ch) {
+                return hipMemcpy2DAsync(e + off, n * per_ch, static_cast<const char*>(src) + ch0 * per_ch, nch * per_ch,
+                                        n * per_ch, nf, hipMemcpyDeviceToDevice, stream);
+            };
+            HIPCHK(gather(0, db->q, 2048));
+            HIPCHK(gather(o_sf, db->sf, 128));
+            HIPCHK(gather(o_cb, db->cb, 128));
+            HIPCHK(gather(o_ics, db->ics, sizeof(jaad_ics_info)));
+            if (db->tns) HIPCHK(gather(o_tns, db->tns, sizeof(jaad_tns)));
+            if (n == 2)
+                HIPCHK(hipMemcpy2DAsync(e + o_ms, 16, db->ms_used + 2 * cpe, 16 * (size_t)ctx->n_cpe, 16, nf,
+                                        hipMemcpyDeviceToDevice, stream));
+        }
+        ctx->h_mc_sbr.resize(nf);
+        for (size_t f = 0; f < nf; f++) ctx->h_mc_sbr[f] = db->sbr[f * ne + k];
+        jaad_batch c{};
+        c.n_frames = db->n_frames;
+        c.n_runs = db->n_runs;
+        c.stream_slot = db->stream_slot;
+        c.frame_begin = db->frame_begin;
+        c.q = reinterpret_cast<const int16_t*>(e);
+        c.sf = reinterpret_cast<const uint8_t*>(e + o_sf);
+        c.cb = reinterpret_cast<const uint8_t*>(e + o_cb);
+        c.ics = reinterpret_cast<const jaad_ics_info*>(e + o_ics);
+        c.ms_used = n == 2 ? reinterpret_cast<const uint64_t*>(e + o_ms) : nullptr;
+        c.tns = db->tns ? reinterpret_cast<const jaad_tns*>(e + o_tns) : nullptr;
+        c.sbr = ctx->h_mc_sbr.data();
+        // the child's SBR records are built on the host during this call (launch_sbr_stage), so
+        // h_mc_sbr is free again when it returns
+        const int rc = launch(ctx->children[k], &c, e + o_pcm, flags, stream);
+        if (rc) return rc;
+        ch0 += n;
+        cpe += n == 2;
+    }
+    McInterleave m{};
+    m.n_out = 0;
+    for (int k = 0; k < ne; k++) {
+        const int outs = mc_is_lfe(ctx->cfg.channel_config, k, ne) ? 1 : 2;
+        for (int j = 0; j < outs; j++) {
+            m.src[m.n_out] = base + per_el * k + o_pcm;
+            m.chan[m.n_out] = j;
+            m.n_out++;
+        }
+    }
+    HIPCHK(launch_mc_interleave(m, pcm, (uint32_t)nf, (uint32_t)S, (int)bps, stream));
+    return JAAD_OK;
+}
+
 int launch(jaad_ctx* ctx, const jaad_batch* db, void* pcm, uint32_t flags, hipStream_t stream)
 {
     // a call on the stream of the previous call is ordered after it by the stream itself; only a
@@ -1018,7 +1114,17 @@ int jaad_cfg_channel_count(const jaad_stream_cfg* cfg)
 {
     // mono is duplicated while sbrEnabled (A/DecoderConfig.java:108-115); configurations 3..7 carry
     // 3, 4, 5, 6 (5.1) and 8 (7.1) channels (ChannelConfiguration, A/ChannelConfiguration.java)
-    if (cfg && cfg->channel_config >= 3 && cfg->channel_config <= 7) return cfg->channel_config == 7 ? 8 : cfg->channel_config;
+    if (cfg && cfg->channel_config >= 3 && cfg->channel_config <= 7) {
+        if (!cfg->sbr) return cfg->channel_config == 7 ? 8 : cfg->channel_config;
+        // multichannel HE-AAC: SyntacticElements.process collects dataL and dataR of every SCE with
+        // SBR (A/syntax/SCE.java:115-132) and of every CPE, one channel of the LFE (no SBR data,
+        // upsampled): configuration 3 -> 4, 4 -> 6, 5 -> 6, 6 -> 7, 7 -> 9
+        uint8_t nch[kMaxElements];
+        const int n = mc_elements(cfg->channel_config, nch);
+        int out = 0;
+        for (int k = 0; k < n; k++) out += mc_is_lfe(cfg->channel_config, k, n) ? 1 : 2;
+        return out;
+    }
     return 2;
 }
 
@@ -1127,7 +1233,22 @@ int jaad_ctx_create(const jaad_stream_cfg* cfg, uint32_t n_slots, int device, ja
     if ((e = hipMalloc(&ctx->d_iq, sizeof(JAAD_IQ_TABLE))) != hipSuccess) return bail(e, "hipMalloc iq");
     if ((e = hipMemcpy(ctx->d_iq, JAAD_IQ_TABLE, sizeof(JAAD_IQ_TABLE), hipMemcpyHostToDevice)) != hipSuccess)
         return bail(e, "hipMemcpy iq");
-    if (cfg->sbr) {
+    if (cfg->sbr && ctx->n_elem > 1) {
+        // multichannel HE-AAC: one SBR context per channel element (ChannelElement owns its SBR,
+        // A/syntax/ChannelElement.java:39-74); the LFE too (it is upsampled as SBR.upsample does)
+        for (int k = 0; k < ctx->n_elem; k++) {
+            jaad_stream_cfg c = *cfg;
+            c.channel_config = ctx->elem_nch[k] == 2 ? 2 : 1;
+            c.ps = 0;
+            jaad_ctx* child = nullptr;
+            const int crc = jaad_ctx_create(&c, n_slots, device, &child);
+            if (crc) {
+                jaad_ctx_destroy(ctx);
+                return crc;
+            }
+            ctx->children.push_back(child);
+        }
+    } else if (cfg->sbr) {
         ctx->sbr_host.reset(new (std::nothrow) SbrHost(cfg->ext_sf_index));
         if (!ctx->sbr_host) {
             jaad_ctx_destroy(ctx);
@@ -1185,6 +1306,9 @@ void jaad_ctx_destroy(jaad_ctx* ctx)
     (void)hipSetDevice(ctx->device);
     if (ctx->done_live) (void)hipEventSynchronize(ctx->done);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    for (jaad_ctx* c : ctx->children) jaad_ctx_destroy(c);
+    ctx->children.clear();
+    ctx->d_mc.release();
     for (int i = 0; i < 2; i++)
         if (ctx->d_state[i]) (void)hipFree(ctx->d_state[i]);
     if (ctx->d_tables) (void)hipFree(ctx->d_tables);
@@ -1821,6 +1945,11 @@ int jaad_ctx_core_channels(const jaad_ctx* ctx) { return ctx ? ctx->nch : JAAD_E
 size_t jaad_state_bytes(const jaad_ctx* ctx)
 {
     if (!ctx) return 0;
+    if (!ctx->children.empty()) {  // multichannel HE-AAC: the elements' blobs back to back
+        size_t n = 0;
+        for (const jaad_ctx* c : ctx->children) n += jaad_state_bytes(c);
+        return n;
+    }
     return (size_t)ctx->n_elem * 2048 * sizeof(float) + (ctx->cfg.sbr ? 2 * sizeof(SbrChState) + sizeof(SbrHostSlot) : 0) +
            (ctx->cfg.ps ? sizeof(PsState) : 0);
 }
@@ -1831,6 +1960,14 @@ int jaad_state_export(jaad_ctx* ctx, uint32_t slot, void* buf, size_t bytes)
     int rc = sync_ctx(ctx);
     if (rc) return rc;
     char* o = static_cast<char*>(buf);
+    if (!ctx->children.empty()) {
+        for (jaad_ctx* c : ctx->children) {
+            const size_t n = jaad_state_bytes(c);
+            if ((rc = jaad_state_export(c, slot, o, n))) return rc;
+            o += n;
+        }
+        return JAAD_OK;
+    }
     for (int k = 0; k < ctx->n_elem; k++)  // one overlap record per channel element
         HIPCHK(hipMemcpy(o + (size_t)k * 2048 * sizeof(float), ctx->d_state[ctx->parity] + ((size_t)k * ctx->n_slots + slot) * 2048,
                          2048 * sizeof(float), hipMemcpyDeviceToHost));
@@ -1851,6 +1988,14 @@ int jaad_state_import(jaad_ctx* ctx, uint32_t slot, const void* buf, size_t byte
     int rc = sync_ctx(ctx);
     if (rc) return rc;
     const char* in = static_cast<const char*>(buf);
+    if (!ctx->children.empty()) {
+        for (jaad_ctx* c : ctx->children) {
+            const size_t n = jaad_state_bytes(c);
+            if ((rc = jaad_state_import(c, slot, in, n))) return rc;
+            in += n;
+        }
+        return JAAD_OK;
+    }
     for (int k = 0; k < ctx->n_elem; k++) {  // the overlap must be finite (the LC kernel's PCM rounding relies on it, jaad_lc.hip round_pk16)
         float ov[2048];
         std::memcpy(ov, in + (size_t)k * sizeof ov, sizeof ov);
@@ -1882,6 +2027,11 @@ int jaad_state_reset(jaad_ctx* ctx, uint32_t slot)
     if (!ctx || slot >= ctx->n_slots) return JAAD_ERR_INVALID_ARG;
     int rc = sync_ctx(ctx);
     if (rc) return rc;
+    if (!ctx->children.empty()) {
+        for (jaad_ctx* c : ctx->children)
+            if ((rc = jaad_state_reset(c, slot))) return rc;
+        return JAAD_OK;
+    }
     for (int k = 0; k < ctx->n_elem; k++)
         HIPCHK(hipMemset(ctx->d_state[ctx->parity] + ((size_t)k * ctx->n_slots + slot) * 2048, 0, 2048 * sizeof(float)));
     if (ctx->cfg.sbr) {

@@ -131,6 +131,15 @@ hipError_t launch_cce_terms(const CceArgs& a, hipStream_t stream);
 hipError_t launch_check_q(const int16_t* q, size_t n, int* flag, hipStream_t stream);
 // SampleBuffer.accept for a multichannel frame: planar f32 [frame][n_ch][1024] -> n_ch
 // interleaved samples per instant (int16 BE/LE after Math.round + clamp, or f32; JAAD_PCM_*)
+// multichannel HE-AAC output: output channel c of every (frame, sample) comes from channel chan[c] of
+// the [frame][sample][2] PCM at src[c] (bps-byte samples, already in the output byte order)
+struct McInterleave {
+    const void* src[16];
+    int chan[16];
+    int n_out;
+};
+hipError_t launch_mc_interleave(const McInterleave& m, void* pcm, uint32_t n_frames, uint32_t samples, int bps,
+                                hipStream_t stream);
 hipError_t launch_pack(const float* planar, void* pcm, uint32_t n_frames, int n_ch, uint32_t flags,
                        hipStream_t stream);
 // LC kernel waves that can be resident on one CU (occupancy query; 0 on failure)

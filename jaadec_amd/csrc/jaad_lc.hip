@@ -1524,6 +1524,30 @@ hipError_t launch_check_q(const int16_t* q, size_t n, int* flag, hipStream_t str
     return hipGetLastError();
 }
 
+namespace {
+// one thread per (frame, sample instant): the output channels' words from the elements' PCM
+template <typename W>
+__global__ __launch_bounds__(256) void mc_interleave_kernel(McInterleave m, W* __restrict__ out, size_t n)
+{
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;  // frame * samples + sample
+    if (i >= n) return;
+    W* o = out + i * m.n_out;
+    for (int c = 0; c < m.n_out; c++) o[c] = static_cast<const W*>(m.src[c])[2 * i + m.chan[c]];
+}
+}  // namespace
+
+hipError_t launch_mc_interleave(const McInterleave& m, void* pcm, uint32_t n_frames, uint32_t samples, int bps,
+                                hipStream_t stream)
+{
+    const size_t n = (size_t)n_frames * samples;
+    if (!n) return hipSuccess;
+    if (m.n_out < 1 || m.n_out > 16) return hipErrorInvalidValue;
+    const dim3 grid((unsigned)((n + 255) / 256));
+    if (bps == 4) hipLaunchKernelGGL(mc_interleave_kernel<uint32_t>, grid, dim3(256), 0, stream, m, static_cast<uint32_t*>(pcm), n);
+    else hipLaunchKernelGGL(mc_interleave_kernel<uint16_t>, grid, dim3(256), 0, stream, m, static_cast<uint16_t*>(pcm), n);
+    return hipGetLastError();
+}
+
 hipError_t launch_pack(const float* planar, void* pcm, uint32_t n_frames, int n_ch, uint32_t flags, hipStream_t stream)
 {
     const size_t n = (size_t)n_frames * 1024;

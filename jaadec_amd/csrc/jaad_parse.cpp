@@ -380,7 +380,10 @@ using namespace jaad::parse;
 
 struct jaad_parser {
     Cfg C;
-    ParseState st;
+    ParseState st;  // st.sbr: the SBR state of channel element 0
+    // multichannel HE-AAC: the SBR state of channel elements 1.. (each ChannelElement owns its SBR,
+    // A/syntax/ChannelElement.java:39-74); empty otherwise
+    std::vector<SbrParseState> sbr_el;
 };
 
 namespace {
@@ -558,7 +561,7 @@ int jaad_asc_parse(const uint8_t* asc, size_t bytes, jaad_stream_cfg* cfg)
     if (aot != 2) return JAAD_ERR_UNSUPPORTED;
     if (sfi > 11 || (cfg->sbr && cfg->ext_sf_index > 11)) return JAAD_ERR_UNSUPPORTED;
     if (chc < 1 || chc > 7) return JAAD_ERR_UNSUPPORTED;
-    if (chc > 2 && cfg->sbr) return JAAD_ERR_UNSUPPORTED;  // multichannel HE-AAC: not decoded here
+    if (chc > 2 && cfg->ps) cfg->ps = 0;  // PS only in a mono (SCE) stream
     cfg->profile = 2;
     cfg->sf_index = (uint8_t)sfi;
     cfg->channel_config = (uint8_t)chc;
@@ -629,7 +632,6 @@ int jaad_parser_create(const jaad_stream_cfg* cfg, jaad_parser** out)
     if (cfg->abi_version != JAAD_ABI_VERSION) return JAAD_ERR_ABI;
     if (cfg->profile != 2 || cfg->channel_config < 1 || cfg->channel_config > 7) return JAAD_ERR_UNSUPPORTED;
     if (cfg->ps && (!cfg->sbr || cfg->channel_config != 1)) return JAAD_ERR_UNSUPPORTED;
-    if (cfg->channel_config > 2 && cfg->sbr) return JAAD_ERR_UNSUPPORTED;  // multichannel: AAC-LC elements only
     jaad_parser* p = new (std::nothrow) jaad_parser;
     if (!p) return JAAD_ERR_NOMEM;
     p->C.cfg = *cfg;
@@ -653,6 +655,7 @@ int jaad_parser_create(const jaad_stream_cfg* cfg, jaad_parser** out)
         delete p;
         return st;
     }
+    if (cfg->sbr && p->C.n_elem > 1) p->sbr_el.resize((size_t)p->C.n_elem - 1);
     books();
     *out = p;
     return JAAD_OK;
@@ -820,6 +823,10 @@ int cce_terms(const CceElem* cces, int n_cce, const ChElem* els, int n_el, jaad_
     return JAAD_OK;
 }
 
+// the LFE position of a multichannel layout (configurations 6 and 7 end with the LFE, ISO/IEC
+// 14496-3 Table 1.19; configuration 4 ends with a back SCE)
+bool mc_lfe(const Cfg& C, int e) { return (C.cfg.channel_config == 6 || C.cfg.channel_config == 7) && e == C.n_elem - 1; }
+
 // probe != nullptr: stop at the first SBR extension payload after the channel element
 // (bit 0 of *probe) and commit nothing
 int parse_frame(jaad_parser* p, const uint8_t* data, size_t bytes, jaad_frame_out* out, uint32_t* probe)
@@ -832,10 +839,13 @@ int parse_frame(jaad_parser* p, const uint8_t* data, size_t bytes, jaad_frame_ou
     if (C.cfg.sbr && !out->sbr) return JAAD_ERR_INVALID_ARG;
     BitReader br(data, bytes);
     ParseState ns = p->st;  // committed only when the whole frame parsed
+    std::vector<SbrParseState> nsel;  // multichannel HE-AAC: elements 1.. (committed with ns)
+    if (!p->sbr_el.empty()) nsel = p->sbr_el;
     bool have_channels = false;
     int elem = 0, ch0 = 0, cpe = 0;  // channel elements parsed so far, their channels, CPEs
-    int sbr_seen = 0;
-    if (C.cfg.sbr) std::memset(out->sbr, 0, sizeof *out->sbr);
+    // SBR records: one per channel element (multichannel: out->sbr[0 .. n_elem), element order)
+    uint32_t sbr_seen = 0;           // bit k: element k carried an SBR payload this frame
+    if (C.cfg.sbr) std::memset(out->sbr, 0, sizeof *out->sbr * (size_t)C.n_elem);
     ChElem els[8];
     int n_els = 0;
     std::vector<CceElem> cces;  // 7.7 KB each: only when the frame has CCEs
@@ -866,9 +876,15 @@ int parse_frame(jaad_parser* p, const uint8_t* data, size_t bytes, jaad_frame_ou
                     return JAAD_OK;
                 }
                 if (!C.cfg.sbr) return JAAD_ERR_UNSUPPORTED;
-                const int st = parse_sbr(sub, C, type == 14, ns, *out->sbr);
+                // SyntacticElements.decodeSBR: the payload belongs to the last audio element
+                // (A/syntax/SyntacticElements.java:207-211).  SBR on the LFE of a multichannel
+                // stream would add a channel to the reference's output (LFE extends SCE): refused.
+                const int e = elem - 1;
+                if (C.n_elem > 1 && mc_lfe(C, e)) return JAAD_ERR_UNSUPPORTED;
+                SbrParseState& S = e == 0 ? ns.sbr : nsel[(size_t)e - 1];
+                const int st = parse_sbr(sub, C, C.elem_nch[e], type == 14, S, out->sbr[e]);
                 if (st) return st;
-                sbr_seen = 1;
+                sbr_seen |= 1u << e;
             }
             continue;
         }
@@ -956,16 +972,25 @@ int parse_frame(jaad_parser* p, const uint8_t* data, size_t bytes, jaad_frame_ou
     }
     if (!have_channels) return JAAD_ERR_BITSTREAM;  // a frame without audio: nothing to decode
     if (elem != C.n_elem) return JAAD_ERR_UNSUPPORTED;  // a frame without all the configuration's elements
-    if (C.cfg.sbr && !sbr_seen) {
-        const int st = sbr_missing(C, ns, *out->sbr);
-        if (st) return st;
-    }
+    if (C.cfg.sbr)
+        for (int e = 0; e < C.n_elem; e++) {
+            if (sbr_seen & (1u << e)) continue;
+            // an SCE of a multichannel stream without SBR data would drop to one output channel in
+            // the reference (SCE.process accepts dataR only with SBR, A/syntax/SCE.java:122-132),
+            // changing the frame's channel count: refused.  CPEs and LFEs are upsampled.
+            if (C.n_elem > 1 && C.elem_nch[e] == 1 && !mc_lfe(C, e)) return JAAD_ERR_UNSUPPORTED;
+            const int st = sbr_missing(C, ns, out->sbr[e]);
+            if (st) return st;
+        }
     if (n_cce) {
         const int st = cce_terms(cces.data(), n_cce, els, n_els, out);
         if (st) return st;
         out->n_cce = (uint32_t)n_cce;
     }
-    if (!probe) p->st = ns;
+    if (!probe) {
+        p->st = ns;
+        if (!nsel.empty()) p->sbr_el.swap(nsel);
+    }
     return JAAD_OK;
 }
 }  // namespace

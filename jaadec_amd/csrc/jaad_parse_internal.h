@@ -113,8 +113,9 @@ struct ChOut {
     jaad_tns* tns;
 };
 
-// one sbr_extension_data payload (after the 4-bit extension type) into rec
-int parse_sbr(BitReader& br, const Cfg& C, bool crc, ParseState& st, jaad_sbr_frame& rec);
+// one sbr_extension_data payload (after the 4-bit extension type) of a channel element with nch
+// channels (1 SCE/LFE: SBR1, 2 CPE: SBR2) into rec, with that element's SBR state S
+int parse_sbr(BitReader& br, const Cfg& C, int nch, bool crc, SbrParseState& S, jaad_sbr_frame& rec);
 // a frame of an SBR configuration that carried no SBR payload
 int sbr_missing(const Cfg& C, ParseState& st, jaad_sbr_frame& rec);
 

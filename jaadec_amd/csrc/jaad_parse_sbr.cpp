@@ -659,9 +659,8 @@ void couple(ChWork& w, const ChWork& o, int N_Q)
 
 }  // namespace
 
-int parse_sbr(BitReader& br, const Cfg& C, bool crc, ParseState& st, jaad_sbr_frame& rec)
+int parse_sbr(BitReader& br, const Cfg& C, int nch, bool crc, SbrParseState& S, jaad_sbr_frame& rec)
 {
-    SbrParseState& S = st.sbr;
     std::memset(&rec, 0, sizeof rec);
     if (crc) {
         if (br.left() < 10) return JAAD_ERR_EOS;
@@ -722,7 +721,7 @@ int parse_sbr(BitReader& br, const Cfg& C, bool crc, ParseState& st, jaad_sbr_fr
         rec.status = JAAD_SBR_UPSAMPLE;
         return JAAD_OK;
     };
-    if (C.nch == 1) {  // SBR1.sbr_data (A/sbr/SBR1.java:34-60)
+    if (nch == 1) {  // SBR1.sbr_data (A/sbr/SBR1.java:34-60)
         if (br.left() < 1) return JAAD_ERR_EOS;
         if (br.read(1)) br.skip(4);
         if ((rc = grid(w[0])) == kGridInvalid) return invalid();
@@ -768,7 +767,7 @@ int parse_sbr(BitReader& br, const Cfg& C, bool crc, ParseState& st, jaad_sbr_fr
         br.skip(8 * cnt);
         while (sub.left() > 7) {
             const int id = (int)sub.read(2);
-            if (id != 2 || C.nch != 1) continue;  // EXTENSION_ID_PS, SCE only
+            if (id != 2 || nch != 1) continue;  // EXTENSION_ID_PS, SCE only
             // psEnabled is on by default (A/DecoderConfig.java:36): PS data in a stream whose
             // configuration has no PS would be applied by the reference; not representable here
             if (!C.cfg.ps) return JAAD_ERR_UNSUPPORTED;
@@ -777,7 +776,7 @@ int parse_sbr(BitReader& br, const Cfg& C, bool crc, ParseState& st, jaad_sbr_fr
             rec.ps_present = 1;
         }
     }
-    for (int c = 0; c < C.nch; c++) {
+    for (int c = 0; c < nch; c++) {
         to_record(w[c], S, rec.ch[c]);
         save_prev(w[c]);
     }

@@ -276,7 +276,7 @@ class Decoder:
                 LOGGER.warning("unexpected end of frame: frame %d dropped", self.frames + i)
                 continue  # the reference swallows the EOSException: this buffer keeps what it had
             want = buf.big_endian
-            buf._set(pcm[i].tobytes(), rate, self.config.getSampleLength(), self.config.getChannelCount())
+            buf._set(pcm[i].tobytes(), rate, self.config.getSampleLength(), N.out_channels(self.config.cfg()))
             buf.big_endian = flags == N.PCM_BIG_ENDIAN
             buf.setBigEndian(want)  # no-op unless this buffer asked for the other byte order
         self.frames += batch.n_frames

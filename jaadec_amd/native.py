@@ -378,6 +378,24 @@ def n_cpe(cfg) -> int:
     return sum(e == 1 for e in MC_ELEMENTS[cc]) if cc in MC_ELEMENTS else int(cc == 2)
 
 
+def n_elements(cfg) -> int:
+    """Channel elements per frame (one jaad_sbr_frame each in a multichannel HE-AAC batch)."""
+    cc = cfg.channel_config
+    return len(MC_ELEMENTS[cc]) if cc in MC_ELEMENTS else 1
+
+
+def out_channels(cfg) -> int:
+    """PCM channels per sample instant (jaad_cfg_channel_count): 2 for mono/stereo (an SCE's output is
+    duplicated); multichannel AAC-LC: the core channels; multichannel HE-AAC: every SCE and CPE gives
+    two (SCE.process with SBR accepts dataL and dataR, A/syntax/SCE.java:122-129), an LFE one."""
+    cc = cfg.channel_config
+    if cc not in MC_ELEMENTS:
+        return 2
+    if not cfg.sbr:
+        return core_channels(cfg)
+    return sum(1 if e == 3 else 2 for e in MC_ELEMENTS[cc])
+
+
 def mc_batch(elements: list, ids) -> "Batch":
     """One multichannel batch (all channels' records per frame, element order) from per-element
     batches of the same runs (SCE/LFE: 1 channel, CPE: 2 with ms_used)."""
@@ -399,7 +417,17 @@ def mc_batch(elements: list, ids) -> "Batch":
                 tns[:, c:c + e.nch] = e.tns.reshape(nf, e.nch)
             c += e.nch
         tns = tns.reshape(nf * nch)
-    return Batch(q, sf, cb, ics, ms, tns, elements[0].stream_slot.copy(), elements[0].frame_begin.copy(), nch)
+    sbr = None
+    if any(e.sbr is not None for e in elements):
+        # multichannel HE-AAC: one record per element per frame; an element without records (the
+        # LFE) is upsampled (JAAD_SBR_UPSAMPLE)
+        sbr = np.zeros((nf, len(elements)), SBR_FRAME_DTYPE)
+        for k, e in enumerate(elements):
+            if e.sbr is not None:
+                sbr[:, k] = e.sbr
+            else:
+                sbr[:, k]["status"] = SBR_UPSAMPLE
+    return Batch(q, sf, cb, ics, ms, tns, elements[0].stream_slot.copy(), elements[0].frame_begin.copy(), nch, sbr)
 
 
 def pcm_frame_bytes(flags: int, sbr: bool = False, down: bool = False) -> int:
@@ -655,7 +683,8 @@ class Parser:
         ics = np.zeros(nf * nch, ICS_DTYPE)
         ms = np.zeros((nf, 2 * ncpe), np.uint64) if ncpe else None
         tns = np.zeros(nf * nch, TNS_DTYPE)
-        sbr = np.zeros(nf, SBR_FRAME_DTYPE) if self.cfg.sbr else None
+        ne = n_elements(self.cfg)
+        sbr = np.zeros((nf, ne) if ne > 1 else nf, SBR_FRAME_DTYPE) if self.cfg.sbr else None
         # coupling channel elements: up to 8 records and 64 terms per frame
         cq = np.zeros((8, 1024), np.int16)
         csf = np.zeros((8, 128), np.uint8)

@@ -317,6 +317,37 @@ long jaad_write_frame_mc(int sf_index, int n_elem, const int* ids, const int16_t
 }
 
 /*
+ * A raw_data_block of a multichannel HE-AAC frame: as jaad_write_frame_mc, with element k's SBR
+ * record sbr[k] written as a FIL (EXT_SBR_DATA) right after the element when its status is
+ * JAAD_SBR_OK and sbr_state[k] (that element's writer state) is set.
+ */
+long jaad_write_frame_mc_sbr(int sf_index, int n_elem, const int* ids, const int16_t* q, const uint8_t* sf,
+                             const uint8_t* cb, const jaad_ics_info* ics, const uint64_t* ms_used, const jaad_tns* tns,
+                             const jaad_sbr_frame* sbr, void* const* sbr_state, uint8_t* out, size_t cap)
+{
+    Bw w = {out, cap, 0, 0};
+    memset(out, 0, cap);
+    int ch = 0, cpe = 0, tags[8] = {0};
+    for (int k = 0; k < n_elem; k++) {
+        const int id = ids[k];
+        if (put_element(&w, sf_index, id, tags[id]++, q + (size_t)ch * 1024, sf + ch * 128, cb + ch * 128, ics + ch,
+                        id == 1 ? ms_used + 2 * cpe : NULL, tns ? tns + ch : NULL, 0))
+            return -1;
+        if (sbr && sbr_state && sbr_state[k] && sbr[k].status == JAAD_SBR_OK) {
+            uint8_t fil[512];
+            const long nbits = jaad_sbr_fil_bits(sbr_state[k], id == 1 ? 2 : 1, &sbr[k], fil, sizeof fil);
+            if (nbits < 0) return -1;
+            for (long i = 0; i < nbits; i++) put(&w, (fil[i >> 3] >> (7 - (i & 7))) & 1u, 1);
+        }
+        ch += id == 1 ? 2 : 1;
+        cpe += id == 1;
+    }
+    put(&w, 7, 3); /* END */
+    align(&w);
+    return w.overflow ? -1 : (long)(w.pos / 8);
+}
+
+/*
  * coupling_channel_element (the syntax CCE.decode reads, A/syntax/CCE.java:112-175) of a test
  * description: targets, coupling domain, gain sign/scale, the CCE's ICStream records and its gain
  * element codes.  gain list i (i >= 1): cge[i] = common_gain_element_present; with it, code[i][0]

@@ -62,6 +62,9 @@ def lib() -> C.CDLL:
         L.jaad_write_frame_cce.argtypes = ([C.c_int, C.c_int, C.c_void_p] + [C.c_void_p] * 5 + [C.c_int] +
                                            [C.c_void_p] * 5 + [C.c_void_p, C.c_size_t])
         L.jaad_write_frame_mc.restype = C.c_long
+        L.jaad_write_frame_mc_sbr.argtypes = ([C.c_int, C.c_int, C.c_void_p] + [C.c_void_p] * 6 + [C.c_void_p] * 2 +
+                                              [C.c_void_p, C.c_size_t])
+        L.jaad_write_frame_mc_sbr.restype = C.c_long
         _lib = L
     return _lib
 
@@ -206,13 +209,33 @@ def write_frames(batch, sf_index: int, frames=None, extras: int = 0, sbr_writer:
     return out
 
 
-def write_frames_mc(batch, sf_index: int, ids) -> list:
+def write_frames_mc(batch, sf_index: int, ids, sbr_writers=None) -> list:
     """TEST WRITER: raw_data_blocks of a multichannel batch (native.mc_batch layout): the elements
-    `ids` (0 SCE, 1 CPE, 3 LFE) in order, then END (jaad_write_frame_mc)."""
+    `ids` (0 SCE, 1 CPE, 3 LFE) in order, then END (jaad_write_frame_mc).  With sbr_writers (one
+    SbrWriter or None per element), element k's SBR record batch.sbr[f, k] follows it as a FIL
+    (jaad_write_frame_mc_sbr)."""
     nch = batch.nch
     ids_a = (C.c_int * len(ids))(*ids)
     buf = np.zeros(65536, np.uint8)
     out = []
+    if sbr_writers is not None:
+        states = (C.c_void_p * len(ids))(*[w.buf.ctypes.data if w is not None else None for w in sbr_writers])
+        for f in range(batch.n_frames):
+            cf = f * nch
+            q = np.ascontiguousarray(batch.q[cf:cf + nch])
+            sf = np.ascontiguousarray(batch.sf[cf:cf + nch])
+            cb = np.ascontiguousarray(batch.cb[cf:cf + nch])
+            ics = np.ascontiguousarray(batch.ics[cf:cf + nch])
+            ms = np.ascontiguousarray(batch.ms_used[f]) if batch.ms_used is not None else np.zeros(2, np.uint64)
+            tns = np.ascontiguousarray(batch.tns[cf:cf + nch]) if batch.tns is not None else None
+            rec = np.ascontiguousarray(batch.sbr[f])
+            n = lib().jaad_write_frame_mc_sbr(sf_index, len(ids), ids_a, q.ctypes.data, sf.ctypes.data, cb.ctypes.data,
+                                              ics.ctypes.data, ms.ctypes.data, tns.ctypes.data if tns is not None else None,
+                                              rec.ctypes.data, states, buf.ctypes.data, buf.nbytes)
+            if n < 0:
+                raise ValueError(f"frame {f} cannot be written")
+            out.append(buf[:n].tobytes())
+        return out
     for f in range(batch.n_frames):
         cf = f * nch
         q = np.ascontiguousarray(batch.q[cf:cf + nch])
@@ -270,17 +293,21 @@ def write_frames_cce(batch, sf_index: int, ids, cces) -> list:
     return out
 
 
-def decode_batch_mc(sf_index: int, batch, ids, flags: int = 0, threads: int = 1, tns_mode: int = 0) -> np.ndarray:
+def decode_batch_mc(sf_index: int, batch, ids, flags: int = 0, threads: int = 1, tns_mode: int = 0,
+                    sbr: bool = False, down: bool = False) -> np.ndarray:
     """TEST ORACLE for a multichannel batch, from fresh stream states: every element decoded on its
     own (SCE/LFE as a mono, CPE as a stereo stream: SyntacticElements.process runs them in turn)
-    and the channels interleaved in element order (SampleBuffer.accept); uint8 [n_frames, bytes]."""
+    and the channels interleaved in element order (SampleBuffer.accept); uint8 [n_frames, bytes].
+    With sbr (multichannel HE-AAC, batch.sbr [frame][element]): each element runs its own SBR
+    (SCE: SBR1, whose dataL and dataR are both output, A/syntax/SCE.java:115-132; CPE: SBR2,
+    A/syntax/CPE.java:195-204); the LFE has no SBR data and is upsampled (one channel)."""
     import jaadec_amd.native as N
 
     nf, nch = batch.n_frames, batch.nch
     fb = 4 if flags & 2 else 2
     planes = []
     c, cpe = 0, 0
-    for i in ids:
+    for e_idx, i in enumerate(ids):
         k = 2 if i == 1 else 1
         cfr = (np.arange(nf)[:, None] * nch + c + np.arange(k)[None, :]).reshape(-1)
         el = N.Batch(np.ascontiguousarray(batch.q[cfr]), np.ascontiguousarray(batch.sf[cfr]),
@@ -294,11 +321,14 @@ def decode_batch_mc(sf_index: int, batch, ids, flags: int = 0, threads: int = 1,
             t["channel"] -= c
             el.cce_q, el.cce_sf, el.cce_cb, el.cce_ics = batch.cce_q, batch.cce_sf, batch.cce_cb, batch.cce_ics
             el.cce_terms = np.ascontiguousarray(t)
-        cfg = N.make_cfg(sf_index, 2 if k == 2 else 1, tns_mode)
+        cfg = N.make_cfg(sf_index, 2 if k == 2 else 1, tns_mode, sbr=sbr, down=down)
+        if sbr:
+            el.sbr = np.ascontiguousarray(batch.sbr[:, e_idx])
         pcm = decode_batch(cfg, el, Streams(int(batch.stream_slot.max()) + 1), flags, threads)
         dt = np.uint32 if fb == 4 else np.uint16
-        frames = pcm.view(dt).reshape(nf, 1024, 2)
-        planes += [frames[:, :, j] for j in range(k)]
+        frames = pcm.view(dt).reshape(nf, -1, 2)
+        out_ch = (1 if i == 3 else 2) if sbr else k
+        planes += [frames[:, :, j] for j in range(out_ch)]
         c += k
         cpe += k == 2
     return np.ascontiguousarray(np.stack(planes, 2)).view(np.uint8).reshape(nf, -1)

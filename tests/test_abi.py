@@ -69,6 +69,11 @@ def test_config_queries_mirror_decoderconfig():
         mc = N.make_cfg(channel_config=cc)
         assert L.jaad_cfg_channel_count(C.byref(mc)) == n
         assert L.jaad_frame_pcm_bytes(C.byref(mc), N.PCM_BIG_ENDIAN) == 1024 * n * 2
+    # multichannel HE-AAC: SCE and CPE give two channels each, the LFE one (SCE.java:115-132)
+    for cc, n in ((3, 4), (4, 6), (5, 6), (6, 7), (7, 9)):
+        mc = N.make_cfg(sf_index=6, channel_config=cc, sbr=True)
+        assert L.jaad_cfg_channel_count(C.byref(mc)) == n == N.out_channels(mc)
+        assert L.jaad_frame_pcm_bytes(C.byref(mc), N.PCM_FLOAT32) == 2048 * n * 4
 
 
 @pytest.mark.parametrize("fields,status", [
@@ -76,7 +81,7 @@ def test_config_queries_mirror_decoderconfig():
     ({"profile": 1}, N.ERR_UNSUPPORTED),      # AAC Main: ICPrediction is out of scope
     ({"sf_index": 12}, N.ERR_UNSUPPORTED),
     ({"channel_config": 8}, N.ERR_UNSUPPORTED),               # no configuration 8
-    ({"channel_config": 6, "sbr": 1, "ext_sf_index": 0}, N.ERR_UNSUPPORTED),  # multichannel: AAC-LC only
+    ({"channel_config": 6, "sbr": 1, "ps": 1, "ext_sf_index": 0}, N.ERR_UNSUPPORTED),  # PS: mono streams only
     ({"sbr": 1, "ext_sf_index": 1}, N.ERR_UNSUPPORTED),    # SBR output rate must be 2x the core rate
     ({"sbr": 1, "sf_index": 1, "ext_sf_index": 0}, N.ERR_UNSUPPORTED),
     ({"ps": 1, "sbr": 1, "channel_config": 2}, N.ERR_UNSUPPORTED),  # PS needs an SCE core
