@@ -265,6 +265,7 @@ struct jaad_ctx {
     std::vector<jaad_ctx*> children;
     DevBuf d_mc;                                   // gathered element records + element PCM
     std::vector<jaad_sbr_frame> h_mc_sbr;          // one element's SBR records of the call
+    std::vector<jaad_cce_term> h_mc_terms;         // one element's coupling terms of the call
 };
 
 namespace jaad {
@@ -1066,8 +1067,25 @@ int launch_mc_sbr(jaad_ctx* ctx, const jaad_batch* db, void* pcm, uint32_t flags
         c.ms_used = n == 2 ? reinterpret_cast<const uint64_t*>(e + o_ms) : nullptr;
         c.tns = db->tns ? reinterpret_cast<const jaad_tns*>(e + o_tns) : nullptr;
         c.sbr = ctx->h_mc_sbr.data();
-        // the child's SBR records are built on the host during this call (launch_sbr_stage), so
-        // h_mc_sbr is free again when it returns
+        // dependent coupling of this element's channels (the CCE records are shared)
+        ctx->h_mc_terms.clear();
+        for (uint32_t t = 0; t < db->n_cce_terms; t++) {
+            const jaad_cce_term& T = db->cce_terms[t];
+            if (T.channel < ch0 || T.channel >= ch0 + n) continue;
+            ctx->h_mc_terms.push_back(T);
+            ctx->h_mc_terms.back().channel = (uint8_t)(T.channel - ch0);
+        }
+        if (!ctx->h_mc_terms.empty()) {
+            c.n_cce = db->n_cce;
+            c.cce_q = db->cce_q;
+            c.cce_sf = db->cce_sf;
+            c.cce_cb = db->cce_cb;
+            c.cce_ics = db->cce_ics;
+            c.n_cce_terms = (uint32_t)ctx->h_mc_terms.size();
+            c.cce_terms = ctx->h_mc_terms.data();
+        }
+        // the child's SBR records and coupling terms are consumed on the host during this call
+        // (launch_sbr_stage, setup_coupling), so h_mc_sbr / h_mc_terms are free again when it returns
         const int rc = launch(ctx->children[k], &c, e + o_pcm, flags, stream);
         if (rc) return rc;
         ch0 += n;
@@ -1368,8 +1386,8 @@ static int check_batch(const jaad_ctx* ctx, const jaad_batch* b, size_t pcm_byte
     if (ctx->cfg.sbr && b->n_frames && !b->sbr) return JAAD_ERR_INVALID_ARG;
     if (pcm_bytes < pcm_bytes_per_frame(ctx, flags) * b->n_frames) return JAAD_ERR_INVALID_ARG;
     if (flags & ~(uint32_t)(JAAD_PCM_LITTLE_ENDIAN | JAAD_PCM_FLOAT32)) return JAAD_ERR_INVALID_ARG;
-    if (b->n_cce_terms) {  // dependent coupling: AAC-LC in TNS compat mode (jaad_gpu.h)
-        if (ctx->cfg.sbr || ctx->cfg.tns_mode != JAAD_TNS_COMPAT) return JAAD_ERR_UNSUPPORTED;
+    if (b->n_cce_terms) {  // dependent coupling: TNS compat mode (jaad_gpu.h); with SBR the core is coupled
+        if (ctx->cfg.tns_mode != JAAD_TNS_COMPAT) return JAAD_ERR_UNSUPPORTED;
         if (!b->cce_terms || !b->n_cce || !b->cce_q || !b->cce_sf || !b->cce_cb || !b->cce_ics) return JAAD_ERR_INVALID_ARG;
         if (b->n_cce > JAAD_CCE_MAX_RECORDS) return JAAD_ERR_UNSUPPORTED;  // jaad_cce_term.cce is 16-bit
         for (uint32_t t = 0; t < b->n_cce_terms; t++) {

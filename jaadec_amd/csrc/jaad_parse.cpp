@@ -903,7 +903,6 @@ int parse_frame(jaad_parser* p, const uint8_t* data, size_t bytes, jaad_frame_ou
         if (id == 2) {  // CCE: its ICStream as a record, its gains for the terms made at the end
             if (!out->cce_q || !out->cce_sf || !out->cce_cb || !out->cce_ics || !out->cce_terms) return JAAD_ERR_UNSUPPORTED;
             if ((uint32_t)n_cce >= out->cce_cap || n_cce >= 8) return JAAD_ERR_UNSUPPORTED;
-            if (C.cfg.sbr) return JAAD_ERR_UNSUPPORTED;  // coupling with SBR: not decoded here
             cces.emplace_back();
             CceElem& E = cces.back();
             E.rec = n_cce;

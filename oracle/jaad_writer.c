@@ -405,10 +405,28 @@ static int put_cce(Bw* w, int sf_index, int tag, const jaad_cce_desc* d, const i
  * channel elements (records cq/csf/ccb/cics, descriptions d) inserted before their d[k].pos-th
  * channel element (pos = n_elem: after the last), then END.
  */
+long jaad_write_frame_cce_sbr(int sf_index, int n_elem, const int* ids, const int16_t* q, const uint8_t* sf,
+                              const uint8_t* cb, const jaad_ics_info* ics, const uint64_t* ms_used, int n_cce,
+                              const jaad_cce_desc* d, const int16_t* cq, const uint8_t* csf, const uint8_t* ccb,
+                              const jaad_ics_info* cics, const jaad_sbr_frame* sbr, void* const* sbr_state,
+                              uint8_t* out, size_t cap);
+
 long jaad_write_frame_cce(int sf_index, int n_elem, const int* ids, const int16_t* q, const uint8_t* sf,
                           const uint8_t* cb, const jaad_ics_info* ics, const uint64_t* ms_used, int n_cce,
                           const jaad_cce_desc* d, const int16_t* cq, const uint8_t* csf, const uint8_t* ccb,
                           const jaad_ics_info* cics, uint8_t* out, size_t cap)
+{
+    return jaad_write_frame_cce_sbr(sf_index, n_elem, ids, q, sf, cb, ics, ms_used, n_cce, d, cq, csf, ccb, cics, NULL,
+                                    NULL, out, cap);
+}
+
+/* as jaad_write_frame_cce, with element k's SBR record sbr[k] as a FIL right after the element
+ * (when sbr_state[k] is set and the record's status is JAAD_SBR_OK) */
+long jaad_write_frame_cce_sbr(int sf_index, int n_elem, const int* ids, const int16_t* q, const uint8_t* sf,
+                              const uint8_t* cb, const jaad_ics_info* ics, const uint64_t* ms_used, int n_cce,
+                              const jaad_cce_desc* d, const int16_t* cq, const uint8_t* csf, const uint8_t* ccb,
+                              const jaad_ics_info* cics, const jaad_sbr_frame* sbr, void* const* sbr_state,
+                              uint8_t* out, size_t cap)
 {
     Bw w = {out, cap, 0, 0};
     memset(out, 0, cap);
@@ -423,6 +441,12 @@ long jaad_write_frame_cce(int sf_index, int n_elem, const int* ids, const int16_
         if (put_element(&w, sf_index, id, tags[id]++, q + (size_t)ch * 1024, sf + ch * 128, cb + ch * 128, ics + ch,
                         id == 1 ? ms_used + 2 * cpe : NULL, NULL, 0))
             return -1;
+        if (sbr && sbr_state && sbr_state[k] && sbr[k].status == JAAD_SBR_OK) {
+            uint8_t fil[512];
+            const long nbits = jaad_sbr_fil_bits(sbr_state[k], id == 1 ? 2 : 1, &sbr[k], fil, sizeof fil);
+            if (nbits < 0) return -1;
+            for (long i = 0; i < nbits; i++) put(&w, (fil[i >> 3] >> (7 - (i & 7))) & 1u, 1);
+        }
         ch += id == 1 ? 2 : 1;
         cpe += id == 1;
     }

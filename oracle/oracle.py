@@ -65,6 +65,9 @@ def lib() -> C.CDLL:
         L.jaad_write_frame_mc_sbr.argtypes = ([C.c_int, C.c_int, C.c_void_p] + [C.c_void_p] * 6 + [C.c_void_p] * 2 +
                                               [C.c_void_p, C.c_size_t])
         L.jaad_write_frame_mc_sbr.restype = C.c_long
+        L.jaad_write_frame_cce_sbr.argtypes = ([C.c_int, C.c_int, C.c_void_p] + [C.c_void_p] * 5 + [C.c_int] +
+                                               [C.c_void_p] * 5 + [C.c_void_p] * 2 + [C.c_void_p, C.c_size_t])
+        L.jaad_write_frame_cce_sbr.restype = C.c_long
         _lib = L
     return _lib
 
@@ -259,12 +262,16 @@ CCE_DESC_DTYPE = np.dtype([("ind_sw", "u1"), ("count", "u1"), ("domain", "u1"), 
                            ("cge", "u1", (16,)), ("code", "i1", (16, 120))])
 
 
-def write_frames_cce(batch, sf_index: int, ids, cces) -> list:
+def write_frames_cce(batch, sf_index: int, ids, cces, sbr_writers=None) -> list:
     """TEST WRITER: raw_data_blocks of a (multichannel) batch with coupling channel elements:
     cces[f] = list of (desc CCE_DESC_DTYPE scalar, q [1024], sf [128], cb [128], ics ICS_DTYPE scalar)
-    written before channel element desc["pos"] (jaad_write_frame_cce)."""
+    written before channel element desc["pos"] (jaad_write_frame_cce); with sbr_writers (one SbrWriter
+    or None per element) each element's SBR record (batch.sbr [frame] or [frame][element]) follows it."""
     nch = batch.nch
     ids_a = (C.c_int * len(ids))(*ids)
+    states = None
+    if sbr_writers is not None:
+        states = (C.c_void_p * len(ids))(*[w.buf.ctypes.data if w is not None else None for w in sbr_writers])
     buf = np.zeros(1 << 17, np.uint8)
     out = []
     for f in range(batch.n_frames):
@@ -284,9 +291,12 @@ def write_frames_cce(batch, sf_index: int, ids, cces) -> list:
         cics = np.zeros(max(n, 1), N.ICS_DTYPE)
         for k, (dk, qk, sfk, cbk, icsk) in enumerate(lst):
             d[k], cq[k], csf[k], ccb[k], cics[k] = dk, qk, sfk, cbk, icsk
-        r = lib().jaad_write_frame_cce(sf_index, len(ids), ids_a, q.ctypes.data, sf.ctypes.data, cb.ctypes.data,
-                                       ics.ctypes.data, ms.ctypes.data, n, d.ctypes.data, cq.ctypes.data,
-                                       csf.ctypes.data, ccb.ctypes.data, cics.ctypes.data, buf.ctypes.data, buf.nbytes)
+        rec = np.ascontiguousarray(batch.sbr[f]).reshape(-1) if states is not None else None
+        r = lib().jaad_write_frame_cce_sbr(sf_index, len(ids), ids_a, q.ctypes.data, sf.ctypes.data, cb.ctypes.data,
+                                           ics.ctypes.data, ms.ctypes.data, n, d.ctypes.data, cq.ctypes.data,
+                                           csf.ctypes.data, ccb.ctypes.data, cics.ctypes.data,
+                                           rec.ctypes.data if rec is not None else None, states, buf.ctypes.data,
+                                           buf.nbytes)
         if r < 0:
             raise ValueError(f"frame {f} cannot be written")
         out.append(buf[:r].tobytes())

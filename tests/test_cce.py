@@ -83,10 +83,10 @@ def ref_terms(descs, recs, elements):
     return out
 
 
-def cce_records(n, seed, pns=0, short=1):
+def cce_records(n, seed, pns=0, short=1, sf_index=3):
     """n CCE ICStream records (a mono synthetic stream's channel records)."""
     p = N.synth_params(3, n_streams=1, frames_per_stream=max(n, 1), channel_config=1, pns_percent=pns, tns_percent=0,
-                       window_switching=short)
+                       window_switching=short, sf_index=sf_index)
     p.seed = p.seed ^ (0xCCE0 + seed)
     b = N.synth_batch(p)
     ics = b.ics.copy()
@@ -411,3 +411,70 @@ def test_gpu_coupling_rejects_bad_gains_and_too_many_records():
         # the context still decodes a good batch afterwards
         want = O.decode_batch(N.make_cfg(channel_config=2), b, O.Streams(2), N.PCM_BIG_ENDIAN)
         assert (ctx.decode(b) == want).all()
+
+
+# ------------------------------------------------------------------------------------------------
+# coupling with SBR: the reference couples the core spectrum before its SBR runs (A/syntax/CPE.java:
+# 172-179 then :195-204; SCE.java:100-108 then :122-132)
+# ------------------------------------------------------------------------------------------------
+
+def coupled_sbr_batch(cc, n_streams, fps, seed):
+    """An HE-AAC batch (mono / stereo SBR, or multichannel SBR) with random coupling terms."""
+    rng = np.random.default_rng(seed)
+    if cc in N.MC_ELEMENTS:
+        from tests.test_mc_sbr import mc_sbr_synth
+        b = mc_sbr_synth(cc, n_streams=n_streams, fps=fps, seed=seed)
+    else:
+        p = N.synth_params(4, n_streams=n_streams, frames_per_stream=fps, channel_config=cc)
+        p.seed ^= seed
+        b = N.synth_batch(p)
+    n_rec = max(4, b.n_frames // 4)
+    b.cce_q, b.cce_sf, b.cce_cb, b.cce_ics = cce_records(n_rec, seed, pns=10, sf_index=6)
+    terms = []
+    for f in range(b.n_frames):
+        if rng.integers(2):
+            continue
+        for _ in range(int(rng.integers(1, 4))):
+            t = np.zeros((), N.CCE_TERM_DTYPE)
+            t["frame"], t["channel"], t["point"] = f, rng.integers(b.nch), rng.integers(2)
+            t["cce"] = rng.integers(n_rec)
+            t["gain"] = rng.choice([0.0, 1.0, -0.5, 2.0, -3.25, 1.0905077], 120).astype(np.float32)
+            terms.append(t)
+    b.cce_terms = np.array(terms, N.CCE_TERM_DTYPE)
+    return b
+
+
+def test_cce_with_sbr_parses():
+    """A stereo HE-AAC frame with a CCE: the CCE and the SBR payload (which attaches to the last
+    channel element, not to the CCE) both parse."""
+    from tests.test_parse_sbr import _assert_sbr_equal
+    p = N.synth_params(4, n_streams=1, frames_per_stream=4, channel_config=2)
+    b = N.synth_batch(p)
+    rng = np.random.default_rng(3)
+    per_frame = []
+    for f in range(4):
+        q, sf, cb, ics = cce_records(1, 40 + f, sf_index=6)
+        d = rand_desc(rng, [(1, 0, 3)], cb[0], ics[0], pos=int(rng.integers(2)))
+        per_frame.append([(d, q[0], sf[0], cb[0], ics[0])])
+    cfg = N.cfg_for(p)
+    frames = O.write_frames_cce(b, p.sf_index, (1,), per_frame, sbr_writers=[O.SbrWriter(cfg.ext_sf_index, 5)])
+    P = N.Parser(cfg)
+    P.pns_state = int(b.ics["pns_state"][0])
+    got = P.parse(frames)
+    assert got.q.tobytes() == b.q.tobytes() and got.n_cce == 4 and len(got.cce_terms) >= 4
+    _assert_sbr_equal(got.sbr, b.sbr, 2, cfg.ext_sf_index)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cc", [1, 2, 6])
+def test_gpu_coupling_with_sbr_matches_oracle(cc):
+    b = coupled_sbr_batch(cc, n_streams=4, fps=16, seed=30 + cc)
+    if cc in N.MC_ELEMENTS:
+        cfg = N.make_cfg(sf_index=6, channel_config=cc, sbr=True)
+        want = O.decode_batch_mc(6, b, N.MC_ELEMENTS[cc], N.PCM_BIG_ENDIAN, threads=8, sbr=True)
+    else:
+        cfg = N.make_cfg(sf_index=6, channel_config=cc, sbr=True)
+        want = O.decode_batch(cfg, b, O.Streams(4), N.PCM_BIG_ENDIAN, threads=8)
+    with N.Context(cfg, 4) as ctx:
+        got = ctx.decode(b, N.PCM_BIG_ENDIAN)
+    assert (got == want).all(), np.flatnonzero((got != want).any(1))[:8]
