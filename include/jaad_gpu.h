@@ -325,11 +325,15 @@ int jaad_ctx_core_channels(const jaad_ctx* ctx);
 int jaad_decode_batch(jaad_ctx* ctx, const jaad_batch* batch, void* pcm_out, size_t pcm_bytes,
                       uint32_t flags);
 
+/* On an error status the PCM buffer's contents are unspecified (pieces decoded before a later piece
+ * failed its checks may have been written); the stream states are as before the call.        */
+
 /* Page-lock [p, p + bytes) (hipHostRegister) for the context's host-buffer entry: batch arrays
  * and PCM buffers that lie inside a registered range skip the staging copy.  Register buffers
  * that are reused call after call (a JNI caller: its direct ByteBuffers, once per stream);
  * unregister before freeing them.  jaad_ctx_destroy unregisters what is left.  Memory that is
- * page-locked already (hipHostMalloc) is accepted and only recorded.                         */
+ * page-locked already (hipHostMalloc) is accepted and only recorded.  Registering the same start
+ * address again is a no-op (JAAD_ERR_INVALID_ARG if it asks for a longer range).             */
 int jaad_host_register(jaad_ctx* ctx, void* p, size_t bytes);
 int jaad_host_unregister(jaad_ctx* ctx, void* p);
 /* Page-locked host memory owned by the context (hipHostMalloc), counted as registered: batch

@@ -1559,8 +1559,25 @@ static int decode_batch_serial(jaad_ctx* ctx, const jaad_batch* b, void* pcm_out
 // ics, ms_used, tns of the piece back to back; four small copies per piece cost ~0.5 ms of DMA
 // set-up per C2 batch).  The piece's kernel gets pointers into its block, offset by the piece's
 // first channel-frame so that the batch-wide indices land in it.
+static int decode_batch_pieces_impl(jaad_ctx* ctx, const jaad_batch* b, void* pcm_out, uint32_t flags,
+                                    const std::vector<uint32_t>& run0);
+
+// Every exit waits for the copies and kernels already queued: they read and write caller memory
+// (registered buffers are copied by DMA directly), which the caller may free once this returns.
 static int decode_batch_pieces(jaad_ctx* ctx, const jaad_batch* b, void* pcm_out, uint32_t flags,
                                const std::vector<uint32_t>& run0)
+{
+    const int rc = decode_batch_pieces_impl(ctx, b, pcm_out, flags, run0);
+    if (rc) {
+        for (hipStream_t st : {ctx->h2d, ctx->d2h, ctx->stream})
+            if (st) (void)hipStreamSynchronize(st);
+        (void)hipGetLastError();
+    }
+    return rc;
+}
+
+static int decode_batch_pieces_impl(jaad_ctx* ctx, const jaad_batch* b, void* pcm_out, uint32_t flags,
+                                    const std::vector<uint32_t>& run0)
 {
     const int nch = ctx->nch;
     const size_t nf = b->n_frames, ncf = nf * nch;
@@ -1867,9 +1884,15 @@ static int decode_batch_whole(jaad_ctx* ctx, const jaad_batch* b, void* pcm_out,
     return decode_batch_pieces(ctx, b, pcm_out, flags, run0);
 }
 
+static std::vector<jaad_ctx::PinRange>::iterator find_pin(jaad_ctx* ctx, void* p);
+
 int jaad_host_register(jaad_ctx* ctx, void* p, size_t bytes)
 {
     if (!ctx || !p || !bytes) return JAAD_ERR_INVALID_ARG;
+    {  // a second registration of the same range is a no-op (one entry, one unregister)
+        auto it = find_pin(ctx, p);
+        if (it != ctx->pinned.end()) return it->n >= bytes ? JAAD_OK : JAAD_ERR_INVALID_ARG;
+    }
     HIPCHK(hipSetDevice(ctx->device));
     // memory that is page-locked already (hipHostMalloc, another registration) is recorded as is
     hipPointerAttribute_t at{};

@@ -531,9 +531,13 @@ int jaad_asc_parse(const uint8_t* asc, size_t bytes, jaad_stream_cfg* cfg)
         if (br.read(1)) br.skip(1);                   // extensionFlag -> extensionFlag3
         if (br.overrun()) return JAAD_ERR_EOS;
         if (chc == 0) {  // DecoderConfig.decode: PCE.read + setAudioDecoderInfo (A/DecoderConfig.java:231-235)
-            int pprof = 0;
-            const int st = read_pce_layout(br, pprof, sfi, chc);
+            int pprof = 0, psfi = sfi;
+            const int st = read_pce_layout(br, pprof, psfi, chc);
             if (st) return st;
+            // outputFrequency was set to the ASC's rate before the PCE (A/DecoderConfig.java:180);
+            // setAudioDecoderInfo then takes the PCE's.  With different rates the reference's
+            // getSampleLength turns 2048 and it outputs at the ASC's rate: not reproduced, refused.
+            if (psfi != sfi) return JAAD_ERR_UNSUPPORTED;
             aot = pprof;
         }
         // readSyncExtension (A/DecoderConfig.java:238, 260-291; sbrEnabled is always on): a

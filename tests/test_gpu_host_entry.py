@@ -138,3 +138,25 @@ def test_host_alloc_buffers_and_foreign_pinned_memory():
         ctx.decode(tb, out=out2)
         ctx.unregister(*arrays)
     assert (out2 == want).all()
+
+
+@pytest.mark.gpu
+def test_registering_a_range_twice_is_idempotent():
+    """a second jaad_host_register of the same range keeps one entry, so one unregister
+    releases it and a second one is refused; a longer range at the same address is refused."""
+    p = N.synth_params(2, n_streams=2, frames_per_stream=8)
+    b = N.synth_batch(p)
+    with N.Context(N.cfg_for(p), 2) as ctx:
+        want = ctx.decode(b, N.PCM_BIG_ENDIAN)
+        ctx.register(b.q)
+        ctx.register(b.q)
+        import ctypes as C
+        assert N.lib().jaad_host_register(ctx.h, C.c_void_p(b.q.ctypes.data), C.c_size_t(b.q.nbytes + 4096)) == \
+            N.ERR_INVALID_ARG
+        for s in range(2):
+            ctx.state_reset(s)
+        assert (ctx.decode(b, N.PCM_BIG_ENDIAN) == want).all()
+        ctx.unregister(b.q)
+        with pytest.raises(N.JaadError) as e:
+            ctx.unregister(b.q)
+        assert e.value.status == N.ERR_INVALID_ARG

@@ -159,8 +159,13 @@ def test_asc_program_config_element_layouts(layout, cc):
 
 
 def test_asc_program_config_element_rate_and_refusals():
-    # setAudioDecoderInfo(pce): the PCE's sample rate replaces the ASC's
-    assert N.asc_parse(_pce_asc(4, front=[True], pce_sfi=3)).sf_index == 3
+    # setAudioDecoderInfo(pce) replaces sampleFrequency with the PCE's rate after outputFrequency was
+    # set to the ASC's (A/DecoderConfig.java:180, 231-235): with different rates the reference's
+    # getSampleLength becomes 2048 at the ASC's output rate -- not reproduced, refused
+    with pytest.raises(N.JaadError) as e:
+        N.asc_parse(_pce_asc(4, front=[True], pce_sfi=3))
+    assert e.value.status == N.ERR_UNSUPPORTED
+    assert N.asc_parse(_pce_asc(3, front=[True], pce_sfi=3)).sf_index == 3  # equal rates decode
     for layout in (dict(front=[False, False]),                        # dual mono: SCE SCE is not the CPE list
                    dict(front=[True, False]),                         # CPE then SCE: not the 3.0 list
                    dict(front=[False, True, True], back=[True]),      # 7 channels: forChannelCount throws

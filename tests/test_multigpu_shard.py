@@ -72,3 +72,67 @@ def test_gloo_world2_sharded_decode_is_byte_identical(world):
     slots = [s for g in got for s in g[0]]
     assert slots == list(range(6))
     assert b"".join(g[1] for g in got) == want
+
+
+@pytest.mark.gpu
+def test_gpu_c5_whole_job_as_eight_shards():
+    """the whole C5 job (HE-AAC v2, 2048 streams x 128 frames = 262 144 frames) on
+    the HIP engine, once in one context and once as the 8 shard_runs slices of an 8-GPU run (each
+    slice in its own context, one after the other on this GPU): the slices' PCM concatenates to the
+    single-context PCM, and a sample of streams equals the restatement (0 LSB)."""
+    from oracle import oracle as O
+    p = N.synth_params(5)  # 2048 streams x 128 frames
+    full = N.synth_batch(p)
+    assert full.n_frames == 262144
+    cfg = N.cfg_for(p)
+    with N.Context(cfg, len(full.stream_slot)) as ctx:
+        one = ctx.decode(full, N.PCM_BIG_ENDIAN)
+    parts = []
+    for r in range(8):
+        mine = rank_batch(full, 8, r)
+        assert len(mine.stream_slot) == 256
+        with N.Context(cfg, len(full.stream_slot)) as ctx:
+            parts.append(ctx.decode(mine, N.PCM_BIG_ENDIAN))
+    assert np.array_equal(np.concatenate(parts), one)
+    sample = [0, 511, 1024, 2047]
+    want = O.decode_batch(cfg, full.select_runs(sample), O.Streams(len(full.stream_slot)), N.PCM_BIG_ENDIAN, threads=4)
+    fb = full.frame_begin
+    got = np.concatenate([one[fb[r]:fb[r + 1]] for r in sample])
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.gpu
+def test_gpu_two_contexts_from_two_threads():
+    """INTEGRATION s6 "(or thread)": two contexts on one GPU driven from two host threads at once
+    (AAC-LC and HE-AAC v1), five calls each; every call's PCM equals the single-threaded decode."""
+    import threading
+    jobs = []
+    for config, ns in ((2, 64), (4, 16)):
+        p = N.synth_params(config, n_streams=ns, frames_per_stream=64)
+        b = N.synth_batch(p)
+        with N.Context(N.cfg_for(p), ns) as ctx:
+            want = [ctx.decode(c, N.PCM_BIG_ENDIAN) for c in b.split_frames(32)]
+        jobs.append((N.cfg_for(p), ns, b, want))
+    errors = []
+
+    def run(cfg, ns, b, want):
+        try:
+            a1, a2 = b.split_frames(32)
+            with N.Context(cfg, ns) as ctx:
+                for _ in range(5):
+                    for s in range(ns):
+                        ctx.state_reset(s)
+                    g1 = ctx.decode(a1, N.PCM_BIG_ENDIAN)
+                    g2 = ctx.decode(a2, N.PCM_BIG_ENDIAN)
+                    if not (np.array_equal(g1, want[0]) and np.array_equal(g2, want[1])):
+                        errors.append("PCM differs")
+        except Exception as e:  # noqa: BLE001 -- reported below
+            errors.append(repr(e))
+
+    th = [threading.Thread(target=run, args=j) for j in jobs]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    assert not any(t.is_alive() for t in th)
+    assert not errors, errors
