@@ -58,6 +58,16 @@ WORKLOADS = {
 PER_GPU_STREAMS = {5: 256}  # C5 is quoted for 8 GPUs: each rank decodes 1/8 of the 2048-stream job
 
 
+def cpu_model() -> str:
+    try:
+        for line in Path("/proc/cpuinfo").read_text().splitlines():
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -271,7 +281,9 @@ def run(args, engine_cls=HipEngine, backend: str = "nccl"):
         O.decode_batch(cfg, sub, O.Streams(nsl), flags, threads=1)
         dt1 = time.perf_counter() - t1
         ncores = os.cpu_count() or 1
-        thr = min(ncores, 64)
+        # the box's CPU share, not the whole machine's CPUs (os.cpu_count() shows all of them there;
+        # the GPU pool sets OMP_NUM_THREADS to the share of one GPU)
+        thr = max(1, min(ncores, len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "64") or 64)))
         t1 = time.perf_counter()
         O.decode_batch(cfg, sub, O.Streams(nsl), flags, threads=thr)
         dtn = time.perf_counter() - t1
@@ -279,16 +291,20 @@ def run(args, engine_cls=HipEngine, backend: str = "nccl"):
                "sample": f"{sub.n_frames} frames ({ns} streams x {p.frames_per_stream}) of the same workload, "
                          f"C restatement of the JAAD Java DSP (oracle/, -O2 -ffp-contract=off), 1 thread, "
                          f"parse excluded on both sides",
-               "multicore_value": round(sub.n_frames / dtn, 1), "multicore_threads": thr}
+               "multicore_value": round(sub.n_frames / dtn, 1), "multicore_threads": thr,
+               "nproc": ncores, "affinity_cpus": len(os.sched_getaffinity(0)), "cpu_model": cpu_model()}
 
-    # HBM bytes per launch measured by rocprofv3 PMC passes of this same command
-    # (scripts/gpu_prof.sh -> scripts/summarize_prof.py -> profiles/current.json)
+    # HBM bytes per step measured by rocprofv3 PMC passes of this same command at the same config
+    # (scripts/gpu_prof.sh [config] -> scripts/summarize_prof.py -> profiles/current_c<config>.json)
     traffic, traffic_src = None, None
-    cur = ROOT / "profiles" / "current.json"
-    if cur.exists() and args.config == 2:
+    cur = ROOT / "profiles" / f"current_c{args.config}.json"
+    if not cur.exists() and args.config == 2:
+        cur = ROOT / "profiles" / "current.json"
+    if cur.exists():
         prof = json.loads(cur.read_text())
-        traffic = prof.get("hbm_traffic_bytes_per_launch")
-        traffic_src = f"profiles/{prof.get('tag')}.json ({prof.get('hbm_traffic_note')})" if traffic else None
+        if prof.get("frames_per_step", n_frames) == n_frames:  # the profile's workload is this one
+            traffic = prof.get("hbm_traffic_bytes_per_launch")
+            traffic_src = f"profiles/{prof.get('tag')}.json ({prof.get('hbm_traffic_note')})" if traffic else None
 
     line = None
     if rank == 0:

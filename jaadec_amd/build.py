@@ -48,17 +48,41 @@ def _deps(*globs: str) -> list[Path]:
 
 # per-source extra flags (the LC kernel: see DESIGN.md §4a, scheduler strategy)
 GPU_FILE_FLAGS: dict[str, list[str]] = {}
+# kernel sources whose device assembly goes through tools/vop3_rewrite.py (VCC-implicit VOP2 /
+# VOPC forms re-encoded as VOP3: DESIGN.md §4a, round 4) before it is assembled
+VOP3_REWRITE: dict[str, tuple[str, ...]] = {}
+LLVM = Path(os.environ.get("ROCM_LLVM", "/opt/rocm/lib/llvm/bin"))
+
+
+def _hip_obj_rewritten(cmd_common: list[str], src: Path, obj: Path, forms: tuple[str, ...]) -> None:
+    """hipcc -c of `src` with its device code taken through vop3_rewrite: device assembly
+    (branches kept within 2^14 words so the longer encodings still reach), rewrite, assemble,
+    link the code object, bundle it, then the host compile embeds the bundle."""
+    base = obj.with_suffix("")
+    s, s2, do, co, fb = (base.with_suffix(x) for x in (".dev.s", ".dev3.s", ".dev.o", ".dev.co", ".hipfb"))
+    _run(cmd_common + ["--cuda-device-only", "-S", "-mllvm", "-amdgpu-s-branch-bits=14", "-o", str(s), str(src)])
+    _run([sys.executable, str(ROOT / "tools" / "vop3_rewrite.py"), str(s), str(s2)] + list(forms))
+    _run([str(LLVM / "clang"), "-cc1as", "-triple", "amdgcn-amd-amdhsa", "-target-cpu", ARCH, "-filetype", "obj",
+          "-o", str(do), str(s2)])
+    _run([str(LLVM / "lld"), "-flavor", "gnu", "-m", "elf64_amdgpu", "--no-undefined", "-shared", "-o", str(co), str(do)])
+    _run([str(LLVM / "clang-offload-bundler"), "-type=o", "-bundle-align=4096",
+          f"-targets=host-x86_64-unknown-linux-gnu,hipv4-amdgcn-amd-amdhsa--{ARCH}", "-input=/dev/null",
+          f"-input={co}", f"-output={fb}"])
+    _run(cmd_common + ["--cuda-host-only", "-Xclang", "-fcuda-include-gpubinary", "-Xclang", str(fb), "-c", "-o", str(obj),
+                       str(src)])
 
 
 def build_gpu(force: bool = False, out: Path | None = None, defines: list[str] | None = None,
-              extra: list[str] | None = None) -> Path:
-    """Build the product library (or, with `defines`, an experimental variant at `out`): every
-    source compiled on its own (in parallel, with its GPU_FILE_FLAGS), then linked."""
+              extra: list[str] | None = None, vop3: dict[str, tuple[str, ...]] | None = None) -> Path:
+    """Build the product library (or, with `defines`/`vop3`, an experimental variant at `out`): every
+    source compiled on its own (in parallel, with its GPU_FILE_FLAGS; VOP3_REWRITE sources through
+    the re-encoding pipeline), then linked."""
     out = out or LIB
+    rewrite = VOP3_REWRITE if vop3 is None else vop3
     srcs = [CSRC / "jaad_lc.hip", CSRC / "jaad_sbr.hip", CSRC / "jaad_ps.hip", CSRC / "jaad_capi.cpp", CSRC / "jaad_sbr_host.cpp",
             CSRC / "jaad_parse.cpp", CSRC / "jaad_parse_sbr.cpp", CSRC / "jaad_mp4.cpp"]
-    deps = srcs + _deps("jaadec_amd/csrc/*.h", "jaadec_amd/csrc/tables/*.inc", "include/*.h")
-    if force or defines or extra or _stale(out, deps):
+    deps = srcs + _deps("jaadec_amd/csrc/*.h", "jaadec_amd/csrc/tables/*.inc", "include/*.h") + [ROOT / "tools" / "vop3_rewrite.py"]
+    if force or defines or extra or vop3 is not None or _stale(out, deps):
         objdir = ROOT / "build" / "obj" / out.stem
         objdir.mkdir(parents=True, exist_ok=True)
         common = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
@@ -66,9 +90,16 @@ def build_gpu(force: bool = False, out: Path | None = None, defines: list[str] |
         common += [f"-D{d}" for d in (defines or [])] + (extra or [])
         objs = [objdir / (s.name + ".o") for s in srcs]
         from concurrent.futures import ThreadPoolExecutor
+        def one(so):
+            src, obj = so
+            cmd = common + GPU_FILE_FLAGS.get(src.name, [])
+            if src.name in rewrite:
+                _hip_obj_rewritten(cmd, src, obj, rewrite[src.name])
+            else:
+                _run(cmd + ["-c", "-o", str(obj), str(src)])
+
         with ThreadPoolExecutor(min(8, os.cpu_count() or 1)) as ex:
-            list(ex.map(lambda so: _run(common + GPU_FILE_FLAGS.get(so[0].name, []) + ["-c", "-o", str(so[1]), str(so[0])]),
-                        zip(srcs, objs)))
+            list(ex.map(one, zip(srcs, objs)))
         tmp = out.with_suffix(".so.tmp")
         _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fno-gpu-rdc", "-o", str(tmp)] + [str(o) for o in objs])
         tmp.replace(out)

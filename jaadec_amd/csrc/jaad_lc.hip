@@ -295,6 +295,7 @@ __device__ __forceinline__ void xch_hi(float& a, float& b)
 // Swizzles: lane ^ 1, ^ 2 by quad_perm; ^ 8 by row_ror:8; ^ 4 by row_ror:4 (lanes with bit 2 set
 // read lane - 4) and row_ror:12 (bit 2 clear read lane + 4).  A DPP read of a VGPR that a VALU
 // instruction wrote needs 2 wait states: the copies (bits 2, 3) or an s_nop (bits 0, 1) give them.
+#ifndef JAAD_XCH_VCC
 template <int L>
 __device__ __forceinline__ void xch2(f2& a0, f2& b0, f2& a1, f2& b1)
 {
@@ -352,6 +353,43 @@ __device__ __forceinline__ void xch2(f2& a0, f2& b0, f2& a1, f2& b1)
 #undef JAAD_XCH_QUAD
     }
 }
+#else  // round-3 form (VOP2 v_cndmask_b32_dpp through VCC), kept for A/B timing
+template <int L>
+__device__ __forceinline__ void xch2(f2& a0, f2& b0, f2& a1, f2& b1)
+{
+    // lanes with bit L set (the pattern repeats per 32 lanes: vcc_lo = vcc_hi, literal operands,
+    // no SGPRs held across the exchanges)
+    constexpr uint32_t kHi = L == 0 ? 0xAAAAAAAAu : L == 1 ? 0xCCCCCCCCu : L == 2 ? 0xF0F0F0F0u : 0xFF00FF00u;
+    f2 na0, nb0, na1, nb1;
+#define JAAD_XCH_BODY(QA, QB)                                                                    \
+    asm("s_mov_b32 vcc_lo, %[lo]\n\t"                                                            \
+        "s_mov_b32 vcc_hi, %[lo]\n\t"                                                            \
+        "v_cndmask_b32_dpp %[na0x], %[b0x], %[a0x], vcc " QA " row_mask:0xf bank_mask:0xf\n\t"   \
+        "v_cndmask_b32_dpp %[na0y], %[b0y], %[a0y], vcc " QA " row_mask:0xf bank_mask:0xf\n\t"   \
+        "v_cndmask_b32_dpp %[na1x], %[b1x], %[a1x], vcc " QA " row_mask:0xf bank_mask:0xf\n\t"   \
+        "v_cndmask_b32_dpp %[na1y], %[b1y], %[a1y], vcc " QA " row_mask:0xf bank_mask:0xf\n\t"   \
+        "s_mov_b32 vcc_lo, %[hi]\n\t"                                                            \
+        "s_mov_b32 vcc_hi, %[hi]\n\t"                                                            \
+        "v_cndmask_b32_dpp %[nb0x], %[a0x], %[b0x], vcc " QB " row_mask:0xf bank_mask:0xf\n\t"   \
+        "v_cndmask_b32_dpp %[nb0y], %[a0y], %[b0y], vcc " QB " row_mask:0xf bank_mask:0xf\n\t"   \
+        "v_cndmask_b32_dpp %[nb1x], %[a1x], %[b1x], vcc " QB " row_mask:0xf bank_mask:0xf\n\t"   \
+        "v_cndmask_b32_dpp %[nb1y], %[a1y], %[b1y], vcc " QB " row_mask:0xf bank_mask:0xf"       \
+        : [na0x] "=&v"(na0.x), [na0y] "=&v"(na0.y), [na1x] "=&v"(na1.x), [na1y] "=&v"(na1.y),     \
+          [nb0x] "=&v"(nb0.x), [nb0y] "=&v"(nb0.y), [nb1x] "=&v"(nb1.x), [nb1y] "=&v"(nb1.y)      \
+        : [a0x] "v"(a0.x), [a0y] "v"(a0.y), [a1x] "v"(a1.x), [a1y] "v"(a1.y), [b0x] "v"(b0.x),    \
+          [b0y] "v"(b0.y), [b1x] "v"(b1.x), [b1y] "v"(b1.y), [lo] "i"(~kHi), [hi] "i"(kHi)        \
+        : "vcc")
+    if constexpr (L == 0) JAAD_XCH_BODY("quad_perm:[1,0,3,2]", "quad_perm:[1,0,3,2]");
+    else if constexpr (L == 1) JAAD_XCH_BODY("quad_perm:[2,3,0,1]", "quad_perm:[2,3,0,1]");
+    else if constexpr (L == 2) JAAD_XCH_BODY("row_ror:4", "row_ror:12");
+    else JAAD_XCH_BODY("row_ror:8", "row_ror:8");
+#undef JAAD_XCH_BODY
+    a0 = na0;
+    b0 = nb0;
+    a1 = na1;
+    b1 = nb1;
+}
+#endif
 
 // register bit I <-> lane bit L for all four register pairs, both floats of each complex value
 template <int I, int L>
