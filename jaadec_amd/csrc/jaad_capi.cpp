@@ -654,12 +654,14 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
                         __builtin_prefetch(reinterpret_cast<const char*>(&b->sbr[f + 2]) + o);
                 const jaad_sbr_frame& F = b->sbr[f];
                 if (F.status == JAAD_SBR_UPSAMPLE) {
-                    // the reference would still take this frame's header: a table reset it then
-                    // never applies (the next frame's reset flag is read afresh, A/sbr/SBR.java:168)
-                    if (F.header_present && (!hs.have_hdr || SbrHost::header_changes(hs.hdr, F.hdr))) {
-                        rcs[t] = JAAD_ERR_UNSUPPORTED;
-                        bad[t] = (int)f;
-                        break;
+                    // the reference still takes this frame's header (SbrHost::take_header)
+                    if (F.header_present) {
+                        const int hr = ctx->sbr_host->take_header(hs, F.hdr);
+                        if (hr) {
+                            rcs[t] = hr;
+                            bad[t] = (int)f;
+                            break;
+                        }
                     }
                     continue;
                 }
@@ -2050,8 +2052,8 @@ int jaad_state_import(jaad_ctx* ctx, uint32_t slot, const void* buf, size_t byte
         in += 2048 * sizeof(float);
         SbrHostSlot hs;
         std::memcpy(&hs, in + 2 * sizeof(SbrChState), sizeof hs);
-        if (hs.have_hdr) {  // re-derive the table index in this context from the saved header
-            hs.table = ctx->sbr_host->table_index(hs.hdr);
+        if (hs.have_hdr) {  // re-derive the table index in this context from the saved header(s)
+            hs.table = ctx->sbr_host->table_index(hs);
             if (hs.table < 0) return JAAD_ERR_INVALID_ARG;
         }
         HIPCHK(hipMemcpy(ctx->d_sbr_state + (size_t)slot * 2, in, 2 * sizeof(SbrChState), hipMemcpyHostToDevice));

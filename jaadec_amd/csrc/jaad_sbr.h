@@ -206,6 +206,11 @@ struct SbrHostSlot {
     int table;        // index into the context's table list, -1 before the first header
     int kx_prev, M_prev;
     SbrHostCh ch[2];
+    // a header taken on a JAAD_SBR_UPSAMPLE frame: the frequency tables are hdr's, the patches
+    // and limiter bands still those of phdr (the header of the last reset that ran
+    // patch_construction / limiter_frequency_table, SbrHost::take_header)
+    int mixed;
+    jaad_sbr_header phdr;
 };
 
 // Full derived tables of one header (host copy of the SBR object's table fields).
@@ -242,6 +247,17 @@ public:
     const std::vector<SbrTab>& tabs() const { return tabs_; }
     // table index for a header (built on first use); -1 if its tables are invalid
     int table_index(const jaad_sbr_header& h) { return table_for(h); }
+    // the table a slot's state uses (pure or mixed, see SbrHostSlot.mixed); -1 if invalid
+    int table_index(const SbrHostSlot& s) { return s.mixed ? mixed_for(s.hdr, s.phdr) : table_for(s.hdr); }
+    // The header of a JAAD_SBR_UPSAMPLE frame.  SBR.decode reads it into this.hdr and, when it
+    // differs, recomputes the frequency tables (calc_sbr_tables, A/sbr/SBR.java:168-177,212-221)
+    // even though the frame's SBR then does not run; patch_construction and
+    // limiter_frequency_table run only inside a processed frame's HF generation with its own reset
+    // flag (A/sbr/HFGeneration.java:27-28,95-97), so the next frames use the new frequency tables
+    // with the old patches and limiter bands until a processed frame resets.  JAAD_ERR_UNSUPPORTED
+    // where that mix would make the reference read outside its arrays or stale values (a different
+    // M, a patch past band 63, a patch source at or above the new kx, no previous header).
+    int take_header(SbrHostSlot& st, const jaad_sbr_header& h);
 
 private:
     int out_sf_;
@@ -249,7 +265,11 @@ private:
     std::vector<SbrTab> tabs_;                       // capacity fixed: elements never move
     std::vector<std::unique_ptr<SbrFbt>> fbt_;
     std::vector<jaad_sbr_header> keys_;
+    std::vector<std::pair<jaad_sbr_header, jaad_sbr_header>> mixed_keys_;
+    std::vector<int> mixed_idx_;
     int table_for(const jaad_sbr_header& h);
+    int mixed_for(const jaad_sbr_header& h, const jaad_sbr_header& ph);
+    int push_table(std::unique_ptr<SbrFbt> t, const jaad_sbr_header& key);
 };
 
 }  // namespace jaad

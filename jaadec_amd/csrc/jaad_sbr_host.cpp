@@ -351,7 +351,14 @@ int SbrHost::table_for(const jaad_sbr_header& h)
     }
     limiter_tables(t);
     band_maps(t);
+    return push_table(std::move(tp), h);
+}
 
+// the kernels' copy of a derived table set; appended under mu_ (held by the caller)
+int SbrHost::push_table(std::unique_ptr<SbrFbt> tp, const jaad_sbr_header& h)
+{
+    if (keys_.size() >= kMaxTables) return -1;
+    const SbrFbt& t = *tp;
     SbrTab g;
     std::memset(&g, 0, sizeof g);
     g.kx = (uint8_t)t.kx;
@@ -383,6 +390,55 @@ int SbrHost::table_for(const jaad_sbr_header& h)
     return (int)tabs_.size() - 1;
 }
 
+int SbrHost::mixed_for(const jaad_sbr_header& h, const jaad_sbr_header& ph)
+{
+    const int a = table_for(h), b = table_for(ph);
+    if (a < 0 || b < 0) return -1;
+    if (a == b) return a;
+    std::lock_guard<std::mutex> lock(mu_);
+    for (size_t i = 0; i < mixed_keys_.size(); i++)
+        if (!header_differs(mixed_keys_[i].first, h) && !header_differs(mixed_keys_[i].second, ph)) return mixed_idx_[i];
+    const SbrFbt& N = *fbt_[a];
+    const SbrFbt& O = *fbt_[b];
+    // the reference would index outside its arrays (patches past band 63, limiter bands against
+    // another M) or read sources the new analysis leaves zero: not reproduced
+    if (N.M != O.M || N.kx + O.gen_cnt > 64 || O.max_src >= N.kx) return -1;
+    auto tp = std::make_unique<SbrFbt>(N);
+    SbrFbt& t = *tp;
+    t.noPatches = O.noPatches;
+    std::memcpy(t.patchNoSubbands, O.patchNoSubbands, sizeof t.patchNoSubbands);
+    std::memcpy(t.patchStartSubband, O.patchStartSubband, sizeof t.patchStartSubband);
+    t.max_src = O.max_src;
+    t.gen_cnt = O.gen_cnt;
+    std::memcpy(t.f_table_lim, O.f_table_lim, sizeof t.f_table_lim);
+    std::memcpy(t.N_L, O.N_L, sizeof t.N_L);
+    band_maps(t);
+    jaad_sbr_header key = h;
+    key.start_freq = 0xFF;  // the pure-table lookup must never find this one (a 4-bit field)
+    const int idx = push_table(std::move(tp), key);
+    if (idx < 0) return -1;
+    mixed_keys_.push_back({h, ph});
+    mixed_idx_.push_back(idx);
+    return idx;
+}
+
+int SbrHost::take_header(SbrHostSlot& st, const jaad_sbr_header& h)
+{
+    if (!st.have_hdr) return JAAD_ERR_UNSUPPORTED;  // no patches or limiter bands yet
+    if (!header_differs(h, st.hdr)) {                // the same tables: the other fields move
+        st.hdr = h;
+        return JAAD_OK;
+    }
+    const jaad_sbr_header ph = st.mixed ? st.phdr : st.hdr;
+    const int idx = mixed_for(h, ph);
+    if (idx < 0) return JAAD_ERR_UNSUPPORTED;
+    st.mixed = header_differs(h, ph) ? 1 : 0;
+    st.phdr = ph;
+    st.hdr = h;
+    st.table = idx;
+    return JAAD_OK;
+}
+
 int SbrHost::frame(SbrHostSlot& st, const jaad_sbr_frame& fr, int nch, bool first, uint32_t slot, SbrRec* rec,
                    float* epool, uint32_t& epos, uint32_t e_base)
 {
@@ -393,6 +449,7 @@ int SbrHost::frame(SbrHostSlot& st, const jaad_sbr_frame& fr, int nch, bool firs
         st.have_hdr = 1;
         if (reset) {
             st.table = table_for(fr.hdr);
+            st.mixed = 0;  // patch_construction and the limiter tables run with this reset
             if (st.table < 0) return JAAD_ERR_BITSTREAM;
         }
     }

@@ -538,6 +538,11 @@ static int decode_frame(const jaad_stream_cfg* cfg, orc_stream* st, const jaad_b
                        st->overlap[c]);
     }
     if (cfg->sbr && b->sbr[f].status == JAAD_SBR_UPSAMPLE) {
+        if (b->sbr[f].header_present) { /* SBR.decode still took the header (orc_sbr_take_header) */
+            if (!st->sbr) return JAAD_ERR_UNSUPPORTED;  /* no SBR object has seen a header yet */
+            rc = orc_sbr_take_header(st->sbr, &b->sbr[f].hdr);
+            if (rc) return rc;
+        }
         /* SBR invalid (ChannelElement.isSBRPresent false, A/syntax/ChannelElement.java:76-78):
          * CPE.process / SCE.process upsample the core instead (A/syntax/CPE.java:201-204,
          * A/syntax/SCE.java:129-131) when the buffer is longer than a frame; the SBR object is

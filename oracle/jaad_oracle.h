@@ -72,6 +72,7 @@ size_t orc_sbr_bytes(void);
 void orc_sbr_init(orc_sbr* s, int out_sf_index);
 /* SBR.decode for one frame's parsed SBR data (header handling, NoiseEnvelope dequantisation) */
 int orc_sbr_decode(orc_sbr* s, const jaad_sbr_frame* fr, int nch);
+int orc_sbr_take_header(orc_sbr* s, const jaad_sbr_header* h);
 /* SBR2.process / SBR1.process (no PS): 2048-float channel buffers, first 1024 = core output */
 void orc_sbr_process(orc_sbr* s, float* left, float* right, int nch);
 /* SBR.downSampled (extension rate = core rate): 32-band synthesis, 1024 samples per channel */

@@ -1196,6 +1196,33 @@ static int ps_frame_valid(const jaad_ps_frame* p)
     return 1;
 }
 
+/* The header of a frame whose SBR data is invalid (JAAD_SBR_UPSAMPLE).  SBR.decode has read it into
+ * this.hdr and, if it differs, recomputed the frequency tables (A/sbr/SBR.java:168-177, readHeader
+ * :212-221) before sbr_data failed; the frame's SBR does not run, so patch_construction and
+ * limiter_frequency_table (HF generation, reset frames only: A/sbr/HFGeneration.java:27-28,95-97)
+ * keep their old results until a processed frame resets.  The library refuses the mixes where the
+ * reference would index outside its arrays or read stale values (jaad_sbr.h SbrHost::take_header);
+ * so does this restatement (JAAD_ERR_UNSUPPORTED). */
+int orc_sbr_take_header(orc_sbr* s, const jaad_sbr_header* h)
+{
+    if (!s->have_hdr) return JAAD_ERR_UNSUPPORTED;
+    const int differs = header_differs(h, &s->hdr);
+    const int M_old = s->M;
+    s->hdr_saved = s->hdr;
+    s->have_saved = s->have_hdr;
+    s->hdr = *h;
+    if (!differs) return JAAD_OK;
+    if (calc_sbr_tables(s)) return JAAD_ERR_UNSUPPORTED; /* the Java would revert the header */
+    int gen = 0, max_src = -1;
+    for (int i = 0; i < s->noPatches; i++) {
+        gen += s->patchNoSubbands[i];
+        if (s->patchNoSubbands[i] > 0 && s->patchStartSubband[i] + s->patchNoSubbands[i] - 1 > max_src)
+            max_src = s->patchStartSubband[i] + s->patchNoSubbands[i] - 1;
+    }
+    if (s->M != M_old || s->kx + gen > 64 || max_src >= s->kx) return JAAD_ERR_UNSUPPORTED;
+    return JAAD_OK;
+}
+
 int orc_sbr_decode(orc_sbr* s, const jaad_sbr_frame* fr, int nch)
 {
     if (fr->header_present) {
