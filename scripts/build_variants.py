@@ -6,9 +6,14 @@ ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 from jaadec_amd import build as B  # noqa: E402
 
+KSRC = ("jaad_lc.hip", "jaad_sbr.hip", "jaad_ps.hip")
+# name: (defines, extra flags, VOP3 rewrite forms per kernel source or None for the product's)
 VARIANTS = {
-    "c_head": ([], []),
-    "s_stamps": (["JAAD_STAMPS"], []),
+    "a_xvcc": (["JAAD_XCH_VCC"], [], None),
+    "b_head": ([], [], None),
+    "c_vop3": ([], [], {k: ("cndmask", "vopc") for k in KSRC}),
+    "d_vop3c": ([], [], {k: ("cndmask",) for k in KSRC}),
+    "s_stamps": (["JAAD_STAMPS"], [], None),
 }
 
 if __name__ == "__main__":
@@ -20,4 +25,5 @@ if __name__ == "__main__":
     from concurrent.futures import ThreadPoolExecutor
     todo = [(n, d) for n, d in VARIANTS.items() if not only or n in only]
     with ThreadPoolExecutor(6) as ex:
-        list(ex.map(lambda nd: B.build_gpu(out=out / f"lib_{nd[0]}.so", defines=nd[1][0], extra=nd[1][1]), todo))
+        list(ex.map(lambda nd: B.build_gpu(out=out / f"lib_{nd[0]}.so", defines=nd[1][0], extra=nd[1][1],
+                                           vop3=nd[1][2], force=True), todo))
