@@ -266,7 +266,8 @@ typedef struct jaad_batch {
     const jaad_ics_info* ics;     /* [dev] [ch-frame]                                              */
     const uint64_t* ms_used;      /* [dev] [frame][2] bit idx = g*max_sfb+sfb (CPE only, else NULL) */
     const jaad_tns* tns;          /* [dev] [ch-frame] or NULL when no ch-frame sets JAAD_ICS_TNS    */
-    const jaad_sbr_frame* sbr;    /* host [frame] when cfg.sbr, else NULL                            */
+    const jaad_sbr_frame* sbr;    /* host [frame] when cfg.sbr ([frame][channel element] for channel
+                                     configurations 3..7), else NULL                             */
     /* dependent coupling (jaad_cce_term above); all zero / NULL for a batch without CCEs.  AAC-LC
        configurations in JAAD_TNS_COMPAT mode only (JAAD_ERR_UNSUPPORTED otherwise). */
     uint32_t n_cce;               /* CCE records                                                    */

@@ -118,9 +118,12 @@ typedef struct jaad_frame_out {
     uint32_t n_cce, n_cce_terms; /* out */
 } jaad_frame_out;
 
-/* Parse one raw_data_block (SyntacticElements.decode) into *out.  On error nothing of the
- * parser's state (window shapes, PNS LCG, SBR/PS history) changes, so the caller may drop
- * the frame as Decoder.decodeFrame drops an EOS frame (A/Decoder.java:96-100). */
+/* Parse one raw_data_block (SyntacticElements.decode) into *out.  JAAD_ERR_EOS (the bitstream
+ * ended early: the reference's EOSException, which Decoder.decodeFrame swallows, dropping the
+ * frame, A/Decoder.java:96-100) leaves the state where the reference's reads left it: the window
+ * shape of every ICSInfo whose shape bit was read, the PNS LCG advanced over the noise bands
+ * decodeSpectralData reached, the SBR/PS state of payloads parsed whole (a payload cut short
+ * moves none).  Any other error changes nothing of the parser's state. */
 int jaad_parse_frame(jaad_parser* p, const uint8_t* data, size_t bytes, jaad_frame_out* out);
 
 /* Implicit SBR signalling (ADTS, LC-only AudioSpecificConfig): the reference opens SBR when it

@@ -1769,16 +1769,17 @@ struct Segments {
     std::vector<jaad_cce_term> terms;
 };
 
-// -1: no frame is dropped; else the number of dropped frames (JAAD_ERR_INVALID_ARG for a bad value)
+// the number of dropped frames (0: none, or no status array); JAAD_ERR_INVALID_ARG (< 0) for a
+// status value that is not a JAAD_FRAME_*
 int dropped_frames(const jaad_batch* b)
 {
-    if (!b->frame_status) return -1;
+    if (!b->frame_status) return 0;
     int n = 0;
     for (uint32_t f = 0; f < b->n_frames; f++) {
         if (b->frame_status[f] > JAAD_FRAME_EOS) return JAAD_ERR_INVALID_ARG;
         n += b->frame_status[f] != JAAD_FRAME_DECODE;
     }
-    return n ? n : -1;
+    return n;
 }
 
 // the sub-batch of frames [s, e) (none dropped); `seg` owns its run and term arrays
@@ -1804,7 +1805,7 @@ jaad_batch segment(const jaad_ctx* ctx, const jaad_batch* b, uint32_t s, uint32_
     d.ics = b->ics + (size_t)s * nch;
     d.ms_used = b->ms_used ? b->ms_used + (size_t)s * 2 * ctx->n_cpe : nullptr;
     d.tns = b->tns ? b->tns + (size_t)s * nch : nullptr;
-    d.sbr = b->sbr ? b->sbr + s : nullptr;
+    d.sbr = b->sbr ? b->sbr + (size_t)s * (ctx->cfg.sbr && ctx->n_elem > 1 ? ctx->n_elem : 1) : nullptr;  // [frame][element]
     d.frame_status = nullptr;
     seg.terms.clear();
     for (uint32_t t = 0; t < b->n_cce_terms; t++)
@@ -1851,8 +1852,8 @@ int jaad_decode_batch(jaad_ctx* ctx, const jaad_batch* b, void* pcm_out, size_t 
     if (rc) return rc;
     if (!pcm_out && b->n_frames) return JAAD_ERR_INVALID_ARG;
     const int dropped = dropped_frames(b);
-    if (dropped < -1) return dropped;
-    if (dropped < 0) {
+    if (dropped < 0) return dropped;
+    if (dropped == 0) {
         jaad_batch d = *b;
         d.frame_status = nullptr;
         return decode_batch_whole(ctx, &d, pcm_out, flags);
@@ -1963,8 +1964,8 @@ int jaad_decode_batch_device(jaad_ctx* ctx, const jaad_batch* b, void* pcm_dev, 
     HIPCHK(hipSetDevice(ctx->device));
     hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : ctx->stream;
     const int dropped = dropped_frames(b);
-    if (dropped < -1) return dropped;
-    if (dropped < 0) {
+    if (dropped < 0) return dropped;
+    if (dropped == 0) {
         jaad_batch d = *b;
         d.frame_status = nullptr;
         return launch(ctx, &d, pcm_dev, flags, s);

@@ -60,6 +60,7 @@ __device__ __forceinline__ void wave_sync()
     asm volatile("" ::: "memory");
 }
 
+#ifndef JAAD_LDS_COMPACT
 constexpr int kWaveBuf = 1152;  // floats of LDS per wave
 
 // spectrum layout in a wave's buffer: even bins at [0,576), odd bins at [576,1152), bin-pair
@@ -72,6 +73,11 @@ __device__ __forceinline__ int eo_idx(int p)
 }
 // IFFT transpose layout (complex index): one pad slot every 16 (<= 2-way conflicts, affine)
 __device__ __forceinline__ int xs(int i) { return i + (i >> 4); }
+#else  // experiment: unpadded 4 KiB buffers (16 waves per CU fit the LDS)
+constexpr int kWaveBuf = 1024;
+__device__ __forceinline__ int eo_idx(int p) { return (p & 1) * 512 + (p >> 1); }
+__device__ __forceinline__ int xs(int i) { return i; }
+#endif
 // long-window IFFT transpose layout: slot = sum of per-bit weights {1,2,4,8,16,33,72,138,276}
 // (550 slots).  Additive per bit, so the compile-time index bits of every access fold into the
 // instruction offset; the weights were searched (tools/lds_sim.py model of the gfx950 LDS
@@ -283,19 +289,17 @@ __device__ __forceinline__ void xch_hi(float& a, float& b)
 }
 // Lane bits 0..3 for two register pairs (a0, b0) and (a1, b1) at once:
 //   a' = bit clear ? a : b(partner),  b' = bit set ? b : a(partner).
-// VOP2 v_cndmask_b32 (its lane mask is the implicit VCC operand, DPP forms included) issues at
-// ~13.9 SIMD cycles per wave-instruction at 3 waves/SIMD on gfx950, against 3.3 for a DPP move and
-// 3.6 for the VOP3 v_cndmask_b32_e64 with an SGPR-pair mask (tools/valu_rate.hip,
-// profiles/round4_valu_rate.txt), so no exchange selects through VCC:
-// * lane bits 2, 3: DPP moves under a bank mask (bank = lane bits 3..2 of the 16-lane row) write
-//   only the lanes of one half: b' <- a(partner) in the bit-clear banks, a' <- b(partner) in the
-//   bit-set banks, from a copy of b (the first move overwrites b);
-// * lane bits 0, 1 (below the bank granularity): both partners' values by full DPP moves, then one
-//   v_cndmask_b32_e64 per output with the constant lane mask in an SGPR pair.
-// Swizzles: lane ^ 1, ^ 2 by quad_perm; ^ 8 by row_ror:8; ^ 4 by row_ror:4 (lanes with bit 2 set
-// read lane - 4) and row_ror:12 (bit 2 clear read lane + 4).  A DPP read of a VGPR that a VALU
-// instruction wrote needs 2 wait states: the copies (bits 2, 3) or an s_nop (bits 0, 1) give them.
-#ifndef JAAD_XCH_VCC
+// Each output is one VOP2 v_cndmask_b32_dpp: src0 read through the swizzle (quad_perm for lane
+// bits 0, 1; row_ror:4 / row_ror:12 for bit 2, row_ror:8 for bit 3), VCC = the lanes that keep
+// their own value, set by two s_mov_b32 of a literal (which also give the 2 wait states a DPP
+// read of a freshly written VGPR needs).  Round 4 measured the alternative without VCC (DPP
+// moves under bank masks for bits 2, 3; DPP moves + v_cndmask_b32_e64 on an SGPR-pair mask for
+// bits 0, 1; JAAD_XCH_NOVCC): an instruction micro-benchmark prices the VOP2 select at ~13.9
+// SIMD cycles against 3.3-3.6 for the other forms (tools/valu_rate.hip,
+// profiles/round4_valu_rate.txt), yet inside this kernel the VCC form is 1-2 % faster per C2
+// batch (same-call A/B over 30 launches, profiles/round4_xch_ab.txt) -- the exchanges are not
+// issue-bound here, and the VCC form needs fewer instructions and temporaries.
+#ifdef JAAD_XCH_NOVCC
 template <int L>
 __device__ __forceinline__ void xch2(f2& a0, f2& b0, f2& a1, f2& b1)
 {
@@ -353,7 +357,7 @@ __device__ __forceinline__ void xch2(f2& a0, f2& b0, f2& a1, f2& b1)
 #undef JAAD_XCH_QUAD
     }
 }
-#else  // round-3 form (VOP2 v_cndmask_b32_dpp through VCC), kept for A/B timing
+#else  // product form (VOP2 v_cndmask_b32_dpp through VCC)
 template <int L>
 __device__ __forceinline__ void xch2(f2& a0, f2& b0, f2& a1, f2& b1)
 {

@@ -3,8 +3,9 @@
 // Follows the reference's parse (A/ = aac/src/main/java/net/sourceforge/jaad/aac/), element by
 // element, with the same validity checks; where the reference would throw (AACException,
 // EOSException, or an ArrayIndexOutOfBounds its tables would raise) the frame is rejected
-// with JAAD_ERR_BITSTREAM / JAAD_ERR_EOS / JAAD_ERR_UNSUPPORTED and the parser's state is left
-// as it was.  SBR/PS extension payloads go to jaad_parse_sbr.cpp.
+// with JAAD_ERR_BITSTREAM / JAAD_ERR_EOS / JAAD_ERR_UNSUPPORTED.  The parser's state is left as
+// it was, except after JAAD_ERR_EOS, where it moves as far as the reference's reads got
+// (parse_frame).  SBR/PS extension payloads go to jaad_parse_sbr.cpp.
 #include "../../include/jaad_parse.h"
 
 #include <cmath>
@@ -106,17 +107,21 @@ struct IcsInfo {  // ICSInfo after decode / setCommonData
 };
 
 // ICSInfo.decode (A/syntax/ICSInfo.java:86-119); prediction data is not part of AAC LC
-// (readPredictionData throws for every other profile, :122-138)
-int read_ics_info(BitReader& br, const Cfg& C, IcsInfo& I)
+// (readPredictionData throws for every other profile, :122-138).  `shape_state` (the channel's
+// windowShape[CURRENT]) takes the new shape as soon as its bit is read, as the reference's field
+// does: a frame that ends later in its bitstream (EOSException) has moved it already (:90-91).
+int read_ics_info(BitReader& br, const Cfg& C, IcsInfo& I, int* shape_state)
 {
-    if (br.left() < 11) return JAAD_ERR_EOS;
+    if (br.left() < 4) return JAAD_ERR_EOS;
     br.skip(1);  // ics_reserved_bit
     I.seq = (int)br.read(2);
     I.shape = (int)br.read(1);
+    if (shape_state) *shape_state = I.shape;
     I.ngroups = 1;
     I.glen[0] = 1;
     I.grouping = 0;
     if (I.seq == JAAD_EIGHT_SHORT_SEQUENCE) {
+        if (br.left() < 11) return JAAD_ERR_EOS;
         I.max_sfb = (int)br.read(4);
         for (int i = 0; i < 7; i++) {
             if (br.read(1)) {
@@ -128,6 +133,7 @@ int read_ics_info(BitReader& br, const Cfg& C, IcsInfo& I)
         }
         if (I.max_sfb > C.nswb_s) return JAAD_ERR_BITSTREAM;
     } else {
+        if (br.left() < 6) return JAAD_ERR_EOS;
         I.max_sfb = (int)br.read(6);
         if (br.left() < 1) return JAAD_ERR_EOS;
         if (br.read(1)) return JAAD_ERR_UNSUPPORTED;  // predictor_data_present: AAC Main / LTP only
@@ -137,15 +143,21 @@ int read_ics_info(BitReader& br, const Cfg& C, IcsInfo& I)
 }
 
 // ICStream.decode (A/syntax/ICStream.java:60-111) of one channel into its records.
+// State moves as the reference's does while it reads, so that a frame whose bitstream ends early
+// (JAAD_ERR_EOS: the reference's EOSException, which Decoder.decodeFrame swallows) leaves what the
+// next frame sees: `shape_state` takes the window shape once its bit is read (non-common window),
+// and `pns` (the static randomState) has advanced over the noise bands decodeSpectralData
+// reached before the read that ran out (A/syntax/ICStream.java:222-275: bands in order, a noise
+// band consuming its LCG steps without reading bits).
 // `prev_shape` is ICSInfo.windowShape[CURRENT] of the previous frame of this channel.
-int read_ics(BitReader& br, const Cfg& C, bool common_window, IcsInfo& I, int prev_shape, uint32_t& pns,
-             ChOut& o)
+int read_ics(BitReader& br, const Cfg& C, bool common_window, IcsInfo& I, int prev_shape, int* shape_state,
+             uint32_t& pns, ChOut& o)
 {
     const Books& B = books();
     if (br.left() < 8) return JAAD_ERR_EOS;
     const int global_gain = (int)br.read(8);
     if (!common_window) {
-        const int st = read_ics_info(br, C, I);
+        const int st = read_ics_info(br, C, I, shape_state);
         if (st) return st;
     }
     const bool is_short = I.seq == JAAD_EIGHT_SHORT_SEQUENCE;
@@ -291,6 +303,13 @@ int read_ics(BitReader& br, const Cfg& C, bool common_window, IcsInfo& I, int pr
     int16_t q[1024];
     std::memset(q, 0, sizeof q);
     uint64_t noise_steps = 0;
+    auto lcg = [&]() {  // the static LCG advances once per noise bin (ICStream.java:247)
+        for (uint64_t i = 0; i < noise_steps; i++) pns = 1664525u * pns + 1013904223u;
+    };
+    auto eos = [&]() {  // the bands before this one are done, noise bands included
+        lcg();
+        return JAAD_ERR_EOS;
+    };
     for (int g = 0, idx = 0, group_off = 0; g < I.ngroups; g++) {
         const int gl = I.glen[g];
         for (int s = 0; s < max_sfb; s++, idx++) {
@@ -311,13 +330,13 @@ int read_ics(BitReader& br, const Cfg& C, bool common_window, IcsInfo& I, int pr
                 const int off = group_off + w * 128 + swb[s];
                 for (int k = 0; k < width; k += num) {
                     const int r = L.decode(br);
-                    if (r < 0) return r == -2 ? JAAD_ERR_EOS : JAAD_ERR_BITSTREAM;
+                    if (r < 0) return r == -2 ? eos() : JAAD_ERR_BITSTREAM;
                     int v[4];
                     for (int j = 0; j < num; j++) v[j] = rows[r * stride + 2 + j];
                     if (unsigned_cb)  // Huffman.signValues (:30-37)
                         for (int j = 0; j < num; j++)
                             if (v[j] != 0) {
-                                if (br.left() < 1) return JAAD_ERR_EOS;
+                                if (br.left() < 1) return eos();
                                 if (br.read(1)) v[j] = -v[j];
                             }
                     if (c == JAAD_ESCAPE_HCB)  // Huffman.getEscape (:39-50)
@@ -325,11 +344,11 @@ int read_ics(BitReader& br, const Cfg& C, bool common_window, IcsInfo& I, int pr
                             if (v[j] != 16 && v[j] != -16) continue;
                             int n = 4;
                             for (;;) {
-                                if (br.left() < 1) return JAAD_ERR_EOS;
+                                if (br.left() < 1) return eos();
                                 if (!br.read(1)) break;
                                 if (++n > 12) return JAAD_ERR_BITSTREAM;  // |q| > 8191: beyond IQ_TABLE
                             }
-                            if (br.left() < n) return JAAD_ERR_EOS;
+                            if (br.left() < n) return eos();
                             const int m = (int)br.read(n) | (1 << n);
                             v[j] = v[j] < 0 ? -m : m;
                         }
@@ -367,8 +386,7 @@ int read_ics(BitReader& br, const Cfg& C, bool common_window, IcsInfo& I, int pr
     ic.flags = (uint8_t)((has_pns ? JAAD_ICS_HAS_PNS : 0) | (has_is ? JAAD_ICS_HAS_IS : 0) |
                          (tns_present ? JAAD_ICS_TNS : 0) | (common_window ? JAAD_ICS_COMMON_WINDOW : 0));
     ic.pns_state = pns;
-    // the static LCG advances once per noise bin (ICStream.java:247)
-    for (uint64_t i = 0; i < noise_steps; i++) pns = 1664525u * pns + 1013904223u;
+    lcg();
     if (o.tns) *o.tns = tns;
     return JAAD_OK;
 }
@@ -736,7 +754,7 @@ int read_cce(BitReader& br, const Cfg& C, ParseState& ns, ChOut& o, CceElem& E)
     const bool sign = br.read(1) != 0;
     const double scale = kScale[br.read(2)];
     IcsInfo I;
-    int st = read_ics(br, C, false, I, 0, ns.pns, o);
+    int st = read_ics(br, C, false, I, 0, nullptr, ns.pns, o);
     if (st) return st;
     const Books& B = books();
     auto sfcode = [&](int& v) {  // Huffman.decodeScaleFactor
@@ -831,9 +849,12 @@ int cce_terms(const CceElem* cces, int n_cce, const ChElem* els, int n_el, jaad_
 // 14496-3 Table 1.19; configuration 4 ends with a back SCE)
 bool mc_lfe(const Cfg& C, int e) { return (C.cfg.channel_config == 6 || C.cfg.channel_config == 7) && e == C.n_elem - 1; }
 
-// probe != nullptr: stop at the first SBR extension payload after the channel element
-// (bit 0 of *probe) and commit nothing
-int parse_frame(jaad_parser* p, const uint8_t* data, size_t bytes, jaad_frame_out* out, uint32_t* probe)
+// One raw_data_block into `out`, moving the parse state ns / nsel (multichannel HE-AAC: SBR
+// state of elements 1..) as the reference moves its fields; parse_frame commits them.
+// probe != nullptr: stop at the first SBR extension payload after the channel element (bit 0 of
+// *probe).
+int parse_frame_body(const jaad_parser* p, const uint8_t* data, size_t bytes, jaad_frame_out* out, uint32_t* probe,
+                     ParseState& ns, std::vector<SbrParseState>& nsel)
 {
     if (!p || !out || (!data && bytes) || !out->q || !out->sf || !out->cb || !out->ics) return JAAD_ERR_INVALID_ARG;
     const Cfg& C = p->C;
@@ -842,9 +863,6 @@ int parse_frame(jaad_parser* p, const uint8_t* data, size_t bytes, jaad_frame_ou
     if (n_cpe && !out->ms_used) return JAAD_ERR_INVALID_ARG;
     if (C.cfg.sbr && !out->sbr) return JAAD_ERR_INVALID_ARG;
     BitReader br(data, bytes);
-    ParseState ns = p->st;  // committed only when the whole frame parsed
-    std::vector<SbrParseState> nsel;  // multichannel HE-AAC: elements 1.. (committed with ns)
-    if (!p->sbr_el.empty()) nsel = p->sbr_el;
     bool have_channels = false;
     int elem = 0, ch0 = 0, cpe = 0;  // channel elements parsed so far, their channels, CPEs
     // SBR records: one per channel element (multichannel: out->sbr[0 .. n_elem), element order)
@@ -886,7 +904,9 @@ int parse_frame(jaad_parser* p, const uint8_t* data, size_t bytes, jaad_frame_ou
                 const int e = elem - 1;
                 if (C.n_elem > 1 && mc_lfe(C, e)) return JAAD_ERR_UNSUPPORTED;
                 SbrParseState& S = e == 0 ? ns.sbr : nsel[(size_t)e - 1];
+                const SbrParseState before = S;
                 const int st = parse_sbr(sub, C, C.elem_nch[e], type == 14, S, out->sbr[e]);
+                if (st == JAAD_ERR_EOS) S = before;  // a payload cut short moves no SBR state
                 if (st) return st;
                 sbr_seen |= 1u << e;
             }
@@ -927,9 +947,8 @@ int parse_frame(jaad_parser* p, const uint8_t* data, size_t bytes, jaad_frame_ou
             IcsInfo I;
             ChOut o{out->q + (size_t)ch0 * 1024, out->sf + ch0 * 128, out->cb + ch0 * 128, out->ics + ch0,
                     out->tns ? out->tns + ch0 : nullptr};
-            const int st = read_ics(br, C, false, I, ns.shape[ch0], ns.pns, o);
+            const int st = read_ics(br, C, false, I, ns.shape[ch0], &ns.shape[ch0], ns.pns, o);
             if (st) return st;
-            ns.shape[ch0] = I.shape;
         } else {
             // CPE.decode (A/syntax/CPE.java:85-123)
             if (br.left() < 1) return JAAD_ERR_EOS;
@@ -937,10 +956,12 @@ int parse_frame(jaad_parser* p, const uint8_t* data, size_t bytes, jaad_frame_ou
             IcsInfo IL, IR;
             uint64_t ms[2] = {0, 0};
             bool ms_present = false;
+            const int prevL = ns.shape[ch0], prevR = ns.shape[ch0 + 1];
             if (common) {
-                int st = read_ics_info(br, C, IL);
+                int st = read_ics_info(br, C, IL, &ns.shape[ch0]);
                 if (st) return st;
-                IR = IL;  // ICSInfo.setCommonData
+                IR = IL;  // ICSInfo.setCommonData, right after infoL.decode (A/syntax/CPE.java:93-94)
+                ns.shape[ch0 + 1] = IR.shape;
                 if (br.left() < 2) return JAAD_ERR_EOS;
                 const int mask = (int)br.read(2);
                 const int nb = IL.ngroups * IL.max_sfb;
@@ -959,12 +980,10 @@ int parse_frame(jaad_parser* p, const uint8_t* data, size_t bytes, jaad_frame_ou
                      out->tns ? out->tns + ch0 : nullptr};
             ChOut oR{out->q + (size_t)(ch0 + 1) * 1024, out->sf + (ch0 + 1) * 128, out->cb + (ch0 + 1) * 128,
                      out->ics + ch0 + 1, out->tns ? out->tns + ch0 + 1 : nullptr};
-            int st = read_ics(br, C, common, IL, ns.shape[ch0], ns.pns, oL);
+            int st = read_ics(br, C, common, IL, prevL, &ns.shape[ch0], ns.pns, oL);
             if (st) return st;
-            st = read_ics(br, C, common, IR, ns.shape[ch0 + 1], ns.pns, oR);
+            st = read_ics(br, C, common, IR, prevR, &ns.shape[ch0 + 1], ns.pns, oR);
             if (st) return st;
-            ns.shape[ch0] = IL.shape;
-            ns.shape[ch0 + 1] = IR.shape;
             if (ms_present) out->ics[ch0].flags |= JAAD_ICS_MS_PRESENT;
             out->ms_used[2 * cpe] = ms[0];
             out->ms_used[2 * cpe + 1] = ms[1];
@@ -990,11 +1009,24 @@ int parse_frame(jaad_parser* p, const uint8_t* data, size_t bytes, jaad_frame_ou
         if (st) return st;
         out->n_cce = (uint32_t)n_cce;
     }
-    if (!probe) {
-        p->st = ns;
-        if (!nsel.empty()) p->sbr_el.swap(nsel);
-    }
     return JAAD_OK;
+}
+
+// The state moves with a frame that parsed, and with one whose bitstream ended early as far as the
+// reference's reads got before its EOSException (Decoder.decodeFrame drops that frame and the next
+// one sees those fields: A/Decoder.java:89-101).  Any other error leaves the parser as it was (the
+// reference throws an AACException out of decodeFrame; this decoder rejects the frame whole).
+int parse_frame(jaad_parser* p, const uint8_t* data, size_t bytes, jaad_frame_out* out, uint32_t* probe)
+{
+    if (!p) return JAAD_ERR_INVALID_ARG;
+    ParseState ns = p->st;
+    std::vector<SbrParseState> nsel = p->sbr_el;
+    const int st = parse_frame_body(p, data, bytes, out, probe, ns, nsel);
+    if (!probe && (st == JAAD_OK || st == JAAD_ERR_EOS)) {
+        p->st = ns;
+        p->sbr_el.swap(nsel);
+    }
+    return st;
 }
 }  // namespace
 

@@ -673,7 +673,8 @@ class Parser:
         drop_eos: a frame whose bitstream ends early (JAAD_ERR_EOS) is marked FRAME_EOS in
         batch.frame_status -- the decode then drops it as Decoder.decodeFrame drops a frame that
         throws EOSException (A/Decoder.java:89-101) -- and parsing goes on with the next frame
-        (the parser is atomic: the failed frame left its state as it was).  Without it the
+        (from the state the truncated frame left: window shapes and the PNS LCG moved as far as
+        the reference's reads got before its EOSException, jaad_parse.h).  Without it the
         JaadError propagates."""
         nf, nch, ncpe = len(frames), self.nch, n_cpe(self.cfg)
         status = None

@@ -9,11 +9,13 @@ from jaadec_amd import build as B  # noqa: E402
 KSRC = ("jaad_lc.hip", "jaad_sbr.hip", "jaad_ps.hip")
 # name: (defines, extra flags, VOP3 rewrite forms per kernel source or None for the product's)
 VARIANTS = {
-    "a_xvcc": (["JAAD_XCH_VCC"], [], None),
+    "a_novcc": (["JAAD_XCH_NOVCC"], [], None),
     "b_head": ([], [], None),
     "c_vop3": ([], [], {k: ("cndmask", "vopc") for k in KSRC}),
     "d_vop3c": ([], [], {k: ("cndmask",) for k in KSRC}),
     "s_stamps": (["JAAD_STAMPS"], [], None),
+    "e_w16c": (["JAAD_LDS_COMPACT", "JAAD_LC_WAVES=16"], [], None),
+    "f_w12c": (["JAAD_LDS_COMPACT"], [], None),
 }
 
 if __name__ == "__main__":

@@ -68,31 +68,95 @@ def test_oracle_status_equals_the_batch_without_the_frames():
     assert (got[st == 0] == want).all()
 
 
-def test_parser_marks_a_truncated_frame_and_goes_on():
-    p = N.synth_params(3, n_streams=1, frames_per_stream=10, pns_percent=10)
+LCG_A, LCG_C = 1664525, 1013904223  # ICStream.randomState (A/syntax/ICStream.java:247)
+
+
+def noise_prefix(b: N.Batch, f: int) -> list:
+    """Noise bins that decodeSpectralData has consumed at each band boundary of frame f, channels in
+    bitstream order (A/syntax/ICStream.java:222-275: groups, bands, windows; a noise band takes
+    width x group-length LCG steps)."""
+    from test_tables import table
+    swl = table("JAAD_SWB_OFFSET_1024_48").astype(int)
+    sws = table("JAAD_SWB_OFFSET_128_48").astype(int)
+    out, n = [0], 0
+    for c in range(b.nch):
+        ic = b.ics[f * b.nch + c]
+        short = int(ic["window_sequence"]) == 2
+        glen = [1]
+        if short:
+            for i in range(7):
+                if (int(ic["grouping"]) >> i) & 1:
+                    glen[-1] += 1
+                else:
+                    glen.append(1)
+        sw, msfb = (sws if short else swl), int(ic["max_sfb"])
+        cb = b.cb[f * b.nch + c]
+        for g, gl in enumerate(glen):
+            for s in range(msfb):
+                if cb[g * msfb + s] == 13:
+                    n += gl * int(sw[s + 1] - sw[s])
+                out.append(n)
+    return out
+
+
+def test_parser_truncated_frame_moves_state_as_far_as_the_reference_read():
+    """A frame cut short anywhere: it is marked FRAME_EOS, the next frame parses to the same records,
+    and the state that frame sees is the reference's after its EOSException -- every window shape
+    whose bit was read (A/syntax/ICSInfo.java:90-91, CPE setCommonData :193-197) and the static PNS
+    LCG advanced over the noise bands decodeSpectralData reached (A/syntax/ICStream.java:222-275):
+    for every cut length, the next frame's first pns_state is the start state advanced by one of
+    the frame's band-boundary noise prefix sums, never decreasing with the cut length; a shape
+    switches from the previous frame's to this frame's once and stays."""
+    p = N.synth_params(3, n_streams=1, frames_per_stream=8, pns_percent=35, sf_index=3)
     b = N.synth_batch(p)
     frames = O.write_frames(b, p.sf_index)
-    k = 4
-    bad = list(frames)
-    bad[k] = frames[k][:len(frames[k]) // 3]
-    P = N.Parser(N.make_cfg(sf_index=p.sf_index))
+    cfg = N.make_cfg(sf_index=p.sf_index)
+    k = next(f for f in range(2, 7) if noise_prefix(b, f)[-1] > 0 and
+             (b.ics["window_shape"][2 * f:2 * f + 2] != b.ics["window_shape"][2 * f - 2:2 * f]).any())
+    prefix = noise_prefix(b, k)
+    s0 = int(b.ics["pns_state"][2 * k])
+    states = {}
+    x = s0
+    for n in range(prefix[-1] + 1):
+        states.setdefault(x, n)
+        if n < prefix[-1]:
+            x = (LCG_A * x + LCG_C) & 0xFFFFFFFF
+    assert int(b.ics["pns_state"][2 * k + 2]) == x  # the synthetic chain: frame k consumed whole
+    full = N.Parser(cfg)
+    full.pns_state = int(b.ics["pns_state"][0])
+    ref = full.parse(frames[:k + 2])
+    last_n, switched, seen = 0, [False, False], set()
+    for cut in range(1, len(frames[k])):
+        P = N.Parser(cfg)
+        P.pns_state = int(b.ics["pns_state"][0])
+        got = P.parse(frames[:k] + [frames[k][:cut], frames[k + 1]], drop_eos=True)
+        assert np.flatnonzero(got.frame_status).tolist() == [k], cut
+        assert not got.q[2 * k:2 * k + 2].any()
+        for f in ("q", "sf", "cb"):
+            assert (getattr(got, f)[2 * k + 2:] == getattr(ref, f)[2 * k + 2:]).all(), (cut, f)
+        st = int(got.ics["pns_state"][2 * k + 2])
+        assert st in states and states[st] in prefix, (cut, st)
+        assert states[st] >= last_n, cut
+        last_n = states[st]
+        seen.add(last_n)
+        for c in range(2):
+            sp = int(got.ics["window_shape_prev"][2 * k + 2 + c])
+            old, new = int(b.ics["window_shape"][2 * k - 2 + c]), int(b.ics["window_shape"][2 * k + c])
+            assert sp in (old, new), (cut, c)
+            if old != new:
+                if switched[c]:
+                    assert sp == new, (cut, c)
+                switched[c] = sp == new
+    assert len(seen) > 2, "no cut ended between noise bands"
+    # a one-byte frame ends before any ICSInfo: nothing moved
+    P = N.Parser(cfg)
     P.pns_state = int(b.ics["pns_state"][0])
-    with pytest.raises(N.JaadError) as e:
-        P.parse(bad)
-    assert e.value.status == N.ERR_EOS
-    P = N.Parser(N.make_cfg(sf_index=p.sf_index))
-    P.pns_state = int(b.ics["pns_state"][0])
-    got = P.parse(bad, drop_eos=True)
-    assert got.frame_status is not None and np.flatnonzero(got.frame_status).tolist() == [k]
-    assert not got.q[2 * k:2 * k + 2].any() and not got.ics[2 * k:2 * k + 2]["max_sfb"].any()
-    # the frames after it parse exactly as frames after an absent frame: the PNS LCG did not move
-    Q = N.Parser(N.make_cfg(sf_index=p.sf_index))
-    Q.pns_state = int(b.ics["pns_state"][0])
-    ref = Q.parse(frames[:k] + frames[k + 1:])
-    keep = np.r_[0:2 * k, 2 * k + 2:2 * len(frames)]
-    for f in ("q", "sf", "cb"):
-        assert (getattr(got, f)[keep] == getattr(ref, f)).all(), f
-    assert (got.ics[keep]["pns_state"] == ref.ics["pns_state"]).all()
+    got = P.parse(frames[:k] + [frames[k][:1], frames[k + 1]], drop_eos=True)
+    assert int(got.ics["pns_state"][2 * k + 2]) == s0
+    assert (got.ics["window_shape_prev"][2 * k + 2:2 * k + 4] == b.ics["window_shape"][2 * k - 2:2 * k]).all()
+    # the last cut before the full frame has read every band
+    assert last_n == prefix[-1] and all(switched[c] or b.ics["window_shape"][2 * k - 2 + c] == b.ics["window_shape"][2 * k + c]
+                                        for c in range(2))
 
 
 # ------------------------------------------------------------------------------------------------
@@ -216,10 +280,14 @@ def test_decode_frames_drops_a_truncated_frame_per_frame():
     k = 17
     bad = list(frames)
     bad[k] = frames[k][:len(frames[k]) // 2]
-    st = np.zeros(40, np.uint8)
-    st[k] = N.FRAME_EOS
-    b.frame_status = st
-    want = oracle_pcm(N.make_cfg(sf_index=p.sf_index), b, N.PCM_BIG_ENDIAN)
+    # the records and the state the frames after k see (the parser moves the window shapes and
+    # the PNS LCG as far as the reference's reads got: test_parser_truncated_frame_moves_state_...)
+    P = N.Parser(N.make_cfg(sf_index=p.sf_index))
+    P.pns_state = int(b.ics["pns_state"][0])
+    pb = P.parse(bad, drop_eos=True)
+    P.close()
+    assert np.flatnonzero(pb.frame_status).tolist() == [k]
+    want = oracle_pcm(N.make_cfg(sf_index=p.sf_index), pb, N.PCM_BIG_ENDIAN)
     dec = Decoder.create(bytes([0x11, 0x90]))
     dec._parse([])
     dec._parser.pns_state = int(b.ics["pns_state"][0])

@@ -83,8 +83,11 @@ def test_adts_split_and_parse():
 
 
 def test_errors_leave_the_parser_state_untouched():
-    """A failed frame (EOSException / AACException in the reference) changes nothing: the next
-    good frame parses exactly as if the bad one had never been offered (A/Decoder.java:96-100)."""
+    """A frame that fails with an AACException in the reference (a bitstream error) changes
+    nothing: the next good frame parses exactly as if the bad one had never been offered.  A frame
+    whose bitstream ends early (EOSException, swallowed by Decoder.decodeFrame, A/Decoder.java:96-100)
+    moves the state as far as the reference's reads got (tests/test_frame_status.py); restoring a
+    snapshot taken before it undoes that."""
     p = N.synth_params(1, n_streams=1, frames_per_stream=12, window_switching=1, pns_percent=10)
     b = N.synth_batch(p)
     frames = O.write_frames(b, p.sf_index)
@@ -95,16 +98,27 @@ def test_errors_leave_the_parser_state_untouched():
     for i, fr in enumerate(frames):
         if i == 5:
             st = P.pns_state
+            snap = P.snapshot()
             with pytest.raises(N.JaadError) as e:
                 P.parse([fr[: len(fr) // 2]])
             assert e.value.status == N.ERR_EOS
+            P.restore(snap)
             assert P.pns_state == st
             bad = bytearray(fr)
             bad[0] = (bad[0] & 0x1F) | 0x40  # element id SCE -> CCE: its bits do not parse as one
             with pytest.raises(N.JaadError) as e:
                 P.parse([bytes(bad)])
             assert e.value.status in (N.ERR_BITSTREAM, N.ERR_EOS, N.ERR_UNSUPPORTED)
+            if e.value.status == N.ERR_EOS:
+                P.restore(snap)
             assert P.pns_state == st
+            bad = bytearray(fr)
+            bad[0] = (bad[0] & 0x1F) | 0x20  # element id SCE -> CPE: refused by a mono configuration
+            with pytest.raises(N.JaadError) as e:
+                P.parse([bytes(bad)])
+            assert e.value.status == N.ERR_UNSUPPORTED
+            assert P.pns_state == st
+            snap.close()
         out.append(P.parse([fr]))
     for i, g in enumerate(out):
         w = b.select_runs([0])
