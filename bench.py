@@ -77,6 +77,9 @@ def parse(argv=None):
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-buffer (PCIe-inclusive) leg")
     ap.add_argument("--cpu-streams", type=int, default=256, help="streams in the CPU baseline sample")
+    ap.add_argument("--settle", type=float, default=0.25,
+                    help="seconds of untimed back-to-back steps before the warmup: the GPU's power management "
+                         "takes ~60 ms of continuous load to leave its load-onset transient (DESIGN.md 5)")
     # diagnostics / CPU tests only: a smaller job than the config's (the line's config says so)
     ap.add_argument("--streams-per-gpu", type=int, default=0)
     ap.add_argument("--frames-per-stream", type=int, default=0)
@@ -239,6 +242,23 @@ def run(args, engine_cls=HipEngine, backend: str = "nccl"):
         parity = {"frames_checked": int(want.shape[0]), "max_abs_lsb": int(d.max()),
                   "samples_off_by_1": int((d == 1).sum())}
 
+    # ---- load onset: the first steps after the GPU idled (here: while the CPU checked the parity
+    # sample) run in the power manager's transient -- reported beside, never as value
+    cold = None
+    if args.settle > 0 and args.steps:
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            eng.step()
+        eng.sync()
+        cold = (time.perf_counter() - t1) / args.steps * 1e3
+    # ---- settle: untimed back-to-back steps until the clock has left that transient
+    n_settle, t_settle = 0, time.perf_counter()
+    while time.perf_counter() - t_settle < args.settle:
+        for _ in range(10):
+            eng.step()
+        eng.sync()
+        n_settle += 10
+    t_settle = time.perf_counter() - t_settle
     for _ in range(max(0, args.warmup - 1)):
         eng.step()
     eng.sync()
@@ -323,6 +343,10 @@ def run(args, engine_cls=HipEngine, backend: str = "nccl"):
                        "parallelism": f"stream-sharded x{world} (no collectives)", "pcm": "int16 big-endian",
                        "samples_per_frame": 2048 if sbr else 1024},
             "roofline": roofline(args.config, n_frames, kern_ms, achieved, traffic, traffic_src),
+            "settle": {"steps": n_settle, "seconds": round(t_settle, 3),
+                       "cold_ms_per_step": round(cold, 4) if cold is not None else None,
+                       "note": "untimed steps before the warmup; cold_ms_per_step = the first K steps after "
+                               "the GPU idled (load-onset clock transient), beside the timed steady state"},
             "cpu_baseline": cpu,
             "parity_sample": parity,
             "e2e_pcie_frames_per_s": round(e2e["registered"], 1) if e2e else None,

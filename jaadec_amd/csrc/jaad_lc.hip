@@ -176,7 +176,7 @@ struct Ics {
 };
 // The fields are clamped to what the kernel can index safely: jaad_decode_batch rejects out-of-
 // range side info on the host, jaad_decode_batch_device does not look at it (jaad_gpu.h).
-__device__ __forceinline__ Ics ics_from_lanes(uint32_t side, int base, const LdsTables& T)
+__device__ __forceinline__ Ics ics_from_lanes(uint32_t side, int base, int nswb_l, int nswb_s)
 {
     const uint32_t a = __builtin_amdgcn_readlane(side, base);
     const uint32_t b = __builtin_amdgcn_readlane(side, base + 1);
@@ -184,7 +184,7 @@ __device__ __forceinline__ Ics ics_from_lanes(uint32_t side, int base, const Lds
     r.seq = a & 3;
     r.shape = (a >> 8) & 1;
     r.shape_prev = (a >> 16) & 1;
-    const int lim = r.seq == JAAD_EIGHT_SHORT_SEQUENCE ? T.nswb_s : T.nswb_l;
+    const int lim = r.seq == JAAD_EIGHT_SHORT_SEQUENCE ? nswb_s : nswb_l;
     r.max_sfb = min((int)(a >> 24), lim);
     r.grouping = b & 0xff;
     r.flags = (b >> 8) & 0xff;
@@ -395,6 +395,95 @@ __device__ __forceinline__ void xch2(f2& a0, f2& b0, f2& a1, f2& b1)
 }
 #endif
 
+// Lane bits 0..3 for 16 register pairs at once (both channels of the lockstep long IMDCT): the
+// same selects as xch2, with VCC set twice per 32 selects instead of twice per 8.
+//   a'[i] = bit clear ? a[i] : b[i](partner),  b'[i] = bit set ? b[i] : a[i](partner).
+template <int L>
+__device__ __forceinline__ void xch16(float (&a)[16], float (&b)[16])
+{
+    constexpr uint32_t kHi = L == 0 ? 0xAAAAAAAAu : L == 1 ? 0xCCCCCCCCu : L == 2 ? 0xF0F0F0F0u : 0xFF00FF00u;
+    float na[16], nb[16];
+#define JAAD_X16(QA, QB) \
+    asm("s_mov_b32 vcc_lo, %[lo]\n\t" \
+        "s_mov_b32 vcc_hi, %[lo]\n\t" \
+        "v_cndmask_b32_dpp %[na0], %[b0], %[a0], vcc " QA " row_mask:0xf bank_mask:0xf\n\t" \
+        "v_cndmask_b32_dpp %[na1], %[b1], %[a1], vcc " QA " row_mask:0xf bank_mask:0xf\n\t" \
+        "v_cndmask_b32_dpp %[na2], %[b2], %[a2], vcc " QA " row_mask:0xf bank_mask:0xf\n\t" \
+        "v_cndmask_b32_dpp %[na3], %[b3], %[a3], vcc " QA " row_mask:0xf bank_mask:0xf\n\t" \
+        "v_cndmask_b32_dpp %[na4], %[b4], %[a4], vcc " QA " row_mask:0xf bank_mask:0xf\n\t" \
+        "v_cndmask_b32_dpp %[na5], %[b5], %[a5], vcc " QA " row_mask:0xf bank_mask:0xf\n\t" \
+        "v_cndmask_b32_dpp %[na6], %[b6], %[a6], vcc " QA " row_mask:0xf bank_mask:0xf\n\t" \
+        "v_cndmask_b32_dpp %[na7], %[b7], %[a7], vcc " QA " row_mask:0xf bank_mask:0xf\n\t" \
+        "v_cndmask_b32_dpp %[na8], %[b8], %[a8], vcc " QA " row_mask:0xf bank_mask:0xf\n\t" \
+        "v_cndmask_b32_dpp %[na9], %[b9], %[a9], vcc " QA " row_mask:0xf bank_mask:0xf\n\t" \
+        "v_cndmask_b32_dpp %[na10], %[b10], %[a10], vcc " QA " row_mask:0xf bank_mask:0xf\n\t" \
+        "v_cndmask_b32_dpp %[na11], %[b11], %[a11], vcc " QA " row_mask:0xf bank_mask:0xf\n\t" \
+        "v_cndmask_b32_dpp %[na12], %[b12], %[a12], vcc " QA " row_mask:0xf bank_mask:0xf\n\t" \
+        "v_cndmask_b32_dpp %[na13], %[b13], %[a13], vcc " QA " row_mask:0xf bank_mask:0xf\n\t" \
+        "v_cndmask_b32_dpp %[na14], %[b14], %[a14], vcc " QA " row_mask:0xf bank_mask:0xf\n\t" \
+        "v_cndmask_b32_dpp %[na15], %[b15], %[a15], vcc " QA " row_mask:0xf bank_mask:0xf\n\t" \
+        "s_mov_b32 vcc_lo, %[hi]\n\t" \
+        "s_mov_b32 vcc_hi, %[hi]\n\t" \
+        "v_cndmask_b32_dpp %[nb0], %[a0], %[b0], vcc " QB " row_mask:0xf bank_mask:0xf\n\t" \
+        "v_cndmask_b32_dpp %[nb1], %[a1], %[b1], vcc " QB " row_mask:0xf bank_mask:0xf\n\t" \
+        "v_cndmask_b32_dpp %[nb2], %[a2], %[b2], vcc " QB " row_mask:0xf bank_mask:0xf\n\t" \
+        "v_cndmask_b32_dpp %[nb3], %[a3], %[b3], vcc " QB " row_mask:0xf bank_mask:0xf\n\t" \
+        "v_cndmask_b32_dpp %[nb4], %[a4], %[b4], vcc " QB " row_mask:0xf bank_mask:0xf\n\t" \
+        "v_cndmask_b32_dpp %[nb5], %[a5], %[b5], vcc " QB " row_mask:0xf bank_mask:0xf\n\t" \
+        "v_cndmask_b32_dpp %[nb6], %[a6], %[b6], vcc " QB " row_mask:0xf bank_mask:0xf\n\t" \
+        "v_cndmask_b32_dpp %[nb7], %[a7], %[b7], vcc " QB " row_mask:0xf bank_mask:0xf\n\t" \
+        "v_cndmask_b32_dpp %[nb8], %[a8], %[b8], vcc " QB " row_mask:0xf bank_mask:0xf\n\t" \
+        "v_cndmask_b32_dpp %[nb9], %[a9], %[b9], vcc " QB " row_mask:0xf bank_mask:0xf\n\t" \
+        "v_cndmask_b32_dpp %[nb10], %[a10], %[b10], vcc " QB " row_mask:0xf bank_mask:0xf\n\t" \
+        "v_cndmask_b32_dpp %[nb11], %[a11], %[b11], vcc " QB " row_mask:0xf bank_mask:0xf\n\t" \
+        "v_cndmask_b32_dpp %[nb12], %[a12], %[b12], vcc " QB " row_mask:0xf bank_mask:0xf\n\t" \
+        "v_cndmask_b32_dpp %[nb13], %[a13], %[b13], vcc " QB " row_mask:0xf bank_mask:0xf\n\t" \
+        "v_cndmask_b32_dpp %[nb14], %[a14], %[b14], vcc " QB " row_mask:0xf bank_mask:0xf\n\t" \
+        "v_cndmask_b32_dpp %[nb15], %[a15], %[b15], vcc " QB " row_mask:0xf bank_mask:0xf" \
+        : [na0] "=&v"(na[0]), [na1] "=&v"(na[1]), [na2] "=&v"(na[2]), [na3] "=&v"(na[3]), [na4] "=&v"(na[4]), [na5] "=&v"(na[5]), [na6] "=&v"(na[6]), [na7] "=&v"(na[7]), [na8] "=&v"(na[8]), [na9] "=&v"(na[9]), [na10] "=&v"(na[10]), [na11] "=&v"(na[11]), [na12] "=&v"(na[12]), [na13] "=&v"(na[13]), [na14] "=&v"(na[14]), [na15] "=&v"(na[15]), [nb0] "=&v"(nb[0]), [nb1] "=&v"(nb[1]), [nb2] "=&v"(nb[2]), [nb3] "=&v"(nb[3]), [nb4] "=&v"(nb[4]), [nb5] "=&v"(nb[5]), [nb6] "=&v"(nb[6]), [nb7] "=&v"(nb[7]), [nb8] "=&v"(nb[8]), [nb9] "=&v"(nb[9]), [nb10] "=&v"(nb[10]), [nb11] "=&v"(nb[11]), [nb12] "=&v"(nb[12]), [nb13] "=&v"(nb[13]), [nb14] "=&v"(nb[14]), [nb15] "=&v"(nb[15]) \
+        : [a0] "v"(a[0]), [a1] "v"(a[1]), [a2] "v"(a[2]), [a3] "v"(a[3]), [a4] "v"(a[4]), [a5] "v"(a[5]), [a6] "v"(a[6]), [a7] "v"(a[7]), [a8] "v"(a[8]), [a9] "v"(a[9]), [a10] "v"(a[10]), [a11] "v"(a[11]), [a12] "v"(a[12]), [a13] "v"(a[13]), [a14] "v"(a[14]), [a15] "v"(a[15]), [b0] "v"(b[0]), [b1] "v"(b[1]), [b2] "v"(b[2]), [b3] "v"(b[3]), [b4] "v"(b[4]), [b5] "v"(b[5]), [b6] "v"(b[6]), [b7] "v"(b[7]), [b8] "v"(b[8]), [b9] "v"(b[9]), [b10] "v"(b[10]), [b11] "v"(b[11]), [b12] "v"(b[12]), [b13] "v"(b[13]), [b14] "v"(b[14]), [b15] "v"(b[15]), [lo] "i"(~kHi), [hi] "i"(kHi) \
+        : "vcc")
+    if constexpr (L == 0) JAAD_X16("quad_perm:[1,0,3,2]", "quad_perm:[1,0,3,2]");
+    else if constexpr (L == 1) JAAD_X16("quad_perm:[2,3,0,1]", "quad_perm:[2,3,0,1]");
+    else if constexpr (L == 2) JAAD_X16("row_ror:4", "row_ror:12");
+    else JAAD_X16("row_ror:8", "row_ror:8");
+#undef JAAD_X16
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+        a[i] = na[i];
+        b[i] = nb[i];
+    }
+}
+
+// register bit I <-> lane bit L (<= 3) for both channels of the lockstep long IMDCT
+template <int I, int L>
+__device__ __forceinline__ void xch_bit_pair(f2 (&c0)[8], f2 (&c1)[8])
+{
+    static_assert(L <= 3, "lane bits 4, 5 go through xch_hi");
+    constexpr int m = 1 << I;
+    auto clr = [](int k) { return ((k >> I) << (I + 1)) | (k & (m - 1)); };
+    float a[16], b[16];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        a[4 * k + 0] = c0[clr(k)].x;
+        a[4 * k + 1] = c0[clr(k)].y;
+        a[4 * k + 2] = c1[clr(k)].x;
+        a[4 * k + 3] = c1[clr(k)].y;
+        b[4 * k + 0] = c0[clr(k) | m].x;
+        b[4 * k + 1] = c0[clr(k) | m].y;
+        b[4 * k + 2] = c1[clr(k) | m].x;
+        b[4 * k + 3] = c1[clr(k) | m].y;
+    }
+    xch16<L>(a, b);
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        c0[clr(k)] = f2{a[4 * k + 0], a[4 * k + 1]};
+        c1[clr(k)] = f2{a[4 * k + 2], a[4 * k + 3]};
+        c0[clr(k) | m] = f2{b[4 * k + 0], b[4 * k + 1]};
+        c1[clr(k) | m] = f2{b[4 * k + 2], b[4 * k + 3]};
+    }
+}
+
 // register bit I <-> lane bit L for all four register pairs, both floats of each complex value
 template <int I, int L>
 __device__ __forceinline__ void xch_bit(f2 (&c)[8], int u)
@@ -449,17 +538,34 @@ __device__ __forceinline__ void imdct_long_pk(float* const (&bufs)[N], const Lds
     for (int n = 0; n < N; n++) {
         xch_bit<0, 5>(c[n], u);  // e bit 3 (lane bit 5) <-> e bit 2
         xch_bit<1, 4>(c[n], u);  // e bit 4 (lane bit 4) <-> e bit 1
-        xch_bit<2, 3>(c[n], u);  // e bit 5 (lane bit 3) <-> e bit 0
+        if constexpr (N == 1) xch_bit<2, 3>(c[n], u);  // e bit 5 (lane bit 3) <-> e bit 0
     }
+#ifndef JAAD_XCH_NOVCC
+    if constexpr (N == 2) xch_bit_pair<2, 3>(c[0], c[1]);
+#else
+    if constexpr (N == 2) {
+        xch_bit<2, 3>(c[0], u);
+        xch_bit<2, 3>(c[1], u);
+    }
+#endif
     // pass 2: register bits 0,1,2 = e bits 3,4,5; e mod 8 = u >> 3
     const int b = u >> 3;
 #pragma unroll
     for (int n = 0; n < N; n++) fft_3stages_pk(c[n], [&](int j) { return ld2(T.tw2[j][b]); });
+#ifndef JAAD_XCH_NOVCC
+    if constexpr (N == 2) {
+        xch_bit_pair<0, 2>(c[0], c[1]);  // e bit 6 (lane bit 2) <-> e bit 3
+        xch_bit_pair<1, 1>(c[0], c[1]);  // e bit 7 (lane bit 1) <-> e bit 4
+        xch_bit_pair<2, 0>(c[0], c[1]);  // e bit 8 (lane bit 0) <-> e bit 5
+    } else
+#endif
+    {
 #pragma unroll
-    for (int n = 0; n < N; n++) {
-        xch_bit<0, 2>(c[n], u);  // e bit 6 (lane bit 2) <-> e bit 3
-        xch_bit<1, 1>(c[n], u);  // e bit 7 (lane bit 1) <-> e bit 4
-        xch_bit<2, 0>(c[n], u);  // e bit 8 (lane bit 0) <-> e bit 5
+        for (int n = 0; n < N; n++) {
+            xch_bit<0, 2>(c[n], u);  // e bit 6 (lane bit 2) <-> e bit 3
+            xch_bit<1, 1>(c[n], u);  // e bit 7 (lane bit 1) <-> e bit 4
+            xch_bit<2, 0>(c[n], u);  // e bit 8 (lane bit 0) <-> e bit 5
+        }
     }
     // pass 3: register bits 0,1,2 = e bits 6,7,8, e mod 64 = lane_pos(u)
 #pragma unroll
@@ -810,7 +916,7 @@ __device__ __forceinline__ void store16(v4u v, __amdgpu_buffer_rsrc_t r, int off
 }
 
 // per-wave LDS area: 8.5 KiB (16 waves + the 20 KiB table image fill a CU's 160 KiB)
-//   buf  band records [0,512) + raw sf/cb rows [512,640) -> spectrum (E/O) -> IFFT transposes ->
+//   buf  band records [0,512) -> spectrum (E/O) -> IFFT transposes ->
 //        OLA scratch -> PCM staging
 //   rsp  the right channel's spectrum while the left one is transformed (PNS: raw row copy)
 constexpr int kRspFloats = kWaveBuf;  // second channel buffer (spectrum + PCM staging)
@@ -833,7 +939,6 @@ constexpr int waves_per_wg()
 {
     return kTns ? 8 : JAAD_LC_WAVES;
 }
-constexpr int kRawOff = 512;  // raw rows in buf: channel c's 64 dwords at buf[kRawOff + 64c]
 
 // One scalefactor band (index g*max_sfb+sfb) of one frame, both channels:
 //   gl / gr   gain applied to IQ values, 0 for bands that are not spectral (ZERO/NOISE/IS)
@@ -900,7 +1005,7 @@ __device__ void pns_fill(float* buf, const uint32_t* raw, const LdsTables& T, co
 
 struct Prefetch {
     v4i q[2][2];       // [channel][h]: bins 8u+512h .. +7
-    uint32_t sfcb[2];  // [channel] lane u < 32: sf bytes 4u..4u+3; lane u >= 32: cb bytes 4(u-32)..
+    uint32_t sf2[2], cb2[2];  // [channel] sf / cb bytes of bands 2u, 2u+1 (zero-extended 16 bits)
     uint32_t side;     // lane i < 4*nch: dword i of the frame's jaad_ics_info records;
                        // lanes 8..11: the frame's ms_used words (read back with readlane)
 };
@@ -917,8 +1022,9 @@ __device__ __forceinline__ void prefetch(const KernelArgs& A, int f, bool stereo
         const v4i* q = reinterpret_cast<const v4i*>(A.q + cf * 1024);
         pf.q[c][0] = __builtin_nontemporal_load(q + u);
         pf.q[c][1] = __builtin_nontemporal_load(q + 64 + u);
-        const uint32_t* row = reinterpret_cast<const uint32_t*>(u < 32 ? A.sf + cf * 128 : A.cb + cf * 128);
-        pf.sfcb[c] = row[u & 31];
+        // lane u's two bands straight from the rows (no LDS round trip to regroup row dwords)
+        pf.sf2[c] = reinterpret_cast<const uint16_t*>(A.sf + cf * 128)[u];
+        pf.cb2[c] = reinterpret_cast<const uint16_t*>(A.cb + cf * 128)[u];
     }
     const uint32_t* side = u < 8 ? reinterpret_cast<const uint32_t*>(A.ics + (size_t)f * A.cf_stride) + (u < 4 * nch ? u : 0)
                                  : (A.ms_used ? reinterpret_cast<const uint32_t*>(A.ms_used + (size_t)f * 2 * A.ms_stride) + (u & 3)
@@ -1016,6 +1122,8 @@ __device__ __forceinline__ void synth_channel(const KernelArgs& A, const LdsTabl
         st_acc[k] += (uint32_t)(t_ - st_prev);                    \
         st_prev = t_;                                             \
     } while (0)
+#elif defined(JAAD_MARKS)  // design tool: phase markers in the device assembly (tools/phase_mix.py)
+#define STAMP(k) asm volatile(";PHASE " #k)
 #else
 #define STAMP(k) \
     do {         \
@@ -1059,9 +1167,10 @@ __global__ __launch_bounds__(64 * waves_per_wg<kMode == 1>()) void lc_decode_ker
     constexpr bool stereo = kStereo;
     constexpr int nch = stereo ? 2 : 1;
     WaveLds<kTnsSpec>& W = S.W[wave];
-    uint32_t* raw = reinterpret_cast<uint32_t*>(W.buf + kRawOff);
     BandRec* rec = reinterpret_cast<BandRec*>(W.buf);
 
+    // scalefactor band counts (frame invariant: read once, not from LDS in every frame)
+    const int nswb_l = __builtin_amdgcn_readfirstlane(T.nswb_l), nswb_s = __builtin_amdgcn_readfirstlane(T.nswb_s);
     // long-window band of each of the lane's 4 bin quads (frame invariant)
     uint32_t q2b_long = 0;
     {
@@ -1127,8 +1236,8 @@ __global__ __launch_bounds__(64 * waves_per_wg<kMode == 1>()) void lc_decode_ker
             const Prefetch cur = pf;
 
             // ---------------- side info ----------------
-            const Ics iL = ics_from_lanes(cur.side, 0, T);
-            const Ics iR = stereo ? ics_from_lanes(cur.side, 4, T) : iL;
+            const Ics iL = ics_from_lanes(cur.side, 0, nswb_l, nswb_s);
+            const Ics iR = stereo ? ics_from_lanes(cur.side, 4, nswb_l, nswb_s) : iL;
             const bool ms_on = stereo && (iL.flags & JAAD_ICS_COMMON_WINDOW) && (iL.flags & JAAD_ICS_MS_PRESENT);
             const bool is_on = stereo && (iR.flags & JAAD_ICS_HAS_IS);
             const bool same_bands = !stereo || (iL.seq == iR.seq && iL.max_sfb == iR.max_sfb && iL.grouping == iR.grouping);
@@ -1143,15 +1252,9 @@ __global__ __launch_bounds__(64 * waves_per_wg<kMode == 1>()) void lc_decode_ker
 
             STAMP(0);
             // ---------------- band records (lane u: bands 2u, 2u+1) ----------------
-            wave_sync();
-            raw[u] = cur.sfcb[0];
-            if (stereo) raw[64 + u] = cur.sfcb[1];
-            wave_sync();
             {
-                const uint16_t* r0 = reinterpret_cast<const uint16_t*>(raw);
-                const uint16_t* r1 = reinterpret_cast<const uint16_t*>(raw + 64);
-                const uint32_t sfL2 = r0[u], cbL2 = r0[64 + u];
-                const uint32_t sfR2 = stereo ? (uint32_t)r1[u] : 0u, cbR2 = stereo ? (uint32_t)r1[64 + u] : 0u;
+                const uint32_t sfL2 = cur.sf2[0], cbL2 = cur.cb2[0];
+                const uint32_t sfR2 = stereo ? cur.sf2[1] : 0u, cbR2 = stereo ? cur.cb2[1] : 0u;
                 const uint64_t mw = u < 32 ? m0 : m1;
                 const uint32_t msb = (uint32_t)(mw >> ((2 * u) & 63)) & 3u;
                 BandRec br[2];
@@ -1191,21 +1294,33 @@ __global__ __launch_bounds__(64 * waves_per_wg<kMode == 1>()) void lc_decode_ker
             float gL[4], gR[4], msq[4], isq[4];
             uint32_t q2b = q2b_long;
             asm volatile("" : "+v"(q2b));  // one packed register across frames, unpacked here
+            if (iL.seq != JAAD_EIGHT_SHORT_SEQUENCE && same_bands) {
+                // the common frame (long windows, one band layout): one record read per quad
 #pragma unroll
-            for (int qd = 0; qd < 4; qd++) {
-                const int p = 512 * (qd >> 1) + 8 * u + 4 * (qd & 1);
-                const int bl = iL.seq == JAAD_EIGHT_SHORT_SEQUENCE ? band_short(T, iL, p) : (int)((q2b >> (8 * qd)) & 255u);
-                const float4 r = reinterpret_cast<const float4*>(rec)[bl];
-                gL[qd] = r.x;
-                msq[qd] = r.y;
-                if (same_bands) {
+                for (int qd = 0; qd < 4; qd++) {
+                    const float4 r = reinterpret_cast<const float4*>(rec)[(q2b >> (8 * qd)) & 255u];
+                    gL[qd] = r.x;
+                    msq[qd] = r.y;
                     gR[qd] = r.z;
                     isq[qd] = r.w;
-                } else {
-                    const int br = iR.seq == JAAD_EIGHT_SHORT_SEQUENCE ? band_short(T, iR, p) : (int)((q2b >> (8 * qd)) & 255u);
-                    const float2 rr = reinterpret_cast<const float2*>(rec)[2 * br + 1];
-                    gR[qd] = rr.x;
-                    isq[qd] = rr.y;
+                }
+            } else {
+#pragma unroll
+                for (int qd = 0; qd < 4; qd++) {
+                    const int p = 512 * (qd >> 1) + 8 * u + 4 * (qd & 1);
+                    const int bl = iL.seq == JAAD_EIGHT_SHORT_SEQUENCE ? band_short(T, iL, p) : (int)((q2b >> (8 * qd)) & 255u);
+                    const float4 r = reinterpret_cast<const float4*>(rec)[bl];
+                    gL[qd] = r.x;
+                    msq[qd] = r.y;
+                    if (same_bands) {
+                        gR[qd] = r.z;
+                        isq[qd] = r.w;
+                    } else {
+                        const int br = iR.seq == JAAD_EIGHT_SHORT_SEQUENCE ? band_short(T, iR, p) : (int)((q2b >> (8 * qd)) & 255u);
+                        const float2 rr = reinterpret_cast<const float2*>(rec)[2 * br + 1];
+                        gR[qd] = rr.x;
+                        isq[qd] = rr.y;
+                    }
                 }
             }
             float xL[16], xR[16];
@@ -1220,11 +1335,18 @@ __global__ __launch_bounds__(64 * waves_per_wg<kMode == 1>()) void lc_decode_ker
             prefetch(A, it + 1 < my_n ? f + 1 : f, stereo, u, pf);
 
             if ((iL.flags | (stereo ? iR.flags : 0)) & JAAD_ICS_HAS_PNS) {  // rare: lane 0 replays the LCG
-                // the spectrum overwrites the raw rows: pns_fill reads a copy in rsp
+                // pns_fill reads the channel's raw sf/cb rows from rsp
                 uint32_t* rcopy = reinterpret_cast<uint32_t*>(W.rsp);
                 wave_sync();
-                rcopy[u] = raw[u];
-                if (stereo) rcopy[64 + u] = raw[64 + u];
+                {  // the raw rows as the prefetch left them: sf bytes [0,128), cb bytes [128,256) per channel
+                    uint16_t* r16 = reinterpret_cast<uint16_t*>(rcopy);
+                    r16[u] = (uint16_t)cur.sf2[0];
+                    r16[64 + u] = (uint16_t)cur.cb2[0];
+                    if (stereo) {
+                        r16[128 + u] = (uint16_t)cur.sf2[1];
+                        r16[192 + u] = (uint16_t)cur.cb2[1];
+                    }
+                }
                 if (iL.flags & JAAD_ICS_HAS_PNS) {
                     wave_sync();
                     store_spec(W.buf, u, xL);

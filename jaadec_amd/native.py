@@ -130,49 +130,55 @@ def lib() -> C.CDLL:
         if not LIB_PATH.exists():
             raise RuntimeError(f"{LIB_PATH} is missing: build it with `python -m jaadec_amd.build` "
                                "(there is no CPU fallback for the HIP path)")
-        L = C.CDLL(str(LIB_PATH))
-        L.jaad_cfg_sample_length.argtypes = [C.POINTER(StreamCfg)]
-        L.jaad_cfg_channel_count.argtypes = [C.POINTER(StreamCfg)]
-        L.jaad_frame_pcm_bytes.argtypes = [C.POINTER(StreamCfg), C.c_uint32]
-        L.jaad_frame_pcm_bytes.restype = C.c_size_t
-        L.jaad_ctx_create.argtypes = [C.POINTER(StreamCfg), C.c_uint32, C.c_int, C.POINTER(C.c_void_p)]
-        L.jaad_ctx_destroy.argtypes = [C.c_void_p]
-        L.jaad_ctx_destroy.restype = None
-        L.jaad_ctx_core_channels.argtypes = [C.c_void_p]
-        L.jaad_decode_batch.argtypes = [C.c_void_p, C.POINTER(BatchStruct), C.c_void_p, C.c_size_t, C.c_uint32]
-        L.jaad_decode_batch_device.argtypes = [C.c_void_p, C.POINTER(BatchStruct), C.c_void_p, C.c_size_t,
-                                               C.c_uint32, C.c_void_p]
-        L.jaad_wait.argtypes = [C.c_void_p]
-        L.jaad_host_register.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
-        L.jaad_host_unregister.argtypes = [C.c_void_p, C.c_void_p]
-        L.jaad_host_alloc.argtypes = [C.c_void_p, C.c_size_t, C.POINTER(C.c_void_p)]
-        L.jaad_host_free.argtypes = [C.c_void_p, C.c_void_p]
-        L.jaad_state_bytes.argtypes = [C.c_void_p]
-        L.jaad_state_bytes.restype = C.c_size_t
-        L.jaad_state_export.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_size_t]
-        L.jaad_state_import.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_size_t]
-        L.jaad_state_reset.argtypes = [C.c_void_p, C.c_uint32]
-        L.jaad_strerror.argtypes = [C.c_int]
-        L.jaad_strerror.restype = C.c_char_p
-        L.jaad_last_error.argtypes = [C.c_void_p]
-        L.jaad_last_error.restype = C.c_char_p
-        L.jaad_asc_parse.argtypes = [C.c_char_p, C.c_size_t, C.POINTER(StreamCfg)]
-        L.jaad_adts_find.argtypes = [C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t), C.POINTER(AdtsHeader)]
-        L.jaad_adts_cfg.argtypes = [C.POINTER(AdtsHeader), C.POINTER(StreamCfg)]
-        L.jaad_raw_pce_cfg.argtypes = [C.c_char_p, C.c_size_t, C.POINTER(StreamCfg)]
-        L.jaad_parser_create.argtypes = [C.POINTER(StreamCfg), C.POINTER(C.c_void_p)]
-        L.jaad_parser_destroy.argtypes = [C.c_void_p]
-        L.jaad_parser_clone.argtypes = [C.c_void_p, C.POINTER(C.c_void_p)]
-        L.jaad_parser_copy.argtypes = [C.c_void_p, C.c_void_p]
-        L.jaad_parser_destroy.restype = None
-        L.jaad_parser_pns_state.argtypes = [C.c_void_p]
-        L.jaad_parser_pns_state.restype = C.c_uint32
-        L.jaad_parser_set_pns_state.argtypes = [C.c_void_p, C.c_uint32]
-        L.jaad_parser_set_pns_state.restype = None
-        L.jaad_parse_frame.argtypes = [C.c_void_p, C.c_char_p, C.c_size_t, C.POINTER(FrameOut)]
-        L.jaad_probe_sbr.argtypes = [C.POINTER(StreamCfg), C.c_char_p, C.c_size_t, C.POINTER(C.c_uint32)]
-        _lib = L
+        _lib = load_lib(LIB_PATH)
     return _lib
+
+
+def load_lib(path) -> C.CDLL:
+    """The C-ABI of one libjaadgpu.so build with its prototypes (lib() holds the product's; A/B
+    timing scripts load variants side by side)."""
+    L = C.CDLL(str(path))
+    L.jaad_cfg_sample_length.argtypes = [C.POINTER(StreamCfg)]
+    L.jaad_cfg_channel_count.argtypes = [C.POINTER(StreamCfg)]
+    L.jaad_frame_pcm_bytes.argtypes = [C.POINTER(StreamCfg), C.c_uint32]
+    L.jaad_frame_pcm_bytes.restype = C.c_size_t
+    L.jaad_ctx_create.argtypes = [C.POINTER(StreamCfg), C.c_uint32, C.c_int, C.POINTER(C.c_void_p)]
+    L.jaad_ctx_destroy.argtypes = [C.c_void_p]
+    L.jaad_ctx_destroy.restype = None
+    L.jaad_ctx_core_channels.argtypes = [C.c_void_p]
+    L.jaad_decode_batch.argtypes = [C.c_void_p, C.POINTER(BatchStruct), C.c_void_p, C.c_size_t, C.c_uint32]
+    L.jaad_decode_batch_device.argtypes = [C.c_void_p, C.POINTER(BatchStruct), C.c_void_p, C.c_size_t,
+                                           C.c_uint32, C.c_void_p]
+    L.jaad_wait.argtypes = [C.c_void_p]
+    L.jaad_host_register.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
+    L.jaad_host_unregister.argtypes = [C.c_void_p, C.c_void_p]
+    L.jaad_host_alloc.argtypes = [C.c_void_p, C.c_size_t, C.POINTER(C.c_void_p)]
+    L.jaad_host_free.argtypes = [C.c_void_p, C.c_void_p]
+    L.jaad_state_bytes.argtypes = [C.c_void_p]
+    L.jaad_state_bytes.restype = C.c_size_t
+    L.jaad_state_export.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_size_t]
+    L.jaad_state_import.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_size_t]
+    L.jaad_state_reset.argtypes = [C.c_void_p, C.c_uint32]
+    L.jaad_strerror.argtypes = [C.c_int]
+    L.jaad_strerror.restype = C.c_char_p
+    L.jaad_last_error.argtypes = [C.c_void_p]
+    L.jaad_last_error.restype = C.c_char_p
+    L.jaad_asc_parse.argtypes = [C.c_char_p, C.c_size_t, C.POINTER(StreamCfg)]
+    L.jaad_adts_find.argtypes = [C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t), C.POINTER(AdtsHeader)]
+    L.jaad_adts_cfg.argtypes = [C.POINTER(AdtsHeader), C.POINTER(StreamCfg)]
+    L.jaad_raw_pce_cfg.argtypes = [C.c_char_p, C.c_size_t, C.POINTER(StreamCfg)]
+    L.jaad_parser_create.argtypes = [C.POINTER(StreamCfg), C.POINTER(C.c_void_p)]
+    L.jaad_parser_destroy.argtypes = [C.c_void_p]
+    L.jaad_parser_clone.argtypes = [C.c_void_p, C.POINTER(C.c_void_p)]
+    L.jaad_parser_copy.argtypes = [C.c_void_p, C.c_void_p]
+    L.jaad_parser_destroy.restype = None
+    L.jaad_parser_pns_state.argtypes = [C.c_void_p]
+    L.jaad_parser_pns_state.restype = C.c_uint32
+    L.jaad_parser_set_pns_state.argtypes = [C.c_void_p, C.c_uint32]
+    L.jaad_parser_set_pns_state.restype = None
+    L.jaad_parse_frame.argtypes = [C.c_void_p, C.c_char_p, C.c_size_t, C.POINTER(FrameOut)]
+    L.jaad_probe_sbr.argtypes = [C.POINTER(StreamCfg), C.c_char_p, C.c_size_t, C.POINTER(C.c_uint32)]
+    return L
 
 
 def synth_lib() -> C.CDLL:

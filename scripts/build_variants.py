@@ -16,6 +16,9 @@ VARIANTS = {
     "s_stamps": (["JAAD_STAMPS"], [], None),
     "e_w16c": (["JAAD_LDS_COMPACT", "JAAD_LC_WAVES=16"], [], None),
     "f_w12c": (["JAAD_LDS_COMPACT"], [], None),
+    "g_w8": (["JAAD_LC_WAVES=8"], [], None),
+    "c_sfcb": (["JAAD_SFCB_LOADS"], [], None),
+    "h_w4": (["JAAD_LC_WAVES=4"], [], None),
 }
 
 if __name__ == "__main__":
