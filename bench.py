@@ -318,8 +318,6 @@ def run(args, engine_cls=HipEngine, backend: str = "nccl"):
     # (scripts/gpu_prof.sh [config] -> scripts/summarize_prof.py -> profiles/current_c<config>.json)
     traffic, traffic_src = None, None
     cur = ROOT / "profiles" / f"current_c{args.config}.json"
-    if not cur.exists() and args.config == 2:
-        cur = ROOT / "profiles" / "current.json"
     if cur.exists():
         prof = json.loads(cur.read_text())
         if prof.get("frames_per_step", n_frames) == n_frames:  # the profile's workload is this one
