@@ -271,6 +271,59 @@ __device__ __forceinline__ void fft_3stages_pk(f2 (&c)[8], TW tw)
     for (int s = 0; s < 4; s++) bfly_pk(c[s], c[s + 4], tw(3 + s));
 }
 
+// The same stages on two channels in lockstep, interleaved operation by operation: each packed
+// operation's successor is the other channel's (independent) one, so the one wait state that a
+// dependent pair of packed FP32 operations needs is filled with work instead of an s_nop.
+__device__ __forceinline__ void bfly_pk2(f2& a0, f2& b0, f2& a1, f2& b1, f2 w)
+{
+    const f2 m0 = b0 * w.xx, m1 = b1 * w.xx;
+    const f2 n0 = pk_mul_swap_nlo(b0, w), n1 = pk_mul_swap_nlo(b1, w);
+    const f2 z0 = m0 + n0, z1 = m1 + n1;
+    b0 = a0 - z0;
+    b1 = a1 - z1;
+    a0 = a0 + z0;
+    a1 = a1 + z1;
+}
+__device__ __forceinline__ void radix4_pk2(f2 (&c)[8], f2 (&d)[8], int i0, int i1, int i2, int i3)
+{
+    const f2 a0 = c[i0] + c[i1], a1 = d[i0] + d[i1];
+    const f2 b0 = c[i2] + c[i3], b1 = d[i2] + d[i3];
+    const f2 e0 = c[i0] - c[i1], e1 = d[i0] - d[i1];
+    const f2 g0 = c[i2] - c[i3], g1 = d[i2] - d[i3];
+    c[i0] = a0 + b0;
+    d[i0] = a1 + b1;
+    c[i2] = a0 - b0;
+    d[i2] = a1 - b1;
+    c[i1] = pk_rot_p(e0, g0);
+    d[i1] = pk_rot_p(e1, g1);
+    c[i3] = pk_rot_m(e0, g0);
+    d[i3] = pk_rot_m(e1, g1);
+}
+__device__ __forceinline__ void fft_pass1_pk2(f2 (&c)[8], f2 (&d)[8], const float (*w)[2])
+{
+    radix4_pk2(c, d, BR3[0], BR3[1], BR3[2], BR3[3]);
+    radix4_pk2(c, d, BR3[4], BR3[5], BR3[6], BR3[7]);
+#pragma unroll
+    for (int k = 0; k < 4; k++) bfly_pk2(c[BR3[k]], c[BR3[k + 4]], d[BR3[k]], d[BR3[k + 4]], ld2(w[k]));
+}
+template <typename TW>
+__device__ __forceinline__ void fft_3stages_pk2(f2 (&c)[8], f2 (&d)[8], TW tw)
+{
+    {
+        const f2 w = tw(0);
+#pragma unroll
+        for (int s = 0; s < 8; s += 2) bfly_pk2(c[s], c[s + 1], d[s], d[s + 1], w);
+    }
+#pragma unroll
+    for (int e = 0; e < 2; e++) {
+        const f2 w = tw(1 + e);
+        bfly_pk2(c[e], c[e + 2], d[e], d[e + 2], w);
+        bfly_pk2(c[4 + e], c[6 + e], d[4 + e], d[6 + e], w);
+    }
+#pragma unroll
+    for (int s = 0; s < 4; s++) bfly_pk2(c[s], c[s + 4], d[s], d[s + 4], tw(3 + s));
+}
+
 
 // Register transposes between the IFFT passes.  A pair of registers (a: register bit i clear,
 // b: set) trades register bit i for lane bit L: the element at (register bit, lane bit L) =
@@ -532,8 +585,8 @@ __device__ __forceinline__ void imdct_long_pk(float* const (&bufs)[N], const Lds
             c[n][s] = cmul(x, ld2(T.mdct_l[k]));
         }
     // pass 1: register s holds e bits (s2, s1, s0) = e bits 0, 1, 2 (fft_pass1_pk's BR3 order)
-#pragma unroll
-    for (int n = 0; n < N; n++) fft_pass1_pk(c[n], T.tw1);
+    if constexpr (N == 2) fft_pass1_pk2(c[0], c[1], T.tw1);
+    else fft_pass1_pk(c[0], T.tw1);
 #pragma unroll
     for (int n = 0; n < N; n++) {
         xch_bit<0, 5>(c[n], u);  // e bit 3 (lane bit 5) <-> e bit 2
@@ -550,8 +603,8 @@ __device__ __forceinline__ void imdct_long_pk(float* const (&bufs)[N], const Lds
 #endif
     // pass 2: register bits 0,1,2 = e bits 3,4,5; e mod 8 = u >> 3
     const int b = u >> 3;
-#pragma unroll
-    for (int n = 0; n < N; n++) fft_3stages_pk(c[n], [&](int j) { return ld2(T.tw2[j][b]); });
+    if constexpr (N == 2) fft_3stages_pk2(c[0], c[1], [&](int j) { return ld2(T.tw2[j][b]); });
+    else fft_3stages_pk(c[0], [&](int j) { return ld2(T.tw2[j][b]); });
 #ifndef JAAD_XCH_NOVCC
     if constexpr (N == 2) {
         xch_bit_pair<0, 2>(c[0], c[1]);  // e bit 6 (lane bit 2) <-> e bit 3
@@ -568,13 +621,13 @@ __device__ __forceinline__ void imdct_long_pk(float* const (&bufs)[N], const Lds
         }
     }
     // pass 3: register bits 0,1,2 = e bits 6,7,8, e mod 64 = lane_pos(u)
+    if constexpr (N == 2) fft_3stages_pk2(c[0], c[1], [&](int j) { return ld2(T.tw3[j][u]); });
+    else fft_3stages_pk(c[0], [&](int j) { return ld2(T.tw3[j][u]); });
+    // MDCT.java:48-53: re = t0*c - t1*sn, im = t1*c + t0*sn = cmul((t0, t1), (c, sn))
 #pragma unroll
-    for (int n = 0; n < N; n++) {
-        fft_3stages_pk(c[n], [&](int j) { return ld2(T.tw3[j][u]); });
-        // MDCT.java:48-53: re = t0*c - t1*sn, im = t1*c + t0*sn = cmul((t0, t1), (c, sn))
+    for (int s = 0; s < 8; s++)
 #pragma unroll
-        for (int s = 0; s < 8; s++) c[n][s] = cmul(c[n][s], ld2(T.mdct_post[s][u]));
-    }
+        for (int n = 0; n < N; n++) c[n][s] = cmul(c[n][s], ld2(T.mdct_post[s][u]));
 }
 
 // FilterBank.process for ONLY_LONG / LONG_START / LONG_STOP (FilterBank.java:41-70, 102-119).
