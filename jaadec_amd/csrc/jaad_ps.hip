@@ -10,11 +10,12 @@
 // HBM:
 //   ps_analysis_kernel  X_left (SBR output, carry-patched) -> xps[f][0]; hybrid analysis -> xhl;
 //                       band energies P -> pg                                  (wave per frame)
-//   ps_decor_kernel     per run, four waves: QMF bands (lane = band) / hybrid groups / transient
-//                       detector / mixing-parameter scan (IPD/OPD phase history, h_prev),
-//                       sequential over the run's frames; rings in VGPRs with compile-time
-//                       indices (32 slots per frame), raw all-pass output -> xps[f][1], xhr;
-//                       G_TransientRatio -> pg; H start/delta per (env, group) -> hb (block per run)
+//   ps_decor_kernel     per run, eight waves: the three all-pass links of the QMF bands (lane =
+//                       band) and of the hybrid groups pipelined over waves, transient detector,
+//                       mixing-parameter scan (IPD/OPD phase history, h_prev), sequential over
+//                       the run's frames; rings in VGPRs with compile-time indices (32 slots per
+//                       frame), raw all-pass output -> xps[f][1], xhr; G_TransientRatio -> pg;
+//                       H start/delta per (env, group) -> hb (block per run)
 //   ps_mix_kernel       H interpolation, G scaling, mixing (+ IPD/OPD rotation), hybrid
 //                       synthesis -> xps[f][0..1]                              (wave per frame)
 //   ps_state_kernel     filterbank history of each run's last frame -> slot state
@@ -283,143 +284,187 @@ constexpr int kPsFrameDw = (int)(sizeof(jaad_ps_frame) / 4);
 constexpr int kPsFrameDwPerLane = (kPsFrameDw + 19) / 20;
 static_assert(sizeof(jaad_ps_frame) % 4 == 0, "PS records are copied dword-wise");
 
+// One lane per parameter band (u < 20), frame by frame: scan_init, scan_frame(j) for j = 0 ..
+// nfr-1, scan_finish.  The scan's arrays are the caller's locals (kept out of a struct so that they
+// stay in registers: a dynamically indexed array member would go to scratch).
+struct ScanCtx {
+    const SbrArgs& A;
+    const PsConst& K;
+    const uint32_t* fl;
+    uint32_t nfr;
+    PsState& S;
+    int u;
+    uint32_t (*pbuf)[kPsFrameDw];
+};
+struct ScanArrays {
+    uint32_t (&pre)[kPsFrameDwPerLane];
+    int (&grs)[2];
+    float (&hp)[2][8];
+    float (&ipd)[2][2];
+    float (&opd)[2][2];
+    int& phase;
+};
+
+__device__ __forceinline__ void scan_fetch(const ScanCtx& C, const ScanArrays& Z, uint32_t f)
+{
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(C.A.psf + f);
+#pragma unroll
+    for (int i = 0; i < kPsFrameDwPerLane; i++) {
+        const int d = C.u + 20 * i;
+        Z.pre[i] = d < kPsFrameDw ? src[d] : 0u;
+    }
+}
+__device__ __forceinline__ void scan_park(const ScanCtx& C, const ScanArrays& Z, uint32_t* dst)
+{
+#pragma unroll
+    for (int i = 0; i < kPsFrameDwPerLane; i++) {
+        const int d = C.u + 20 * i;
+        if (d < kPsFrameDw) dst[d] = Z.pre[i];
+    }
+}
+__device__ __forceinline__ void scan_init(const ScanCtx& C, const ScanArrays& Z, bool fresh)
+{
+    scan_fetch(C, Z, C.fl[0]);
+    scan_park(C, Z, C.pbuf[0]);
+    wave_sync();
+    const int bk = C.u;
+    Z.grs[0] = bk == 0 ? 1 : (bk == 1 ? 0 : bk + 2);
+    Z.grs[1] = bk == 0 ? 2 : (bk == 1 ? 3 : -1);
+    for (int j = 0; j < 2; j++)
+        for (int k = 0; k < 8; k++) {
+            const int gr = Z.grs[j] < 0 ? 0 : Z.grs[j];
+            // PSImpl constructor (:87-92): h11_prev = (1, 0), h12_prev = (0, 1), h21/h22 = 0
+            Z.hp[j][k] = fresh ? (k == 0 || k == 5 ? 1.0f : 0.0f) : C.S.h_prev[gr][k];
+        }
+    for (int ph = 0; ph < 2; ph++)
+        for (int c = 0; c < 2; c++) {
+            Z.ipd[ph][c] = fresh ? 0.0f : C.S.ipd_prev[bk][ph][c];
+            Z.opd[ph][c] = fresh ? 0.0f : C.S.opd_prev[bk][ph][c];
+        }
+    Z.phase = fresh ? 0 : C.S.phase_hist;
+    if (C.nfr > 1) scan_fetch(C, Z, C.fl[1]);  // lands during frame 0's scan
+}
+// frame j (its record parked in pbuf[j & 1]); frame j + 1's record (fetched during frame j) is
+// parked at its end and frame j + 2's fetched
+__device__ __forceinline__ void scan_frame(const ScanCtx& C, const ScanArrays& Z, uint32_t j)
+{
+    const SbrArgs& A = C.A;
+    const PsConst& K = C.K;
+    const int bk = C.u;
+    float (&hp)[2][8] = Z.hp;
+    float (&ipd)[2][2] = Z.ipd;
+    float (&opd)[2][2] = Z.opd;
+    const uint32_t f = C.fl[j];
+    const jaad_ps_frame& P = *reinterpret_cast<const jaad_ps_frame*>(C.pbuf[j & 1]);
+    const int E = P.num_env, nr = P.nr_ipdopd_par;
+    const bool elig = bk < nr;
+    float* hbf = A.hb + (size_t)f * (5 * 22 * 16);
+    for (int g = 0; g < 2; g++) {
+        const int gr = Z.grs[g];
+        if (gr < 0) break;
+        for (int env = 0; env < E; env++) {
+            float h[8];
+            ps_h(K, P, env, gr, h);
+            h[4] = h[5] = h[6] = h[7] = 0.0f;
+            if (elig) {  // phase rotation (:484-567)
+                const int ph = (Z.phase + gr * E + env) & 1;
+                float* ip = ipd[ph];
+                float* op = opd[ph];
+                float tl0 = (ip[0] * 0.25f), tl1 = (ip[1] * 0.25f);
+                float tr0 = (op[0] * 0.25f), tr1 = (op[1] * 0.25f);
+                const int idx = P.ipd[env][bk] < 0 ? -P.ipd[env][bk] : P.ipd[env][bk];  // IPD for both
+                ip[0] = K.ipdopd_cos[idx];
+                ip[1] = K.ipdopd_sin[idx];
+                op[0] = K.ipdopd_cos[idx];
+                op[1] = K.ipdopd_sin[idx];
+                tl0 += ip[0];
+                tl1 += ip[1];
+                tr0 += op[0];
+                tr1 += op[1];
+                const float* pp = opd[ph ^ 1];  // value before previous: opd.prev for both
+                tl0 += (pp[0] * 0.5f);
+                tl1 += (pp[1] * 0.5f);
+                tr0 += (pp[0] * 0.5f);
+                tr1 += (pp[1] * 0.5f);
+                const float xy = magnitude_c(tr0, tr1), pq = magnitude_c(tl0, tl1);
+                float pl0 = 0.0f, pl1 = 0.0f, pr0 = 0.0f, pr1 = 0.0f;
+                if (xy != 0.0f) {
+                    pl0 = __fdiv_rn(tr0, xy);
+                    pl1 = __fdiv_rn(tr1, xy);
+                }
+                const float xypq = (xy * pq);
+                if (xypq != 0.0f) {
+                    const float tmp1 = (tr0 * tl0) + (tr1 * tl1);
+                    const float tmp2 = (tr1 * tl0) - (tr0 * tl1);
+                    pr0 = __fdiv_rn(tmp1, xypq);
+                    pr1 = __fdiv_rn(tmp2, xypq);
+                }
+                h[4] = (h[0] * pl1);
+                h[5] = (h[1] * pr1);
+                h[6] = (h[2] * pl1);
+                h[7] = (h[3] * pr1);
+                h[0] = (h[0] * pl0);
+                h[1] = (h[1] * pr0);
+                h[2] = (h[2] * pl0);
+                h[3] = (h[3] * pr0);
+            }
+            const float Lf = (float)(P.border[env + 1] - P.border[env]);
+            float* o = hbf + (env * 22 + gr) * 16;
+            for (int k = 0; k < 4; k++) {
+                o[8 + k] = __fdiv_rn(h[k] - hp[g][k], Lf);
+                o[k] = hp[g][k];
+                hp[g][k] = h[k];
+            }
+            for (int k = 4; k < 8; k++) {
+                float d = 0.0f, st = 0.0f;
+                if (elig) {
+                    d = __fdiv_rn(h[k] - hp[g][k], Lf);
+                    st = hp[g][k];
+                    if (bk != 0) {  // FBType.bkm tests the band bits (A/ps/FBType.java:71-73)
+                        d = -d;
+                        st = -st;
+                    }
+                    hp[g][k] = h[k];
+                }
+                o[8 + k] = d;
+                o[k] = st;
+            }
+        }
+    }
+    if (nr) Z.phase = (Z.phase + (nr + 2) * E) & 1;
+    if (j + 1 < C.nfr) {
+        wave_sync();  // every lane is done with buffer (j + 1) & 1's previous frame
+        scan_park(C, Z, C.pbuf[(j + 1) & 1]);
+        wave_sync();
+        if (j + 2 < C.nfr) scan_fetch(C, Z, C.fl[j + 2]);  // lands during frame j + 1's scan
+    }
+}
+__device__ __forceinline__ void scan_finish(const ScanCtx& C, const ScanArrays& Z)
+{
+    const int bk = C.u;
+    for (int g = 0; g < 2; g++)
+        if (Z.grs[g] >= 0)
+            for (int k = 0; k < 8; k++) C.S.h_prev[Z.grs[g]][k] = Z.hp[g][k];
+    for (int ph = 0; ph < 2; ph++)
+        for (int c = 0; c < 2; c++) {
+            C.S.ipd_prev[bk][ph][c] = Z.ipd[ph][c];
+            C.S.opd_prev[bk][ph][c] = Z.opd[ph][c];
+        }
+    if (C.u == 0) C.S.phase_hist = Z.phase;
+}
+
 __device__ void ps_param_scan(const SbrArgs& A, const PsConst& K, const uint32_t* fl, uint32_t nfr, PsState& S,
                               bool fresh, int u, uint32_t (*pbuf)[kPsFrameDw])
 {
     if (u >= 20) return;
     uint32_t pre[kPsFrameDwPerLane];
-    auto fetch = [&](uint32_t f) {
-        const uint32_t* src = reinterpret_cast<const uint32_t*>(A.psf + f);
-#pragma unroll
-        for (int i = 0; i < kPsFrameDwPerLane; i++) {
-            const int d = u + 20 * i;
-            pre[i] = d < kPsFrameDw ? src[d] : 0u;
-        }
-    };
-    auto park = [&](uint32_t* dst) {
-#pragma unroll
-        for (int i = 0; i < kPsFrameDwPerLane; i++) {
-            const int d = u + 20 * i;
-            if (d < kPsFrameDw) dst[d] = pre[i];
-        }
-    };
-    fetch(fl[0]);
-    park(pbuf[0]);
-    wave_sync();
-    const int bk = u;
-    const int grs[2] = {bk == 0 ? 1 : (bk == 1 ? 0 : bk + 2), bk == 0 ? 2 : (bk == 1 ? 3 : -1)};
-    float hp[2][8];
-    for (int j = 0; j < 2; j++)
-        for (int k = 0; k < 8; k++) {
-            const int gr = grs[j] < 0 ? 0 : grs[j];
-            // PSImpl constructor (:87-92): h11_prev = (1, 0), h12_prev = (0, 1), h21/h22 = 0
-            hp[j][k] = fresh ? (k == 0 || k == 5 ? 1.0f : 0.0f) : S.h_prev[gr][k];
-        }
-    float ipd[2][2], opd[2][2];
-    for (int ph = 0; ph < 2; ph++)
-        for (int c = 0; c < 2; c++) {
-            ipd[ph][c] = fresh ? 0.0f : S.ipd_prev[bk][ph][c];
-            opd[ph][c] = fresh ? 0.0f : S.opd_prev[bk][ph][c];
-        }
-    int phase = fresh ? 0 : S.phase_hist;
-    uint32_t f = fl[0], f_next = nfr > 1 ? fl[1] : 0u;
-    for (uint32_t j = 0; j < nfr; j++) {
-        if (j + 1 < nfr) fetch(f_next);  // lands during this frame's scan
-        const uint32_t f_after = j + 2 < nfr ? fl[j + 2] : 0u;
-        const jaad_ps_frame& P = *reinterpret_cast<const jaad_ps_frame*>(pbuf[j & 1]);
-        const int E = P.num_env, nr = P.nr_ipdopd_par;
-        const bool elig = bk < nr;
-        float* hbf = A.hb + (size_t)f * (5 * 22 * 16);
-        for (int g = 0; g < 2; g++) {
-            const int gr = grs[g];
-            if (gr < 0) break;
-            for (int env = 0; env < E; env++) {
-                float h[8];
-                ps_h(K, P, env, gr, h);
-                h[4] = h[5] = h[6] = h[7] = 0.0f;
-                if (elig) {  // phase rotation (:484-567)
-                    const int ph = (phase + gr * E + env) & 1;
-                    float* ip = ipd[ph];
-                    float* op = opd[ph];
-                    float tl0 = (ip[0] * 0.25f), tl1 = (ip[1] * 0.25f);
-                    float tr0 = (op[0] * 0.25f), tr1 = (op[1] * 0.25f);
-                    const int idx = P.ipd[env][bk] < 0 ? -P.ipd[env][bk] : P.ipd[env][bk];  // IPD for both
-                    ip[0] = K.ipdopd_cos[idx];
-                    ip[1] = K.ipdopd_sin[idx];
-                    op[0] = K.ipdopd_cos[idx];
-                    op[1] = K.ipdopd_sin[idx];
-                    tl0 += ip[0];
-                    tl1 += ip[1];
-                    tr0 += op[0];
-                    tr1 += op[1];
-                    const float* pp = opd[ph ^ 1];  // value before previous: opd.prev for both
-                    tl0 += (pp[0] * 0.5f);
-                    tl1 += (pp[1] * 0.5f);
-                    tr0 += (pp[0] * 0.5f);
-                    tr1 += (pp[1] * 0.5f);
-                    const float xy = magnitude_c(tr0, tr1), pq = magnitude_c(tl0, tl1);
-                    float pl0 = 0.0f, pl1 = 0.0f, pr0 = 0.0f, pr1 = 0.0f;
-                    if (xy != 0.0f) {
-                        pl0 = __fdiv_rn(tr0, xy);
-                        pl1 = __fdiv_rn(tr1, xy);
-                    }
-                    const float xypq = (xy * pq);
-                    if (xypq != 0.0f) {
-                        const float tmp1 = (tr0 * tl0) + (tr1 * tl1);
-                        const float tmp2 = (tr1 * tl0) - (tr0 * tl1);
-                        pr0 = __fdiv_rn(tmp1, xypq);
-                        pr1 = __fdiv_rn(tmp2, xypq);
-                    }
-                    h[4] = (h[0] * pl1);
-                    h[5] = (h[1] * pr1);
-                    h[6] = (h[2] * pl1);
-                    h[7] = (h[3] * pr1);
-                    h[0] = (h[0] * pl0);
-                    h[1] = (h[1] * pr0);
-                    h[2] = (h[2] * pl0);
-                    h[3] = (h[3] * pr0);
-                }
-                const float Lf = (float)(P.border[env + 1] - P.border[env]);
-                float* o = hbf + (env * 22 + gr) * 16;
-                for (int k = 0; k < 4; k++) {
-                    o[8 + k] = __fdiv_rn(h[k] - hp[g][k], Lf);
-                    o[k] = hp[g][k];
-                    hp[g][k] = h[k];
-                }
-                for (int k = 4; k < 8; k++) {
-                    float d = 0.0f, st = 0.0f;
-                    if (elig) {
-                        d = __fdiv_rn(h[k] - hp[g][k], Lf);
-                        st = hp[g][k];
-                        if (bk != 0) {  // FBType.bkm tests the band bits (A/ps/FBType.java:71-73)
-                            d = -d;
-                            st = -st;
-                        }
-                        hp[g][k] = h[k];
-                    }
-                    o[8 + k] = d;
-                    o[k] = st;
-                }
-            }
-        }
-        if (nr) phase = (phase + (nr + 2) * E) & 1;
-        if (j + 1 < nfr) {
-            wave_sync();  // every lane is done with buffer (j + 1) & 1's previous frame
-            park(pbuf[(j + 1) & 1]);
-            wave_sync();
-        }
-        f = f_next;
-        f_next = f_after;
-    }
-    for (int g = 0; g < 2; g++)
-        if (grs[g] >= 0)
-            for (int k = 0; k < 8; k++) S.h_prev[grs[g]][k] = hp[g][k];
-    for (int ph = 0; ph < 2; ph++)
-        for (int c = 0; c < 2; c++) {
-            S.ipd_prev[bk][ph][c] = ipd[ph][c];
-            S.opd_prev[bk][ph][c] = opd[ph][c];
-        }
-    if (u == 0) S.phase_hist = phase;
+    int grs[2], phase;
+    float hp[2][8], ipd[2][2], opd[2][2];
+    const ScanCtx C{A, K, fl, nfr, S, u, pbuf};
+    const ScanArrays Z{pre, grs, hp, ipd, opd, phase};
+    scan_init(C, Z, fresh);
+    for (uint32_t j = 0; j < nfr; j++) scan_frame(C, Z, j);
+    scan_finish(C, Z);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -484,7 +529,9 @@ __device__ __forceinline__ void run_frames(const uint32_t* fl, uint32_t nfr, Loa
     }
 }
 
-__global__ __launch_bounds__(256) void ps_decor_kernel(SbrArgs A)
+// round-3 form (one wave per recurrence, the QMF and hybrid all-pass chains whole), kept as the
+// JAAD_DECOR_V1 build for A/B timing against the pipelined ps_decor_kernel below
+__global__ __launch_bounds__(256) void ps_decor_kernel_v1(SbrArgs A)
 {
     // the run's frames that carry PS data, in time order: the recurrences advance only there
     const uint32_t run = blockIdx.x;
@@ -614,6 +661,371 @@ __global__ __launch_bounds__(256) void ps_decor_kernel(SbrArgs A)
         S.smooth[u] = smooth;
         S.pprev[u] = pprev;
     }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Pipelined decorrelator: the all-pass chain of a band (2-slot delay, then links 0, 1, 2:
+// PSImpl.java:283-344) is a sequence of three independent recurrences -- link m's ring holds only
+// link m's own past inputs and outputs -- so each link runs on its own wave, one frame behind the
+// link before it, the links' outputs handed over through LDS.  Eight waves per run (two per SIMD:
+// 256 VGPRs each), in lockstep steps separated by a workgroup barrier; at step k the roles do:
+//   role 0 (Q0) QMF bands: 2-slot delay + link 0 of frame k
+//   role 1 (Q1) QMF link 1 of frame k-1, and the plain delay lines of bands >= 23 (-> xps[f][1])
+//   role 2 (Q2) QMF link 2 of frame k-2 (-> xps[f][1])
+//   roles 3-5   the same three links for the hybrid groups 0..9 (-> xhr); role 4 also computes
+//               G_TransientRatio of frame k-1 (the compare and the division, -> pg)
+//   role 6      transient detector recurrences of frame k (peak, smooth, energy)
+//   role 7      mixing-parameter scan of frame k (-> hb)
+// Every value is computed by the same binary32 operations as in ps_decor_kernel_v1 (bit-exact);
+// only the waves that compute them differ.  The run's critical path drops from the whole chain
+// of a QMF band (2-slot delay + 3 links per slot) to one link per slot.
+// ---------------------------------------------------------------------------------------------
+constexpr int kDecorWaves = 8;
+constexpr int kApBands = 23;  // QMF bands 0..22 run the all-pass chain
+
+// link m (0, 1, 2) of the all-pass chain at slot N: ring length 3, 4, 5; r = input (after the
+// 2-slot delay's phi rotation for link 0, the previous link's output otherwise) -> output
+template <int M, int N, int Len>
+__device__ __forceinline__ float2 ap_link(float2 (&d)[Len], float2 r, const float q[2], float g)
+{
+    const float2 t = d[N % Len];
+    float tr = (t.x * q[0]) + (t.y * q[1]);
+    float ti = (t.y * q[0]) - (t.x * q[1]);
+    tr -= g * r.x;
+    ti -= g * r.y;
+    d[N % Len] = make_float2(r.x + (g * tr), r.y + (g * ti));
+    return make_float2(tr, ti);
+}
+// the 2-slot delay and its phi rotation (the input of link 0)
+template <int N>
+__device__ __forceinline__ float2 ap_delay2(float2 (&d)[2], float2 x, const float phi[2])
+{
+    const float2 t0 = d[N % 2];
+    d[N % 2] = x;
+    return make_float2((t0.x * phi[0]) + (t0.y * phi[1]), (t0.y * phi[0]) - (t0.x * phi[1]));
+}
+
+// the lane index as an opaque value: each role recomputes it (two VALU) instead of the compiler
+// keeping one copy alive across the whole kernel (which it spilled to scratch and reloaded per slot)
+__device__ __forceinline__ int lane_id_fresh()
+{
+    int v;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(v));
+    return v;
+}
+
+// lanes of mask m take a, the others b, as one v_cndmask per float: a plain ?: on two array
+// elements is turned into a load from a selected address, which puts the arrays in scratch
+__device__ __forceinline__ float2 lane_sel(uint64_t m, float2 a, float2 b)
+{
+    float2 r;
+    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r.x) : "v"(b.x), "v"(a.x), "s"(m));
+    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r.y) : "v"(b.y), "v"(a.y), "s"(m));
+    return r;
+}
+
+struct DecorLds {
+    float2 q01[2][32][64], q12[2][32][64];  // QMF link outputs, [frame & 1][slot][band]
+    float2 h01[2][32][10], h12[2][32][10];              // hybrid groups
+    float2 tr[2][32][20];                               // (sm * gamma, nrg) per slot and parameter band
+};
+
+// The lockstep: nfr + 2 steps, a workgroup barrier after each; body(j, x, xn) runs for this wave's
+// frame j = k - lag when there is one.  Readers (lag 0) find frame j's inputs in x and load frame
+// j + 1's into xn; the two buffers alternate with the step's parity, as compile-time choices.
+#ifdef JAAD_DECOR_STAMPS  // profiling build: per-wave busy (body) and total ticks of the steps
+#define DECOR_T(v) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v)::"memory")
+#else
+#define DECOR_T(v)
+#endif
+template <typename Body>
+__device__ __forceinline__ void decor_steps(uint64_t& busy, uint32_t nfr, int lag, float2 (&xa)[32], float2 (&xb)[32],
+                                            Body&& body)
+{
+    [[maybe_unused]] uint64_t t0 = 0, t1 = 0, acc = 0;
+    for (uint32_t k = 0; k < nfr + 2; k += 2) {
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const int64_t j = (int64_t)k + h - lag;
+            DECOR_T(t0);
+            if (j >= 0 && j < (int64_t)nfr) {
+                if ((j & 1) == 0) body((uint32_t)j, xa, xb);
+                else body((uint32_t)j, xb, xa);
+            }
+            DECOR_T(t1);
+            acc += t1 - t0;
+            __syncthreads();
+        }
+    }
+    busy = acc;
+}
+
+__global__ __launch_bounds__(64 * kDecorWaves) __attribute__((amdgpu_waves_per_eu(1, 2))) void ps_decor_kernel(SbrArgs A)
+{
+    const uint32_t run = blockIdx.x;
+    const uint32_t* fl = A.ps_list + A.runs[2 * run];
+    const uint32_t nfr = A.runs[2 * run + 1];
+    if (nfr == 0) return;  // uniform over the block
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    __shared__ PsConst Ks;
+    __shared__ uint32_t pbuf[2][kPsFrameDw];
+    __shared__ DecorLds L;
+    {
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(A.psc);
+        uint32_t* dst = reinterpret_cast<uint32_t*>(&Ks);
+        for (int i = threadIdx.x; i < (int)(sizeof(PsConst) / 4); i += 64 * kDecorWaves) dst[i] = src[i];
+    }
+    __syncthreads();
+    PsState& S = A.pss[A.recs[fl[0]].slot];
+    const PsConst& K = Ks;
+    const bool fresh = S.init == 0;
+    const float2 zero = make_float2(0.0f, 0.0f);
+    float2 xa[32], xb[32];
+    uint64_t busy = 0;
+#ifdef JAAD_DECOR_STAMPS
+    uint64_t t_start;
+    DECOR_T(t_start);
+#endif
+
+    // role of this wave: 0..2 QMF links, 3..5 hybrid links, 6 transient detector, 7 parameter
+    // scan.  Waves w and w + 4 share a SIMD when waves are placed round robin, so the roles are
+    // paired for similar issue counts per step (profiles/round4_decor_stamps.txt):
+    // (hybrid 0, hybrid 1), (QMF 0, hybrid 2), (QMF 1, scan), (QMF 2, transient).
+#ifndef JAAD_DECOR_ROLES_PLAIN
+    constexpr int kRole[kDecorWaves] = {3, 0, 1, 2, 4, 5, 7, 6};
+#else
+    constexpr int kRole[kDecorWaves] = {0, 1, 2, 3, 4, 5, 6, 7};
+#endif
+    const int role = kRole[wave];
+    if (role <= 5) {
+        const int u = lane_id_fresh();
+        // ---- all-pass waves: QMF bands (waves 0-2, lane = band) / hybrid groups (3-5, lane = group)
+        const bool hyb = role >= 3;
+        const int link = hyb ? role - 3 : role;
+        const int sb = hyb && u < 10 ? kBorder[u] : 0;
+        // lanes that run the chain: every QMF lane (bands >= 23 too: v1 kept their rings running,
+        // so the exported slot state is the same), the hybrid lanes with a group
+        const bool act = hyb ? u < 10 : true;
+        float phi[2], q[2], g;
+        if (!hyb) {
+            float slope = 1.0f;
+            if (u > 3) {
+                const int decay = 3 - u;
+                slope = decay <= -20 ? 0.0f : 1.0f + kDecaySlope * (float)decay;
+            }
+            phi[0] = K.phi_qmf[u][0];
+            phi[1] = K.phi_qmf[u][1];
+            q[0] = K.q_qmf[u][link][0];
+            q[1] = K.q_qmf[u][link][1];
+            g = slope * K.filter_a[link];
+        } else {
+            phi[0] = K.phi_sub[sb][0];
+            phi[1] = K.phi_sub[sb][1];
+            q[0] = K.q_sub[sb][link][0];
+            q[1] = K.q_sub[sb][link][1];
+            g = 1.0f * K.filter_a[link];
+        }
+        const int hu = u < 10 ? u : 0;
+        float2* const apst = hyb ? &S.aph[0][hu] : &S.ap[0][u];  // ring k at apst[k * stride]
+        const int apstride = hyb ? 16 : 64;
+        auto st_ap = [&](int k) -> float2& { return apst[k * apstride]; };
+        if (link == 0) {
+            // 2-slot delay + link 0
+            float2 d2[2], r3[3];
+            for (int k = 0; k < 2; k++) d2[k] = zero;
+            for (int k = 0; k < 3; k++) r3[k] = zero;
+            if (!fresh) {
+                for (int k = 0; k < 2; k++) d2[k] = st_ap(k);
+                for (int k = 0; k < 3; k++) r3[k] = st_ap(2 + k);
+            }
+            auto load = [&](float2 (&x)[32], uint32_t f) {
+                if (!hyb) {
+                    const float2* src = reinterpret_cast<const float2*>(A.xps + (size_t)f * 8192);
+#pragma unroll
+                    for (int n = 0; n < 32; n++) x[n] = src[n * 64 + u];
+                } else {
+                    const float2* src = reinterpret_cast<const float2*>(A.xhl + (size_t)f * 768);
+#pragma unroll
+                    for (int n = 0; n < 32; n++) x[n] = src[n * 12 + sb];
+                }
+            };
+            load(xa, fl[0]);
+            decor_steps(busy, nfr, 0, xa, xb, [&](uint32_t j, float2 (&x)[32], float2 (&xn)[32]) __attribute__((always_inline)) {
+                const int u = lane_id_fresh();  // per step: a short live range
+                const uint32_t pj = j & 1;
+                if (j + 1 < nfr) load(xn, fl[j + 1]);  // lands during this frame
+                if (!hyb) {
+                    static_for<0, 32>([&](auto I) {
+                        constexpr int n = decltype(I)::value;
+                        L.q01[pj][n][u] = ap_link<0, n>(r3, ap_delay2<n>(d2, x[n], phi), q, g);
+                    });
+                } else if (act) {
+                    static_for<0, 32>([&](auto I) {
+                        constexpr int n = decltype(I)::value;
+                        L.h01[pj][n][u] = ap_link<0, n>(r3, ap_delay2<n>(d2, x[n], phi), q, g);
+                    });
+                }
+                rotate<0, 2, 32 % 2>(d2);
+                rotate<0, 3, 32 % 3>(r3);
+            });
+            if (act) {
+                for (int k = 0; k < 2; k++) st_ap(k) = d2[k];
+                for (int k = 0; k < 3; k++) st_ap(2 + k) = r3[k];
+            }
+        } else if (link == 1) {
+            // link 1 (+ the plain delay lines of QMF bands >= 23: 14 slots to band 34, 1 above, on
+            // the frame's inputs, loaded at the step's start for those lanes and used after link 1)
+            float2 r4[4], dl[14], d1 = zero;
+            for (int k = 0; k < 4; k++) r4[k] = zero;
+            for (int k = 0; k < 14; k++) dl[k] = zero;
+            const bool dlane = !hyb && u >= kApBands, is14 = u < 35;
+            if (!fresh) {
+                for (int k = 0; k < 4; k++) r4[k] = st_ap(5 + k);
+                if (!hyb)
+                    for (int k = 0; k < 14; k++) dl[k] = S.dl[k][u];
+            }
+            d1 = dl[0];
+            auto load = [&](float2 (&x)[32], uint32_t f) {
+                const float2* src = reinterpret_cast<const float2*>(A.xps + (size_t)f * 8192);
+#pragma unroll
+                for (int n = 0; n < 32; n++) x[n] = src[n * 64 + u];
+            };
+            decor_steps(busy, nfr, 1, xa, xb, [&](uint32_t j, float2 (&)[32], float2 (&)[32]) __attribute__((always_inline)) {
+                const int u = lane_id_fresh();  // per step: a short live range
+                const uint32_t f = fl[j], pj = j & 1;
+                if (!hyb) {
+                    float2 x[32];
+                    load(x, f);  // lands during link 1
+                    static_for<0, 32>([&](auto I) {
+                        constexpr int n = decltype(I)::value;
+                        L.q12[pj][n][u] = ap_link<1, n>(r4, L.q01[pj][n][u], q, g);
+                    });
+                    rotate<0, 4, 32 % 4>(r4);
+                    float2* dst = reinterpret_cast<float2*>(A.xps + (size_t)f * 8192) + 2048;
+                    constexpr uint64_t kIs14 = (1ull << 35) - 1;  // lanes (bands) < 35: 14-slot delay
+                    static_for<0, 32>([&](auto I) {
+                        constexpr int n = decltype(I)::value;
+                        const float2 rl = lane_sel(kIs14, dl[n % 14], d1);
+                        dl[n % 14] = lane_sel(kIs14, x[n], dl[n % 14]);
+                        d1 = x[n];
+                        if (dlane) dst[n * 64 + u] = rl;
+                    });
+                    rotate<0, 14, 32 % 14>(dl);
+                } else {
+                    if (act) {
+                        static_for<0, 32>([&](auto I) {
+                            constexpr int n = decltype(I)::value;
+                            L.h12[pj][n][u] = ap_link<1, n>(r4, L.h01[pj][n][u], q, g);
+                        });
+                        rotate<0, 4, 32 % 4>(r4);
+                    }
+                    if (u < 20) {  // G_TransientRatio (PSImpl.java:264-269), one frame behind role 6
+                        float* dst = A.pg + (size_t)f * 640;
+#pragma unroll
+                        for (int n = 0; n < 32; n++) {
+                            const float2 t = L.tr[pj][n][u];
+                            dst[n * 20 + u] = t.x <= t.y ? 1.0f : __fdiv_rn(t.y, t.x);
+                        }
+                    }
+                }
+            });
+            if (act)
+                for (int k = 0; k < 4; k++) st_ap(5 + k) = r4[k];
+            if (!hyb) {
+                if (!is14) dl[0] = d1;
+                for (int k = 0; k < 14; k++) S.dl[k][u] = dl[k];
+            }
+        } else {
+            float2 r5[5];
+            for (int k = 0; k < 5; k++) r5[k] = zero;
+            if (!fresh)
+                for (int k = 0; k < 5; k++) r5[k] = st_ap(9 + k);
+            decor_steps(busy, nfr, 2, xa, xb, [&](uint32_t j, float2 (&)[32], float2 (&)[32]) {
+                const int u = lane_id_fresh();  // per step: a short live range
+                const uint32_t f = fl[j], pj = j & 1;
+                if (!act) return;
+                if (!hyb) {
+                    float2* dst = reinterpret_cast<float2*>(A.xps + (size_t)f * 8192) + 2048;
+                    static_for<0, 32>([&](auto I) {
+                        constexpr int n = decltype(I)::value;
+                        const float2 o = ap_link<2, n>(r5, L.q12[pj][n][u], q, g);
+                        if (u >= 3 && u < kApBands) dst[n * 64 + u] = o;
+                    });
+                } else {
+                    float2* dst = reinterpret_cast<float2*>(A.xhr + (size_t)f * 768);
+                    static_for<0, 32>([&](auto I) {
+                        constexpr int n = decltype(I)::value;
+                        dst[n * 12 + sb] = ap_link<2, n>(r5, L.h12[pj][n][u], q, g);
+                    });
+                }
+                rotate<0, 5, 32 % 5>(r5);
+            });
+            if (act)
+                for (int k = 0; k < 5; k++) st_ap(9 + k) = r5[k];
+        }
+    } else if (role == 6) {
+        const int u = lane_id_fresh();
+        // ---- transient detector recurrences (lane = parameter band), PSImpl.java:238-270 ----
+        const bool act = u < 20;
+        const int pu = act ? u : 0;
+        float peak = fresh ? 0.0f : S.peak[pu], smooth = fresh ? 0.0f : S.smooth[pu], pprev = fresh ? 0.0f : S.pprev[pu];
+        auto load = [&](float2 (&x)[32], uint32_t f) {
+            const float* src = A.pg + (size_t)f * 640;
+#pragma unroll
+            for (int n = 0; n < 32; n++) x[n].x = src[n * 20 + pu];
+        };
+        load(xa, fl[0]);
+        decor_steps(busy, nfr, 0, xa, xb, [&](uint32_t j, float2 (&x)[32], float2 (&xn)[32]) __attribute__((always_inline)) {
+                const int u = lane_id_fresh();  // per step: a short live range
+            const uint32_t pj = j & 1;
+            if (j + 1 < nfr) load(xn, fl[j + 1]);
+#pragma unroll
+            for (int n = 0; n < 32; n++) {
+                const float Pn = x[n].x;
+                const float gamma = 1.5f;
+                peak = (peak * kAlphaDecay);
+                if (peak < Pn) peak = Pn;
+                float sm = smooth;
+                sm += ((peak - Pn - smooth) * kAlphaSmooth);
+                smooth = sm;
+                float nrg = pprev;
+                nrg += ((Pn - pprev) * kAlphaSmooth);
+                pprev = nrg;
+                if (act) L.tr[pj][n][u] = make_float2((sm * gamma), nrg);
+            }
+        });
+        if (act) {
+            S.peak[u] = peak;
+            S.smooth[u] = smooth;
+            S.pprev[u] = pprev;
+        }
+    } else {
+        const int u = lane_id_fresh();
+        // ---- mixing-parameter scan ----
+        const bool act = u < 20;
+        uint32_t sc_pre[kPsFrameDwPerLane];
+        int sc_grs[2], sc_phase;
+        float sc_hp[2][8], sc_ipd[2][2], sc_opd[2][2];
+        const ScanCtx SC{A, K, fl, nfr, S, act ? u : 0, pbuf};
+        const ScanArrays SZ{sc_pre, sc_grs, sc_hp, sc_ipd, sc_opd, sc_phase};
+        if (act) scan_init(SC, SZ, fresh);
+        decor_steps(busy, nfr, 0, xa, xb, [&](uint32_t j, float2 (&)[32], float2 (&)[32]) {
+                const int u = lane_id_fresh();  // per step: a short live range
+            if (act) scan_frame(SC, SZ, j);
+        });
+        if (act) scan_finish(SC, SZ);
+    }
+#ifdef JAAD_DECOR_STAMPS
+    uint64_t t_end;
+    DECOR_T(t_end);
+    if (A.dbg && lane_id_fresh() == 0) {
+        uint32_t* d = reinterpret_cast<uint32_t*>(A.dbg) + 4096 + (blockIdx.x * kDecorWaves + wave) * 4;
+        d[0] = (uint32_t)busy;
+        d[1] = (uint32_t)(t_end - t_start);
+        d[2] = (uint32_t)kRole[wave];
+        d[3] = nfr;
+    }
+#endif
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -780,7 +1192,11 @@ hipError_t launch_ps(const SbrArgs& a, hipStream_t stream)
     if (!a.n_runs) return hipSuccess;
     const dim3 g((a.n_cf + kPsWaves - 1) / kPsWaves);
     hipLaunchKernelGGL(ps_analysis_kernel, g, dim3(64 * kPsWaves), 0, stream, a);
-    hipLaunchKernelGGL(ps_decor_kernel, dim3(a.n_runs), dim3(256), 0, stream, a);
+#ifdef JAAD_DECOR_V1
+    hipLaunchKernelGGL(ps_decor_kernel_v1, dim3(a.n_runs), dim3(256), 0, stream, a);
+#else
+    hipLaunchKernelGGL(ps_decor_kernel, dim3(a.n_runs), dim3(64 * kDecorWaves), 0, stream, a);
+#endif
     hipLaunchKernelGGL(ps_mix_kernel, g, dim3(64 * kPsWaves), 0, stream, a);
     hipLaunchKernelGGL(ps_state_kernel, dim3(a.n_runs), dim3(64), 0, stream, a);
     return hipGetLastError();

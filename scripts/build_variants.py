@@ -17,7 +17,9 @@ VARIANTS = {
     "e_w16c": (["JAAD_LDS_COMPACT", "JAAD_LC_WAVES=16"], [], None),
     "f_w12c": (["JAAD_LDS_COMPACT"], [], None),
     "g_w8": (["JAAD_LC_WAVES=8"], [], None),
-    "c_sfcb": (["JAAD_SFCB_LOADS"], [], None),
+    "d_v1": (["JAAD_DECOR_V1"], [], None),
+    "d_plain": (["JAAD_DECOR_ROLES_PLAIN"], [], None),
+    "d_stamps": (["JAAD_DECOR_STAMPS"], [], None),
     "h_w4": (["JAAD_LC_WAVES=4"], [], None),
 }
 
