@@ -40,12 +40,25 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # + 4096 PCM) = 15296; C5 (mono core + SBR + PS -> stereo) = 2048 q + 188 gains + 16 side + 1300 SBR
 # params + 352 PS params + 8192 PCM = 12096
 ALGO_BYTES = {2: 8624, 3: 8624, 4: 15296, 5: 12096}
-# C4 / C5 are compute-leaning (~26 and ~49 flop/B): graded against the FP32 VALU
-# roof (MFMA unused) with an algorithmic flop count per frame: core IMDCT ~33k per ch-frame, QMF
-# analysis ~58k, HF generation ~40k, HF adjustment ~22k, 64-band synthesis ~123k per ch-frame;
-# C5 = one core/SBR channel + PS (hybrid analysis, decorrelation, mixing, hybrid synthesis) + two
-# synthesis channels, ~590k
-ALGO_FLOPS = {4: 2 * (33e3 + 58e3 + 40e3 + 22e3 + 123e3), 5: 590e3}
+# C4 / C5 are compute-leaning: graded against the FP32 VALU roof (MFMA unused) with
+# the binary32 operations the reference performs per frame, counted from its loops (round 4, from
+# the restatement oracle/jaad_oracle*.c, which follows them operation for operation; C4/C5 headers:
+# kx 13, M 32, 2 envelopes, interpol_freq on, smoothing off):
+#   core (24 kHz, per channel): IQ 1k + IMDCT (pre/post twiddle 2 x 3.1k, 512-point IFFT 20k) +
+#       window/OLA 3.1k                                                             = 30k
+#   QMF analysis, 32 slots: 64 x 5-tap window (576) + DCT-IV (pre 192, 32-point FFT 544,
+#       post 192) + output scaling (64)                                 = 1.57k/slot = 50k
+#   HF generation, 32 high bands: autocorrelation over 38 slots (790) + prediction
+#       coefficients (30) + 32 slots of the 2nd-order predictor (516)   = 1.34k/band = 43k
+#   HF adjustment: envelope estimate (4.1k) + gains/limiter/boost incl. 3 square roots per band
+#       and envelope (1.6k) + assembly (32 x 32 x 10)                               = 16k
+#   64-band synthesis, 32 slots: 2 DCT-IV (1.86k) + v-block butterflies (128) + 64 x 10-tap
+#       window (1.22k) + input scaling (64)                             = 3.26k/slot = 104k
+#   PS (C5): hybrid analysis 10k, decorrelation (all-pass chains of 23 QMF bands + 10 hybrid
+#       groups, 48 per slot each: 51k; transient detector 11k), parameter scan 5k, mixing incl.
+#       IPD/OPD rotation (71 bands x 24 per slot: 55k), hybrid synthesis 1k          = 133k
+# C4 = 2 channels x 243k = 486k; C5 = one core/SBR channel (139k) + PS + two synthesis channels
+ALGO_FLOPS = {4: 2 * (30e3 + 50e3 + 43e3 + 16e3 + 104e3), 5: (30e3 + 50e3 + 43e3 + 16e3) + 133e3 + 2 * 104e3}
 VALU_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 vector peak
 
 WORKLOADS = {
