@@ -23,6 +23,7 @@
 
 #include <type_traits>
 
+#include "jaad_ps_mix.h"
 #include "jaad_sbr.h"
 #include "jaad_wave.h"
 
@@ -976,7 +977,7 @@ __global__ __launch_bounds__(64 * kDecorWaves) __attribute__((amdgpu_waves_per_e
         };
         load(xa, fl[0]);
         decor_steps(busy, nfr, 0, xa, xb, [&](uint32_t j, float2 (&x)[32], float2 (&xn)[32]) __attribute__((always_inline)) {
-                const int u = lane_id_fresh();  // per step: a short live range
+            const int u = lane_id_fresh();  // per step: a short live range
             const uint32_t pj = j & 1;
             if (j + 1 < nfr) load(xn, fl[j + 1]);
 #pragma unroll
@@ -1010,7 +1011,6 @@ __global__ __launch_bounds__(64 * kDecorWaves) __attribute__((amdgpu_waves_per_e
         const ScanArrays SZ{sc_pre, sc_grs, sc_hp, sc_ipd, sc_opd, sc_phase};
         if (act) scan_init(SC, SZ, fresh);
         decor_steps(busy, nfr, 0, xa, xb, [&](uint32_t j, float2 (&)[32], float2 (&)[32]) {
-                const int u = lane_id_fresh();  // per step: a short live range
             if (act) scan_frame(SC, SZ, j);
         });
         if (act) scan_finish(SC, SZ);
@@ -1031,53 +1031,22 @@ __global__ __launch_bounds__(64 * kDecorWaves) __attribute__((amdgpu_waves_per_e
 // ---------------------------------------------------------------------------------------------
 // mixing (PSImpl.ps_mix_phase :592-679) + hybrid synthesis (A/ps/Filterbank.java:70-86)
 // ---------------------------------------------------------------------------------------------
-// Walk the 32 slots of a frame for one (sub)band of group gr (inputs already in registers): H
-// advances by its delta every slot and restarts at each envelope border, as the Java interpolates.
-// hbf: the frame's H start/delta rows (in LDS); bw: border_position[0..5] as bytes
-template <typename Store>
-__device__ __forceinline__ void mix_band(const float* hbf, uint64_t bw, int gr, bool rot, const float2 (&l)[32],
-                                         const float2 (&r0)[32], const float (&G)[32], Store&& store)
-{
-    float H[8], D[8];
-    int env = 0, next = 0;
-#pragma unroll
-    for (int n = 0; n < 32; n++) {
-        if (n == next) {  // uniform: the borders are per frame
-            const float* hv = hbf + (env * 22 + gr) * 16;
-#pragma unroll
-            for (int k = 0; k < 8; k++) {
-                H[k] = hv[k];
-                D[k] = hv[8 + k];
-            }
-            env++;
-            next = (int)((bw >> (8 * env)) & 255u);
-        }
-#pragma unroll
-        for (int k = 0; k < 4; k++) H[k] += D[k];
-        if (rot)
-#pragma unroll
-            for (int k = 4; k < 8; k++) H[k] += D[k];
-        const float2 x = l[n];
-        const float2 r = make_float2((G[n] * r0[n].x), (G[n] * r0[n].y));
-        float2 ol = make_float2((H[0] * x.x) + (H[2] * r.x), (H[0] * x.y) + (H[2] * r.y));
-        float2 orr = make_float2((H[1] * x.x) + (H[3] * r.x), (H[1] * x.y) + (H[3] * r.y));
-        if (rot) {
-            ol.x -= (H[4] * x.y) + (H[6] * r.y);
-            ol.y += (H[4] * x.x) + (H[6] * r.x);
-            orr.x -= (H[5] * x.y) + (H[7] * r.y);
-            orr.y += (H[5] * x.x) + (H[7] * r.x);
-        }
-        store(n, ol, orr);
-    }
-}
-
+// One wave per frame, in place on xps.  QMF bands 3..63 (lane = band), then the hybrid groups
+// (lane = sub-band), each as four chunks of 8 slots with the next chunk's inputs in flight while
+// this one mixes (two 8-slot buffers instead of all 32 slots in registers: 4 waves/SIMD); H walks
+// the slots in order (PsHWalk: restart at each envelope border, one delta step per slot).
 static_assert(offsetof(jaad_ps_frame, num_env) == 2 && offsetof(jaad_ps_frame, nr_ipdopd_par) == 3 &&
                   offsetof(jaad_ps_frame, border) == 4 && sizeof(jaad_ps_frame) % 4 == 0,
               "ps_mix_kernel reads the frame header as three dwords");
 
+constexpr int kMixChunk = 8;
 struct MixLds {
-    float2 ml[32][12], mr[32][12];
-    float4 hb[5 * 22 * 16 / 4];  // the frame's H start/delta rows (ps_decor_kernel's hb)
+    float4 hb[5 * 22 * 16 / 4];                 // the frame's H start/delta rows (ps_decor_kernel's hb)
+    float2 ml[kMixChunk][12], mr[kMixChunk][12];  // a chunk's mixed sub-bands (hybrid synthesis)
+};
+struct MixBuf {
+    float2 x[kMixChunk], r[kMixChunk];
+    float G[kMixChunk];
 };
 
 __global__ __launch_bounds__(256) void ps_mix_kernel(SbrArgs A)
@@ -1106,62 +1075,101 @@ __global__ __launch_bounds__(256) void ps_mix_kernel(SbrArgs A)
     const float* pg = A.pg + (size_t)f * 640;
     float2* xl = reinterpret_cast<float2*>(A.xps + (size_t)f * 8192);
     float2* xr = xl + 2048;
-    // ---- QMF bands 3..63 (lane = band), then hybrid groups 0..9 (lane = group, one sub-band
-    // each, into LDS); all 32 slots of inputs are loaded before the mixing walk ----
+    // (chunks c = 0..3 unrolled, so the two buffers are compile-time choices)
+    auto chunks = [&](auto&& load, auto&& mix) {
+        MixBuf b0, b1;
+        load(b0, 0);
+        static_for<0, 4>([&](auto C) {
+            constexpr int c = decltype(C)::value;
+            MixBuf& cur = (c & 1) ? b1 : b0;
+            MixBuf& nxt = (c & 1) ? b0 : b1;
+            if constexpr (c < 3) load(nxt, kMixChunk * (c + 1));
+            mix(cur, kMixChunk * c);
+        });
+    };
+    // ---- QMF bands 3..63, lane = band ----
+    if (u >= 3) {
+        const int gr = ps_qmf_group(u), bk = gr - 2;
+        const bool rot = bk < nr;
+        PsHWalk W;
+        W.begin();
+        chunks(
+            [&](MixBuf& b, int s0) {
+#pragma unroll
+                for (int i = 0; i < kMixChunk; i++) {
+                    b.x[i] = xl[(s0 + i) * 64 + u];
+                    b.r[i] = xr[(s0 + i) * 64 + u];
+                    b.G[i] = pg[(s0 + i) * 20 + bk];
+                }
+            },
+            [&](const MixBuf& b, int s0) {
+#pragma unroll
+                for (int i = 0; i < kMixChunk; i++) {
+                    const int n = s0 + i;
+                    W.step(hbf, bw, gr, rot, n);
+                    float2 ol, orr;
+                    ps_mix_slot(W.H, rot, b.x[i], b.r[i], b.G[i], ol, orr);
+                    xl[n * 64 + u] = ol;
+                    xr[n * 64 + u] = orr;
+                }
+            });
+    }
+    // ---- hybrid groups 0..9 (lane = group, sub-band kBorder[group]) and sub-bands 4, 5 (zero
+    // after grouping, never decorrelated or mixed), a chunk at a time into LDS, then the hybrid
+    // synthesis of the chunk's slots (lane = slot + 8 channel) into bands 0..2 ----
     const float2* hl = reinterpret_cast<const float2*>(A.xhl + (size_t)f * 768);
     const float2* hr = reinterpret_cast<const float2*>(A.xhr + (size_t)f * 768);
-    {
-        float2 l[32], r[32];
-        float G[32];
-        if (u >= 3) {
-            int gr = 10;
-            for (int g = 10; g < 22; g++)
-                if (u >= kBorder[g]) gr = g;
-            const int bk = gr - 2;
+    const int t = u < 12 ? u : 0;
+    const int sb = t < 10 ? kBorder[t] : t - 6, bk = t < 10 ? group_bk(t) : 0;
+    const bool rot = bk < nr;
+    PsHWalk W;
+    W.begin();
+    chunks(
+        [&](MixBuf& b, int s0) {
 #pragma unroll
-            for (int n = 0; n < 32; n++) {
-                l[n] = xl[n * 64 + u];
-                r[n] = xr[n * 64 + u];
-                G[n] = pg[n * 20 + bk];
+            for (int i = 0; i < kMixChunk; i++) {
+                b.x[i] = hl[(s0 + i) * 12 + sb];
+                b.r[i] = hr[(s0 + i) * 12 + sb];
+                b.G[i] = pg[(s0 + i) * 20 + bk];
             }
-            mix_band(hbf, bw, gr, bk < nr, l, r, G,
-                     [&](int n, float2 a, float2 b) { xl[n * 64 + u] = a; xr[n * 64 + u] = b; });
-        }
-        if (u < 10) {
-            const int sb = kBorder[u], bk = group_bk(u);
+        },
+        [&](const MixBuf& b, int s0) {
+            if (u < 10) {
 #pragma unroll
-            for (int n = 0; n < 32; n++) {
-                l[n] = hl[n * 12 + sb];
-                r[n] = hr[n * 12 + sb];
-                G[n] = pg[n * 20 + bk];
+                for (int i = 0; i < kMixChunk; i++) {
+                    W.step(hbf, bw, t, rot, s0 + i);
+                    float2 ol, orr;
+                    ps_mix_slot(W.H, rot, b.x[i], b.r[i], b.G[i], ol, orr);
+                    L.ml[i][sb] = ol;
+                    L.mr[i][sb] = orr;
+                }
+            } else if (u < 12) {
+#pragma unroll
+                for (int i = 0; i < kMixChunk; i++) {
+                    L.ml[i][sb] = b.x[i];
+                    L.mr[i][sb] = make_float2(0.0f, 0.0f);
+                }
             }
-            mix_band(hbf, bw, u, bk < nr, l, r, G,
-                     [&](int n, float2 a, float2 b) { L.ml[n][sb] = a; L.mr[n][sb] = b; });
-        } else if (u < 12) {  // sub-bands 4, 5: zero after grouping, never decorrelated or mixed
-            const int sb = u - 6;
-            for (int n = 0; n < 32; n++) {
-                L.ml[n][sb] = hl[n * 12 + sb];
-                L.mr[n][sb] = make_float2(0.0f, 0.0f);
+            wave_sync();
+            if (u < 2 * kMixChunk) {
+                const int i = u & (kMixChunk - 1), n = s0 + i;
+                const float2* m = u < kMixChunk ? L.ml[i] : L.mr[i];
+                float2* x = u < kMixChunk ? xl : xr;
+                constexpr int res[3] = {8, 2, 2};
+#pragma unroll
+                for (int band = 0, off = 0; band < 3; band++) {
+                    float re = 0.0f, im = 0.0f;  // (0 + the first term: -0 becomes +0, as in the Java)
+#pragma unroll
+                    for (int k = 0; k < res[band]; k++) {
+                        re += m[off + k].x;
+                        im += m[off + k].y;
+                    }
+                    x[n * 64 + band] = make_float2(re, im);
+                    off += res[band];
+                }
             }
-        }
-    }
-    wave_sync();
-    // ---- hybrid synthesis (lane = slot; 0..31 left, 32..63 right) into bands 0..2 ----
-    {
-        const int n = u & 31;
-        const float2* m = u < 32 ? L.ml[n] : L.mr[n];
-        float2* x = u < 32 ? xl : xr;
-        const int res[3] = {8, 2, 2};
-        for (int band = 0, off = 0; band < 3; band++) {
-            float re = 0.0f, im = 0.0f;
-            for (int k = 0; k < res[band]; k++) {
-                re += m[off + k].x;
-                im += m[off + k].y;
-            }
-            x[n * 64 + band] = make_float2(re, im);
-            off += res[band];
-        }
-    }
+            wave_sync();  // (the next chunk rewrites ml / mr)
+        });
 }
 
 // ---------------------------------------------------------------------------------------------
