@@ -605,7 +605,29 @@ __device__ __forceinline__ void imdct_long_pk(float* const (&bufs)[N], const Lds
     const int b = u >> 3;
     if constexpr (N == 2) fft_3stages_pk2(c[0], c[1], [&](int j) { return ld2(T.tw2[j][b]); });
     else fft_3stages_pk(c[0], [&](int j) { return ld2(T.tw2[j][b]); });
-#ifndef JAAD_XCH_NOVCC
+#if defined(JAAD_X3_LDS)
+    if constexpr (N == 2) {
+        // experiment: the three exchanges as one 8 x 8 transpose per 8-lane group through LDS (the
+        // spectrum buffers are free once the pre-twiddle has read them): after it lane g8 + r,
+        // register s holds what lane g8 + rev3(s), register rev3(r) held.  Row stride 9 (f2).
+        const int g = u >> 3, r = u & 7;
+        const int rr = ((r & 1) << 2) | (r & 2) | (r >> 2);
+        wave_sync();
+#pragma unroll
+        for (int n = 0; n < N; n++) {
+            f2* Tn = reinterpret_cast<f2*>(bufs[n]) + 72 * g;
+#pragma unroll
+            for (int s = 0; s < 8; s++) Tn[9 * r + s] = c[n][s];
+        }
+        wave_sync();
+#pragma unroll
+        for (int n = 0; n < N; n++) {
+            const f2* Tn = reinterpret_cast<const f2*>(bufs[n]) + 72 * g + rr;
+#pragma unroll
+            for (int s = 0; s < 8; s++) c[n][s] = Tn[9 * (((s & 1) << 2) | (s & 2) | (s >> 2))];
+        }
+    } else
+#elif !defined(JAAD_XCH_NOVCC)
     if constexpr (N == 2) {
         xch_bit_pair<0, 2>(c[0], c[1]);  // e bit 6 (lane bit 2) <-> e bit 3
         xch_bit_pair<1, 1>(c[0], c[1]);  // e bit 7 (lane bit 1) <-> e bit 4

@@ -20,6 +20,7 @@ VARIANTS = {
     "d_v1": (["JAAD_DECOR_V1"], [], None),
     "d_plain": (["JAAD_DECOR_ROLES_PLAIN"], [], None),
     "d_stamps": (["JAAD_DECOR_STAMPS"], [], None),
+    "x3lds": (["JAAD_X3_LDS"], [], None),
     "h_w4": (["JAAD_LC_WAVES=4"], [], None),
 }
 
