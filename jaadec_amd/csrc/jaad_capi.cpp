@@ -219,6 +219,7 @@ struct jaad_ctx {
     int n_cu = 256;
     uint32_t lc_waves = 0;       // LC kernel waves resident on the whole device (one per chunk)
     uint32_t chunk_frames = 0;   // 0 = size chunks from lc_waves; JAAD_CHUNK_FRAMES overrides
+    uint32_t syn_frames = 0;     // 0 = kSbrSynFrames frames per synthesis chunk; JAAD_SYN_FRAMES overrides
     float* dbg = nullptr;
     int dbg_frame = 0;
     std::string err;
@@ -564,17 +565,23 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
     const size_t nr = fmap.size(), ncf = nr * nch;  // records, record ch-frames
     const bool identity = ups.empty();
 
-    // chunk plan (records of each run)
+    // chunk plan (records of each run).  Synthesis chunks: one wave each, its 9-slot v history
+    // recomputed, a run's records split into chunks of equal length (+-1) of about kSbrSynFrames.
+    // (Round 4: chunks sized to fill the resident waves once -- 13 frames on C4 -- ran 10 % slower
+    // than 4-frame chunks in 3+ rounds: the synthesis is latency-bound per wave.)
     ctx->sbr_chunks.clear();
     ctx->sbr_last.clear();
     ctx->ps_runs.clear();
+    const uint32_t syn_len = std::min<uint32_t>(ctx->syn_frames ? ctx->syn_frames : (uint32_t)kSbrSynFrames, 0xffff);
     for (uint32_t r = 0; r < b->n_runs; r++) {
         const uint32_t i0 = rbeg[r], i1 = rbeg[r + 1];
         if (i1 == i0) continue;  // no SBR frame in this call: the slot's SBR state stays as it is
+        const uint32_t len = i1 - i0, parts = (len + syn_len - 1) / syn_len;
         for (int c = 0; c < och; c++)
-            for (uint32_t i = i0; i < i1; i += kSbrSynFrames) {
-                const uint32_t n = i1 - i < (uint32_t)kSbrSynFrames ? i1 - i : (uint32_t)kSbrSynFrames;
-                ctx->sbr_chunks.push_back(SbrChunk{i, (uint16_t)n, (uint8_t)c, 0});
+            for (uint32_t k = 0; k < parts; k++) {
+                const uint32_t a = i0 + (uint32_t)((uint64_t)len * k / parts);
+                const uint32_t e = i0 + (uint32_t)((uint64_t)len * (k + 1) / parts);
+                ctx->sbr_chunks.push_back(SbrChunk{a, (uint16_t)(e - a), (uint8_t)c, 0});
             }
         for (int c = 0; c < nch; c++) ctx->sbr_last.push_back((i1 - 1) * nch + c);
         if (ps) {
@@ -1220,6 +1227,7 @@ int jaad_ctx_create(const jaad_stream_cfg* cfg, uint32_t n_slots, int device, ja
     ctx->n_cu = prop.multiProcessorCount;
     ctx->slot_used.assign(n_slots, 0);
     if (const char* ev = std::getenv("JAAD_CHUNK_FRAMES")) ctx->chunk_frames = (uint32_t)std::atoi(ev);
+    if (const char* ev = std::getenv("JAAD_SYN_FRAMES")) ctx->syn_frames = (uint32_t)std::atoi(ev);
     auto bail = [&](hipError_t e, const char* what) {
         std::fprintf(stderr, "jaad_ctx_create: %s: %s\n", what, hipGetErrorString(e));
         jaad_ctx_destroy(ctx);
