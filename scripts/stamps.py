@@ -25,8 +25,14 @@ nw = 8192
 dbg = torch.zeros(nw * 16, dtype=torch.int32, device=dev)
 N.lib().jaad__debug_attach.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
 N.lib().jaad__debug_attach(ctx.h, dbg.data_ptr(), -1)
-for _ in range(3):
-    ctx.decode_device(ptr, b, pcm.data_ptr(), pcm.numel(), 0, None)
+import time
+t_end = time.perf_counter() + 0.4  # past the clock's load-onset transient, then the measured call
+while time.perf_counter() < t_end:
+    for _ in range(10):
+        ctx.decode_device(ptr, b, pcm.data_ptr(), pcm.numel(), 0, None)
+    torch.cuda.synchronize()
+dbg.zero_()
+ctx.decode_device(ptr, b, pcm.data_ptr(), pcm.numel(), 0, None)
 torch.cuda.synchronize()
 S = dbg.cpu().numpy().view(np.uint32).reshape(nw, 16).astype(np.int64)
 S = S[S.sum(1) > 0]
