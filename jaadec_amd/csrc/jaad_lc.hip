@@ -798,6 +798,46 @@ __device__ __forceinline__ void imdct_short(float* buf, const LdsTables& T, int 
     }
 }
 
+// The same transform in packed FP32 (one register pair per complex value, the long path's
+// primitives: every product and sum is the scalar version's, a - b as a + (-b))
+__device__ __forceinline__ void imdct_short_pk(float* buf, const LdsTables& T, int u, float (&re)[8], float (&im)[8])
+{
+    const int w = u >> 3, b = u & 7;
+    f2 c[8];
+#pragma unroll
+    for (int s = 0; s < 8; s++) {
+        const int k = b + 8 * s;
+        // MDCT.java:39-42: re = in1*c - in0*sn, im = in0*c + in1*sn = cmul((in1, in0), (c, sn))
+        const f2 x = {buf[eo_idx(128 * w + 127 - 2 * k)], buf[eo_idx(128 * w + 2 * k)]};
+        c[s] = cmul(x, ld2(T.mdct_s[k]));
+    }
+    wave_sync();
+    radix4_pk(c[BR3[0]], c[BR3[1]], c[BR3[2]], c[BR3[3]]);
+    radix4_pk(c[BR3[4]], c[BR3[5]], c[BR3[6]], c[BR3[7]]);
+#pragma unroll
+    for (int k = 0; k < 4; k++) bfly_pk(c[BR3[k]], c[BR3[k + 4]], ld2(T.roots_s[8 * k]));
+    f2* X = reinterpret_cast<f2*>(buf);
+    const int t = (int)(__builtin_bitreverse32((uint32_t)b) >> 29);
+#pragma unroll
+    for (int r = 0; r < 8; r++) X[xs(64 * w + 8 * t + r)] = c[BR3[r]];
+    wave_sync();
+#pragma unroll
+    for (int s = 0; s < 8; s++) c[s] = X[xs(64 * w + b + 8 * s)];
+    wave_sync();
+    // stages i = 8, 16, 32 of the 64-point IFFT: roots[k*m], m = 4, 2, 1
+    fft_3stages_pk(c, [&](int j) {
+        const int idx = j == 0 ? 4 * b : (j < 3 ? 2 * (b + 8 * (j - 1)) : b + 8 * (j - 3));
+        return ld2(T.roots_s[idx]);
+    });
+#pragma unroll
+    for (int s = 0; s < 8; s++) {
+        // MDCT.java:48-53: re = t0*c - t1*sn, im = t1*c + t0*sn = cmul((t0, t1), (c, sn))
+        const f2 z = cmul(c[s], ld2(T.mdct_s[b + 8 * s]));
+        re[s] = z.x;
+        im[s] = z.y;
+    }
+}
+
 // window position n (0..255) of short slot (s, j), j = 0..3, and its IMDCT value
 __device__ __forceinline__ void short_slot(int b, int s, int j, const float (&re)[8], const float (&im)[8], int& n,
                                            float& v)
@@ -1176,7 +1216,11 @@ __device__ __forceinline__ void synth_channel(const KernelArgs& A, const LdsTabl
     const FrameCtx fc{ic.seq, ic.shape, ic.shape_prev};
     if (fc.seq == JAAD_EIGHT_SHORT_SEQUENCE) {
         float re[8], im[8];
+#ifdef JAAD_SHORT_SCALAR
         imdct_short(buf, T, u, re, im);
+#else
+        imdct_short_pk(buf, T, u, re, im);
+#endif
         ola_short(buf, T, u, fc, re, im, ov, out);
     } else {
         float* const bufs[1] = {buf};
