@@ -1145,9 +1145,14 @@ __global__ __launch_bounds__(256) void sbr_synthesis_kernel(SbrArgs A)
         S.rows = 9;
         return S;
     };
-    auto load_group = [&](const SynSrc& S, int l0, float (&ga)[4], float (&gb)[4], int (&kl)[4]) {
+    // slots per software-pipeline group: the next group's rows are loaded while this one computes
+#ifndef JAAD_SYN_GROUP
+#define JAAD_SYN_GROUP 4
+#endif
+    constexpr int kG = JAAD_SYN_GROUP;
+    auto load_group = [&](const SynSrc& S, int l0, float (&ga)[kG], float (&gb)[kG], int (&kl)[kG]) {
 #pragma unroll
-        for (int i = 0; i < 4; i++) {
+        for (int i = 0; i < kG; i++) {
             const int l = min(l0 + i, S.rows - 1);  // (rows past the frame's last are not used)
             const bool carry = l < S.t0;
             kl[i] = carry ? S.kprev : 64;
@@ -1171,10 +1176,10 @@ __global__ __launch_bounds__(256) void sbr_synthesis_kernel(SbrArgs A)
             else reinterpret_cast<uint32_t*>(A.pcm)[n] = s16 | (s16 << 16);
         }
     };
-    auto store_group = [&](const SynSrc& S, int l0, const float (&res)[4]) {
+    auto store_group = [&](const SynSrc& S, int l0, const float (&res)[kG]) {
         if (!S.emit) return;
 #pragma unroll
-        for (int i = 0; i < 4; i++) {
+        for (int i = 0; i < kG; i++) {
             const int l = l0 + i;
             if (l >= S.rows) break;
             store_pcm(S, S.n0 + sps * l + u, res[i]);
@@ -1189,25 +1194,25 @@ __global__ __launch_bounds__(256) void sbr_synthesis_kernel(SbrArgs A)
     SynSrc S = history_src();
     SynRec W{};                  // record fields of frame j + 1
     rec_load(0, W);
-    float ga[4] = {0, 0, 0, 0}, gb[4] = {0, 0, 0, 0};
-    int kl[4] = {64, 64, 64, 64};
+    float ga[kG] = {}, gb[kG] = {};
+    int kl[kG];
     load_group(S, 0, ga, gb, kl);
     vmem_drain();
     bool have = true;            // ga/gb hold the rows of the group about to run
     for (int j = -1;;) {
-        for (int l0 = 0; l0 < S.rows; l0 += 4) {
+        for (int l0 = 0; l0 < S.rows; l0 += kG) {
             if (!have) {         // first group after a frame without rows
                 load_group(S, l0, ga, gb, kl);
                 vmem_drain();
             }
             have = false;
-            float na[4] = {0, 0, 0, 0}, nb[4] = {0, 0, 0, 0};
-            int nk[4] = {64, 64, 64, 64};
+            float na[kG] = {}, nb[kG] = {};
+            int nk[kG];
             // the next group: later rows of this frame or the first rows of the next one (only
             // scalar selects branch; the loads themselves are unconditional, a reload of the
             // current rows when there is nothing to fetch)
             SynSrc Sn = S;
-            int ln = l0 + 4;
+            int ln = l0 + kG;
             if (ln >= S.rows) {
                 have = false;
                 if (j + 1 < (int)ck.n) {
@@ -1223,9 +1228,9 @@ __global__ __launch_bounds__(256) void sbr_synthesis_kernel(SbrArgs A)
                 have = true;
             }
             load_group(Sn, ln, na, nb, nk);
-            float res[4] = {0, 0, 0, 0};
+            float res[kG] = {};
 #pragma unroll
-            for (int i = 0; i < 4; i++) {
+            for (int i = 0; i < kG; i++) {
                 if (l0 + i >= S.rows) break;
                 mask(kl[i], ga[i], gb[i]);
                 slot(ga[i], gb[i], S.emit, res[i]);
@@ -1233,7 +1238,7 @@ __global__ __launch_bounds__(256) void sbr_synthesis_kernel(SbrArgs A)
             vmem_drain();
             store_group(S, l0, res);
 #pragma unroll
-            for (int i = 0; i < 4; i++) {
+            for (int i = 0; i < kG; i++) {
                 ga[i] = na[i];
                 gb[i] = nb[i];
                 kl[i] = nk[i];
