@@ -22,7 +22,7 @@ ptr["ms_used"] = None
 ptr["tns"] = None
 pcm = torch.empty(b.n_frames * N.pcm_frame_bytes(0, True), dtype=torch.uint8, device=dev)
 ctx = N.Context(cfg, int(b.stream_slot.max()) + 1)
-W = 12  # waves per run (kDecorWaves)
+W = 8  # waves per run (kDecorWaves; 12 in the mixing-role experiments)
 dbg = torch.zeros(4096 + 256 * W * 4 + 64, dtype=torch.int32, device=dev)
 N.lib().jaad__sbr_debug_attach.argtypes = [C.c_void_p, C.c_void_p]
 N.lib().jaad__sbr_debug_attach(ctx.h, dbg.data_ptr())
