@@ -1253,37 +1253,62 @@ __global__ __launch_bounds__(256) void sbr_synthesis_kernel(SbrArgs A)
 // ---------------------------------------------------------------------------------------------
 // slot state after the last frame of each run
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void sbr_state_kernel(SbrArgs A)
+// A wave's copy of N floats (N % 4 == 0, both ends 16-byte aligned) in two halves: wave_load issues
+// the float4 loads into registers (unconditional: a clamped duplicate instead of a branch per load),
+// wave_store writes them.  sbr_state_kernel issues every load of a slot's state before the first
+// store: copied element by element, each store would make the next load wait a memory round trip
+// behind it (the state and the rows may alias as far as the compiler knows) -- 49 round trips per wave.
+template <int N>
+constexpr int wave_copy_regs() { return (N / 4 + 63) / 64; }
+template <int N>
+__device__ __forceinline__ void wave_load(float4 (&v)[wave_copy_regs<N>()], const float* src, int u)
+{
+    static_assert(N % 4 == 0, "wave_load: float4 units");
+    const float4* s4 = reinterpret_cast<const float4*>(src);
+#pragma unroll
+    for (int i = 0; i < wave_copy_regs<N>(); i++) v[i] = s4[min(u + 64 * i, N / 4 - 1)];
+}
+template <int N>
+__device__ __forceinline__ void wave_store(const float4 (&v)[wave_copy_regs<N>()], float* dst, int u)
+{
+    float4* d4 = reinterpret_cast<float4*>(dst);
+#pragma unroll
+    for (int i = 0; i < wave_copy_regs<N>(); i++)
+        if (u + 64 * i < N / 4) d4[u + 64 * i] = v[i];
+}
+static_assert(offsetof(SbrChState, xcarry) % 16 == 0 && offsetof(SbrChState, xsyn) % 16 == 0 &&
+                  offsetof(SbrChState, gq) % 16 == 0 && sizeof(SbrChState) % 16 == 0,
+              "sbr_state_kernel copies float4s");
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) void sbr_state_kernel(SbrArgs A)
 {
     const uint32_t i = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
     if (i >= A.n_last) return;
     const int u = lane_id();
     const uint32_t cf = A.last_cf[i];
     const int c = (int)(cf % (uint32_t)A.nch);
+    // the record's fields first (vmcnt counts in issue order: a wait for them must not wait for the
+    // rows), then the parts whose source depends on cf alone, in flight while the record arrives
     const SbrRec& R = A.recs[cf];
-    SbrChState& S = A.state[(size_t)R.slot * 2 + c];
-    const float* t = A.time + batch_cf(A, cf) * 1024 + 736;
-    for (int k = u; k < 288; k += 64) S.tail[k] = t[k];
-    if (A.ps) {  // synthesis history of both output channels comes from xps
-        for (int oc = 0; oc < 2; oc++) {
-            // the right channel's synthesis (qmfs1) last ran on the run's last PS frame
-            size_t fs = cf;
-            if (oc == 1 && !(R.flags & kSbrPsOn)) {
-                if (R.ps_back == 0) continue;  // no PS frame in this call: its history stays
-                fs = cf - R.ps_back;
-            }
-            const float* xs = A.xps + (fs * 2 + oc) * 4096 + 23 * 128;
-            SbrChState& T = A.state[(size_t)R.slot * 2 + oc];
-            for (int k = u; k < 9 * 128; k += 64) (&T.xsyn[0][0][0])[k] = xs[k];
-        }
-    } else {
-        const float* xs = A.xsyn + (size_t)cf * 4096 + 23 * 128;
-        for (int k = u; k < 9 * 128; k += 64) (&S.xsyn[0][0][0])[k] = xs[k];
-    }
-    const float* xc = A.xcarry + (size_t)cf * kSbrCarryFloats;
-    for (int k = u; k < kSbrCarryFloats; k += 64) (&S.xcarry[0][0][0])[k] = xc[k];
-    const float* g = A.gq + (size_t)cf * 640;
-    for (int k = u; k < 640; k += 64) (&S.gq[0][0][0])[k] = g[k];
+    const uint32_t slot = R.slot, flags = R.flags, ps_back = R.ps_back;
+    float4 vt[wave_copy_regs<288>()], vc[wave_copy_regs<kSbrCarryFloats>()], vg[wave_copy_regs<640>()];
+    wave_load<288>(vt, A.time + batch_cf(A, cf) * 1024 + 736, u);
+    wave_load<kSbrCarryFloats>(vc, A.xcarry + (size_t)cf * kSbrCarryFloats, u);
+    wave_load<640>(vg, A.gq + (size_t)cf * 640, u);
+    // synthesis history: the channel's own rows, or with PS both output channels' from xps -- the
+    // right channel's synthesis (qmfs1) last ran on the run's last PS frame (none in this call:
+    // its history stays)
+    float4 vs0[wave_copy_regs<9 * 128>()], vs1[wave_copy_regs<9 * 128>()];
+    const bool ps_right = A.ps && ((flags & kSbrPsOn) || ps_back != 0);
+    const size_t fs1 = (flags & kSbrPsOn) ? cf : cf - ps_back;
+    wave_load<9 * 128>(vs0, A.ps ? A.xps + (size_t)cf * 2 * 4096 + 23 * 128 : A.xsyn + (size_t)cf * 4096 + 23 * 128, u);
+    if (A.ps) wave_load<9 * 128>(vs1, A.xps + ((ps_right ? fs1 : cf) * 2 + 1) * 4096 + 23 * 128, u);  // (xps is null without PS)
+    SbrChState& S = A.state[(size_t)slot * 2 + c];
+    wave_store<288>(vt, S.tail, u);
+    wave_store<kSbrCarryFloats>(vc, &S.xcarry[0][0][0], u);
+    wave_store<640>(vg, &S.gq[0][0][0], u);
+    wave_store<9 * 128>(vs0, &S.xsyn[0][0][0], u);  // (PS: c = 0, the left output channel)
+    if (ps_right) wave_store<9 * 128>(vs1, &A.state[(size_t)slot * 2 + 1].xsyn[0][0][0], u);
 }
 
 // ---------------------------------------------------------------------------------------------
