@@ -1,6 +1,7 @@
 // PS mixing step (PSImpl.ps_mix_phase, A/ = aac/src/main/java/net/sourceforge/jaad/aac/,
-// A/ps/PSImpl.java:592-679), shared by the mixing waves of ps_decor_kernel and ps_mix_kernel
-// (jaad_ps.hip).  Both perform the same binary32 operations in the same order (-ffp-contract=off).
+// A/ps/PSImpl.java:592-679) used by ps_mix_kernel (jaad_ps.hip), kept apart so that any other kernel
+// mixing rows (the round-4 fusion experiments) performs the same binary32 operations in
+// the same order (-ffp-contract=off).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -66,28 +67,6 @@ __device__ __forceinline__ void ps_mix_slot(const float (&H)[8], bool rot, float
         ol.y += (H[4] * x.x) + (H[6] * r.x);
         orr.x -= (H[5] * x.y) + (H[7] * r.y);
         orr.y += (H[5] * x.x) + (H[7] * r.x);
-    }
-}
-
-// Slots s0 .. s0 + NS - 1 (those < 32) of one (sub)band, inputs already in registers (x, r0, G
-// indexed by slot - s0, arrays of N >= NS): H walked from slot 0, store(n, l, r) per slot.
-template <int NS, int N, typename Store>
-__device__ __forceinline__ void ps_mix_range(const float* hbf, uint64_t bw, int gr, bool rot, int s0, const float2 (&x)[N],
-                                             const float2 (&r0)[N], const float (&G)[N], Store&& store)
-{
-    static_assert(NS <= N, "ps_mix_range: slot count");
-    PsHWalk W;
-    W.begin();
-#pragma unroll 1
-    for (int n = 0; n < s0; n++) W.step(hbf, bw, gr, rot, n);
-#pragma unroll
-    for (int i = 0; i < NS; i++) {
-        const int n = s0 + i;
-        if (n >= 32) break;
-        W.step(hbf, bw, gr, rot, n);
-        float2 ol, orr;
-        ps_mix_slot(W.H, rot, x[i], r0[i], G[i], ol, orr);
-        store(n, ol, orr);
     }
 }
 
