@@ -60,7 +60,6 @@ __device__ __forceinline__ void wave_sync()
     asm volatile("" ::: "memory");
 }
 
-#ifndef JAAD_LDS_COMPACT
 constexpr int kWaveBuf = 1152;  // floats of LDS per wave
 
 // spectrum layout in a wave's buffer: even bins at [0,576), odd bins at [576,1152), bin-pair
@@ -73,11 +72,6 @@ __device__ __forceinline__ int eo_idx(int p)
 }
 // IFFT transpose layout (complex index): one pad slot every 16 (<= 2-way conflicts, affine)
 __device__ __forceinline__ int xs(int i) { return i + (i >> 4); }
-#else  // experiment: unpadded 4 KiB buffers (16 waves per CU fit the LDS)
-constexpr int kWaveBuf = 1024;
-__device__ __forceinline__ int eo_idx(int p) { return (p & 1) * 512 + (p >> 1); }
-__device__ __forceinline__ int xs(int i) { return i; }
-#endif
 // long-window IFFT transpose layout: slot = sum of per-bit weights {1,2,4,8,16,33,72,138,276}
 // (550 slots).  Additive per bit, so the compile-time index bits of every access fold into the
 // instruction offset; the weights were searched (tools/lds_sim.py model of the gfx950 LDS
@@ -88,73 +82,6 @@ __device__ __forceinline__ int xs_l(int i)
 }
 
 __device__ constexpr int BR3[8] = {0, 4, 2, 6, 1, 5, 3, 7};
-
-// FFT.java:113-130 radix-2 butterfly (inverse twiddle = column 1 = +sin)
-__device__ __forceinline__ void bfly(float& r0, float& i0, float& r1, float& i1, float wr, float wi)
-{
-    float zRe = r1 * wr - i1 * wi;
-    float zIm = r1 * wi + i1 * wr;
-    r1 = r0 - zRe;
-    i1 = i0 - zIm;
-    r0 = r0 + zRe;
-    i0 = i0 + zIm;
-}
-
-// FFT.java:69-108 bottom radix-4 round, inverse direction
-__device__ __forceinline__ void radix4_inv(float& r0, float& i0, float& r1, float& i1, float& r2, float& i2,
-                                           float& r3, float& i3)
-{
-    float aRe = r0 + r1, aIm = i0 + i1;
-    float bRe = r2 + r3, bIm = i2 + i3;
-    float cRe = r0 - r1, cIm = i0 - i1;
-    float dRe = r2 - r3, dIm = i2 - i3;
-    r0 = aRe + bRe;
-    i0 = aIm + bIm;
-    r2 = aRe - bRe;
-    i2 = aIm - bIm;
-    r1 = cRe - dIm;
-    i1 = cIm + dRe;
-    r3 = cRe + dIm;
-    i3 = cIm - dRe;
-}
-
-// Pass 1 on a lane's 8 elements held in bit-reversed order r <-> register BR3[r]:
-// radix-4 on r=0..3 and r=4..7, then the i=4 radix-2 stage with twiddles w[k*wstride], k=0..3.
-__device__ __forceinline__ void fft_pass1(float (&re)[8], float (&im)[8], const float (*w)[2], int wstride)
-{
-    radix4_inv(re[BR3[0]], im[BR3[0]], re[BR3[1]], im[BR3[1]], re[BR3[2]], im[BR3[2]], re[BR3[3]], im[BR3[3]]);
-    radix4_inv(re[BR3[4]], im[BR3[4]], re[BR3[5]], im[BR3[5]], re[BR3[6]], im[BR3[6]], re[BR3[7]], im[BR3[7]]);
-#pragma unroll
-    for (int k = 0; k < 4; k++)
-        bfly(re[BR3[k]], im[BR3[k]], re[BR3[k + 4]], im[BR3[k + 4]], w[k * wstride][0], w[k * wstride][1]);
-}
-
-// Three radix-2 stages on elements (base + b + B*s), s = 0..7: pairs (s,s+1), (s,s+2), (s,s+4).
-// tw(j) returns the twiddle of "slot" j: 0 for the first stage, 1+(s&1) for the second,
-// 3+s for the third (the tables are pre-arranged that way, see build_lds_tables).
-template <typename TW>
-__device__ __forceinline__ void fft_3stages(float (&re)[8], float (&im)[8], TW tw)
-{
-    {
-        float wr, wi;
-        tw(0, wr, wi);
-#pragma unroll
-        for (int s = 0; s < 8; s += 2) bfly(re[s], im[s], re[s + 1], im[s + 1], wr, wi);
-    }
-#pragma unroll
-    for (int e = 0; e < 2; e++) {
-        float wr, wi;
-        tw(1 + e, wr, wi);
-        bfly(re[e], im[e], re[e + 2], im[e + 2], wr, wi);
-        bfly(re[4 + e], im[4 + e], re[6 + e], im[6 + e], wr, wi);
-    }
-#pragma unroll
-    for (int s = 0; s < 4; s++) {
-        float wr, wi;
-        tw(3 + s, wr, wi);
-        bfly(re[s], im[s], re[s + 4], im[s + 4], wr, wi);
-    }
-}
 
 // position of IMDCT output slot o = 2s+h for lane u (MDCT.java:56-80 reorder)
 __device__ __forceinline__ int long_pos(int u, int o)
@@ -347,70 +274,11 @@ __device__ __forceinline__ void xch_hi(float& a, float& b)
 // their own value, set by two s_mov_b32 of a literal (which also give the 2 wait states a DPP
 // read of a freshly written VGPR needs).  Round 4 measured the alternative without VCC (DPP
 // moves under bank masks for bits 2, 3; DPP moves + v_cndmask_b32_e64 on an SGPR-pair mask for
-// bits 0, 1; JAAD_XCH_NOVCC): an instruction micro-benchmark prices the VOP2 select at ~13.9
+// bits 0, 1; measured and removed): an instruction micro-benchmark prices the VOP2 select at ~13.9
 // SIMD cycles against 3.3-3.6 for the other forms (tools/valu_rate.hip,
 // profiles/round4_valu_rate.txt), yet inside this kernel the VCC form is 1-2 % faster per C2
 // batch (same-call A/B over 30 launches, profiles/round4_xch_ab.txt) -- the exchanges are not
 // issue-bound here, and the VCC form needs fewer instructions and temporaries.
-#ifdef JAAD_XCH_NOVCC
-template <int L>
-__device__ __forceinline__ void xch2(f2& a0, f2& b0, f2& a1, f2& b1)
-{
-    if constexpr (L >= 2) {
-        float t0x, t0y, t1x, t1y;
-#define JAAD_XCH_BANK(RLO, BLO, RHI, BHI)                                                               \
-    asm("v_mov_b32 %[t0x], %[b0x]\n\t"                                                                  \
-        "v_mov_b32 %[t0y], %[b0y]\n\t"                                                                  \
-        "v_mov_b32 %[t1x], %[b1x]\n\t"                                                                  \
-        "v_mov_b32 %[t1y], %[b1y]\n\t"                                                                  \
-        "v_mov_b32_dpp %[b0x], %[a0x] " RLO " row_mask:0xf bank_mask:" BLO "\n\t"                       \
-        "v_mov_b32_dpp %[b0y], %[a0y] " RLO " row_mask:0xf bank_mask:" BLO "\n\t"                       \
-        "v_mov_b32_dpp %[b1x], %[a1x] " RLO " row_mask:0xf bank_mask:" BLO "\n\t"                       \
-        "v_mov_b32_dpp %[b1y], %[a1y] " RLO " row_mask:0xf bank_mask:" BLO "\n\t"                       \
-        "v_mov_b32_dpp %[a0x], %[t0x] " RHI " row_mask:0xf bank_mask:" BHI "\n\t"                       \
-        "v_mov_b32_dpp %[a0y], %[t0y] " RHI " row_mask:0xf bank_mask:" BHI "\n\t"                       \
-        "v_mov_b32_dpp %[a1x], %[t1x] " RHI " row_mask:0xf bank_mask:" BHI "\n\t"                       \
-        "v_mov_b32_dpp %[a1y], %[t1y] " RHI " row_mask:0xf bank_mask:" BHI                              \
-        : [a0x] "+v"(a0.x), [a0y] "+v"(a0.y), [a1x] "+v"(a1.x), [a1y] "+v"(a1.y), [b0x] "+v"(b0.x),     \
-          [b0y] "+v"(b0.y), [b1x] "+v"(b1.x), [b1y] "+v"(b1.y), [t0x] "=&v"(t0x), [t0y] "=&v"(t0y),     \
-          [t1x] "=&v"(t1x), [t1y] "=&v"(t1y))
-        // bit 2: clear = banks 0, 2 (0x5), set = banks 1, 3 (0xA); bit 3: clear = banks 0, 1 (0x3)
-        if constexpr (L == 2) JAAD_XCH_BANK("row_ror:12", "0x5", "row_ror:4", "0xa");
-        else JAAD_XCH_BANK("row_ror:8", "0x3", "row_ror:8", "0xc");
-#undef JAAD_XCH_BANK
-    } else {
-        // lanes with bit L set
-        constexpr uint64_t kHi = L == 0 ? 0xAAAAAAAAAAAAAAAAull : 0xCCCCCCCCCCCCCCCCull;
-        float u0x, u0y, u1x, u1y, w0x, w0y, w1x, w1y;
-#define JAAD_XCH_QUAD(QP)                                                                             \
-    asm("s_nop 1\n\t"                                                                                 \
-        "v_mov_b32_dpp %[u0x], %[a0x] " QP " row_mask:0xf bank_mask:0xf\n\t"                          \
-        "v_mov_b32_dpp %[u0y], %[a0y] " QP " row_mask:0xf bank_mask:0xf\n\t"                          \
-        "v_mov_b32_dpp %[u1x], %[a1x] " QP " row_mask:0xf bank_mask:0xf\n\t"                          \
-        "v_mov_b32_dpp %[u1y], %[a1y] " QP " row_mask:0xf bank_mask:0xf\n\t"                          \
-        "v_mov_b32_dpp %[w0x], %[b0x] " QP " row_mask:0xf bank_mask:0xf\n\t"                          \
-        "v_mov_b32_dpp %[w0y], %[b0y] " QP " row_mask:0xf bank_mask:0xf\n\t"                          \
-        "v_mov_b32_dpp %[w1x], %[b1x] " QP " row_mask:0xf bank_mask:0xf\n\t"                          \
-        "v_mov_b32_dpp %[w1y], %[b1y] " QP " row_mask:0xf bank_mask:0xf\n\t"                          \
-        "v_cndmask_b32_e64 %[a0x], %[a0x], %[w0x], %[hi]\n\t"                                         \
-        "v_cndmask_b32_e64 %[a0y], %[a0y], %[w0y], %[hi]\n\t"                                         \
-        "v_cndmask_b32_e64 %[a1x], %[a1x], %[w1x], %[hi]\n\t"                                         \
-        "v_cndmask_b32_e64 %[a1y], %[a1y], %[w1y], %[hi]\n\t"                                         \
-        "v_cndmask_b32_e64 %[b0x], %[u0x], %[b0x], %[hi]\n\t"                                         \
-        "v_cndmask_b32_e64 %[b0y], %[u0y], %[b0y], %[hi]\n\t"                                         \
-        "v_cndmask_b32_e64 %[b1x], %[u1x], %[b1x], %[hi]\n\t"                                         \
-        "v_cndmask_b32_e64 %[b1y], %[u1y], %[b1y], %[hi]"                                             \
-        : [a0x] "+v"(a0.x), [a0y] "+v"(a0.y), [a1x] "+v"(a1.x), [a1y] "+v"(a1.y), [b0x] "+v"(b0.x),   \
-          [b0y] "+v"(b0.y), [b1x] "+v"(b1.x), [b1y] "+v"(b1.y), [u0x] "=&v"(u0x), [u0y] "=&v"(u0y),   \
-          [u1x] "=&v"(u1x), [u1y] "=&v"(u1y), [w0x] "=&v"(w0x), [w0y] "=&v"(w0y), [w1x] "=&v"(w1x),   \
-          [w1y] "=&v"(w1y)                                                                            \
-        : [hi] "s"(kHi))
-        if constexpr (L == 0) JAAD_XCH_QUAD("quad_perm:[1,0,3,2]");
-        else JAAD_XCH_QUAD("quad_perm:[2,3,0,1]");
-#undef JAAD_XCH_QUAD
-    }
-}
-#else  // product form (VOP2 v_cndmask_b32_dpp through VCC)
 template <int L>
 __device__ __forceinline__ void xch2(f2& a0, f2& b0, f2& a1, f2& b1)
 {
@@ -446,7 +314,6 @@ __device__ __forceinline__ void xch2(f2& a0, f2& b0, f2& a1, f2& b1)
     a1 = na1;
     b1 = nb1;
 }
-#endif
 
 // Lane bits 0..3 for 16 register pairs at once (both channels of the lockstep long IMDCT): the
 // same selects as xch2, with VCC set twice per 32 selects instead of twice per 8.
@@ -593,48 +460,16 @@ __device__ __forceinline__ void imdct_long_pk(float* const (&bufs)[N], const Lds
         xch_bit<1, 4>(c[n], u);  // e bit 4 (lane bit 4) <-> e bit 1
         if constexpr (N == 1) xch_bit<2, 3>(c[n], u);  // e bit 5 (lane bit 3) <-> e bit 0
     }
-#ifndef JAAD_XCH_NOVCC
     if constexpr (N == 2) xch_bit_pair<2, 3>(c[0], c[1]);
-#else
-    if constexpr (N == 2) {
-        xch_bit<2, 3>(c[0], u);
-        xch_bit<2, 3>(c[1], u);
-    }
-#endif
     // pass 2: register bits 0,1,2 = e bits 3,4,5; e mod 8 = u >> 3
     const int b = u >> 3;
     if constexpr (N == 2) fft_3stages_pk2(c[0], c[1], [&](int j) { return ld2(T.tw2[j][b]); });
     else fft_3stages_pk(c[0], [&](int j) { return ld2(T.tw2[j][b]); });
-#if defined(JAAD_X3_LDS)
-    if constexpr (N == 2) {
-        // experiment: the three exchanges as one 8 x 8 transpose per 8-lane group through LDS (the
-        // spectrum buffers are free once the pre-twiddle has read them): after it lane g8 + r,
-        // register s holds what lane g8 + rev3(s), register rev3(r) held.  Row stride 9 (f2).
-        const int g = u >> 3, r = u & 7;
-        const int rr = ((r & 1) << 2) | (r & 2) | (r >> 2);
-        wave_sync();
-#pragma unroll
-        for (int n = 0; n < N; n++) {
-            f2* Tn = reinterpret_cast<f2*>(bufs[n]) + 72 * g;
-#pragma unroll
-            for (int s = 0; s < 8; s++) Tn[9 * r + s] = c[n][s];
-        }
-        wave_sync();
-#pragma unroll
-        for (int n = 0; n < N; n++) {
-            const f2* Tn = reinterpret_cast<const f2*>(bufs[n]) + 72 * g + rr;
-#pragma unroll
-            for (int s = 0; s < 8; s++) c[n][s] = Tn[9 * (((s & 1) << 2) | (s & 2) | (s >> 2))];
-        }
-    } else
-#elif !defined(JAAD_XCH_NOVCC)
     if constexpr (N == 2) {
         xch_bit_pair<0, 2>(c[0], c[1]);  // e bit 6 (lane bit 2) <-> e bit 3
         xch_bit_pair<1, 1>(c[0], c[1]);  // e bit 7 (lane bit 1) <-> e bit 4
         xch_bit_pair<2, 0>(c[0], c[1]);  // e bit 8 (lane bit 0) <-> e bit 5
-    } else
-#endif
-    {
+    } else {
 #pragma unroll
         for (int n = 0; n < N; n++) {
             xch_bit<0, 2>(c[n], u);  // e bit 6 (lane bit 2) <-> e bit 3
@@ -756,50 +591,8 @@ __device__ __forceinline__ void ola_long_pk(const LdsTables& T, const FrameCtx& 
 // EIGHT_SHORT_SEQUENCE: 8 x MDCT(256) (64-point IFFTs), FilterBank.java:71-101.
 // Lane (w = u>>3, b = u&7) holds window w's elements b + 8s.
 // ------------------------------------------------------------------------------------------
-__device__ __forceinline__ void imdct_short(float* buf, const LdsTables& T, int u, float (&re)[8], float (&im)[8])
-{
-    const int w = u >> 3, b = u & 7;
-#pragma unroll
-    for (int s = 0; s < 8; s++) {
-        int k = b + 8 * s;
-        float in0 = buf[eo_idx(128 * w + 2 * k)];
-        float in1 = buf[eo_idx(128 * w + 127 - 2 * k)];
-        float c = T.mdct_s[k][0], sn = T.mdct_s[k][1];
-        im[s] = (in0 * c) + (in1 * sn);
-        re[s] = (in1 * c) - (in0 * sn);
-    }
-    wave_sync();
-    fft_pass1(re, im, T.roots_s, 8);
-    float2* X = reinterpret_cast<float2*>(buf);
-    const int t = (int)(__builtin_bitreverse32((uint32_t)b) >> 29);
-#pragma unroll
-    for (int r = 0; r < 8; r++) X[xs(64 * w + 8 * t + r)] = make_float2(re[BR3[r]], im[BR3[r]]);
-    wave_sync();
-#pragma unroll
-    for (int s = 0; s < 8; s++) {
-        float2 v = X[xs(64 * w + b + 8 * s)];
-        re[s] = v.x;
-        im[s] = v.y;
-    }
-    wave_sync();
-    // stages i = 8, 16, 32 of the 64-point IFFT: roots[k*m], m = 4, 2, 1
-    fft_3stages(re, im, [&](int j, float& wr, float& wi) {
-        int idx = j == 0 ? 4 * b : (j < 3 ? 2 * (b + 8 * (j - 1)) : b + 8 * (j - 3));
-        wr = T.roots_s[idx][0];
-        wi = T.roots_s[idx][1];
-    });
-#pragma unroll
-    for (int s = 0; s < 8; s++) {
-        int k = b + 8 * s;
-        float c = T.mdct_s[k][0], sn = T.mdct_s[k][1];
-        float t0 = re[s], t1 = im[s];
-        im[s] = (t1 * c) + (t0 * sn);
-        re[s] = (t0 * c) - (t1 * sn);
-    }
-}
-
-// The same transform in packed FP32 (one register pair per complex value, the long path's
-// primitives: every product and sum is the scalar version's, a - b as a + (-b))
+// 8 x 64-point IFFTs in packed FP32 (one register pair per complex value, the long path's
+// primitives; a - b as a + (-b))
 __device__ __forceinline__ void imdct_short_pk(float* buf, const LdsTables& T, int u, float (&re)[8], float (&im)[8])
 {
     const int w = u >> 3, b = u & 7;
@@ -1216,11 +1009,7 @@ __device__ __forceinline__ void synth_channel(const KernelArgs& A, const LdsTabl
     const FrameCtx fc{ic.seq, ic.shape, ic.shape_prev};
     if (fc.seq == JAAD_EIGHT_SHORT_SEQUENCE) {
         float re[8], im[8];
-#ifdef JAAD_SHORT_SCALAR
-        imdct_short(buf, T, u, re, im);
-#else
         imdct_short_pk(buf, T, u, re, im);
-#endif
         ola_short(buf, T, u, fc, re, im, ov, out);
     } else {
         float* const bufs[1] = {buf};
@@ -1241,7 +1030,7 @@ __device__ __forceinline__ void synth_channel(const KernelArgs& A, const LdsTabl
         st_acc[k] += (uint32_t)(t_ - st_prev);                    \
         st_prev = t_;                                             \
     } while (0)
-#elif defined(JAAD_MARKS)  // design tool: phase markers in the device assembly (tools/phase_mix.py)
+#elif defined(JAAD_MARKS)  // design tool: phase markers in the device assembly (tools/isa_mix.py)
 #define STAMP(k) asm volatile(";PHASE " #k)
 #else
 #define STAMP(k) \

@@ -515,155 +515,6 @@ __device__ __forceinline__ void rotate_allpass(float2 (&d)[14])
     rotate<9, 5, 32 % 5>(d);
 }
 
-// walk the frames of a run with the next frame's 32 inputs in flight while this one computes
-template <typename Load, typename Step>
-__device__ __forceinline__ void run_frames(const uint32_t* fl, uint32_t nfr, Load&& load, Step&& step)
-{
-    float2 xa[32], xb[32];
-    if (nfr) load(xa, fl[0]);
-    for (uint32_t j = 0; j < nfr; j += 2) {
-        if (j + 1 < nfr) load(xb, fl[j + 1]);
-        step(xa, fl[j]);
-        if (j + 1 >= nfr) break;
-        if (j + 2 < nfr) load(xa, fl[j + 2]);
-        step(xb, fl[j + 1]);
-    }
-}
-
-// round-3 form (one wave per recurrence, the QMF and hybrid all-pass chains whole), kept as the
-// JAAD_DECOR_V1 build for A/B timing against the pipelined ps_decor_kernel below
-__global__ __launch_bounds__(256) void ps_decor_kernel_v1(SbrArgs A)
-{
-    // the run's frames that carry PS data, in time order: the recurrences advance only there
-    const uint32_t run = blockIdx.x;
-    const uint32_t* fl = A.ps_list + A.runs[2 * run];
-    const uint32_t nfr = A.runs[2 * run + 1];
-    if (nfr == 0) return;
-    const int wave = threadIdx.x >> 6, u = lane_id();
-    // PsConst in LDS: the parameter scan indexes its tables at every (frame, envelope, group)
-    __shared__ PsConst Ks;
-    __shared__ uint32_t pbuf[2][kPsFrameDw];
-    {
-        const uint32_t* src = reinterpret_cast<const uint32_t*>(A.psc);
-        uint32_t* dst = reinterpret_cast<uint32_t*>(&Ks);
-        for (int i = threadIdx.x; i < (int)(sizeof(PsConst) / 4); i += 256) dst[i] = src[i];
-    }
-    __syncthreads();
-    PsState& S = A.pss[A.recs[fl[0]].slot];
-    const PsConst& K = Ks;
-    const bool fresh = S.init == 0;
-
-    if (wave == 0) {
-        // ---- QMF bands (lane = sb): all-pass below 23, 14-slot delay to 34, 1-slot above ----
-        float2 ap[14], dl[14], d1;
-#pragma unroll
-        for (int k = 0; k < 14; k++) {
-            ap[k] = fresh ? make_float2(0.0f, 0.0f) : S.ap[k][u];
-            dl[k] = fresh ? make_float2(0.0f, 0.0f) : S.dl[k][u];
-        }
-        d1 = dl[0];
-        float phi[2] = {K.phi_qmf[u][0], K.phi_qmf[u][1]}, q[3][2], g[3];
-        float slope = 1.0f;
-        if (u > 3) {
-            const int decay = 3 - u;
-            slope = decay <= -20 ? 0.0f : 1.0f + kDecaySlope * (float)decay;
-        }
-        for (int m = 0; m < 3; m++) {
-            q[m][0] = K.q_qmf[u][m][0];
-            q[m][1] = K.q_qmf[u][m][1];
-            g[m] = slope * K.filter_a[m];
-        }
-        const bool isap = u <= 22, is14 = u < 35;
-        auto load = [&](float2 (&x)[32], uint32_t f) {
-            const float2* src = reinterpret_cast<const float2*>(A.xps + (size_t)f * 8192);
-#pragma unroll
-            for (int n = 0; n < 32; n++) x[n] = src[n * 64 + u];
-        };
-        auto step = [&](float2 (&x)[32], uint32_t f) {
-            float2* dst = reinterpret_cast<float2*>(A.xps + (size_t)f * 8192) + 2048;
-            static_for<0, 32>([&](auto I) {
-                constexpr int n = decltype(I)::value;
-                const float2 ra = allpass_step<n>(ap, x[n], phi, q, g);
-                const float2 rl = is14 ? dl[n % 14] : d1;
-                dl[n % 14] = is14 ? x[n] : dl[n % 14];
-                d1 = x[n];
-                const float2 r = isap ? ra : rl;
-                if (u >= 3) dst[n * 64 + u] = r;
-            });
-            rotate_allpass(ap);
-            rotate<0, 14, 32 % 14>(dl);
-        };
-        run_frames(fl, nfr, load, step);
-        if (!is14) dl[0] = d1;
-#pragma unroll
-        for (int k = 0; k < 14; k++) {
-            S.ap[k][u] = ap[k];
-            S.dl[k][u] = dl[k];
-        }
-    } else if (wave == 1) {
-        // ---- hybrid groups 0..9 (lane = group, sub-band kBorder[group]) ----
-        if (u >= 10) return;
-        const int sb = kBorder[u];
-        float2 ap[14];
-#pragma unroll
-        for (int k = 0; k < 14; k++) ap[k] = fresh ? make_float2(0.0f, 0.0f) : S.aph[k][u];
-        float phi[2] = {K.phi_sub[sb][0], K.phi_sub[sb][1]}, q[3][2], g[3];
-        for (int m = 0; m < 3; m++) {
-            q[m][0] = K.q_sub[sb][m][0];
-            q[m][1] = K.q_sub[sb][m][1];
-            g[m] = 1.0f * K.filter_a[m];
-        }
-        auto load = [&](float2 (&x)[32], uint32_t f) {
-            const float2* src = reinterpret_cast<const float2*>(A.xhl + (size_t)f * 768);
-#pragma unroll
-            for (int n = 0; n < 32; n++) x[n] = src[n * 12 + sb];
-        };
-        auto step = [&](float2 (&x)[32], uint32_t f) {
-            float2* dst = reinterpret_cast<float2*>(A.xhr + (size_t)f * 768);
-            static_for<0, 32>([&](auto I) {
-                constexpr int n = decltype(I)::value;
-                dst[n * 12 + sb] = allpass_step<n>(ap, x[n], phi, q, g);
-            });
-            rotate_allpass(ap);
-        };
-        run_frames(fl, nfr, load, step);
-#pragma unroll
-        for (int k = 0; k < 14; k++) S.aph[k][u] = ap[k];
-    } else if (wave == 3) {
-        ps_param_scan(A, K, fl, nfr, S, fresh, u, pbuf);
-    } else {
-        // ---- transient detector (lane = parameter band), PSImpl.java:238-270 ----
-        if (u >= 20) return;
-        float peak = fresh ? 0.0f : S.peak[u], smooth = fresh ? 0.0f : S.smooth[u], pprev = fresh ? 0.0f : S.pprev[u];
-        auto load = [&](float2 (&x)[32], uint32_t f) {
-            const float* src = A.pg + (size_t)f * 640;
-#pragma unroll
-            for (int n = 0; n < 32; n++) x[n].x = src[n * 20 + u];
-        };
-        auto step = [&](float2 (&x)[32], uint32_t f) {
-            float* dst = A.pg + (size_t)f * 640;
-#pragma unroll
-            for (int n = 0; n < 32; n++) {
-                const float Pn = x[n].x;
-                const float gamma = 1.5f;
-                peak = (peak * kAlphaDecay);
-                if (peak < Pn) peak = Pn;
-                float sm = smooth;
-                sm += ((peak - Pn - smooth) * kAlphaSmooth);
-                smooth = sm;
-                float nrg = pprev;
-                nrg += ((Pn - pprev) * kAlphaSmooth);
-                pprev = nrg;
-                dst[n * 20 + u] = (sm * gamma) <= nrg ? 1.0f : __fdiv_rn(nrg, (sm * gamma));
-            }
-        };
-        run_frames(fl, nfr, load, step);
-        S.peak[u] = peak;
-        S.smooth[u] = smooth;
-        S.pprev[u] = pprev;
-    }
-}
-
 // ---------------------------------------------------------------------------------------------
 // Pipelined decorrelator: the all-pass chain of a band (2-slot delay, then links 0, 1, 2:
 // PSImpl.java:283-344) is a sequence of three independent recurrences -- link m's ring holds only
@@ -677,7 +528,8 @@ __global__ __launch_bounds__(256) void ps_decor_kernel_v1(SbrArgs A)
 //               G_TransientRatio of frame k-1 (the compare and the division, -> pg)
 //   role 6      transient detector recurrences of frame k (peak, smooth, energy)
 //   role 7      mixing-parameter scan of frame k (-> hb)
-// Every value is computed by the same binary32 operations as in ps_decor_kernel_v1 (bit-exact);
+// Every value is computed by the same binary32 operations as the round-3 one-wave-per-recurrence form
+// (measured 0.72 ms per C5 call; removed), bit-exact;
 // only the waves that compute them differ.  The run's critical path drops from the whole chain
 // of a QMF band (2-slot delay + 3 links per slot) to one link per slot.
 // ---------------------------------------------------------------------------------------------
@@ -1200,11 +1052,7 @@ hipError_t launch_ps(const SbrArgs& a, hipStream_t stream)
     if (!a.n_runs) return hipSuccess;
     const dim3 g((a.n_cf + kPsWaves - 1) / kPsWaves);
     hipLaunchKernelGGL(ps_analysis_kernel, g, dim3(64 * kPsWaves), 0, stream, a);
-#ifdef JAAD_DECOR_V1
-    hipLaunchKernelGGL(ps_decor_kernel_v1, dim3(a.n_runs), dim3(256), 0, stream, a);
-#else
     hipLaunchKernelGGL(ps_decor_kernel, dim3(a.n_runs), dim3(64 * kDecorWaves), 0, stream, a);
-#endif
     hipLaunchKernelGGL(ps_mix_kernel, g, dim3(64 * kPsWaves), 0, stream, a);
     hipLaunchKernelGGL(ps_state_kernel, dim3(a.n_runs), dim3(64), 0, stream, a);
     return hipGetLastError();

@@ -3,7 +3,11 @@ inputs, and blocks of launches alternate between the libs (A B C A B C ...), so 
 box state hit all alike.  Prints per lib: median / min ms per batch over the blocks, PCM hash.
 
     python scripts/ab_inproc.py CONFIG BLOCKS LAUNCHES_PER_BLOCK lib1.so lib2.so ...
+
+A lib argument may carry environment settings applied before its context is created, e.g.
+``lib_b.so@JAAD_LC_PAIR=0`` (copies of one build then differ only in those settings).
 """
+import os
 import hashlib
 import sys
 from pathlib import Path
@@ -35,12 +39,18 @@ def main():
     s = torch.cuda.Stream(dev)
     torch.cuda.set_stream(s)
     runs = []
-    for path in paths:
+    for arg in paths:
+        path, *envs = arg.split("@")
+        for kv in envs:
+            k, v = kv.split("=", 1)
+            os.environ[k] = v
         L = N.load_lib(path)
         N._lib = L
         ctx = N.Context(cfg, int(b.stream_slot.max()) + 1)
         pcm = torch.empty(b.n_frames * N.pcm_frame_bytes(0, bool(p.sbr)), dtype=torch.uint8, device=dev)
-        runs.append((Path(path).stem, L, ctx, pcm, []))
+        runs.append((Path(path).stem + ("@" + "@".join(envs) if envs else ""), L, ctx, pcm, []))
+        for kv in envs:
+            os.environ.pop(kv.split("=", 1)[0], None)
     import time
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < 0.4:  # warm-up past the GPU clock's load-onset transient

@@ -9,18 +9,13 @@ from jaadec_amd import build as B  # noqa: E402
 KSRC = ("jaad_lc.hip", "jaad_sbr.hip", "jaad_ps.hip")
 # name: (defines, extra flags, VOP3 rewrite forms per kernel source or None for the product's)
 VARIANTS = {
-    "a_novcc": (["JAAD_XCH_NOVCC"], [], None),
     "b_head": ([], [], None),
     "c_vop3": ([], [], {k: ("cndmask", "vopc") for k in KSRC}),
     "d_vop3c": ([], [], {k: ("cndmask",) for k in KSRC}),
     "s_stamps": (["JAAD_STAMPS"], [], None),
-    "e_w16c": (["JAAD_LDS_COMPACT", "JAAD_LC_WAVES=16"], [], None),
-    "f_w12c": (["JAAD_LDS_COMPACT"], [], None),
     "g_w8": (["JAAD_LC_WAVES=8"], [], None),
-    "d_v1": (["JAAD_DECOR_V1"], [], None),
     "d_plain": (["JAAD_DECOR_ROLES_PLAIN"], [], None),
     "d_stamps": (["JAAD_DECOR_STAMPS"], [], None),
-    "x3lds": (["JAAD_X3_LDS"], [], None),
     "h_w4": (["JAAD_LC_WAVES=4"], [], None),
 }
 

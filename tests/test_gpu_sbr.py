@@ -223,8 +223,9 @@ def test_c4_single_frame_runs_and_empty_runs():
                                          (5, N.PCM_FLOAT32)])
 def test_downsampled_sbr(cfgid, flags):
     """Downsampled SBR (a15': extension rate = core rate, SynthesisFilterbank32): 1024 samples per
-    frame at the core rate; GPU == the oracle's restatement bit for bit (both evaluate the 32-point
-    DCT-IV / DST-IV as the same double sums; to the reference itself +-1 LSB, see jaad_oracle_sbr.c)."""
+    frame at the core rate; GPU == the oracle's restatement bit for bit (both run the reference's own
+    DCT4_32 / DST4_32 straight-line programs, carried as op lists in tables/jaad_sbr_dct32.inc, so the
+    binary32 operations and their order are the reference's: DESIGN.md section 0)."""
     p = N.synth_params(cfgid, n_streams=3, frames_per_stream=36)
     b = N.synth_batch(p)
     cfg = N.make_cfg(p.sf_index, p.channel_config, sbr=True, ps=p.sbr == 2, down=True)
