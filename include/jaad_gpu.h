@@ -317,10 +317,11 @@ int jaad_ctx_core_channels(const jaad_ctx* ctx);
  * frames marked JAAD_FRAME_EOS are not written).
  * Replaces the per-frame Decoder.decodeFrame(byte[], SampleBuffer) (A/Decoder.java:131-150)
  * for a batch of already parsed frames.  The side info is range-checked first
- * (JAAD_ERR_BITSTREAM, every slot's state left as before the call; with dropped frames the
- * frames between them decode as consecutive sub-batches, all checked before the first runs,
- * except for SBR record rejections, which stop at the failing sub-batch).  An AAC-LC batch of
- * >= 4096 frames is cut into run-aligned pieces whose copies and kernels overlap; caller
+ * (JAAD_ERR_BITSTREAM, every slot's state left as before the call).  Dropped frames (ABI 4
+ * frame_status) are left out of the call's plan: one launch sequence decodes every run's kept
+ * frames as consecutive ones (the SBR header of a dropped frame whose payload was parsed whole is
+ * still taken, as for a JAAD_SBR_UPSAMPLE frame).  An AAC-LC batch of >= 4096 frames without
+ * dropped frames is cut into run-aligned pieces whose copies and kernels overlap; caller
  * buffers registered with jaad_host_register are copied by DMA directly, others through
  * page-locked staging.                                                                      */
 int jaad_decode_batch(jaad_ctx* ctx, const jaad_batch* batch, void* pcm_out, size_t pcm_bytes,

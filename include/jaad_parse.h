@@ -122,8 +122,12 @@ typedef struct jaad_frame_out {
  * ended early: the reference's EOSException, which Decoder.decodeFrame swallows, dropping the
  * frame, A/Decoder.java:96-100) leaves the state where the reference's reads left it: the window
  * shape of every ICSInfo whose shape bit was read, the PNS LCG advanced over the noise bands
- * decodeSpectralData reached, the SBR/PS state of payloads parsed whole (a payload cut short
- * moves none).  Any other error changes nothing of the parser's state. */
+ * decodeSpectralData reached, the SBR/PS state of payloads parsed whole -- and out->sbr keeps
+ * those payloads' records (header included: the reference swapped it in before the exception,
+ * A/sbr/SBR.java:162-184; jaad_decode_batch applies it for a frame marked JAAD_FRAME_EOS).  An
+ * SBR payload that ends inside its fill element's bytes is JAAD_ERR_UNSUPPORTED: the reference
+ * would have applied part of it.  Any error other than JAAD_ERR_EOS changes nothing of the
+ * parser's state. */
 int jaad_parse_frame(jaad_parser* p, const uint8_t* data, size_t bytes, jaad_frame_out* out);
 
 /* Implicit SBR signalling (ADTS, LC-only AudioSpecificConfig): the reference opens SBR when it

@@ -214,6 +214,14 @@ struct jaad_ctx {
     hipStream_t last_stream = nullptr;  // stream of the previous device call
     std::vector<ChunkDesc> chunks;
     std::vector<uint32_t> plan_slots, plan_begin;  // plan cache key
+    // dropped frames (jaad_batch.frame_status): the call's kept batch frames in order (virtual
+    // frame -> batch frame) and the runs' first virtual frames; the list's device copy is
+    // KernelArgs::fkeep (staged like the chunk table)
+    std::vector<uint32_t> keep, vbegin;
+    DevBuf d_keep;
+    PinnedBuf h_keep;
+    hipEvent_t keep_copied = nullptr;
+    bool keep_live = false;
     std::vector<uint8_t> slot_used;
     bool plan_valid = false;
     int n_cu = 256;
@@ -451,6 +459,46 @@ int sync_ctx(jaad_ctx* ctx)
     return JAAD_OK;
 }
 
+// Dropped frames (jaad_batch.frame_status, A/Decoder.java:89-101): the kernels of the call walk
+// the kept frames only.  `vb` becomes the planner's view of the batch (the kept frames numbered
+// consecutively, runs in the same order and slots); `*d_keep` (null when nothing is dropped) is
+// the device copy of virtual frame -> batch frame, which the LC kernel and the pack passes read.
+int keep_map(jaad_ctx* ctx, const jaad_batch* b, hipStream_t stream, jaad_batch& vb, const uint32_t** d_keep)
+{
+    vb = *b;
+    *d_keep = nullptr;
+    if (!b->frame_status) return JAAD_OK;
+    if (!b->stream_slot || !b->frame_begin) return JAAD_ERR_INVALID_ARG;
+    if (b->frame_begin[0] != 0 || b->frame_begin[b->n_runs] != b->n_frames) return JAAD_ERR_INVALID_ARG;
+    std::vector<uint32_t>& keep = ctx->keep;
+    std::vector<uint32_t>& vbeg = ctx->vbegin;
+    keep.clear();
+    vbeg.assign(1, 0);
+    for (uint32_t r = 0; r < b->n_runs; r++) {
+        if (b->frame_begin[r + 1] < b->frame_begin[r]) return JAAD_ERR_INVALID_ARG;
+        for (uint32_t f = b->frame_begin[r]; f < b->frame_begin[r + 1]; f++)
+            if (b->frame_status[f] == JAAD_FRAME_DECODE) keep.push_back(f);
+        vbeg.push_back((uint32_t)keep.size());
+    }
+    vb.n_frames = (uint32_t)keep.size();
+    vb.frame_begin = vbeg.data();
+    if (keep.size() == b->n_frames) return JAAD_OK;  // nothing dropped
+    const size_t bytes = keep.size() * sizeof(uint32_t);
+    if (ctx->keep_live) HIPCHK(hipEventSynchronize(ctx->keep_copied));  // staging in use?
+    HIPCHK(ctx->h_keep.ensure(bytes + 16));
+    HIPCHK(ctx->d_keep.ensure(bytes + 16));
+    if (bytes) {
+        std::memcpy(ctx->h_keep.p, keep.data(), bytes);
+        HIPCHK(hipMemcpyAsync(ctx->d_keep.p, ctx->h_keep.p, bytes, hipMemcpyHostToDevice, stream));
+        HIPCHK(hipEventRecord(ctx->keep_copied, stream));
+        ctx->keep_live = true;
+    }
+    *d_keep = static_cast<const uint32_t*>(ctx->d_keep.p);
+    return JAAD_OK;
+}
+
+bool frame_dropped(const jaad_batch* b, size_t f) { return b->frame_status && b->frame_status[f] != JAAD_FRAME_DECODE; }
+
 bool sbr_downsampled(const jaad_stream_cfg& c) { return c.sbr && c.ext_sf_index == c.sf_index; }
 
 size_t pcm_bytes_per_frame(const jaad_ctx* ctx, uint32_t flags)
@@ -553,6 +601,7 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
     for (uint32_t r = 0; r < b->n_runs; r++) {
         rbeg[r] = (uint32_t)fmap.size();
         for (uint32_t f = b->frame_begin[r]; f < b->frame_begin[r + 1]; f++) {
+            if (frame_dropped(b, f)) continue;  // no record and no PCM (its header: below)
             if (b->sbr[f].status == JAAD_SBR_UPSAMPLE) ups.push_back(f);
             else if (b->sbr[f].status == JAAD_SBR_OK) fmap.push_back(f);
             else {
@@ -660,8 +709,10 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
                     for (size_t o = 0; o < sizeof(jaad_sbr_frame); o += 64)
                         __builtin_prefetch(reinterpret_cast<const char*>(&b->sbr[f + 2]) + o);
                 const jaad_sbr_frame& F = b->sbr[f];
-                if (F.status == JAAD_SBR_UPSAMPLE) {
-                    // the reference still takes this frame's header (SbrHost::take_header)
+                // an upsampled frame, and a dropped one whose SBR payload was read before the
+                // bitstream ended (SBR.decode ran readHeader / calc_sbr_tables before the
+                // EOSException, A/sbr/SBR.java:117-184): the reference still takes its header
+                if (F.status == JAAD_SBR_UPSAMPLE || frame_dropped(b, f)) {
                     if (F.header_present) {
                         const int hr = ctx->sbr_host->take_header(hs, F.hdr);
                         if (hr) {
@@ -942,7 +993,11 @@ int launch_mc_sbr(jaad_ctx* ctx, const jaad_batch* db, void* pcm, uint32_t flags
 int launch_work(jaad_ctx* ctx, const jaad_batch* db, void* pcm, uint32_t flags, hipStream_t stream)
 {
     if (!ctx->children.empty()) return launch_mc_sbr(ctx, db, pcm, flags, stream);
-    int rc = plan(ctx, db, stream);
+    jaad_batch vb;  // the kept frames (dropped frames are not planned)
+    const uint32_t* d_keep = nullptr;
+    int rc = keep_map(ctx, db, stream, vb, &d_keep);
+    if (rc) return rc;
+    rc = plan(ctx, &vb, stream);
     if (rc) return rc;
     KernelArgs a{};
     a.q = db->q;
@@ -969,6 +1024,7 @@ int launch_work(jaad_ctx* ctx, const jaad_batch* db, void* pcm, uint32_t flags, 
     a.tns_mode = ctx->cfg.tns_mode;
     a.dbg = ctx->dbg;
     a.dbg_frame = ctx->dbg_frame;
+    a.fkeep = d_keep;
     if (a.n_chunks == 0) return JAAD_OK;
     if (db->n_cce_terms && (rc = setup_coupling(ctx, db, a, stream))) return rc;
     if (ctx->n_elem > 1) {
@@ -999,7 +1055,7 @@ int launch_work(jaad_ctx* ctx, const jaad_batch* db, void* pcm, uint32_t flags, 
             ch0 += n;
             cpe += n == 2;
         }
-        HIPCHK(launch_pack(static_cast<const float*>(ctx->d_time.p), pcm, db->n_frames, ctx->nch, flags, stream));
+        HIPCHK(launch_pack(static_cast<const float*>(ctx->d_time.p), pcm, vb.n_frames, ctx->nch, flags, stream, d_keep));
         ctx->parity ^= 1;
         return JAAD_OK;
     }
@@ -1014,6 +1070,38 @@ int launch_work(jaad_ctx* ctx, const jaad_batch* db, void* pcm, uint32_t flags, 
 
 int launch(jaad_ctx* ctx, const jaad_batch* db, void* pcm, uint32_t flags, hipStream_t stream);
 
+// Dry run of launch_sbr_stage's record checks (header tables, mixed tables of a header taken on an
+// upsampled or dropped frame, PS parameters) on copies of the slots' host SBR state: nothing of the
+// context moves.  A multichannel call runs it for every element before it launches any of them, so
+// a rejected batch leaves every element's state as it was.
+int sbr_records_ok(jaad_ctx* ctx, const jaad_batch* b)
+{
+    const int nch = ctx->nch;
+    std::vector<SbrRec> rec(nch);
+    std::vector<float> pool((size_t)nch * SbrHost::kMaxEorig + 64);
+    for (uint32_t r = 0; r < b->n_runs; r++) {
+        SbrHostSlot hs = ctx->sbr_slots[b->stream_slot[r]];
+        bool first = true;
+        for (uint32_t f = b->frame_begin[r]; f < b->frame_begin[r + 1]; f++) {
+            const jaad_sbr_frame& F = b->sbr[f];
+            if (F.status == JAAD_SBR_UPSAMPLE || frame_dropped(b, f)) {
+                if (F.header_present) {
+                    const int rc = ctx->sbr_host->take_header(hs, F.hdr);
+                    if (rc) return rc;
+                }
+                continue;
+            }
+            if (F.status != JAAD_SBR_OK) return JAAD_ERR_INVALID_ARG;
+            if (ctx->cfg.ps && !ps_frame_ok(F)) return JAAD_ERR_BITSTREAM;
+            uint32_t epos = 0;
+            const int rc = ctx->sbr_host->frame(hs, F, nch, first, b->stream_slot[r], rec.data(), pool.data(), epos, 0);
+            if (rc) return rc;
+            first = false;
+        }
+    }
+    return JAAD_OK;
+}
+
 // Multichannel HE-AAC.  Element k's records (its channel columns of q/sf/cb/ics/tns, its ms_used pair,
 // its SBR record of each frame) are gathered into contiguous arrays by strided device copies and
 // decoded by the element's own SBR context into [frame][sample][2] PCM (an SCE's SBR1 output is
@@ -1026,15 +1114,32 @@ int launch_mc_sbr(jaad_ctx* ctx, const jaad_batch* db, void* pcm, uint32_t flags
     const size_t nf = db->n_frames;
     const int ne = ctx->n_elem, nch = ctx->nch;
     if (!db->sbr) return JAAD_ERR_INVALID_ARG;
+    jaad_batch vb;  // dropped frames: each child skips them, the interleave pass leaves their PCM
+    const uint32_t* d_keep = nullptr;
+    int krc = keep_map(ctx, db, stream, vb, &d_keep);
+    if (krc) return krc;
     // element kinds of the layout: an SCE must carry SBR data in every frame (without it the
     // reference's channel list shrinks, A/syntax/SCE.java:122-132), an LFE never does
     for (size_t f = 0; f < nf; f++)
         for (int k = 0; k < ne; k++) {
+            if (frame_dropped(db, f)) continue;
             const jaad_sbr_frame& r = db->sbr[f * ne + k];
             const bool lfe = mc_is_lfe(ctx->cfg.channel_config, k, ne);
             if (lfe ? r.status != JAAD_SBR_UPSAMPLE : (ctx->elem_nch[k] == 1 && r.status == JAAD_SBR_UPSAMPLE))
                 return JAAD_ERR_UNSUPPORTED;
         }
+    // every element's SBR records are checked before the first element is launched
+    for (int k = 0; k < ne; k++) {
+        ctx->h_mc_sbr.resize(nf);
+        for (size_t f = 0; f < nf; f++) ctx->h_mc_sbr[f] = db->sbr[f * ne + k];
+        jaad_batch c = *db;
+        c.sbr = ctx->h_mc_sbr.data();
+        const int rc = sbr_records_ok(ctx->children[k], &c);
+        if (rc) {
+            ctx->err = "SBR side info of element " + std::to_string(k);
+            return rc;
+        }
+    }
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     const size_t S = (size_t)jaad_cfg_sample_length(&ctx->cfg), bps = (flags & JAAD_PCM_FLOAT32) ? 4 : 2;
     const size_t pcm_k = al(nf * S * 2 * bps);  // one element's PCM
@@ -1069,6 +1174,7 @@ int launch_mc_sbr(jaad_ctx* ctx, const jaad_batch* db, void* pcm, uint32_t flags
         c.n_runs = db->n_runs;
         c.stream_slot = db->stream_slot;
         c.frame_begin = db->frame_begin;
+        c.frame_status = db->frame_status;
         c.q = reinterpret_cast<const int16_t*>(e);
         c.sf = reinterpret_cast<const uint8_t*>(e + o_sf);
         c.cb = reinterpret_cast<const uint8_t*>(e + o_cb);
@@ -1110,7 +1216,7 @@ int launch_mc_sbr(jaad_ctx* ctx, const jaad_batch* db, void* pcm, uint32_t flags
             m.n_out++;
         }
     }
-    HIPCHK(launch_mc_interleave(m, pcm, (uint32_t)nf, (uint32_t)S, (int)bps, stream));
+    HIPCHK(launch_mc_interleave(m, pcm, vb.n_frames, (uint32_t)S, (int)bps, stream, d_keep));
     return JAAD_OK;
 }
 
@@ -1238,6 +1344,8 @@ int jaad_ctx_create(const jaad_stream_cfg* cfg, uint32_t n_slots, int device, ja
     if ((e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking)) != hipSuccess) return bail(e, "hipStreamCreate");
     if ((e = hipEventCreateWithFlags(&ctx->done, hipEventDisableTiming)) != hipSuccess) return bail(e, "hipEventCreate");
     if ((e = hipEventCreateWithFlags(&ctx->chunks_copied, hipEventDisableTiming)) != hipSuccess)
+        return bail(e, "hipEventCreate");
+    if ((e = hipEventCreateWithFlags(&ctx->keep_copied, hipEventDisableTiming)) != hipSuccess)
         return bail(e, "hipEventCreate");
     size_t sbytes = (size_t)ctx->n_elem * n_slots * 2048 * sizeof(float);  // [element][slot][2][1024]
     for (int i = 0; i < 2; i++) {
@@ -1382,6 +1490,9 @@ void jaad_ctx_destroy(jaad_ctx* ctx)
     ctx->h_chunks.release();
     if (ctx->done) (void)hipEventDestroy(ctx->done);
     if (ctx->chunks_copied) (void)hipEventDestroy(ctx->chunks_copied);
+    if (ctx->keep_copied) (void)hipEventDestroy(ctx->keep_copied);
+    ctx->d_keep.release();
+    ctx->h_keep.release();
     ctx->d_batch.release();
     ctx->d_pcm.release();
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -1418,6 +1529,7 @@ static bool side_info_ok(const jaad_ctx* ctx, const jaad_batch* b, size_t c0, si
 {
     const int nl = JAAD_SWB_LONG_WINDOW_COUNT[ctx->cfg.sf_index], ns = JAAD_SWB_SHORT_WINDOW_COUNT[ctx->cfg.sf_index];
     for (size_t i = c0; i < c1; i++) {
+        if (b->frame_status && b->frame_status[i / ctx->nch] != JAAD_FRAME_DECODE) continue;  // not read
         const jaad_ics_info& ic = b->ics[i];
         if (ic.window_sequence > 3 || ic.window_shape > 1 || ic.window_shape_prev > 1) return false;
         const int lim = ic.window_sequence == JAAD_EIGHT_SHORT_SEQUENCE ? ns : nl;
@@ -1443,6 +1555,23 @@ static bool q_ok_copy(const int16_t* src, int16_t* dst, size_t n)
         for (size_t k = 0; k < m; k++) bad |= (src[o + k] > 8190) | (src[o + k] < -8190);
         if (bad) return false;
         if (dst) std::memcpy(dst + o, src + o, m * sizeof(int16_t));
+    }
+    return true;
+}
+
+// q_ok_copy (check only) over the ch-frames [c0, c1) of the batch's kept frames
+static bool q_ok_kept(const jaad_ctx* ctx, const jaad_batch* b, size_t c0, size_t c1)
+{
+    if (!b->frame_status) return q_ok_copy(b->q + c0 * 1024, nullptr, (c1 - c0) * 1024);
+    for (size_t i = c0; i < c1;) {
+        if (b->frame_status[i / ctx->nch] != JAAD_FRAME_DECODE) {
+            i++;
+            continue;
+        }
+        size_t e = i + 1;
+        while (e < c1 && b->frame_status[e / ctx->nch] == JAAD_FRAME_DECODE) e++;
+        if (!q_ok_copy(b->q + i * 1024, nullptr, (e - i) * 1024)) return false;
+        i = e;
     }
     return true;
 }
@@ -1502,7 +1631,7 @@ static int decode_batch_serial(jaad_ctx* ctx, const jaad_batch* b, void* pcm_out
     const int W = ctx->io->size();
     ctx->io->run([&](int t) {
         const size_t c0 = ncf * t / W, c1 = ncf * (t + 1) / W;
-        if (!side_info_ok(ctx, b, c0, c1) || !q_ok_copy(b->q + c0 * 1024, nullptr, (c1 - c0) * 1024)) bad = true;
+        if (!side_info_ok(ctx, b, c0, c1) || !q_ok_kept(ctx, b, c0, c1)) bad = true;
     });
     if (bad) return JAAD_ERR_BITSTREAM;
     if (b->n_cce_terms) {  // the CCE records get the channel records' checks
@@ -1555,8 +1684,23 @@ static int decode_batch_serial(jaad_ctx* ctx, const jaad_batch* b, void* pcm_out
     }
     int rc = launch(ctx, &db, ctx->d_pcm.p, flags, s);
     if (rc) return rc;
+    // the slots of dropped frames keep what the caller's buffer holds: the copy back covers the
+    // whole batch, so they are saved before it and restored after it
+    std::vector<uint8_t> kept_pcm;
+    const size_t per = pcm_bytes_per_frame(ctx, flags);
+    if (b->frame_status)
+        for (size_t f = 0; f < nf; f++)
+            if (b->frame_status[f] != JAAD_FRAME_DECODE)
+                kept_pcm.insert(kept_pcm.end(), static_cast<uint8_t*>(pcm_out) + f * per,
+                                static_cast<uint8_t*>(pcm_out) + (f + 1) * per);
     if (nf) HIPCHK(hipMemcpyAsync(pcm_out, ctx->d_pcm.p, pbytes, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
+    if (!kept_pcm.empty())
+        for (size_t f = 0, k = 0; f < nf; f++)
+            if (b->frame_status[f] != JAAD_FRAME_DECODE) {
+                std::memcpy(static_cast<uint8_t*>(pcm_out) + f * per, kept_pcm.data() + k * per, per);
+                k++;
+            }
     return JAAD_OK;
 }
 
@@ -1765,21 +1909,14 @@ static int decode_batch_pieces_impl(jaad_ctx* ctx, const jaad_batch* b, void* pc
 }
 
 // ---- dropped frames (jaad_batch.frame_status) ----
-// The frames between dropped ones decode as consecutive sub-batches: segment [s, e) of the batch
-// with the runs clipped to it (a run that has no frame there is left out: its slot keeps its state),
-// array pointers advanced to frame s and the coupling terms of those frames renumbered.  A run cut
-// by a dropped frame continues in the next segment from the state its previous frame left, which is
-// what the reference's next decodeFrame sees after it swallowed the EOSException.
-extern "C++" {
-namespace {
-struct Segments {
-    std::vector<uint32_t> slot, begin;
-    std::vector<jaad_cce_term> terms;
-};
+// A dropped frame is left out of the call's plan (keep_map): the kernels walk each run's kept
+// frames as consecutive ones, so a run cut by a dropped frame continues from the state its
+// previous frame left -- what the reference's next decodeFrame sees after it swallowed the
+// EOSException (A/Decoder.java:89-101) -- and the dropped frame's PCM slot is not written.
 
 // the number of dropped frames (0: none, or no status array); JAAD_ERR_INVALID_ARG (< 0) for a
 // status value that is not a JAAD_FRAME_*
-int dropped_frames(const jaad_batch* b)
+static int dropped_frames(const jaad_batch* b)
 {
     if (!b->frame_status) return 0;
     int n = 0;
@@ -1790,68 +1927,6 @@ int dropped_frames(const jaad_batch* b)
     return n;
 }
 
-// the sub-batch of frames [s, e) (none dropped); `seg` owns its run and term arrays
-jaad_batch segment(const jaad_ctx* ctx, const jaad_batch* b, uint32_t s, uint32_t e, Segments& seg)
-{
-    seg.slot.clear();
-    seg.begin.assign(1, 0);
-    for (uint32_t r = 0; r < b->n_runs; r++) {
-        const uint32_t lo = std::max(b->frame_begin[r], s), hi = std::min(b->frame_begin[r + 1], e);
-        if (hi <= lo) continue;
-        seg.slot.push_back(b->stream_slot[r]);
-        seg.begin.push_back(hi - s);
-    }
-    jaad_batch d = *b;
-    const size_t nch = (size_t)ctx->nch;
-    d.n_frames = e - s;
-    d.n_runs = (uint32_t)seg.slot.size();
-    d.stream_slot = seg.slot.data();
-    d.frame_begin = seg.begin.data();
-    d.q = b->q + (size_t)s * nch * 1024;
-    d.sf = b->sf + (size_t)s * nch * 128;
-    d.cb = b->cb + (size_t)s * nch * 128;
-    d.ics = b->ics + (size_t)s * nch;
-    d.ms_used = b->ms_used ? b->ms_used + (size_t)s * 2 * ctx->n_cpe : nullptr;
-    d.tns = b->tns ? b->tns + (size_t)s * nch : nullptr;
-    d.sbr = b->sbr ? b->sbr + (size_t)s * (ctx->cfg.sbr && ctx->n_elem > 1 ? ctx->n_elem : 1) : nullptr;  // [frame][element]
-    d.frame_status = nullptr;
-    seg.terms.clear();
-    for (uint32_t t = 0; t < b->n_cce_terms; t++)
-        if (b->cce_terms[t].frame >= s && b->cce_terms[t].frame < e) {
-            seg.terms.push_back(b->cce_terms[t]);
-            seg.terms.back().frame -= s;
-        }
-    d.n_cce_terms = (uint32_t)seg.terms.size();
-    d.cce_terms = seg.terms.empty() ? nullptr : seg.terms.data();
-    return d;
-}
-
-// fn(sub-batch, first frame) for every maximal run of non-dropped frames, in order
-template <class F>
-int for_each_segment(const jaad_ctx* ctx, const jaad_batch* b, F&& fn)
-{
-    if (!b->stream_slot || !b->frame_begin) return JAAD_ERR_INVALID_ARG;
-    if (b->frame_begin[0] != 0 || b->frame_begin[b->n_runs] != b->n_frames) return JAAD_ERR_INVALID_ARG;
-    for (uint32_t r = 0; r < b->n_runs; r++)
-        if (b->frame_begin[r + 1] < b->frame_begin[r]) return JAAD_ERR_INVALID_ARG;
-    Segments seg;
-    for (uint32_t s = 0; s < b->n_frames;) {
-        if (b->frame_status[s] != JAAD_FRAME_DECODE) {
-            s++;
-            continue;
-        }
-        uint32_t e = s;
-        while (e < b->n_frames && b->frame_status[e] == JAAD_FRAME_DECODE) e++;
-        const jaad_batch d = segment(ctx, b, s, e, seg);
-        const int rc = fn(d, s);
-        if (rc) return rc;
-        s = e;
-    }
-    return JAAD_OK;
-}
-}  // namespace
-}  // extern "C++"
-
 static int decode_batch_whole(jaad_ctx* ctx, const jaad_batch* b, void* pcm_out, uint32_t flags);
 
 int jaad_decode_batch(jaad_ctx* ctx, const jaad_batch* b, void* pcm_out, size_t pcm_bytes, uint32_t flags)
@@ -1861,21 +1936,9 @@ int jaad_decode_batch(jaad_ctx* ctx, const jaad_batch* b, void* pcm_out, size_t 
     if (!pcm_out && b->n_frames) return JAAD_ERR_INVALID_ARG;
     const int dropped = dropped_frames(b);
     if (dropped < 0) return dropped;
-    if (dropped == 0) {
-        jaad_batch d = *b;
-        d.frame_status = nullptr;
-        return decode_batch_whole(ctx, &d, pcm_out, flags);
-    }
-    // every segment's side info first: a rejected batch leaves every slot's state as it was
-    rc = for_each_segment(ctx, b, [&](const jaad_batch& d, uint32_t) {
-        const size_t ncf = (size_t)d.n_frames * ctx->nch;
-        return side_info_ok(ctx, &d, 0, ncf) && q_ok_copy(d.q, nullptr, ncf * 1024) ? JAAD_OK : JAAD_ERR_BITSTREAM;
-    });
-    if (rc) return rc;
-    const size_t per = pcm_bytes_per_frame(ctx, flags);
-    return for_each_segment(ctx, b, [&](const jaad_batch& d, uint32_t s) {
-        return decode_batch_whole(ctx, &d, static_cast<uint8_t*>(pcm_out) + per * s, flags);
-    });
+    jaad_batch d = *b;
+    if (!dropped) d.frame_status = nullptr;  // the kernels then read no frame map
+    return decode_batch_whole(ctx, &d, pcm_out, flags);
 }
 
 static int decode_batch_whole(jaad_ctx* ctx, const jaad_batch* b, void* pcm_out, uint32_t flags)
@@ -1883,8 +1946,8 @@ static int decode_batch_whole(jaad_ctx* ctx, const jaad_batch* b, void* pcm_out,
     int rc;
     HIPCHK(hipSetDevice(ctx->device));
     if ((rc = io_setup(ctx))) return rc;
-    if (ctx->cfg.sbr || ctx->n_elem > 1 || b->n_cce_terms || b->n_frames < 2 * kMinPieceFrames || !b->stream_slot ||
-        !b->frame_begin)
+    if (ctx->cfg.sbr || ctx->n_elem > 1 || b->n_cce_terms || b->frame_status || b->n_frames < 2 * kMinPieceFrames ||
+        !b->stream_slot || !b->frame_begin)
         return decode_batch_serial(ctx, b, pcm_out, flags);
     // the run layout is checked by plan(); pieces need it sane before cutting
     if (b->frame_begin[0] != 0 || b->frame_begin[b->n_runs] != b->n_frames) return JAAD_ERR_INVALID_ARG;
@@ -1973,15 +2036,9 @@ int jaad_decode_batch_device(jaad_ctx* ctx, const jaad_batch* b, void* pcm_dev, 
     hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : ctx->stream;
     const int dropped = dropped_frames(b);
     if (dropped < 0) return dropped;
-    if (dropped == 0) {
-        jaad_batch d = *b;
-        d.frame_status = nullptr;
-        return launch(ctx, &d, pcm_dev, flags, s);
-    }
-    const size_t per = pcm_bytes_per_frame(ctx, flags);
-    return for_each_segment(ctx, b, [&](const jaad_batch& d, uint32_t f0) {
-        return launch(ctx, &d, static_cast<uint8_t*>(pcm_dev) + per * f0, flags, s);
-    });
+    jaad_batch d = *b;
+    if (!dropped) d.frame_status = nullptr;
+    return launch(ctx, &d, pcm_dev, flags, s);
 }
 
 int jaad_wait(jaad_ctx* ctx)
@@ -2034,37 +2091,34 @@ int jaad_state_export(jaad_ctx* ctx, uint32_t slot, void* buf, size_t bytes)
     return JAAD_OK;
 }
 
-int jaad_state_import(jaad_ctx* ctx, uint32_t slot, const void* buf, size_t bytes)
+// a state blob's checks (finite overlap, a table set this context can derive from its SBR header):
+// all of them run before anything is written, so a refused import leaves the slot (and, for a
+// multichannel context, every element's slot) as it was
+static int state_blob_check(jaad_ctx* ctx, const char* in, SbrHostSlot* hs)
 {
-    if (!ctx || !buf || slot >= ctx->n_slots || bytes < jaad_state_bytes(ctx)) return JAAD_ERR_INVALID_ARG;
-    int rc = sync_ctx(ctx);
-    if (rc) return rc;
-    const char* in = static_cast<const char*>(buf);
-    if (!ctx->children.empty()) {
-        for (jaad_ctx* c : ctx->children) {
-            const size_t n = jaad_state_bytes(c);
-            if ((rc = jaad_state_import(c, slot, in, n))) return rc;
-            in += n;
-        }
-        return JAAD_OK;
-    }
     for (int k = 0; k < ctx->n_elem; k++) {  // the overlap must be finite (the LC kernel's PCM rounding relies on it, jaad_lc.hip round_pk16)
         float ov[2048];
         std::memcpy(ov, in + (size_t)k * sizeof ov, sizeof ov);
         for (float v : ov)
             if (!std::isfinite(v)) return JAAD_ERR_INVALID_ARG;
     }
+    if (ctx->cfg.sbr) {
+        std::memcpy(hs, in + 2048 * sizeof(float) + 2 * sizeof(SbrChState), sizeof *hs);
+        if (hs->have_hdr) {  // re-derive the table index in this context from the saved header(s)
+            hs->table = ctx->sbr_host->table_index(*hs);
+            if (hs->table < 0) return JAAD_ERR_INVALID_ARG;
+        }
+    }
+    return JAAD_OK;
+}
+
+static int state_blob_apply(jaad_ctx* ctx, uint32_t slot, const char* in, const SbrHostSlot& hs)
+{
     for (int k = 0; k < ctx->n_elem; k++)
         HIPCHK(hipMemcpy(ctx->d_state[ctx->parity] + ((size_t)k * ctx->n_slots + slot) * 2048, in + (size_t)k * 2048 * sizeof(float),
                          2048 * sizeof(float), hipMemcpyHostToDevice));
     if (ctx->cfg.sbr) {
         in += 2048 * sizeof(float);
-        SbrHostSlot hs;
-        std::memcpy(&hs, in + 2 * sizeof(SbrChState), sizeof hs);
-        if (hs.have_hdr) {  // re-derive the table index in this context from the saved header(s)
-            hs.table = ctx->sbr_host->table_index(hs);
-            if (hs.table < 0) return JAAD_ERR_INVALID_ARG;
-        }
         HIPCHK(hipMemcpy(ctx->d_sbr_state + (size_t)slot * 2, in, 2 * sizeof(SbrChState), hipMemcpyHostToDevice));
         if (ctx->cfg.ps)
             HIPCHK(hipMemcpy(ctx->d_ps_state + slot, in + 2 * sizeof(SbrChState) + sizeof(SbrHostSlot), sizeof(PsState),
@@ -2072,6 +2126,32 @@ int jaad_state_import(jaad_ctx* ctx, uint32_t slot, const void* buf, size_t byte
         ctx->sbr_slots[slot] = hs;
     }
     return JAAD_OK;
+}
+
+int jaad_state_import(jaad_ctx* ctx, uint32_t slot, const void* buf, size_t bytes)
+{
+    if (!ctx || !buf || slot >= ctx->n_slots || bytes < jaad_state_bytes(ctx)) return JAAD_ERR_INVALID_ARG;
+    int rc = sync_ctx(ctx);
+    if (rc) return rc;
+    const char* in = static_cast<const char*>(buf);
+    if (!ctx->children.empty()) {
+        std::vector<SbrHostSlot> hs(ctx->children.size());
+        const char* p = in;
+        for (size_t k = 0; k < ctx->children.size(); k++) {  // every element's blob first
+            jaad_ctx* c = ctx->children[k];
+            if ((rc = sync_ctx(c)) || (rc = state_blob_check(c, p, &hs[k]))) return rc;
+            p += jaad_state_bytes(c);
+        }
+        for (size_t k = 0; k < ctx->children.size(); k++) {
+            jaad_ctx* c = ctx->children[k];
+            if ((rc = state_blob_apply(c, slot, in, hs[k]))) return rc;
+            in += jaad_state_bytes(c);
+        }
+        return JAAD_OK;
+    }
+    SbrHostSlot hs{};
+    if ((rc = state_blob_check(ctx, in, &hs))) return rc;
+    return state_blob_apply(ctx, slot, in, hs);
 }
 
 int jaad_state_reset(jaad_ctx* ctx, uint32_t slot)

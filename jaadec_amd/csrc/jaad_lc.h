@@ -82,6 +82,11 @@ struct KernelArgs {
     const uint32_t* cce_meta;
     const float* cce_spec;
     uint32_t ch0;
+    // batches with dropped frames (jaad_batch.frame_status): the planner's chunks cover the kept
+    // frames only, numbered consecutively ("virtual" frames, runs in the same order); fkeep[v] is
+    // the batch frame of virtual frame v, read for every input record and PCM frame.  Null: v is
+    // the batch frame.
+    const uint32_t* fkeep;
 };
 
 // inputs of cce_term_kernel: one wave per term
@@ -139,9 +144,9 @@ struct McInterleave {
     int n_out;
 };
 hipError_t launch_mc_interleave(const McInterleave& m, void* pcm, uint32_t n_frames, uint32_t samples, int bps,
-                                hipStream_t stream);
+                                hipStream_t stream, const uint32_t* fkeep = nullptr);
 hipError_t launch_pack(const float* planar, void* pcm, uint32_t n_frames, int n_ch, uint32_t flags,
-                       hipStream_t stream);
+                       hipStream_t stream, const uint32_t* fkeep = nullptr);
 // LC kernel waves that can be resident on one CU (occupancy query; 0 on failure)
 int lc_resident_waves_per_cu(bool tns_spec);
 }

@@ -920,7 +920,7 @@ struct Prefetch {
 
 // Everything frame f needs from HBM, as vector loads (vmcnt is in order; scalar loads would
 // share lgkmcnt with the LDS traffic and could not be left in flight).
-__device__ __forceinline__ void prefetch(const KernelArgs& A, int f, bool stereo, int u, Prefetch& pf)
+__device__ __forceinline__ void prefetch(const KernelArgs& A, int f, bool stereo, int u, Prefetch& pf, int vnext = 0)
 {
     const int nch = stereo ? 2 : 1;
 #pragma unroll
@@ -937,6 +937,9 @@ __device__ __forceinline__ void prefetch(const KernelArgs& A, int f, bool stereo
     const uint32_t* side = u < 8 ? reinterpret_cast<const uint32_t*>(A.ics + (size_t)f * A.cf_stride) + (u < 4 * nch ? u : 0)
                                  : (A.ms_used ? reinterpret_cast<const uint32_t*>(A.ms_used + (size_t)f * 2 * A.ms_stride) + (u & 3)
                                               : reinterpret_cast<const uint32_t*>(A.ics));
+    // batches with dropped frames: lane 63 carries the batch frame of the next kept frame
+    // (KernelArgs::fkeep[vnext]), which the loop needs for the prefetch one frame later
+    if (A.fkeep && u == 63) side = A.fkeep + vnext;
     pf.side = *side;
 }
 
@@ -1050,6 +1053,7 @@ __global__ __launch_bounds__(64 * waves_per_wg<kMode == 1>()) void lc_decode_ker
     struct Lds {
         LdsTables T;
         WaveLds<kTnsSpec> W[kW];
+        uint32_t rem[kW];  // frames each wave has left in its chunk (issue priority, below)
     };
     __shared__ Lds S;
     LdsTables& T = S.T;
@@ -1058,6 +1062,7 @@ __global__ __launch_bounds__(64 * waves_per_wg<kMode == 1>()) void lc_decode_ker
         const uint4* src = reinterpret_cast<const uint4*>(A.tables);
         uint4* dst = reinterpret_cast<uint4*>(&T);
         for (int i = threadIdx.x; i < (int)(sizeof(LdsTables) / 16); i += kThreads) dst[i] = src[i];
+        if (threadIdx.x < kW) S.rem[threadIdx.x] = 0u;
     }
     __syncthreads();  // the only workgroup barrier: waves are independent from here on
 #ifdef JAAD_WAVETIME
@@ -1117,8 +1122,13 @@ __global__ __launch_bounds__(64 * waves_per_wg<kMode == 1>()) void lc_decode_ker
                 for (int o = 0; o < 16; o++) ovL[o] = ovR[o] = 0.0f;
             }
         }
+        // Frames are "virtual" indices v (chunks cover consecutive v); the batch frame of v is
+        // fkeep[v] when the batch drops frames (KernelArgs::fkeep), else v itself.
+        const int v_last = f_first + my_n - 1;
+        int fr_next = f_first;  // batch frame of the iteration's frame
+        if (A.fkeep && my_n > 0) fr_next = (int)__builtin_amdgcn_readfirstlane(A.fkeep[f_first]);
         Prefetch pf;
-        if (my_n > 0) prefetch(A, f_first, stereo, lane_id(), pf);
+        if (my_n > 0) prefetch(A, fr_next, stereo, lane_id(), pf, min(f_first + 1, v_last));
         vmem_drain();  // (see vmem_drain) the loop head then finds no load pending on any path
 
         for (int it = 0; it < my_n; it++) {
@@ -1127,6 +1137,26 @@ __global__ __launch_bounds__(64 * waves_per_wg<kMode == 1>()) void lc_decode_ker
             // latency exposed.  A wave's priority drops as it advances through its chunk: the
             // waves that are behind catch up (C2: wave lifetimes 83 -> 89 % of the kernel span,
             // batch time -5 %, scripts/wavetime.py).
+#ifdef JAAD_PRIO_RANK
+            {
+                // the waves sharing this wave's SIMD are w +- 4 (a workgroup's waves go to the SIMDs
+                // in a fixed cyclic order): the one with the most frames left gets the highest
+                // priority, so that the SIMD's waves end together (longest remaining first)
+                const uint32_t rem = (uint32_t)(my_n - it);
+                volatile uint32_t* R = S.rem;
+                R[wave] = rem;
+                int p = 0;
+#pragma unroll
+                for (int m = 1; m < kW / 4; m++) {
+                    const int mate = (wave + 4 * m) % kW;
+                    const uint32_t r = __builtin_amdgcn_readfirstlane(R[mate]);
+                    p += (rem > r || (rem == r && wave > mate)) ? 1 : 0;
+                }
+                if (p >= 2) __builtin_amdgcn_s_setprio(3);
+                else if (p == 1) __builtin_amdgcn_s_setprio(2);
+                else __builtin_amdgcn_s_setprio(1);
+            }
+#else
             {
                 const int q4 = (4 * it) / my_n;
                 if (q4 == 0) __builtin_amdgcn_s_setprio(3);
@@ -1134,14 +1164,17 @@ __global__ __launch_bounds__(64 * waves_per_wg<kMode == 1>()) void lc_decode_ker
                 else if (q4 == 2) __builtin_amdgcn_s_setprio(1);
                 else __builtin_amdgcn_s_setprio(0);
             }
+#endif
 #ifdef JAAD_WAVETIME
             wt_frames++;
 #endif
             const int u = lane_id();
-            const int f = f_first + it;
-            const bool emit = f >= (int)cd.frame0;
+            const int fv = f_first + it;            // virtual frame
+            const bool emit = fv >= (int)cd.frame0;
+            const int f = fr_next;                   // batch frame
             const size_t cf0 = (size_t)f * A.cf_stride;
             const Prefetch cur = pf;
+            fr_next = A.fkeep ? (int)__builtin_amdgcn_readlane(cur.side, 63) : fv + 1;
 
             // ---------------- side info ----------------
             const Ics iL = ics_from_lanes(cur.side, 0, nswb_l, nswb_s);
@@ -1240,7 +1273,7 @@ __global__ __launch_bounds__(64 * waves_per_wg<kMode == 1>()) void lc_decode_ker
             STAMP(12);
             // issued on every iteration (the last one reloads its own frame) so that the VMEM
             // pattern of the loop body is the same on every path: see the PCM stores below
-            prefetch(A, it + 1 < my_n ? f + 1 : f, stereo, u, pf);
+            prefetch(A, it + 1 < my_n ? fr_next : f, stereo, u, pf, min(fv + 2, v_last));
 
             if ((iL.flags | (stereo ? iR.flags : 0)) & JAAD_ICS_HAS_PNS) {  // rare: lane 0 replays the LCG
                 // pns_fill reads the channel's raw sf/cb rows from rsp
@@ -1415,6 +1448,9 @@ __global__ __launch_bounds__(64 * waves_per_wg<kMode == 1>()) void lc_decode_ker
             STAMP(10);
         }
         STAMP(11);
+#ifdef JAAD_PRIO_RANK
+        reinterpret_cast<volatile uint32_t*>(S.rem)[wave] = 0u;
+#endif
         if (cd.info & kChunkStoreState) {
             const int u = lane_id();
             float* st = A.state_out + (size_t)cd.slot * 2048;
@@ -1470,11 +1506,15 @@ static hipError_t launch_lc_ch(const KernelArgs& a, hipStream_t stream, bool tns
 
 namespace {
 // one thread per (frame, sample instant): its n_ch planar samples -> n_ch interleaved outputs
+// (n_frames kept frames; fkeep, when not null, maps them to their batch frames: dropped frames'
+// PCM is left as it is)
 __global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ planar, void* __restrict__ pcm,
-                                                   uint32_t n_frames, int n_ch, uint32_t flags)
+                                                   uint32_t n_frames, int n_ch, uint32_t flags,
+                                                   const uint32_t* __restrict__ fkeep)
 {
-    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;  // frame * 1024 + sample
+    size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;  // frame * 1024 + sample
     if (i >= (size_t)n_frames * 1024) return;
+    if (fkeep) i = ((size_t)fkeep[i >> 10] << 10) | (i & 1023);
     const size_t f = i >> 10, n = i & 1023;
     const float* src = planar + f * (size_t)n_ch * 1024 + n;
     if (flags & JAAD_PCM_FLOAT32) {
@@ -1599,33 +1639,40 @@ hipError_t launch_check_q(const int16_t* q, size_t n, int* flag, hipStream_t str
 namespace {
 // one thread per (frame, sample instant): the output channels' words from the elements' PCM
 template <typename W>
-__global__ __launch_bounds__(256) void mc_interleave_kernel(McInterleave m, W* __restrict__ out, size_t n)
+__global__ __launch_bounds__(256) void mc_interleave_kernel(McInterleave m, W* __restrict__ out, size_t n,
+                                                            uint32_t samples, const uint32_t* __restrict__ fkeep)
 {
-    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;  // frame * samples + sample
+    size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;  // frame * samples + sample
     if (i >= n) return;
+    if (fkeep) i = (size_t)fkeep[i / samples] * samples + i % samples;  // kept frames only
     W* o = out + i * m.n_out;
     for (int c = 0; c < m.n_out; c++) o[c] = static_cast<const W*>(m.src[c])[2 * i + m.chan[c]];
 }
 }  // namespace
 
 hipError_t launch_mc_interleave(const McInterleave& m, void* pcm, uint32_t n_frames, uint32_t samples, int bps,
-                                hipStream_t stream)
+                                hipStream_t stream, const uint32_t* fkeep)
 {
     const size_t n = (size_t)n_frames * samples;
     if (!n) return hipSuccess;
     if (m.n_out < 1 || m.n_out > 16) return hipErrorInvalidValue;
     const dim3 grid((unsigned)((n + 255) / 256));
-    if (bps == 4) hipLaunchKernelGGL(mc_interleave_kernel<uint32_t>, grid, dim3(256), 0, stream, m, static_cast<uint32_t*>(pcm), n);
-    else hipLaunchKernelGGL(mc_interleave_kernel<uint16_t>, grid, dim3(256), 0, stream, m, static_cast<uint16_t*>(pcm), n);
+    if (bps == 4)
+        hipLaunchKernelGGL(mc_interleave_kernel<uint32_t>, grid, dim3(256), 0, stream, m, static_cast<uint32_t*>(pcm), n,
+                           samples, fkeep);
+    else
+        hipLaunchKernelGGL(mc_interleave_kernel<uint16_t>, grid, dim3(256), 0, stream, m, static_cast<uint16_t*>(pcm), n,
+                           samples, fkeep);
     return hipGetLastError();
 }
 
-hipError_t launch_pack(const float* planar, void* pcm, uint32_t n_frames, int n_ch, uint32_t flags, hipStream_t stream)
+hipError_t launch_pack(const float* planar, void* pcm, uint32_t n_frames, int n_ch, uint32_t flags, hipStream_t stream,
+                       const uint32_t* fkeep)
 {
     const size_t n = (size_t)n_frames * 1024;
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(pack_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, planar, pcm, n_frames, n_ch,
-                       flags);
+                       flags, fkeep);
     return hipGetLastError();
 }
 

@@ -906,7 +906,17 @@ int parse_frame_body(const jaad_parser* p, const uint8_t* data, size_t bytes, ja
                 SbrParseState& S = e == 0 ? ns.sbr : nsel[(size_t)e - 1];
                 const SbrParseState before = S;
                 const int st = parse_sbr(sub, C, C.elem_nch[e], type == 14, S, out->sbr[e]);
-                if (st == JAAD_ERR_EOS) S = before;  // a payload cut short moves no SBR state
+                if (st == JAAD_ERR_EOS) {
+                    // The bitstream ends inside the SBR payload.  The reference has read as much of
+                    // it as was there when its EOSException comes (SBR.decode: readHeader with its
+                    // header swap and calc_sbr_tables, then part of sbr_data, A/sbr/SBR.java:162-184),
+                    // a partial state change that no record here describes: the frame is refused
+                    // instead of dropped, so the stream cannot go on out of step (the parser keeps
+                    // its state).  A frame cut after its SBR payload is dropped with the payload's
+                    // record, header included (jaad_decode_batch applies it).
+                    S = before;
+                    return JAAD_ERR_UNSUPPORTED;
+                }
                 if (st) return st;
                 sbr_seen |= 1u << e;
             }

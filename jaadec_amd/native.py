@@ -714,8 +714,9 @@ class Parser:
                     a[i * nch:(i + 1) * nch] = 0
                 if ms is not None:
                     ms[i] = 0
-                if sbr is not None:
-                    sbr[i] = np.zeros((), SBR_FRAME_DTYPE)
+                # the SBR records stay as the parser left them: an SBR payload read whole before
+                # the bitstream ended keeps its header, which the reference swapped in before the
+                # EOSException (A/sbr/SBR.java:162-184) and the DSP stage applies (zero otherwise)
                 continue
             if rc:
                 raise JaadError(rc, f"jaad_parse_frame (frame {i})")

@@ -591,6 +591,17 @@ static int check_batch(const jaad_stream_cfg* cfg, const jaad_batch* b, size_t p
     return JAAD_OK;
 }
 
+/* A frame dropped as Decoder.decodeFrame drops it (EOSException caught, process() and accept skipped,
+ * A/Decoder.java:89-101): no DSP.  If its SBR payload was read whole before the bitstream ended,
+ * SBR.decode had already swapped in its header and recomputed the frequency tables (A/sbr/SBR.java:
+ * 162-184), as for a frame whose SBR data is invalid: orc_sbr_take_header. */
+static int dropped_frame(const jaad_stream_cfg* cfg, orc_stream* st, const jaad_batch* b, uint32_t f)
+{
+    if (!cfg->sbr || !b->sbr || !b->sbr[f].header_present) return JAAD_OK;
+    if (!st->sbr) return JAAD_ERR_UNSUPPORTED; /* no SBR frame has run: no patches to keep */
+    return orc_sbr_take_header(st->sbr, &b->sbr[f].hdr);
+}
+
 int orc_decode_batch(const jaad_stream_cfg* cfg, orc_stream* streams, const jaad_batch* b, void* pcm_out,
                      size_t pcm_bytes, uint32_t flags)
 {
@@ -601,8 +612,8 @@ int orc_decode_batch(const jaad_stream_cfg* cfg, orc_stream* streams, const jaad
     for (uint32_t r = 0; r < b->n_runs; r++) {
         orc_stream* st = &streams[b->stream_slot[r]];
         for (uint32_t f = b->frame_begin[r]; f < b->frame_begin[r + 1]; f++) {
-            if (b->frame_status && b->frame_status[f]) continue;  /* dropped (A/Decoder.java:96-100) */
-            rc = decode_frame(cfg, st, b, f, &rs, (unsigned char*)pcm_out + per * f, flags);
+            if (b->frame_status && b->frame_status[f]) rc = dropped_frame(cfg, st, b, f);
+            else rc = decode_frame(cfg, st, b, f, &rs, (unsigned char*)pcm_out + per * f, flags);
             if (rc) return rc;
         }
     }
@@ -627,8 +638,9 @@ static void* mt_worker(void* p)
     for (uint32_t r = j->r0; r < j->r1 && !j->rc; r++) {
         orc_stream* st = &j->streams[j->b->stream_slot[r]];
         for (uint32_t f = j->b->frame_begin[r]; f < j->b->frame_begin[r + 1] && !j->rc; f++)
-            if (!j->b->frame_status || !j->b->frame_status[f])
-                j->rc = decode_frame(j->cfg, st, j->b, f, &rs, j->pcm + j->per * f, j->flags);
+            j->rc = j->b->frame_status && j->b->frame_status[f]
+                        ? dropped_frame(j->cfg, st, j->b, f)
+                        : decode_frame(j->cfg, st, j->b, f, &rs, j->pcm + j->per * f, j->flags);
     }
     return NULL;
 }

@@ -162,6 +162,8 @@ def test_gpu_mc_sbr_calls_device_entry_drops_and_state():
     st = np.zeros(b.n_frames, np.uint8)
     st[[0, 7, 8, 30, 59]] = N.FRAME_EOS
     b.frame_status = st
+    from tests.test_frame_status import no_header_before_first_sbr
+    no_header_before_first_sbr(b, st)
     want2 = O.decode_batch_mc(6, b, IDS[cc], N.PCM_BIG_ENDIAN, threads=8, sbr=True)
     out = np.full(want2.shape, 0x11, np.uint8)
     with N.Context(cfg, 3) as ctx:
@@ -190,3 +192,44 @@ def test_gpu_mc_sbr_bitstream_through_the_decoder_facade():
         dec.decodeFrame(fr, buf)
         assert buf.getChannels() == 7 and buf.getData() == want[i].tobytes(), i
     dec.close()
+
+
+@pytest.mark.gpu
+def test_gpu_mc_sbr_rejected_element_leaves_every_element_as_it_was():
+    """element 2 of a 5.1 HE-AAC batch carries SBR data the stage refuses (a PS payload
+    with borders out of order is not what ps_data_decode produces; here: an unknown SBR status);
+    the call fails before any element launches, every element's slot state (core overlap, SBR
+    rings, host SBR state) is as before, and the same stream then decodes as if the call had not
+    happened.  And a state blob whose last element is bad is refused whole."""
+    cc = 6
+    b = mc_sbr_synth(cc, n_streams=2, fps=16, seed=9)
+    cfg = N.make_cfg(sf_index=6, channel_config=cc, sbr=True)
+    want = O.decode_batch_mc(6, b, IDS[cc], N.PCM_BIG_ENDIAN, threads=8, sbr=True)
+    a1, a2 = b.split_frames(6)
+    bad = N.Batch(a2.q, a2.sf, a2.cb, a2.ics, a2.ms_used, a2.tns, a2.stream_slot, a2.frame_begin, a2.nch,
+                  a2.sbr.copy(), **a2._cce_for(np.arange(a2.n_frames)))
+    bad.sbr["status"][3, 2] = 7  # element 2 (a CPE), frame 3 of the first run
+    with N.Context(cfg, 2) as ctx:
+        p1 = ctx.decode(a1, N.PCM_BIG_ENDIAN)
+        before = [ctx.state_export(s) for s in range(2)]
+        with pytest.raises(N.JaadError) as e:
+            ctx.decode(bad, N.PCM_BIG_ENDIAN)
+        assert e.value.status in (N.ERR_INVALID_ARG, N.ERR_BITSTREAM)
+        for s in range(2):
+            assert (ctx.state_export(s) == before[s]).all(), s
+        p2 = ctx.decode(a2, N.PCM_BIG_ENDIAN)
+        # a blob whose last element's overlap is not finite: refused before any element is written
+        blob = ctx.state_export(0)
+        broken = blob.copy()
+        n = len(broken)
+        last = 3 * n // 4  # four elements with blobs of one size: the LFE's overlap starts here
+        broken[last:last + 4] = np.frombuffer(np.float32(np.inf).tobytes(), np.uint8)
+        ctx.state_reset(0)
+        reset = ctx.state_export(0)
+        with pytest.raises(N.JaadError):
+            ctx.state_import(0, broken)
+        assert (ctx.state_export(0) == reset).all()
+    fb = b.frame_begin
+    for r in range(2):
+        assert (p1[6 * r:6 * r + 6] == want[fb[r]:fb[r] + 6]).all()
+        assert (p2[10 * r:10 * r + 10] == want[fb[r] + 6:fb[r + 1]]).all()

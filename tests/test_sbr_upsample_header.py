@@ -151,3 +151,120 @@ def test_gpu_upsample_header_refused(name):
         with pytest.raises(N.JaadError) as e:
             ctx.decode(b, N.PCM_FLOAT32)
     assert e.value.status == N.ERR_UNSUPPORTED
+
+
+# ------------------------------------------------------------------------------------------------
+# A dropped frame (jaad_batch.frame_status) whose SBR payload was read whole before the bitstream
+# ended: Decoder.decodeFrame catches the EOSException after SBR.decode swapped in the header
+# (A/Decoder.java:89-101, A/sbr/SBR.java:162-184) and skips process() -- the same SBR state change
+# as an upsampled frame's header, without any PCM.
+# ------------------------------------------------------------------------------------------------
+
+def _dropped(b, frame):
+    """b with frame `frame` of every stream marked dropped (its records, header included, kept)."""
+    st = np.zeros(b.n_frames, np.uint8)
+    st[np.arange(b.n_frames) % FPS == frame] = N.FRAME_EOS
+    d = N.Batch(b.q, b.sf, b.cb, b.ics, b.ms_used, b.tns, b.stream_slot, b.frame_begin, b.nch, b.sbr.copy())
+    d.frame_status = st
+    return d
+
+
+@pytest.mark.parametrize("name", ["kx_up", "back_and_forth", "kx_up_then_reset"])
+def test_oracle_dropped_frame_takes_its_header(name):
+    """The header of the dropped frame is in the SBR state afterwards: the next frame, which carries
+    the same header, runs without a reset on the mixed tables (SbrHost::take_header), so the stream
+    decodes differently from the same batch with the dropped frame's header removed (the next frame
+    then resets), and equally up to the dropped frame."""
+    p, up = _batch(4, ACCEPTED[name])
+    frame = ACCEPTED[name][0][0]
+    cfg = N.cfg_for(p)
+    with_hdr = _dropped(up, frame)
+    no_hdr = _dropped(up, frame)
+    no_hdr.sbr["header_present"][np.arange(up.n_frames) % FPS == frame] = 0
+    a = O.decode_batch(cfg, with_hdr, O.Streams(2), N.PCM_FLOAT32, threads=4)
+    b = O.decode_batch(cfg, no_hdr, O.Streams(2), N.PCM_FLOAT32, threads=4)
+    rows = np.arange(up.n_frames) % FPS
+    assert not a[rows == frame].any() and not b[rows == frame].any()
+    assert np.array_equal(a[rows < frame], b[rows < frame])
+    assert not np.array_equal(a[rows > frame], b[rows > frame])
+
+
+def test_oracle_dropped_first_header_refused():
+    """A stream's first SBR header on a dropped frame: no processed frame has built patches."""
+    p, b = _batch(4, [])
+    s = b.sbr.copy()
+    s["header_present"][np.arange(b.n_frames) % FPS == 1] = 0  # frame 1 would bring the header too
+    d = _dropped(N.Batch(b.q, b.sf, b.cb, b.ics, b.ms_used, b.tns, b.stream_slot, b.frame_begin, b.nch, s), 0)
+    with pytest.raises(RuntimeError) as e:
+        O.decode_batch(N.cfg_for(p), d, O.Streams(2), N.PCM_FLOAT32)
+    assert _refused(str(e.value))
+
+
+def _cut_after_payload():
+    """A stream whose frame k = FPS // 2 changes the SBR header, written with a fill element after
+    the SBR payload (the writer's `extras`), and the shortest cut of frame k that leaves the SBR
+    payload whole.  Returns (p, cfg, frames, k, cut, cut_batch, whole_batch)."""
+    from tests.test_parse_sbr import _stream
+    k = FPS // 2
+    p, b = _stream(4, FPS, 5, header_gaps=False, header_change=True)
+    cfg = N.cfg_for(p)
+    frames = O.write_frames(b, p.sf_index, extras=1, sbr_writer=O.SbrWriter(cfg.ext_sf_index, 5))
+    P = N.Parser(cfg)
+    P.pns_state = int(b.ics["pns_state"][0])
+    whole = P.parse(frames)
+    P.close()
+    for cut in range(1, 8):
+        P = N.Parser(cfg)
+        P.pns_state = int(b.ics["pns_state"][0])
+        try:
+            got = P.parse(frames[:k] + [frames[k][:-cut]] + frames[k + 1:], drop_eos=True)
+        except N.JaadError as e:
+            assert e.status == N.ERR_UNSUPPORTED  # a cut inside the SBR payload is refused
+            continue
+        finally:
+            P.close()
+        assert np.flatnonzero(got.frame_status).tolist() == [k]
+        if got.sbr[k]["header_present"]:
+            return p, cfg, frames, k, cut, got, whole
+    raise AssertionError("no cut of frame k left its SBR payload whole")
+
+
+def test_parser_frame_cut_after_its_sbr_payload_keeps_the_header():
+    """a HE-AAC frame whose bitstream ends after its SBR payload is dropped with the
+    payload's record, the new header included, and the frames after it parse as in the whole stream
+    (the parser state moved with the payload, as the reference's SBR.decode had run); a cut inside
+    the SBR payload is refused instead (the reference would have applied part of it)."""
+    p, cfg, frames, k, cut, got, whole = _cut_after_payload()
+    assert whole.sbr[k]["hdr"].tobytes() != whole.sbr[k - 1]["hdr"].tobytes()
+    assert got.sbr[k]["hdr"].tobytes() == whole.sbr[k]["hdr"].tobytes()
+    assert got.sbr[k + 1:].tobytes() == whole.sbr[k + 1:].tobytes()
+    assert (got.q[(k + 1) * got.nch:] == whole.q[(k + 1) * got.nch:]).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfgid", [4, 5])
+def test_gpu_dropped_frame_header_matches_oracle(cfgid):
+    p, up = _batch(cfgid, ACCEPTED["kx_up"])
+    d = _dropped(up, 8)
+    cfg = N.cfg_for(p)
+    want = O.decode_batch(cfg, d, O.Streams(2), N.PCM_FLOAT32, threads=8)
+    nb = want.shape[1]
+    out = np.full((d.n_frames, nb), 0x6B, np.uint8)
+    with N.Context(cfg, 2) as ctx:
+        ctx.decode(d, N.PCM_FLOAT32, out=out)
+    rows = np.arange(d.n_frames) % FPS
+    assert (out[rows == 8] == 0x6B).all()
+    _same(out[rows != 8], want[rows != 8])
+
+
+@pytest.mark.gpu
+def test_gpu_bitstream_frame_cut_after_its_sbr_payload():
+    """The parsed stream of test_parser_frame_cut_after_its_sbr_payload_keeps_the_header through the
+    HIP path == the restatement (both take the dropped frame's header); its PCM slot untouched."""
+    p, cfg, frames, k, cut, got, whole = _cut_after_payload()
+    want = O.decode_batch(cfg, got, O.Streams(1), N.PCM_BIG_ENDIAN)
+    with N.Context(cfg, 1) as ctx:
+        out = np.full(want.shape, 0x22, np.uint8)
+        ctx.decode(got, N.PCM_BIG_ENDIAN, out=out)
+    assert (out[k] == 0x22).all()
+    assert (np.delete(out, k, 0) == np.delete(want, k, 0)).all()
