@@ -215,13 +215,15 @@ struct jaad_ctx {
     std::vector<ChunkDesc> chunks;
     std::vector<uint32_t> plan_slots, plan_begin;  // plan cache key
     // dropped frames (jaad_batch.frame_status): the call's kept batch frames in order (virtual
-    // frame -> batch frame) and the runs' first virtual frames; the list's device copy is
-    // KernelArgs::fkeep (staged like the chunk table)
-    std::vector<uint32_t> keep, vbegin;
-    DevBuf d_keep;
-    PinnedBuf h_keep;
-    hipEvent_t keep_copied = nullptr;
-    bool keep_live = false;
+    // frame -> batch frame), the runs' first virtual frames, and the runs of dropped frames as
+    // (first, count) pairs + sentinel (KernelArgs::skips: uploaded behind the chunk table, and
+    // part of the plan cache key).  d_skips: a copy for the multichannel HE-AAC interleave.
+    std::vector<uint32_t> keep, vbegin, skips, plan_skips;
+    DevBuf d_skips;
+    PinnedBuf h_skips;
+    hipEvent_t skips_copied = nullptr;
+    bool skips_live = false;
+    uint32_t plan_n_chunks = 0;  // skip list offset in d_chunks (ChunkDesc units)
     std::vector<uint8_t> slot_used;
     bool plan_valid = false;
     int n_cu = 256;
@@ -389,6 +391,9 @@ int validate_cfg(const jaad_stream_cfg* cfg)
 // call's stream (ordered after the previous call by launch()) from page-locked staging.
 // `size_frames` (0: the batch's) is the frame count one launch covers: the host-buffer entry
 // launches the kernel once per piece of the batch, so its chunks are sized for a piece.
+// b: the planner's view of the call (with dropped frames: keep_map's virtual batch, the kept
+// frames numbered consecutively); the chunks it writes hold batch frames (ctx->keep translates
+// them when ctx->skips is not empty, the skip list then follows the chunk table on the device)
 int plan(jaad_ctx* ctx, const jaad_batch* b, hipStream_t stream, uint32_t size_frames = 0)
 {
     if (!b->stream_slot || !b->frame_begin) return JAAD_ERR_INVALID_ARG;
@@ -405,7 +410,8 @@ int plan(jaad_ctx* ctx, const jaad_batch* b, hipStream_t stream, uint32_t size_f
     L = std::min<uint32_t>(L, 0xffff);
     bool same = ctx->plan_valid && ctx->plan_L == L && ctx->plan_slots.size() == b->n_runs &&
                 std::memcmp(ctx->plan_slots.data(), b->stream_slot, b->n_runs * sizeof(uint32_t)) == 0 &&
-                std::memcmp(ctx->plan_begin.data(), b->frame_begin, (b->n_runs + 1) * sizeof(uint32_t)) == 0;
+                std::memcmp(ctx->plan_begin.data(), b->frame_begin, (b->n_runs + 1) * sizeof(uint32_t)) == 0 &&
+                ctx->plan_skips == ctx->skips;
     if (same) return JAAD_OK;
     std::vector<ChunkDesc> chunks;
     std::vector<uint8_t> used(ctx->n_slots, 0);
@@ -430,13 +436,34 @@ int plan(jaad_ctx* ctx, const jaad_batch* b, hipStream_t stream, uint32_t size_f
             chunks.push_back(ChunkDesc{f, info, slot, 0});
         }
     }
+    if (!ctx->skips.empty()) {  // virtual frames -> batch frames; each chunk's first skip entry
+        const std::vector<uint32_t>& k = ctx->keep;
+        const uint32_t ns = (uint32_t)ctx->skips.size() / 2;  // incl. the sentinel
+        for (ChunkDesc& c : chunks) {
+            if ((c.info & 0xffff) == 0) continue;  // empty run: no frame is read
+            const uint32_t v0 = c.frame0 - ((c.info & kChunkPrefix) ? 1 : 0);
+            c.frame0 = k[v0];
+            uint32_t lo = 0, hi = ns - 1;  // first run of dropped frames starting after frame0
+            while (lo < hi) {
+                const uint32_t m = (lo + hi) / 2;
+                if (ctx->skips[2 * m] <= c.frame0) lo = m + 1;
+                else hi = m;
+            }
+            c.skip = lo;
+        }
+    } else {
+        for (ChunkDesc& c : chunks) c.frame0 -= (c.info & kChunkPrefix) ? 1 : 0;
+    }
     ctx->plan_valid = false;  // from here on the cached layout no longer describes d_chunks
-    const size_t bytes = chunks.size() * sizeof(ChunkDesc);
+    const size_t cbytes = chunks.size() * sizeof(ChunkDesc);
+    const size_t bytes = cbytes + ctx->skips.size() * sizeof(uint32_t);
     if (ctx->chunks_live) HIPCHK(hipEventSynchronize(ctx->chunks_copied));  // staging in use?
     HIPCHK(ctx->h_chunks.ensure(bytes + 16));
     HIPCHK(ctx->d_chunks.ensure(bytes + 16));
     if (bytes) {
-        std::memcpy(ctx->h_chunks.p, chunks.data(), bytes);
+        std::memcpy(ctx->h_chunks.p, chunks.data(), cbytes);
+        if (!ctx->skips.empty())
+            std::memcpy(static_cast<char*>(ctx->h_chunks.p) + cbytes, ctx->skips.data(), bytes - cbytes);
         HIPCHK(hipMemcpyAsync(ctx->d_chunks.p, ctx->h_chunks.p, bytes, hipMemcpyHostToDevice, stream));
         HIPCHK(hipEventRecord(ctx->chunks_copied, stream));
         ctx->chunks_live = true;
@@ -446,6 +473,8 @@ int plan(jaad_ctx* ctx, const jaad_batch* b, hipStream_t stream, uint32_t size_f
     ctx->plan_slots.assign(b->stream_slot, b->stream_slot + b->n_runs);
     ctx->plan_begin.assign(b->frame_begin, b->frame_begin + b->n_runs + 1);
     ctx->plan_L = L;
+    ctx->plan_skips = ctx->skips;
+    ctx->plan_n_chunks = (uint32_t)ctx->chunks.size();
     ctx->plan_valid = true;
     return JAAD_OK;
 }
@@ -461,12 +490,13 @@ int sync_ctx(jaad_ctx* ctx)
 
 // Dropped frames (jaad_batch.frame_status, A/Decoder.java:89-101): the kernels of the call walk
 // the kept frames only.  `vb` becomes the planner's view of the batch (the kept frames numbered
-// consecutively, runs in the same order and slots); `*d_keep` (null when nothing is dropped) is
-// the device copy of virtual frame -> batch frame, which the LC kernel and the pack passes read.
-int keep_map(jaad_ctx* ctx, const jaad_batch* b, hipStream_t stream, jaad_batch& vb, const uint32_t** d_keep)
+// consecutively, runs in the same order and slots); ctx->keep maps them back to batch frames and
+// ctx->skips lists the runs of dropped frames (empty when nothing is dropped), which plan() turns
+// into batch-frame chunks and the device skip list.
+int keep_map(jaad_ctx* ctx, const jaad_batch* b, jaad_batch& vb)
 {
     vb = *b;
-    *d_keep = nullptr;
+    ctx->skips.clear();
     if (!b->frame_status) return JAAD_OK;
     if (!b->stream_slot || !b->frame_begin) return JAAD_ERR_INVALID_ARG;
     if (b->frame_begin[0] != 0 || b->frame_begin[b->n_runs] != b->n_frames) return JAAD_ERR_INVALID_ARG;
@@ -483,19 +513,48 @@ int keep_map(jaad_ctx* ctx, const jaad_batch* b, hipStream_t stream, jaad_batch&
     vb.n_frames = (uint32_t)keep.size();
     vb.frame_begin = vbeg.data();
     if (keep.size() == b->n_frames) return JAAD_OK;  // nothing dropped
-    const size_t bytes = keep.size() * sizeof(uint32_t);
-    if (ctx->keep_live) HIPCHK(hipEventSynchronize(ctx->keep_copied));  // staging in use?
-    HIPCHK(ctx->h_keep.ensure(bytes + 16));
-    HIPCHK(ctx->d_keep.ensure(bytes + 16));
-    if (bytes) {
-        std::memcpy(ctx->h_keep.p, keep.data(), bytes);
-        HIPCHK(hipMemcpyAsync(ctx->d_keep.p, ctx->h_keep.p, bytes, hipMemcpyHostToDevice, stream));
-        HIPCHK(hipEventRecord(ctx->keep_copied, stream));
-        ctx->keep_live = true;
+    for (uint32_t f = 0; f < b->n_frames;) {
+        if (b->frame_status[f] == JAAD_FRAME_DECODE) {
+            f++;
+            continue;
+        }
+        uint32_t e = f + 1;
+        while (e < b->n_frames && b->frame_status[e] != JAAD_FRAME_DECODE) e++;
+        ctx->skips.push_back(f);
+        ctx->skips.push_back(e - f);
+        f = e;
     }
-    *d_keep = static_cast<const uint32_t*>(ctx->d_keep.p);
+    ctx->skips.push_back(UINT32_MAX);  // sentinel: never the frame after a kept one
+    ctx->skips.push_back(0);
     return JAAD_OK;
 }
+
+// device copy of ctx->skips for a launch that plans no LC chunks itself (the multichannel HE-AAC
+// interleave); null when nothing is dropped
+int upload_skips(jaad_ctx* ctx, hipStream_t stream, const uint32_t** d)
+{
+    *d = nullptr;
+    if (ctx->skips.empty()) return JAAD_OK;
+    const size_t bytes = ctx->skips.size() * sizeof(uint32_t);
+    if (ctx->skips_live) HIPCHK(hipEventSynchronize(ctx->skips_copied));  // staging in use?
+    HIPCHK(ctx->h_skips.ensure(bytes));
+    HIPCHK(ctx->d_skips.ensure(bytes));
+    std::memcpy(ctx->h_skips.p, ctx->skips.data(), bytes);
+    HIPCHK(hipMemcpyAsync(ctx->d_skips.p, ctx->h_skips.p, bytes, hipMemcpyHostToDevice, stream));
+    HIPCHK(hipEventRecord(ctx->skips_copied, stream));
+    ctx->skips_live = true;
+    *d = static_cast<const uint32_t*>(ctx->d_skips.p);
+    return JAAD_OK;
+}
+
+// the device skip list behind the chunk table of the current plan (null: nothing dropped)
+const uint32_t* plan_skips_dev(const jaad_ctx* ctx)
+{
+    if (ctx->plan_skips.empty()) return nullptr;
+    return reinterpret_cast<const uint32_t*>(static_cast<const ChunkDesc*>(ctx->d_chunks.p) + ctx->plan_n_chunks);
+}
+
+uint32_t n_skip_runs(const jaad_ctx* ctx) { return ctx->skips.empty() ? 0u : (uint32_t)ctx->skips.size() / 2 - 1; }
 
 bool frame_dropped(const jaad_batch* b, size_t f) { return b->frame_status && b->frame_status[f] != JAAD_FRAME_DECODE; }
 
@@ -612,7 +671,7 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
     }
     rbeg[b->n_runs] = (uint32_t)fmap.size();
     const size_t nr = fmap.size(), ncf = nr * nch;  // records, record ch-frames
-    const bool identity = ups.empty();
+    const bool identity = nr == nf;  // no upsampled and no dropped frame: record = batch frame
 
     // chunk plan (records of each run).  Synthesis chunks: one wave each, its 9-slot v history
     // recomputed, a run's records split into chunks of equal length (+-1) of about kSbrSynFrames.
@@ -994,8 +1053,7 @@ int launch_work(jaad_ctx* ctx, const jaad_batch* db, void* pcm, uint32_t flags, 
 {
     if (!ctx->children.empty()) return launch_mc_sbr(ctx, db, pcm, flags, stream);
     jaad_batch vb;  // the kept frames (dropped frames are not planned)
-    const uint32_t* d_keep = nullptr;
-    int rc = keep_map(ctx, db, stream, vb, &d_keep);
+    int rc = keep_map(ctx, db, vb);
     if (rc) return rc;
     rc = plan(ctx, &vb, stream);
     if (rc) return rc;
@@ -1024,7 +1082,7 @@ int launch_work(jaad_ctx* ctx, const jaad_batch* db, void* pcm, uint32_t flags, 
     a.tns_mode = ctx->cfg.tns_mode;
     a.dbg = ctx->dbg;
     a.dbg_frame = ctx->dbg_frame;
-    a.fkeep = d_keep;
+    a.skips = plan_skips_dev(ctx);
     if (a.n_chunks == 0) return JAAD_OK;
     if (db->n_cce_terms && (rc = setup_coupling(ctx, db, a, stream))) return rc;
     if (ctx->n_elem > 1) {
@@ -1055,7 +1113,8 @@ int launch_work(jaad_ctx* ctx, const jaad_batch* db, void* pcm, uint32_t flags, 
             ch0 += n;
             cpe += n == 2;
         }
-        HIPCHK(launch_pack(static_cast<const float*>(ctx->d_time.p), pcm, vb.n_frames, ctx->nch, flags, stream, d_keep));
+        HIPCHK(launch_pack(static_cast<const float*>(ctx->d_time.p), pcm, db->n_frames, ctx->nch, flags, stream, a.skips,
+                           n_skip_runs(ctx)));
         ctx->parity ^= 1;
         return JAAD_OK;
     }
@@ -1115,9 +1174,11 @@ int launch_mc_sbr(jaad_ctx* ctx, const jaad_batch* db, void* pcm, uint32_t flags
     const int ne = ctx->n_elem, nch = ctx->nch;
     if (!db->sbr) return JAAD_ERR_INVALID_ARG;
     jaad_batch vb;  // dropped frames: each child skips them, the interleave pass leaves their PCM
-    const uint32_t* d_keep = nullptr;
-    int krc = keep_map(ctx, db, stream, vb, &d_keep);
+    int krc = keep_map(ctx, db, vb);
     if (krc) return krc;
+    const uint32_t* d_skips = nullptr;
+    if ((krc = upload_skips(ctx, stream, &d_skips))) return krc;
+    const uint32_t n_skips = n_skip_runs(ctx);
     // element kinds of the layout: an SCE must carry SBR data in every frame (without it the
     // reference's channel list shrinks, A/syntax/SCE.java:122-132), an LFE never does
     for (size_t f = 0; f < nf; f++)
@@ -1216,7 +1277,7 @@ int launch_mc_sbr(jaad_ctx* ctx, const jaad_batch* db, void* pcm, uint32_t flags
             m.n_out++;
         }
     }
-    HIPCHK(launch_mc_interleave(m, pcm, vb.n_frames, (uint32_t)S, (int)bps, stream, d_keep));
+    HIPCHK(launch_mc_interleave(m, pcm, (uint32_t)nf, (uint32_t)S, (int)bps, stream, d_skips, n_skips));
     return JAAD_OK;
 }
 
@@ -1345,7 +1406,7 @@ int jaad_ctx_create(const jaad_stream_cfg* cfg, uint32_t n_slots, int device, ja
     if ((e = hipEventCreateWithFlags(&ctx->done, hipEventDisableTiming)) != hipSuccess) return bail(e, "hipEventCreate");
     if ((e = hipEventCreateWithFlags(&ctx->chunks_copied, hipEventDisableTiming)) != hipSuccess)
         return bail(e, "hipEventCreate");
-    if ((e = hipEventCreateWithFlags(&ctx->keep_copied, hipEventDisableTiming)) != hipSuccess)
+    if ((e = hipEventCreateWithFlags(&ctx->skips_copied, hipEventDisableTiming)) != hipSuccess)
         return bail(e, "hipEventCreate");
     size_t sbytes = (size_t)ctx->n_elem * n_slots * 2048 * sizeof(float);  // [element][slot][2][1024]
     for (int i = 0; i < 2; i++) {
@@ -1490,9 +1551,9 @@ void jaad_ctx_destroy(jaad_ctx* ctx)
     ctx->h_chunks.release();
     if (ctx->done) (void)hipEventDestroy(ctx->done);
     if (ctx->chunks_copied) (void)hipEventDestroy(ctx->chunks_copied);
-    if (ctx->keep_copied) (void)hipEventDestroy(ctx->keep_copied);
-    ctx->d_keep.release();
-    ctx->h_keep.release();
+    if (ctx->skips_copied) (void)hipEventDestroy(ctx->skips_copied);
+    ctx->d_skips.release();
+    ctx->h_skips.release();
     ctx->d_batch.release();
     ctx->d_pcm.release();
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -1771,8 +1832,9 @@ static int decode_batch_pieces_impl(jaad_ctx* ctx, const jaad_batch* b, void* pc
 
     hipStream_t s = ctx->stream;
     if (ctx->done_live && ctx->last_stream != s) HIPCHK(hipStreamWaitEvent(s, ctx->done, 0));
-    {   // the planner reads only the run layout and the frame count
+    {   // the planner reads only the run layout and the frame count (no frame is dropped here)
         jaad_batch db = *b;
+        ctx->skips.clear();
         int rc = plan(ctx, &db, s, (uint32_t)maxf);
         if (rc) return rc;
     }

@@ -15,11 +15,13 @@ constexpr int kIqHead = 1024;
 // FilterBank.process depends only on the frame that writes it:
 // A/filterbank/FilterBank.java:46-51,61-70,90-100,116-118 overwrite all 1024 samples).
 struct ChunkDesc {
-    uint32_t frame0;
+    uint32_t frame0; // batch frame of the chunk's first iteration (the re-decoded previous frame
+                     // when bit16 is set)
     uint32_t info;   // [15:0] frames, bit16 recompute previous frame, bit17 load slot state,
                      // bit18 store slot state after the last frame
     uint32_t slot;
-    uint32_t pad;
+    uint32_t skip;   // batches with dropped frames: index of the first KernelArgs::skips entry
+                     // past frame0 (0 otherwise)
 };
 enum : uint32_t { kChunkPrefix = 1u << 16, kChunkLoadState = 1u << 17, kChunkStoreState = 1u << 18 };
 
@@ -82,11 +84,11 @@ struct KernelArgs {
     const uint32_t* cce_meta;
     const float* cce_spec;
     uint32_t ch0;
-    // batches with dropped frames (jaad_batch.frame_status): the planner's chunks cover the kept
-    // frames only, numbered consecutively ("virtual" frames, runs in the same order); fkeep[v] is
-    // the batch frame of virtual frame v, read for every input record and PCM frame.  Null: v is
-    // the batch frame.
-    const uint32_t* fkeep;
+    // batches with dropped frames (jaad_batch.frame_status): the maximal runs of dropped batch
+    // frames as (first frame, count) pairs in frame order, closed by (0xFFFFFFFF, 0).  A chunk's
+    // wave steps from frame f to f + 1, or past the run of dropped frames that starts there.
+    // Null: no frame is dropped.
+    const uint32_t* skips;
 };
 
 // inputs of cce_term_kernel: one wave per term
@@ -143,10 +145,11 @@ struct McInterleave {
     int chan[16];
     int n_out;
 };
+// (skips / n_skips: the dropped-frame runs as in KernelArgs::skips, whose PCM is left as it is)
 hipError_t launch_mc_interleave(const McInterleave& m, void* pcm, uint32_t n_frames, uint32_t samples, int bps,
-                                hipStream_t stream, const uint32_t* fkeep = nullptr);
+                                hipStream_t stream, const uint32_t* skips = nullptr, uint32_t n_skips = 0);
 hipError_t launch_pack(const float* planar, void* pcm, uint32_t n_frames, int n_ch, uint32_t flags,
-                       hipStream_t stream, const uint32_t* fkeep = nullptr);
+                       hipStream_t stream, const uint32_t* skips = nullptr, uint32_t n_skips = 0);
 // LC kernel waves that can be resident on one CU (occupancy query; 0 on failure)
 int lc_resident_waves_per_cu(bool tns_spec);
 }

@@ -920,7 +920,7 @@ struct Prefetch {
 
 // Everything frame f needs from HBM, as vector loads (vmcnt is in order; scalar loads would
 // share lgkmcnt with the LDS traffic and could not be left in flight).
-__device__ __forceinline__ void prefetch(const KernelArgs& A, int f, bool stereo, int u, Prefetch& pf, int vnext = 0)
+__device__ __forceinline__ void prefetch(const KernelArgs& A, int f, bool stereo, int u, Prefetch& pf, int skip = 0)
 {
     const int nch = stereo ? 2 : 1;
 #pragma unroll
@@ -937,9 +937,9 @@ __device__ __forceinline__ void prefetch(const KernelArgs& A, int f, bool stereo
     const uint32_t* side = u < 8 ? reinterpret_cast<const uint32_t*>(A.ics + (size_t)f * A.cf_stride) + (u < 4 * nch ? u : 0)
                                  : (A.ms_used ? reinterpret_cast<const uint32_t*>(A.ms_used + (size_t)f * 2 * A.ms_stride) + (u & 3)
                                               : reinterpret_cast<const uint32_t*>(A.ics));
-    // batches with dropped frames: lane 63 carries the batch frame of the next kept frame
-    // (KernelArgs::fkeep[vnext]), which the loop needs for the prefetch one frame later
-    if (A.fkeep && u == 63) side = A.fkeep + vnext;
+    // batches with dropped frames: lanes 63 / 62 carry skip entry `skip` (first frame, count of
+    // the next run of dropped frames), which the loop reads to step to the frame after this one
+    if (A.skips && u >= 62) side = A.skips + 2 * skip + (u == 62);
     pf.side = *side;
 }
 
@@ -1105,7 +1105,7 @@ __global__ __launch_bounds__(64 * waves_per_wg<kMode == 1>()) void lc_decode_ker
         const int nfr = cd.info & 0xffff;
         const bool prefix = (cd.info & kChunkPrefix) != 0;
         const int my_n = nfr + (prefix ? 1 : 0);
-        const int f_first = (int)cd.frame0 - (prefix ? 1 : 0);
+        const int f_first = (int)cd.frame0;  // batch frame of the first iteration
 
         float ovL[16], ovR[16];
         {
@@ -1122,13 +1122,13 @@ __global__ __launch_bounds__(64 * waves_per_wg<kMode == 1>()) void lc_decode_ker
                 for (int o = 0; o < 16; o++) ovL[o] = ovR[o] = 0.0f;
             }
         }
-        // Frames are "virtual" indices v (chunks cover consecutive v); the batch frame of v is
-        // fkeep[v] when the batch drops frames (KernelArgs::fkeep), else v itself.
-        const int v_last = f_first + my_n - 1;
+        // The chunk's frames are batch frames f_first, then f + 1 after each frame f, except
+        // where a run of dropped frames starts (KernelArgs::skips: entry `skip` is the next such
+        // run, loaded with each frame's side info).
+        int skip = (int)cd.skip;
         int fr_next = f_first;  // batch frame of the iteration's frame
-        if (A.fkeep && my_n > 0) fr_next = (int)__builtin_amdgcn_readfirstlane(A.fkeep[f_first]);
         Prefetch pf;
-        if (my_n > 0) prefetch(A, fr_next, stereo, lane_id(), pf, min(f_first + 1, v_last));
+        if (my_n > 0) prefetch(A, fr_next, stereo, lane_id(), pf, skip);
         vmem_drain();  // (see vmem_drain) the loop head then finds no load pending on any path
 
         for (int it = 0; it < my_n; it++) {
@@ -1169,12 +1169,15 @@ __global__ __launch_bounds__(64 * waves_per_wg<kMode == 1>()) void lc_decode_ker
             wt_frames++;
 #endif
             const int u = lane_id();
-            const int fv = f_first + it;            // virtual frame
-            const bool emit = fv >= (int)cd.frame0;
+            const bool emit = it >= (prefix ? 1 : 0);
             const int f = fr_next;                   // batch frame
             const size_t cf0 = (size_t)f * A.cf_stride;
             const Prefetch cur = pf;
-            fr_next = A.fkeep ? (int)__builtin_amdgcn_readlane(cur.side, 63) : fv + 1;
+            fr_next = f + 1;
+            if (A.skips && fr_next == __builtin_amdgcn_readlane(cur.side, 63)) {  // step over dropped frames
+                fr_next += __builtin_amdgcn_readlane(cur.side, 62);
+                skip++;
+            }
 
             // ---------------- side info ----------------
             const Ics iL = ics_from_lanes(cur.side, 0, nswb_l, nswb_s);
@@ -1273,7 +1276,7 @@ __global__ __launch_bounds__(64 * waves_per_wg<kMode == 1>()) void lc_decode_ker
             STAMP(12);
             // issued on every iteration (the last one reloads its own frame) so that the VMEM
             // pattern of the loop body is the same on every path: see the PCM stores below
-            prefetch(A, it + 1 < my_n ? fr_next : f, stereo, u, pf, min(fv + 2, v_last));
+            prefetch(A, it + 1 < my_n ? fr_next : f, stereo, u, pf, skip);
 
             if ((iL.flags | (stereo ? iR.flags : 0)) & JAAD_ICS_HAS_PNS) {  // rare: lane 0 replays the LCG
                 // pns_fill reads the channel's raw sf/cb rows from rsp
@@ -1505,17 +1508,28 @@ static hipError_t launch_lc_ch(const KernelArgs& a, hipStream_t stream, bool tns
 }
 
 namespace {
+// is batch frame f in one of the n dropped-frame runs of `skips` (KernelArgs::skips)?
+__device__ __forceinline__ bool frame_skipped(const uint32_t* __restrict__ skips, uint32_t n, uint32_t f)
+{
+    uint32_t lo = 0, hi = n;  // first run starting after f
+    while (lo < hi) {
+        const uint32_t m = (lo + hi) >> 1;
+        if (skips[2 * m] <= f) lo = m + 1;
+        else hi = m;
+    }
+    return lo > 0 && f - skips[2 * (lo - 1)] < skips[2 * (lo - 1) + 1];
+}
+
 // one thread per (frame, sample instant): its n_ch planar samples -> n_ch interleaved outputs
-// (n_frames kept frames; fkeep, when not null, maps them to their batch frames: dropped frames'
-// PCM is left as it is)
+// (dropped frames' PCM is left as it is)
 __global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ planar, void* __restrict__ pcm,
                                                    uint32_t n_frames, int n_ch, uint32_t flags,
-                                                   const uint32_t* __restrict__ fkeep)
+                                                   const uint32_t* __restrict__ skips, uint32_t n_skips)
 {
-    size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;  // frame * 1024 + sample
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;  // frame * 1024 + sample
     if (i >= (size_t)n_frames * 1024) return;
-    if (fkeep) i = ((size_t)fkeep[i >> 10] << 10) | (i & 1023);
     const size_t f = i >> 10, n = i & 1023;
+    if (n_skips && frame_skipped(skips, n_skips, (uint32_t)f)) return;
     const float* src = planar + f * (size_t)n_ch * 1024 + n;
     if (flags & JAAD_PCM_FLOAT32) {
         float* o = reinterpret_cast<float*>(pcm) + i * n_ch;
@@ -1640,18 +1654,19 @@ namespace {
 // one thread per (frame, sample instant): the output channels' words from the elements' PCM
 template <typename W>
 __global__ __launch_bounds__(256) void mc_interleave_kernel(McInterleave m, W* __restrict__ out, size_t n,
-                                                            uint32_t samples, const uint32_t* __restrict__ fkeep)
+                                                            uint32_t samples, const uint32_t* __restrict__ skips,
+                                                            uint32_t n_skips)
 {
-    size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;  // frame * samples + sample
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;  // frame * samples + sample
     if (i >= n) return;
-    if (fkeep) i = (size_t)fkeep[i / samples] * samples + i % samples;  // kept frames only
+    if (n_skips && frame_skipped(skips, n_skips, (uint32_t)(i / samples))) return;  // dropped frame
     W* o = out + i * m.n_out;
     for (int c = 0; c < m.n_out; c++) o[c] = static_cast<const W*>(m.src[c])[2 * i + m.chan[c]];
 }
 }  // namespace
 
 hipError_t launch_mc_interleave(const McInterleave& m, void* pcm, uint32_t n_frames, uint32_t samples, int bps,
-                                hipStream_t stream, const uint32_t* fkeep)
+                                hipStream_t stream, const uint32_t* skips, uint32_t n_skips)
 {
     const size_t n = (size_t)n_frames * samples;
     if (!n) return hipSuccess;
@@ -1659,20 +1674,20 @@ hipError_t launch_mc_interleave(const McInterleave& m, void* pcm, uint32_t n_fra
     const dim3 grid((unsigned)((n + 255) / 256));
     if (bps == 4)
         hipLaunchKernelGGL(mc_interleave_kernel<uint32_t>, grid, dim3(256), 0, stream, m, static_cast<uint32_t*>(pcm), n,
-                           samples, fkeep);
+                           samples, skips, n_skips);
     else
         hipLaunchKernelGGL(mc_interleave_kernel<uint16_t>, grid, dim3(256), 0, stream, m, static_cast<uint16_t*>(pcm), n,
-                           samples, fkeep);
+                           samples, skips, n_skips);
     return hipGetLastError();
 }
 
 hipError_t launch_pack(const float* planar, void* pcm, uint32_t n_frames, int n_ch, uint32_t flags, hipStream_t stream,
-                       const uint32_t* fkeep)
+                       const uint32_t* skips, uint32_t n_skips)
 {
     const size_t n = (size_t)n_frames * 1024;
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(pack_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, planar, pcm, n_frames, n_ch,
-                       flags, fkeep);
+                       flags, skips, n_skips);
     return hipGetLastError();
 }
 

@@ -159,7 +159,7 @@ def _random_ps(ps, rng, prev_modes):
     return iid_mode, icc_mode
 
 
-def _stream(cfgid, frames, seed, grids=False, ps_modes=False, header_gaps=True, header_change=False):
+def _stream(cfgid, frames, seed, grids=False, ps_modes=False, header_gaps=True, header_change=False, new_header=None):
     p = N.synth_params(cfgid, n_streams=1, frames_per_stream=frames)
     b = N.synth_batch(p)
     rng = np.random.default_rng(seed)
@@ -170,7 +170,8 @@ def _stream(cfgid, frames, seed, grids=False, ps_modes=False, header_gaps=True, 
             r["header_present"] = 0
         if header_change and f >= frames // 2:
             h = r["hdr"]
-            h["start_freq"], h["stop_freq"], h["alter_scale"] = 4, 6, 0
+            for key, v in (new_header or dict(start_freq=4, stop_freq=6, alter_scale=0)).items():
+                h[key] = v
             r["hdr"] = h
             if f == frames // 2:
                 r["header_present"] = 1

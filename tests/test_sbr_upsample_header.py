@@ -206,7 +206,8 @@ def _cut_after_payload():
     payload whole.  Returns (p, cfg, frames, k, cut, cut_batch, whole_batch)."""
     from tests.test_parse_sbr import _stream
     k = FPS // 2
-    p, b = _stream(4, FPS, 5, header_gaps=False, header_change=True)
+    # a header change the SBR state can take on a frame it does not process (ACCEPTED["kx_up"])
+    p, b = _stream(4, FPS, 5, header_gaps=False, header_change=True, new_header=dict(start_freq=8, stop_freq=15))
     cfg = N.cfg_for(p)
     frames = O.write_frames(b, p.sf_index, extras=1, sbr_writer=O.SbrWriter(cfg.ext_sf_index, 5))
     P = N.Parser(cfg)
