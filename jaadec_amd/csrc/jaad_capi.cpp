@@ -252,6 +252,7 @@ struct jaad_ctx {
     // ---- PS (cfg.ps) ----
     PsState* d_ps_state = nullptr;               // [slot]
     PsConst* d_ps_const = nullptr;
+    float* d_ps_zero = nullptr;  // SbrArgs::zero (behind d_ps_const, one allocation)
     DevBuf d_xps, d_xhl, d_xhr, d_pg, d_hb;
     std::vector<uint32_t> ps_runs;
     // ---- host-buffer entry (jaad_decode_batch), set up on its first call ----
@@ -757,6 +758,7 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
         uint32_t epos = 0;
         uint32_t last_ps = UINT32_MAX;
         bool sm = false, dp = false;
+        int kmin = 64, kmax = 0;  // records' band limits of the current run
         for (uint32_t r = rr[t]; r < rr[t + 1] && !rcs[t]; r++) {
             SbrHostSlot& hs = ctx->sbr_slots[b->stream_slot[r]];
             saved[r] = hs;
@@ -815,9 +817,23 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
                     }
                 }
                 sm |= (rec[0].flags & kSbrSmooth) != 0;
-                for (int c = 0; c < nch; c++) dp |= (rec[c].flags & kSbrDep) != 0;
+                for (int c = 0; c < nch; c++) {
+                    dp |= (rec[c].flags & kSbrDep) != 0;
+                    kmin = std::min<int>(kmin, rec[c].blim);
+                    kmax = std::max<int>(kmax, rec[c].blim);
+                }
                 i++;
             }
+            if (rcs[t]) break;
+            // one band limit for the whole run: the highest of its records' and of the stream's
+            // past (a band's PS all-pass state is zero only if no frame ever had input there);
+            // rewritten only where a record's own limit is lower
+            const int K = std::max(hs.blim_hw, kmax);
+            if (kmin < K)
+                for (size_t cf = (size_t)rbeg[r] * nch; cf < (size_t)i * nch; cf++) recs[cf].blim = (uint8_t)K;
+            hs.blim_hw = K;
+            kmin = 64;
+            kmax = 0;
         }
         used[t] = epos;
         smooth[t] = sm;
@@ -965,6 +981,7 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
         a.ps = 1;
         a.psf = reinterpret_cast<const jaad_ps_frame*>(d1 + o_psf);
         a.psc = ctx->d_ps_const;
+        a.zero = ctx->d_ps_zero;
         a.pss = ctx->d_ps_state;
         a.xps = static_cast<float*>(ctx->d_xps.p);
         a.xhl = static_cast<float*>(ctx->d_xhl.p);
@@ -1489,7 +1506,10 @@ int jaad_ctx_create(const jaad_stream_cfg* cfg, uint32_t n_slots, int device, ja
             return JAAD_ERR_NOMEM;
         }
         build_ps_const(k.get());
-        if ((e = hipMalloc(&ctx->d_ps_const, sizeof(PsConst))) != hipSuccess) return bail(e, "hipMalloc ps const");
+        const size_t kz = (sizeof(PsConst) + 255) & ~(size_t)255, zb = 32 * 64 * 2 * sizeof(float);
+        if ((e = hipMalloc(&ctx->d_ps_const, kz + zb)) != hipSuccess) return bail(e, "hipMalloc ps const");
+        ctx->d_ps_zero = reinterpret_cast<float*>(reinterpret_cast<char*>(ctx->d_ps_const) + kz);
+        if ((e = hipMemset(ctx->d_ps_zero, 0, zb)) != hipSuccess) return bail(e, "hipMemset ps zero");
         if ((e = hipMemcpy(ctx->d_ps_const, k.get(), sizeof(PsConst), hipMemcpyHostToDevice)) != hipSuccess)
             return bail(e, "hipMemcpy ps const");
     }

@@ -151,27 +151,29 @@ __global__ __launch_bounds__(256) void ps_analysis_kernel(SbrArgs A)
     const SbrRec& R = A.recs[f];
     const PsConst& K = *A.psc;
     {
-        const int t0 = R.t_E[0], kprev = R.kx_prev + R.M_prev;
+        const int t0 = R.t_E[0], kprev = R.kx_prev + R.M_prev, K = R.blim;
         const float2* xs = reinterpret_cast<const float2*>(A.xsyn + (size_t)f * 4096);
         const float2* xc = x_carry_prev(A, R, f);
         const float2* xn = reinterpret_cast<const float2*>(A.xcarry + (size_t)f * kSbrCarryFloats);
         float2* xo = reinterpret_cast<float2*>(A.xps + (size_t)f * 8192);
         // every row load is issued before the first store: xo might alias the sources as far as
-        // the compiler knows, so a load-store-load loop waits out one global round trip per row
+        // the compiler knows, so a load-store-load loop waits out one global round trip per row.
+        // Bands >= the run's limit K are zero (SbrRec::blim): their lanes read lane 0's word (no
+        // extra bytes) and store nothing.
         const bool ps_on = (R.flags & kSbrPsOn) != 0;
         float2 v[38];
 #pragma unroll
         for (int l = 0; l < 38; l++) {
             const float2* src = l >= 32 ? xn + (l - 30) * 64 : l < t0 ? xc + (l + 2) * 64 : xs + l * 64;
-            const bool ok = l >= 32 ? u < 5 && ps_on : l < t0 ? u < kprev : true;
+            const bool ok = l >= 32 ? u < 5 && ps_on : l < t0 ? u < kprev : u < K;
             const float2 t = src[ok ? u : 0];
             v[l] = ok ? t : make_float2(0.0f, 0.0f);
         }
 #pragma unroll
-        for (int l = 0; l < 32; l++) {
-            L.xl[l][u] = v[l];
-            xo[l * 64 + u] = v[l];
-        }
+        for (int l = 0; l < 32; l++) L.xl[l][u] = v[l];
+        if (u < K)
+#pragma unroll
+            for (int l = 0; l < 32; l++) xo[l * 64 + u] = v[l];
         // a frame without PS data only hands its X (qmfs0 input) to the synthesis
         if (!ps_on) return;
 #pragma unroll
@@ -632,6 +634,9 @@ __global__ __launch_bounds__(64 * kDecorWaves) __attribute__((amdgpu_waves_per_e
     PsState& S = A.pss[A.recs[fl[0]].slot];
     const PsConst& K = Ks;
     const bool fresh = S.init == 0;
+    // the run's band limit: X_left is zero from band kb up and so is every all-pass ring there
+    // (SbrRec::blim), so those lanes read a block of zeros and store nothing
+    const int kb = (int)__builtin_amdgcn_readfirstlane(A.recs[fl[0]].blim);
     const float2 zero = make_float2(0.0f, 0.0f);
     float2 xa[32], xb[32];
     uint64_t busy = 0;
@@ -693,7 +698,7 @@ __global__ __launch_bounds__(64 * kDecorWaves) __attribute__((amdgpu_waves_per_e
             }
             auto load = [&](float2 (&x)[32], uint32_t f) {
                 if (!hyb) {
-                    const float2* src = reinterpret_cast<const float2*>(A.xps + (size_t)f * 8192);
+                    const float2* src = reinterpret_cast<const float2*>(u < kb ? A.xps + (size_t)f * 8192 : A.zero);
 #pragma unroll
                     for (int n = 0; n < 32; n++) x[n] = src[n * 64 + u];
                 } else {
@@ -731,15 +736,17 @@ __global__ __launch_bounds__(64 * kDecorWaves) __attribute__((amdgpu_waves_per_e
             float2 r4[4], dl[14], d1 = zero;
             for (int k = 0; k < 4; k++) r4[k] = zero;
             for (int k = 0; k < 14; k++) dl[k] = zero;
-            const bool dlane = !hyb && u >= kApBands, is14 = u < 35;
+            const bool dlane = !hyb && u >= kApBands && u < kb, is14 = u < 35;
             if (!fresh) {
                 for (int k = 0; k < 4; k++) r4[k] = st_ap(5 + k);
                 if (!hyb)
                     for (int k = 0; k < 14; k++) dl[k] = S.dl[k][u];
             }
             d1 = dl[0];
+            // (only the plain delay lanes use the inputs: the others read the zero block, and their
+            // unused delay slots in the state stay zero)
             auto load = [&](float2 (&x)[32], uint32_t f) {
-                const float2* src = reinterpret_cast<const float2*>(A.xps + (size_t)f * 8192);
+                const float2* src = reinterpret_cast<const float2*>(dlane ? A.xps + (size_t)f * 8192 : A.zero);
 #pragma unroll
                 for (int n = 0; n < 32; n++) x[n] = src[n * 64 + u];
             };
@@ -939,8 +946,9 @@ __global__ __launch_bounds__(256) void ps_mix_kernel(SbrArgs A)
             mix(cur, kMixChunk * c);
         });
     };
-    // ---- QMF bands 3..63, lane = band ----
-    if (u >= 3) {
+    // ---- QMF bands 3..K-1, lane = band (from the run's band limit up X_left and the all-pass
+    // output are zero, and so are the mixed rows: nothing to load or store) ----
+    if (u >= 3 && u < (int)A.recs[f].blim) {
         const int gr = ps_qmf_group(u), bk = gr - 2;
         const bool rot = bk < nr;
         PsHWalk W;

@@ -62,7 +62,10 @@ struct SbrRec {
     uint8_t f[6];
     uint8_t tnb[5];             // current_t_noise_band of envelope l
     uint8_t gq0;                // GQ_ringbuf_index when the frame's first row is assembled
-    uint8_t sine0, pad0;
+    uint8_t sine0;
+    uint8_t blim;               // band limit of the record's run: QMF bands >= blim are zero in every
+                                // row the SBR/PS stages hand on (X, X_left, all-pass output, mixed
+                                // rows), so the kernels neither load nor store them (launch_sbr_stage)
     uint16_t ps_back;           // PS config: records back to the previous PS record of the run in this
                                 // call (0: none, the PS state of the slot holds it)
     float lim_gain;             // limGain[bs_limiter_gains]
@@ -165,6 +168,8 @@ struct SbrArgs {
     // parametric stereo (cfg.ps): the SBR stages run on the mono channel; the PS kernels turn
     // X_left into (X_left', X_right) in xps, the synthesis runs on xps with 2 output channels
     int ps;
+    const float* zero;          // 32 rows x 64 bands x float2 of zeros: the rows all-pass lanes
+                                // above their run's band limit read instead of X_left
     const jaad_ps_frame* psf;   // [frame]
     const PsConst* psc;
     PsState* pss;               // [slot]
@@ -211,6 +216,9 @@ struct SbrHostSlot {
     // patch_construction / limiter_frequency_table, SbrHost::take_header)
     int mixed;
     jaad_sbr_header phdr;
+    // highest band limit (SbrRec::blim) any frame of the stream has had since the last reset: PS
+    // all-pass / delay state above it is zero, so above it every stage may skip the bands
+    int blim_hw;
 };
 
 // Full derived tables of one header (host copy of the SBR object's table fields).

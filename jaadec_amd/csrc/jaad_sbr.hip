@@ -849,12 +849,15 @@ __global__ __launch_bounds__(256, 3) void sbr_hf_kernel(SbrArgs A)
     {
         // rows l < t_E[0] are Xsbr rows 2..7 as frame f-1 left them: its carry rows 2..7, which
         // the synthesis / PS analysis read (a later launch) with kx_prev + M_prev bands
+        // (from the run's band limit up nothing is stored: no stage reads those bands, SbrRec::blim)
         float2* xs = reinterpret_cast<float2*>(A.xsyn + (size_t)cf * 4096);
         const int kcur = kx + M;
+        if (u < (int)R.blim) {
 #pragma unroll
-        for (int l = 0; l < 32; l++) {
-            const bool keep = u < kcur;
-            xs[l * 64 + u] = make_float2(keep ? xr[l + 2] : 0.0f, keep ? xi[l + 2] : 0.0f);
+            for (int l = 0; l < 32; l++) {
+                const bool keep = u < kcur;
+                xs[l * 64 + u] = make_float2(keep ? xr[l + 2] : 0.0f, keep ? xi[l + 2] : 0.0f);
+            }
         }
         // Xsbr rows 32..39, every band (zero from kx + M up): the next frame's rows 0..7, the PS
         // look-ahead rows, the slot state
@@ -1031,9 +1034,12 @@ __global__ __launch_bounds__(256) void sbr_synthesis_kernel(SbrArgs A)
     //             half 1 (in_real2[e], in_imag2[e]) = (Im X[63-2e], Im X[2e])  (SynthesisFilterbank64.java:25-42)
     const int band_a = half ? 63 - 2 * e : 2 * e;
     const int band_b = half ? 2 * e : 63 - 2 * e;
-    const int ia = 2 * band_a + half, ib = 2 * band_b + half;
     // Rows hold 64 bands in memory; bands >= klim read as zero.  The mask is applied where the
-    // slot consumes the values (a select next to the load would wait for it).
+    // slot consumes the values (a select next to the load would wait for it).  From the run's band
+    // limit up (SbrRec::blim; the same for every record of a chunk) nothing is read: those lanes
+    // load the word of band 0 (fetched by other lanes anyway) and the mask zeroes it.
+    const int kb = (int)__builtin_amdgcn_readfirstlane(A.recs[(size_t)ck.frame0 * nch + rc].blim);
+    const int ia = band_a < kb ? 2 * band_a + half : half, ib = band_b < kb ? 2 * band_b + half : half;
     auto fetch = [&](const gfloat* r, float& a, float& b) {
         a = r[ia];
         b = r[ib];
@@ -1155,7 +1161,7 @@ __global__ __launch_bounds__(256) void sbr_synthesis_kernel(SbrArgs A)
         for (int i = 0; i < kG; i++) {
             const int l = min(l0 + i, S.rows - 1);  // (rows past the frame's last are not used)
             const bool carry = l < S.t0;
-            kl[i] = carry ? S.kprev : 64;
+            kl[i] = carry ? S.kprev : kb;
             fetch(carry ? S.xc + (l + 2) * 128 : S.xs + l * 128, ga[i], gb[i]);
         }
     };
@@ -1290,7 +1296,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     // the record's fields first (vmcnt counts in issue order: a wait for them must not wait for the
     // rows), then the parts whose source depends on cf alone, in flight while the record arrives
     const SbrRec& R = A.recs[cf];
-    const uint32_t slot = R.slot, flags = R.flags, ps_back = R.ps_back;
+    const uint32_t slot = R.slot, flags = R.flags, ps_back = R.ps_back, kb = R.blim;
     float4 vt[wave_copy_regs<288>()], vc[wave_copy_regs<kSbrCarryFloats>()], vg[wave_copy_regs<640>()];
     wave_load<288>(vt, A.time + batch_cf(A, cf) * 1024 + 736, u);
     wave_load<kSbrCarryFloats>(vc, A.xcarry + (size_t)cf * kSbrCarryFloats, u);
@@ -1303,6 +1309,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     const size_t fs1 = (flags & kSbrPsOn) ? cf : cf - ps_back;
     wave_load<9 * 128>(vs0, A.ps ? A.xps + (size_t)cf * 2 * 4096 + 23 * 128 : A.xsyn + (size_t)cf * 4096 + 23 * 128, u);
     if (A.ps) wave_load<9 * 128>(vs1, A.xps + ((ps_right ? fs1 : cf) * 2 + 1) * 4096 + 23 * 128, u);  // (xps is null without PS)
+    // bands from the run's limit up are not written by the stages (SbrRec::blim): the state keeps
+    // them zero, as a later call with a higher limit reads them
+    auto band_mask = [&](float4 (&v)[wave_copy_regs<9 * 128>()]) {
+#pragma unroll
+        for (int i = 0; i < wave_copy_regs<9 * 128>(); i++) {
+            const uint32_t b = 2 * ((uint32_t)(u + 64 * i) & 31);  // float4 = bands b, b + 1 of a row
+            if (b >= kb) v[i].x = v[i].y = 0.0f;
+            if (b + 1 >= kb) v[i].z = v[i].w = 0.0f;
+        }
+    };
+    band_mask(vs0);
+    if (A.ps) band_mask(vs1);
     SbrChState& S = A.state[(size_t)slot * 2 + c];
     wave_store<288>(vt, S.tail, u);
     wave_store<kSbrCarryFloats>(vc, &S.xcarry[0][0][0], u);

@@ -469,6 +469,8 @@ int SbrHost::frame(SbrHostSlot& st, const jaad_sbr_frame& fr, int nch, bool firs
             r.kx_prev = (uint8_t)st.kx_prev;
             r.M_prev = (uint8_t)st.M_prev;
             r.e_off = e_base + epos;
+            // X = the 32 analysis bands (Channel.java:604-613; rows l < t_E[0] none: t_E[0] = 0)
+            r.blim = 32;
         }
         return JAAD_OK;
     }
@@ -498,6 +500,8 @@ int SbrHost::frame(SbrHostSlot& st, const jaad_sbr_frame& fr, int nch, bool firs
         r.slot = slot;
         r.kx_prev = (uint8_t)st.kx_prev;
         r.M_prev = (uint8_t)st.M_prev;
+        // X is zero from kx + M up (rows l < t_E[0]: kx_prev + M_prev, Channel.java:618-645)
+        r.blim = (uint8_t)std::min(64, std::max(t.kx + t.M, st.kx_prev + st.M_prev));
         for (int l = 0; l <= L_E; l++) r.t_E[l] = in.t_E[l];
         for (int l = 0; l < L_E; l++) r.f[l] = in.f[l];
         r.lim_gain = JAAD_SBR_LIM_GAIN[h.limiter_gains & 3];
