@@ -89,6 +89,7 @@ def parse(argv=None):
     ap.add_argument("--config", type=int, default=2, choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-buffer (PCIe-inclusive) leg")
+    ap.add_argument("--no-host", action="store_true", help="skip the host front-end (bitstream parse) leg")
     ap.add_argument("--cpu-streams", type=int, default=256, help="streams in the CPU baseline sample")
     ap.add_argument("--settle", type=float, default=0.25,
                     help="seconds of untimed back-to-back steps before the warmup: the GPU's power management "
@@ -327,6 +328,12 @@ def run(args, engine_cls=HipEngine, backend: str = "nccl"):
                "multicore_value": round(sub.n_frames / dtn, 1), "multicore_threads": thr,
                "nproc": ncores, "affinity_cpus": len(os.sched_getaffinity(0)), "cpu_model": cpu_model()}
 
+    host = None
+    if rank == 0 and world == 1 and not args.no_host:
+        ncores = os.cpu_count() or 1
+        thr = max(1, min(ncores, len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "64") or 64)))
+        host = host_front_end(args.config, thr, frames_all * args.steps / elapsed)
+
     # HBM bytes per step measured by rocprofv3 PMC passes of this same command at the same config
     # (scripts/gpu_prof.sh [config] -> scripts/summarize_prof.py -> profiles/current_c<config>.json)
     traffic, traffic_src = None, None
@@ -362,9 +369,39 @@ def run(args, engine_cls=HipEngine, backend: str = "nccl"):
             "parity_sample": parity,
             "e2e_pcie_frames_per_s": round(e2e["registered"], 1) if e2e else None,
             "e2e_pcie_pageable_frames_per_s": round(e2e["pageable"], 1) if e2e else None,
+            "host_front_end": host,
         }
     eng.close()
     return line, pcm
+
+
+def host_front_end(config: int, threads: int, gpu_value: float) -> dict | None:
+    """The bitstream half of the drop-in (include/jaad_parse.h) on this host, with tools/bench_parse
+    over the config's corpus (tests/golden/parse_c<config>.bin: the same synthetic frames, written
+    as raw_data_blocks): parse frames/s on 1 and `threads` cores, the cores that would keep one GPU
+    fed at `value`, and a measured bitstream -> PCM pipeline (parse threads fill the next batch while
+    jaad_decode_batch decodes the current one through host buffers).  Reported beside, never as value."""
+    tool, corpus = ROOT / "tools" / "bench_parse", ROOT / "tests" / "golden" / f"parse_c{config}.bin"
+    if not tool.exists() or not corpus.exists():
+        return None
+
+    def run_tool(*a):
+        r = subprocess.run([str(tool), str(corpus), *map(str, a)], capture_output=True, text=True, timeout=120)
+        return json.loads(r.stdout) if r.returncode == 0 and r.stdout.strip() else None
+
+    one, many = run_tool(1, 1.0), run_tool(threads, 1.0)
+    pipe = run_tool(threads, 2.0, 128 if config == 4 else 256)
+    if not one:
+        return None
+    return {"parse_frames_per_s_1core": one["frames_per_s"], "parse_frames_per_s": many["frames_per_s"] if many else None,
+            "parse_threads": threads, "bitstream_bytes_per_frame": one["bytes_per_frame"],
+            "bitstream_MB_per_s_1core": one["bitstream_MB_per_s"],
+            "cores_to_feed_one_gpu": round(gpu_value / one["frames_per_s"], 1),
+            "bitstream_to_pcm_frames_per_s": pipe["bitstream_to_pcm_frames_per_s"] if pipe else None,
+            "pipeline": pipe,
+            "note": "tools/bench_parse: jaad_parse_frame over tests/golden/parse_c<config>.bin (synthetic frames "
+                    "at ~1.4 KB = 530 kb/s stereo: a dense, high-rate workload); pipeline = parse on the threads "
+                    "+ jaad_decode_batch (registered host buffers, PCIe both ways), measured"}
 
 
 def roofline(config: int, n_frames: int, kern_ms: float, gbs: float, traffic, traffic_src) -> dict:

@@ -162,12 +162,23 @@ def build_jni_mock(force: bool = False) -> Path:
     return out
 
 
+def build_tools(force: bool = False) -> Path:
+    """tools/bench_parse: the host front end's frames/s over a bitstream corpus (bench.py host_parse)."""
+    out = ROOT / "tools" / "bench_parse"
+    src = ROOT / "tools" / "bench_parse.cpp"
+    if force or _stale(out, [src, ROOT / "include" / "jaad_parse.h", LIB]):
+        _run(["g++", "-O2", "-std=c++17", "-pthread", "-Wall", "-I", str(ROOT / "include"), "-o", str(out), str(src),
+              "-L", str(PKG), "-ljaadgpu", f"-Wl,-rpath,{PKG}", "-Wl,-rpath,$ORIGIN/../jaadec_amd"])
+    return out
+
+
 def build_all(force: bool = False) -> None:
     build_oracle(force)
     build_synth(force)
     build_gpu(force)
     build_jni(force)
     build_jni_mock(force)
+    build_tools(force)
 
 
 if __name__ == "__main__":

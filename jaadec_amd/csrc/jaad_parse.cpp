@@ -58,6 +58,19 @@ struct Lut {
             }
         }
     }
+    // decode() on a register window (the caller keeps >= maxlen bits in it)
+    int decode(BitReader::Window& br) const
+    {
+        const uint32_t peek = br.peek(maxlen);
+        uint32_t ent = e[peek >> (maxlen - pbits)];
+        if (ent != 0xFFFFFFFFu && (ent & 0x80000000u))
+            ent = e[(ent & 0x7FFFFFFFu) + (peek & ((1u << (maxlen - pbits)) - 1u))];
+        if (ent == 0xFFFFFFFFu) return br.left() < maxlen ? -2 : -1;
+        const int len = (int)(ent >> 16);
+        if (br.left() < len) return -2;
+        br.skip(len);
+        return (int)(ent & 0xFFFFu);
+    }
     // row index, or -1 (no codeword) / -2 (bitstream ended)
     int decode(BitReader& br) const
     {
@@ -310,6 +323,7 @@ int read_ics(BitReader& br, const Cfg& C, bool common_window, IcsInfo& I, int pr
         lcg();
         return JAAD_ERR_EOS;
     };
+    BitReader::Window bw = br.window();  // (br's position is handed back after the loop)
     for (int g = 0, idx = 0, group_off = 0; g < I.ngroups; g++) {
         const int gl = I.glen[g];
         for (int s = 0; s < max_sfb; s++, idx++) {
@@ -329,39 +343,50 @@ int read_ics(BitReader& br, const Cfg& C, bool common_window, IcsInfo& I, int pr
             for (int w = 0; w < gl; w++) {
                 const int off = group_off + w * 128 + swb[s];
                 for (int k = 0; k < width; k += num) {
-                    const int r = L.decode(br);
+                    bw.need(L.maxlen + 4);  // the codeword and its sign bits
+                    const int r = L.decode(bw);
                     if (r < 0) return r == -2 ? eos() : JAAD_ERR_BITSTREAM;
                     int v[4];
                     for (int j = 0; j < num; j++) v[j] = rows[r * stride + 2 + j];
-                    if (unsigned_cb)  // Huffman.signValues (:30-37)
-                        for (int j = 0; j < num; j++)
-                            if (v[j] != 0) {
-                                if (br.left() < 1) return eos();
-                                if (br.read(1)) v[j] = -v[j];
-                            }
+                    if (unsigned_cb) {  // Huffman.signValues (:30-37): one sign bit per nonzero value
+                        int nz = 0;
+                        for (int j = 0; j < num; j++) nz += v[j] != 0;
+                        if (bw.left() < nz) return eos();
+                        uint32_t bits = nz ? bw.read(nz) << (32 - nz) : 0u;  // next sign bit on top
+                        for (int j = 0; j < num; j++) {  // (branch-free: the bits are data)
+                            const uint32_t has = v[j] != 0;
+                            const bool neg = (bits >> 31) & has;
+                            bits <<= has;
+                            v[j] = neg ? -v[j] : v[j];
+                        }
+                    }
                     if (c == JAAD_ESCAPE_HCB)  // Huffman.getEscape (:39-50)
                         for (int j = 0; j < 2; j++) {
                             if (v[j] != 16 && v[j] != -16) continue;
-                            int n = 4;
-                            for (;;) {
-                                if (br.left() < 1) return eos();
-                                if (!br.read(1)) break;
-                                if (++n > 12) return JAAD_ERR_BITSTREAM;  // |q| > 8191: beyond IQ_TABLE
-                            }
-                            if (br.left() < n) return eos();
-                            const int m = (int)br.read(n) | (1 << n);
+                            // escape_sequence prefix: n = 4 + the 1-bits before the first 0-bit, read
+                            // bit by bit in the reference -- counted at once here with the same
+                            // outcomes (EOS when the bits end first, an error at the 9th 1-bit)
+                            bw.need(9 + 13);  // the escape prefix and its value bits
+                            const int avail = bw.left() < 9 ? (int)bw.left() : 9;
+                            const int ones = avail > 0 ? __builtin_clz(~(bw.peek(avail) << (32 - avail))) : 0;
+                            if (ones >= 9) return JAAD_ERR_BITSTREAM;  // |q| > 8191: beyond IQ_TABLE
+                            if (ones == avail) return eos();            // no 0-bit before the end
+                            bw.skip(ones + 1);
+                            const int n = 4 + ones;
+                            if (bw.left() < n) return eos();
+                            const int m = (int)bw.read(n) | (1 << n);
+                            // IQ_TABLE has 8191 entries (A/syntax/IQTable.java): |q| <= 8190
+                            if (m > 8190) return JAAD_ERR_BITSTREAM;
                             v[j] = v[j] < 0 ? -m : m;
                         }
-                    for (int j = 0; j < num; j++) {
-                        // IQ_TABLE has 8191 entries (A/syntax/IQTable.java): |q| <= 8190
-                        if (v[j] > 8190 || v[j] < -8190) return JAAD_ERR_BITSTREAM;
+                    for (int j = 0; j < num; j++)
                         if (k + j < width) q[off + k + j] = (int16_t)v[j];
-                    }
                 }
             }
         }
         group_off += gl << 7;
     }
+    br.commit(bw);
     if (br.overrun()) return JAAD_ERR_EOS;
     if (C.cfg.tns_mode == JAAD_TNS_SPEC)  // spec-mode pulse tool (4.6.3.3, long windows only)
         for (int i = 0; i < pulse_n; i++) {

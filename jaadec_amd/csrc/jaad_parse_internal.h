@@ -3,6 +3,7 @@
 #include <stdint.h>
 
 #include <cstddef>
+#include <cstring>
 
 #include "../../include/jaad_gpu.h"
 
@@ -15,12 +16,26 @@ namespace parse {
 // sharing the parent's absolute position (byte alignment stays absolute, as in the reference).
 class BitReader {
 public:
-    BitReader(const uint8_t* d, size_t bytes) : d_(d), end_(bytes * 8), pos_(0) {}
+    BitReader(const uint8_t* d, size_t bytes) : d_(d), phys_(bytes), end_(bytes * 8), pos_(0) {}
     int64_t left() const { return (int64_t)end_ - (int64_t)pos_; }
     bool overrun() const { return pos_ > end_; }
     size_t pos() const { return pos_; }
+    // the next n <= 32 bits, MSB first (zero past the end).  Fast path: one big-endian 64-bit
+    // window at the current byte (the reads stay inside the caller's buffer), bits at or past the
+    // window's end masked off; the tail of the buffer goes bit by bit.
     uint32_t peek(int n) const
     {
+        if (n <= 0) return 0;
+        const size_t byte = pos_ >> 3;
+        if (byte + 8 <= phys_) {
+            uint64_t w;
+            std::memcpy(&w, d_ + byte, 8);
+            w = __builtin_bswap64(w) << (pos_ & 7);
+            uint32_t v = (uint32_t)(w >> (64 - n));
+            if (pos_ + (size_t)n > end_)  // sub-stream window: bits from end_ on read as zero
+                v = pos_ >= end_ ? 0u : v & ~((1u << (pos_ + (size_t)n - end_)) - 1u) ;
+            return v;
+        }
         uint64_t v = 0;
         size_t p = pos_;
         for (int i = 0; i < n; i++, p++) v = (v << 1) | (p < end_ ? ((d_[p >> 3] >> (7 - (p & 7))) & 1u) : 0u);
@@ -28,19 +43,8 @@ public:
     }
     uint32_t read(int n)
     {
-        if (n <= 0) return 0;
-        uint32_t v;
-        if (pos_ + (size_t)n <= end_ && n <= 25) {  // fast path: one unaligned 32-bit window
-            const size_t byte = pos_ >> 3;
-            const int sh = (int)(pos_ & 7);
-            uint32_t w = 0;
-            const size_t avail = (end_ + 7) / 8 - byte;
-            for (size_t i = 0; i < 4; i++) w = (w << 8) | (i < avail ? d_[byte + i] : 0u);
-            v = (w << sh) >> (32 - n);
-        } else {
-            v = peek(n);
-        }
-        pos_ += (size_t)n;
+        const uint32_t v = peek(n);
+        pos_ += (size_t)(n > 0 ? n : 0);
         return v;
     }
     void skip(int64_t n) { pos_ += (size_t)(n > 0 ? n : 0); }
@@ -52,8 +56,63 @@ public:
         return r;
     }
 
+    // The same stream with its next bits held in a 64-bit register (the spectral data's inner
+    // loop: a codeword's peek is then one shift, not a load).  Valid peeks need n <= cnt; refill()
+    // reloads the window at pos (>= 57 bits, zero from the end on).  commit() hands the position back.
+    struct Window {
+        const uint8_t* d;
+        size_t phys, end, pos;
+        uint64_t buf = 0;
+        int cnt = 0;
+        void refill()
+        {
+            const size_t byte = pos >> 3;
+            const int sh = (int)(pos & 7);
+            uint64_t w = 0;
+            if (byte + 8 <= phys) {
+                std::memcpy(&w, d + byte, 8);
+                w = __builtin_bswap64(w);
+            } else {
+                for (size_t i = 0; i < 8; i++) w = (w << 8) | (byte + i < phys ? d[byte + i] : 0u);
+            }
+            w <<= sh;
+            cnt = 64 - sh;
+            if (pos + (size_t)cnt > end) {  // bits from end on read as zero
+                const size_t keep = end > pos ? end - pos : 0;
+                w = keep ? w & ~(~0ull >> keep) : 0;
+            }
+            buf = w;
+        }
+        void need(int n)
+        {
+            if (cnt < n) refill();
+        }
+        int64_t left() const { return (int64_t)end - (int64_t)pos; }
+        uint32_t peek(int n) const { return n ? (uint32_t)(buf >> (64 - n)) : 0u; }  // n <= cnt, <= 32
+        void skip(int n)
+        {
+            buf <<= n;
+            cnt -= n;
+            pos += (size_t)n;
+        }
+        uint32_t read(int n)
+        {
+            const uint32_t v = peek(n);
+            skip(n);
+            return v;
+        }
+    };
+    Window window() const
+    {
+        Window w{d_, phys_, end_, pos_};
+        w.refill();
+        return w;
+    }
+    void commit(const Window& w) { pos_ = w.pos; }
+
 private:
     const uint8_t* d_;
+    size_t phys_;  // bytes of the caller's buffer (a sub-stream keeps its parent's)
     size_t end_, pos_;
 };
 

@@ -12,7 +12,7 @@ import torch.multiprocessing as mp
 import bench
 from jaadec_amd import native as N
 
-SMALL = ["--config", "2", "--steps", "2", "--warmup", "2", "--settle", "0.02", "--no-cpu", "--no-e2e", "--streams-per-gpu", "3",
+SMALL = ["--config", "2", "--steps", "2", "--warmup", "2", "--settle", "0.02", "--no-cpu", "--no-e2e", "--no-host", "--streams-per-gpu", "3",
          "--frames-per-stream", "6"]
 
 
@@ -136,7 +136,7 @@ def test_gloo_world2_bench_line_and_pcm_match_world1(monkeypatch):
     # world 1 over the same global job (6 streams) decodes byte-identically to the two shards
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
         monkeypatch.delenv(k, raising=False)
-    args = bench.parse(["--config", "2", "--steps", "2", "--warmup", "2", "--settle", "0.02", "--no-cpu", "--no-e2e",
+    args = bench.parse(["--config", "2", "--steps", "2", "--warmup", "2", "--settle", "0.02", "--no-cpu", "--no-e2e", "--no-host",
                         "--streams-per-gpu", "6", "--frames-per-stream", "6"])
     line1, pcm1 = bench.run(args, engine_cls=OracleEngine, backend="gloo")
     assert line1["n_gpus"] == 1
@@ -177,7 +177,7 @@ def test_gpu_world2_bench_path_on_the_hip_engine(monkeypatch):
     assert line["n_gpus"] == 2 and line["parity_sample"]["max_abs_lsb"] == 0
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
         monkeypatch.delenv(k, raising=False)
-    args = bench.parse(["--config", "2", "--steps", "2", "--warmup", "2", "--settle", "0.02", "--no-cpu", "--no-e2e",
+    args = bench.parse(["--config", "2", "--steps", "2", "--warmup", "2", "--settle", "0.02", "--no-cpu", "--no-e2e", "--no-host",
                         "--streams-per-gpu", "6", "--frames-per-stream", "6"])
     _, pcm1 = bench.run(args)
     assert b"".join(got) == pcm1.tobytes()

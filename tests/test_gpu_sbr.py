@@ -153,6 +153,34 @@ def test_header_change_moves_kx_across_calls(cfgid):
         _assert_same(g2[13 * r:13 * (r + 1)], want[fb[r] + 23:fb[r + 1]], N.PCM_FLOAT32)
 
 
+@pytest.mark.parametrize("cfgid", [4, 5])
+@pytest.mark.parametrize("direction", ["fall", "rise"])
+def test_band_limit_moves_across_calls(cfgid, direction):
+    """The stages skip the QMF bands from the run's band limit up (SbrRec::blim: the stream's
+    highest kx + M so far).  stop_freq 9 -> 5 moves kx + M from 45 to 32: falling (frame 12 on), the
+    PS all-pass / delay state of bands 32..44 keeps ringing and must still run; rising (frame 23 =
+    the call boundary), the history rows the slot state carries must read as zero from 32 up.
+    Float32 output, bit-exact against the restatement (A/sbr/Channel.java:618-645)."""
+    fps = 36
+    p = N.synth_params(cfgid, n_streams=3, frames_per_stream=fps)
+
+    def edit(s):
+        f = np.arange(len(s)) % fps
+        s["hdr"]["stop_freq"][(f >= 12) if direction == "fall" else (f < 23)] = 5
+
+    b = _edit(N.synth_batch(p), edit)
+    cfg = N.cfg_for(p)
+    want = O.decode_batch(cfg, b, O.Streams(3), N.PCM_FLOAT32, threads=8)
+    first, second = b.split_frames(23)
+    with N.Context(cfg, 3) as ctx:
+        g1 = ctx.decode(first, N.PCM_FLOAT32)
+        g2 = ctx.decode(second, N.PCM_FLOAT32)
+    fb = b.frame_begin
+    for r in range(3):
+        _assert_same(g1[23 * r:23 * (r + 1)], want[fb[r]:fb[r] + 23], N.PCM_FLOAT32)
+        _assert_same(g2[13 * r:13 * (r + 1)], want[fb[r] + 23:fb[r + 1]], N.PCM_FLOAT32)
+
+
 @pytest.mark.parametrize("cfgid,smoothing", [(4, 1), (5, 1), (4, 0)])
 def test_dropped_patch_with_trailing_borders(cfgid, smoothing):
     """A header whose patch_construction drops bands (start_freq 0, stop_freq 7, freq_scale 0 at

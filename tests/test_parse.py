@@ -262,3 +262,45 @@ def test_parser_snapshot_and_restore():
     with pytest.raises(N.JaadError):
         other.restore(snap)  # a snapshot of another configuration
     snap.close()
+
+
+@pytest.mark.parametrize("cfgid", [2, 3, 4, 5])
+def test_parse_corpus_round_trips_and_times(cfgid):
+    """The host front-end corpus (tests/golden/parse_c*.bin, bench.py host_front_end) parses back to
+    the synthetic records it was written from, and tools/bench_parse times it without an error."""
+    import json
+    import struct
+    import subprocess
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parents[1]
+    data = (root / "tests" / "golden" / f"parse_c{cfgid}.bin").read_bytes()
+    n = struct.unpack_from("<I", data, 4)[0]
+    cfg = N.StreamCfg.from_buffer_copy(data[8:8 + n])
+    at = 8 + n
+    streams, fps = struct.unpack_from("<II", data, at)
+    at += 8
+    p = N.synth_params(cfgid, n_streams=streams, frames_per_stream=fps)
+    b = N.synth_batch(p)
+    for s in range(streams):
+        pns = struct.unpack_from("<I", data, at)[0]
+        at += 4
+        frames = []
+        for _ in range(fps):
+            ln = struct.unpack_from("<I", data, at)[0]
+            frames.append(data[at + 4:at + 4 + ln])
+            at += 4 + ln
+        P = N.Parser(cfg)
+        P.pns_state = pns
+        got = P.parse(frames)
+        P.close()
+        c0, c1 = int(b.frame_begin[s]) * b.nch, int(b.frame_begin[s + 1]) * b.nch
+        assert (got.q == b.q[c0:c1]).all() and (got.sf == b.sf[c0:c1]).all() and (got.cb == b.cb[c0:c1]).all()
+    tool = root / "tools" / "bench_parse"
+    if not tool.exists():
+        pytest.skip("tools/bench_parse not built")
+    r = subprocess.run([str(tool), str(root / "tests" / "golden" / f"parse_c{cfgid}.bin"), "2", "0.1"],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    line = json.loads(r.stdout)
+    assert line["frames"] > 0 and line["frames_per_s"] > 0
