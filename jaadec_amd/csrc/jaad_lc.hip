@@ -1132,16 +1132,13 @@ __global__ __launch_bounds__(64 * waves_per_wg<kMode == 1>()) void lc_decode_ker
         vmem_drain();  // (see vmem_drain) the loop head then finds no load pending on any path
 
         for (int it = 0; it < my_n; it++) {
-            // Issue arbitration between the waves of a SIMD favours the oldest wave, so the
-            // waves of a SIMD would finish one after another and the last ones run with their
-            // latency exposed.  A wave's priority drops as it advances through its chunk: the
-            // waves that are behind catch up (C2: wave lifetimes 83 -> 89 % of the kernel span,
-            // batch time -5 %, scripts/wavetime.py).
-#ifdef JAAD_PRIO_RANK
+            // Issue arbitration between the waves of a SIMD favours the oldest wave: left alone,
+            // the three waves of a SIMD end ~12 us apart and the last ones run with their latency
+            // exposed.  The waves sharing this wave's SIMD are w +- 4 (a workgroup's waves go to the
+            // SIMDs in a fixed cyclic order); the one with the most frames left gets the highest
+            // priority, so that they end together (C2 wave ends 132-171 -> 147-160 us, busy 88 ->
+            // 95 % of span x waves; batch -1 %, profiles/round5_balance/).
             {
-                // the waves sharing this wave's SIMD are w +- 4 (a workgroup's waves go to the SIMDs
-                // in a fixed cyclic order): the one with the most frames left gets the highest
-                // priority, so that the SIMD's waves end together (longest remaining first)
                 const uint32_t rem = (uint32_t)(my_n - it);
                 volatile uint32_t* R = S.rem;
                 R[wave] = rem;
@@ -1156,15 +1153,6 @@ __global__ __launch_bounds__(64 * waves_per_wg<kMode == 1>()) void lc_decode_ker
                 else if (p == 1) __builtin_amdgcn_s_setprio(2);
                 else __builtin_amdgcn_s_setprio(1);
             }
-#else
-            {
-                const int q4 = (4 * it) / my_n;
-                if (q4 == 0) __builtin_amdgcn_s_setprio(3);
-                else if (q4 == 1) __builtin_amdgcn_s_setprio(2);
-                else if (q4 == 2) __builtin_amdgcn_s_setprio(1);
-                else __builtin_amdgcn_s_setprio(0);
-            }
-#endif
 #ifdef JAAD_WAVETIME
             wt_frames++;
 #endif
@@ -1451,9 +1439,7 @@ __global__ __launch_bounds__(64 * waves_per_wg<kMode == 1>()) void lc_decode_ker
             STAMP(10);
         }
         STAMP(11);
-#ifdef JAAD_PRIO_RANK
-        reinterpret_cast<volatile uint32_t*>(S.rem)[wave] = 0u;
-#endif
+        reinterpret_cast<volatile uint32_t*>(S.rem)[wave] = 0u;  // (done: no longer ahead of its mates)
         if (cd.info & kChunkStoreState) {
             const int u = lane_id();
             float* st = A.state_out + (size_t)cd.slot * 2048;

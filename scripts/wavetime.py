@@ -46,6 +46,10 @@ xcc, nf = S[:, 2] & 15, S[:, 3]
 for x in range(8):
     m = xcc == x
     if m.any(): print(f"  xcc {x}: waves {m.sum()} end p50 {np.median(en[m]):.1f} max {en[m].max():.1f}  us/frame {np.median(life[m] / np.maximum(nf[m], 1)):.2f}")
+idx = np.flatnonzero(dbg.cpu().numpy().view(np.uint64).reshape(nw, 4)[:, 0] > 0)
+for sl in range(3):  # waves w, w+4, w+8 of a 12-wave workgroup share a SIMD
+    m = (idx % 12) // 4 == sl
+    if m.any(): print(f"  simd slot {sl}: waves {m.sum()} end p50 {np.median(en[m]):.1f} frames mean {nf[m].mean():.2f}")
 for k in sorted(set(nf.tolist())):
     m = nf == k
     print(f"  frames {k}: waves {m.sum()} end p50 {np.median(en[m]):.1f}")
