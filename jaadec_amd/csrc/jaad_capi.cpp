@@ -202,10 +202,14 @@ struct jaad_ctx {
     LdsTables* d_tables = nullptr;
     GlobalTables* d_gtab = nullptr;
     float* d_iq = nullptr;
-    DevBuf d_chunks, d_batch, d_pcm;
-    PinnedBuf h_chunks;                  // staging of the chunk table's upload
-    hipEvent_t chunks_copied = nullptr;  // h_chunks may be rewritten once this has completed
-    bool chunks_live = false;
+    DevBuf d_batch, d_pcm;
+    // the chunk table (+ skip list) of the current plan: two slots, so that a new plan (the launch
+    // pipeline re-plans every piece) does not wait for the kernels of the previous one
+    DevBuf d_chunks[2];
+    PinnedBuf h_chunks[2];                   // staging of each slot's upload
+    hipEvent_t chunks_copied[2] = {};        // h_chunks[i] may be rewritten once this has completed
+    bool chunks_live[2] = {false, false};
+    int chunk_slot = 0;                      // slot of the current plan
     // Every call's device work (whatever stream it is queued on) waits for the previous call's
     // `done`: the chunk table, the double-buffered state and the SBR/PS state are reused call
     // after call.  The state_* entry points and jaad_wait wait for it too.
@@ -242,6 +246,7 @@ struct jaad_ctx {
                                                  // qmf32_pre_twiddle[32][2]
     DevBuf d_time, d_xlow, d_xsyn, d_xcarry, d_gq;
     hipStream_t cstream = nullptr;               // record uploads
+    hipStream_t rec_stream = nullptr;            // (the launch pipeline: uploads on its H2D stream)
     RecSet rsets[2];
     int rset = 0;
     std::unique_ptr<WorkerPool> workers;
@@ -259,6 +264,9 @@ struct jaad_ctx {
     hipStream_t h2d = nullptr, d2h = nullptr;      // copy streams beside `stream` (one DMA engine each)
     hipEvent_t ev_in[kMaxPieces] = {}, ev_k[kMaxPieces] = {}, ev_out[kMaxPieces] = {};
     PinnedBuf stage_in[kStageSlots], stage_out[kStageSlots];
+    // the launch pipeline's roll-back copies (device: core overlap, SBR and PS state of every slot)
+    DevBuf d_backup;
+    uint32_t sbr_pieces = 0;  // JAAD_SBR_PIECES (tuning): pieces of a launch-pipeline call
     DevBuf d_flag;                                 // |q| check result of a host-buffer call (device)
     PinnedBuf h_flag;
     DevBuf d_cce;                                  // coupling: term offsets / meta / gains, then addends
@@ -392,6 +400,9 @@ int validate_cfg(const jaad_stream_cfg* cfg)
 // call's stream (ordered after the previous call by launch()) from page-locked staging.
 // `size_frames` (0: the batch's) is the frame count one launch covers: the host-buffer entry
 // launches the kernel once per piece of the batch, so its chunks are sized for a piece.
+// device chunk table of the current plan
+const ChunkDesc* chunks_dev(const jaad_ctx* ctx) { return static_cast<const ChunkDesc*>(ctx->d_chunks[ctx->chunk_slot].p); }
+
 // b: the planner's view of the call (with dropped frames: keep_map's virtual batch, the kept
 // frames numbered consecutively); the chunks it writes hold batch frames (ctx->keep translates
 // them when ctx->skips is not empty, the skip list then follows the chunk table on the device)
@@ -458,17 +469,19 @@ int plan(jaad_ctx* ctx, const jaad_batch* b, hipStream_t stream, uint32_t size_f
     ctx->plan_valid = false;  // from here on the cached layout no longer describes d_chunks
     const size_t cbytes = chunks.size() * sizeof(ChunkDesc);
     const size_t bytes = cbytes + ctx->skips.size() * sizeof(uint32_t);
-    if (ctx->chunks_live) HIPCHK(hipEventSynchronize(ctx->chunks_copied));  // staging in use?
-    HIPCHK(ctx->h_chunks.ensure(bytes + 16));
-    HIPCHK(ctx->d_chunks.ensure(bytes + 16));
+    const int slot = ctx->chunk_slot ^ 1;  // (the current plan's slot may still be read by queued kernels)
+    if (ctx->chunks_live[slot]) HIPCHK(hipEventSynchronize(ctx->chunks_copied[slot]));  // staging in use?
+    HIPCHK(ctx->h_chunks[slot].ensure(bytes + 16));
+    HIPCHK(ctx->d_chunks[slot].ensure(bytes + 16));
     if (bytes) {
-        std::memcpy(ctx->h_chunks.p, chunks.data(), cbytes);
+        std::memcpy(ctx->h_chunks[slot].p, chunks.data(), cbytes);
         if (!ctx->skips.empty())
-            std::memcpy(static_cast<char*>(ctx->h_chunks.p) + cbytes, ctx->skips.data(), bytes - cbytes);
-        HIPCHK(hipMemcpyAsync(ctx->d_chunks.p, ctx->h_chunks.p, bytes, hipMemcpyHostToDevice, stream));
-        HIPCHK(hipEventRecord(ctx->chunks_copied, stream));
-        ctx->chunks_live = true;
+            std::memcpy(static_cast<char*>(ctx->h_chunks[slot].p) + cbytes, ctx->skips.data(), bytes - cbytes);
+        HIPCHK(hipMemcpyAsync(ctx->d_chunks[slot].p, ctx->h_chunks[slot].p, bytes, hipMemcpyHostToDevice, stream));
+        HIPCHK(hipEventRecord(ctx->chunks_copied[slot], stream));
+        ctx->chunks_live[slot] = true;
     }
+    ctx->chunk_slot = slot;
     ctx->chunks.swap(chunks);
     ctx->slot_used.swap(used);
     ctx->plan_slots.assign(b->stream_slot, b->stream_slot + b->n_runs);
@@ -552,7 +565,7 @@ int upload_skips(jaad_ctx* ctx, hipStream_t stream, const uint32_t** d)
 const uint32_t* plan_skips_dev(const jaad_ctx* ctx)
 {
     if (ctx->plan_skips.empty()) return nullptr;
-    return reinterpret_cast<const uint32_t*>(static_cast<const ChunkDesc*>(ctx->d_chunks.p) + ctx->plan_n_chunks);
+    return reinterpret_cast<const uint32_t*>(chunks_dev(ctx) + ctx->plan_n_chunks);
 }
 
 uint32_t n_skip_runs(const jaad_ctx* ctx) { return ctx->skips.empty() ? 0u : (uint32_t)ctx->skips.size() / 2 - 1; }
@@ -935,16 +948,19 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
     }
     HIPCHK(S.d1.ensure(n1 + 256));
     HIPCHK(S.d2.ensure(n2 + 256));
-    if (S.live) HIPCHK(hipStreamWaitEvent(ctx->cstream, S.used, 0));  // kernels of two calls ago
-    HIPCHK(hipMemcpyAsync(S.d1.p, h1, n1, hipMemcpyHostToDevice, ctx->cstream));
+    // (the launch pipeline queues them on its H2D stream: a third copy stream shared an engine with
+    // its D2H copies, and the records of every piece waited for the previous piece's PCM)
+    hipStream_t up = ctx->rec_stream ? ctx->rec_stream : ctx->cstream;
+    if (S.live) HIPCHK(hipStreamWaitEvent(up, S.used, 0));  // kernels of two calls ago
+    HIPCHK(hipMemcpyAsync(S.d1.p, h1, n1, hipMemcpyHostToDevice, up));
     for (int t = 0; t < nt; t++)
         if (used[t])
             HIPCHK(hipMemcpyAsync(static_cast<char*>(S.d2.p) + rbase[t] * sizeof(float), h2 + rbase[t] * sizeof(float),
-                                  used[t] * sizeof(float), hipMemcpyHostToDevice, ctx->cstream));
+                                  used[t] * sizeof(float), hipMemcpyHostToDevice, up));
     if (!tabs.empty())
         HIPCHK(hipMemcpyAsync(static_cast<char*>(S.d2.p) + o_tabs, h2 + o_tabs, tabs.size() * sizeof(SbrTab),
-                              hipMemcpyHostToDevice, ctx->cstream));
-    HIPCHK(hipEventRecord(S.copied, ctx->cstream));
+                              hipMemcpyHostToDevice, up));
+    HIPCHK(hipEventRecord(S.copied, up));
     HIPCHK(hipStreamWaitEvent(stream, S.copied, 0));
     const char* d1 = static_cast<const char*>(S.d1.p);
     const char* d2 = static_cast<const char*>(S.d2.p);
@@ -1084,7 +1100,7 @@ int launch_work(jaad_ctx* ctx, const jaad_batch* db, void* pcm, uint32_t flags, 
     a.iq_table = ctx->d_iq;
     a.tables = ctx->d_tables;
     a.gtab = ctx->d_gtab;
-    a.chunks = static_cast<const ChunkDesc*>(ctx->d_chunks.p);
+    a.chunks = chunks_dev(ctx);
     a.state_in = ctx->d_state[ctx->parity];
     a.state_out = ctx->d_state[ctx->parity ^ 1];
     const bool sbr = ctx->cfg.sbr != 0;
@@ -1411,6 +1427,7 @@ int jaad_ctx_create(const jaad_stream_cfg* cfg, uint32_t n_slots, int device, ja
     ctx->n_cu = prop.multiProcessorCount;
     ctx->slot_used.assign(n_slots, 0);
     if (const char* ev = std::getenv("JAAD_CHUNK_FRAMES")) ctx->chunk_frames = (uint32_t)std::atoi(ev);
+    if (const char* ev = std::getenv("JAAD_SBR_PIECES")) ctx->sbr_pieces = (uint32_t)std::atoi(ev);
     if (const char* ev = std::getenv("JAAD_SYN_FRAMES")) ctx->syn_frames = (uint32_t)std::atoi(ev);
     auto bail = [&](hipError_t e, const char* what) {
         std::fprintf(stderr, "jaad_ctx_create: %s: %s\n", what, hipGetErrorString(e));
@@ -1421,7 +1438,8 @@ int jaad_ctx_create(const jaad_stream_cfg* cfg, uint32_t n_slots, int device, ja
     if ((e = hipSetDevice(device)) != hipSuccess) return bail(e, "hipSetDevice");
     if ((e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking)) != hipSuccess) return bail(e, "hipStreamCreate");
     if ((e = hipEventCreateWithFlags(&ctx->done, hipEventDisableTiming)) != hipSuccess) return bail(e, "hipEventCreate");
-    if ((e = hipEventCreateWithFlags(&ctx->chunks_copied, hipEventDisableTiming)) != hipSuccess)
+    if ((e = hipEventCreateWithFlags(&ctx->chunks_copied[0], hipEventDisableTiming)) != hipSuccess ||
+        (e = hipEventCreateWithFlags(&ctx->chunks_copied[1], hipEventDisableTiming)) != hipSuccess)
         return bail(e, "hipEventCreate");
     if ((e = hipEventCreateWithFlags(&ctx->skips_copied, hipEventDisableTiming)) != hipSuccess)
         return bail(e, "hipEventCreate");
@@ -1567,15 +1585,19 @@ void jaad_ctx_destroy(jaad_ctx* ctx)
         if (r.kind == kPinOwned) (void)hipHostFree(reinterpret_cast<void*>(r.p));
     }
     ctx->io.reset();
-    ctx->d_chunks.release();
-    ctx->h_chunks.release();
+    for (int i = 0; i < 2; i++) {
+        ctx->d_chunks[i].release();
+        ctx->h_chunks[i].release();
+    }
     if (ctx->done) (void)hipEventDestroy(ctx->done);
-    if (ctx->chunks_copied) (void)hipEventDestroy(ctx->chunks_copied);
+    for (hipEvent_t ev : ctx->chunks_copied)
+        if (ev) (void)hipEventDestroy(ev);
     if (ctx->skips_copied) (void)hipEventDestroy(ctx->skips_copied);
     ctx->d_skips.release();
     ctx->h_skips.release();
     ctx->d_batch.release();
     ctx->d_pcm.release();
+    ctx->d_backup.release();
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -1963,7 +1985,7 @@ static int decode_batch_pieces_impl(jaad_ctx* ctx, const jaad_batch* b, void* pc
         a.tns = b->tns ? reinterpret_cast<const jaad_tns*>(sd + L.tns) - c0 : nullptr;
         HIPCHK(hipStreamWaitEvent(s, ctx->ev_in[i], 0));
         HIPCHK(launch_check_q(dq + c0 * 1024, nci * 1024, dflag, s));
-        a.chunks = static_cast<const ChunkDesc*>(ctx->d_chunks.p) + C[i];
+        a.chunks = chunks_dev(ctx) + C[i];
         a.n_chunks = C[i + 1] - C[i];
         if (a.n_chunks) HIPCHK(launch_lc(a, s, tns_spec));
         HIPCHK(hipEventRecord(ctx->ev_k[i], s));
@@ -1988,6 +2010,291 @@ static int decode_batch_pieces_impl(jaad_ctx* ctx, const jaad_batch* b, void* pc
     if (bad || *hflag) return JAAD_ERR_BITSTREAM;  // state not flipped: every slot as before the call
     ctx->parity ^= 1;
     return JAAD_OK;
+}
+
+// HE-AAC (SBR / PS) and AAC-LC batches with dropped frames: the pieces pipeline through launch().
+// Each piece is gathered into a batch of its own and decoded exactly as a call of its own would be
+// (LC kernel, SBR records and kernels).  Two ways to cut the batch:
+//  * run0 given: run-aligned pieces (whole runs, as the AAC-LC pipeline): a piece is one contiguous
+//    range of the caller's arrays, so registered memory goes by plain DMA both ways, and the H2D and
+//    D2H copies run on their two engines at once;
+//  * run0 null (PS): piece i is the i-th time slice of every run (run r's frames
+//    [fb_r + len_r i / P, fb_r + len_r (i+1) / P)), i.e. the i-th of P consecutive calls: the PS
+//    decorrelator walks a run's frames in order, so a run-aligned piece would cost a whole run's walk
+//    (0.6 ms on C5) however few runs it holds; a slice costs 1/P of it.  The PCM of a slice is R rows
+//    of the caller's buffer (a strided D2H copy into registered memory; that copy measured as sharing
+//    one engine with the H2D copies, profiles/round5_pipeline/).
+// Piece i+1's gather
+// (with the host checks: side info, |q|) and H2D copy overlap piece i's kernels and piece i-1's D2H
+// copy and scatter.  The call stays all-or-nothing: the core overlap, SBR and PS state of every slot
+// are copied aside on the device when it starts (a few us), the host SBR slots on the host, and a
+// piece that fails a check or whose SBR records are refused puts them all back.  (The reference
+// decodes frame by frame, A/Decoder.java:103-121; multichannel and coupling batches keep the serial
+// path.)
+static int decode_batch_pieces_launch_impl(jaad_ctx* ctx, const jaad_batch* b, void* pcm_out, uint32_t flags, int P,
+                                           const std::vector<uint32_t>* run0, std::vector<SbrHostSlot>& host_saved,
+                                           int& parity0, bool& saved)
+{
+    const int nch = ctx->nch;
+    const uint32_t R = b->n_runs;
+    const size_t fbytes = pcm_bytes_per_frame(ctx, flags);
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    auto cut = [&](uint32_t r, int i) {  // first batch frame of run r in pieces >= i
+        if (run0) return r < (*run0)[i] ? b->frame_begin[r + 1] : b->frame_begin[r];
+        const uint64_t len = b->frame_begin[r + 1] - b->frame_begin[r];
+        return b->frame_begin[r] + (uint32_t)(len * (uint64_t)i / (uint64_t)P);
+    };
+    std::vector<size_t> NF(P + 1, 0);  // first frame of each piece in the pieces' concatenation
+    for (int i = 0; i < P; i++) {
+        size_t n = 0;
+        for (uint32_t r = 0; r < R; r++) n += cut(r, i + 1) - cut(r, i);
+        NF[i + 1] = NF[i] + n;
+    }
+    size_t maxf = 0;
+    for (int i = 0; i < P; i++) maxf = std::max(maxf, NF[i + 1] - NF[i]);
+    struct Layout {
+        size_t q, sf, cb, ics, ms, tns, bytes;
+    };
+    auto layout = [&](size_t nfi) {
+        const size_t nci = nfi * nch;
+        Layout L;
+        L.q = 0;
+        L.sf = al(nci * 2048);
+        L.cb = L.sf + al(nci * 128);
+        L.ics = L.cb + al(nci * 128);
+        L.ms = L.ics + al(nci * sizeof(jaad_ics_info));
+        L.tns = L.ms + (b->ms_used ? al(nfi * 16) : 0);
+        L.bytes = L.tns + (b->tns ? al(nci * sizeof(jaad_tns)) : 0);
+        return L;
+    };
+    std::vector<size_t> SB(P + 1, 0);  // device input block of each piece
+    for (int i = 0; i < P; i++) SB[i + 1] = SB[i] + layout(NF[i + 1] - NF[i]).bytes;
+    HIPCHK(ctx->d_batch.ensure(SB[P] + 256));
+    HIPCHK(ctx->d_pcm.ensure(fbytes * NF[P] + 256));
+    char* base = static_cast<char*>(ctx->d_batch.p);
+    char* dpcm = static_cast<char*>(ctx->d_pcm.p);
+    hipStream_t s = ctx->stream;
+    if (ctx->done_live && ctx->last_stream != s) HIPCHK(hipStreamWaitEvent(s, ctx->done, 0));
+
+    // roll-back copies, queued ahead of every kernel of the call
+    const size_t lc_b = (size_t)ctx->n_elem * ctx->n_slots * 2048 * sizeof(float);
+    const size_t sbr_b = ctx->cfg.sbr ? (size_t)ctx->n_slots * 2 * sizeof(SbrChState) : 0;
+    const size_t ps_b = ctx->cfg.ps ? (size_t)ctx->n_slots * sizeof(PsState) : 0;
+    HIPCHK(ctx->d_backup.ensure(al(lc_b) + al(sbr_b) + ps_b + 256));
+    char* bk = static_cast<char*>(ctx->d_backup.p);
+    parity0 = ctx->parity;
+    HIPCHK(hipMemcpyAsync(bk, ctx->d_state[parity0], lc_b, hipMemcpyDeviceToDevice, s));
+    if (sbr_b) HIPCHK(hipMemcpyAsync(bk + al(lc_b), ctx->d_sbr_state, sbr_b, hipMemcpyDeviceToDevice, s));
+    if (ps_b) HIPCHK(hipMemcpyAsync(bk + al(lc_b) + al(sbr_b), ctx->d_ps_state, ps_b, hipMemcpyDeviceToDevice, s));
+    host_saved = ctx->sbr_slots;
+    saved = true;
+
+    // Runs of one length L laid out back to back (the usual batch): a piece is then R rows of one
+    // slice length, so registered caller memory is copied by strided DMA straight from / to its
+    // place (hipMemcpy2DAsync), no host gather of q or scatter of PCM
+    const uint32_t L0 = R ? b->frame_begin[1] - b->frame_begin[0] : 0;
+    bool uniform = R > 0;
+    for (uint32_t r = 0; r <= R && uniform; r++) uniform = b->frame_begin[r] == r * L0;
+    const size_t ncf = (size_t)b->n_frames * nch;
+    // Run-aligned pieces: registered q and PCM by plain DMA.  Time slices: q gathered by the workers
+    // as they check it (a strided H2D copy measured as sharing one engine with the strided D2H
+    // copies: piece i+1's inputs waited for piece i's PCM), PCM by strided DMA when the runs are
+    // uniform.
+    const bool dma_q = run0 && is_pinned(ctx, b->q, ncf * 2048);
+    const bool dma_out = (run0 || uniform) && !b->frame_status && is_pinned(ctx, pcm_out, fbytes * b->n_frames);
+    for (auto& st : ctx->stage_in) HIPCHK(st.ensure(layout(maxf).bytes));
+    if (!dma_out)
+        for (auto& st : ctx->stage_out) HIPCHK(st.ensure(maxf * fbytes));
+    WorkerPool& io = *ctx->io;
+    const int W = io.size();
+    std::atomic<bool> bad{false};
+    auto kept = [&](size_t f) { return !b->frame_status || b->frame_status[f] == JAAD_FRAME_DECODE; };
+    // the piece's host-side arrays (read by launch() before it returns, so one set serves every piece)
+    std::vector<uint32_t> pslot, pbeg, prun;  // runs with frames in the piece: slot, first frame, batch run
+    std::vector<jaad_sbr_frame> psbr;
+    std::vector<uint8_t> pstat;
+    auto piece_runs = [&](int i, std::vector<uint32_t>& runs, std::vector<uint32_t>& beg) {
+        runs.clear();
+        beg.assign(1, 0);
+        for (uint32_t r = 0; r < R; r++) {
+            const uint32_t a = cut(r, i), e = cut(r, i + 1);
+            if (e == a) continue;  // no frame of run r in this piece: its slot keeps its state
+            runs.push_back(r);
+            beg.push_back(beg.back() + (e - a));
+        }
+    };
+    // piece i's PCM (stage_out slot) -> the caller's frames, dropped frames left as they are
+    std::vector<uint32_t> out_runs, out_beg;
+    auto copy_out = [&](int i) -> int {
+        HIPCHK(hipEventSynchronize(ctx->ev_out[i]));
+        piece_runs(i, out_runs, out_beg);
+        const char* src = static_cast<const char*>(ctx->stage_out[i % kStageSlots].p);
+        const size_t nr = out_runs.size();
+        io.run([&](int t) {
+            for (size_t k = nr * t / W; k < nr * (t + 1) / W; k++) {
+                const uint32_t a = cut(out_runs[k], i), n = out_beg[k + 1] - out_beg[k];
+                const char* sp = src + (size_t)out_beg[k] * fbytes;
+                char* dp = static_cast<char*>(pcm_out) + (size_t)a * fbytes;
+                if (!b->frame_status) {
+                    std::memcpy(dp, sp, (size_t)n * fbytes);
+                    continue;
+                }
+                for (uint32_t j = 0; j < n; j++)
+                    if (kept(a + j)) std::memcpy(dp + (size_t)j * fbytes, sp + (size_t)j * fbytes, fbytes);
+            }
+        });
+        return JAAD_OK;
+    };
+    // piece i: the runs' slices gathered into staging slot i % 2 by the workers, checked on the way
+    // (side info; |q| as q_ok_copy copies it), then one H2D copy (ev_in[i])
+    std::vector<uint32_t> st_runs, st_beg;
+    auto stage_piece = [&](int i) -> int {
+        const size_t nfi = NF[i + 1] - NF[i];
+        const Layout L = layout(nfi);
+        if (i >= kStageSlots) HIPCHK(hipEventSynchronize(ctx->ev_in[i - kStageSlots]));
+        char* st = static_cast<char*>(ctx->stage_in[i % kStageSlots].p);
+        piece_runs(i, st_runs, st_beg);
+        const size_t nr = st_runs.size();
+        if (!nfi) return hipEventRecord(ctx->ev_in[i], ctx->h2d) == hipSuccess ? JAAD_OK : JAAD_ERR_HIP;
+        io.run([&](int t) {
+            for (size_t k = nr * t / W; k < nr * (t + 1) / W; k++) {
+                const size_t a = cut(st_runs[k], i), n = st_beg[k + 1] - st_beg[k], o = st_beg[k];
+                const size_t c0 = a * nch, nc = n * nch, oc = o * nch;
+                if (!side_info_ok(ctx, b, c0, c0 + nc)) bad = true;
+                int16_t* qd = dma_q ? nullptr : reinterpret_cast<int16_t*>(st + L.q) + oc * 1024;
+                if (!q_ok_copy(b->q + c0 * 1024, qd, nc * 1024)) {  // (stopped at the bad block)
+                    if (!b->frame_status || !q_ok_kept(ctx, b, c0, c0 + nc)) bad = true;
+                    else if (qd) std::memcpy(qd, b->q + c0 * 1024, nc * 2048);  // the bad values are in dropped frames
+                }
+                std::memcpy(st + L.sf + oc * 128, b->sf + c0 * 128, nc * 128);
+                std::memcpy(st + L.cb + oc * 128, b->cb + c0 * 128, nc * 128);
+                std::memcpy(st + L.ics + oc * sizeof(jaad_ics_info), b->ics + c0, nc * sizeof(jaad_ics_info));
+                if (b->ms_used) std::memcpy(st + L.ms + o * 16, b->ms_used + a * 2, n * 16);
+                if (b->tns) std::memcpy(st + L.tns + oc * sizeof(jaad_tns), b->tns + c0, nc * sizeof(jaad_tns));
+            }
+        });
+        if (bad) return JAAD_ERR_BITSTREAM;
+        if (dma_q) {  // q straight from the caller's registered memory (one range), the side info from staging
+            const size_t f0 = b->frame_begin[(*run0)[i]];
+            HIPCHK(hipMemcpyAsync(base + SB[i] + L.q, b->q + f0 * nch * 1024, nfi * nch * 2048, hipMemcpyHostToDevice, ctx->h2d));
+            HIPCHK(hipMemcpyAsync(base + SB[i] + L.sf, st + L.sf, L.bytes - L.sf, hipMemcpyHostToDevice, ctx->h2d));
+        } else {
+            HIPCHK(hipMemcpyAsync(base + SB[i], st, L.bytes, hipMemcpyHostToDevice, ctx->h2d));
+        }
+        HIPCHK(hipEventRecord(ctx->ev_in[i], ctx->h2d));
+        return JAAD_OK;
+    };
+    static const bool trace = std::getenv("JAAD_TRACE_HOST") != nullptr;  // per-piece host timings (tuning aid)
+    using clk = std::chrono::steady_clock;
+    auto ms = [](clk::time_point a, clk::time_point e) { return std::chrono::duration<double, std::milli>(e - a).count(); };
+    const auto t_call = clk::now();
+    int rc = stage_piece(0);
+    if (rc) return rc;
+    int queued = 0;
+    for (int i = 0; i < P; i++) {
+        const auto t0 = clk::now();
+        const size_t nfi = NF[i + 1] - NF[i];
+        if (!nfi) {  // (runs shorter than P frames: no frame falls in this slice)
+            HIPCHK(hipEventRecord(ctx->ev_out[i], ctx->d2h));
+            if (i + 1 < P && (rc = stage_piece(i + 1))) return rc;
+            queued = i + 1;
+            continue;
+        }
+        const Layout L = layout(nfi);
+        const char* blk = base + SB[i];
+        piece_runs(i, prun, pbeg);
+        pslot.resize(prun.size());
+        for (size_t k = 0; k < prun.size(); k++) pslot[k] = b->stream_slot[prun[k]];
+        if (b->sbr || b->frame_status) {  // host-side per-frame arrays of the piece
+            if (b->sbr) psbr.resize(nfi);
+            if (b->frame_status) pstat.resize(nfi);
+            const size_t nr = prun.size();
+            io.run([&](int t) {
+                for (size_t k = nr * t / W; k < nr * (t + 1) / W; k++) {
+                    const size_t a = cut(prun[k], i), n = pbeg[k + 1] - pbeg[k];
+                    if (b->sbr) std::memcpy(&psbr[pbeg[k]], b->sbr + a, n * sizeof(jaad_sbr_frame));
+                    if (b->frame_status) std::memcpy(&pstat[pbeg[k]], b->frame_status + a, n);
+                }
+            });
+        }
+        jaad_batch pb = *b;  // the piece as a batch of its own
+        pb.n_frames = (uint32_t)nfi;
+        pb.n_runs = (uint32_t)prun.size();
+        pb.stream_slot = pslot.data();
+        pb.frame_begin = pbeg.data();
+        pb.q = reinterpret_cast<const int16_t*>(blk + L.q);
+        pb.sf = reinterpret_cast<const uint8_t*>(blk + L.sf);
+        pb.cb = reinterpret_cast<const uint8_t*>(blk + L.cb);
+        pb.ics = reinterpret_cast<const jaad_ics_info*>(blk + L.ics);
+        pb.ms_used = b->ms_used ? reinterpret_cast<const uint64_t*>(blk + L.ms) : nullptr;
+        pb.tns = b->tns ? reinterpret_cast<const jaad_tns*>(blk + L.tns) : nullptr;
+        pb.sbr = b->sbr ? psbr.data() : nullptr;
+        pb.frame_status = b->frame_status ? pstat.data() : nullptr;
+        // piece i's launch first (its SBR records go to the H2D stream now, ahead of piece i+1's
+        // inputs), then piece i+1's gather and copy while piece i's kernels run
+        HIPCHK(hipStreamWaitEvent(s, ctx->ev_in[i], 0));
+        char* dp = dpcm + NF[i] * fbytes;
+        if ((rc = launch(ctx, &pb, dp, flags, s))) return rc;
+        HIPCHK(hipEventRecord(ctx->ev_k[i], s));
+        const auto t1 = clk::now();
+        if (i + 1 < P && (rc = stage_piece(i + 1))) return rc;
+        const auto t2 = clk::now();
+        HIPCHK(hipStreamWaitEvent(ctx->d2h, ctx->ev_k[i], 0));
+        if (dma_out && run0) {  // the piece's frames straight into the caller's registered memory
+            HIPCHK(hipMemcpyAsync(static_cast<char*>(pcm_out) + (size_t)b->frame_begin[(*run0)[i]] * fbytes, dp, nfi * fbytes,
+                                  hipMemcpyDeviceToHost, ctx->d2h));
+        } else if (dma_out) {  // the piece's R rows straight into the caller's registered memory
+            const size_t w = (size_t)(cut(0, i + 1) - cut(0, i)) * fbytes;
+            HIPCHK(hipMemcpy2DAsync(static_cast<char*>(pcm_out) + (size_t)cut(0, i) * fbytes, (size_t)L0 * fbytes, dp, w, w,
+                                    prun.size(), hipMemcpyDeviceToHost, ctx->d2h));
+        } else {
+            if (i >= kStageSlots && (rc = copy_out(i - kStageSlots))) return rc;  // frees staging slot i % 2
+            HIPCHK(hipMemcpyAsync(ctx->stage_out[i % kStageSlots].p, dp, nfi * fbytes, hipMemcpyDeviceToHost, ctx->d2h));
+        }
+        HIPCHK(hipEventRecord(ctx->ev_out[i], ctx->d2h));
+        queued = i + 1;
+        if (trace)
+            std::fprintf(stderr, "jaad pieces: piece %d/%d (%zu frames) at %.3f ms: launch %.3f, stage next %.3f, out %.3f ms\n", i,
+                         P, nfi, ms(t_call, t0), ms(t0, t1), ms(t1, t2), ms(t2, clk::now()));
+    }
+    if (!dma_out)
+        for (int i = std::max(0, queued - kStageSlots); i < queued; i++)
+            if ((rc = copy_out(i))) return rc;
+    HIPCHK(hipStreamSynchronize(ctx->d2h));
+    HIPCHK(hipStreamSynchronize(s));
+    if (trace) std::fprintf(stderr, "jaad pieces: call %.3f ms (q %s, PCM %s)\n", ms(t_call, clk::now()), dma_q ? "dma" : "staged",
+                            dma_out ? "dma" : "staged");
+    return JAAD_OK;
+}
+
+static int decode_batch_pieces_launch(jaad_ctx* ctx, const jaad_batch* b, void* pcm_out, uint32_t flags, int P,
+                                      const std::vector<uint32_t>* run0)
+{
+    std::vector<SbrHostSlot> host_saved;
+    int parity0 = ctx->parity;
+    bool saved = false;
+    ctx->rec_stream = ctx->h2d;
+    const int rc = decode_batch_pieces_launch_impl(ctx, b, pcm_out, flags, P, run0, host_saved, parity0, saved);
+    ctx->rec_stream = nullptr;
+    if (rc) {
+        for (hipStream_t st : {ctx->h2d, ctx->d2h, ctx->stream})
+            if (st) (void)hipStreamSynchronize(st);
+        (void)hipGetLastError();
+        if (saved) {  // every slot back to the state it had when the call started
+            auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+            const size_t lc_b = (size_t)ctx->n_elem * ctx->n_slots * 2048 * sizeof(float);
+            const size_t sbr_b = ctx->cfg.sbr ? (size_t)ctx->n_slots * 2 * sizeof(SbrChState) : 0;
+            const size_t ps_b = ctx->cfg.ps ? (size_t)ctx->n_slots * sizeof(PsState) : 0;
+            const char* bk = static_cast<const char*>(ctx->d_backup.p);
+            ctx->parity = parity0;
+            (void)hipMemcpy(ctx->d_state[parity0], bk, lc_b, hipMemcpyDeviceToDevice);
+            if (sbr_b) (void)hipMemcpy(ctx->d_sbr_state, bk + al(lc_b), sbr_b, hipMemcpyDeviceToDevice);
+            if (ps_b) (void)hipMemcpy(ctx->d_ps_state, bk + al(lc_b) + al(sbr_b), ps_b, hipMemcpyDeviceToDevice);
+            ctx->sbr_slots.swap(host_saved);
+            (void)hipDeviceSynchronize();
+        }
+    }
+    return rc;
 }
 
 // ---- dropped frames (jaad_batch.frame_status) ----
@@ -2028,13 +2335,23 @@ static int decode_batch_whole(jaad_ctx* ctx, const jaad_batch* b, void* pcm_out,
     int rc;
     HIPCHK(hipSetDevice(ctx->device));
     if ((rc = io_setup(ctx))) return rc;
-    if (ctx->cfg.sbr || ctx->n_elem > 1 || b->n_cce_terms || b->frame_status || b->n_frames < 2 * kMinPieceFrames ||
-        !b->stream_slot || !b->frame_begin)
+    if (ctx->n_elem > 1 || b->n_cce_terms || b->n_frames < 2 * kMinPieceFrames || !b->stream_slot || !b->frame_begin)
         return decode_batch_serial(ctx, b, pcm_out, flags);
     // the run layout is checked by plan(); pieces need it sane before cutting
     if (b->frame_begin[0] != 0 || b->frame_begin[b->n_runs] != b->n_frames) return JAAD_ERR_INVALID_ARG;
     for (uint32_t r = 0; r < b->n_runs; r++)
         if (b->frame_begin[r + 1] < b->frame_begin[r]) return JAAD_ERR_INVALID_ARG;
+    if (ctx->cfg.ps) {  // time-sliced pieces through launch()
+        const uint32_t P = std::min<uint32_t>(ctx->sbr_pieces ? std::min<uint32_t>(ctx->sbr_pieces, kMaxPieces) : 8u,
+                                              b->n_frames / kMinPieceFrames);
+        if (P < 2) return decode_batch_serial(ctx, b, pcm_out, flags);
+        return decode_batch_pieces_launch(ctx, b, pcm_out, flags, (int)P, nullptr);
+    }
+    if (ctx->cfg.sbr || b->frame_status) {  // run-aligned pieces through launch()
+        const std::vector<uint32_t> run0 = cut_pieces(b);
+        if (run0.size() <= 2) return decode_batch_serial(ctx, b, pcm_out, flags);
+        return decode_batch_pieces_launch(ctx, b, pcm_out, flags, (int)run0.size() - 1, &run0);
+    }
     const std::vector<uint32_t> run0 = cut_pieces(b);
     if (run0.size() <= 2) return decode_batch_serial(ctx, b, pcm_out, flags);
     return decode_batch_pieces(ctx, b, pcm_out, flags, run0);

@@ -1,4 +1,5 @@
-"""The host-buffer entry (jaad_decode_batch): the pieces pipeline for large AAC-LC batches, with
+"""The host-buffer entry (jaad_decode_batch): the pieces pipelines for large batches (AAC-LC: the
+LC kernel per piece; HE-AAC v1/v2 and batches with dropped frames: whole launches per piece), with
 pageable and registered (jaad_host_register) caller buffers, against the device-resident entry
 and the C restatement; validation failures leave every slot's state untouched."""
 import numpy as np
@@ -16,7 +17,7 @@ def _device_decode(cfg, b, n_slots, flags):
     t = lambda a: None if a is None else torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1)).to(dev)
     d = {k: t(getattr(b, k)) for k in ("q", "sf", "cb", "ics", "ms_used", "tns")}
     ptr = {k: (v.data_ptr() if v is not None else None) for k, v in d.items()}
-    nb = N.pcm_frame_bytes(flags)
+    nb = N.pcm_frame_bytes(flags, bool(cfg.sbr), N.sbr_downsampled(cfg))
     pcm = torch.empty(b.n_frames * nb, dtype=torch.uint8, device=dev)
     with N.Context(cfg, n_slots) as ctx:
         ctx.decode_device(ptr, b, pcm.data_ptr(), pcm.numel(), flags)
@@ -160,3 +161,90 @@ def test_registering_a_range_twice_is_idempotent():
         with pytest.raises(N.JaadError) as e:
             ctx.unregister(b.q)
         assert e.value.status == N.ERR_INVALID_ARG
+
+
+def _runs_of(pcm_a, pcm_b, fb_a, fb_b, runs):
+    return all((pcm_a[fb_a[r]:fb_a[r + 1]] == pcm_b[fb_b[r]:fb_b[r + 1]]).all() for r in runs)
+
+
+@pytest.mark.parametrize("cfgid,flags", [(4, N.PCM_BIG_ENDIAN), (5, N.PCM_LITTLE_ENDIAN), (5, N.PCM_FLOAT32)])
+def test_sbr_ps_pieces_pipeline_matches_device_entry(cfgid, flags):
+    """HE-AAC v1 / v2 batches through the host-buffer entry run as pieces of whole
+    launches whose copies overlap; two calls (the second continuing every stream) == the device
+    entry over the whole streams, and == the restatement on a sample of streams."""
+    p = N.synth_params(cfgid, n_streams=64, frames_per_stream=160)  # 10 240 frames: 5 pieces
+    b = N.synth_batch(p)
+    cfg = N.cfg_for(p)
+    first, second = b.split_frames(100)
+    with N.Context(cfg, 64) as ctx:
+        g1 = ctx.decode(first, flags)
+        g2 = ctx.decode(second, flags)
+    want = _device_decode(cfg, b, 64, flags)
+    fb = b.frame_begin
+    for r in range(64):
+        assert (g1[100 * r:100 * (r + 1)] == want[fb[r]:fb[r] + 100]).all(), r
+        assert (g2[60 * r:60 * (r + 1)] == want[fb[r] + 100:fb[r + 1]]).all(), r
+    sub = b.select_runs([0, 63])
+    o = O.decode_batch(cfg, sub, O.Streams(64), flags, threads=8)
+    assert (np.concatenate([want[fb[r]:fb[r + 1]] for r in (0, 63)]) == o).all()
+
+
+def test_sbr_pieces_registered_buffers_and_dropped_frames():
+    """The same pipeline with registered caller buffers, and with a dropped frame in every stream
+    (their PCM rows keep the caller's bytes)."""
+    p = N.synth_params(4, n_streams=48, frames_per_stream=128)
+    b = N.synth_batch(p)
+    cfg = N.cfg_for(p)
+    rng = np.random.default_rng(3)
+    st = np.zeros(b.n_frames, np.uint8)
+    for r in range(48):
+        st[int(b.frame_begin[r]) + int(rng.integers(1, 128))] = N.FRAME_EOS
+    b.frame_status = st
+    want = O.decode_batch(cfg, b.select_runs([5, 40]), O.Streams(48), N.PCM_BIG_ENDIAN, threads=8)
+    want_dev = _device_decode(cfg, b, 48, N.PCM_BIG_ENDIAN)
+    for registered in (False, True):
+        out = np.full((b.n_frames, 8192), 0x5A, np.uint8)
+        with N.Context(cfg, 48) as ctx:
+            arrays = [b.q, b.sf, b.cb, b.ics, b.ms_used, out]
+            if registered:
+                ctx.register(*arrays)
+            ctx.decode(b, N.PCM_BIG_ENDIAN, out=out)
+            if registered:
+                ctx.unregister(*arrays)
+        assert (out[st == 1] == 0x5A).all(), registered
+        assert (out[st == 0] == want_dev[st == 0]).all(), registered
+        fb = b.frame_begin
+        got = np.concatenate([out[fb[r]:fb[r + 1]] for r in (5, 40)])
+        keep = np.concatenate([st[fb[r]:fb[r + 1]] for r in (5, 40)]) == 0
+        assert (got[keep] == want[keep]).all()
+
+
+@pytest.mark.parametrize("what", ["q", "sbr"])
+def test_sbr_bad_piece_rolls_the_call_back(what):
+    """A bad record in the last piece (|q| > 8190, or an SBR envelope count the reference cannot
+    have parsed) fails the call after earlier pieces' kernels ran: every slot's core, SBR and PS
+    state is put back, and the good batch then continues every stream exactly."""
+    p = N.synth_params(5, n_streams=64, frames_per_stream=160)
+    b = N.synth_batch(p)
+    cfg = N.cfg_for(p)
+    want = _device_decode(cfg, b, 64, N.PCM_BIG_ENDIAN)
+    half, rest = b.split_frames(80)
+    with N.Context(cfg, 64) as ctx:
+        ctx.decode(half)
+        before = [ctx.state_export(s) for s in range(64)]
+        bad = rest.select_runs(range(64))
+        if what == "q":
+            bad.q[-1, 7] = 9000
+        else:
+            s = bad.sbr.copy()
+            s["ch"]["L_E"][-3, 0] = 7
+            bad = N.Batch(bad.q, bad.sf, bad.cb, bad.ics, bad.ms_used, bad.tns, bad.stream_slot, bad.frame_begin,
+                          bad.nch, s)
+        with pytest.raises(N.JaadError) as e:
+            ctx.decode(bad)
+        assert e.value.status == N.ERR_BITSTREAM
+        assert all((ctx.state_export(s) == before[s]).all() for s in range(64))
+        g2 = ctx.decode(rest)
+    fb = b.frame_begin
+    for r in range(64):
+        assert (g2[80 * r:80 * (r + 1)] == want[fb[r] + 80:fb[r + 1]]).all(), r
