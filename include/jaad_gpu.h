@@ -220,8 +220,9 @@ typedef struct jaad_sbr_frame {
  * order (CCEs in bitstream order, then coupled targets in order).  The reference applies them
  * after M/S and I/S in two passes, every point-0 (BEFORE_TNS) term, TNS, then every point-1
  * (AFTER_TNS) term; the library does the same.  The reference's TNS is a no-op, so only the order
- * of the additions tells the points apart in JAAD_TNS_COMPAT mode (JAAD_TNS_SPEC batches with
- * terms are refused).  Independent switching
+ * of the additions tells the points apart in JAAD_TNS_COMPAT mode; in JAAD_TNS_SPEC mode the
+ * point-1 terms are added after the spec filters (channel configurations 1 and 2; JAAD_TNS_SPEC
+ * batches with terms in configurations 3..7 are refused).  Independent switching
  * CCEs (ind_sw_cce_flag) never apply in the reference (couplingPoint becomes 3, matching neither
  * BEFORE_TNS, AFTER_TNS nor AFTER_IMDCT: CCE.java:113-129), so they produce no terms.
  * Limits (JAAD_ERR_UNSUPPORTED): a gain that is not finite or whose magnitude exceeds
@@ -268,8 +269,8 @@ typedef struct jaad_batch {
     const jaad_tns* tns;          /* [dev] [ch-frame] or NULL when no ch-frame sets JAAD_ICS_TNS    */
     const jaad_sbr_frame* sbr;    /* host [frame] when cfg.sbr ([frame][channel element] for channel
                                      configurations 3..7), else NULL                             */
-    /* dependent coupling (jaad_cce_term above); all zero / NULL for a batch without CCEs.  AAC-LC
-       configurations in JAAD_TNS_COMPAT mode only (JAAD_ERR_UNSUPPORTED otherwise). */
+    /* dependent coupling (jaad_cce_term above); all zero / NULL for a batch without CCEs.  JAAD_TNS_SPEC
+       mode: channel configurations 1 and 2 only (JAAD_ERR_UNSUPPORTED otherwise). */
     uint32_t n_cce;               /* CCE records                                                    */
     uint32_t n_cce_terms;
     const int16_t* cce_q;         /* [dev] [n_cce][1024]                                            */

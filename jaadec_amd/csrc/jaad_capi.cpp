@@ -1052,7 +1052,7 @@ int setup_coupling(jaad_ctx* ctx, const jaad_batch* db, KernelArgs& a, hipStream
             for (uint32_t i = t; i < e; i++) {
                 const jaad_cce_term& T = db->cce_terms[i];
                 if (T.point != point) continue;
-                meta[o] = (uint32_t)T.cce | ((uint32_t)T.channel << 16);
+                meta[o] = (uint32_t)T.cce | ((uint32_t)T.channel << 16) | ((uint32_t)T.point << 24);
                 std::memcpy(gain + (size_t)o * 120, T.gain, 480);
                 o++;
             }
@@ -1610,8 +1610,9 @@ static int check_batch(const jaad_ctx* ctx, const jaad_batch* b, size_t pcm_byte
     if (ctx->cfg.sbr && b->n_frames && !b->sbr) return JAAD_ERR_INVALID_ARG;
     if (pcm_bytes < pcm_bytes_per_frame(ctx, flags) * b->n_frames) return JAAD_ERR_INVALID_ARG;
     if (flags & ~(uint32_t)(JAAD_PCM_LITTLE_ENDIAN | JAAD_PCM_FLOAT32)) return JAAD_ERR_INVALID_ARG;
-    if (b->n_cce_terms) {  // dependent coupling: TNS compat mode (jaad_gpu.h); with SBR the core is coupled
-        if (ctx->cfg.tns_mode != JAAD_TNS_COMPAT) return JAAD_ERR_UNSUPPORTED;
+    if (b->n_cce_terms) {  // dependent coupling (jaad_gpu.h); with SBR the core is coupled
+        // spec TNS: mono and stereo configurations (the coupling points around the filters, kernel mode 3)
+        if (ctx->cfg.tns_mode != JAAD_TNS_COMPAT && ctx->n_elem > 1) return JAAD_ERR_UNSUPPORTED;
         if (!b->cce_terms || !b->n_cce || !b->cce_q || !b->cce_sf || !b->cce_cb || !b->cce_ics) return JAAD_ERR_INVALID_ARG;
         if (b->n_cce > JAAD_CCE_MAX_RECORDS) return JAAD_ERR_UNSUPPORTED;  // jaad_cce_term.cce is 16-bit
         for (uint32_t t = 0; t < b->n_cce_terms; t++) {

@@ -78,7 +78,8 @@ struct KernelArgs {
     float* dbg;                 // internal: stage dump of frame dbg_frame of chunk 0 (or null)
     int dbg_frame;
     // dependent coupling (CCE terms, jaad_gpu.h jaad_cce_term): null cce_off = none.  Frame f's
-    // terms are [cce_off[f], cce_off[f+1]); term t targets frame channel cce_meta[t] >> 16 and adds
+    // terms are [cce_off[f], cce_off[f+1]) (BEFORE_TNS terms first); term t is CCE record
+    // cce_meta[t] & 0xFFFF, targets frame channel (cce_meta[t] >> 16) & 0xFF, point cce_meta[t] >> 24, and adds
     // cce_spec[t][0..1023] (cce_term_kernel); ch0 = this launch's first channel of the frame
     const uint32_t* cce_off;
     const uint32_t* cce_meta;

@@ -1002,13 +1002,43 @@ __device__ __forceinline__ void iq_channel(const LdsTables& T, const float* iq_g
 
 // (TNS) -> IMDCT -> window/OLA of one channel whose spectrum is in buf (E/O layout); result
 // in out (slot o = position long_pos(u, o)), new overlap in ov
-template <bool kTnsSpec>
+// Dependent coupling with spec TNS (kernel mode 3): frame f's AFTER_TNS terms for channel ch of
+// this launch, added to the channel's spectrum in LDS once its TNS filters have run (CPE.java:
+// 172-179, SCE.java:100-108; the terms' addends from cce_term_kernel, -0.0 adds nothing)
+__device__ __forceinline__ void couple_after_tns(const KernelArgs& A, float* buf, int f, int ch, int u)
+{
+    const uint32_t t0 = A.cce_off[f], t1 = A.cce_off[f + 1];
+    bool any = false;
+    float x[16];
+    for (uint32_t t = t0; t < t1; t++) {
+        const uint32_t meta = A.cce_meta[t];
+        if (!(meta >> 24) || (int)((meta >> 16) & 0xFF) - (int)A.ch0 != ch) continue;
+        if (!any) load_spec(buf, u, x);  // (the TNS filters ended with a wave_sync)
+        any = true;
+        const float4* sp = reinterpret_cast<const float4*>(A.cce_spec + (size_t)t * 1024);
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const float4 a = sp[(512 * h + 8 * u) / 4], c = sp[(512 * h + 8 * u) / 4 + 1];
+            const float v[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
+#pragma unroll
+            for (int i = 0; i < 8; i++) x[8 * h + i] += v[i];
+        }
+    }
+    if (any) {
+        store_spec(buf, u, x);
+        wave_sync();
+    }
+}
+
+template <bool kTnsSpec, bool kCoupleAfter = false>
 __device__ __forceinline__ void synth_channel(const KernelArgs& A, const LdsTables& T, WaveLds<kTnsSpec>& W, float* buf,
-                                              const Ics& ic, size_t cf, float (&ov)[16], float (&out)[16])
+                                              const Ics& ic, size_t cf, float (&ov)[16], float (&out)[16], int f = 0,
+                                              int ch = 0)
 {
     const int u = lane_id();
     if constexpr (kTnsSpec)
         if (A.tns_mode == JAAD_TNS_SPEC && (ic.flags & JAAD_ICS_TNS) && A.tns) tns_spec(buf, W.tns, T, *A.gtab, u, ic, A.tns + cf);
+    if constexpr (kCoupleAfter) couple_after_tns(A, buf, f, ch, u);
     const FrameCtx fc{ic.seq, ic.shape, ic.shape_prev};
     if (fc.seq == JAAD_EIGHT_SHORT_SEQUENCE) {
         float re[8], im[8];
@@ -1041,12 +1071,13 @@ __device__ __forceinline__ void synth_channel(const KernelArgs& A, const LdsTabl
     } while (0)
 #endif
 
-// kMode: 0 = TNS compat (the reference), 1 = spec TNS, 2 = TNS compat with dependent coupling
+// kMode: 0 = TNS compat (the reference), 1 = spec TNS, 2 = TNS compat with dependent coupling,
+// 3 = spec TNS with dependent coupling (BEFORE_TNS terms, the TNS filters, AFTER_TNS terms)
 template <int kMode, int kOut, bool kStereo>
-__global__ __launch_bounds__(64 * waves_per_wg<kMode == 1>()) void lc_decode_kernel(KernelArgs A)
+__global__ __launch_bounds__(64 * waves_per_wg<kMode == 1 || kMode == 3>()) void lc_decode_kernel(KernelArgs A)
 {
-    constexpr bool kTnsSpec = kMode == 1;
-    [[maybe_unused]] constexpr bool kCouple = kMode == 2;
+    constexpr bool kTnsSpec = kMode == 1 || kMode == 3;
+    [[maybe_unused]] constexpr bool kCouple = kMode == 2 || kMode == 3;
     constexpr int kW = waves_per_wg<kTnsSpec>();
     constexpr int kThreads = 64 * kW;
     // one LDS object with the tables first: every table access is a 16-bit immediate offset
@@ -1326,9 +1357,12 @@ __global__ __launch_bounds__(64 * waves_per_wg<kMode == 1>()) void lc_decode_ker
                 // dependent coupling after M/S and I/S (CPE.java:172-179, SCE.java:100-108): the
                 // frame's terms in order, each adding its addend (CCE.applyDependentCoupling,
                 // A/syntax/CCE.java:188-215, precomputed by cce_term_kernel; -0.0 adds nothing)
+                // (with spec TNS, mode 3, the AFTER_TNS terms -- the frame's last ones -- wait for
+                // the filters: couple_after_tns)
                 const uint32_t t0 = A.cce_off[f], t1 = A.cce_off[f + 1];
                 for (uint32_t t = t0; t < t1; t++) {
-                    const int ch = (int)(A.cce_meta[t] >> 16) - (int)A.ch0;
+                    if (kMode == 3 && (A.cce_meta[t] >> 24)) break;
+                    const int ch = (int)((A.cce_meta[t] >> 16) & 0xFF) - (int)A.ch0;
                     if (ch < 0 || ch >= nch) continue;
                     const float4* sp = reinterpret_cast<const float4*>(A.cce_spec + (size_t)t * 1024);
                     float v[16];
@@ -1372,6 +1406,10 @@ __global__ __launch_bounds__(64 * waves_per_wg<kMode == 1>()) void lc_decode_ker
                         if (iR.flags & JAAD_ICS_TNS) tns_spec(W.rsp, W.tns, T, *A.gtab, u, iR, A.tns + cf0 + 1);
                     }
                 }
+                if constexpr (kMode == 3) {
+                    couple_after_tns(A, W.buf, f, 0, u);
+                    couple_after_tns(A, W.rsp, f, 1, u);
+                }
                 float* const bufs[2] = {W.buf, W.rsp};
                 f2 cx[2][8];
                 imdct_long_pk<2>(bufs, T, lane_id(), cx);
@@ -1379,8 +1417,8 @@ __global__ __launch_bounds__(64 * waves_per_wg<kMode == 1>()) void lc_decode_ker
                 ola_long_pk(T, FrameCtx{iR.seq, iR.shape, iR.shape_prev}, cx[1], ovR, outR);
                 wave_sync();
             } else {
-                synth_channel<kTnsSpec>(A, T, W, W.buf, iL, cf0, ovL, outL);
-                if (stereo) synth_channel<kTnsSpec>(A, T, W, W.rsp, iR, cf0 + 1, ovR, outR);
+                synth_channel<kTnsSpec, kMode == 3>(A, T, W, W.buf, iL, cf0, ovL, outL, f, 0);
+                if (stereo) synth_channel<kTnsSpec, kMode == 3>(A, T, W, W.rsp, iR, cf0 + 1, ovR, outR, f, 1);
             }
             STAMP(8);
             // frame f+1's inputs (loaded since the IQ, a whole IMDCT ago) are in registers before
@@ -1473,7 +1511,7 @@ __global__ __launch_bounds__(64 * waves_per_wg<kMode == 1>()) void lc_decode_ker
 template <int kMode, bool kStereo>
 static void launch_lc_mode(const KernelArgs& a, hipStream_t stream)
 {
-    constexpr int W = waves_per_wg<kMode == 1>();
+    constexpr int W = waves_per_wg<kMode == 1 || kMode == 3>();
 #define JAAD_LAUNCH(O) \
     hipLaunchKernelGGL((lc_decode_kernel<kMode, O, kStereo>), dim3((a.n_chunks + W - 1) / W), dim3(64 * W), 0, stream, a)
     const int o = (a.out_mode == kOutPlanarF32) ? 4 : (a.out_mode & JAAD_PCM_FLOAT32) ? 2 : (a.out_mode & JAAD_PCM_LITTLE_ENDIAN) ? 1 : 0;
@@ -1487,7 +1525,8 @@ static void launch_lc_mode(const KernelArgs& a, hipStream_t stream)
 template <bool kStereo>
 static hipError_t launch_lc_ch(const KernelArgs& a, hipStream_t stream, bool tns_spec)
 {
-    if (a.cce_off) launch_lc_mode<2, kStereo>(a, stream);  // coupling: TNS compat only (jaad_gpu.h)
+    if (a.cce_off && tns_spec) launch_lc_mode<3, kStereo>(a, stream);  // coupling around the spec TNS filters
+    else if (a.cce_off) launch_lc_mode<2, kStereo>(a, stream);
     else if (tns_spec) launch_lc_mode<1, kStereo>(a, stream);
     else launch_lc_mode<0, kStereo>(a, stream);
     return hipGetLastError();

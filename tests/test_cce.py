@@ -6,7 +6,7 @@ CPU: CCE elements written by the test writer parse into records and terms equal 
 restatement of CCE.decode's gain lists and of processDependentCoupling's target walk (including
 the SCE/LFE tag quirk and the never-applied independent-switching CCE).  GPU: batches with
 coupling terms decode byte-exactly as the C restatement (oracle/jaad_oracle.c orc_couple) --
-stereo, mono, 5.1, noise bands in the CCE, short windows, several terms per frame -- through the
+stereo, mono, 5.1, spec TNS between the two coupling points, noise bands in the CCE, short windows, several terms per frame -- through the
 host entry, the device entry and the Decoder facade."""
 import math
 
@@ -287,12 +287,33 @@ def test_gpu_coupling_multichannel_and_device_entry():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("cc", [1, 2])
+def test_gpu_coupling_with_spec_tns_matches_oracle(cc):
+    """JAAD_TNS_SPEC with coupling: BEFORE_TNS terms, the TNS filters, AFTER_TNS terms
+    (A/syntax/CPE.java:172-179; oracle/jaad_oracle.c orc_couple / orc_tns_spec), long and short
+    windows, frames with terms at both points on one channel."""
+    b = coupled_batch(cc, n_streams=6, fps=40, seed=50 + cc)
+    assert (b.ics["flags"] & N.ICS_TNS).any() and (b.cce_terms["point"] == 1).any()
+    cfg = N.make_cfg(channel_config=cc, tns_mode=N.TNS_SPEC)
+    want = O.decode_batch(cfg, b, O.Streams(6), N.PCM_BIG_ENDIAN, threads=8)
+    with N.Context(cfg, 6) as ctx:
+        got = ctx.decode(b, N.PCM_BIG_ENDIAN)
+    assert (got == want).all(), np.flatnonzero((got != want).any(1))[:8]
+    # the AFTER_TNS point is not the BEFORE_TNS one once the filters are live
+    b.cce_terms["point"] ^= 1
+    assert (O.decode_batch(cfg, b, O.Streams(6), N.PCM_BIG_ENDIAN, threads=8) != want).any()
+    with N.Context(cfg, 6) as ctx:
+        assert (ctx.decode(b, N.PCM_BIG_ENDIAN) == O.decode_batch(cfg, b, O.Streams(6), N.PCM_BIG_ENDIAN, threads=8)).all()
+
+
+@pytest.mark.gpu
 def test_gpu_coupling_rejections():
-    b = coupled_batch(2, n_streams=2, fps=8, seed=2)
-    with N.Context(N.make_cfg(channel_config=2, tns_mode=N.TNS_SPEC), 2) as ctx:
-        with pytest.raises(N.JaadError) as e:
+    b = coupled_batch(6, n_streams=2, fps=8, seed=2)
+    with N.Context(N.make_cfg(channel_config=6, tns_mode=N.TNS_SPEC), 2) as ctx:
+        with pytest.raises(N.JaadError) as e:  # spec TNS with coupling: configurations 1 and 2
             ctx.decode(b)
         assert e.value.status == N.ERR_UNSUPPORTED
+    b = coupled_batch(2, n_streams=2, fps=8, seed=2)
     with N.Context(N.make_cfg(channel_config=2), 2) as ctx:
         bad = b.cce_terms.copy()
         bad = bad[::-1].copy()  # not sorted by frame
