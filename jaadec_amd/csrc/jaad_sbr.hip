@@ -240,6 +240,130 @@ __device__ __forceinline__ void dct4(const DctConst& K, int e, int E, float xr, 
     oi = o2[0];
 }
 
+// Two 32-point DCT-IVs per half-wave, packed: the same transform of two slots (slot 0, slot 1)
+// whose element e sits in lane e as a float2 (xr, xi) -- v_pk_* arithmetic does both slots at
+// once.  Stage 1's xor-16 exchange is a single v_permlane16_swap of the two slots' registers: it
+// leaves lanes 0..15 holding both partners (j, j+16) of slot 0 and lanes 16..31 both partners of
+// slot 1, so from stage 1 on lane j (+16) computes positions j (S) and j + 16 (D) of one slot, with
+// the same twiddles as before (they depend on j only), and no exchange crosses 16 lanes again.
+// Outputs: (orr, oi).x = output element E_S = bitrev5(j), .y = element E_S + 1, of slot e >> 4.
+// Every element sees exactly the binary32 operations of dct4_n.
+typedef float f2 __attribute__((ext_vector_type(2)));
+struct DctPairConst {
+    float t0, t32, t64;     // pre-modulation (element e, both slots)
+    float w1r, w1i, w2r, w2i, w3;
+    f2 t96, t128, t160;     // post-modulation of elements E_S (x) and E_S + 1 (y)
+};
+__device__ __forceinline__ DctPairConst load_dct_pair_const(const float* dct, int e)
+{
+    const DctConst K = load_dct_const(dct, e, 0);
+    const int es = bitrev5(e & 15);
+    DctPairConst P;
+    P.t0 = K.t0;
+    P.t32 = K.t32;
+    P.t64 = K.t64;
+    P.w1r = K.w1r;
+    P.w1i = K.w1i;
+    P.w2r = K.w2r;
+    P.w2i = K.w2i;
+    P.w3 = K.w3;
+    P.t96 = f2{dct[es + 96], dct[es + 97]};
+    P.t128 = f2{dct[es + 128], dct[es + 129]};
+    P.t160 = f2{dct[es + 160], dct[es + 161]};
+    return P;
+}
+// (xor 4 through the LDS crossbar, ds_swizzle bit mode: one instruction instead of two DPP moves)
+template <int kXor>
+__device__ __forceinline__ float swz_x(float v)
+{
+    if constexpr (kXor == 4) return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), 0x1F | (4 << 10)));
+    else return swz<kXor>(v);
+}
+template <int kXor>
+__device__ __forceinline__ f2 swz2(f2 v) { return f2{swz_x<kXor>(v.x), swz_x<kXor>(v.y)}; }
+
+__device__ __forceinline__ void dct4_pair(const DctPairConst& K, int e, f2 xr, f2 xi, f2& orr, f2& oi)
+{
+    const f2 tmp = (xr + xi) * K.t0;
+    const f2 r0 = (xi * K.t64) + tmp;
+    const f2 i0 = (xr * K.t32) + tmp;
+    // stage 1 (DCT.java:143-164), transposed: A = position j, B = position j + 16 of this lane's slot
+    const auto sr = __builtin_amdgcn_permlane16_swap(__float_as_int(r0.x), __float_as_int(r0.y), false, false);
+    const auto si = __builtin_amdgcn_permlane16_swap(__float_as_int(i0.x), __float_as_int(i0.y), false, false);
+    const f2 A = f2{__int_as_float(sr[0]), __int_as_float(si[0])}, B = f2{__int_as_float(sr[1]), __int_as_float(si[1])};
+    const f2 sum = A + B, dif = A - B;
+    // (r, i).x = position j, .y = position j + 16
+    f2 r = f2{sum.x, (dif.x * K.w1r) - (dif.y * K.w1i)};
+    f2 i = f2{sum.y, (dif.x * K.w1i) + (dif.y * K.w1r)};
+    // stage 2 (:166-207): pairs (i, i+8) in each 16-group, twiddle w[2j]
+    {
+        const f2 pr = swz2<8>(r), pi = swz2<8>(i);
+        if (!(e & 8)) {
+            r = r + pr;
+            i = i + pi;
+        } else {
+            const f2 tr = pr - r, ti = pi - i;
+            r = (tr * K.w2r) - (ti * K.w2i);
+            i = (tr * K.w2i) + (ti * K.w2r);
+        }
+    }
+    // stage 3 (:212-287): pairs (i, i+4) in each 8-group; four bottom variants
+    {
+        const f2 pr = swz2<4>(r), pi = swz2<4>(i);
+        if (!(e & 4)) {
+            r = r + pr;
+            i = i + pi;
+        } else {
+            const int v = e & 3;
+            const f2 tr = pr - r, ti = pi - i;
+            if (v == 0) {
+                r = tr;
+                i = ti;
+            } else if (v == 1) {
+                r = (tr + ti) * K.w3;
+                i = (ti - tr) * K.w3;
+            } else if (v == 2) {
+                const f2 ni = r - pr;
+                r = ti;
+                i = ni;
+            } else {
+                r = (tr - ti) * K.w3;
+                i = (tr + ti) * K.w3;
+            }
+        }
+    }
+    // stage 4 (:291-322): pairs (i, i+2) in each 4-group
+    {
+        const f2 pr = swz2<2>(r), pi = swz2<2>(i);
+        if (!(e & 2)) {
+            r = r + pr;
+            i = i + pi;
+        } else if (!(e & 1)) {
+            r = pr - r;
+            i = pi - i;
+        } else {
+            const f2 nr = pi - i, ni = r - pr;
+            r = nr;
+            i = ni;
+        }
+    }
+    // stage 5 (:326-341): pairs (i, i+1)
+    {
+        const f2 pr = swz2<1>(r), pi = swz2<1>(i);
+        if (!(e & 1)) {
+            r = r + pr;
+            i = i + pi;
+        } else {
+            r = pr - r;
+            i = pi - i;
+        }
+    }
+    // post-modulation; element 16 (E_S of j == 1) has its own form
+    const f2 t = (r + i) * K.t96;
+    orr = (i * K.t160) + t;
+    oi = (r * K.t128) + t;
+    if ((e & 15) == 1) oi.x = (i.x - r.x) * K.t96.x, orr.x = t.x;
+}
 
 constexpr int kWavesPerBlock = 4;
 
@@ -886,6 +1010,7 @@ struct SynSrc {
     const gfloat* xs;  // rows l >= t0 (64 bands, 128 floats a row)
     const gfloat* xc;  // rows l < t0: the carried Xsbr rows 2..7, kprev bands
     int t0, kprev, rows;
+    int lo;            // rows below lo are clamped to it (the 64-band history's leading dummy slot)
     size_t n0;         // first output sample (emitting frames)
     bool emit, dup;
 };
@@ -1009,11 +1134,14 @@ __device__ __forceinline__ void synthesis32(const SbrArgs& A, const SbrChunk& ck
 template <bool kDown>
 __global__ __launch_bounds__(256) void sbr_synthesis_kernel(SbrArgs A)
 {
-    __shared__ float vring_s[kWavesPerBlock][kDown ? 1 : 10][128];
+    // v ring: 10 blocks, each also kept 10 blocks up (a window reads ring blocks q+1..q+10 at fixed
+    // offsets); half h of ring block q at [h][q][64], so the two slots of a pair read a tap's words
+    // 256 bytes apart (one ds_read2st64 a tap, the pair's values in one register pair)
+    __shared__ float vring_s[kWavesPerBlock][kDown ? 1 : 40][64];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t ci = blockIdx.x * kWavesPerBlock + wave;
     if (ci >= A.n_chunks) return;
-    float(*vring)[128] = vring_s[wave];
+    float(*vring)[64] = vring_s[wave];
     const SbrChunk ck = A.chunks[ci];
     const int u = lane_id();
     const int e = u & 31, half = u >> 5;
@@ -1021,13 +1149,19 @@ __global__ __launch_bounds__(256) void sbr_synthesis_kernel(SbrArgs A)
     // X_right from ps_kernel (xps), whose rows need no carry patch
     const int c = ck.ch, nch = A.nch, ps = A.ps;
     const int rc = ps ? 0 : c;  // channel of the SBR records
-    const int E = bitrev5(e);  // output element of this lane's DCT-IV
-    const DctConst K = load_dct_const(A.dct, e, E);
+    const DctPairConst K = load_dct_pair_const(A.dct, e);
+    // v-block words of this lane's DCT outputs (dct4_pair: elements n = E_S (.x) and E_S + 1 (.y) of
+    // slot e >> 4; half 0 holds the x1 outputs and gets the x2 real parts, half 1 the x2 outputs
+    // and gets the x1 imaginary parts): with a = x2 + x1, b = x2 - x1 (SynthesisFilterbank64.java:99-129)
+    //   half 0: v[2n] = b, v[127-2n] = a       half 1: v[63-2n] = a, v[64+2n] = b
+    const int es = bitrev5(e & 15), sl = 128 * ((e >> 4) & 1);
+    auto ring_word = [&](int w) { return (w >> 6) * 20 * 64 + (w & 63) + (sl >> 1); };  // v[w] of ring block 0 (+ slot)
+    const int wa_x = ring_word(half ? 63 - 2 * es : 127 - 2 * es), wb_x = ring_word(half ? 64 + 2 * es : 2 * es);
+    const int wa_y = ring_word(half ? 61 - 2 * es : 125 - 2 * es), wb_y = ring_word(half ? 66 + 2 * es : 2 * es + 2);
     float cw[10];
 #pragma unroll
     for (int t = 0; t < 10; t++) cw[t] = kDown ? A.qmf_c[64 * t + 2 * e] : A.qmf_c[u + 64 * t];
     const float scale = 1.f / 64.f;
-    int vpos = 0;
     // This lane's two DCT inputs of a slot, gathered straight from the row of X (64 float2, band
     // order) instead of exchanged through cross-lane permutes:
     //   64 bands: half 0 (in_real1[e], in_imag1[e]) = (Re X[2e], Re X[63-2e]),
@@ -1049,45 +1183,49 @@ __global__ __launch_bounds__(256) void sbr_synthesis_kernel(SbrArgs A)
         b = band_b < klim ? b : 0.0f;
     };
 
-    // one slot: DCT-IV pair -> v block (:99-129); emit: window (:134-146), sample u in `res`
-    auto slot64 = [&](float a, float b, bool emit, float& res) {
-        const float in_r = scale * a;  // (fetch) d = 0: in_real1[e] / d = 1: in_real2[e]
-        const float in_i = scale * b;  //            in_imag1[e] /        in_imag2[e]
-        float orr, oi;
-        dct4(K, e, E, in_r, in_i, orr, oi);
-        const float Ap = shfl(orr, u ^ 32);
-        const float Bp = shfl(oi, 32 + (31 - e));
-        const float Cp = shfl(oi, 31 - e);
-        float* vb = vring[vpos];
-        if (!half) {
-            vb[2 * E] = Ap - orr;
-            vb[127 - 2 * E] = Ap + orr;
-        } else {
-            vb[2 * E + 1] = Bp + Cp;
-            vb[126 - 2 * E] = Bp - Cp;
-        }
+    // two slots at ring blocks p, p + 1 (p even): DCT-IV pairs -> v blocks (:99-129); emit: their
+    // windows (:134-146), sample u in res0 / res1
+    auto slot_pair = [&](float a0, float b0, float a1, float b1, int p, bool emit, float& res0, float& res1) {
+        const f2 in_r = f2{a0, a1} * scale;  // (fetch) d = 0: in_real1[e] / d = 1: in_real2[e]
+        const f2 in_i = f2{b0, b1} * scale;  //            in_imag1[e] /        in_imag2[e]
+        f2 orr, oi;
+        dct4_pair(K, e, in_r, in_i, orr, oi);
+        // half 0 gets x2's real parts, half 1 x1's imaginary parts (v_permlane32_swap)
+        const auto px = __builtin_amdgcn_permlane32_swap(__float_as_int(orr.x), __float_as_int(oi.x), false, false);
+        const auto py = __builtin_amdgcn_permlane32_swap(__float_as_int(orr.y), __float_as_int(oi.y), false, false);
+        const f2 x1 = f2{__int_as_float(px[0]), __int_as_float(py[0])};
+        const f2 x2 = f2{__int_as_float(px[1]), __int_as_float(py[1])};
+        const f2 a = x2 + x1, b = x2 - x1;
+        // the pair's windows read blocks p+1..p+11 of the ring, i.e. the upper copies of both new
+        // blocks and, at p+1, the old block p-9 that slot 0's last tap needs: the lower copies
+        // (p, p+1) are written after the windows
+        float* vb = vring[p];
+        vb[wa_x + 640] = a.x;
+        vb[wb_x + 640] = b.x;
+        vb[wa_y + 640] = a.y;
+        vb[wb_y + 640] = b.y;
         wave_sync();
         if (emit) {
-            const float* v0 = vring[vpos];
-            const float* v1 = vring[(vpos + 9) % 10];
-            const float* v2 = vring[(vpos + 8) % 10];
-            const float* v3 = vring[(vpos + 7) % 10];
-            const float* v4 = vring[(vpos + 6) % 10];
-            const float* v5 = vring[(vpos + 5) % 10];
-            const float* v6 = vring[(vpos + 4) % 10];
-            const float* v7 = vring[(vpos + 3) % 10];
-            const float* v8 = vring[(vpos + 2) % 10];
-            const float* v9 = vring[(vpos + 1) % 10];
-            res = (v0[u] * cw[0]) + (v1[64 + u] * cw[1]) + (v2[u] * cw[2]) + (v3[64 + u] * cw[3]) +
-                  (v4[u] * cw[4]) + (v5[64 + u] * cw[5]) + (v6[u] * cw[6]) + (v7[64 + u] * cw[7]) +
-                  (v8[u] * cw[8]) + (v9[64 + u] * cw[9]);
+            // tap t of the slot at block q reads block q - t = ring q + 10 - t, half t & 1
+            const float* v = &vring[p][u];
+            f2 acc;
+#pragma unroll
+            for (int t = 0; t < 10; t++) {
+                const f2 x = f2{v[64 * (20 * (t & 1) + 10 - t)], v[64 * (20 * (t & 1) + 11 - t)]};
+                const f2 pr = x * cw[t];
+                acc = t == 0 ? pr : acc + pr;
+            }
+            res0 = acc.x;
+            res1 = acc.y;
         }
         wave_sync();
-        vpos = vpos == 9 ? 0 : vpos + 1;
+        vb[wa_x] = a.x;
+        vb[wb_x] = b.x;
+        vb[wa_y] = a.y;
+        vb[wb_y] = b.y;
     };
 
     const size_t spf = kDown ? 1024 : 2048, sps = kDown ? 32 : 64;  // output samples per frame / slot
-    auto slot = [&](float Xr, float Xi, bool emit, float& res) { slot64(Xr, Xi, emit, res); };
 
     // The chunk's slots (9 history slots, then 32 per frame) run as a software pipeline of 4-slot
     // groups: the rows of group g+1 are loaded while group g computes, and group g's PCM is
@@ -1156,10 +1294,11 @@ __global__ __launch_bounds__(256) void sbr_synthesis_kernel(SbrArgs A)
 #define JAAD_SYN_GROUP 4
 #endif
     constexpr int kG = JAAD_SYN_GROUP;
+    static_assert(kG % 2 == 0, "slots run in pairs");
     auto load_group = [&](const SynSrc& S, int l0, float (&ga)[kG], float (&gb)[kG], int (&kl)[kG]) {
 #pragma unroll
         for (int i = 0; i < kG; i++) {
-            const int l = min(l0 + i, S.rows - 1);  // (rows past the frame's last are not used)
+            const int l = max(min(l0 + i, S.rows - 1), S.lo);  // (rows past the frame's last are not used)
             const bool carry = l < S.t0;
             kl[i] = carry ? S.kprev : kb;
             fetch(carry ? S.xc + (l + 2) * 128 : S.xs + l * 128, ga[i], gb[i]);
@@ -1197,9 +1336,16 @@ __global__ __launch_bounds__(256) void sbr_synthesis_kernel(SbrArgs A)
         return;
     }
 
+    // the history's 9 slots go to ring blocks 1..9 behind a dummy slot at block 0 (overwritten by
+    // the first frame's slot 0 before any window reads it), so every frame's slot pairs start at
+    // an even block
     SynSrc S = history_src();
+    S.xs -= 128;
+    S.rows = 10;
+    S.lo = 1;
     SynRec W{};                  // record fields of frame j + 1
     rec_load(0, W);
+    int p = 0;                   // ring block of the next pair's first slot
     float ga[kG] = {}, gb[kG] = {};
     int kl[kG];
     load_group(S, 0, ga, gb, kl);
@@ -1236,10 +1382,12 @@ __global__ __launch_bounds__(256) void sbr_synthesis_kernel(SbrArgs A)
             load_group(Sn, ln, na, nb, nk);
             float res[kG] = {};
 #pragma unroll
-            for (int i = 0; i < kG; i++) {
-                if (l0 + i >= S.rows) break;
+            for (int i = 0; i < kG; i += 2) {
+                if (l0 + i >= S.rows) break;  // (rows come in pairs: 10 or 32)
                 mask(kl[i], ga[i], gb[i]);
-                slot(ga[i], gb[i], S.emit, res[i]);
+                mask(kl[i + 1], ga[i + 1], gb[i + 1]);
+                slot_pair(ga[i], gb[i], ga[i + 1], gb[i + 1], p, S.emit, res[i], res[i + 1]);
+                p = p == 8 ? 0 : p + 2;
             }
             vmem_drain();
             store_group(S, l0, res);

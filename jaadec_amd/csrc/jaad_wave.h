@@ -15,10 +15,12 @@ __device__ __forceinline__ void wave_sync()
 
 __device__ __forceinline__ int lane_id() { return (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
 
+// (every control used here has a source lane in the row for every lane: no old value is read, so
+// none is materialised -- update_dpp(0, ...) cost a v_mov 0 per exchange)
 template <int kCtrl>
 __device__ __forceinline__ float dpp_mov(float v)
 {
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), kCtrl, 0xF, 0xF, false));
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), kCtrl, 0xF, 0xF, true));
 }
 // value held by lane ^ kXor inside a 16-lane row (DPP, no LDS)
 template <int kXor>
