@@ -540,16 +540,24 @@ constexpr int kApBands = 23;  // QMF bands 0..22 run the all-pass chain
 
 // link m (0, 1, 2) of the all-pass chain at slot N: ring length 3, 4, 5; r = input (after the
 // 2-slot delay's phi rotation for link 0, the previous link's output otherwise) -> output
+// (packed: both components of each step in one v_pk_* instruction, the same binary32 operations --
+// x + (-y) is x - y exactly)
+typedef float pf2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ pf2 pk(float2 v) { return pf2{v.x, v.y}; }
+__device__ __forceinline__ float2 unpk(pf2 v) { return make_float2(v.x, v.y); }
+// (t.x * c0) + (t.y * c1), (t.y * c0) - (t.x * c1)
+__device__ __forceinline__ pf2 rot_conj(pf2 t, float c0, float c1)
+{
+    return (t * c0) + (pf2{t.y, t.x} * pf2{c1, -c1});  // (-c1 * x is -(c1 * x) exactly)
+}
 template <int M, int N, int Len>
 __device__ __forceinline__ float2 ap_link(float2 (&d)[Len], float2 r, const float q[2], float g)
 {
-    const float2 t = d[N % Len];
-    float tr = (t.x * q[0]) + (t.y * q[1]);
-    float ti = (t.y * q[0]) - (t.x * q[1]);
-    tr -= g * r.x;
-    ti -= g * r.y;
-    d[N % Len] = make_float2(r.x + (g * tr), r.y + (g * ti));
-    return make_float2(tr, ti);
+    const pf2 R = pk(r);
+    pf2 T = rot_conj(pk(d[N % Len]), q[0], q[1]);
+    T = T - (R * g);                    // tr -= g * r.x; ti -= g * r.y
+    d[N % Len] = unpk(R + (T * g));     // r.x + (g * tr), r.y + (g * ti)
+    return unpk(T);
 }
 // the 2-slot delay and its phi rotation (the input of link 0)
 template <int N>
@@ -557,7 +565,7 @@ __device__ __forceinline__ float2 ap_delay2(float2 (&d)[2], float2 x, const floa
 {
     const float2 t0 = d[N % 2];
     d[N % 2] = x;
-    return make_float2((t0.x * phi[0]) + (t0.y * phi[1]), (t0.y * phi[0]) - (t0.x * phi[1]));
+    return unpk(rot_conj(pk(t0), phi[0], phi[1]));
 }
 
 // the lane index as an opaque value: each role recomputes it (two VALU) instead of the compiler
