@@ -936,7 +936,7 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
 
     // device side: intermediates (stream-ordered) and this set's record copy (copy stream)
     HIPCHK(ctx->d_xlow.ensure(ncf * 2048 * sizeof(float) + 256));
-    HIPCHK(ctx->d_xsyn.ensure(ncf * 4096 * sizeof(float) + 256));
+    if (!ps) HIPCHK(ctx->d_xsyn.ensure(ncf * 4096 * sizeof(float) + 256));  // (PS: the HF kernel writes into xps)
     HIPCHK(ctx->d_xcarry.ensure(ncf * kSbrCarryFloats * sizeof(float) + 256));
     HIPCHK(ctx->d_gq.ensure(ncf * 640 * sizeof(float) + 256));
     if (ps) {

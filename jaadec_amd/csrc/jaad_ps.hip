@@ -8,7 +8,8 @@
 // decorrelator and the transient detector's peak/smooth IIRs.  Everything else reaches back at
 // most one frame and runs frame-parallel (one wave per frame) on what the previous stage left in
 // HBM:
-//   ps_analysis_kernel  X_left (SBR output, carry-patched) -> xps[f][0]; hybrid analysis -> xhl;
+//   ps_analysis_kernel  X_left = the SBR output the HF kernel wrote into xps[f][0], rows l < t_E[0]
+//                       patched with the carried rows; hybrid analysis -> xhl;
 //                       band energies P -> pg                                  (wave per frame)
 //   ps_decor_kernel     per run, eight waves: the three all-pass links of the QMF bands (lane =
 //                       band) and of the hybrid groups pipelined over waves, transient detector,
@@ -132,7 +133,7 @@ __device__ __forceinline__ const float2* x_carry_prev(const SbrArgs& A, const Sb
 // Filterbank.buffer after frame f, element i of band b: work[32 + i] = X_left[26 + i][b] (b < 3)
 __device__ __forceinline__ float2 hyb_history_after(const SbrArgs& A, uint32_t f, int b, int i)
 {
-    return i < 6 ? reinterpret_cast<const float2*>(A.xsyn + (size_t)f * 4096)[(26 + i) * 64 + b]
+    return i < 6 ? reinterpret_cast<const float2*>(A.xps + (size_t)f * 8192)[(26 + i) * 64 + b]
                  : reinterpret_cast<const float2*>(A.xcarry + (size_t)f * kSbrCarryFloats)[(i - 4) * 64 + b];
 }
 
@@ -152,14 +153,15 @@ __global__ __launch_bounds__(256) void ps_analysis_kernel(SbrArgs A)
     const PsConst& K = *A.psc;
     {
         const int t0 = R.t_E[0], kprev = R.kx_prev + R.M_prev, K = R.blim;
-        const float2* xs = reinterpret_cast<const float2*>(A.xsyn + (size_t)f * 4096);
+        // The HF kernel wrote this frame's X rows into X_left's place (xs = xo): only rows
+        // l < t_E[0] are replaced, by the carried ones.
+        float2* xo = reinterpret_cast<float2*>(A.xps + (size_t)f * 8192);
+        const float2* xs = xo;
         const float2* xc = x_carry_prev(A, R, f);
         const float2* xn = reinterpret_cast<const float2*>(A.xcarry + (size_t)f * kSbrCarryFloats);
-        float2* xo = reinterpret_cast<float2*>(A.xps + (size_t)f * 8192);
-        // every row load is issued before the first store: xo might alias the sources as far as
-        // the compiler knows, so a load-store-load loop waits out one global round trip per row.
-        // Bands >= the run's limit K are zero (SbrRec::blim): their lanes read lane 0's word (no
-        // extra bytes) and store nothing.
+        // every row load is issued before the first store: a load-store-load loop would wait out
+        // one global round trip per row.  Bands >= the run's limit K are zero (SbrRec::blim): their
+        // lanes read lane 0's word (no extra bytes) and store nothing.
         const bool ps_on = (R.flags & kSbrPsOn) != 0;
         float2 v[38];
 #pragma unroll
@@ -173,7 +175,8 @@ __global__ __launch_bounds__(256) void ps_analysis_kernel(SbrArgs A)
         for (int l = 0; l < 32; l++) L.xl[l][u] = v[l];
         if (u < K)
 #pragma unroll
-            for (int l = 0; l < 32; l++) xo[l * 64 + u] = v[l];
+            for (int l = 0; l < 32; l++)
+                if (l < t0) xo[l * 64 + u] = v[l];
         // a frame without PS data only hands its X (qmfs0 input) to the synthesis
         if (!ps_on) return;
 #pragma unroll
@@ -1069,8 +1072,9 @@ hipError_t launch_ps(const SbrArgs& a, hipStream_t stream)
     const dim3 g((a.n_cf + kPsWaves - 1) / kPsWaves);
     hipLaunchKernelGGL(ps_analysis_kernel, g, dim3(64 * kPsWaves), 0, stream, a);
     hipLaunchKernelGGL(ps_decor_kernel, dim3(a.n_runs), dim3(64 * kDecorWaves), 0, stream, a);
-    hipLaunchKernelGGL(ps_mix_kernel, g, dim3(64 * kPsWaves), 0, stream, a);
+    // (before the mixing: the state's hybrid history is X_left, which the mixing overwrites)
     hipLaunchKernelGGL(ps_state_kernel, dim3(a.n_runs), dim3(64), 0, stream, a);
+    hipLaunchKernelGGL(ps_mix_kernel, g, dim3(64 * kPsWaves), 0, stream, a);
     return hipGetLastError();
 }
 

@@ -142,7 +142,7 @@ struct SbrArgs {
     const float* epool;
     const SbrTab* tabs;
     float* xlow;                // [ch-frame][32 slots][32 bands][2]
-    float* xsyn;                // [ch-frame][32 slots][64 bands][2]
+    float* xsyn;                // [ch-frame][32 slots][64 bands][2] (not with PS: the HF kernel writes xps[f][0])
     float* xcarry;              // [ch-frame][8][64][2]: Xsbr rows 32..39 after HF adjustment
     float* gq;                  // [ch-frame][2][5][64] ring after the frame (smoothing / state)
     const SbrChunk* chunks;     // synthesis chunks

@@ -507,8 +507,17 @@ __global__ __launch_bounds__(256, 3) void sbr_hf_kernel(SbrArgs A)
     }
     const SbrRec& R = L.rec;
     const SbrTab& T = L.tab;
-    const int kx = T.kx, M = T.M, L_E = R.L_E;
-    const int first = R.t_E[0], last = R.t_E[L_E];
+    // The fields that steer loops, branches and selects, read into SGPRs: a field read from the
+    // LDS copy is a VGPR the compiler cannot prove wave-uniform, so every envelope-border test,
+    // border walk and table-width loop over it was a VALU compare + select or an exec-masked
+    // divergent loop (C4 HF 715 -> ~600 us, profiles/round5_hf_uniform/).
+    auto ufl = [](int v) { return (int)__builtin_amdgcn_readfirstlane(v); };
+    const int kx = ufl(T.kx), M = ufl(T.M), L_E = ufl(R.L_E);
+    const uint32_t noise0 = (uint32_t)ufl(R.noise0), sine0 = (uint32_t)ufl(R.sine0);
+    int tE[6];
+#pragma unroll
+    for (int k = 0; k < 6; k++) tE[k] = ufl(R.t_E[k]);
+    const int first = tE[0], last = ufl(R.t_E[L_E]);
     const int s_lim = R.lim_bands;
     const float rel = __fdiv_rn(1.0f, 1.0f + 1e-6f);
 
@@ -569,20 +578,25 @@ __global__ __launch_bounds__(256, 3) void sbr_hf_kernel(SbrArgs A)
             eo += on ? (fl ? T.n_hi : T.n_lo) : 0;
         }
     }
+    // The G/Q smoothing ring in age order: gr[0] is the entry the frame's first assembled row
+    // overwrites (ring position GQ_ringbuf_index = gq0), gr[4] the newest; each row shifts it by one
+    // and appends, so its five filter taps are gr[0..4] in order -- compile-time registers instead
+    // of a select over the ring per tap (positions read rotated once here, gq0 wave-uniform).
     float gr[5] = {0, 0, 0, 0, 0}, qr[5] = {0, 0, 0, 0, 0};
-    int gidx = R.gq0;
+    const int gq0 = ufl(R.gq0);
     if ((P == 2 || (P == 3 && A.smoothing)) && !(R.flags & kSbrReset)) {
         const float* ring = R.first ? &A.state[(size_t)R.slot * 2 + c].gq[0][0][0] : A.gq + (size_t)(cf - A.nch) * 640;
         const int mm = u - kx >= 0 && u - kx < 64 ? u - kx : 0;
 #pragma unroll
         for (int j = 0; j < 5; j++) {
-            gr[j] = ring[j * 64 + mm];
-            qr[j] = ring[320 + j * 64 + mm];
+            const int pj = (gq0 + j) % 5;
+            gr[j] = ring[pj * 64 + mm];
+            qr[j] = ring[320 + pj * 64 + mm];
         }
         if (A.dbg && cf == 2)
             for (int j = 0; j < 5; j++) {
-                A.dbg[j * 64 + u] = gr[j];
-                A.dbg[320 + j * 64 + u] = qr[j];
+                A.dbg[((gq0 + j) % 5) * 64 + u] = gr[j];
+                A.dbg[320 + ((gq0 + j) % 5) * 64 + u] = qr[j];
             }
     }
 
@@ -672,12 +686,12 @@ __global__ __launch_bounds__(256, 3) void sbr_hf_kernel(SbrArgs A)
             const int i = r - 2;
 #pragma unroll
             for (int l = 0; l < 5; l++)
-                if (l < L_E && i >= R.t_E[l] && i < R.t_E[l + 1]) acc[l] += en;
+                if (l < L_E && i >= tE[l] && i < tE[l + 1]) acc[l] += en;
         }
 #pragma unroll
         for (int l = 0; l < 5; l++) {
             if (l < L_E && band) {
-                float div = (float)(R.t_E[l + 1] - R.t_E[l]);
+                float div = (float)(tE[l + 1] - tE[l]);
                 if (div == 0.0f) div = 1.0f;
                 L.ecurr[l][m] = __fdiv_rn(acc[l], div);
             }
@@ -685,8 +699,8 @@ __global__ __launch_bounds__(256, 3) void sbr_hf_kernel(SbrArgs A)
     } else {
         // band-group averages: nrg over rows (outer) and bands of the group (inner)
         for (int l = 0; l < L_E; l++) {
-            const int fl = R.f[l];
-            const int nb = fl ? T.n_hi : T.n_lo;
+            const int fl = ufl(R.f[l]);
+            const int nb = ufl(fl ? T.n_hi : T.n_lo);
             int k_l = -1, k_h = -1;
             for (int p = 0; p < nb; p++)
                 if (u >= T.f_res[fl][p] && u < T.f_res[fl][p + 1]) {
@@ -694,14 +708,14 @@ __global__ __launch_bounds__(256, 3) void sbr_hf_kernel(SbrArgs A)
                     k_h = T.f_res[fl][p + 1];
                 }
             int maxw = 0;
-            for (int p = 0; p < nb; p++) maxw = max(maxw, (int)T.f_res[fl][p + 1] - (int)T.f_res[fl][p]);
+            for (int p = 0; p < nb; p++) maxw = max(maxw, ufl((int)T.f_res[fl][p + 1] - (int)T.f_res[fl][p]));
             const int w = k_h - k_l;
             float nrg = 0.0f;
 #pragma unroll
             for (int r = 2; r < 40; r++) {
                 const float en = (xr[r] * xr[r]) + (xi[r] * xi[r]);
                 const int i = r - 2;
-                if (i >= R.t_E[l] && i < R.t_E[l + 1]) {
+                if (i >= ufl(R.t_E[l]) && i < ufl(R.t_E[l + 1])) {
                     for (int d = 0; d < maxw; d++) {
                         const float v = shfl(en, (u + d) & 63);
                         if (u == k_l && d < w) nrg += v;
@@ -857,14 +871,13 @@ __global__ __launch_bounds__(256, 3) void sbr_hf_kernel(SbrArgs A)
     {
         const int mi = band ? m : 0;
         const bool smooth = (R.flags & kSbrSmooth) != 0;
-        if (R.flags & kSbrReset) {
+        if (R.flags & kSbrReset) {  // ring positions 0..3 = the first envelope's values, position 4 (0) is written first
             const float g0 = L.gl[0][mi], q0 = L.ql[0][mi];
 #pragma unroll
-            for (int j = 0; j < 4; j++) {
+            for (int j = 1; j < 5; j++) {
                 gr[j] = g0;
                 qr[j] = q0;
             }
-            gidx = 4;
         }
         const float rev = (u & 1) ? -1.0f : 1.0f;
         if (!smooth) {
@@ -878,15 +891,15 @@ __global__ __launch_bounds__(256, 3) void sbr_hf_kernel(SbrArgs A)
                 const int i = r - 2;
                 if (i < first || i >= last) continue;
                 if (i >= next) {  // wave-uniform
-                    while (l + 1 < L_E && i >= R.t_E[l + 1]) l++;
-                    next = l + 1 < L_E ? R.t_E[l + 1] : 64;
-                    const bool no_noise = (R.no_noise >> l) & 1;
+                    while (l + 1 < L_E && i >= ufl(R.t_E[l + 1])) l++;
+                    next = l + 1 < L_E ? ufl(R.t_E[l + 1]) : 64;
+                    const bool no_noise = (ufl(R.no_noise) >> l) & 1;
                     G_filt = L.gl[l][mi];
                     S = L.sl[l][mi];
                     Q_filt = (S != 0.0f || no_noise) ? 0.0f : L.ql[l][mi];
                 }
-                const int fi = (int)((R.noise0 + (uint32_t)(i - first) * (uint32_t)M + (uint32_t)mi + 1u) & 511u);
-                const int fs = (int)((R.sine0 + (uint32_t)(i - first)) & 3u);
+                const int fi = (int)((noise0 + (uint32_t)(i - first) * (uint32_t)M + (uint32_t)mi + 1u) & 511u);
+                const int fs = (int)((sine0 + (uint32_t)(i - first)) & 3u);
                 if (band) {
                     const float2 nz = noise_s[fi];
                     float vr = G_filt * xr[r] + (Q_filt * nz.x);
@@ -908,46 +921,37 @@ __global__ __launch_bounds__(256, 3) void sbr_hf_kernel(SbrArgs A)
             const int i = r - 2;
             if (i < first || i >= last) continue;
             if (i >= next) {  // wave-uniform
-                while (l + 1 < L_E && i >= R.t_E[l + 1]) l++;
-                next = l + 1 < L_E ? R.t_E[l + 1] : 64;
-                no_noise = (R.no_noise >> l) & 1;
+                while (l + 1 < L_E && i >= ufl(R.t_E[l + 1])) l++;
+                next = l + 1 < L_E ? ufl(R.t_E[l + 1]) : 64;
+                no_noise = (ufl(R.no_noise) >> l) & 1;
                 gnew = L.gl[l][mi];
                 qnew = L.ql[l][mi];
                 S = L.sl[l][mi];
             }
 #pragma unroll
-            for (int j = 0; j < 5; j++) {
-                if (j == gidx) {
-                    gr[j] = gnew;
-                    qr[j] = qnew;
-                }
+            for (int j = 0; j < 4; j++) {
+                gr[j] = gr[j + 1];
+                qr[j] = qr[j + 1];
             }
+            gr[4] = gnew;
+            qr[4] = qnew;
             float G_filt = 0.0f, Q_filt = 0.0f;
             if (smooth && !no_noise) {
-                int ri = gidx;
+                // taps from the oldest entry (ring position GQ_ringbuf_index + 1) to this row's (A/sbr/HFAdjustment.java:188-195)
 #pragma unroll
                 for (int n = 0; n <= 4; n++) {
                     const float h = n == 0 ? 0.03183050093751f : n == 1 ? 0.11516383427084f
                                   : n == 2 ? 0.21816949906249f : n == 3 ? 0.30150283239582f : 0.33333333333333f;
-                    ri++;
-                    if (ri >= 5) ri -= 5;
-                    float gv = gr[0], qv = qr[0];
-#pragma unroll
-                    for (int j = 1; j < 5; j++)
-                        if (j == ri) {
-                            gv = gr[j];
-                            qv = qr[j];
-                        }
-                    G_filt += gv * h;
-                    Q_filt += qv * h;
+                    G_filt += gr[n] * h;
+                    Q_filt += qr[n] * h;
                 }
             } else {
                 G_filt = gnew;
                 Q_filt = qnew;
             }
             Q_filt = (S != 0.0f || no_noise) ? 0.0f : Q_filt;
-            const int fi = (int)((R.noise0 + (uint32_t)(i - first) * (uint32_t)M + (uint32_t)mi + 1u) & 511u);
-            const int fs = (int)((R.sine0 + (uint32_t)(i - first)) & 3u);
+            const int fi = (int)((noise0 + (uint32_t)(i - first) * (uint32_t)M + (uint32_t)mi + 1u) & 511u);
+            const int fs = (int)((sine0 + (uint32_t)(i - first)) & 3u);
             if (band) {
                 const float2 nz = noise_s[fi];
                 const float nr = nz.x, ni = nz.y;
@@ -960,7 +964,6 @@ __global__ __launch_bounds__(256, 3) void sbr_hf_kernel(SbrArgs A)
                 xr[r] = vr;
                 xi[r] = vi;
             }
-            gidx = gidx + 1 >= 5 ? 0 : gidx + 1;
             __builtin_amdgcn_sched_barrier(0);
         }
         }
@@ -974,7 +977,9 @@ __global__ __launch_bounds__(256, 3) void sbr_hf_kernel(SbrArgs A)
         // rows l < t_E[0] are Xsbr rows 2..7 as frame f-1 left them: its carry rows 2..7, which
         // the synthesis / PS analysis read (a later launch) with kx_prev + M_prev bands
         // (from the run's band limit up nothing is stored: no stage reads those bands, SbrRec::blim)
-        float2* xs = reinterpret_cast<float2*>(A.xsyn + (size_t)cf * 4096);
+        // (PS: straight into X_left's place, xps[f][0], which the PS analysis patches rows
+        // l < t_E[0] of; nch = 1 there)
+        float2* xs = reinterpret_cast<float2*>(A.ps ? A.xps + (size_t)cf * 8192 : A.xsyn + (size_t)cf * 4096);
         const int kcur = kx + M;
         if (u < (int)R.blim) {
 #pragma unroll
