@@ -48,6 +48,20 @@ __device__ __forceinline__ int java_round16(float s)
     return r > 32767 ? 32767 : (r < -32768 ? -32768 : r);
 }
 
+// The same as a 16-bit word pair (s16, s16), byte-swapped within each half when swap: NaN -> 0,
+// then v_cvt_rpi_i32_f32 = (int)floor(x + 0.5) evaluated exactly, which is Math.round for every
+// non-NaN float (saturating like Java's int conversion; exhaustive check on MI355X,
+// tools/probe_round.hip), and v_cvt_pk_i16_i32's int16 saturation is SampleBuffer's clamp.
+__device__ __forceinline__ uint32_t java_round16_pair(float s, bool swap)
+{
+    const float v = s != s ? 0.0f : s;
+    int i;
+    uint32_t w;
+    asm("v_cvt_rpi_i32_f32 %0, %1" : "=v"(i) : "v"(v));
+    asm("v_cvt_pk_i16_i32 %0, %1, %1" : "=v"(w) : "v"(i));
+    return swap ? __builtin_amdgcn_perm(w, w, 0x02030001u) : w;
+}
+
 __device__ __forceinline__ float java_minf(float a, float b)
 {
     if (a != a) return a;
@@ -1320,10 +1334,9 @@ __global__ __launch_bounds__(256) void sbr_synthesis_kernel(SbrArgs A)
             if (one) o[c] = v;
             else *reinterpret_cast<float2*>(o) = make_float2(v, v);
         } else {
-            uint32_t s16 = (uint32_t)(uint16_t)(int16_t)java_round16(v);
-            if (swap) s16 = ((s16 & 0xFF) << 8) | (s16 >> 8);
-            if (one) reinterpret_cast<uint16_t*>(A.pcm)[2 * n + c] = (uint16_t)s16;
-            else reinterpret_cast<uint32_t*>(A.pcm)[n] = s16 | (s16 << 16);
+            const uint32_t w = java_round16_pair(v, swap);
+            if (one) reinterpret_cast<uint16_t*>(A.pcm)[2 * n + c] = (uint16_t)w;
+            else reinterpret_cast<uint32_t*>(A.pcm)[n] = w;
         }
     };
     auto store_group = [&](const SynSrc& S, int l0, const float (&res)[kG]) {
