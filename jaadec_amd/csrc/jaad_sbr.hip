@@ -361,16 +361,13 @@ __device__ __forceinline__ void dct4_pair(const DctPairConst& K, int e, f2 xr, f
             i = ni;
         }
     }
-    // stage 5 (:326-341): pairs (i, i+1)
+    // stage 5 (:326-341): pairs (i, i+1): x + p on even lanes, p - x on odd ones, as p + (x * +-1)
+    // (a sign flip is exact and + commutes: the same binary32 results, no select)
     {
         const f2 pr = swz2<1>(r), pi = swz2<1>(i);
-        if (!(e & 1)) {
-            r = r + pr;
-            i = i + pi;
-        } else {
-            r = pr - r;
-            i = pi - i;
-        }
+        const float sg = (e & 1) ? -1.0f : 1.0f;
+        r = pr + (r * sg);
+        i = pi + (i * sg);
     }
     // post-modulation; element 16 (E_S of j == 1) has its own form
     const f2 t = (r + i) * K.t96;

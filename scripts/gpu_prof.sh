@@ -5,7 +5,7 @@ cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out/prof
 export TMPDIR=/tmp
 TAG=${1:-r1}
 CFG=${2:-2}
-B="python3 bench.py --config $CFG --no-cpu --no-e2e"
+B="python3 bench.py --config $CFG --no-cpu --no-e2e --no-host"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof/$TAG -o trace --output-format csv -- $B --steps 20 --warmup 5 > gpurun_out/prof/$TAG.bench.log 2>&1
 rc=$?; echo "trace rc=$rc" >> gpurun_out/prof/$TAG.bench.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES -d gpurun_out/prof/$TAG -o pmc1 --output-format csv -- $B --steps 3 --warmup 1 > gpurun_out/prof/$TAG.pmc1.log 2>&1
