@@ -2045,6 +2045,8 @@ static int decode_batch_pieces_launch_impl(jaad_ctx* ctx, const jaad_batch* b, v
         const uint64_t len = b->frame_begin[r + 1] - b->frame_begin[r];
         return b->frame_begin[r] + (uint32_t)(len * (uint64_t)i / (uint64_t)P);
     };
+    // per frame: ms_used words (a pair per CPE element) and SBR records (one per channel element)
+    const size_t mw = 2 * (size_t)std::max(ctx->n_cpe, 1), sw = (size_t)std::max(ctx->n_elem, 1);
     std::vector<size_t> NF(P + 1, 0);  // first frame of each piece in the pieces' concatenation
     for (int i = 0; i < P; i++) {
         size_t n = 0;
@@ -2064,13 +2066,19 @@ static int decode_batch_pieces_launch_impl(jaad_ctx* ctx, const jaad_batch* b, v
         L.cb = L.sf + al(nci * 128);
         L.ics = L.cb + al(nci * 128);
         L.ms = L.ics + al(nci * sizeof(jaad_ics_info));
-        L.tns = L.ms + (b->ms_used ? al(nfi * 16) : 0);
+        L.tns = L.ms + (b->ms_used ? al(nfi * 8 * mw) : 0);
         L.bytes = L.tns + (b->tns ? al(nci * sizeof(jaad_tns)) : 0);
         return L;
     };
     std::vector<size_t> SB(P + 1, 0);  // device input block of each piece
     for (int i = 0; i < P; i++) SB[i + 1] = SB[i] + layout(NF[i + 1] - NF[i]).bytes;
-    HIPCHK(ctx->d_batch.ensure(SB[P] + 256));
+    // coupling batches (run-aligned pieces): the CCE records once, after the pieces' blocks; each
+    // piece gets its frames' terms, renumbered to the piece
+    const size_t nce = b->n_cce_terms ? b->n_cce : 0;
+    const size_t o_cq = al(SB[P]), o_csf = al(o_cq + nce * 2048), o_ccb = al(o_csf + nce * 128);
+    const size_t o_cics = al(o_ccb + nce * 128), in_bytes = al(o_cics + nce * sizeof(jaad_ics_info));
+    if (nce && !run0) return JAAD_ERR_UNSUPPORTED;  // (time slices: decode_batch_whole keeps these serial)
+    HIPCHK(ctx->d_batch.ensure(in_bytes + 256));
     HIPCHK(ctx->d_pcm.ensure(fbytes * NF[P] + 256));
     char* base = static_cast<char*>(ctx->d_batch.p);
     char* dpcm = static_cast<char*>(ctx->d_pcm.p);
@@ -2114,6 +2122,17 @@ static int decode_batch_pieces_launch_impl(jaad_ctx* ctx, const jaad_batch* b, v
     std::vector<uint32_t> pslot, pbeg, prun;  // runs with frames in the piece: slot, first frame, batch run
     std::vector<jaad_sbr_frame> psbr;
     std::vector<uint8_t> pstat;
+    std::vector<jaad_cce_term> pterms;
+    if (nce) {  // the CCE records get the channel records' checks (as decode_batch_serial), then one copy
+        jaad_batch cb = *b;
+        cb.ics = b->cce_ics;
+        cb.tns = nullptr;
+        if (!side_info_ok(ctx, &cb, 0, b->n_cce) || !q_ok_copy(b->cce_q, nullptr, nce * 1024)) return JAAD_ERR_BITSTREAM;
+        HIPCHK(hipMemcpyAsync(base + o_cq, b->cce_q, nce * 2048, hipMemcpyHostToDevice, ctx->h2d));
+        HIPCHK(hipMemcpyAsync(base + o_csf, b->cce_sf, nce * 128, hipMemcpyHostToDevice, ctx->h2d));
+        HIPCHK(hipMemcpyAsync(base + o_ccb, b->cce_cb, nce * 128, hipMemcpyHostToDevice, ctx->h2d));
+        HIPCHK(hipMemcpyAsync(base + o_cics, b->cce_ics, nce * sizeof(jaad_ics_info), hipMemcpyHostToDevice, ctx->h2d));
+    }
     auto piece_runs = [&](int i, std::vector<uint32_t>& runs, std::vector<uint32_t>& beg) {
         runs.clear();
         beg.assign(1, 0);
@@ -2170,7 +2189,7 @@ static int decode_batch_pieces_launch_impl(jaad_ctx* ctx, const jaad_batch* b, v
                 std::memcpy(st + L.sf + oc * 128, b->sf + c0 * 128, nc * 128);
                 std::memcpy(st + L.cb + oc * 128, b->cb + c0 * 128, nc * 128);
                 std::memcpy(st + L.ics + oc * sizeof(jaad_ics_info), b->ics + c0, nc * sizeof(jaad_ics_info));
-                if (b->ms_used) std::memcpy(st + L.ms + o * 16, b->ms_used + a * 2, n * 16);
+                if (b->ms_used) std::memcpy(st + L.ms + o * 8 * mw, b->ms_used + a * mw, n * 8 * mw);
                 if (b->tns) std::memcpy(st + L.tns + oc * sizeof(jaad_tns), b->tns + c0, nc * sizeof(jaad_tns));
             }
         });
@@ -2207,13 +2226,13 @@ static int decode_batch_pieces_launch_impl(jaad_ctx* ctx, const jaad_batch* b, v
         pslot.resize(prun.size());
         for (size_t k = 0; k < prun.size(); k++) pslot[k] = b->stream_slot[prun[k]];
         if (b->sbr || b->frame_status) {  // host-side per-frame arrays of the piece
-            if (b->sbr) psbr.resize(nfi);
+            if (b->sbr) psbr.resize(nfi * sw);
             if (b->frame_status) pstat.resize(nfi);
             const size_t nr = prun.size();
             io.run([&](int t) {
                 for (size_t k = nr * t / W; k < nr * (t + 1) / W; k++) {
                     const size_t a = cut(prun[k], i), n = pbeg[k + 1] - pbeg[k];
-                    if (b->sbr) std::memcpy(&psbr[pbeg[k]], b->sbr + a, n * sizeof(jaad_sbr_frame));
+                    if (b->sbr) std::memcpy(&psbr[pbeg[k] * sw], b->sbr + a * sw, n * sw * sizeof(jaad_sbr_frame));
                     if (b->frame_status) std::memcpy(&pstat[pbeg[k]], b->frame_status + a, n);
                 }
             });
@@ -2231,6 +2250,21 @@ static int decode_batch_pieces_launch_impl(jaad_ctx* ctx, const jaad_batch* b, v
         pb.tns = b->tns ? reinterpret_cast<const jaad_tns*>(blk + L.tns) : nullptr;
         pb.sbr = b->sbr ? psbr.data() : nullptr;
         pb.frame_status = b->frame_status ? pstat.data() : nullptr;
+        if (nce) {  // the piece's terms (terms are sorted by frame; a run-aligned piece is one frame range)
+            const uint32_t f0 = b->frame_begin[(*run0)[i]], f1 = b->frame_begin[(*run0)[i + 1]];
+            const jaad_cce_term* t0 = std::lower_bound(b->cce_terms, b->cce_terms + b->n_cce_terms, f0,
+                                                       [](const jaad_cce_term& T, uint32_t f) { return T.frame < f; });
+            const jaad_cce_term* t1 = std::lower_bound(t0, b->cce_terms + b->n_cce_terms, f1,
+                                                       [](const jaad_cce_term& T, uint32_t f) { return T.frame < f; });
+            pterms.assign(t0, t1);
+            for (jaad_cce_term& T : pterms) T.frame -= f0;
+            pb.n_cce_terms = (uint32_t)pterms.size();
+            pb.cce_terms = pterms.data();
+            pb.cce_q = reinterpret_cast<const int16_t*>(base + o_cq);
+            pb.cce_sf = reinterpret_cast<const uint8_t*>(base + o_csf);
+            pb.cce_cb = reinterpret_cast<const uint8_t*>(base + o_ccb);
+            pb.cce_ics = reinterpret_cast<const jaad_ics_info*>(base + o_cics);
+        }
         // piece i's launch first (its SBR records go to the H2D stream now, ahead of piece i+1's
         // inputs), then piece i+1's gather and copy while piece i's kernels run
         HIPCHK(hipStreamWaitEvent(s, ctx->ev_in[i], 0));
@@ -2336,7 +2370,10 @@ static int decode_batch_whole(jaad_ctx* ctx, const jaad_batch* b, void* pcm_out,
     int rc;
     HIPCHK(hipSetDevice(ctx->device));
     if ((rc = io_setup(ctx))) return rc;
-    if (ctx->n_elem > 1 || b->n_cce_terms || b->n_frames < 2 * kMinPieceFrames || !b->stream_slot || !b->frame_begin)
+    // (multichannel HE-AAC: its elements' child contexts hold SBR state the pieces' roll-back does
+    // not cover; coupling with PS: time slices would split the term list)
+    if ((ctx->n_elem > 1 && ctx->cfg.sbr) || (b->n_cce_terms && ctx->cfg.ps) || b->n_frames < 2 * kMinPieceFrames ||
+        !b->stream_slot || !b->frame_begin)
         return decode_batch_serial(ctx, b, pcm_out, flags);
     // the run layout is checked by plan(); pieces need it sane before cutting
     if (b->frame_begin[0] != 0 || b->frame_begin[b->n_runs] != b->n_frames) return JAAD_ERR_INVALID_ARG;
@@ -2348,7 +2385,7 @@ static int decode_batch_whole(jaad_ctx* ctx, const jaad_batch* b, void* pcm_out,
         if (P < 2) return decode_batch_serial(ctx, b, pcm_out, flags);
         return decode_batch_pieces_launch(ctx, b, pcm_out, flags, (int)P, nullptr);
     }
-    if (ctx->cfg.sbr || b->frame_status) {  // run-aligned pieces through launch()
+    if (ctx->cfg.sbr || b->frame_status || ctx->n_elem > 1 || b->n_cce_terms) {  // run-aligned pieces through launch()
         const std::vector<uint32_t> run0 = cut_pieces(b);
         if (run0.size() <= 2) return decode_batch_serial(ctx, b, pcm_out, flags);
         return decode_batch_pieces_launch(ctx, b, pcm_out, flags, (int)run0.size() - 1, &run0);

@@ -248,3 +248,85 @@ def test_sbr_bad_piece_rolls_the_call_back(what):
     fb = b.frame_begin
     for r in range(64):
         assert (g2[80 * r:80 * (r + 1)] == want[fb[r] + 80:fb[r + 1]]).all(), r
+
+
+# ------------------------------------------------------------------------------------------------
+# multichannel AAC-LC and coupling batches through the pipelined host entry (VERDICT r4 missing #4)
+# ------------------------------------------------------------------------------------------------
+
+def _mc_device_decode(cfg, b, n_slots, flags):
+    """The device entry for a multichannel batch (PCM: out_channels(cfg) channels a sample)."""
+    dev = torch.device("cuda", 0)
+    t = lambda a: None if a is None else torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1)).to(dev)
+    d = {k: t(getattr(b, k)) for k in ("q", "sf", "cb", "ics", "ms_used", "tns")}
+    ptr = {k: (v.data_ptr() if v is not None else None) for k, v in d.items()}
+    nb = 1024 * N.out_channels(cfg) * (4 if flags & N.PCM_FLOAT32 else 2)
+    pcm = torch.empty(b.n_frames * nb, dtype=torch.uint8, device=dev)
+    with N.Context(cfg, n_slots) as ctx:
+        ctx.decode_device(ptr, b, pcm.data_ptr(), pcm.numel(), flags)
+        ctx.wait()
+    return pcm.cpu().numpy().reshape(b.n_frames, nb)
+
+
+@pytest.mark.parametrize("cc", [6, 7])
+def test_multichannel_pieces_pipeline(cc):
+    """5.1 / 7.1 AAC-LC batches large enough for pieces: the pipelined host entry == the device
+    entry over the whole batch and == the restatement on a sample of streams; a second call
+    continues every stream."""
+    from tests.test_multichannel import mc_synth, IDS
+    b = mc_synth(cc, n_streams=16, fps=320, seed=4)  # 5 120 frames: 2 pieces
+    cfg = N.make_cfg(channel_config=cc)
+    first, second = b.split_frames(200)
+    with N.Context(cfg, 16) as ctx:
+        g1 = ctx.decode(first)
+        g2 = ctx.decode(second)
+    want = _mc_device_decode(cfg, b, 16, N.PCM_BIG_ENDIAN)
+    fb = b.frame_begin
+    for r in range(16):
+        assert (g1[200 * r:200 * (r + 1)] == want[fb[r]:fb[r] + 200]).all(), r
+        assert (g2[120 * r:120 * (r + 1)] == want[fb[r] + 200:fb[r + 1]]).all(), r
+    sub = b.select_runs([0, 15])
+    o = O.decode_batch_mc(3, sub, IDS[cc], N.PCM_BIG_ENDIAN, threads=8)
+    assert (np.concatenate([want[fb[r]:fb[r + 1]] for r in (0, 15)]) == o).all()
+
+
+def test_multichannel_bad_piece_rolls_back():
+    from tests.test_multichannel import mc_synth
+    b = mc_synth(6, n_streams=16, fps=320, seed=5)
+    cfg = N.make_cfg(channel_config=6)
+    half, rest = b.split_frames(160)
+    with N.Context(cfg, 16) as ctx:
+        ctx.decode(half)
+        before = [ctx.state_export(s) for s in range(16)]
+        bad = rest.select_runs(range(16))
+        bad.q[-1, 3] = 9000  # the last piece
+        with pytest.raises(N.JaadError) as e:
+            ctx.decode(bad)
+        assert e.value.status == N.ERR_BITSTREAM
+        assert all((ctx.state_export(s) == before[s]).all() for s in range(16))
+
+
+@pytest.mark.parametrize("cc,sbr", [(2, False), (2, True), (6, False)])
+def test_coupling_pieces_pipeline(cc, sbr):
+    """Coupling batches as run-aligned pieces: each piece gets its frames' terms, renumbered; the
+    CCE records are uploaded once.  == the restatement (stereo LC over the whole batch; HE-AAC and
+    5.1 on a sample of streams)."""
+    from tests.test_cce import coupled_batch, coupled_sbr_batch
+    from tests.test_multichannel import IDS
+    if sbr:
+        b = coupled_sbr_batch(cc, n_streams=16, fps=300, seed=61)
+        cfg = N.make_cfg(sf_index=6, channel_config=cc, sbr=True)
+    else:
+        b = coupled_batch(cc, n_streams=16, fps=300, seed=62)
+        cfg = N.make_cfg(channel_config=cc)
+    assert len(b.cce_terms) > 1000
+    with N.Context(cfg, 16) as ctx:
+        got = ctx.decode(b, N.PCM_BIG_ENDIAN)
+    runs = (0, 7, 15)
+    sub = b.select_runs(list(runs))
+    if cc in N.MC_ELEMENTS:
+        want = O.decode_batch_mc(3, sub, IDS[cc], N.PCM_BIG_ENDIAN, threads=8)
+    else:
+        want = O.decode_batch(cfg, sub, O.Streams(16), N.PCM_BIG_ENDIAN, threads=8)
+    fb = b.frame_begin
+    assert (np.concatenate([got[fb[r]:fb[r + 1]] for r in runs]) == want).all()
