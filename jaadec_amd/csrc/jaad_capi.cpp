@@ -2032,9 +2032,36 @@ static int decode_batch_pieces_impl(jaad_ctx* ctx, const jaad_batch* b, void* pc
 // piece that fails a check or whose SBR records are refused puts them all back.  (The reference
 // decodes frame by frame, A/Decoder.java:103-121; multichannel and coupling batches keep the serial
 // path.)
+// The device state of every slot of a context (and of its elements' child contexts: multichannel
+// HE-AAC), copied aside before the first piece's kernels so that a failing piece rolls the whole call
+// back: core overlap (the current parity), SBR and PS slot state, and the host-side SBR slot records.
+struct StateSnap {
+    jaad_ctx* c;
+    int parity;
+    size_t lc_b, sbr_b, ps_b, off;  // bytes of each part; offset of the context's parts in d_backup
+    std::vector<SbrHostSlot> host;
+};
+static std::vector<StateSnap> state_snaps(jaad_ctx* ctx)
+{
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    std::vector<StateSnap> v;
+    size_t off = 0;
+    auto add = [&](jaad_ctx* c) {
+        // (a multichannel HE-AAC parent holds no SBR state of its own: its children do)
+        StateSnap S{c, c->parity, c->d_state[c->parity] ? (size_t)c->n_elem * c->n_slots * 2048 * sizeof(float) : 0,
+                    c->cfg.sbr && c->d_sbr_state ? (size_t)c->n_slots * 2 * sizeof(SbrChState) : 0,
+                    c->cfg.ps && c->d_ps_state ? (size_t)c->n_slots * sizeof(PsState) : 0, off, {}};
+        off += al(S.lc_b) + al(S.sbr_b) + al(S.ps_b);
+        v.push_back(std::move(S));
+    };
+    add(ctx);
+    for (jaad_ctx* c : ctx->children) add(c);
+    return v;
+}
+
 static int decode_batch_pieces_launch_impl(jaad_ctx* ctx, const jaad_batch* b, void* pcm_out, uint32_t flags, int P,
-                                           const std::vector<uint32_t>* run0, std::vector<SbrHostSlot>& host_saved,
-                                           int& parity0, bool& saved)
+                                           const std::vector<uint32_t>* run0, std::vector<StateSnap>& snaps,
+                                           bool& saved)
 {
     const int nch = ctx->nch;
     const uint32_t R = b->n_runs;
@@ -2086,16 +2113,16 @@ static int decode_batch_pieces_launch_impl(jaad_ctx* ctx, const jaad_batch* b, v
     if (ctx->done_live && ctx->last_stream != s) HIPCHK(hipStreamWaitEvent(s, ctx->done, 0));
 
     // roll-back copies, queued ahead of every kernel of the call
-    const size_t lc_b = (size_t)ctx->n_elem * ctx->n_slots * 2048 * sizeof(float);
-    const size_t sbr_b = ctx->cfg.sbr ? (size_t)ctx->n_slots * 2 * sizeof(SbrChState) : 0;
-    const size_t ps_b = ctx->cfg.ps ? (size_t)ctx->n_slots * sizeof(PsState) : 0;
-    HIPCHK(ctx->d_backup.ensure(al(lc_b) + al(sbr_b) + ps_b + 256));
+    snaps = state_snaps(ctx);
+    HIPCHK(ctx->d_backup.ensure(snaps.back().off + al(snaps.back().lc_b) + al(snaps.back().sbr_b) + snaps.back().ps_b + 256));
     char* bk = static_cast<char*>(ctx->d_backup.p);
-    parity0 = ctx->parity;
-    HIPCHK(hipMemcpyAsync(bk, ctx->d_state[parity0], lc_b, hipMemcpyDeviceToDevice, s));
-    if (sbr_b) HIPCHK(hipMemcpyAsync(bk + al(lc_b), ctx->d_sbr_state, sbr_b, hipMemcpyDeviceToDevice, s));
-    if (ps_b) HIPCHK(hipMemcpyAsync(bk + al(lc_b) + al(sbr_b), ctx->d_ps_state, ps_b, hipMemcpyDeviceToDevice, s));
-    host_saved = ctx->sbr_slots;
+    for (StateSnap& S : snaps) {
+        char* o = bk + S.off;
+        if (S.lc_b) HIPCHK(hipMemcpyAsync(o, S.c->d_state[S.parity], S.lc_b, hipMemcpyDeviceToDevice, s));
+        if (S.sbr_b) HIPCHK(hipMemcpyAsync(o + al(S.lc_b), S.c->d_sbr_state, S.sbr_b, hipMemcpyDeviceToDevice, s));
+        if (S.ps_b) HIPCHK(hipMemcpyAsync(o + al(S.lc_b) + al(S.sbr_b), S.c->d_ps_state, S.ps_b, hipMemcpyDeviceToDevice, s));
+        S.host = S.c->sbr_slots;
+    }
     saved = true;
 
     // Runs of one length L laid out back to back (the usual batch): a piece is then R rows of one
@@ -2305,27 +2332,28 @@ static int decode_batch_pieces_launch_impl(jaad_ctx* ctx, const jaad_batch* b, v
 static int decode_batch_pieces_launch(jaad_ctx* ctx, const jaad_batch* b, void* pcm_out, uint32_t flags, int P,
                                       const std::vector<uint32_t>* run0)
 {
-    std::vector<SbrHostSlot> host_saved;
-    int parity0 = ctx->parity;
+    std::vector<StateSnap> snaps;
     bool saved = false;
     ctx->rec_stream = ctx->h2d;
-    const int rc = decode_batch_pieces_launch_impl(ctx, b, pcm_out, flags, P, run0, host_saved, parity0, saved);
+    for (jaad_ctx* c : ctx->children) c->rec_stream = ctx->h2d;
+    const int rc = decode_batch_pieces_launch_impl(ctx, b, pcm_out, flags, P, run0, snaps, saved);
     ctx->rec_stream = nullptr;
+    for (jaad_ctx* c : ctx->children) c->rec_stream = nullptr;
     if (rc) {
         for (hipStream_t st : {ctx->h2d, ctx->d2h, ctx->stream})
             if (st) (void)hipStreamSynchronize(st);
         (void)hipGetLastError();
-        if (saved) {  // every slot back to the state it had when the call started
+        if (saved) {  // every slot (of every element context) back to the state it had when the call started
             auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-            const size_t lc_b = (size_t)ctx->n_elem * ctx->n_slots * 2048 * sizeof(float);
-            const size_t sbr_b = ctx->cfg.sbr ? (size_t)ctx->n_slots * 2 * sizeof(SbrChState) : 0;
-            const size_t ps_b = ctx->cfg.ps ? (size_t)ctx->n_slots * sizeof(PsState) : 0;
             const char* bk = static_cast<const char*>(ctx->d_backup.p);
-            ctx->parity = parity0;
-            (void)hipMemcpy(ctx->d_state[parity0], bk, lc_b, hipMemcpyDeviceToDevice);
-            if (sbr_b) (void)hipMemcpy(ctx->d_sbr_state, bk + al(lc_b), sbr_b, hipMemcpyDeviceToDevice);
-            if (ps_b) (void)hipMemcpy(ctx->d_ps_state, bk + al(lc_b) + al(sbr_b), ps_b, hipMemcpyDeviceToDevice);
-            ctx->sbr_slots.swap(host_saved);
+            for (StateSnap& S : snaps) {
+                const char* o = bk + S.off;
+                S.c->parity = S.parity;
+                if (S.lc_b) (void)hipMemcpy(S.c->d_state[S.parity], o, S.lc_b, hipMemcpyDeviceToDevice);
+                if (S.sbr_b) (void)hipMemcpy(S.c->d_sbr_state, o + al(S.lc_b), S.sbr_b, hipMemcpyDeviceToDevice);
+                if (S.ps_b) (void)hipMemcpy(S.c->d_ps_state, o + al(S.lc_b) + al(S.sbr_b), S.ps_b, hipMemcpyDeviceToDevice);
+                S.c->sbr_slots.swap(S.host);
+            }
             (void)hipDeviceSynchronize();
         }
     }
@@ -2370,9 +2398,8 @@ static int decode_batch_whole(jaad_ctx* ctx, const jaad_batch* b, void* pcm_out,
     int rc;
     HIPCHK(hipSetDevice(ctx->device));
     if ((rc = io_setup(ctx))) return rc;
-    // (multichannel HE-AAC: its elements' child contexts hold SBR state the pieces' roll-back does
-    // not cover; coupling with PS: time slices would split the term list)
-    if ((ctx->n_elem > 1 && ctx->cfg.sbr) || (b->n_cce_terms && ctx->cfg.ps) || b->n_frames < 2 * kMinPieceFrames ||
+    // (coupling with PS: time slices would split the term list)
+    if ((b->n_cce_terms && ctx->cfg.ps) || b->n_frames < 2 * kMinPieceFrames ||
         !b->stream_slot || !b->frame_begin)
         return decode_batch_serial(ctx, b, pcm_out, flags);
     // the run layout is checked by plan(); pieces need it sane before cutting

@@ -330,3 +330,28 @@ def test_coupling_pieces_pipeline(cc, sbr):
         want = O.decode_batch(cfg, sub, O.Streams(16), N.PCM_BIG_ENDIAN, threads=8)
     fb = b.frame_begin
     assert (np.concatenate([got[fb[r]:fb[r + 1]] for r in runs]) == want).all()
+
+
+def test_multichannel_he_aac_pieces_and_roll_back():
+    """5.1 HE-AAC (one SBR child context per element) through the pipelined entry: two calls ==
+    the restatement on every stream; then a call whose last piece fails puts every element's core
+    and SBR state back (the good call after it continues the streams exactly)."""
+    from tests.test_mc_sbr import mc_sbr_synth, IDS
+    b = mc_sbr_synth(6, n_streams=24, fps=300, seed=21)
+    cfg = N.make_cfg(sf_index=6, channel_config=6, sbr=True)
+    want = O.decode_batch_mc(6, b, IDS[6], N.PCM_BIG_ENDIAN, threads=8, sbr=True)
+    first, second = b.split_frames(120)  # 2 880 frames (one launch), then 4 320 (2 pieces)
+    fb = b.frame_begin
+    with N.Context(cfg, 24) as ctx:
+        g1 = ctx.decode(first)
+        before = [ctx.state_export(s) for s in range(24)]
+        bad = second.select_runs(range(24))
+        bad.q[-1, 5] = 9000  # in the last piece
+        with pytest.raises(N.JaadError) as e:
+            ctx.decode(bad)
+        assert e.value.status == N.ERR_BITSTREAM
+        assert all((ctx.state_export(s) == before[s]).all() for s in range(24))
+        g2 = ctx.decode(second)
+    for r in range(24):
+        assert (g1[120 * r:120 * (r + 1)] == want[fb[r]:fb[r] + 120]).all(), r
+        assert (g2[180 * r:180 * (r + 1)] == want[fb[r] + 120:fb[r + 1]]).all(), r
