@@ -2099,12 +2099,11 @@ static int decode_batch_pieces_launch_impl(jaad_ctx* ctx, const jaad_batch* b, v
     };
     std::vector<size_t> SB(P + 1, 0);  // device input block of each piece
     for (int i = 0; i < P; i++) SB[i + 1] = SB[i] + layout(NF[i + 1] - NF[i]).bytes;
-    // coupling batches (run-aligned pieces): the CCE records once, after the pieces' blocks; each
-    // piece gets its frames' terms, renumbered to the piece
+    // coupling batches: the CCE records once, after the pieces' blocks; each piece gets its frames'
+    // terms, renumbered to the piece
     const size_t nce = b->n_cce_terms ? b->n_cce : 0;
     const size_t o_cq = al(SB[P]), o_csf = al(o_cq + nce * 2048), o_ccb = al(o_csf + nce * 128);
     const size_t o_cics = al(o_ccb + nce * 128), in_bytes = al(o_cics + nce * sizeof(jaad_ics_info));
-    if (nce && !run0) return JAAD_ERR_UNSUPPORTED;  // (time slices: decode_batch_whole keeps these serial)
     HIPCHK(ctx->d_batch.ensure(in_bytes + 256));
     HIPCHK(ctx->d_pcm.ensure(fbytes * NF[P] + 256));
     char* base = static_cast<char*>(ctx->d_batch.p);
@@ -2277,14 +2276,19 @@ static int decode_batch_pieces_launch_impl(jaad_ctx* ctx, const jaad_batch* b, v
         pb.tns = b->tns ? reinterpret_cast<const jaad_tns*>(blk + L.tns) : nullptr;
         pb.sbr = b->sbr ? psbr.data() : nullptr;
         pb.frame_status = b->frame_status ? pstat.data() : nullptr;
-        if (nce) {  // the piece's terms (terms are sorted by frame; a run-aligned piece is one frame range)
-            const uint32_t f0 = b->frame_begin[(*run0)[i]], f1 = b->frame_begin[(*run0)[i + 1]];
-            const jaad_cce_term* t0 = std::lower_bound(b->cce_terms, b->cce_terms + b->n_cce_terms, f0,
-                                                       [](const jaad_cce_term& T, uint32_t f) { return T.frame < f; });
-            const jaad_cce_term* t1 = std::lower_bound(t0, b->cce_terms + b->n_cce_terms, f1,
-                                                       [](const jaad_cce_term& T, uint32_t f) { return T.frame < f; });
-            pterms.assign(t0, t1);
-            for (jaad_cce_term& T : pterms) T.frame -= f0;
+        if (nce) {  // the piece's terms: each run's slice of frames, renumbered (terms are sorted by frame)
+            pterms.clear();
+            auto at = [&](uint32_t f) {
+                return std::lower_bound(b->cce_terms, b->cce_terms + b->n_cce_terms, f,
+                                        [](const jaad_cce_term& T, uint32_t v) { return T.frame < v; });
+            };
+            for (size_t k = 0; k < prun.size(); k++) {
+                const uint32_t a = cut(prun[k], i), e = cut(prun[k], i + 1);
+                for (const jaad_cce_term* t = at(a); t < b->cce_terms + b->n_cce_terms && t->frame < e; t++) {
+                    pterms.push_back(*t);
+                    pterms.back().frame = pbeg[k] + (t->frame - a);
+                }
+            }
             pb.n_cce_terms = (uint32_t)pterms.size();
             pb.cce_terms = pterms.data();
             pb.cce_q = reinterpret_cast<const int16_t*>(base + o_cq);
@@ -2398,8 +2402,7 @@ static int decode_batch_whole(jaad_ctx* ctx, const jaad_batch* b, void* pcm_out,
     int rc;
     HIPCHK(hipSetDevice(ctx->device));
     if ((rc = io_setup(ctx))) return rc;
-    // (coupling with PS: time slices would split the term list)
-    if ((b->n_cce_terms && ctx->cfg.ps) || b->n_frames < 2 * kMinPieceFrames ||
+    if (b->n_frames < 2 * kMinPieceFrames ||
         !b->stream_slot || !b->frame_begin)
         return decode_batch_serial(ctx, b, pcm_out, flags);
     // the run layout is checked by plan(); pieces need it sane before cutting

@@ -355,3 +355,30 @@ def test_multichannel_he_aac_pieces_and_roll_back():
     for r in range(24):
         assert (g1[120 * r:120 * (r + 1)] == want[fb[r]:fb[r] + 120]).all(), r
         assert (g2[180 * r:180 * (r + 1)] == want[fb[r] + 120:fb[r + 1]]).all(), r
+
+
+def test_coupling_with_ps_time_slices():
+    """An HE-AAC v2 batch with coupling terms through the time-sliced pipeline: each slice gets its
+    runs' terms, renumbered; == the restatement on a sample of streams."""
+    from tests.test_cce import cce_records
+    p = N.synth_params(5, n_streams=16, frames_per_stream=300)
+    b = N.synth_batch(p)
+    cfg = N.cfg_for(p)
+    rng = np.random.default_rng(71)
+    n_rec = 64
+    b.cce_q, b.cce_sf, b.cce_cb, b.cce_ics = cce_records(n_rec, 71, pns=10, sf_index=p.sf_index)
+    terms = []
+    for f in range(b.n_frames):
+        if rng.integers(3):
+            continue
+        t = np.zeros((), N.CCE_TERM_DTYPE)
+        t["frame"], t["channel"], t["point"], t["cce"] = f, 0, rng.integers(2), rng.integers(n_rec)
+        t["gain"] = rng.choice([0.0, 1.0, -0.5, 2.0, 1.0905077], 120).astype(np.float32)
+        terms.append(t)
+    b.cce_terms = np.array(terms, N.CCE_TERM_DTYPE)
+    with N.Context(cfg, 16) as ctx:
+        got = ctx.decode(b, N.PCM_BIG_ENDIAN)
+    runs = (0, 9, 15)
+    want = O.decode_batch(cfg, b.select_runs(list(runs)), O.Streams(16), N.PCM_BIG_ENDIAN, threads=8)
+    fb = b.frame_begin
+    assert (np.concatenate([got[fb[r]:fb[r + 1]] for r in runs]) == want).all()
