@@ -593,7 +593,7 @@ __global__ __launch_bounds__(256, 3) void sbr_hf_kernel(SbrArgs A)
     // overwrites (ring position GQ_ringbuf_index = gq0), gr[4] the newest; each row shifts it by one
     // and appends, so its five filter taps are gr[0..4] in order -- compile-time registers instead
     // of a select over the ring per tap (positions read rotated once here, gq0 wave-uniform).
-    float gr[5] = {0, 0, 0, 0, 0}, qr[5] = {0, 0, 0, 0, 0};
+    f2 gq[5] = {};  // (G, Q) pairs: the smoothing filter runs packed
     const int gq0 = ufl(R.gq0);
     if ((P == 2 || (P == 3 && A.smoothing)) && !(R.flags & kSbrReset)) {
         const float* ring = R.first ? &A.state[(size_t)R.slot * 2 + c].gq[0][0][0] : A.gq + (size_t)(cf - A.nch) * 640;
@@ -601,13 +601,12 @@ __global__ __launch_bounds__(256, 3) void sbr_hf_kernel(SbrArgs A)
 #pragma unroll
         for (int j = 0; j < 5; j++) {
             const int pj = (gq0 + j) % 5;
-            gr[j] = ring[pj * 64 + mm];
-            qr[j] = ring[320 + pj * 64 + mm];
+            gq[j] = f2{ring[pj * 64 + mm], ring[320 + pj * 64 + mm]};
         }
         if (A.dbg && cf == 2)
             for (int j = 0; j < 5; j++) {
-                A.dbg[((gq0 + j) % 5) * 64 + u] = gr[j];
-                A.dbg[320 + ((gq0 + j) % 5) * 64 + u] = qr[j];
+                A.dbg[((gq0 + j) % 5) * 64 + u] = gq[j].x;
+                A.dbg[320 + ((gq0 + j) % 5) * 64 + u] = gq[j].y;
             }
     }
 
@@ -886,8 +885,7 @@ __global__ __launch_bounds__(256, 3) void sbr_hf_kernel(SbrArgs A)
             const float g0 = L.gl[0][mi], q0 = L.ql[0][mi];
 #pragma unroll
             for (int j = 1; j < 5; j++) {
-                gr[j] = g0;
-                qr[j] = q0;
+                gq[j] = f2{g0, q0};
             }
         }
         const float rev = (u & 1) ? -1.0f : 1.0f;
@@ -941,21 +939,22 @@ __global__ __launch_bounds__(256, 3) void sbr_hf_kernel(SbrArgs A)
             }
 #pragma unroll
             for (int j = 0; j < 4; j++) {
-                gr[j] = gr[j + 1];
-                qr[j] = qr[j + 1];
+                gq[j] = gq[j + 1];
             }
-            gr[4] = gnew;
-            qr[4] = qnew;
+            gq[4] = f2{gnew, qnew};
             float G_filt = 0.0f, Q_filt = 0.0f;
             if (smooth && !no_noise) {
-                // taps from the oldest entry (ring position GQ_ringbuf_index + 1) to this row's (A/sbr/HFAdjustment.java:188-195)
+                // taps from the oldest entry (ring position GQ_ringbuf_index + 1) to this row's
+                // (A/sbr/HFAdjustment.java:188-195), G and Q in one packed accumulator
+                f2 acc = f2{0.0f, 0.0f};
 #pragma unroll
                 for (int n = 0; n <= 4; n++) {
                     const float h = n == 0 ? 0.03183050093751f : n == 1 ? 0.11516383427084f
                                   : n == 2 ? 0.21816949906249f : n == 3 ? 0.30150283239582f : 0.33333333333333f;
-                    G_filt += gr[n] * h;
-                    Q_filt += qr[n] * h;
+                    acc += gq[n] * h;
                 }
+                G_filt = acc.x;
+                Q_filt = acc.y;
             } else {
                 G_filt = gnew;
                 Q_filt = qnew;
