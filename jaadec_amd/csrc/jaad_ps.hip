@@ -137,8 +137,12 @@ __device__ __forceinline__ float2 hyb_history_after(const SbrArgs& A, uint32_t f
                  : reinterpret_cast<const float2*>(A.xcarry + (size_t)f * kSbrCarryFloats)[(i - 4) * 64 + b];
 }
 
+// (rows transposed through LDS: the hybrid analysis reads bands 0..2 of rows 0..37, the band
+// energies |X|^2 of rows 0..31 -- stored as energies, not complex rows, so four waves fit a CU's
+// LDS per block and four blocks a CU instead of two)
 struct AnaLds {
-    float2 xl[38][65];
+    float2 xl3[38][3];
+    float en[32][65];
     float2 hist[3][12];
 };
 
@@ -172,15 +176,19 @@ __global__ __launch_bounds__(256) void ps_analysis_kernel(SbrArgs A)
             v[l] = ok ? t : make_float2(0.0f, 0.0f);
         }
 #pragma unroll
-        for (int l = 0; l < 32; l++) L.xl[l][u] = v[l];
+        for (int l = 0; l < 32; l++) {
+            L.en[l][u] = (v[l].x * v[l].x) + (v[l].y * v[l].y);
+            if (u < 3) L.xl3[l][u] = v[l];
+        }
         if (u < K)
 #pragma unroll
             for (int l = 0; l < 32; l++)
                 if (l < t0) xo[l * 64 + u] = v[l];
         // a frame without PS data only hands its X (qmfs0 input) to the synthesis
         if (!ps_on) return;
+        if (u < 3)
 #pragma unroll
-        for (int l = 32; l < 38; l++) L.xl[l][u] = v[l];
+            for (int l = 32; l < 38; l++) L.xl3[l][u] = v[l];
         if (u < 36) {
             // Filterbank.buffer as the previous PS frame left it (frames without PS data do not
             // run the hybrid analysis)
@@ -205,7 +213,7 @@ __global__ __launch_bounds__(256) void ps_analysis_kernel(SbrArgs A)
 #pragma unroll
             for (int i = 0; i < 13; i++) {
                 const int w = n + i;  // work[w]: history (w < 12) or X_left[w - 6]
-                b[i] = w < 12 ? L.hist[band][w] : L.xl[w - 6][band];
+                b[i] = w < 12 ? L.hist[band][w] : L.xl3[w - 6][band];
             }
             if (band == 0) filter8(b, K.p8, hy);
             else filter2(b, K.p2, hy + 6 + 2 * band);
@@ -226,10 +234,7 @@ __global__ __launch_bounds__(256) void ps_analysis_kernel(SbrArgs A)
             P[bk] += (v.x * v.x) + (v.y * v.y);
         } else {
 #pragma unroll
-            for (int sb = kBorder[gr]; sb < kBorder[gr + 1]; sb++) {
-                const float2 v = L.xl[n][sb];
-                P[bk] += (v.x * v.x) + (v.y * v.y);
-            }
+            for (int sb = kBorder[gr]; sb < kBorder[gr + 1]; sb++) P[bk] += L.en[n][sb];
         }
     }
     float* pg = A.pg + (size_t)f * 640 + n * 20;
