@@ -128,19 +128,20 @@ JNIEXPORT void JNICALL Java_net_sourceforge_jaad_aac_gpu_GpuDSP_nativeDecode(
 
 /* static native void nativeDecodeCoupled(long h, int nFrames, int nRuns, int nch, ByteBuffer streamSlot,
  *     ByteBuffer frameBegin, ByteBuffer q, ByteBuffer sf, ByteBuffer cb, ByteBuffer ics,
- *     ByteBuffer msUsed, ByteBuffer tns, ByteBuffer pcm, int flags, int nCce, int nTerms,
- *     ByteBuffer cceQ, ByteBuffer cceSf, ByteBuffer cceCb, ByteBuffer cceIcs, ByteBuffer cceTerms,
- *     ByteBuffer frameStatus);
- * an AAC-LC batch with coupling channel elements: nCce CCE ICStream records and nTerms
- * jaad_cce_term (488 B) in the reference's order (jaad_gpu.h); frameStatus as nativeDecode's */
+ *     ByteBuffer msUsed, ByteBuffer tns, ByteBuffer sbr, ByteBuffer pcm, int flags, int nCce,
+ *     int nTerms, ByteBuffer cceQ, ByteBuffer cceSf, ByteBuffer cceCb, ByteBuffer cceIcs,
+ *     ByteBuffer cceTerms, ByteBuffer frameStatus);
+ * a batch with coupling channel elements: nCce CCE ICStream records and nTerms jaad_cce_term
+ * (488 B) in the reference's order (jaad_gpu.h); sbr and frameStatus as nativeDecode's (null sbr
+ * for AAC-LC; coupling is applied to the core spectra before the SBR/PS stage either way) */
 JNIEXPORT void JNICALL Java_net_sourceforge_jaad_aac_gpu_GpuDSP_nativeDecodeCoupled(
     JNIEnv* env, jclass cls, jlong h, jint n_frames, jint n_runs, jint nch, jobject stream_slot, jobject frame_begin,
-    jobject q, jobject sf, jobject cb, jobject ics, jobject ms_used, jobject tns, jobject pcm, jint flags, jint n_cce,
-    jint n_terms, jobject cce_q, jobject cce_sf, jobject cce_cb, jobject cce_ics, jobject cce_terms,
+    jobject q, jobject sf, jobject cb, jobject ics, jobject ms_used, jobject tns, jobject sbr, jobject pcm, jint flags,
+    jint n_cce, jint n_terms, jobject cce_q, jobject cce_sf, jobject cce_cb, jobject cce_ics, jobject cce_terms,
     jobject frame_status) {
     (void)cls;
     decode_common(env, (jaad_ctx*)(intptr_t)h, n_frames, n_runs, nch, stream_slot, frame_begin, q, sf, cb, ics, ms_used,
-                  tns, NULL, pcm, flags, n_cce, n_terms, cce_q, cce_sf, cce_cb, cce_ics, cce_terms, frame_status);
+                  tns, sbr, pcm, flags, n_cce, n_terms, cce_q, cce_sf, cce_cb, cce_ics, cce_terms, frame_status);
 }
 
 /* static native int nativeStateBytes(long h): size of one slot's state blob (jaad_state_bytes).

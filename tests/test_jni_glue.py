@@ -36,7 +36,7 @@ def _lib():
     for name in ("nativeRegister", "nativeUnregister", "nativeFreeDirect"):
         getattr(L, PFX + name).argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p]
     coupled = getattr(L, PFX + "nativeDecodeCoupled")
-    coupled.argtypes = ([C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_int32, C.c_int32] + [C.c_void_p] * 9 +
+    coupled.argtypes = ([C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_int32, C.c_int32] + [C.c_void_p] * 10 +
                         [C.c_int32, C.c_int32, C.c_int32] + [C.c_void_p] * 6)
     getattr(L, PFX + "nativeStateBytes").argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
     getattr(L, PFX + "nativeStateBytes").restype = C.c_int32
@@ -209,7 +209,8 @@ def test_coupled_decode_through_direct_buffers():
     try:
         out = np.zeros_like(want)
         keep = []
-        a = [_buf(x, keep) for x in (b.stream_slot, b.frame_begin, b.q, b.sf, b.cb, b.ics, b.ms_used, None, out)]
+        a = [_buf(x, keep) for x in (b.stream_slot, b.frame_begin, b.q, b.sf, b.cb, b.ics, b.ms_used, None, None,
+                                     out)]
         c = [_buf(x, keep) for x in (b.cce_q, b.cce_sf, b.cce_cb, b.cce_ics, b.cce_terms)]
         getattr(L, PFX + "nativeDecodeCoupled")(env, None, h, b.n_frames, len(b.stream_slot), 2, *a, N.PCM_BIG_ENDIAN,
                                                b.n_cce, len(b.cce_terms), *c, None)
@@ -220,6 +221,53 @@ def test_coupled_decode_through_direct_buffers():
         keep.append(short)
         c[4] = C.addressof(short)
         getattr(L, PFX + "nativeDecodeCoupled")(env, None, h, b.n_frames, len(b.stream_slot), 2, *a, N.PCM_BIG_ENDIAN,
+                                               b.n_cce, len(b.cce_terms), *c, None)
+        cls, msg = _exception(L)
+        assert cls == AAC_EXC and N.strerror(N.ERR_INVALID_ARG) in msg
+    finally:
+        getattr(L, PFX + "nativeDestroy")(env, None, h)
+
+
+@pytest.mark.gpu
+def test_coupled_he_aac_v2_decode_through_direct_buffers():
+    """nativeDecodeCoupled with an sbr buffer: an HE-AAC v2 batch (mono core + PS) whose frames carry
+    coupling terms on the core channel equals the Python entry, PCM for PCM."""
+    from tests.test_cce import cce_records
+    L = _lib()
+    env = L.jni_mock_env()
+    p = N.synth_params(5, n_streams=3, frames_per_stream=16)
+    b = N.synth_batch(p)
+    cfg = N.cfg_for(p)
+    rng = np.random.default_rng(23)
+    n_rec = 8
+    b.cce_q, b.cce_sf, b.cce_cb, b.cce_ics = cce_records(n_rec, 23, pns=10, sf_index=p.sf_index)
+    terms = []
+    for f in range(b.n_frames):
+        if rng.integers(2):
+            continue
+        t = np.zeros((), N.CCE_TERM_DTYPE)
+        t["frame"], t["channel"], t["point"], t["cce"] = f, 0, rng.integers(2), rng.integers(n_rec)
+        t["gain"] = rng.choice([0.0, 1.0, -0.5, 2.0, 1.0905077], 120).astype(np.float32)
+        terms.append(t)
+    b.cce_terms = np.array(terms, N.CCE_TERM_DTYPE)
+    with N.Context(cfg, 3) as ctx:
+        want = ctx.decode(b, N.PCM_BIG_ENDIAN)
+    h = getattr(L, PFX + "nativeCreate")(env, None, p.sf_index, p.channel_config, 0, 1, 1, 3, 0)
+    assert h and _exception(L) is None
+    try:
+        out = np.zeros_like(want)
+        keep = []
+        a = [_buf(x, keep) for x in (b.stream_slot, b.frame_begin, b.q, b.sf, b.cb, b.ics, None, b.tns, b.sbr, out)]
+        c = [_buf(x, keep) for x in (b.cce_q, b.cce_sf, b.cce_cb, b.cce_ics, b.cce_terms)]
+        getattr(L, PFX + "nativeDecodeCoupled")(env, None, h, b.n_frames, len(b.stream_slot), 1, *a, N.PCM_BIG_ENDIAN,
+                                               b.n_cce, len(b.cce_terms), *c, None)
+        assert _exception(L) is None
+        assert (out == want).all()
+        # an sbr buffer one frame short is refused before any copy
+        short = Buf(b.sbr.ctypes.data, b.sbr.nbytes - b.sbr.itemsize)
+        keep.append(short)
+        a[8] = C.addressof(short)
+        getattr(L, PFX + "nativeDecodeCoupled")(env, None, h, b.n_frames, len(b.stream_slot), 1, *a, N.PCM_BIG_ENDIAN,
                                                b.n_cce, len(b.cce_terms), *c, None)
         cls, msg = _exception(L)
         assert cls == AAC_EXC and N.strerror(N.ERR_INVALID_ARG) in msg
