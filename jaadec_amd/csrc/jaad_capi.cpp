@@ -375,6 +375,26 @@ int fail(jaad_ctx* c, hipError_t e, const char* what)
         if (e_ != hipSuccess) return fail(ctx, e_, #call); \
     } while (0)
 
+// JAAD_SYNC_LAUNCHES=1 (diagnostics only): each launch group is followed by a synchronize of its
+// stream, so that a device fault is reported against the launch that raised it rather than at a
+// later copy (the error text names the launch call)
+bool sync_launches()
+{
+    static const bool on = [] {
+        const char* e = std::getenv("JAAD_SYNC_LAUNCHES");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
+#define LAUNCHCHK(call, strm)                                                   \
+    do {                                                                        \
+        HIPCHK(call);                                                           \
+        if (sync_launches()) {                                                  \
+            hipError_t s_ = hipStreamSynchronize(strm);                         \
+            if (s_ != hipSuccess) return fail(ctx, s_, "after " #call);         \
+        }                                                                       \
+    } while (0)
+
 int validate_cfg(const jaad_stream_cfg* cfg)
 {
     if (!cfg) return JAAD_ERR_INVALID_ARG;
@@ -1010,8 +1030,8 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
     }
     a.chains = reinterpret_cast<const uint32_t*>(d1 + o_chains);
     a.n_chains = n_chains;
-    HIPCHK(launch_sbr(a, stream, reinterpret_cast<const uint32_t*>(d1 + o_fix), fix_counts.data(),
-                      (int)fix_counts.size()));
+    LAUNCHCHK(launch_sbr(a, stream, reinterpret_cast<const uint32_t*>(d1 + o_fix), fix_counts.data(),
+                         (int)fix_counts.size()), stream);
     HIPCHK(hipEventRecord(S.used, stream));
     S.live = true;
     if (trace) {
@@ -1072,7 +1092,7 @@ int setup_coupling(jaad_ctx* ctx, const jaad_batch* db, KernelArgs& a, hipStream
     c.tables = ctx->d_tables;
     c.gtab = ctx->d_gtab;
     c.n_terms = nt;
-    HIPCHK(launch_cce_terms(c, stream));
+    LAUNCHCHK(launch_cce_terms(c, stream), stream);
     a.cce_off = reinterpret_cast<const uint32_t*>(d + o_off);
     a.cce_meta = c.meta;
     a.cce_spec = c.spec;
@@ -1142,19 +1162,19 @@ int launch_work(jaad_ctx* ctx, const jaad_batch* db, void* pcm, uint32_t flags, 
             e.out_mode = kOutPlanarF32;
             e.ch0 = (uint32_t)ch0;
             if ((rc = carry_untouched(ctx, e.state_out, e.state_in, 2048, stream))) return rc;
-            HIPCHK(launch_lc(e, stream, tns_spec));
+            LAUNCHCHK(launch_lc(e, stream, tns_spec), stream);
             ch0 += n;
             cpe += n == 2;
         }
-        HIPCHK(launch_pack(static_cast<const float*>(ctx->d_time.p), pcm, db->n_frames, ctx->nch, flags, stream, a.skips,
-                           n_skip_runs(ctx)));
+        LAUNCHCHK(launch_pack(static_cast<const float*>(ctx->d_time.p), pcm, db->n_frames, ctx->nch, flags, stream, a.skips,
+                              n_skip_runs(ctx)), stream);
         ctx->parity ^= 1;
         return JAAD_OK;
     }
     rc = carry_untouched(ctx, a.state_out, a.state_in, 2048, stream);
     if (rc) return rc;
     const bool tns_spec = ctx->cfg.tns_mode == JAAD_TNS_SPEC && db->tns != nullptr;
-    HIPCHK(launch_lc(a, stream, tns_spec));
+    LAUNCHCHK(launch_lc(a, stream, tns_spec), stream);
     if (sbr && (rc = launch_sbr_stage(ctx, db, pcm, flags, stream))) return rc;
     ctx->parity ^= 1;
     return JAAD_OK;
@@ -1310,7 +1330,7 @@ int launch_mc_sbr(jaad_ctx* ctx, const jaad_batch* db, void* pcm, uint32_t flags
             m.n_out++;
         }
     }
-    HIPCHK(launch_mc_interleave(m, pcm, (uint32_t)nf, (uint32_t)S, (int)bps, stream, d_skips, n_skips));
+    LAUNCHCHK(launch_mc_interleave(m, pcm, (uint32_t)nf, (uint32_t)S, (int)bps, stream, d_skips, n_skips), stream);
     return JAAD_OK;
 }
 
@@ -1985,10 +2005,10 @@ static int decode_batch_pieces_impl(jaad_ctx* ctx, const jaad_batch* b, void* pc
         a.ms_used = b->ms_used ? reinterpret_cast<const uint64_t*>(sd + L.ms) - f0 * 2 : nullptr;
         a.tns = b->tns ? reinterpret_cast<const jaad_tns*>(sd + L.tns) - c0 : nullptr;
         HIPCHK(hipStreamWaitEvent(s, ctx->ev_in[i], 0));
-        HIPCHK(launch_check_q(dq + c0 * 1024, nci * 1024, dflag, s));
+        LAUNCHCHK(launch_check_q(dq + c0 * 1024, nci * 1024, dflag, s), s);
         a.chunks = chunks_dev(ctx) + C[i];
         a.n_chunks = C[i + 1] - C[i];
-        if (a.n_chunks) HIPCHK(launch_lc(a, s, tns_spec));
+        if (a.n_chunks) LAUNCHCHK(launch_lc(a, s, tns_spec), s);
         HIPCHK(hipEventRecord(ctx->ev_k[i], s));
         HIPCHK(hipStreamWaitEvent(ctx->d2h, ctx->ev_k[i], 0));
         void* dst = pin_out ? static_cast<char*>(pcm_out) + f0 * fbytes : ctx->stage_out[i % kStageSlots].p;
