@@ -87,6 +87,10 @@ def parse(argv=None):
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", type=int, default=2, choices=sorted(WORKLOADS))
+    ap.add_argument("--precision", choices=("lsb1", "exact"), default="lsb1",
+                    help="jaad_stream_cfg.precision of the AAC-LC kernel: lsb1 = PCM within +-1 LSB of the "
+                         "reference (BASELINE.json's bar; fused multiply-adds in the IMDCT), exact = "
+                         "bit-identical; SBR/PS configs (4, 5) always decode exactly")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-buffer (PCIe-inclusive) leg")
     ap.add_argument("--no-host", action="store_true", help="skip the host front-end (bitstream parse) leg")
@@ -211,9 +215,15 @@ class HipEngine:
         self.ctx.close()
 
 
-def run(args, engine_cls=HipEngine, backend: str = "nccl"):
+def run(args, engine_cls=HipEngine):
     """One rank of the benchmark; returns the JSON line on rank 0 (None elsewhere) and this
-    rank's PCM after the timed steps."""
+    rank's PCM after the timed steps.
+
+    The ranks share nothing on the data path (north_star: "RCCL over xGMI not
+    required"): the only collectives are the barrier around the timed region, the max-over-ranks
+    time and the frame count, three host-side scalars.  They go through a gloo group for every
+    world size (round 6), so the code an 8-GPU run executes is exactly the code the
+    world-2 gloo tests run (tests/test_bench_multirank.py)."""
     import torch.distributed as dist
 
     from jaadec_amd import native as N
@@ -223,18 +233,13 @@ def run(args, engine_cls=HipEngine, backend: str = "nccl"):
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1 and not dist.is_initialized():
-        if backend == "nccl":
-            import torch
-
-            torch.cuda.set_device(local)
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(backend)
+        dist.init_process_group("gloo")
 
     # ---- this rank's slice of the global job
     p, n_global_streams = shard_params(N, args.config, world, rank, args.streams_per_gpu, args.frames_per_stream)
     batch = N.synth_batch(p)
-    cfg = N.cfg_for(p)
+    precision = N.PRECISION_LSB1 if args.precision == "lsb1" and not p.sbr else N.PRECISION_EXACT
+    cfg = N.cfg_for(p, precision=precision)
     sbr = bool(p.sbr)
     n_frames = batch.n_frames
     flags = N.PCM_BIG_ENDIAN
@@ -293,9 +298,7 @@ def run(args, engine_cls=HipEngine, backend: str = "nccl"):
     if world > 1:
         import torch
 
-        t = torch.tensor([n_frames], dtype=torch.int64)
-        if backend == "nccl":
-            t = t.to(eng.dev)
+        t = torch.tensor([n_frames], dtype=torch.int64)  # (a host scalar: gloo)
         dist.all_reduce(t)
         frames_all = int(t.item())
     pcm = eng.pcm()
@@ -359,7 +362,11 @@ def run(args, engine_cls=HipEngine, backend: str = "nccl"):
             "config": {"workload": workload, "frames_per_gpu": n_frames, "frames_per_job": frames_all,
                        "streams_per_job": n_global_streams,
                        "parallelism": f"stream-sharded x{world} (no collectives)", "pcm": "int16 big-endian",
-                       "samples_per_frame": 2048 if sbr else 1024},
+                       "samples_per_frame": 2048 if sbr else 1024,
+                       "precision": ("lsb1: PCM within +-1 LSB of the reference (jaad_stream_cfg.precision = "
+                                     "JAAD_PRECISION_LSB1, fused multiply-adds in the IMDCT; parity_sample checks it)"
+                                     if precision == N.PRECISION_LSB1 else
+                                     "exact: PCM bit-identical to the reference's binary32 arithmetic")},
             "roofline": roofline(args.config, n_frames, kern_ms, achieved, traffic, traffic_src),
             "settle": {"steps": n_settle, "seconds": round(t_settle, 3),
                        "cold_ms_per_step": round(cold, 4) if cold is not None else None,

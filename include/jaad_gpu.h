@@ -87,8 +87,17 @@ typedef struct jaad_stream_cfg {
     uint8_t ext_sf_index;     /* SBR output SampleFrequency index (extensionSampleFrequency of the
                                  ASC, A/DecoderConfig.java:184-198); must be the core index - 3,
                                  i.e. twice the core rate (bs_samplerate_mode = 1)                */
-    uint8_t reserved;
+    uint8_t precision;        /* JAAD_PRECISION_EXACT (0, the default): PCM bit-identical to the
+                                 reference's binary32 arithmetic; JAAD_PRECISION_LSB1: PCM within
+                                 +-1 LSB of it (BASELINE.json's bar) -- the AAC-LC transforms use
+                                 fused multiply-adds (fewer, shorter dependent operations).  Coupling,
+                                 spec TNS and the SBR/PS stages stay exact in either mode.        */
 } jaad_stream_cfg;
+
+enum {
+    JAAD_PRECISION_EXACT = 0,
+    JAAD_PRECISION_LSB1 = 1
+};
 
 /*
  * Per channel-frame side information (16 bytes), one per ICStream per frame.

@@ -209,6 +209,8 @@ struct jaad_ctx {
     PinnedBuf h_chunks[2];                   // staging of each slot's upload
     hipEvent_t chunks_copied[2] = {};        // h_chunks[i] may be rewritten once this has completed
     bool chunks_live[2] = {false, false};
+    hipEvent_t chunks_read[2] = {};          // d_chunks[i] may be rewritten once this has completed (after
+    bool chunks_read_live[2] = {false, false};  // the last LC launch that read it; round 6)
     int chunk_slot = 0;                      // slot of the current plan
     // Every call's device work (whatever stream it is queued on) waits for the previous call's
     // `done`: the chunk table, the double-buffered state and the SBR/PS state are reused call
@@ -405,6 +407,7 @@ int validate_cfg(const jaad_stream_cfg* cfg)
     // multichannel: AAC-LC elements, or SBR per element (HE-AAC v1); PS only in a mono stream
     if (cfg->channel_config > 2 && cfg->ps) return JAAD_ERR_UNSUPPORTED;
     if (cfg->tns_mode > JAAD_TNS_SPEC) return JAAD_ERR_INVALID_ARG;
+    if (cfg->precision > JAAD_PRECISION_LSB1) return JAAD_ERR_INVALID_ARG;
     if (cfg->sbr > 1 || cfg->ps > 1) return JAAD_ERR_UNSUPPORTED;
     if (cfg->ps && (!cfg->sbr || cfg->channel_config != 1)) return JAAD_ERR_UNSUPPORTED;
     // SBR at twice the core rate (bs_samplerate_mode = 1, A/sbr/SBR.java:105), or downsampled
@@ -468,6 +471,23 @@ int plan(jaad_ctx* ctx, const jaad_batch* b, hipStream_t stream, uint32_t size_f
             chunks.push_back(ChunkDesc{f, info, slot, 0});
         }
     }
+    // Self-check of the table before it can reach a launch (round 6): every chunk's
+    // slot in range, its frames (the re-decoded prefix frame included) inside its run's frames of the
+    // planner's view, and with dropped frames its walk inside the kept-frame map and its first skip
+    // entry inside the list.  O(chunks); a failure is an internal error, never a launch.
+    {
+        const uint32_t nv = b->n_frames;
+        for (const ChunkDesc& c : chunks) {
+            const uint32_t n = c.info & 0xffff, pre = (c.info & kChunkPrefix) ? 1u : 0u;
+            const bool ok = c.slot < ctx->n_slots && (n == 0 || (c.frame0 >= pre && (uint64_t)c.frame0 + n <= nv)) &&
+                            (ctx->skips.empty() || n == 0 || (uint64_t)c.frame0 + n <= ctx->keep.size());
+            if (!ok) {
+                ctx->err = "internal: chunk table out of range (frame " + std::to_string(c.frame0) + ", " +
+                           std::to_string(n) + " frames, slot " + std::to_string(c.slot) + ")";
+                return JAAD_ERR_INVALID_ARG;
+            }
+        }
+    }
     if (!ctx->skips.empty()) {  // virtual frames -> batch frames; each chunk's first skip entry
         const std::vector<uint32_t>& k = ctx->keep;
         const uint32_t ns = (uint32_t)ctx->skips.size() / 2;  // incl. the sentinel
@@ -491,6 +511,13 @@ int plan(jaad_ctx* ctx, const jaad_batch* b, hipStream_t stream, uint32_t size_f
     const size_t bytes = cbytes + ctx->skips.size() * sizeof(uint32_t);
     const int slot = ctx->chunk_slot ^ 1;  // (the current plan's slot may still be read by queued kernels)
     if (ctx->chunks_live[slot]) HIPCHK(hipEventSynchronize(ctx->chunks_copied[slot]));  // staging in use?
+    // the slot's device table may still be read by the LC kernels of the plan before last (queued on
+    // another stream, or not yet run): its upload waits for them on the device, a reallocation of
+    // the table on the host (hipFree under a running kernel)
+    if (ctx->chunks_read_live[slot]) {
+        if (bytes + 16 > ctx->d_chunks[slot].cap) HIPCHK(hipEventSynchronize(ctx->chunks_read[slot]));
+        else HIPCHK(hipStreamWaitEvent(stream, ctx->chunks_read[slot], 0));
+    }
     HIPCHK(ctx->h_chunks[slot].ensure(bytes + 16));
     HIPCHK(ctx->d_chunks[slot].ensure(bytes + 16));
     if (bytes) {
@@ -510,6 +537,14 @@ int plan(jaad_ctx* ctx, const jaad_batch* b, hipStream_t stream, uint32_t size_f
     ctx->plan_skips = ctx->skips;
     ctx->plan_n_chunks = (uint32_t)ctx->chunks.size();
     ctx->plan_valid = true;
+    return JAAD_OK;
+}
+
+// the current plan's device chunk table has been read by every LC launch queued so far on `stream`
+int mark_chunks_read(jaad_ctx* ctx, hipStream_t stream)
+{
+    HIPCHK(hipEventRecord(ctx->chunks_read[ctx->chunk_slot], stream));
+    ctx->chunks_read_live[ctx->chunk_slot] = true;
     return JAAD_OK;
 }
 
@@ -1097,6 +1132,7 @@ int setup_coupling(jaad_ctx* ctx, const jaad_batch* db, KernelArgs& a, hipStream
     a.cce_meta = c.meta;
     a.cce_spec = c.spec;
     a.ch0 = 0;
+    a.n_cce_terms = o;
     return JAAD_OK;
 }
 
@@ -1136,6 +1172,13 @@ int launch_work(jaad_ctx* ctx, const jaad_batch* db, void* pcm, uint32_t flags, 
     a.dbg = ctx->dbg;
     a.dbg_frame = ctx->dbg_frame;
     a.skips = plan_skips_dev(ctx);
+    a.n_skip_pairs = (uint32_t)(ctx->plan_skips.size() / 2);
+    a.frame_lo = 0;
+    a.frame_hi = db->n_frames;
+    a.n_slots = ctx->n_slots;
+    // the fused (+-1 LSB) instantiation serves AAC-LC output only: an SBR context's core samples
+    // feed the QMF analysis, whose stages are all kept exact
+    a.precision = sbr ? (uint32_t)JAAD_PRECISION_EXACT : ctx->cfg.precision;
     if (a.n_chunks == 0) return JAAD_OK;
     if (db->n_cce_terms && (rc = setup_coupling(ctx, db, a, stream))) return rc;
     if (ctx->n_elem > 1) {
@@ -1166,6 +1209,7 @@ int launch_work(jaad_ctx* ctx, const jaad_batch* db, void* pcm, uint32_t flags, 
             ch0 += n;
             cpe += n == 2;
         }
+        if ((rc = mark_chunks_read(ctx, stream))) return rc;
         LAUNCHCHK(launch_pack(static_cast<const float*>(ctx->d_time.p), pcm, db->n_frames, ctx->nch, flags, stream, a.skips,
                               n_skip_runs(ctx)), stream);
         ctx->parity ^= 1;
@@ -1175,6 +1219,7 @@ int launch_work(jaad_ctx* ctx, const jaad_batch* db, void* pcm, uint32_t flags, 
     if (rc) return rc;
     const bool tns_spec = ctx->cfg.tns_mode == JAAD_TNS_SPEC && db->tns != nullptr;
     LAUNCHCHK(launch_lc(a, stream, tns_spec), stream);
+    if ((rc = mark_chunks_read(ctx, stream))) return rc;
     if (sbr && (rc = launch_sbr_stage(ctx, db, pcm, flags, stream))) return rc;
     ctx->parity ^= 1;
     return JAAD_OK;
@@ -1459,7 +1504,9 @@ int jaad_ctx_create(const jaad_stream_cfg* cfg, uint32_t n_slots, int device, ja
     if ((e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking)) != hipSuccess) return bail(e, "hipStreamCreate");
     if ((e = hipEventCreateWithFlags(&ctx->done, hipEventDisableTiming)) != hipSuccess) return bail(e, "hipEventCreate");
     if ((e = hipEventCreateWithFlags(&ctx->chunks_copied[0], hipEventDisableTiming)) != hipSuccess ||
-        (e = hipEventCreateWithFlags(&ctx->chunks_copied[1], hipEventDisableTiming)) != hipSuccess)
+        (e = hipEventCreateWithFlags(&ctx->chunks_copied[1], hipEventDisableTiming)) != hipSuccess ||
+        (e = hipEventCreateWithFlags(&ctx->chunks_read[0], hipEventDisableTiming)) != hipSuccess ||
+        (e = hipEventCreateWithFlags(&ctx->chunks_read[1], hipEventDisableTiming)) != hipSuccess)
         return bail(e, "hipEventCreate");
     if ((e = hipEventCreateWithFlags(&ctx->skips_copied, hipEventDisableTiming)) != hipSuccess)
         return bail(e, "hipEventCreate");
@@ -1560,7 +1607,10 @@ void jaad_ctx_destroy(jaad_ctx* ctx)
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     if (ctx->done_live) (void)hipEventSynchronize(ctx->done);
-    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    // every stream of the context drained before any buffer is freed (copies of a failed call, the
+    // record uploads, the pipelines' D2H copies)
+    for (hipStream_t st : {ctx->stream, ctx->cstream, ctx->h2d, ctx->d2h})
+        if (st) (void)hipStreamSynchronize(st);
     for (jaad_ctx* c : ctx->children) jaad_ctx_destroy(c);
     ctx->children.clear();
     ctx->d_mc.release();
@@ -1611,6 +1661,8 @@ void jaad_ctx_destroy(jaad_ctx* ctx)
     }
     if (ctx->done) (void)hipEventDestroy(ctx->done);
     for (hipEvent_t ev : ctx->chunks_copied)
+        if (ev) (void)hipEventDestroy(ev);
+    for (hipEvent_t ev : ctx->chunks_read)
         if (ev) (void)hipEventDestroy(ev);
     if (ctx->skips_copied) (void)hipEventDestroy(ctx->skips_copied);
     ctx->d_skips.release();
@@ -1927,6 +1979,8 @@ static int decode_batch_pieces_impl(jaad_ctx* ctx, const jaad_batch* b, void* pc
     a.tns_mode = ctx->cfg.tns_mode;
     a.dbg = ctx->dbg;
     a.dbg_frame = ctx->dbg_frame;
+    a.n_slots = ctx->n_slots;
+    a.precision = ctx->cfg.precision;
     const bool tns_spec = ctx->cfg.tns_mode == JAAD_TNS_SPEC && b->tns != nullptr;
     int rc;
     if ((rc = carry_untouched(ctx, a.state_out, a.state_in, 2048, s))) return rc;
@@ -2008,6 +2062,8 @@ static int decode_batch_pieces_impl(jaad_ctx* ctx, const jaad_batch* b, void* pc
         LAUNCHCHK(launch_check_q(dq + c0 * 1024, nci * 1024, dflag, s), s);
         a.chunks = chunks_dev(ctx) + C[i];
         a.n_chunks = C[i + 1] - C[i];
+        a.frame_lo = (uint32_t)f0;  // the piece's rows: its side block, q and PCM ranges
+        a.frame_hi = (uint32_t)(f0 + nfi);
         if (a.n_chunks) LAUNCHCHK(launch_lc(a, s, tns_spec), s);
         HIPCHK(hipEventRecord(ctx->ev_k[i], s));
         HIPCHK(hipStreamWaitEvent(ctx->d2h, ctx->ev_k[i], 0));
@@ -2017,6 +2073,7 @@ static int decode_batch_pieces_impl(jaad_ctx* ctx, const jaad_batch* b, void* pc
         HIPCHK(hipEventRecord(ctx->ev_out[i], ctx->d2h));
         queued = i + 1;
     }
+    if ((rc = mark_chunks_read(ctx, s))) return rc;
     if (!pin_out)
         for (int i = std::max(0, queued - kStageSlots); i < queued; i++)
             if ((rc = copy_out(i))) return rc;
@@ -2189,12 +2246,21 @@ static int decode_batch_pieces_launch_impl(jaad_ctx* ctx, const jaad_batch* b, v
             beg.push_back(beg.back() + (e - a));
         }
     };
-    // piece i's PCM (stage_out slot) -> the caller's frames, dropped frames left as they are
+    // piece i's PCM (in the staging slot it was given) -> the caller's frames, dropped frames left as
+    // they are.  The slots go to the non-empty pieces in turn (a time slice of runs shorter than P
+    // frames can be empty: ADVICE r5 -- slot i % 2 by piece index lost a piece's PCM behind an empty
+    // piece), and a slot is drained right before it is reused and at the end.
     std::vector<uint32_t> out_runs, out_beg;
-    auto copy_out = [&](int i) -> int {
+    int slot_owner[kStageSlots];
+    std::fill(slot_owner, slot_owner + kStageSlots, -1);
+    int next_slot = 0;
+    auto copy_out = [&](int slot) -> int {
+        const int i = slot_owner[slot];
+        if (i < 0) return JAAD_OK;
+        slot_owner[slot] = -1;
         HIPCHK(hipEventSynchronize(ctx->ev_out[i]));
         piece_runs(i, out_runs, out_beg);
-        const char* src = static_cast<const char*>(ctx->stage_out[i % kStageSlots].p);
+        const char* src = static_cast<const char*>(ctx->stage_out[slot].p);
         const size_t nr = out_runs.size();
         io.run([&](int t) {
             for (size_t k = nr * t / W; k < nr * (t + 1) / W; k++) {
@@ -2334,8 +2400,11 @@ static int decode_batch_pieces_launch_impl(jaad_ctx* ctx, const jaad_batch* b, v
             HIPCHK(hipMemcpy2DAsync(static_cast<char*>(pcm_out) + (size_t)cut(0, i) * fbytes, (size_t)L0 * fbytes, dp, w, w,
                                     prun.size(), hipMemcpyDeviceToHost, ctx->d2h));
         } else {
-            if (i >= kStageSlots && (rc = copy_out(i - kStageSlots))) return rc;  // frees staging slot i % 2
-            HIPCHK(hipMemcpyAsync(ctx->stage_out[i % kStageSlots].p, dp, nfi * fbytes, hipMemcpyDeviceToHost, ctx->d2h));
+            const int slot = next_slot;
+            next_slot = (next_slot + 1) % kStageSlots;
+            if ((rc = copy_out(slot))) return rc;  // drains the slot's previous piece
+            slot_owner[slot] = i;
+            HIPCHK(hipMemcpyAsync(ctx->stage_out[slot].p, dp, nfi * fbytes, hipMemcpyDeviceToHost, ctx->d2h));
         }
         HIPCHK(hipEventRecord(ctx->ev_out[i], ctx->d2h));
         queued = i + 1;
@@ -2344,8 +2413,9 @@ static int decode_batch_pieces_launch_impl(jaad_ctx* ctx, const jaad_batch* b, v
                          P, nfi, ms(t_call, t0), ms(t0, t1), ms(t1, t2), ms(t2, clk::now()));
     }
     if (!dma_out)
-        for (int i = std::max(0, queued - kStageSlots); i < queued; i++)
-            if ((rc = copy_out(i))) return rc;
+        for (int k = 0; k < kStageSlots; k++)  // the last pieces, oldest first
+            if ((rc = copy_out((next_slot + k) % kStageSlots))) return rc;
+    (void)queued;
     HIPCHK(hipStreamSynchronize(ctx->d2h));
     HIPCHK(hipStreamSynchronize(s));
     if (trace) std::fprintf(stderr, "jaad pieces: call %.3f ms (q %s, PCM %s)\n", ms(t_call, clk::now()), dma_q ? "dma" : "staged",

@@ -90,6 +90,15 @@ struct KernelArgs {
     // wave steps from frame f to f + 1, or past the run of dropped frames that starts there.
     // Null: no frame is dropped.
     const uint32_t* skips;
+    // bounds of this launch (round 6): the batch frames its chunks may touch
+    // [frame_lo, frame_hi) (q/sf/cb/ics/ms/tns/pcm rows), the state slots, the skip-list pairs (incl.
+    // the sentinel) and the coupling terms.  The kernel skips a chunk whose descriptor falls outside
+    // them (plan() has validated the table on the host already); a JAAD_BOUNDS build checks every
+    // global access against them and prints the chunk, frame and access that failed.
+    uint32_t frame_lo, frame_hi, n_slots, n_skip_pairs, n_cce_terms;
+    // jaad_stream_cfg.precision: JAAD_PRECISION_LSB1 selects the fused-multiply-add instantiation of
+    // the TNS-compat, uncoupled kernel (mode 4); every other mode stays bit-exact
+    uint32_t precision;
 };
 
 // inputs of cce_term_kernel: one wave per term

@@ -173,29 +173,95 @@ __device__ __forceinline__ void radix4_pk(f2& c0, f2& c1, f2& c2, f2& c3)
 }
 __device__ __forceinline__ f2 ld2(const float (&p)[2]) { return *reinterpret_cast<const f2*>(p); }
 
+// ------------------------------------------------------------------------------------------
+// +-1 LSB precision (jaad_stream_cfg.precision = JAAD_PRECISION_LSB1, kernel mode 4): the same
+// transform, tables and evaluation structure with the complex products fused into v_pk_fma_f32
+// (one rounding per multiply-add instead of one per product and one per sum).  A complex
+// product is 2 packed operations instead of 3, a twiddled radix-2 butterfly 4 instead of 5 with a
+// dependency depth of 2 instead of 3.  BASELINE.json's bar is PCM within +-1 LSB of the reference;
+// the reordered roundings move a sample by ~1e-6 relative (tests/test_gpu_precision.py measures the
+// off-by-one fraction and asserts max |delta| <= 1 on the full C2 / C3 batches).
+// ------------------------------------------------------------------------------------------
+// a + b.x * w
+__device__ __forceinline__ f2 fma_bx(f2 b, f2 w, f2 a)
+{
+    f2 r;
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1]" : "=v"(r) : "v"(b), "v"(w), "v"(a));
+    return r;
+}
+// a + b.y * (-w.y, w.x)
+__device__ __forceinline__ f2 fma_by(f2 b, f2 w, f2 a)
+{
+    f2 r;
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]" : "=v"(r) : "v"(b), "v"(w), "v"(a));
+    return r;
+}
+// a - b.x * w
+__device__ __forceinline__ f2 fma_nbx(f2 b, f2 w, f2 a)
+{
+    f2 r;
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1] neg_lo:[1,0,0] neg_hi:[1,0,0]" : "=v"(r) : "v"(b), "v"(w), "v"(a));
+    return r;
+}
+// a - b.y * (-w.y, w.x)
+__device__ __forceinline__ f2 fma_nby(f2 b, f2 w, f2 a)
+{
+    f2 r;
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[1,1,0] neg_hi:[1,0,0]"
+        : "=v"(r) : "v"(b), "v"(w), "v"(a));
+    return r;
+}
+// b.x * w
+__device__ __forceinline__ f2 mul_bx(f2 b, f2 w)
+{
+    f2 r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(r) : "v"(b), "v"(w));
+    return r;
+}
+// x * w (complex): 2 packed operations
+__device__ __forceinline__ f2 cmul_fma(f2 x, f2 w) { return fma_by(x, w, mul_bx(x, w)); }
+
+template <bool F>
+__device__ __forceinline__ f2 cmul_t(f2 x, f2 w)
+{
+    if constexpr (F) return cmul_fma(x, w);
+    else return cmul(x, w);
+}
+template <bool F>
+__device__ __forceinline__ void bfly_t(f2& a, f2& b, f2 w)
+{
+    if constexpr (F) {
+        const f2 p = fma_bx(b, w, a), m = fma_nbx(b, w, a);
+        a = fma_by(b, w, p);
+        b = fma_nby(b, w, m);
+    } else {
+        bfly_pk(a, b, w);
+    }
+}
+template <bool F = false>
 __device__ __forceinline__ void fft_pass1_pk(f2 (&c)[8], const float (*w)[2])
 {
     radix4_pk(c[BR3[0]], c[BR3[1]], c[BR3[2]], c[BR3[3]]);
     radix4_pk(c[BR3[4]], c[BR3[5]], c[BR3[6]], c[BR3[7]]);
 #pragma unroll
-    for (int k = 0; k < 4; k++) bfly_pk(c[BR3[k]], c[BR3[k + 4]], ld2(w[k]));
+    for (int k = 0; k < 4; k++) bfly_t<F>(c[BR3[k]], c[BR3[k + 4]], ld2(w[k]));
 }
-template <typename TW>
+template <bool F = false, typename TW>
 __device__ __forceinline__ void fft_3stages_pk(f2 (&c)[8], TW tw)
 {
     {
         const f2 w = tw(0);
 #pragma unroll
-        for (int s = 0; s < 8; s += 2) bfly_pk(c[s], c[s + 1], w);
+        for (int s = 0; s < 8; s += 2) bfly_t<F>(c[s], c[s + 1], w);
     }
 #pragma unroll
     for (int e = 0; e < 2; e++) {
         const f2 w = tw(1 + e);
-        bfly_pk(c[e], c[e + 2], w);
-        bfly_pk(c[4 + e], c[6 + e], w);
+        bfly_t<F>(c[e], c[e + 2], w);
+        bfly_t<F>(c[4 + e], c[6 + e], w);
     }
 #pragma unroll
-    for (int s = 0; s < 4; s++) bfly_pk(c[s], c[s + 4], tw(3 + s));
+    for (int s = 0; s < 4; s++) bfly_t<F>(c[s], c[s + 4], tw(3 + s));
 }
 
 // The same stages on two channels in lockstep, interleaved operation by operation: each packed
@@ -210,6 +276,21 @@ __device__ __forceinline__ void bfly_pk2(f2& a0, f2& b0, f2& a1, f2& b1, f2 w)
     b1 = a1 - z1;
     a0 = a0 + z0;
     a1 = a1 + z1;
+}
+// both channels of the lockstep IMDCT, operation by operation
+template <bool F>
+__device__ __forceinline__ void bfly_t2(f2& a0, f2& b0, f2& a1, f2& b1, f2 w)
+{
+    if constexpr (F) {
+        const f2 p0 = fma_bx(b0, w, a0), p1 = fma_bx(b1, w, a1);
+        const f2 m0 = fma_nbx(b0, w, a0), m1 = fma_nbx(b1, w, a1);
+        a0 = fma_by(b0, w, p0);
+        a1 = fma_by(b1, w, p1);
+        b0 = fma_nby(b0, w, m0);
+        b1 = fma_nby(b1, w, m1);
+    } else {
+        bfly_pk2(a0, b0, a1, b1, w);
+    }
 }
 __device__ __forceinline__ void radix4_pk2(f2 (&c)[8], f2 (&d)[8], int i0, int i1, int i2, int i3)
 {
@@ -226,30 +307,32 @@ __device__ __forceinline__ void radix4_pk2(f2 (&c)[8], f2 (&d)[8], int i0, int i
     c[i3] = pk_rot_m(e0, g0);
     d[i3] = pk_rot_m(e1, g1);
 }
+template <bool F = false>
 __device__ __forceinline__ void fft_pass1_pk2(f2 (&c)[8], f2 (&d)[8], const float (*w)[2])
 {
     radix4_pk2(c, d, BR3[0], BR3[1], BR3[2], BR3[3]);
     radix4_pk2(c, d, BR3[4], BR3[5], BR3[6], BR3[7]);
 #pragma unroll
-    for (int k = 0; k < 4; k++) bfly_pk2(c[BR3[k]], c[BR3[k + 4]], d[BR3[k]], d[BR3[k + 4]], ld2(w[k]));
+    for (int k = 0; k < 4; k++) bfly_t2<F>(c[BR3[k]], c[BR3[k + 4]], d[BR3[k]], d[BR3[k + 4]], ld2(w[k]));
 }
-template <typename TW>
+template <bool F = false, typename TW>
 __device__ __forceinline__ void fft_3stages_pk2(f2 (&c)[8], f2 (&d)[8], TW tw)
 {
     {
         const f2 w = tw(0);
 #pragma unroll
-        for (int s = 0; s < 8; s += 2) bfly_pk2(c[s], c[s + 1], d[s], d[s + 1], w);
+        for (int s = 0; s < 8; s += 2) bfly_t2<F>(c[s], c[s + 1], d[s], d[s + 1], w);
     }
 #pragma unroll
     for (int e = 0; e < 2; e++) {
         const f2 w = tw(1 + e);
-        bfly_pk2(c[e], c[e + 2], d[e], d[e + 2], w);
-        bfly_pk2(c[4 + e], c[6 + e], d[4 + e], d[6 + e], w);
+        bfly_t2<F>(c[e], c[e + 2], d[e], d[e + 2], w);
+        bfly_t2<F>(c[4 + e], c[6 + e], d[4 + e], d[6 + e], w);
     }
 #pragma unroll
-    for (int s = 0; s < 4; s++) bfly_pk2(c[s], c[s + 4], d[s], d[s + 4], tw(3 + s));
+    for (int s = 0; s < 4; s++) bfly_t2<F>(c[s], c[s + 4], d[s], d[s + 4], tw(3 + s));
 }
+
 
 
 // Register transposes between the IFFT passes.  A pair of registers (a: register bit i clear,
@@ -439,7 +522,7 @@ __device__ __forceinline__ void xch_bit(f2 (&c)[8], int u)
 // its bits 0,1,2).  The first exchange trades register bits 0,1,2 for lane bits 5,4,3 (e bits
 // 3,4,5 into registers; lane bits 3-5 then hold e bits 0-2), the second register bits 0,1,2 for
 // lane bits 2,1,0 (e bits 6,7,8 into registers), leaving lane u with positions lane_pos(u) + 64 s.
-template <int N>
+template <int N, bool F = false>
 __device__ __forceinline__ void imdct_long_pk(float* const (&bufs)[N], const LdsTables& T, int u, f2 (&c)[N][8])
 {
 #pragma unroll
@@ -449,11 +532,11 @@ __device__ __forceinline__ void imdct_long_pk(float* const (&bufs)[N], const Lds
             const int k = u + 64 * s;
             // MDCT.java:39-42: re = in1*c - in0*sn, im = in0*c + in1*sn = cmul((in1, in0), (c, sn))
             const f2 x = {bufs[n][eo_idx(1023 - 2 * k)], bufs[n][eo_idx(2 * k)]};
-            c[n][s] = cmul(x, ld2(T.mdct_l[k]));
+            c[n][s] = cmul_t<F>(x, ld2(T.mdct_l[k]));
         }
     // pass 1: register s holds e bits (s2, s1, s0) = e bits 0, 1, 2 (fft_pass1_pk's BR3 order)
-    if constexpr (N == 2) fft_pass1_pk2(c[0], c[1], T.tw1);
-    else fft_pass1_pk(c[0], T.tw1);
+    if constexpr (N == 2) fft_pass1_pk2<F>(c[0], c[1], T.tw1);
+    else fft_pass1_pk<F>(c[0], T.tw1);
 #pragma unroll
     for (int n = 0; n < N; n++) {
         xch_bit<0, 5>(c[n], u);  // e bit 3 (lane bit 5) <-> e bit 2
@@ -463,8 +546,8 @@ __device__ __forceinline__ void imdct_long_pk(float* const (&bufs)[N], const Lds
     if constexpr (N == 2) xch_bit_pair<2, 3>(c[0], c[1]);
     // pass 2: register bits 0,1,2 = e bits 3,4,5; e mod 8 = u >> 3
     const int b = u >> 3;
-    if constexpr (N == 2) fft_3stages_pk2(c[0], c[1], [&](int j) { return ld2(T.tw2[j][b]); });
-    else fft_3stages_pk(c[0], [&](int j) { return ld2(T.tw2[j][b]); });
+    if constexpr (N == 2) fft_3stages_pk2<F>(c[0], c[1], [&](int j) { return ld2(T.tw2[j][b]); });
+    else fft_3stages_pk<F>(c[0], [&](int j) { return ld2(T.tw2[j][b]); });
     if constexpr (N == 2) {
         xch_bit_pair<0, 2>(c[0], c[1]);  // e bit 6 (lane bit 2) <-> e bit 3
         xch_bit_pair<1, 1>(c[0], c[1]);  // e bit 7 (lane bit 1) <-> e bit 4
@@ -478,13 +561,13 @@ __device__ __forceinline__ void imdct_long_pk(float* const (&bufs)[N], const Lds
         }
     }
     // pass 3: register bits 0,1,2 = e bits 6,7,8, e mod 64 = lane_pos(u)
-    if constexpr (N == 2) fft_3stages_pk2(c[0], c[1], [&](int j) { return ld2(T.tw3[j][u]); });
-    else fft_3stages_pk(c[0], [&](int j) { return ld2(T.tw3[j][u]); });
+    if constexpr (N == 2) fft_3stages_pk2<F>(c[0], c[1], [&](int j) { return ld2(T.tw3[j][u]); });
+    else fft_3stages_pk<F>(c[0], [&](int j) { return ld2(T.tw3[j][u]); });
     // MDCT.java:48-53: re = t0*c - t1*sn, im = t1*c + t0*sn = cmul((t0, t1), (c, sn))
 #pragma unroll
     for (int s = 0; s < 8; s++)
 #pragma unroll
-        for (int n = 0; n < N; n++) c[n][s] = cmul(c[n][s], ld2(T.mdct_post[s][u]));
+        for (int n = 0; n < N; n++) c[n][s] = cmul_t<F>(c[n][s], ld2(T.mdct_post[s][u]));
 }
 
 // FilterBank.process for ONLY_LONG / LONG_START / LONG_STOP (FilterBank.java:41-70, 102-119).
@@ -543,6 +626,7 @@ __device__ __forceinline__ void ola_long_t(const LdsTables& T, const FrameCtx& f
 // ONLY_LONG window + overlap-add in packed form (slot pair (2s, 2s+1) of ola_long_t):
 //   out[o] = ov[o] + f_o * W[P_o],  new ov[o] = g * W[1023 - P_o]
 // with (f_0, f_1, g) = (-re, re, -im) for s < 4 and (im, -im, re) for s >= 4
+template <bool F = false>
 __device__ __forceinline__ void ola_only_long_pk(const LdsTables& T, const FrameCtx& fc, const f2 (&c)[8],
                                                  float (&ov)[16], float (&out)[16])
 {
@@ -552,16 +636,25 @@ __device__ __forceinline__ void ola_only_long_pk(const LdsTables& T, const Frame
 #pragma unroll
     for (int s = 0; s < 8; s++) {
         const f2 wp = Wp[64 * s + u], wc = Wc[64 * s + u];
-        f2 fw, nv;
+        f2 fw, nv, o;
+        const f2 ovp = f2{ov[2 * s], ov[2 * s + 1]};
         if (s < 4) {
-            asm("v_pk_mul_f32 %0, %1, %2 op_sel:[0,0] op_sel_hi:[0,1] neg_lo:[1,0]" : "=v"(fw) : "v"(c[s]), "v"(wp));
+            if constexpr (F)  // o = ov + (-re, re) * wp in one fused operation
+                asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,0,0] op_sel_hi:[0,1,1] neg_lo:[1,0,0]"
+                    : "=v"(o) : "v"(c[s]), "v"(wp), "v"(ovp));
+            else
+                asm("v_pk_mul_f32 %0, %1, %2 op_sel:[0,0] op_sel_hi:[0,1] neg_lo:[1,0]" : "=v"(fw) : "v"(c[s]), "v"(wp));
             asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,1] op_sel_hi:[1,0] neg_lo:[1,0] neg_hi:[1,0]"
                 : "=v"(nv) : "v"(c[s]), "v"(wc));
         } else {
-            asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,0] op_sel_hi:[1,1] neg_hi:[1,0]" : "=v"(fw) : "v"(c[s]), "v"(wp));
+            if constexpr (F)  // o = ov + (im, -im) * wp
+                asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,1,1] neg_hi:[1,0,0]"
+                    : "=v"(o) : "v"(c[s]), "v"(wp), "v"(ovp));
+            else
+                asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,0] op_sel_hi:[1,1] neg_hi:[1,0]" : "=v"(fw) : "v"(c[s]), "v"(wp));
             asm("v_pk_mul_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[0,0]" : "=v"(nv) : "v"(c[s]), "v"(wc));
         }
-        const f2 o = f2{ov[2 * s], ov[2 * s + 1]} + fw;
+        if constexpr (!F) o = ovp + fw;
         out[2 * s] = o.x;
         out[2 * s + 1] = o.y;
         ov[2 * s] = nv.x;
@@ -569,11 +662,12 @@ __device__ __forceinline__ void ola_only_long_pk(const LdsTables& T, const Frame
     }
 }
 
+template <bool F = false>
 __device__ __forceinline__ void ola_long_pk(const LdsTables& T, const FrameCtx& fc, const f2 (&c)[8], float (&ov)[16],
                                             float (&out)[16])
 {
     if (fc.seq == JAAD_ONLY_LONG_SEQUENCE) {
-        ola_only_long_pk(T, fc, c, ov, out);
+        ola_only_long_pk<F>(T, fc, c, ov, out);
         return;
     }
     float re[8], im[8];
@@ -593,6 +687,7 @@ __device__ __forceinline__ void ola_long_pk(const LdsTables& T, const FrameCtx& 
 // ------------------------------------------------------------------------------------------
 // 8 x 64-point IFFTs in packed FP32 (one register pair per complex value, the long path's
 // primitives; a - b as a + (-b))
+template <bool F = false>
 __device__ __forceinline__ void imdct_short_pk(float* buf, const LdsTables& T, int u, float (&re)[8], float (&im)[8])
 {
     const int w = u >> 3, b = u & 7;
@@ -602,13 +697,13 @@ __device__ __forceinline__ void imdct_short_pk(float* buf, const LdsTables& T, i
         const int k = b + 8 * s;
         // MDCT.java:39-42: re = in1*c - in0*sn, im = in0*c + in1*sn = cmul((in1, in0), (c, sn))
         const f2 x = {buf[eo_idx(128 * w + 127 - 2 * k)], buf[eo_idx(128 * w + 2 * k)]};
-        c[s] = cmul(x, ld2(T.mdct_s[k]));
+        c[s] = cmul_t<F>(x, ld2(T.mdct_s[k]));
     }
     wave_sync();
     radix4_pk(c[BR3[0]], c[BR3[1]], c[BR3[2]], c[BR3[3]]);
     radix4_pk(c[BR3[4]], c[BR3[5]], c[BR3[6]], c[BR3[7]]);
 #pragma unroll
-    for (int k = 0; k < 4; k++) bfly_pk(c[BR3[k]], c[BR3[k + 4]], ld2(T.roots_s[8 * k]));
+    for (int k = 0; k < 4; k++) bfly_t<F>(c[BR3[k]], c[BR3[k + 4]], ld2(T.roots_s[8 * k]));
     f2* X = reinterpret_cast<f2*>(buf);
     const int t = (int)(__builtin_bitreverse32((uint32_t)b) >> 29);
 #pragma unroll
@@ -618,14 +713,14 @@ __device__ __forceinline__ void imdct_short_pk(float* buf, const LdsTables& T, i
     for (int s = 0; s < 8; s++) c[s] = X[xs(64 * w + b + 8 * s)];
     wave_sync();
     // stages i = 8, 16, 32 of the 64-point IFFT: roots[k*m], m = 4, 2, 1
-    fft_3stages_pk(c, [&](int j) {
+    fft_3stages_pk<F>(c, [&](int j) {
         const int idx = j == 0 ? 4 * b : (j < 3 ? 2 * (b + 8 * (j - 1)) : b + 8 * (j - 3));
         return ld2(T.roots_s[idx]);
     });
 #pragma unroll
     for (int s = 0; s < 8; s++) {
         // MDCT.java:48-53: re = t0*c - t1*sn, im = t1*c + t0*sn = cmul((t0, t1), (c, sn))
-        const f2 z = cmul(c[s], ld2(T.mdct_s[b + 8 * s]));
+        const f2 z = cmul_t<F>(c[s], ld2(T.mdct_s[b + 8 * s]));
         re[s] = z.x;
         im[s] = z.y;
     }
@@ -1030,7 +1125,7 @@ __device__ __forceinline__ void couple_after_tns(const KernelArgs& A, float* buf
     }
 }
 
-template <bool kTnsSpec, bool kCoupleAfter = false>
+template <bool kTnsSpec, bool kCoupleAfter = false, bool F = false>
 __device__ __forceinline__ void synth_channel(const KernelArgs& A, const LdsTables& T, WaveLds<kTnsSpec>& W, float* buf,
                                               const Ics& ic, size_t cf, float (&ov)[16], float (&out)[16], int f = 0,
                                               int ch = 0)
@@ -1042,13 +1137,13 @@ __device__ __forceinline__ void synth_channel(const KernelArgs& A, const LdsTabl
     const FrameCtx fc{ic.seq, ic.shape, ic.shape_prev};
     if (fc.seq == JAAD_EIGHT_SHORT_SEQUENCE) {
         float re[8], im[8];
-        imdct_short_pk(buf, T, u, re, im);
+        imdct_short_pk<F>(buf, T, u, re, im);
         ola_short(buf, T, u, fc, re, im, ov, out);
     } else {
         float* const bufs[1] = {buf};
         f2 cx[1][8];
-        imdct_long_pk<1>(bufs, T, u, cx);
-        ola_long_pk(T, fc, cx[0], ov, out);
+        imdct_long_pk<1, F>(bufs, T, u, cx);
+        ola_long_pk<F>(T, fc, cx[0], ov, out);
     }
     wave_sync();
 }
@@ -1071,13 +1166,36 @@ __device__ __forceinline__ void synth_channel(const KernelArgs& A, const LdsTabl
     } while (0)
 #endif
 
+// JAAD_BOUNDS builds (diagnostics): every global access of lc_decode_kernel is checked
+// against the launch's bounds (KernelArgs::frame_lo/hi, n_slots, n_skip_pairs, n_cce_terms) before
+// it is issued; a failing check prints the chunk, the frame, what was accessed and the two values
+// compared, and the wave leaves the kernel (the conditions are wave-uniform).  Product builds
+// compile the checks away (the chunk-level guard below stays).
+#ifdef JAAD_BOUNDS
+#define JAAD_BOUND(ci, f, cond, what, a, b)                                                                 \
+    do {                                                                                                   \
+        if (!(cond)) {                                                                                     \
+            if (lane_id() == 0)                                                                            \
+                printf("JAAD_BOUNDS lc_decode_kernel: chunk %u frame %d: %s %u vs %u\n", (unsigned)(ci), (int)(f), \
+                       what, (unsigned)(a), (unsigned)(b));                                                \
+            return;                                                                                        \
+        }                                                                                                  \
+    } while (0)
+#else
+#define JAAD_BOUND(ci, f, cond, what, a, b) \
+    do {                                    \
+    } while (0)
+#endif
+
 // kMode: 0 = TNS compat (the reference), 1 = spec TNS, 2 = TNS compat with dependent coupling,
-// 3 = spec TNS with dependent coupling (BEFORE_TNS terms, the TNS filters, AFTER_TNS terms)
+// 3 = spec TNS with dependent coupling (BEFORE_TNS terms, the TNS filters, AFTER_TNS terms),
+// 4 = mode 0 at +-1 LSB precision (JAAD_PRECISION_LSB1: fused multiply-adds in the transforms)
 template <int kMode, int kOut, bool kStereo>
 __global__ __launch_bounds__(64 * waves_per_wg<kMode == 1 || kMode == 3>()) void lc_decode_kernel(KernelArgs A)
 {
     constexpr bool kTnsSpec = kMode == 1 || kMode == 3;
     [[maybe_unused]] constexpr bool kCouple = kMode == 2 || kMode == 3;
+    constexpr bool kFast = kMode == 4;
     constexpr int kW = waves_per_wg<kTnsSpec>();
     constexpr int kThreads = 64 * kW;
     // one LDS object with the tables first: every table access is a 16-bit immediate offset
@@ -1137,6 +1255,13 @@ __global__ __launch_bounds__(64 * waves_per_wg<kMode == 1 || kMode == 3>()) void
         const bool prefix = (cd.info & kChunkPrefix) != 0;
         const int my_n = nfr + (prefix ? 1 : 0);
         const int f_first = (int)cd.frame0;  // batch frame of the first iteration
+        // a descriptor outside this launch's bounds is never walked (plan() validates the table on
+        // the host; this guards the device copy the kernel actually reads): one scalar test per chunk
+        JAAD_BOUND(ci, -1, cd.slot < A.n_slots, "chunk slot", cd.slot, A.n_slots);
+        JAAD_BOUND(ci, f_first, my_n == 0 || (cd.frame0 >= A.frame_lo && cd.frame0 + (uint32_t)my_n <= A.frame_hi),
+                   "chunk frames", cd.frame0 + (uint32_t)my_n, A.frame_hi);
+        JAAD_BOUND(ci, f_first, !A.skips || cd.skip < A.n_skip_pairs, "chunk skip entry", cd.skip, A.n_skip_pairs);
+        if (cd.slot >= A.n_slots || (my_n && (cd.frame0 < A.frame_lo || cd.frame0 >= A.frame_hi))) continue;
 
         float ovL[16], ovR[16];
         {
@@ -1196,6 +1321,16 @@ __global__ __launch_bounds__(64 * waves_per_wg<kMode == 1 || kMode == 3>()) void
             if (A.skips && fr_next == __builtin_amdgcn_readlane(cur.side, 63)) {  // step over dropped frames
                 fr_next += __builtin_amdgcn_readlane(cur.side, 62);
                 skip++;
+            }
+            // (JAAD_BOUNDS: the frame this iteration decodes was prefetched in the previous one; the
+            // frame the next prefetch reads and its skip entry are checked here, before it is issued)
+            JAAD_BOUND(ci, f, (uint32_t)f >= A.frame_lo && (uint32_t)f < A.frame_hi, "frame rows / pcm", f, A.frame_hi);
+            JAAD_BOUND(ci, f, it + 1 >= my_n || ((uint32_t)fr_next >= A.frame_lo && (uint32_t)fr_next < A.frame_hi),
+                       "prefetched frame", fr_next, A.frame_hi);
+            JAAD_BOUND(ci, f, !A.skips || (uint32_t)skip < A.n_skip_pairs, "skip entry", skip, A.n_skip_pairs);
+            if constexpr (kCouple) {
+                JAAD_BOUND(ci, f, A.cce_off[f] <= A.cce_off[f + 1] && A.cce_off[f + 1] <= A.n_cce_terms, "coupling terms",
+                           A.cce_off[f + 1], A.n_cce_terms);
             }
 
             // ---------------- side info ----------------
@@ -1412,13 +1547,13 @@ __global__ __launch_bounds__(64 * waves_per_wg<kMode == 1 || kMode == 3>()) void
                 }
                 float* const bufs[2] = {W.buf, W.rsp};
                 f2 cx[2][8];
-                imdct_long_pk<2>(bufs, T, lane_id(), cx);
-                ola_long_pk(T, FrameCtx{iL.seq, iL.shape, iL.shape_prev}, cx[0], ovL, outL);
-                ola_long_pk(T, FrameCtx{iR.seq, iR.shape, iR.shape_prev}, cx[1], ovR, outR);
+                imdct_long_pk<2, kFast>(bufs, T, lane_id(), cx);
+                ola_long_pk<kFast>(T, FrameCtx{iL.seq, iL.shape, iL.shape_prev}, cx[0], ovL, outL);
+                ola_long_pk<kFast>(T, FrameCtx{iR.seq, iR.shape, iR.shape_prev}, cx[1], ovR, outR);
                 wave_sync();
             } else {
-                synth_channel<kTnsSpec, kMode == 3>(A, T, W, W.buf, iL, cf0, ovL, outL, f, 0);
-                if (stereo) synth_channel<kTnsSpec, kMode == 3>(A, T, W, W.rsp, iR, cf0 + 1, ovR, outR, f, 1);
+                synth_channel<kTnsSpec, kMode == 3, kFast>(A, T, W, W.buf, iL, cf0, ovL, outL, f, 0);
+                if (stereo) synth_channel<kTnsSpec, kMode == 3, kFast>(A, T, W, W.rsp, iR, cf0 + 1, ovR, outR, f, 1);
             }
             STAMP(8);
             // frame f+1's inputs (loaded since the IQ, a whole IMDCT ago) are in registers before
@@ -1448,10 +1583,17 @@ __global__ __launch_bounds__(64 * waves_per_wg<kMode == 1 || kMode == 3>()) void
                     }
                     wave_sync();
                 } else if constexpr (out_f32) {  // tolerance/debug format: strided stores
-                    if (emit) {
-                        float2* dst = reinterpret_cast<float2*>(reinterpret_cast<uint8_t*>(A.pcm) + (size_t)f * 8192);
+                    // through a buffer resource over exactly the frame's 8192 bytes, as the int16
+                    // form: a prefix frame's stores land past it and are dropped by the hardware,
+                    // and no store of this form can leave its frame (round 6: it was the one LC
+                    // output form whose addresses no resource bounded)
+                    typedef unsigned v2u __attribute__((ext_vector_type(2)));
+                    const __amdgpu_buffer_rsrc_t dst = frame_rsrc(reinterpret_cast<uint8_t*>(A.pcm) + (size_t)f * 8192, 8192);
+                    const int drop8 = emit ? 0 : 8192;
 #pragma unroll
-                        for (int o = 0; o < 16; o++) dst[long_pos(u2, o)] = make_float2(outL[o], stereo ? outR[o] : outL[o]);
+                    for (int o = 0; o < 16; o++) {
+                        const v2u w = {__float_as_uint(outL[o]), __float_as_uint(stereo ? outR[o] : outL[o])};
+                        __builtin_amdgcn_raw_buffer_store_b64(w, dst, 8 * long_pos(u2, o) + drop8, 0, 0);
                     }
                 } else {
                     // word P = (L_P, R_P), staged in buf; big endian swaps the bytes of each sample.
@@ -1528,6 +1670,7 @@ static hipError_t launch_lc_ch(const KernelArgs& a, hipStream_t stream, bool tns
     if (a.cce_off && tns_spec) launch_lc_mode<3, kStereo>(a, stream);  // coupling around the spec TNS filters
     else if (a.cce_off) launch_lc_mode<2, kStereo>(a, stream);
     else if (tns_spec) launch_lc_mode<1, kStereo>(a, stream);
+    else if (a.precision == JAAD_PRECISION_LSB1) launch_lc_mode<4, kStereo>(a, stream);
     else launch_lc_mode<0, kStereo>(a, stream);
     return hipGetLastError();
 }

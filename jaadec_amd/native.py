@@ -27,6 +27,7 @@ CCE_GAIN_MAX = float(2 ** 60)  # jaad_gpu.h JAAD_CCE_GAIN_MAX
 ONLY_LONG_SEQUENCE, LONG_START_SEQUENCE, EIGHT_SHORT_SEQUENCE, LONG_STOP_SEQUENCE = 0, 1, 2, 3
 ZERO_HCB, NOISE_HCB, INTENSITY_HCB2, INTENSITY_HCB = 0, 13, 14, 15
 TNS_COMPAT, TNS_SPEC = 0, 1
+PRECISION_EXACT, PRECISION_LSB1 = 0, 1  # jaad_stream_cfg.precision (JAAD_PRECISION_*)
 PCM_BIG_ENDIAN, PCM_LITTLE_ENDIAN, PCM_FLOAT32 = 0, 1, 2
 ICS_HAS_PNS, ICS_HAS_IS, ICS_TNS, ICS_MS_PRESENT, ICS_COMMON_WINDOW = 1, 2, 4, 8, 16
 
@@ -62,7 +63,7 @@ assert CCE_TERM_DTYPE.itemsize == 488
 class StreamCfg(C.Structure):
     _fields_ = [("abi_version", C.c_uint32), ("profile", C.c_uint8), ("sf_index", C.c_uint8),
                 ("channel_config", C.c_uint8), ("tns_mode", C.c_uint8), ("sbr", C.c_uint8), ("ps", C.c_uint8),
-                ("ext_sf_index", C.c_uint8), ("reserved", C.c_uint8)]
+                ("ext_sf_index", C.c_uint8), ("precision", C.c_uint8)]
 
 
 class BatchStruct(C.Structure):
@@ -350,20 +351,21 @@ def synth_batch(p: SynthParams, with_tns: bool | None = None, threads: int = 0) 
 
 
 def make_cfg(sf_index: int = 3, channel_config: int = 2, tns_mode: int = TNS_COMPAT, sbr: bool = False,
-             ps: bool = False, down: bool = False) -> StreamCfg:
+             ps: bool = False, down: bool = False, precision: int = PRECISION_EXACT) -> StreamCfg:
     """jaad_stream_cfg; with sbr the output rate is twice the core rate (index - 3), or the core
-    rate itself with down (downsampled SBR: extension rate = core rate)."""
+    rate itself with down (downsampled SBR: extension rate = core rate).  precision:
+    PRECISION_EXACT (bit-identical to the reference's arithmetic) or PRECISION_LSB1 (+-1 LSB)."""
     sbr = sbr or ps
     return StreamCfg(ABI_VERSION, 2, sf_index, channel_config, tns_mode, int(sbr), int(ps),
-                     (sf_index if down else sf_index - 3) if sbr else 0, 0)
+                     (sf_index if down else sf_index - 3) if sbr else 0, precision)
 
 
 def sbr_downsampled(cfg: StreamCfg) -> bool:
     return bool(cfg.sbr) and cfg.ext_sf_index == cfg.sf_index
 
 
-def cfg_for(p: SynthParams, tns_mode: int = TNS_COMPAT) -> StreamCfg:
-    return make_cfg(p.sf_index, p.channel_config, tns_mode, bool(p.sbr), p.sbr == 2)
+def cfg_for(p: SynthParams, tns_mode: int = TNS_COMPAT, precision: int = PRECISION_EXACT) -> StreamCfg:
+    return make_cfg(p.sf_index, p.channel_config, tns_mode, bool(p.sbr), p.sbr == 2, precision=precision)
 
 
 # channel elements of the AAC-LC multichannel configurations (0 SCE, 1 CPE, 3 LFE; ISO/IEC 14496-3

@@ -30,14 +30,13 @@ def rank_batch(batch: Batch, world: int, rank: int) -> Batch:
 
 
 def reduce_max_time(seconds: float, group=None) -> float:
-    """Max over ranks of a wall time (the benchmark's only collective)."""
+    """Max over ranks of a wall time (the benchmark's only collective besides its barrier and frame
+    count): a host scalar, reduced over the bench's gloo group."""
     import torch
     import torch.distributed as dist
 
     if not dist.is_available() or not dist.is_initialized() or dist.get_world_size() == 1:
         return seconds
-    backend = dist.get_backend(group)
-    dev = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")
-    t = torch.tensor([seconds], dtype=torch.float64, device=dev)
+    t = torch.tensor([seconds], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
     return float(t.item())

@@ -5,7 +5,8 @@ box state hit all alike.  Prints per lib: median / min ms per batch over the blo
     python scripts/ab_inproc.py CONFIG BLOCKS LAUNCHES_PER_BLOCK lib1.so lib2.so ...
 
 A lib argument may carry environment settings applied before its context is created, e.g.
-``lib_b.so@JAAD_LC_PAIR=0`` (copies of one build then differ only in those settings).
+``lib_b.so@JAAD_LC_PAIR=0`` (copies of one build then differ only in those settings), or
+``lib.so@precision=1`` (the context's jaad_stream_cfg.precision).
 """
 import os
 import hashlib
@@ -41,16 +42,21 @@ def main():
     runs = []
     for arg in paths:
         path, *envs = arg.split("@")
+        ccfg = N.cfg_for(p)
         for kv in envs:
             k, v = kv.split("=", 1)
-            os.environ[k] = v
+            if k == "precision":  # a jaad_stream_cfg field, not an environment setting
+                ccfg.precision = int(v)
+            else:
+                os.environ[k] = v
         L = N.load_lib(path)
         N._lib = L
-        ctx = N.Context(cfg, int(b.stream_slot.max()) + 1)
+        ctx = N.Context(ccfg, int(b.stream_slot.max()) + 1)
         pcm = torch.empty(b.n_frames * N.pcm_frame_bytes(0, bool(p.sbr)), dtype=torch.uint8, device=dev)
         runs.append((Path(path).stem + ("@" + "@".join(envs) if envs else ""), L, ctx, pcm, []))
         for kv in envs:
-            os.environ.pop(kv.split("=", 1)[0], None)
+            if not kv.startswith("precision="):
+                os.environ.pop(kv.split("=", 1)[0], None)
     import time
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < 0.4:  # warm-up past the GPU clock's load-onset transient
@@ -71,9 +77,12 @@ def main():
             torch.cuda.synchronize()
             times.append(ev[0].elapsed_time(ev[1]) / per)
         print(f"block {blk}: " + "  ".join(f"{r[0]} {r[4][-1]:.4f}" for r in runs), flush=True)
+    ref = runs[0][3].cpu().numpy().view(">i2").astype(np.int32)
     for name, L, ctx, pcm, times in runs:
         h = hashlib.blake2b(pcm.cpu().numpy().tobytes(), digest_size=6).hexdigest()
-        print(f"{name:24s} median {np.median(times):.4f} min {np.min(times):.4f} ms  pcm {h}")
+        d = np.abs(pcm.cpu().numpy().view(">i2").astype(np.int32) - ref)
+        print(f"{name:24s} median {np.median(times):.4f} min {np.min(times):.4f} ms  pcm {h}  "
+              f"vs first: max |d| {d.max()} LSB, {int((d != 0).sum())} samples differ")
     for name, L, ctx, pcm, times in runs:
         N._lib = L
         ctx.close()

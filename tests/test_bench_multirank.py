@@ -62,7 +62,7 @@ def _worker(rank, world, port, q):
     import torch.distributed as dist
 
     try:
-        line, pcm = bench.run(bench.parse(SMALL + ["--gpus", str(world)]), engine_cls=OracleEngine, backend="gloo")
+        line, pcm = bench.run(bench.parse(SMALL + ["--gpus", str(world)]), engine_cls=OracleEngine)
         got = [None] * world
         dist.all_gather_object(got, pcm.tobytes())
         if rank == 0:
@@ -138,7 +138,7 @@ def test_gloo_world2_bench_line_and_pcm_match_world1(monkeypatch):
         monkeypatch.delenv(k, raising=False)
     args = bench.parse(["--config", "2", "--steps", "2", "--warmup", "2", "--settle", "0.02", "--no-cpu", "--no-e2e", "--no-host",
                         "--streams-per-gpu", "6", "--frames-per-stream", "6"])
-    line1, pcm1 = bench.run(args, engine_cls=OracleEngine, backend="gloo")
+    line1, pcm1 = bench.run(args, engine_cls=OracleEngine)
     assert line1["n_gpus"] == 1
     assert b"".join(got) == pcm1.tobytes()
 
@@ -150,7 +150,7 @@ def _gpu_worker(rank, world, port, q):
     import torch.distributed as dist
 
     try:
-        line, pcm = bench.run(bench.parse(SMALL + ["--gpus", str(world)]), backend="gloo")
+        line, pcm = bench.run(bench.parse(SMALL + ["--gpus", str(world)]))
         got = [None] * world
         dist.all_gather_object(got, pcm.tobytes())
         if rank == 0:

@@ -382,3 +382,26 @@ def test_coupling_with_ps_time_slices():
     want = O.decode_batch(cfg, b.select_runs(list(runs)), O.Streams(16), N.PCM_BIG_ENDIAN, threads=8)
     fb = b.frame_begin
     assert (np.concatenate([got[fb[r]:fb[r + 1]] for r in runs]) == want).all()
+
+
+@pytest.mark.parametrize("fps,pieces", [(3, 8), (4, 6)])
+def test_ps_time_slices_with_runs_shorter_than_the_slice_count(fps, pieces, monkeypatch):
+    """HE-AAC v2 time slices of runs shorter than P frames -- some slices then hold
+    no frame at all.  Every non-empty slice's PCM goes through the two page-locked staging slots
+    (pageable output) and must reach the caller: == the device entry over the whole batch, and ==
+    the restatement on a sample of streams.  (Before round 6 the staging slot was picked by piece
+    index, so the PCM of the piece two before an empty one was never copied out.)"""
+    n_streams = (2048 * pieces + fps - 1) // fps  # P = min(JAAD_SBR_PIECES, frames / 2048) slices
+    p = N.synth_params(5, n_streams=n_streams, frames_per_stream=fps)
+    b = N.synth_batch(p)
+    cfg = N.cfg_for(p)
+    monkeypatch.setenv("JAAD_SBR_PIECES", str(pieces))
+    with N.Context(cfg, n_streams) as ctx:
+        got = ctx.decode(b, N.PCM_BIG_ENDIAN)
+    want = _device_decode(cfg, b, n_streams, N.PCM_BIG_ENDIAN)
+    bad = np.flatnonzero((got != want).any(axis=1))
+    assert bad.size == 0, f"{bad.size} frames differ, first {bad[:8]}"
+    runs = [0, n_streams // 2, n_streams - 1]
+    o = O.decode_batch(cfg, b.select_runs(runs), O.Streams(n_streams), N.PCM_BIG_ENDIAN, threads=8)
+    fb = b.frame_begin
+    assert (np.concatenate([got[fb[r]:fb[r + 1]] for r in runs]) == o).all()

@@ -188,3 +188,31 @@ def test_c3_full_batch_bitexact():
     assert (seqs > 0).all(), seqs
     assert b.tns is not None and (b.tns["n_filters"] > 0).mean() > 0.3  # TNS data in ~50 % of ch-frames
     _assert_pcm_equal(got, want, N.PCM_FLOAT32)
+
+
+@pytest.mark.parametrize("cfg_id", [2, 3])
+def test_float32_output_stays_inside_its_frames(cfg_id, monkeypatch):
+    """the float32 PCM form goes through a buffer resource over exactly its frame, as
+    the int16 form does.  Device entry into a buffer with guard frames on both sides: chunks that
+    re-decode a prefix frame (runs of 40 frames: several chunks each) leave the guards untouched,
+    and the rows equal the host entry's."""
+    import torch
+    p = N.synth_params(cfg_id, n_streams=8, frames_per_stream=40)
+    b = N.synth_batch(p)
+    cfg = N.make_cfg()
+    with N.Context(cfg, 8) as ctx:
+        want = ctx.decode(b, N.PCM_FLOAT32)
+    dev = torch.device("cuda", 0)
+    t = lambda a: None if a is None else torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1)).to(dev)
+    d = {k: t(getattr(b, k)) for k in ("q", "sf", "cb", "ics", "ms_used", "tns")}
+    ptr = {k: (v.data_ptr() if v is not None else None) for k, v in d.items()}
+    nb = 8192
+    guard = 2
+    pcm = torch.full(((b.n_frames + 2 * guard) * nb,), 0x7F, dtype=torch.uint8, device=dev)
+    monkeypatch.setenv("JAAD_CHUNK_FRAMES", "9")  # (read at context creation) prefix frames in every run
+    with N.Context(cfg, 8) as ctx:
+        ctx.decode_device(ptr, b, pcm.data_ptr() + guard * nb, b.n_frames * nb, N.PCM_FLOAT32)
+        ctx.wait()
+    host = pcm.cpu().numpy().reshape(-1, nb)
+    assert (host[:guard] == 0x7F).all() and (host[-guard:] == 0x7F).all()
+    assert (host[guard:-guard] == want).all()
