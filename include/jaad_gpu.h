@@ -68,7 +68,13 @@ enum {
 enum {
     JAAD_PCM_BIG_ENDIAN = 0u,     /* SampleBuffer default (S/SampleBuffer.java:28-30)            */
     JAAD_PCM_LITTLE_ENDIAN = 1u,  /* SampleBuffer.setBigEndian(false)                             */
-    JAAD_PCM_FLOAT32 = 2u         /* native-endian f32 samples BEFORE Math.round (tolerance checks) */
+    JAAD_PCM_FLOAT32 = 2u,        /* native-endian f32 samples BEFORE Math.round (tolerance checks) */
+    /* jaad_decode_batch_device only (a performance hint, never a change of output): the batch holds
+       EIGHT_SHORT_SEQUENCE frames -- the host parser saw their window_sequence -- so the kernel built
+       for mixed windows runs (a CPE's two short-window transforms in lockstep).  Without it the
+       long-window kernel decodes short frames too, one channel after the other.  jaad_decode_batch
+       scans the side info itself and ignores the bit. */
+    JAAD_HINT_SHORT_WINDOWS = 1u << 8
 };
 
 /*

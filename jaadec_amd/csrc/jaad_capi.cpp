@@ -209,9 +209,10 @@ struct jaad_ctx {
     PinnedBuf h_chunks[2];                   // staging of each slot's upload
     hipEvent_t chunks_copied[2] = {};        // h_chunks[i] may be rewritten once this has completed
     bool chunks_live[2] = {false, false};
-    hipEvent_t chunks_read[2] = {};          // d_chunks[i] may be rewritten once this has completed (after
-    bool chunks_read_live[2] = {false, false};  // the last LC launch that read it; round 6)
+    hipEvent_t chunks_read[2] = {};          // d_chunks[i] may be rewritten once this has completed (recorded
+    bool chunks_read_live[2] = {false, false};  // when plan() left slot i; round 6)
     int chunk_slot = 0;                      // slot of the current plan
+    bool hint_short = false;                 // the current call's batch holds EIGHT_SHORT frames (KernelArgs::short_pair)
     // Every call's device work (whatever stream it is queued on) waits for the previous call's
     // `done`: the chunk table, the double-buffered state and the SBR/PS state are reused call
     // after call.  The state_* entry points and jaad_wait wait for it too.
@@ -328,6 +329,13 @@ void build_lds_tables(int sf_index, LdsTables* t, GlobalTables* gt)
         root(4 * p, t->tw3[0][u]);
         for (int e = 0; e < 2; e++) root(2 * (p + 64 * e), t->tw3[1 + e][u]);
         for (int s = 0; s < 4; s++) root(p + 64 * s, t->tw3[3 + s][u]);
+    }
+    // radix-8 twiddles of the +-1 LSB kernel (jaad_lc.hip fft_r8_pass): register r holds the
+    // sub-transform bitrev3(r) of its pass
+    for (int r = 1; r < 8; r++) {
+        const int m = ((r & 1) << 2) | (r & 2) | ((r >> 2) & 1);
+        for (int b = 0; b < 8; b++) root(8 * m * b, t->tw2f[r - 1][b]);
+        for (int u = 0; u < 64; u++) root(m * lane_pos_host(u), t->tw3f[r - 1][u]);
     }
     std::memcpy(t->mdct_s, JAAD_MDCT_TABLE_128, sizeof(t->mdct_s));
     for (int k = 0; k < 32; k++) {
@@ -511,9 +519,13 @@ int plan(jaad_ctx* ctx, const jaad_batch* b, hipStream_t stream, uint32_t size_f
     const size_t bytes = cbytes + ctx->skips.size() * sizeof(uint32_t);
     const int slot = ctx->chunk_slot ^ 1;  // (the current plan's slot may still be read by queued kernels)
     if (ctx->chunks_live[slot]) HIPCHK(hipEventSynchronize(ctx->chunks_copied[slot]));  // staging in use?
-    // the slot's device table may still be read by the LC kernels of the plan before last (queued on
-    // another stream, or not yet run): its upload waits for them on the device, a reallocation of
-    // the table on the host (hipFree under a running kernel)
+    // Every LC launch that read the current plan's table was queued by an earlier call or piece
+    // (this one is ordered after them on `stream`, launch()), so an event here marks the end of
+    // its readers; the other slot's readers ended at the event recorded when it was left, which
+    // its upload waits for on the device (a reallocation of the table on the host: hipFree under
+    // a running kernel).  One event per plan switch, none per call.
+    HIPCHK(hipEventRecord(ctx->chunks_read[ctx->chunk_slot], stream));
+    ctx->chunks_read_live[ctx->chunk_slot] = true;
     if (ctx->chunks_read_live[slot]) {
         if (bytes + 16 > ctx->d_chunks[slot].cap) HIPCHK(hipEventSynchronize(ctx->chunks_read[slot]));
         else HIPCHK(hipStreamWaitEvent(stream, ctx->chunks_read[slot], 0));
@@ -537,14 +549,6 @@ int plan(jaad_ctx* ctx, const jaad_batch* b, hipStream_t stream, uint32_t size_f
     ctx->plan_skips = ctx->skips;
     ctx->plan_n_chunks = (uint32_t)ctx->chunks.size();
     ctx->plan_valid = true;
-    return JAAD_OK;
-}
-
-// the current plan's device chunk table has been read by every LC launch queued so far on `stream`
-int mark_chunks_read(jaad_ctx* ctx, hipStream_t stream)
-{
-    HIPCHK(hipEventRecord(ctx->chunks_read[ctx->chunk_slot], stream));
-    ctx->chunks_read_live[ctx->chunk_slot] = true;
     return JAAD_OK;
 }
 
@@ -1179,6 +1183,7 @@ int launch_work(jaad_ctx* ctx, const jaad_batch* db, void* pcm, uint32_t flags, 
     // the fused (+-1 LSB) instantiation serves AAC-LC output only: an SBR context's core samples
     // feed the QMF analysis, whose stages are all kept exact
     a.precision = sbr ? (uint32_t)JAAD_PRECISION_EXACT : ctx->cfg.precision;
+    a.short_pair = ctx->hint_short ? 1u : 0u;
     if (a.n_chunks == 0) return JAAD_OK;
     if (db->n_cce_terms && (rc = setup_coupling(ctx, db, a, stream))) return rc;
     if (ctx->n_elem > 1) {
@@ -1209,7 +1214,6 @@ int launch_work(jaad_ctx* ctx, const jaad_batch* db, void* pcm, uint32_t flags, 
             ch0 += n;
             cpe += n == 2;
         }
-        if ((rc = mark_chunks_read(ctx, stream))) return rc;
         LAUNCHCHK(launch_pack(static_cast<const float*>(ctx->d_time.p), pcm, db->n_frames, ctx->nch, flags, stream, a.skips,
                               n_skip_runs(ctx)), stream);
         ctx->parity ^= 1;
@@ -1219,7 +1223,6 @@ int launch_work(jaad_ctx* ctx, const jaad_batch* db, void* pcm, uint32_t flags, 
     if (rc) return rc;
     const bool tns_spec = ctx->cfg.tns_mode == JAAD_TNS_SPEC && db->tns != nullptr;
     LAUNCHCHK(launch_lc(a, stream, tns_spec), stream);
-    if ((rc = mark_chunks_read(ctx, stream))) return rc;
     if (sbr && (rc = launch_sbr_stage(ctx, db, pcm, flags, stream))) return rc;
     ctx->parity ^= 1;
     return JAAD_OK;
@@ -1683,8 +1686,8 @@ static int check_batch(const jaad_ctx* ctx, const jaad_batch* b, size_t pcm_byte
     if (pcm_bytes < pcm_bytes_per_frame(ctx, flags) * b->n_frames) return JAAD_ERR_INVALID_ARG;
     if (flags & ~(uint32_t)(JAAD_PCM_LITTLE_ENDIAN | JAAD_PCM_FLOAT32)) return JAAD_ERR_INVALID_ARG;
     if (b->n_cce_terms) {  // dependent coupling (jaad_gpu.h); with SBR the core is coupled
-        // spec TNS: mono and stereo configurations (the coupling points around the filters, kernel mode 3)
-        if (ctx->cfg.tns_mode != JAAD_TNS_COMPAT && ctx->n_elem > 1) return JAAD_ERR_UNSUPPORTED;
+        // (spec TNS: kernel mode 3 couples around the filters; a multichannel configuration runs it
+        // per channel element, the terms' channels relative to the element, round 6)
         if (!b->cce_terms || !b->n_cce || !b->cce_q || !b->cce_sf || !b->cce_cb || !b->cce_ics) return JAAD_ERR_INVALID_ARG;
         if (b->n_cce > JAAD_CCE_MAX_RECORDS) return JAAD_ERR_UNSUPPORTED;  // jaad_cce_term.cce is 16-bit
         for (uint32_t t = 0; t < b->n_cce_terms; t++) {
@@ -1981,6 +1984,7 @@ static int decode_batch_pieces_impl(jaad_ctx* ctx, const jaad_batch* b, void* pc
     a.dbg_frame = ctx->dbg_frame;
     a.n_slots = ctx->n_slots;
     a.precision = ctx->cfg.precision;
+    a.short_pair = ctx->hint_short ? 1u : 0u;
     const bool tns_spec = ctx->cfg.tns_mode == JAAD_TNS_SPEC && b->tns != nullptr;
     int rc;
     if ((rc = carry_untouched(ctx, a.state_out, a.state_in, 2048, s))) return rc;
@@ -2073,7 +2077,6 @@ static int decode_batch_pieces_impl(jaad_ctx* ctx, const jaad_batch* b, void* pc
         HIPCHK(hipEventRecord(ctx->ev_out[i], ctx->d2h));
         queued = i + 1;
     }
-    if ((rc = mark_chunks_read(ctx, s))) return rc;
     if (!pin_out)
         for (int i = std::max(0, queued - kStageSlots); i < queued; i++)
             if ((rc = copy_out(i))) return rc;
@@ -2475,10 +2478,24 @@ static int dropped_frames(const jaad_batch* b)
 
 static int decode_batch_whole(jaad_ctx* ctx, const jaad_batch* b, void* pcm_out, uint32_t flags);
 
+// any EIGHT_SHORT frame among the batch's channel-frames (the host entry's own scan for the
+// mixed-window kernel, KernelArgs::short_pair); multichannel elements decode per element and keep
+// the per-channel short path
+static void set_short_hint(jaad_ctx* ctx, const jaad_batch* b)
+{
+    bool any = false;
+    if (ctx->n_elem == 1 && ctx->nch == 2 && b->ics)
+        for (size_t i = 0, n = (size_t)b->n_frames * ctx->nch; i < n && !any; i++)
+            any = b->ics[i].window_sequence == JAAD_EIGHT_SHORT_SEQUENCE;
+    ctx->hint_short = any;
+}
+
 int jaad_decode_batch(jaad_ctx* ctx, const jaad_batch* b, void* pcm_out, size_t pcm_bytes, uint32_t flags)
 {
+    flags &= ~(uint32_t)JAAD_HINT_SHORT_WINDOWS;  // (a device-entry hint: the host entry scans)
     int rc = check_batch(ctx, b, pcm_bytes, flags);
     if (rc) return rc;
+    set_short_hint(ctx, b);
     if (!pcm_out && b->n_frames) return JAAD_ERR_INVALID_ARG;
     const int dropped = dropped_frames(b);
     if (dropped < 0) return dropped;
@@ -2586,8 +2603,11 @@ int jaad_host_free(jaad_ctx* ctx, void* p)
 int jaad_decode_batch_device(jaad_ctx* ctx, const jaad_batch* b, void* pcm_dev, size_t pcm_bytes, uint32_t flags,
                              void* hip_stream)
 {
+    const bool hint = (flags & JAAD_HINT_SHORT_WINDOWS) != 0;
+    flags &= ~(uint32_t)JAAD_HINT_SHORT_WINDOWS;
     int rc = check_batch(ctx, b, pcm_bytes, flags);
     if (rc) return rc;
+    if (ctx) ctx->hint_short = hint && ctx->n_elem == 1 && ctx->nch == 2;
     if (!pcm_dev && b->n_frames) return JAAD_ERR_INVALID_ARG;
     HIPCHK(hipSetDevice(ctx->device));
     hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : ctx->stream;
@@ -2607,7 +2627,26 @@ int jaad_wait(jaad_ctx* ctx)
 int jaad_ctx_core_channels(const jaad_ctx* ctx) { return ctx ? ctx->nch : JAAD_ERR_INVALID_ARG; }
 
 // per-slot state blob: core overlap [2][1024] f32 | (SBR) device SbrChState[2] | host SbrHostSlot
-// | (PS) device PsState
+// | (PS) device PsState | trailer (round 6, ADVICE r5: a blob names its layout version and the
+// context kind it was written by; an import checks both, so a blob of another build or of another
+// kind of context is refused instead of being read as raw struct bytes)
+struct StateTrailer {
+    uint32_t magic, version, kind, payload;
+};
+constexpr uint32_t kStateMagic = 0x4441414Au;  // "JAAD"
+constexpr uint32_t kStateVersion = 6;          // layout of round 6 (SbrHostSlot with blim_hw)
+static size_t state_payload_bytes(const jaad_ctx* ctx)
+{
+    return (size_t)ctx->n_elem * 2048 * sizeof(float) + (ctx->cfg.sbr ? 2 * sizeof(SbrChState) + sizeof(SbrHostSlot) : 0) +
+           (ctx->cfg.ps ? sizeof(PsState) : 0);
+}
+static StateTrailer state_trailer(const jaad_ctx* ctx)
+{
+    const uint32_t kind = (uint32_t)ctx->n_elem | (uint32_t)ctx->cfg.sbr << 8 | (uint32_t)ctx->cfg.ps << 9 |
+                          (uint32_t)sbr_downsampled(ctx->cfg) << 10 | (uint32_t)ctx->cfg.ext_sf_index << 16;
+    return StateTrailer{kStateMagic, kStateVersion, kind, (uint32_t)state_payload_bytes(ctx)};
+}
+
 size_t jaad_state_bytes(const jaad_ctx* ctx)
 {
     if (!ctx) return 0;
@@ -2616,8 +2655,7 @@ size_t jaad_state_bytes(const jaad_ctx* ctx)
         for (const jaad_ctx* c : ctx->children) n += jaad_state_bytes(c);
         return n;
     }
-    return (size_t)ctx->n_elem * 2048 * sizeof(float) + (ctx->cfg.sbr ? 2 * sizeof(SbrChState) + sizeof(SbrHostSlot) : 0) +
-           (ctx->cfg.ps ? sizeof(PsState) : 0);
+    return state_payload_bytes(ctx) + sizeof(StateTrailer);
 }
 
 int jaad_state_export(jaad_ctx* ctx, uint32_t slot, void* buf, size_t bytes)
@@ -2638,13 +2676,15 @@ int jaad_state_export(jaad_ctx* ctx, uint32_t slot, void* buf, size_t bytes)
         HIPCHK(hipMemcpy(o + (size_t)k * 2048 * sizeof(float), ctx->d_state[ctx->parity] + ((size_t)k * ctx->n_slots + slot) * 2048,
                          2048 * sizeof(float), hipMemcpyDeviceToHost));
     if (ctx->cfg.sbr) {
-        o += 2048 * sizeof(float);
-        HIPCHK(hipMemcpy(o, ctx->d_sbr_state + (size_t)slot * 2, 2 * sizeof(SbrChState), hipMemcpyDeviceToHost));
-        std::memcpy(o + 2 * sizeof(SbrChState), &ctx->sbr_slots[slot], sizeof(SbrHostSlot));
+        char* q = o + 2048 * sizeof(float);
+        HIPCHK(hipMemcpy(q, ctx->d_sbr_state + (size_t)slot * 2, 2 * sizeof(SbrChState), hipMemcpyDeviceToHost));
+        std::memcpy(q + 2 * sizeof(SbrChState), &ctx->sbr_slots[slot], sizeof(SbrHostSlot));
         if (ctx->cfg.ps)
-            HIPCHK(hipMemcpy(o + 2 * sizeof(SbrChState) + sizeof(SbrHostSlot), ctx->d_ps_state + slot, sizeof(PsState),
+            HIPCHK(hipMemcpy(q + 2 * sizeof(SbrChState) + sizeof(SbrHostSlot), ctx->d_ps_state + slot, sizeof(PsState),
                              hipMemcpyDeviceToHost));
     }
+    const StateTrailer t = state_trailer(ctx);
+    std::memcpy(o + state_payload_bytes(ctx), &t, sizeof t);
     return JAAD_OK;
 }
 
@@ -2653,6 +2693,11 @@ int jaad_state_export(jaad_ctx* ctx, uint32_t slot, void* buf, size_t bytes)
 // multichannel context, every element's slot) as it was
 static int state_blob_check(jaad_ctx* ctx, const char* in, SbrHostSlot* hs)
 {
+    StateTrailer t;
+    std::memcpy(&t, in + state_payload_bytes(ctx), sizeof t);
+    const StateTrailer want = state_trailer(ctx);
+    if (t.magic != want.magic || t.version != want.version || t.kind != want.kind || t.payload != want.payload)
+        return JAAD_ERR_INVALID_ARG;
     for (int k = 0; k < ctx->n_elem; k++) {  // the overlap must be finite (the LC kernel's PCM rounding relies on it, jaad_lc.hip round_pk16)
         float ov[2048];
         std::memcpy(ov, in + (size_t)k * sizeof ov, sizeof ov);
@@ -2665,6 +2710,10 @@ static int state_blob_check(jaad_ctx* ctx, const char* in, SbrHostSlot* hs)
             hs->table = ctx->sbr_host->table_index(*hs);
             if (hs->table < 0) return JAAD_ERR_INVALID_ARG;
         }
+        // the PS kernels skip bands at or above the stream's band high-water mark; an imported
+        // value is not trusted (a lower one would drop live all-pass state): all 64 bands, which
+        // decodes identically (a band that never had input keeps zero state either way)
+        hs->blim_hw = 64;
     }
     return JAAD_OK;
 }

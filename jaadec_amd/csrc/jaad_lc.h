@@ -43,6 +43,11 @@ struct alignas(16) LdsTables {
     uint8_t quad2band_l[256];   // long window: scalefactor band of bins 4i..4i+3 (255 = none)
     uint8_t quad2band_s[32];    // short window
     int32_t nswb_l, nswb_s, tns_max_l, tns_max_s;
+    // +-1 LSB kernel (mode 4): the 512-point IFFT's passes 2 and 3 as radix-8 butterflies, the
+    // twiddles of register r (r = 1..7) applied before each pass's 8-point DFT: pass 2
+    // W64^(bitrev3(r) * (lane >> 3)), pass 3 W512^(bitrev3(r) * lane_pos(lane)) (FFT_TABLE_512 entries)
+    float tw2f[7][8][2];
+    float tw3f[7][64][2];
 };
 
 // Tables only the slow paths (PNS, spec TNS) need; read from global memory.
@@ -99,6 +104,10 @@ struct KernelArgs {
     // jaad_stream_cfg.precision: JAAD_PRECISION_LSB1 selects the fused-multiply-add instantiation of
     // the TNS-compat, uncoupled kernel (mode 4); every other mode stays bit-exact
     uint32_t precision;
+    // the batch holds EIGHT_SHORT frames (the host scanned its side info, or the device-entry caller
+    // said so: JAAD_HINT_SHORT_WINDOWS): the mixed-window instantiation (modes 5, 6) runs a CPE's
+    // two short-window transforms in lockstep.  Either instantiation decodes every window sequence.
+    uint32_t short_pair;
 };
 
 // inputs of cce_term_kernel: one wave per term

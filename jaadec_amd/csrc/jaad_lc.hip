@@ -333,6 +333,130 @@ __device__ __forceinline__ void fft_3stages_pk2(f2 (&c)[8], f2 (&d)[8], TW tw)
     for (int s = 0; s < 4; s++) bfly_t2<F>(c[s], c[s + 4], d[s], d[s + 4], tw(3 + s));
 }
 
+// ---- +-1 LSB kernel: the IFFT's 8-point stages with their trivial twiddles exact ----
+// The reference's stage twiddles are FFT_TABLE_512 entries throughout (FFT.java:113-130); the fused
+// kernel multiplies by 1, i, W8 = sqrt(1/2) (1 + i) and W8^3 exactly (their table values differ
+// from these by <= 2.4e-6), so a butterfly by 1 or i is two packed additions and one by W8 or W8^3
+// three packed operations.  Passes 2 and 3 become radix-8 butterflies: register r first takes
+// the twiddle of its sub-transform (LdsTables::tw2f / tw3f), then one 8-point DFT -- the same
+// transform as the three radix-2 stages (checked against them in float64 when this was written),
+// with 26 + 14 packed operations per pass instead of 48.
+__device__ __forceinline__ f2 pkfma(f2 a, f2 b, f2 c)  // a * b + c
+{
+    f2 r;
+    asm("v_pk_fma_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+__device__ __forceinline__ f2 pkfma_n(f2 a, f2 b, f2 c)  // -a * b + c
+{
+    f2 r;
+    asm("v_pk_fma_f32 %0, %1, %2, %3 neg_lo:[1,0,0] neg_hi:[1,0,0]" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+__device__ __forceinline__ f2 pkfma_i(f2 a, f2 b, f2 c)  // (i a) * b + c = (-a.y, a.x) * b + c
+{
+    f2 r;
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[0,1,1] neg_lo:[1,0,0]" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+__device__ __forceinline__ f2 pkfma_ni(f2 a, f2 b, f2 c)  // -(i a) * b + c = (a.y, -a.x) * b + c
+{
+    f2 r;
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[0,1,1] neg_hi:[1,0,0]" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+__device__ __forceinline__ f2 sqrt_half2() { return f2{0.70710678118654752f, 0.70710678118654752f}; }
+// a, b = a + b, a - b
+__device__ __forceinline__ void bf1(f2& a, f2& b)
+{
+    const f2 t = a;
+    a = t + b;
+    b = t - b;
+}
+// a, b = a + i b, a - i b
+__device__ __forceinline__ void bfi(f2& a, f2& b)
+{
+    const f2 t = a;
+    a = pk_rot_p(t, b);
+    b = pk_rot_m(t, b);
+}
+// a, b = a + W8 b, a - W8 b   (W8 b = sqrt(1/2) u, u = (1 + i) b)
+__device__ __forceinline__ void bf8(f2& a, f2& b, f2 h)
+{
+    const f2 u = pk_rot_p(b, b), t = a;
+    a = pkfma(u, h, t);
+    b = pkfma_n(u, h, t);
+}
+// a, b = a + W8^3 b, a - W8^3 b   (W8^3 b = sqrt(1/2) i u)
+__device__ __forceinline__ void bf83(f2& a, f2& b, f2 h)
+{
+    const f2 u = pk_rot_p(b, b), t = a;
+    a = pkfma_i(u, h, t);
+    b = pkfma_ni(u, h, t);
+}
+// 8-point DFT of registers holding the sub-transforms in bit-reversed order (fft_3stages_pk's
+// structure with twiddles 1 | 1, i | 1, W8, i, W8^3), N channels operation by operation
+template <int N>
+__device__ __forceinline__ void dft8_r8(f2 (&c)[N][8])
+{
+    const f2 h = sqrt_half2();
+#pragma unroll
+    for (int s = 0; s < 8; s += 2)
+#pragma unroll
+        for (int n = 0; n < N; n++) bf1(c[n][s], c[n][s + 1]);
+#pragma unroll
+    for (int n = 0; n < N; n++) {
+        bf1(c[n][0], c[n][2]);
+        bf1(c[n][4], c[n][6]);
+    }
+#pragma unroll
+    for (int n = 0; n < N; n++) {
+        bfi(c[n][1], c[n][3]);
+        bfi(c[n][5], c[n][7]);
+    }
+#pragma unroll
+    for (int n = 0; n < N; n++) {
+        bf1(c[n][0], c[n][4]);
+        bfi(c[n][2], c[n][6]);
+    }
+#pragma unroll
+    for (int n = 0; n < N; n++) bf8(c[n][1], c[n][5], h);
+#pragma unroll
+    for (int n = 0; n < N; n++) bf83(c[n][3], c[n][7], h);
+}
+// pass 1 (FFT.java:69-108 radix-4, then the 8-point stage with twiddles W8^k, k = 0..3)
+template <int N>
+__device__ __forceinline__ void fft_pass1_r8(f2 (&c)[N][8])
+{
+    const f2 h = sqrt_half2();
+#pragma unroll
+    for (int n = 0; n < N; n++) {
+        radix4_pk(c[n][BR3[0]], c[n][BR3[1]], c[n][BR3[2]], c[n][BR3[3]]);
+        radix4_pk(c[n][BR3[4]], c[n][BR3[5]], c[n][BR3[6]], c[n][BR3[7]]);
+    }
+#pragma unroll
+    for (int n = 0; n < N; n++) {
+        bf1(c[n][BR3[0]], c[n][BR3[4]]);
+        bfi(c[n][BR3[2]], c[n][BR3[6]]);
+    }
+#pragma unroll
+    for (int n = 0; n < N; n++) bf8(c[n][BR3[1]], c[n][BR3[5]], h);
+#pragma unroll
+    for (int n = 0; n < N; n++) bf83(c[n][BR3[3]], c[n][BR3[7]], h);
+}
+// passes 2 and 3: register r (1..7) times tw(r - 1), then the 8-point DFT
+template <int N, typename TW>
+__device__ __forceinline__ void fft_pass_r8(f2 (&c)[N][8], TW tw)
+{
+#pragma unroll
+    for (int r = 1; r < 8; r++) {
+        const f2 w = tw(r - 1);
+#pragma unroll
+        for (int n = 0; n < N; n++) c[n][r] = cmul_fma(c[n][r], w);
+    }
+    dft8_r8<N>(c);
+}
+
 
 
 // Register transposes between the IFFT passes.  A pair of registers (a: register bit i clear,
@@ -534,24 +658,54 @@ __device__ __forceinline__ void imdct_long_pk(float* const (&bufs)[N], const Lds
             const f2 x = {bufs[n][eo_idx(1023 - 2 * k)], bufs[n][eo_idx(2 * k)]};
             c[n][s] = cmul_t<F>(x, ld2(T.mdct_l[k]));
         }
+    // (JAAD_ABL_* macros: ablation builds of the fused lockstep path, design tool -- wrong output,
+    // time only; scripts/build_exp.py)
+#if defined(JAAD_ABL_NOFFT)
+    constexpr bool kFft = !(F && N == 2);
+#else
+    constexpr bool kFft = true;
+#endif
+#if defined(JAAD_ABL_NODPP)
+    constexpr bool kDpp = !(F && N == 2);
+#else
+    constexpr bool kDpp = kFft;
+#endif
+#if defined(JAAD_ABL_NOPERM)
+    constexpr bool kPerm = !(F && N == 2);
+#else
+    constexpr bool kPerm = kFft;
+#endif
+#if defined(JAAD_NO_R8)  // (A/B builds: the fused kernel with the radix-2 stages)
+    constexpr bool kR8 = false;
+#else
+    constexpr bool kR8 = F;
+#endif
     // pass 1: register s holds e bits (s2, s1, s0) = e bits 0, 1, 2 (fft_pass1_pk's BR3 order)
-    if constexpr (N == 2) fft_pass1_pk2<F>(c[0], c[1], T.tw1);
+    if constexpr (!kFft) {
+    } else if constexpr (kR8) fft_pass1_r8<N>(c);
+    else if constexpr (N == 2) fft_pass1_pk2<F>(c[0], c[1], T.tw1);
     else fft_pass1_pk<F>(c[0], T.tw1);
 #pragma unroll
     for (int n = 0; n < N; n++) {
-        xch_bit<0, 5>(c[n], u);  // e bit 3 (lane bit 5) <-> e bit 2
-        xch_bit<1, 4>(c[n], u);  // e bit 4 (lane bit 4) <-> e bit 1
+        if constexpr (kPerm) {
+            xch_bit<0, 5>(c[n], u);  // e bit 3 (lane bit 5) <-> e bit 2
+            xch_bit<1, 4>(c[n], u);  // e bit 4 (lane bit 4) <-> e bit 1
+        }
         if constexpr (N == 1) xch_bit<2, 3>(c[n], u);  // e bit 5 (lane bit 3) <-> e bit 0
     }
-    if constexpr (N == 2) xch_bit_pair<2, 3>(c[0], c[1]);
+    if constexpr (N == 2 && kDpp) xch_bit_pair<2, 3>(c[0], c[1]);
     // pass 2: register bits 0,1,2 = e bits 3,4,5; e mod 8 = u >> 3
     const int b = u >> 3;
-    if constexpr (N == 2) fft_3stages_pk2<F>(c[0], c[1], [&](int j) { return ld2(T.tw2[j][b]); });
+    if constexpr (!kFft) {
+    } else if constexpr (kR8) fft_pass_r8<N>(c, [&](int j) { return ld2(T.tw2f[j][b]); });
+    else if constexpr (N == 2) fft_3stages_pk2<F>(c[0], c[1], [&](int j) { return ld2(T.tw2[j][b]); });
     else fft_3stages_pk<F>(c[0], [&](int j) { return ld2(T.tw2[j][b]); });
     if constexpr (N == 2) {
-        xch_bit_pair<0, 2>(c[0], c[1]);  // e bit 6 (lane bit 2) <-> e bit 3
-        xch_bit_pair<1, 1>(c[0], c[1]);  // e bit 7 (lane bit 1) <-> e bit 4
-        xch_bit_pair<2, 0>(c[0], c[1]);  // e bit 8 (lane bit 0) <-> e bit 5
+        if constexpr (kDpp) {
+            xch_bit_pair<0, 2>(c[0], c[1]);  // e bit 6 (lane bit 2) <-> e bit 3
+            xch_bit_pair<1, 1>(c[0], c[1]);  // e bit 7 (lane bit 1) <-> e bit 4
+            xch_bit_pair<2, 0>(c[0], c[1]);  // e bit 8 (lane bit 0) <-> e bit 5
+        }
     } else {
 #pragma unroll
         for (int n = 0; n < N; n++) {
@@ -561,7 +715,9 @@ __device__ __forceinline__ void imdct_long_pk(float* const (&bufs)[N], const Lds
         }
     }
     // pass 3: register bits 0,1,2 = e bits 6,7,8, e mod 64 = lane_pos(u)
-    if constexpr (N == 2) fft_3stages_pk2<F>(c[0], c[1], [&](int j) { return ld2(T.tw3[j][u]); });
+    if constexpr (!kFft) {
+    } else if constexpr (kR8) fft_pass_r8<N>(c, [&](int j) { return ld2(T.tw3f[j][u]); });
+    else if constexpr (N == 2) fft_3stages_pk2<F>(c[0], c[1], [&](int j) { return ld2(T.tw3[j][u]); });
     else fft_3stages_pk<F>(c[0], [&](int j) { return ld2(T.tw3[j][u]); });
     // MDCT.java:48-53: re = t0*c - t1*sn, im = t1*c + t0*sn = cmul((t0, t1), (c, sn))
 #pragma unroll
@@ -726,6 +882,67 @@ __device__ __forceinline__ void imdct_short_pk(float* buf, const LdsTables& T, i
     }
 }
 
+// imdct_short_pk on both channels of a CPE whose windows are both EIGHT_SHORT, in lockstep as the
+// long path runs its two IMDCTs: every LDS phase serves both spectra (one wave_sync each instead of
+// one per channel) and the two FFT chains interleave operation by operation, each channel's
+// operations those of imdct_short_pk.  Only the mixed-window instantiations (kernel modes 5, 6,
+// chosen per launch when the batch holds EIGHT_SHORT frames) carry it: in one kernel body with
+// the long path it cost C2's long frames 1-3 % (round 5, profiles/round5_short_pair/).
+template <bool F = false>
+__device__ __forceinline__ void imdct_short_pk2(float* bufL, float* bufR, const LdsTables& T, int u, float (&reL)[8],
+                                                float (&imL)[8], float (&reR)[8], float (&imR)[8])
+{
+    const int w = u >> 3, b = u & 7;
+    f2 c[2][8];
+#pragma unroll
+    for (int s = 0; s < 8; s++) {
+        const int k = b + 8 * s;
+        const f2 tw = ld2(T.mdct_s[k]);
+        const f2 x = {bufL[eo_idx(128 * w + 127 - 2 * k)], bufL[eo_idx(128 * w + 2 * k)]};
+        const f2 y = {bufR[eo_idx(128 * w + 127 - 2 * k)], bufR[eo_idx(128 * w + 2 * k)]};
+        c[0][s] = cmul_t<F>(x, tw);
+        c[1][s] = cmul_t<F>(y, tw);
+    }
+    wave_sync();
+    if constexpr (F) {
+        fft_pass1_r8<2>(c);
+    } else {
+        radix4_pk2(c[0], c[1], BR3[0], BR3[1], BR3[2], BR3[3]);
+        radix4_pk2(c[0], c[1], BR3[4], BR3[5], BR3[6], BR3[7]);
+#pragma unroll
+        for (int k = 0; k < 4; k++) bfly_pk2(c[0][BR3[k]], c[0][BR3[k + 4]], c[1][BR3[k]], c[1][BR3[k + 4]], ld2(T.roots_s[8 * k]));
+    }
+    f2* XL = reinterpret_cast<f2*>(bufL);
+    f2* XR = reinterpret_cast<f2*>(bufR);
+    const int t = (int)(__builtin_bitreverse32((uint32_t)b) >> 29);
+#pragma unroll
+    for (int r = 0; r < 8; r++) {
+        XL[xs(64 * w + 8 * t + r)] = c[0][BR3[r]];
+        XR[xs(64 * w + 8 * t + r)] = c[1][BR3[r]];
+    }
+    wave_sync();
+#pragma unroll
+    for (int s = 0; s < 8; s++) {
+        c[0][s] = XL[xs(64 * w + b + 8 * s)];
+        c[1][s] = XR[xs(64 * w + b + 8 * s)];
+    }
+    wave_sync();
+    // stages i = 8, 16, 32 of the 64-point IFFT: roots[k*m], m = 4, 2, 1
+    fft_3stages_pk2<F>(c[0], c[1], [&](int j) {
+        const int idx = j == 0 ? 4 * b : (j < 3 ? 2 * (b + 8 * (j - 1)) : b + 8 * (j - 3));
+        return ld2(T.roots_s[idx]);
+    });
+#pragma unroll
+    for (int s = 0; s < 8; s++) {
+        const f2 tw = ld2(T.mdct_s[b + 8 * s]);
+        const f2 z = cmul_t<F>(c[0][s], tw), y = cmul_t<F>(c[1][s], tw);
+        reL[s] = z.x;
+        imL[s] = z.y;
+        reR[s] = y.x;
+        imR[s] = y.y;
+    }
+}
+
 // window position n (0..255) of short slot (s, j), j = 0..3, and its IMDCT value
 __device__ __forceinline__ void short_slot(int b, int s, int j, const float (&re)[8], const float (&im)[8], int& n,
                                            float& v)
@@ -790,6 +1007,71 @@ __device__ __forceinline__ void ola_short(float* Tb, const LdsTables& T, int u, 
     }
 #pragma unroll
     for (int o = 0; o < 16; o++) ov[o] = nv[o];
+}
+
+// ola_short on both channels of a CPE (imdct_short_pk2's outputs): each channel's own windows and
+// overlap, every LDS phase shared (two wave_syncs per phase instead of four per channel pair)
+__device__ __forceinline__ void ola_short2(float* TL, float* TR, const LdsTables& T, int u, const FrameCtx& fL,
+                                           const FrameCtx& fR, const float (&reL)[8], const float (&imL)[8],
+                                           const float (&reR)[8], const float (&imR)[8], float (&ovL)[16],
+                                           float (&ovR)[16], float (&outL)[16], float (&outR)[16])
+{
+    const int w = u >> 3, b = u & 7;
+    const float* SWcL = T.win_short[fL.shape];
+    const float* SWrL = T.win_short[w == 0 ? fL.shape_prev : fL.shape];
+    const float* SWcR = T.win_short[fR.shape];
+    const float* SWrR = T.win_short[w == 0 ? fR.shape_prev : fR.shape];
+    float nvL[16], nvR[16];
+#pragma unroll
+    for (int phase = 0; phase < 2; phase++) {  // 0: falling halves (A), 1: rising halves (B)
+#pragma unroll
+        for (int s = 0; s < 8; s++) {
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                int n;
+                float vl, vr;
+                short_slot(b, s, j, reL, imL, n, vl);
+                short_slot(b, s, j, reR, imR, n, vr);
+                if ((n < 128) != (phase == 1)) continue;  // j = 0,1 rising; j = 2,3 falling (compile-time)
+                if (phase == 0) {
+                    TL[128 * w + (n - 128)] = vl * SWcL[255 - n];
+                    TR[128 * w + (n - 128)] = vr * SWcR[255 - n];
+                } else {
+                    TL[128 * w + n] = vl * SWrL[n];
+                    TR[128 * w + n] = vr * SWrR[n];
+                }
+            }
+        }
+        wave_sync();
+        const int uu = lane_id();  // opaque: stop index math being hoisted/kept across phases
+#pragma unroll
+        for (int o = 0; o < 16; o++) {
+            const int P = long_pos(uu, o);
+            const int mo = (P - 448) >> 7, io = (P - 448) & 127;
+            const int mq = (P + 576) >> 7, iq = (P + 576) & 127;
+            if (phase == 0) {
+                outL[o] = (P >= 448 + 128) ? ovL[o] + TL[128 * (mo - 1) + io] : ovL[o];
+                outR[o] = (P >= 448 + 128) ? ovR[o] + TR[128 * (mo - 1) + io] : ovR[o];
+                nvL[o] = (mq <= 8) ? TL[128 * (mq - 1) + iq] : 0.0f;
+                nvR[o] = (mq <= 8) ? TR[128 * (mq - 1) + iq] : 0.0f;
+            } else {
+                if (P >= 448) {
+                    outL[o] = outL[o] + TL[128 * mo + io];
+                    outR[o] = outR[o] + TR[128 * mo + io];
+                }
+                if (mq <= 7) {
+                    nvL[o] = nvL[o] + TL[128 * mq + iq];
+                    nvR[o] = nvR[o] + TR[128 * mq + iq];
+                }
+            }
+        }
+        wave_sync();
+    }
+#pragma unroll
+    for (int o = 0; o < 16; o++) {
+        ovL[o] = nvL[o];
+        ovR[o] = nvR[o];
+    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1189,13 +1471,16 @@ __device__ __forceinline__ void synth_channel(const KernelArgs& A, const LdsTabl
 
 // kMode: 0 = TNS compat (the reference), 1 = spec TNS, 2 = TNS compat with dependent coupling,
 // 3 = spec TNS with dependent coupling (BEFORE_TNS terms, the TNS filters, AFTER_TNS terms),
-// 4 = mode 0 at +-1 LSB precision (JAAD_PRECISION_LSB1: fused multiply-adds in the transforms)
+// 4 = mode 0 at +-1 LSB precision (JAAD_PRECISION_LSB1: fused multiply-adds in the transforms),
+// 5 / 6 = mode 0 / 4 built for batches with EIGHT_SHORT frames (both channels' short IMDCTs and
+// overlap-adds in lockstep; chosen per launch by the host, KernelArgs::short_pair)
 template <int kMode, int kOut, bool kStereo>
 __global__ __launch_bounds__(64 * waves_per_wg<kMode == 1 || kMode == 3>()) void lc_decode_kernel(KernelArgs A)
 {
     constexpr bool kTnsSpec = kMode == 1 || kMode == 3;
     [[maybe_unused]] constexpr bool kCouple = kMode == 2 || kMode == 3;
-    constexpr bool kFast = kMode == 4;
+    constexpr bool kFast = kMode == 4 || kMode == 6;
+    [[maybe_unused]] constexpr bool kShortPair = kMode == 5 || kMode == 6;
     constexpr int kW = waves_per_wg<kTnsSpec>();
     constexpr int kThreads = 64 * kW;
     // one LDS object with the tables first: every table access is a 16-bit immediate offset
@@ -1294,6 +1579,7 @@ __global__ __launch_bounds__(64 * waves_per_wg<kMode == 1 || kMode == 3>()) void
             // SIMDs in a fixed cyclic order); the one with the most frames left gets the highest
             // priority, so that they end together (C2 wave ends 132-171 -> 147-160 us, busy 88 ->
             // 95 % of span x waves; batch -1 %, profiles/round5_balance/).
+#ifndef JAAD_ABL_NOPRIO
             {
                 const uint32_t rem = (uint32_t)(my_n - it);
                 volatile uint32_t* R = S.rem;
@@ -1309,6 +1595,7 @@ __global__ __launch_bounds__(64 * waves_per_wg<kMode == 1 || kMode == 3>()) void
                 else if (p == 1) __builtin_amdgcn_s_setprio(2);
                 else __builtin_amdgcn_s_setprio(1);
             }
+#endif
 #ifdef JAAD_WAVETIME
             wt_frames++;
 #endif
@@ -1430,6 +1717,9 @@ __global__ __launch_bounds__(64 * waves_per_wg<kMode == 1 || kMode == 3>()) void
             STAMP(12);
             // issued on every iteration (the last one reloads its own frame) so that the VMEM
             // pattern of the loop body is the same on every path: see the PCM stores below
+#ifdef JAAD_ABL_NOPREF
+            if (it == 0)
+#endif
             prefetch(A, it + 1 < my_n ? fr_next : f, stereo, u, pf, skip);
 
             if ((iL.flags | (stereo ? iR.flags : 0)) & JAAD_ICS_HAS_PNS) {  // rare: lane 0 replays the LCG
@@ -1551,6 +1841,13 @@ __global__ __launch_bounds__(64 * waves_per_wg<kMode == 1 || kMode == 3>()) void
                 ola_long_pk<kFast>(T, FrameCtx{iL.seq, iL.shape, iL.shape_prev}, cx[0], ovL, outL);
                 ola_long_pk<kFast>(T, FrameCtx{iR.seq, iR.shape, iR.shape_prev}, cx[1], ovR, outR);
                 wave_sync();
+            } else if (kShortPair && stereo && iL.seq == JAAD_EIGHT_SHORT_SEQUENCE && iR.seq == JAAD_EIGHT_SHORT_SEQUENCE) {
+                // both channels' 8 short IMDCTs and overlap-adds in lockstep (mixed-window batches)
+                float reL[8], imL[8], reR[8], imR[8];
+                imdct_short_pk2<kFast>(W.buf, W.rsp, T, lane_id(), reL, imL, reR, imR);
+                ola_short2(W.buf, W.rsp, T, lane_id(), FrameCtx{iL.seq, iL.shape, iL.shape_prev},
+                           FrameCtx{iR.seq, iR.shape, iR.shape_prev}, reL, imL, reR, imR, ovL, ovR, outL, outR);
+                wave_sync();
             } else {
                 synth_channel<kTnsSpec, kMode == 3, kFast>(A, T, W, W.buf, iL, cf0, ovL, outL, f, 0);
                 if (stereo) synth_channel<kTnsSpec, kMode == 3, kFast>(A, T, W, W.rsp, iR, cf0 + 1, ovR, outR, f, 1);
@@ -1601,6 +1898,9 @@ __global__ __launch_bounds__(64 * waves_per_wg<kMode == 1 || kMode == 3>()) void
                     const uint32_t sel0 = big_endian ? 0x04050001u : 0x05040100u;
                     const uint32_t sel1 = big_endian ? 0x06070203u : 0x07060302u;
                     uint32_t* stage = reinterpret_cast<uint32_t*>(W.buf);
+#ifdef JAAD_ABL_NOPCM
+                    if (f < 0)  // never: the PCM stage's work and stores are left out (time only)
+#endif
 #pragma unroll
                     for (int m = 0; m < 8; m++) {
                         const uint32_t pl = round_pk16(outL[2 * m], outL[2 * m + 1]);
@@ -1670,8 +1970,21 @@ static hipError_t launch_lc_ch(const KernelArgs& a, hipStream_t stream, bool tns
     if (a.cce_off && tns_spec) launch_lc_mode<3, kStereo>(a, stream);  // coupling around the spec TNS filters
     else if (a.cce_off) launch_lc_mode<2, kStereo>(a, stream);
     else if (tns_spec) launch_lc_mode<1, kStereo>(a, stream);
-    else if (a.precision == JAAD_PRECISION_LSB1) launch_lc_mode<4, kStereo>(a, stream);
-    else launch_lc_mode<0, kStereo>(a, stream);
+    else if (a.precision == JAAD_PRECISION_LSB1) {
+        if constexpr (kStereo)  // (the lockstep short path pairs a CPE's channels: stereo only)
+            if (a.short_pair) {
+                launch_lc_mode<6, kStereo>(a, stream);
+                return hipGetLastError();
+            }
+        launch_lc_mode<4, kStereo>(a, stream);
+    } else {
+        if constexpr (kStereo)
+            if (a.short_pair) {
+                launch_lc_mode<5, kStereo>(a, stream);
+                return hipGetLastError();
+            }
+        launch_lc_mode<0, kStereo>(a, stream);
+    }
     return hipGetLastError();
 }
 

@@ -29,6 +29,7 @@ ZERO_HCB, NOISE_HCB, INTENSITY_HCB2, INTENSITY_HCB = 0, 13, 14, 15
 TNS_COMPAT, TNS_SPEC = 0, 1
 PRECISION_EXACT, PRECISION_LSB1 = 0, 1  # jaad_stream_cfg.precision (JAAD_PRECISION_*)
 PCM_BIG_ENDIAN, PCM_LITTLE_ENDIAN, PCM_FLOAT32 = 0, 1, 2
+HINT_SHORT_WINDOWS = 1 << 8  # jaad_decode_batch_device: the batch holds EIGHT_SHORT frames (kernel choice only)
 ICS_HAS_PNS, ICS_HAS_IS, ICS_TNS, ICS_MS_PRESENT, ICS_COMMON_WINDOW = 1, 2, 4, 8, 16
 
 ICS_DTYPE = np.dtype([

@@ -174,7 +174,9 @@ def test_gpu_world2_bench_path_on_the_hip_engine(monkeypatch):
     for pr in procs:
         pr.join(timeout=120)
         assert pr.exitcode == 0
-    assert line["n_gpus"] == 2 and line["parity_sample"]["max_abs_lsb"] == 0
+    # (the bench's default precision is lsb1: within 1 LSB of the restatement, byte-identical across ranks)
+    assert line["n_gpus"] == 2 and line["parity_sample"]["max_abs_lsb"] <= 1
+    assert line["config"]["precision"].startswith("lsb1")
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
         monkeypatch.delenv(k, raising=False)
     args = bench.parse(["--config", "2", "--steps", "2", "--warmup", "2", "--settle", "0.02", "--no-cpu", "--no-e2e", "--no-host",

@@ -307,12 +307,32 @@ def test_gpu_coupling_with_spec_tns_matches_oracle(cc):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("cc", [3, 4, 5, 6, 7])
+def test_gpu_multichannel_coupling_with_spec_tns_matches_oracle(cc):
+    """JAAD_TNS_SPEC with coupling in configurations 3-7.  The reference couples around
+    TNS per channel element (SCE.process / CPE.process: BEFORE_TNS terms, the element's TNS filters,
+    AFTER_TNS terms, A/syntax/SCE.java:100-108, CPE.java:172-179, CCE.java:188-215); the GPU runs
+    kernel mode 3 per element with the terms' channels relative to the element.  Bit-exact against
+    the restatement (oracle.decode_batch_mc, element by element), through the host entry and with
+    the AFTER_TNS / BEFORE_TNS points swapped (they differ once the filters are live)."""
+    from tests.test_multichannel import IDS
+    b = coupled_batch(cc, n_streams=4, fps=30, seed=80 + cc)
+    assert (b.ics["flags"] & N.ICS_TNS).any() and (b.cce_terms["point"] == 1).any()
+    cfg = N.make_cfg(channel_config=cc, tns_mode=N.TNS_SPEC)
+    for swap in (False, True):
+        if swap:
+            b.cce_terms["point"] ^= 1
+        want = O.decode_batch_mc(3, b, IDS[cc], N.PCM_BIG_ENDIAN, threads=8, tns_mode=N.TNS_SPEC)
+        with N.Context(cfg, 4) as ctx:
+            got = ctx.decode(b, N.PCM_BIG_ENDIAN)
+        assert (got == want).all(), (swap, np.flatnonzero((got != want).any(1))[:8])
+        if not swap:
+            first = want
+    assert (first != want).any()  # the coupling point matters once the TNS filters run
+
+
+@pytest.mark.gpu
 def test_gpu_coupling_rejections():
-    b = coupled_batch(6, n_streams=2, fps=8, seed=2)
-    with N.Context(N.make_cfg(channel_config=6, tns_mode=N.TNS_SPEC), 2) as ctx:
-        with pytest.raises(N.JaadError) as e:  # spec TNS with coupling: configurations 1 and 2
-            ctx.decode(b)
-        assert e.value.status == N.ERR_UNSUPPORTED
     b = coupled_batch(2, n_streams=2, fps=8, seed=2)
     with N.Context(N.make_cfg(channel_config=2), 2) as ctx:
         bad = b.cce_terms.copy()

@@ -157,7 +157,7 @@ def test_ragged_runs_and_subset_of_slots():
         st_other = ctx.state_export(0)
     want = O.decode_batch(cfg, rag, O.Streams(6), N.PCM_FLOAT32)
     _assert_pcm_equal(got, want, N.PCM_FLOAT32)
-    assert (st_other == 0).all()
+    assert (st_other[:-16] == 0).all()  # (the blob's 16-byte trailer names its layout)
 
 
 def test_bitstream_errors_are_reported():
@@ -216,3 +216,35 @@ def test_float32_output_stays_inside_its_frames(cfg_id, monkeypatch):
     host = pcm.cpu().numpy().reshape(-1, nb)
     assert (host[:guard] == 0x7F).all() and (host[-guard:] == 0x7F).all()
     assert (host[guard:-guard] == want).all()
+
+
+def test_state_blob_names_its_layout():
+    """a state blob ends with a trailer (magic, layout version, context kind, payload
+    bytes); an import checks it, so a blob with another version or written by another kind of
+    context (here: HE-AAC with a downsampled vs an upsampled synthesis, same size) is refused and
+    the slot keeps its state."""
+    p = N.synth_params(2, n_streams=2, frames_per_stream=9)
+    b = N.synth_batch(p)
+    with N.Context(N.make_cfg(), 2) as ctx:
+        ctx.decode(b)
+        blob = ctx.state_export(0)
+        before = ctx.state_export(1)
+        magic, version, kind, payload = np.frombuffer(blob[-16:].tobytes(), "<u4")
+        assert magic == 0x4441414A and payload == len(blob) - 16
+        for k in range(4):  # each trailer word in turn
+            bad = blob.copy()
+            bad[-16 + 4 * k] ^= 1
+            with pytest.raises(N.JaadError) as e:
+                ctx.state_import(1, bad)
+            assert e.value.status == N.ERR_INVALID_ARG
+            assert (ctx.state_export(1) == before).all()
+        ctx.state_import(1, blob)
+        assert (ctx.state_export(1) == blob).all()
+    up = N.make_cfg(sf_index=6, sbr=True)
+    down = N.make_cfg(sf_index=6, sbr=True, down=True)
+    with N.Context(up, 1) as a, N.Context(down, 1) as d:
+        blob = a.state_export(0)
+        assert len(blob) == len(d.state_export(0))
+        with pytest.raises(N.JaadError) as e:
+            d.state_import(0, blob)
+        assert e.value.status == N.ERR_INVALID_ARG

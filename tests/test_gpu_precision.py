@@ -59,18 +59,34 @@ def test_small_batches_within_one_lsb(sf_index, cc, cfg_id, flags):
     assert mx <= 1
 
 
+# Float tolerance of the +-1 LSB kernel (float32 output, the samples before Math.round), per frame:
+# |delta| <= 2e-5 x the frame's peak |sample| and rel-RMS <= 1.5e-5 (measured on MI355X: 1.12e-5 and
+# 7.3e-6, profiles/round6_prec/).  SURVEY 8(d) states 0.01 int16 units / 2e-6 for a transform that
+# follows the reference's own twiddle tables stage by stage, and "expect up to 0.006 x RMS/200
+# extra" otherwise: FFT_TABLE_512 is an f32 recurrence (FFTTables.java:5) whose entries are off by up
+# to 8.7e-6 relative.  The fused kernel multiplies by 1, i, W8, W8^3 exactly and combines
+# the other table entries in radix-8 order, so the reference's table error no longer cancels the
+# same way: every output sample moves in proportion to its frame's level.  The PCM bar (+-1 LSB) is
+# asserted directly by test_full_batch_within_one_lsb.
+FLOAT_TOL_PEAK, FLOAT_TOL_RMS = 2e-5, 1.5e-5
+
+
 def test_float32_within_the_float_tolerance():
-    """Float32 output (the samples before Math.round): |delta| <= 0.01 int16 units and rel-RMS <= 2e-6
-    per frame, C3 (all four window sequences)."""
+    """Float32 output within FLOAT_TOL_* of the restatement's, C3 (all four window sequences)."""
     p = N.synth_params(3, n_streams=8, frames_per_stream=40)
     b = N.synth_batch(p)
     got = _decode(N.make_cfg(precision=N.PRECISION_LSB1), b, N.PCM_FLOAT32).view(np.float32).reshape(b.n_frames, -1)
     want = O.decode_batch(N.make_cfg(), b, O.Streams(8), N.PCM_FLOAT32).view(np.float32).reshape(b.n_frames, -1)
-    d = np.abs(got.astype(np.float64) - want.astype(np.float64))
-    assert d.max() <= 0.01, d.max()
-    rms = np.sqrt((want.astype(np.float64) ** 2).mean(axis=1))
-    rel = np.sqrt((d ** 2).mean(axis=1)) / np.maximum(rms, 1e-30)
-    assert rel.max() <= 2e-6, rel.max()
+    w = want.astype(np.float64)
+    d = np.abs(got.astype(np.float64) - w)
+    peak = np.abs(w).max(axis=1)
+    rms = np.sqrt((w ** 2).mean(axis=1))
+    rel_peak = d.max(axis=1) / np.maximum(peak, 1e-30)
+    rel_rms = np.sqrt((d ** 2).mean(axis=1)) / np.maximum(rms, 1e-30)
+    print(f"float32: max |delta| {d.max():.4g} (int16 units), max |delta| / frame peak {rel_peak.max():.3g}, "
+          f"max rel-RMS {rel_rms.max():.3g}")
+    assert rel_peak.max() <= FLOAT_TOL_PEAK, rel_peak.max()
+    assert rel_rms.max() <= FLOAT_TOL_RMS, rel_rms.max()
     assert (got.view(np.uint32) != want.view(np.uint32)).any()  # the fused kernel ran
 
 
@@ -105,3 +121,32 @@ def test_continuation_and_pieces_under_lsb1():
     ref = np.concatenate([want[fb[r]:fb[r + 1]] for r in range(12)])
     mx, _ = _lsb_report(got, ref)
     assert mx <= 1
+
+
+@pytest.mark.parametrize("precision", [N.PRECISION_EXACT, N.PRECISION_LSB1])
+def test_mixed_window_instantiation_through_the_device_entry(precision):
+    """JAAD_HINT_SHORT_WINDOWS (jaad_decode_batch_device) selects the mixed-window kernel (a CPE's two
+    EIGHT_SHORT transforms in lockstep; the host entry picks it itself when its side-info scan sees a
+    short frame): exact -> bit-identical to the restatement and to the long-window kernel's output;
+    LSB1 -> within 1 LSB.  A C3 batch (all four window sequences, TNS data)."""
+    import torch
+    p = N.synth_params(3, n_streams=8, frames_per_stream=40)
+    b = N.synth_batch(p)
+    cfg = N.make_cfg(precision=precision)
+    dev = torch.device("cuda", 0)
+    t = lambda a: None if a is None else torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1)).to(dev)
+    d = {k: t(getattr(b, k)) for k in ("q", "sf", "cb", "ics", "ms_used", "tns")}
+    ptr = {k: (v.data_ptr() if v is not None else None) for k, v in d.items()}
+    outs = []
+    for hint in (0, N.HINT_SHORT_WINDOWS):
+        pcm = torch.empty(b.n_frames * 4096, dtype=torch.uint8, device=dev)
+        with N.Context(cfg, 8) as ctx:
+            ctx.decode_device(ptr, b, pcm.data_ptr(), pcm.numel(), N.PCM_BIG_ENDIAN | hint)
+            ctx.wait()
+        outs.append(pcm.cpu().numpy().reshape(b.n_frames, -1))
+    want = O.decode_batch(N.make_cfg(), b, O.Streams(8), N.PCM_BIG_ENDIAN)
+    for got in outs:
+        mx, _ = _lsb_report(got, want)
+        assert mx <= (0 if precision == N.PRECISION_EXACT else 1)
+    if precision == N.PRECISION_EXACT:
+        assert (outs[0] == outs[1]).all()
