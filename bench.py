@@ -243,7 +243,12 @@ def run(args, engine_cls=HipEngine):
     sbr = bool(p.sbr)
     n_frames = batch.n_frames
     flags = N.PCM_BIG_ENDIAN
-    eng = engine_cls(cfg, batch, flags, local, int(batch.stream_slot.max()) + 1 if n_frames else 1)
+    # the host knows its batch's window sequences (a parser writes them): with EIGHT_SHORT frames in a
+    # CPE stream the device-entry call says so (JAAD_HINT_SHORT_WINDOWS: the mixed-window kernel
+    # instantiation; jaad_decode_batch scans for itself)
+    short = bool(n_frames) and cfg.channel_config == 2 and bool((batch.ics["window_sequence"] == N.EIGHT_SHORT_SEQUENCE).any())
+    dev_flags = flags | (N.HINT_SHORT_WINDOWS if short else 0)
+    eng = engine_cls(cfg, batch, dev_flags, local, int(batch.stream_slot.max()) + 1 if n_frames else 1)
 
     # ---- parity sample: the first call decodes every stream from a fresh state
     eng.step()
@@ -363,6 +368,8 @@ def run(args, engine_cls=HipEngine):
                        "streams_per_job": n_global_streams,
                        "parallelism": f"stream-sharded x{world} (no collectives)", "pcm": "int16 big-endian",
                        "samples_per_frame": 2048 if sbr else 1024,
+                       "lc_kernel": ("mixed-window instantiation (JAAD_HINT_SHORT_WINDOWS: the batch holds EIGHT_SHORT frames)"
+                                     if short else "long-window instantiation"),
                        "precision": ("lsb1: PCM within +-1 LSB of the reference (jaad_stream_cfg.precision = "
                                      "JAAD_PRECISION_LSB1, fused multiply-adds in the IMDCT; parity_sample checks it)"
                                      if precision == N.PRECISION_LSB1 else

@@ -394,6 +394,31 @@ __device__ __forceinline__ void bf83(f2& a, f2& b, f2 h)
     a = pkfma_i(u, h, t);
     b = pkfma_ni(u, h, t);
 }
+// Two independent complex products / W8 butterflies interleaved: the second one's first operation
+// fills the wait state that a packed FP32 result needs before a dependent packed operation reads it
+// (the compiler keeps the inline-asm order it is given and would put an s_nop between).
+__device__ __forceinline__ void cmul_fma2(f2& a, f2 wa, f2& b, f2 wb)
+{
+    const f2 ma = mul_bx(a, wa), mb = mul_bx(b, wb);
+    a = fma_by(a, wa, ma);
+    b = fma_by(b, wb, mb);
+}
+__device__ __forceinline__ void bf8_2(f2& a0, f2& b0, f2& a1, f2& b1, f2 h)
+{
+    const f2 u0 = pk_rot_p(b0, b0), u1 = pk_rot_p(b1, b1), t0 = a0, t1 = a1;
+    a0 = pkfma(u0, h, t0);
+    a1 = pkfma(u1, h, t1);
+    b0 = pkfma_n(u0, h, t0);
+    b1 = pkfma_n(u1, h, t1);
+}
+__device__ __forceinline__ void bf83_2(f2& a0, f2& b0, f2& a1, f2& b1, f2 h)
+{
+    const f2 u0 = pk_rot_p(b0, b0), u1 = pk_rot_p(b1, b1), t0 = a0, t1 = a1;
+    a0 = pkfma_i(u0, h, t0);
+    a1 = pkfma_i(u1, h, t1);
+    b0 = pkfma_ni(u0, h, t0);
+    b1 = pkfma_ni(u1, h, t1);
+}
 // 8-point DFT of registers holding the sub-transforms in bit-reversed order (fft_3stages_pk's
 // structure with twiddles 1 | 1, i | 1, W8, i, W8^3), N channels operation by operation
 template <int N>
@@ -419,10 +444,16 @@ __device__ __forceinline__ void dft8_r8(f2 (&c)[N][8])
         bf1(c[n][0], c[n][4]);
         bfi(c[n][2], c[n][6]);
     }
-#pragma unroll
-    for (int n = 0; n < N; n++) bf8(c[n][1], c[n][5], h);
-#pragma unroll
-    for (int n = 0; n < N; n++) bf83(c[n][3], c[n][7], h);
+    if constexpr (N == 2) {
+        bf8_2(c[0][1], c[0][5], c[1][1], c[1][5], h);
+        bf83_2(c[0][3], c[0][7], c[1][3], c[1][7], h);
+    } else {
+        const f2 u1 = pk_rot_p(c[0][5], c[0][5]), u3 = pk_rot_p(c[0][7], c[0][7]), t1 = c[0][1], t3 = c[0][3];
+        c[0][1] = pkfma(u1, h, t1);
+        c[0][3] = pkfma_i(u3, h, t3);
+        c[0][5] = pkfma_n(u1, h, t1);
+        c[0][7] = pkfma_ni(u3, h, t3);
+    }
 }
 // pass 1 (FFT.java:69-108 radix-4, then the 8-point stage with twiddles W8^k, k = 0..3)
 template <int N>
@@ -439,20 +470,32 @@ __device__ __forceinline__ void fft_pass1_r8(f2 (&c)[N][8])
         bf1(c[n][BR3[0]], c[n][BR3[4]]);
         bfi(c[n][BR3[2]], c[n][BR3[6]]);
     }
-#pragma unroll
-    for (int n = 0; n < N; n++) bf8(c[n][BR3[1]], c[n][BR3[5]], h);
-#pragma unroll
-    for (int n = 0; n < N; n++) bf83(c[n][BR3[3]], c[n][BR3[7]], h);
+    if constexpr (N == 2) {
+        bf8_2(c[0][BR3[1]], c[0][BR3[5]], c[1][BR3[1]], c[1][BR3[5]], h);
+        bf83_2(c[0][BR3[3]], c[0][BR3[7]], c[1][BR3[3]], c[1][BR3[7]], h);
+    } else {
+        const f2 u1 = pk_rot_p(c[0][BR3[5]], c[0][BR3[5]]), u3 = pk_rot_p(c[0][BR3[7]], c[0][BR3[7]]);
+        const f2 t1 = c[0][BR3[1]], t3 = c[0][BR3[3]];
+        c[0][BR3[1]] = pkfma(u1, h, t1);
+        c[0][BR3[3]] = pkfma_i(u3, h, t3);
+        c[0][BR3[5]] = pkfma_n(u1, h, t1);
+        c[0][BR3[7]] = pkfma_ni(u3, h, t3);
+    }
 }
 // passes 2 and 3: register r (1..7) times tw(r - 1), then the 8-point DFT
 template <int N, typename TW>
 __device__ __forceinline__ void fft_pass_r8(f2 (&c)[N][8], TW tw)
 {
+    if constexpr (N == 2) {
 #pragma unroll
-    for (int r = 1; r < 8; r++) {
-        const f2 w = tw(r - 1);
+        for (int r = 1; r < 8; r++) {
+            const f2 w = tw(r - 1);
+            cmul_fma2(c[0][r], w, c[1][r], w);
+        }
+    } else {
 #pragma unroll
-        for (int n = 0; n < N; n++) c[n][r] = cmul_fma(c[n][r], w);
+        for (int r = 1; r < 7; r += 2) cmul_fma2(c[0][r], tw(r - 1), c[0][r + 1], tw(r));
+        c[0][7] = cmul_fma(c[0][7], tw(6));
     }
     dft8_r8<N>(c);
 }
@@ -649,6 +692,16 @@ __device__ __forceinline__ void xch_bit(f2 (&c)[8], int u)
 template <int N, bool F = false>
 __device__ __forceinline__ void imdct_long_pk(float* const (&bufs)[N], const LdsTables& T, int u, f2 (&c)[N][8])
 {
+    if constexpr (F && N == 2) {  // the two channels' products interleaved (cmul_fma2)
+#pragma unroll
+        for (int s = 0; s < 8; s++) {
+            const int k = u + 64 * s;
+            const f2 w = ld2(T.mdct_l[k]);
+            c[0][s] = f2{bufs[0][eo_idx(1023 - 2 * k)], bufs[0][eo_idx(2 * k)]};
+            c[1][s] = f2{bufs[1][eo_idx(1023 - 2 * k)], bufs[1][eo_idx(2 * k)]};
+            cmul_fma2(c[0][s], w, c[1][s], w);
+        }
+    } else {
 #pragma unroll
     for (int n = 0; n < N; n++)
 #pragma unroll
@@ -658,6 +711,7 @@ __device__ __forceinline__ void imdct_long_pk(float* const (&bufs)[N], const Lds
             const f2 x = {bufs[n][eo_idx(1023 - 2 * k)], bufs[n][eo_idx(2 * k)]};
             c[n][s] = cmul_t<F>(x, ld2(T.mdct_l[k]));
         }
+    }
     // (JAAD_ABL_* macros: ablation builds of the fused lockstep path, design tool -- wrong output,
     // time only; scripts/build_exp.py)
 #if defined(JAAD_ABL_NOFFT)
@@ -720,10 +774,18 @@ __device__ __forceinline__ void imdct_long_pk(float* const (&bufs)[N], const Lds
     else if constexpr (N == 2) fft_3stages_pk2<F>(c[0], c[1], [&](int j) { return ld2(T.tw3[j][u]); });
     else fft_3stages_pk<F>(c[0], [&](int j) { return ld2(T.tw3[j][u]); });
     // MDCT.java:48-53: re = t0*c - t1*sn, im = t1*c + t0*sn = cmul((t0, t1), (c, sn))
+    if constexpr (F && N == 2) {
+#pragma unroll
+        for (int s = 0; s < 8; s++) {
+            const f2 w = ld2(T.mdct_post[s][u]);
+            cmul_fma2(c[0][s], w, c[1][s], w);
+        }
+    } else {
 #pragma unroll
     for (int s = 0; s < 8; s++)
 #pragma unroll
         for (int n = 0; n < N; n++) c[n][s] = cmul_t<F>(c[n][s], ld2(T.mdct_post[s][u]));
+    }
 }
 
 // FilterBank.process for ONLY_LONG / LONG_START / LONG_STOP (FilterBank.java:41-70, 102-119).
@@ -1177,6 +1239,19 @@ __device__ __forceinline__ uint32_t round_pk16(float a, float b)
     return w;
 }
 
+// +-1 LSB kernel: two samples to int16 in one conversion after one packed multiply --
+// v_cvt_pknorm_i16_f32 rounds x * 32767 to nearest and saturates to [-32767, 32767], so the samples
+// are first scaled by 1/32767 (a product rounded once, then re-scaled inside the conversion: the
+// integer can differ from Math.round's by one at a tie, and -32768 comes out as -32767; both within
+// the mode's bar).  2 instructions per sample pair instead of 3.
+__device__ __forceinline__ uint32_t round_pk16_lsb1(float a, float b)
+{
+    const f2 x = f2{a, b} * f2{1.0f / 32767.0f, 1.0f / 32767.0f};
+    uint32_t w;
+    asm("v_cvt_pknorm_i16_f32 %0, %1, %2" : "=v"(w) : "v"(x.x), "v"(x.y));
+    return w;
+}
+
 // s_waitcnt vmcnt(0) that the compiler's wait insertion sees (an asm statement it would not).
 // vmcnt counts loads and stores together, and the compiler cannot rely on a load completing
 // before a younger store (it then waits for vmcnt(0)); so the prefetched loads of frame f+1 are
@@ -1579,7 +1654,16 @@ __global__ __launch_bounds__(64 * waves_per_wg<kMode == 1 || kMode == 3>()) void
             // SIMDs in a fixed cyclic order); the one with the most frames left gets the highest
             // priority, so that they end together (C2 wave ends 132-171 -> 147-160 us, busy 88 ->
             // 95 % of span x waves; batch -1 %, profiles/round5_balance/).
-#ifndef JAAD_ABL_NOPRIO
+#if defined(JAAD_PRIO_LATE)  // (A/B builds: the mates' counts read here, the priority set after the IQ)
+            const uint32_t rem_late = (uint32_t)(my_n - it);
+            uint32_t mates_late[kW / 4 - 1];
+            {
+                volatile uint32_t* R = S.rem;
+                R[wave] = rem_late;
+#pragma unroll
+                for (int m = 1; m < kW / 4; m++) mates_late[m - 1] = R[(wave + 4 * m) % kW];
+            }
+#elif !defined(JAAD_ABL_NOPRIO)
             {
                 const uint32_t rem = (uint32_t)(my_n - it);
                 volatile uint32_t* R = S.rem;
@@ -1713,6 +1797,20 @@ __global__ __launch_bounds__(64 * waves_per_wg<kMode == 1 || kMode == 3>()) void
             iq_channel(T, A.iq_table, cur.q[0], gL, xL);
             STAMP(13);
             if (stereo) iq_channel(T, A.iq_table, cur.q[1], gR, xR);
+#if defined(JAAD_PRIO_LATE)
+            {
+                int p = 0;
+#pragma unroll
+                for (int m = 1; m < kW / 4; m++) {
+                    const int mate = (wave + 4 * m) % kW;
+                    const uint32_t r = __builtin_amdgcn_readfirstlane(mates_late[m - 1]);
+                    p += (rem_late > r || (rem_late == r && wave > mate)) ? 1 : 0;
+                }
+                if (p >= 2) __builtin_amdgcn_s_setprio(3);
+                else if (p == 1) __builtin_amdgcn_s_setprio(2);
+                else __builtin_amdgcn_s_setprio(1);
+            }
+#endif
             // the inputs are consumed: frame f+1's loads fly while this frame's IMDCTs run
             STAMP(12);
             // issued on every iteration (the last one reloads its own frame) so that the VMEM
@@ -1903,8 +2001,19 @@ __global__ __launch_bounds__(64 * waves_per_wg<kMode == 1 || kMode == 3>()) void
 #endif
 #pragma unroll
                     for (int m = 0; m < 8; m++) {
-                        const uint32_t pl = round_pk16(outL[2 * m], outL[2 * m + 1]);
-                        const uint32_t pr = stereo ? round_pk16(outR[2 * m], outR[2 * m + 1]) : pl;
+                        uint32_t pl, pr;
+#if defined(JAAD_NO_PKNORM)  // (A/B builds: the exact rounding in the fused kernel too)
+                        constexpr bool kPkNorm = false;
+#else
+                        constexpr bool kPkNorm = kFast;
+#endif
+                        if constexpr (kPkNorm) {
+                            pl = round_pk16_lsb1(outL[2 * m], outL[2 * m + 1]);
+                            pr = stereo ? round_pk16_lsb1(outR[2 * m], outR[2 * m + 1]) : pl;
+                        } else {
+                            pl = round_pk16(outL[2 * m], outL[2 * m + 1]);
+                            pr = stereo ? round_pk16(outR[2 * m], outR[2 * m + 1]) : pl;
+                        }
                         stage[long_pos(u2, 2 * m)] = __builtin_amdgcn_perm(pr, pl, sel0);
                         stage[long_pos(u2, 2 * m + 1)] = __builtin_amdgcn_perm(pr, pl, sel1);
                     }

@@ -12,7 +12,8 @@ sys.path.insert(0, str(ROOT))
 from jaadec_amd import native as N  # noqa: E402
 
 cfgid = int(sys.argv[1]) if len(sys.argv) > 1 else 2
-p = N.synth_params(cfgid); b = N.synth_batch(p); cfg = N.cfg_for(p)
+prec = int(sys.argv[2]) if len(sys.argv) > 2 else 0  # jaad_stream_cfg.precision (round 6: 1 = the +-1 LSB kernel)
+p = N.synth_params(cfgid); b = N.synth_batch(p); cfg = N.cfg_for(p, precision=prec)
 dev = torch.device("cuda", 0)
 t = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1)).to(dev)
 d = {"q": t(b.q), "sf": t(b.sf), "cb": t(b.cb), "ics": t(b.ics)}
