@@ -1452,6 +1452,48 @@ __device__ __forceinline__ void iq_channel(const LdsTables& T, const float* iq_g
     }
 }
 
+// iq_channel in two halves (the +-1 LSB kernel): the 16 table reads are issued at the top of the
+// frame, from the prefetched q alone, so that their LDS round trip overlaps the band-record phase's
+// two; iq_finish applies the gains once the records are read.  Same arithmetic as iq_channel.
+struct IqPending {
+    float v[16];
+    bool esc;
+};
+__device__ __forceinline__ void iq_issue(const LdsTables& T, const v4i (&q)[2], IqPending& P)
+{
+    typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+    uint32_t t[8];
+#pragma unroll
+    for (int d = 0; d < 8; d++) {
+        const uint32_t w = reinterpret_cast<const uint32_t*>(&q[d >> 2])[d & 3];
+        t[d] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(us2, w) + (us2){kIqHead, kIqHead});
+    }
+    P.esc = ((t[0] | t[1] | t[2] | t[3] | t[4] | t[5] | t[6] | t[7]) & 0xF800F800u) != 0u;
+#pragma unroll
+    for (int e = 0; e < 16; e++) {
+        const uint32_t idx = (e & 1) ? (t[e >> 1] >> 16) : (t[e >> 1] & 0xFFFFu);
+        P.v[e] = T.iq_signed[idx];
+    }
+}
+__device__ __forceinline__ void iq_finish(const LdsTables& T, const float* iq_global, const v4i (&q)[2],
+                                          const IqPending& P, const float (&g)[4], float (&x)[16])
+{
+#pragma unroll
+    for (int e = 0; e < 16; e++) x[e] = P.v[e] * g[e >> 2];
+    if (__builtin_expect(__ballot(P.esc) != 0, 0)) {  // (iq_channel's escape pass)
+#pragma unroll
+        for (int e = 0; e < 16; e++) {
+            const int qq = reinterpret_cast<const int16_t*>(&q[e >> 3])[e & 7];
+            const int qc = qq < -kIqHead ? -kIqHead : (qq > kIqHead - 1 ? kIqHead - 1 : qq);
+            const int aq = qq < 0 ? -qq : qq;
+            const float gn = g[e >> 2];
+            const float m = iq_global[aq > 8190 ? 8190 : aq] * gn;
+            const bool big = (qq > kIqHead - 1 || qq < -kIqHead) && gn != 0.0f;
+            x[e] = big ? (qq > 0 ? m : -m) : T.iq_signed[qc + kIqHead] * gn;
+        }
+    }
+}
+
 // (TNS) -> IMDCT -> window/OLA of one channel whose spectrum is in buf (E/O layout); result
 // in out (slot o = position long_pos(u, o)), new overlap in ov
 // Dependent coupling with spec TNS (kernel mode 3): frame f's AFTER_TNS terms for channel ch of
@@ -1704,6 +1746,16 @@ __global__ __launch_bounds__(64 * waves_per_wg<kMode == 1 || kMode == 3>()) void
                            A.cce_off[f + 1], A.n_cce_terms);
             }
 
+#if defined(JAAD_NO_IQ_EARLY)  // (A/B builds)
+            constexpr bool kIqEarly = false;
+#else
+            constexpr bool kIqEarly = kFast;
+#endif
+            [[maybe_unused]] IqPending iqL, iqR;
+            if constexpr (kIqEarly) {  // the IQ table reads first (iq_issue)
+                iq_issue(T, cur.q[0], iqL);
+                if (stereo) iq_issue(T, cur.q[1], iqR);
+            }
             // ---------------- side info ----------------
             const Ics iL = ics_from_lanes(cur.side, 0, nswb_l, nswb_s);
             const Ics iR = stereo ? ics_from_lanes(cur.side, 4, nswb_l, nswb_s) : iL;
@@ -1794,9 +1846,15 @@ __global__ __launch_bounds__(64 * waves_per_wg<kMode == 1 || kMode == 3>()) void
             }
             float xL[16], xR[16];
             STAMP(14);
-            iq_channel(T, A.iq_table, cur.q[0], gL, xL);
-            STAMP(13);
-            if (stereo) iq_channel(T, A.iq_table, cur.q[1], gR, xR);
+            if constexpr (kIqEarly) {
+                iq_finish(T, A.iq_table, cur.q[0], iqL, gL, xL);
+                STAMP(13);
+                if (stereo) iq_finish(T, A.iq_table, cur.q[1], iqR, gR, xR);
+            } else {
+                iq_channel(T, A.iq_table, cur.q[0], gL, xL);
+                STAMP(13);
+                if (stereo) iq_channel(T, A.iq_table, cur.q[1], gR, xR);
+            }
 #if defined(JAAD_PRIO_LATE)
             {
                 int p = 0;
