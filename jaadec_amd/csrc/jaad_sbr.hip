@@ -471,50 +471,204 @@ __global__ __launch_bounds__(256) void sbr_analysis_kernel(SbrArgs A)
 }
 
 // ---------------------------------------------------------------------------------------------
+// Packed complex arithmetic of the HF kernel: a complex value is an f2 (re, im) in a VGPR pair and
+// one VOP3P instruction makes both halves, each one correctly rounded binary32 operation (no
+// contraction), so the results are the scalar expressions' bits.  op_sel / op_sel_hi pick the half
+// of each source that feeds the lo / hi result, neg_lo / neg_hi negate it (a - b == a + (-b)).
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ f2 pk_mul_xa(f2 a, f2 b)  // (a.x * b.x, a.y * b.x)
+{
+    f2 r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ f2 pk_mul_ya(f2 a, f2 b)  // (a.y * b.y, a.x * b.y)
+{
+    f2 r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,1] op_sel_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ f2 pk_mul_bx(f2 g, f2 v)  // (g.x * v.x, g.x * v.y)
+{
+    f2 r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(r) : "v"(g), "v"(v));
+    return r;
+}
+__device__ __forceinline__ f2 pk_mul_by(f2 g, f2 v)  // (g.y * v.x, g.y * v.y)
+{
+    f2 r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,0] op_sel_hi:[1,1]" : "=v"(r) : "v"(g), "v"(v));
+    return r;
+}
+__device__ __forceinline__ f2 pk_add_nhi(f2 a, f2 b)  // (a.x + b.x, a.y - b.y)
+{
+    f2 r;
+    asm("v_pk_add_f32 %0, %1, %2 neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ f2 pk_add_nlo(f2 a, f2 b)  // (a.x - b.x, a.y + b.y)
+{
+    f2 r;
+    asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ f2 pk_add(f2 a, f2 b)
+{
+    f2 r;
+    asm("v_pk_add_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ f2 pk_mul(f2 a, f2 b)
+{
+    f2 r;
+    asm("v_pk_mul_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+// (t.re * c.re + t.im * c.im, t.im * c.re - t.re * c.im): one autocorrelation term of
+// HFGeneration.calculate_lpc (t * conj(c), the Java's operand order)
+__device__ __forceinline__ f2 pk_mul_conj(f2 t, f2 c) { return pk_add_nhi(pk_mul_xa(t, c), pk_mul_ya(t, c)); }
+// two row loads of the HF kernel through a buffer resource: a lane whose offset is past the
+// resource reads (0, 0), which is the reference's zero above the analysed bands
+__device__ __forceinline__ f2 load_row_pair(__amdgpu_buffer_rsrc_t r, int off)
+{
+    return __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+}
+
+// ---------------------------------------------------------------------------------------------
 // Channel.process_channel HF part: HFGeneration + HFAdjustment (A/sbr/Channel.java:596-604)
 // phase 0: full; phase 1: gains and G/Q ring only; phase 2: full, ring from frame f-1
 // ---------------------------------------------------------------------------------------------
+// JAAD_HF_STAMPS builds (scripts/hf_stamps.py): s_memtime at the phase boundaries of each
+// phase-0 channel-frame, lane 0 stores them to dbg[cf][16] (u64); the debug buffer is attached by
+// jaad__sbr_debug_attach.  Product builds compile them out.
+#if defined(JAAD_HF_STAMPS)
+#define HF_STAMP(k)                                        \
+    do {                                                   \
+        __builtin_amdgcn_sched_barrier(0);                 \
+        hf_t[k] = __builtin_amdgcn_s_memtime();            \
+        __builtin_amdgcn_sched_barrier(0);                 \
+    } while (0)
+#else
+#define HF_STAMP(k) \
+    do {            \
+    } while (0)
+#endif
 // phase 3: fix pass over the listed channel-frames; phase 4: chain walker, one wave per chain
 // stepping its frames in order (each one a phase-3 frame reading the frame before it)
 template <int kPhase>
 __global__ __launch_bounds__(256, 3) void sbr_hf_kernel(SbrArgs A)
 {
     constexpr int P = kPhase == 4 ? 3 : kPhase;  // the body's phase
+#if defined(JAAD_HF_STAMPS)
+    uint64_t hf_t[16] = {};
+#endif
+    HF_STAMP(0);
     __shared__ HfLds Ls[kWavesPerBlock];
     __shared__ float2 noise_s[512];  // NoiseTable.NOISE_TABLE (A/sbr/NoiseTable.java:6), read per slot
-    for (int i = threadIdx.x; i < 512; i += blockDim.x)
-        noise_s[i] = reinterpret_cast<const float2*>(A.noise)[i];
-    __syncthreads();
+    static_assert(kWavesPerBlock * 64 * 2 == 512, "two noise entries per thread");
     const int wave = threadIdx.x >> 6;
+    const int u = lane_id();
     uint32_t cf = blockIdx.x * kWavesPerBlock + wave;
     uint32_t n_iter = 1, o = 0;
+    bool live = true;  // (every wave reaches the barrier below)
     if constexpr (kPhase == 4) {
-        if (cf >= A.n_chains) return;
-        o = A.chains[2 * cf];
-        n_iter = A.chains[2 * cf + 1];
+        live = cf < A.n_chains;
+        if (live) {
+            o = A.chains[2 * cf];
+            n_iter = A.chains[2 * cf + 1];
+        }
+    } else if constexpr (kPhase == 3) {  // fix pass: the listed channel-frames only
+        live = cf < A.n_fix;
+        if (live) cf = A.fix[cf];
+    } else {
+        live = cf < A.n_cf;
     }
-    if constexpr (kPhase == 3) {  // fix pass: the listed channel-frames only
-        if (cf >= A.n_fix) return;
-        cf = A.fix[cf];
-    }
-    if (kPhase != 4 && cf >= A.n_cf) return;
     HfLds& L = Ls[wave];
+    // Xsbr of this lane's band (sbr_save_matrix, A/sbr/SBR.java:286-300, then the analysis at
+    // offset tHFGen = 8).  Rows 0..7 are rows 32..39 of frame f-1 AFTER its HF adjustment: below
+    // kx_prev its analysis slots 24..31, from kx_prev up the high band it adjusted (rows 32, 33
+    // always, 34.. when its last envelope ends past slot 32).  That high band is frame f-1's own
+    // output of this launch, so this pass takes rows 0..7 from the analysis alone (bands < kx_prev,
+    // zero above) -- exact unless the frame reads the high band (source band >= kx_prev, kx above
+    // kx_prev or a band without patch with rows 2..7 carried: kSbrDep, jaad_sbr_host.cpp); those
+    // frames run again in fix passes (kPhase 3) that read frame f-1's finished carry rows.  The
+    // first frame of a run reads the slot state's carry rows (exact).  Rows 8..39 = this frame's
+    // analysis slots 0..31 (zero from kx up).
+    // The loads need nothing from the record: they are issued first, beside the record and table
+    // copies (rows 0..7 from the previous channel-frame; a run's first record replaces them with the
+    // slot state's rows once it has arrived) -- one global round trip before the record instead of
+    // one after it.  (x[r] = (re, im) of row r: the packed complex arithmetic below works on pairs.)
+    f2 x[40];
+    // lanes past a resource's bands read (0, 0) without a select (bands >= 32, or >= kp)
+    auto load_rows = [&](float* base, int r0, int nrows, int kp, int row_bytes) {
+        // (the address is wave-uniform; readfirstlane says so, else every load became a waterfall loop)
+        const uint64_t a = reinterpret_cast<uint64_t>(base);
+        float* ub = reinterpret_cast<float*>((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a) |
+                                             ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(a >> 32)) << 32));
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(ub, (short)0, __builtin_amdgcn_readfirstlane(nrows * row_bytes), 0x00020000);
+        const int off = u < kp ? 8 * u : 1 << 30;
+#pragma unroll
+        for (int r = 0; r < 8; r++) x[r0 + r] = load_row_pair(rs, off + r * row_bytes);
+    };
+    // Branch-free (a resource of 0 rows reads zeros): the loads of every path then sit in one block
+    // and the waits after them count them exactly (a join made the compiler wait for vmcnt(0)).
+    auto issue_rows = [&](const uint32_t cf, const bool live) {
+        float* cur = A.xlow + (size_t)(live ? cf : 0) * 2048;
+#pragma unroll
+        for (int r = 8; r < 40; r += 8) load_rows(cur + (r - 8) * 64, r, live ? 8 : 0, 32, 256);
+        // (a batch's first frame is necessarily its run's first record: zeros until the state rows)
+        const bool prev = live && cf >= (uint32_t)A.nch;
+        const uint32_t pcf = prev ? cf - A.nch : 0;
+        if (P == 3) load_rows(A.xcarry + (size_t)pcf * kSbrCarryFloats, 0, prev ? 8 : 0, 64, 512);
+        else load_rows(A.xlow + (size_t)pcf * 2048 + 24 * 64, 0, prev ? 8 : 0, 32, 256);
+    };
+    // The record's table index and the record itself: loaded beside the noise table (their round
+    // trip overlaps the barrier's), so that the band-table copy can start right after it.
+    constexpr int NR = sizeof(SbrRec) / 4;
+    auto fetch_rec = [&](const uint32_t cf, int& table, uint32_t& rv) {
+        table = A.recs[cf].table;
+        rv = reinterpret_cast<const uint32_t*>(A.recs + cf)[u < NR ? u : NR - 1];
+    };
+    int table0 = 0;
+    uint32_t rv0 = 0;
+    {
+        const float2 n0 = reinterpret_cast<const float2*>(A.noise)[threadIdx.x];
+        const float2 n1 = reinterpret_cast<const float2*>(A.noise)[threadIdx.x + 256];
+        if (kPhase != 4) fetch_rec(live ? cf : 0, table0, rv0);
+        noise_s[threadIdx.x] = n0;
+        noise_s[threadIdx.x + 256] = n1;
+    }
+    // an LDS-only barrier (__syncthreads' release fence would wait for the record loads too)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+    if (!live) return;
+    HF_STAMP(1);
     auto frame = [&](const uint32_t cf) {
-    const int u = lane_id();
     const int c = (int)(cf % (uint32_t)A.nch);
     // The record and its band tables are read field by field all through the kernel: byte loads
     // at wave-uniform addresses, many inside the envelope and limiter-band loops, each a global
     // round trip the wave waits on.  One coalesced copy into the wave's LDS first; every field
     // read after it is an LDS round trip.
     {
-        const int table = A.recs[cf].table;  // issued beside the record copy
-        const uint32_t* rs = reinterpret_cast<const uint32_t*>(A.recs + cf);
+        int table = table0;
+        uint32_t rv = rv0;
+        if constexpr (kPhase == 4) fetch_rec(cf, table, rv);
+        // every lane loads (clamped indices, no lane-masked branch): all loads of the copy are in
+        // flight together and wait once (a masked loop waited per iteration)
+        constexpr int NT = sizeof(SbrTab) / 4, KT = (NT + 63) / 64;
         uint32_t* rd = reinterpret_cast<uint32_t*>(&L.rec);
-        if (u < (int)(sizeof(SbrRec) / 4)) rd[u] = rs[u];
         const uint32_t* ts = reinterpret_cast<const uint32_t*>(A.tabs + table);
         uint32_t* td = reinterpret_cast<uint32_t*>(&L.tab);
-        for (int i = u; i < (int)(sizeof(SbrTab) / 4); i += 64) td[i] = ts[i];
+        uint32_t tv[KT];
+#pragma unroll
+        for (int j = 0; j < KT; j++) tv[j] = ts[u + 64 * j < NT ? u + 64 * j : NT - 1];
+        if (u < NR) rd[u] = rv;
+#pragma unroll
+        for (int j = 0; j < KT; j++)
+            if (u + 64 * j < NT) td[u + 64 * j] = tv[j];
         wave_sync();
+        HF_STAMP(10);
     }
     const SbrRec& R = L.rec;
     const SbrTab& T = L.tab;
@@ -532,60 +686,30 @@ __global__ __launch_bounds__(256, 3) void sbr_hf_kernel(SbrArgs A)
     const int s_lim = R.lim_bands;
     const float rel = __fdiv_rn(1.0f, 1.0f + 1e-6f);
 
-    // Xsbr of this lane's band (sbr_save_matrix, A/sbr/SBR.java:286-300, then the analysis at
-    // offset tHFGen = 8).  Rows 0..7 are rows 32..39 of frame f-1 AFTER its HF adjustment: below
-    // kx_prev its analysis slots 24..31, from kx_prev up the high band it adjusted (rows 32, 33
-    // always, 34.. when its last envelope ends past slot 32).  That high band is frame f-1's own
-    // output of this launch, so this pass takes rows 0..7 from the analysis alone (bands < kx_prev,
-    // zero above) -- exact unless the frame reads the high band (source band >= kx_prev, kx above
-    // kx_prev or a band without patch with rows 2..7 carried: kSbrDep, jaad_sbr_host.cpp); those
-    // frames run again in fix passes (kPhase 3) that read frame f-1's finished carry rows.  The
-    // first frame of a run reads the slot state's carry rows (exact).  Rows 8..39 = this frame's
-    // analysis slots 0..31 (zero from kx up).  The loads wait for nothing but the record's first
-    // flag: masks that need the band tables would put two more dependent round trips first.
-    float xr[40], xi[40];
-    {
-        const float2* cur = reinterpret_cast<const float2*>(A.xlow + (size_t)cf * 2048);
-        const bool carry = R.first || P == 3;
-        const float2* prv = R.first ? reinterpret_cast<const float2*>(&A.state[(size_t)R.slot * 2 + c].xcarry[0][0][0])
-                          : carry   ? reinterpret_cast<const float2*>(A.xcarry + (size_t)(cf - A.nch) * kSbrCarryFloats)
-                                    : reinterpret_cast<const float2*>(A.xlow + (size_t)(cf - A.nch) * 2048) + 24 * 32;
-        const int kp = carry ? 64 : 32;  // carry rows: every band (zero from kx + M up)
-        const int k = u < kp ? u : kp - 1;
-#pragma unroll
-        for (int r = 0; r < 8; r++) {
-            const float2 v = prv[r * kp + k];
-            xr[r] = u < kp ? v.x : 0.0f;
-            xi[r] = u < kp ? v.y : 0.0f;
-        }
-        const int k32 = u < 32 ? u : 31;
-#pragma unroll
-        for (int r = 8; r < 40; r++) {
-            const float2 v = cur[(r - 8) * 32 + k32];
-            xr[r] = u < 32 ? v.x : 0.0f;
-            xi[r] = u < 32 ? v.y : 0.0f;
-        }
-    }
+    // rows 0..7 of a run's first record: the slot state's carry rows (issue_rows above)
+    issue_rows(cf, true);
+    HF_STAMP(11);
+    if (ufl(R.first)) load_rows(&A.state[(size_t)ufl(R.slot) * 2 + c].xcarry[0][0][0], 0, 8, 64, 512);
     // Parameter lookups issued now, while the Xlow rows are in flight: the generation's source band
     // and chirp factor, and calculate_gain's per-band inputs of every envelope (noise band ->
     // Q_div / Q_div2, resolution band -> E_orig).  Each is a two-level table walk in global memory;
     // fetched inside the envelope loop they were two dependent round trips per envelope.
     const int p_src = T.src_p[u];
-    float bw_k, pEo[5], pQd[5], pQd2[5];
+    float bw_k, pEo[5];
+    int nb_m;  // noise band of band m
     {
         const int gk = T.g_of_k[u];
         bw_k = R.bw[gk < 5 ? gk : 0];
         const int mi = (u - kx >= 0 && u - kx < M) ? u - kx : 0;
         const int nb = T.noise_map[s_lim][mi];
+        nb_m = nb;
         const int rm0 = T.res_map[s_lim][0][mi], rm1 = T.res_map[s_lim][1][mi];
         int eo = (int)R.e_off;
 #pragma unroll
         for (int l = 0; l < 5; l++) {
             const bool on = l < L_E;
-            const int fl = on ? R.f[l] : 0, tnb = on ? R.tnb[l] : 0;
+            const int fl = on ? R.f[l] : 0;
             pEo[l] = on ? A.epool[eo + (fl ? rm1 : rm0)] : 0.0f;
-            pQd[l] = R.q_div[tnb][nb];
-            pQd2[l] = R.q_div2[tnb][nb];
             eo += on ? (fl ? T.n_hi : T.n_lo) : 0;
         }
     }
@@ -610,29 +734,32 @@ __global__ __launch_bounds__(256, 3) void sbr_hf_kernel(SbrArgs A)
             }
     }
 
+    HF_STAMP(2);
     // ---------- HF generation (A/sbr/HFGeneration.java:17-98, 100-196) ----------
     float a0r = 0, a0i = 0, a1r = 0, a1i = 0;
     {
-        float r01r = 0, r01i = 0, r02r = 0, r02i = 0, r11r = 0;
-        float t1r, t1i, t2r = xr[0], t2i = xi[0], t3r = xr[1], t3i = xi[1];
-        const float t4r = t2r, t4i = t2i, t5r = t3r, t5i = t3i;
+        // r01 = (r01r, r01i) += (t3r t2r + t3i t2i, t3i t2r - t3r t2i), r02 likewise with t1:
+        // 2 v_pk_mul + 2 v_pk_add each; r11r += t2r t2r + t2i t2i
+        f2 r01 = {0.0f, 0.0f}, r02 = {0.0f, 0.0f};
+        float r11r = 0;
+        f2 t1, t2 = x[0], t3 = x[1];
+        const f2 t4 = t2, t5 = t3;
 #pragma unroll
         for (int j = 2; j < 40; j++) {
-            t1r = t2r;
-            t1i = t2i;
-            t2r = t3r;
-            t2i = t3i;
-            t3r = xr[j];
-            t3i = xi[j];
-            r01r += t3r * t2r + t3i * t2i;
-            r01i += t3i * t2r - t3r * t2i;
-            r02r += t3r * t1r + t3i * t1i;
-            r02i += t3i * t1r - t3r * t1i;
-            r11r += t2r * t2r + t2i * t2i;
+            t1 = t2;
+            t2 = t3;
+            t3 = x[j];
+            r01 = pk_add(r01, pk_mul_conj(t3, t2));
+            r02 = pk_add(r02, pk_mul_conj(t3, t1));
+            const f2 sq = pk_mul(t2, t2);
+            r11r += sq.x + sq.y;
         }
-        const float r12r = r01r - (t3r * t2r + t3i * t2i) + (t5r * t4r + t5i * t4i);
-        const float r12i = r01i - (t3i * t2r - t3r * t2i) + (t5i * t4r - t5r * t4i);
-        const float r22r = r11r - (t2r * t2r + t2i * t2i) + (t4r * t4r + t4i * t4i);
+        const float r01r = r01.x, r01i = r01.y, r02r = r02.x, r02i = r02.y;
+        const f2 c32 = pk_mul_conj(t3, t2), c54 = pk_mul_conj(t5, t4);
+        const f2 s2 = pk_mul(t2, t2), s4 = pk_mul(t4, t4);
+        const float r12r = r01r - c32.x + c54.x;
+        const float r12i = r01i - c32.y + c54.y;
+        const float r22r = r11r - (s2.x + s2.y) + (s4.x + s4.y);
         const float det = (r11r * r22r) - (rel * ((r12r * r12r) + (r12i * r12i)));
         if (det != 0.0f) {
             const float tmp = __fdiv_rn(1.0f, det);
@@ -646,44 +773,44 @@ __global__ __launch_bounds__(256, 3) void sbr_hf_kernel(SbrArgs A)
         }
         if (((a0r * a0r) + (a0i * a0i) >= 16.0f) || ((a1r * a1r) + (a1i * a1i) >= 16.0f)) a0r = a0i = a1r = a1i = 0.0f;
     }
+    HF_STAMP(3);
     {
         const int p = p_src;
         const bool gen = p != 0xFF;
         const int ps = gen ? p : u;
         const float bw = bw_k;
-        const float bw2 = bw * bw;
-        const float A0r = shfl(a0r, ps) * bw, A1r = shfl(a1r, ps) * bw2;
-        const float A0i = shfl(a0i, ps) * bw, A1i = shfl(a1i, ps) * bw2;
-        float p1r = 0, p1i = 0, p2r = 0, p2i = 0;  // source rows r-2, r-1
-        float sbr_[8], sbi_[8];  // source rows, fetched 8 at a time
+        const f2 bwp = f2{bw, bw * bw};  // (bw, bw2)
+        const f2 A0 = pk_mul_bx(bwp, f2{shfl(a0r, ps), shfl(a0i, ps)});  // (A0r, A0i)
+        const f2 A1 = pk_mul_by(bwp, f2{shfl(a1r, ps), shfl(a1i, ps)});  // (A1r, A1i)
+        f2 p1 = {0.0f, 0.0f}, p2 = {0.0f, 0.0f};  // source rows r-2, r-1
+        f2 sb[8];  // source rows, fetched 8 at a time
 #pragma unroll
         for (int r = 0; r < 40; r++) {
             if ((r & 7) == 0) {
 #pragma unroll
-                for (int q = 0; q < 8; q++) {
-                    sbr_[q] = shfl(xr[r + q], ps);
-                    sbi_[q] = shfl(xi[r + q], ps);
-                }
+                for (int q = 0; q < 8; q++) sb[q] = f2{shfl(x[r + q].x, ps), shfl(x[r + q].y, ps)};
             }
-            const float sr = sbr_[r & 7], si = sbi_[r & 7];
+            const f2 sv = sb[r & 7];
             const int l = r - 2;
             if (gen && l >= first && l < last) {
-                if (bw2 > 0.0f) {
-                    xr[r] = sr + ((A0r * p2r) - (A0i * p2i) + (A1r * p1r) - (A1i * p1i));
-                    xi[r] = si + ((A0i * p2r) + (A0r * p2i) + (A1i * p1r) + (A1r * p1i));
+                if (bwp.y > 0.0f) {
+                    // (A0r p2r - A0i p2i + A1r p1r - A1i p1i, A0i p2r + A0r p2i + A1i p1r + A1r p1i),
+                    // left to right as the Java sums them, then added to the source row
+                    f2 w = pk_add_nlo(pk_mul_xa(A0, p2), pk_mul_ya(A0, p2));
+                    w = pk_add(w, pk_mul_xa(A1, p1));
+                    w = pk_add_nlo(w, pk_mul_ya(A1, p1));
+                    x[r] = pk_add(sv, w);
                 } else {
-                    xr[r] = sr;
-                    xi[r] = si;
+                    x[r] = sv;
                 }
             }
-            p1r = p2r;
-            p1i = p2i;
-            p2r = sr;
-            p2i = si;
+            p1 = p2;
+            p2 = sv;
             if ((r & 7) == 7) __builtin_amdgcn_sched_barrier(0);
         }
     }
 
+    HF_STAMP(4);
     // ---------- HF adjustment (A/sbr/HFAdjustment.java) ----------
     const int m = u - kx;
     const bool band = m >= 0 && m < M;
@@ -692,7 +819,8 @@ __global__ __launch_bounds__(256, 3) void sbr_hf_kernel(SbrArgs A)
         float acc[5] = {0, 0, 0, 0, 0};
 #pragma unroll
         for (int r = 2; r < 40; r++) {
-            const float en = (xr[r] * xr[r]) + (xi[r] * xi[r]);
+            const f2 sq = pk_mul(x[r], x[r]);
+            const float en = sq.x + sq.y;
             const int i = r - 2;
 #pragma unroll
             for (int l = 0; l < 5; l++)
@@ -723,7 +851,8 @@ __global__ __launch_bounds__(256, 3) void sbr_hf_kernel(SbrArgs A)
             float nrg = 0.0f;
 #pragma unroll
             for (int r = 2; r < 40; r++) {
-                const float en = (xr[r] * xr[r]) + (xi[r] * xi[r]);
+                const f2 sq = pk_mul(x[r], x[r]);
+                const float en = sq.x + sq.y;
                 const int i = r - 2;
                 if (i >= ufl(R.t_E[l]) && i < ufl(R.t_E[l + 1])) {
                     for (int d = 0; d < maxw; d++) {
@@ -747,6 +876,7 @@ __global__ __launch_bounds__(256, 3) void sbr_hf_kernel(SbrArgs A)
     }
     wave_sync();
 
+    HF_STAMP(5);
     // calculate_gain (:240-415), per envelope, with every per-band step lane-parallel:
     //   (1) lane m: E_orig, E_curr, Q_M, S_M and the unlimited G;
     //   (2) lane kb (limiter band): acc1, acc2 as the Java's ordered sums over its bands -> G_max;
@@ -776,7 +906,8 @@ __global__ __launch_bounds__(256, 3) void sbr_hf_kernel(SbrArgs A)
             const bool sidx = band && ((smask >> m) & 1);
             float Eom = 0.0f, Ec = 0.0f, Q_M = 0.0f, S_M = 0.0f, G = 0.0f;
             if (band) {  // (1)
-                const float Qd = pQd[l], Qd2 = pQd2[l];
+                const int tnb = ufl(R.tnb[l]);
+                const float Qd = R.q_div[tnb][nb_m], Qd2 = R.q_div2[tnb][nb_m];
                 Eom = pEo[l];
                 Ec = L.ecurr[l][m];
                 const bool smap = (mmask >> m) & 1;
@@ -791,19 +922,22 @@ __global__ __launch_bounds__(256, 3) void sbr_hf_kernel(SbrArgs A)
             if (lim_lane) {  // (2)
                 float acc1 = 0.0f, acc2 = 0.0f;
                 if (wmax <= 16) {
-                    float ve[16], vc[16];
 #pragma unroll
-                    for (int j = 0; j < 16; j++) {
-                        const int mm = ml1 + j < ml2 ? ml1 + j : ml1;
-                        ve[j] = L.gq_eo[mm];
-                        vc[j] = L.ecurr[l][mm];
-                    }
+                    for (int h = 0; h < 16; h += 8) {  // (8 reads in flight: fewer live VGPRs than 16)
+                        float ve[8], vc[8];
 #pragma unroll
-                    for (int j = 0; j < 16; j++)
-                        if (ml1 + j < ml2) {
-                            acc1 += ve[j];
-                            acc2 += vc[j];
+                        for (int j = 0; j < 8; j++) {
+                            const int mm = ml1 + h + j < ml2 ? ml1 + h + j : ml1;
+                            ve[j] = L.gq_eo[mm];
+                            vc[j] = L.ecurr[l][mm];
                         }
+#pragma unroll
+                        for (int j = 0; j < 8; j++)
+                            if (ml1 + h + j < ml2) {
+                                acc1 += ve[j];
+                                acc2 += vc[j];
+                            }
+                    }
                 } else {
                     for (int mm = ml1; mm < ml2; mm++) {
                         acc1 += L.gq_eo[mm];
@@ -833,17 +967,20 @@ __global__ __launch_bounds__(256, 3) void sbr_hf_kernel(SbrArgs A)
             if (lim_lane) {  // (4)
                 float den = 0.0f;
                 if (wmax <= 16) {
-                    float ts[16], te[16], tq[16];
 #pragma unroll
-                    for (int j = 0; j < 16; j++) {
-                        const int mm = ml1 + j < ml2 ? ml1 + j : ml1;
-                        ts[j] = L.den_s[mm];
-                        te[j] = L.den_e[mm];
-                        tq[j] = L.den_q[mm];
+                    for (int h = 0; h < 16; h += 8) {
+                        float ts[8], te[8], tq[8];
+#pragma unroll
+                        for (int j = 0; j < 8; j++) {
+                            const int mm = ml1 + h + j < ml2 ? ml1 + h + j : ml1;
+                            ts[j] = L.den_s[mm];
+                            te[j] = L.den_e[mm];
+                            tq[j] = L.den_q[mm];
+                        }
+#pragma unroll
+                        for (int j = 0; j < 8; j++)
+                            if (ml1 + h + j < ml2) den = ((den + ts[j]) + te[j]) + tq[j];
                     }
-#pragma unroll
-                    for (int j = 0; j < 16; j++)
-                        if (ml1 + j < ml2) den = ((den + ts[j]) + te[j]) + tq[j];
                 } else {
                     for (int mm = ml1; mm < ml2; mm++) den = ((den + L.den_s[mm]) + L.den_e[mm]) + L.den_q[mm];
                 }
@@ -861,6 +998,7 @@ __global__ __launch_bounds__(256, 3) void sbr_hf_kernel(SbrArgs A)
         }
     }
 
+    HF_STAMP(6);
     // G/Q ring after this frame: the last 5 assembled rows (rows >= 26 always, see the host check)
     {
         float* ring = A.gq + (size_t)cf * 640;
@@ -877,6 +1015,7 @@ __global__ __launch_bounds__(256, 3) void sbr_hf_kernel(SbrArgs A)
     }
     if (P == 1) return;
 
+    HF_STAMP(7);
     // hf_assembly (:140-238): lane k = m + kx
     {
         const int mi = band ? m : 0;
@@ -894,40 +1033,48 @@ __global__ __launch_bounds__(256, 3) void sbr_hf_kernel(SbrArgs A)
             // (the G/Q ring output above is built from gl/ql directly); the rows walk the
             // envelopes in order, so each envelope's values are read from LDS once
             int l = -1, next = first;  // next: first row of the envelope after l
-            float G_filt = 0.0f, Q_filt = 0.0f, S = 0.0f;
+            f2 gqf = {0.0f, 0.0f}, Sv = {0.0f, 0.0f};  // (G_filt, Q_filt), (S, rev * S)
+            float2 nzv[8];  // noise entries of the next 8 rows
 #pragma unroll
             for (int r = 2; r < 40; r++) {
                 const int i = r - 2;
+                if (((r - 2) & 7) == 0) {
+#pragma unroll
+                    for (int q = 0; q < 8; q++)
+                        nzv[q] = noise_s[(noise0 + (uint32_t)(i + q - first) * (uint32_t)M + (uint32_t)mi + 1u) & 511u];
+                }
                 if (i < first || i >= last) continue;
                 if (i >= next) {  // wave-uniform
                     while (l + 1 < L_E && i >= ufl(R.t_E[l + 1])) l++;
                     next = l + 1 < L_E ? ufl(R.t_E[l + 1]) : 64;
                     const bool no_noise = (ufl(R.no_noise) >> l) & 1;
-                    G_filt = L.gl[l][mi];
-                    S = L.sl[l][mi];
-                    Q_filt = (S != 0.0f || no_noise) ? 0.0f : L.ql[l][mi];
+                    const float S = L.sl[l][mi];
+                    gqf = f2{L.gl[l][mi], (S != 0.0f || no_noise) ? 0.0f : L.ql[l][mi]};
+                    Sv = f2{S, rev * S};
                 }
-                const int fi = (int)((noise0 + (uint32_t)(i - first) * (uint32_t)M + (uint32_t)mi + 1u) & 511u);
                 const int fs = (int)((sine0 + (uint32_t)(i - first)) & 3u);
                 if (band) {
-                    const float2 nz = noise_s[fi];
-                    float vr = G_filt * xr[r] + (Q_filt * nz.x);
-                    float vi = G_filt * xi[r] + (Q_filt * nz.y);
-                    const float phr = fs == 0 ? 1.0f : fs == 2 ? -1.0f : 0.0f;
-                    const float phi = fs == 1 ? 1.0f : fs == 3 ? -1.0f : 0.0f;
-                    vr += S * phr;
-                    vi += (rev * S) * phi;
-                    xr[r] = vr;
-                    xi[r] = vi;
+                    const float2 nz = nzv[(r - 2) & 7];
+                    // (G xr + Q nz.re + S phr, G xi + Q nz.im + (rev S) phi)
+                    const f2 ph = f2{fs == 0 ? 1.0f : fs == 2 ? -1.0f : 0.0f, fs == 1 ? 1.0f : fs == 3 ? -1.0f : 0.0f};
+                    const f2 v = pk_add(pk_mul_bx(gqf, x[r]), pk_mul_by(gqf, f2{nz.x, nz.y}));
+                    x[r] = pk_add(v, pk_mul(Sv, ph));
                 }
             }
         } else {
         int l = -1, next = first;  // envelope walk as above
         bool no_noise = false;
         float gnew = 0.0f, qnew = 0.0f, S = 0.0f;
+        f2 Sv = {0.0f, 0.0f};  // (S, rev * S)
+        float2 nzv[8];  // noise entries of the next 8 rows, read before them (no LDS wait per row)
 #pragma unroll
         for (int r = 2; r < 40; r++) {
             const int i = r - 2;
+            if (((r - 2) & 7) == 0) {
+#pragma unroll
+                for (int q = 0; q < 8; q++)
+                    nzv[q] = noise_s[(noise0 + (uint32_t)(i + q - first) * (uint32_t)M + (uint32_t)mi + 1u) & 511u];
+            }
             if (i < first || i >= last) continue;
             if (i >= next) {  // wave-uniform
                 while (l + 1 < L_E && i >= ufl(R.t_E[l + 1])) l++;
@@ -936,6 +1083,7 @@ __global__ __launch_bounds__(256, 3) void sbr_hf_kernel(SbrArgs A)
                 gnew = L.gl[l][mi];
                 qnew = L.ql[l][mi];
                 S = L.sl[l][mi];
+                Sv = f2{S, rev * S};
             }
 #pragma unroll
             for (int j = 0; j < 4; j++) {
@@ -960,26 +1108,21 @@ __global__ __launch_bounds__(256, 3) void sbr_hf_kernel(SbrArgs A)
                 Q_filt = qnew;
             }
             Q_filt = (S != 0.0f || no_noise) ? 0.0f : Q_filt;
-            const int fi = (int)((noise0 + (uint32_t)(i - first) * (uint32_t)M + (uint32_t)mi + 1u) & 511u);
             const int fs = (int)((sine0 + (uint32_t)(i - first)) & 3u);
             if (band) {
-                const float2 nz = noise_s[fi];
-                const float nr = nz.x, ni = nz.y;
-                float vr = G_filt * xr[r] + (Q_filt * nr);
-                float vi = G_filt * xi[r] + (Q_filt * ni);
-                const float phr = fs == 0 ? 1.0f : fs == 2 ? -1.0f : 0.0f;
-                const float phi = fs == 1 ? 1.0f : fs == 3 ? -1.0f : 0.0f;
-                vr += S * phr;
-                vi += (rev * S) * phi;
-                xr[r] = vr;
-                xi[r] = vi;
+                const float2 nz = nzv[(r - 2) & 7];
+                const f2 gqf = f2{G_filt, Q_filt};
+                const f2 ph = f2{fs == 0 ? 1.0f : fs == 2 ? -1.0f : 0.0f, fs == 1 ? 1.0f : fs == 3 ? -1.0f : 0.0f};
+                const f2 v = pk_add(pk_mul_bx(gqf, x[r]), pk_mul_by(gqf, f2{nz.x, nz.y}));
+                x[r] = pk_add(v, pk_mul(Sv, ph));
             }
-            __builtin_amdgcn_sched_barrier(0);
+            if (((r - 2) & 7) == 7) __builtin_amdgcn_sched_barrier(0);
         }
         }
     }
 
 
+    HF_STAMP(8);
     // ---------- outputs ----------
     // synthesis input X[l][k] = Xsbr[l + tHFAdj][k] for k < kx_band + M_band (Channel.java:619-645);
     // rows l < t_E[0] take kx_prev/M_prev and the carried rows, patched in by the synthesis kernel
@@ -990,20 +1133,26 @@ __global__ __launch_bounds__(256, 3) void sbr_hf_kernel(SbrArgs A)
         // (PS: straight into X_left's place, xps[f][0], which the PS analysis patches rows
         // l < t_E[0] of; nch = 1 there)
         float2* xs = reinterpret_cast<float2*>(A.ps ? A.xps + (size_t)cf * 8192 : A.xsyn + (size_t)cf * 4096);
-        const int kcur = kx + M;
-        if (u < (int)R.blim) {
+        const int kcur = kx + M, blim = ufl(R.blim);
+        // bands below kx + M keep their rows, the rest up to the band limit are zero (two store
+        // loops under complementary lane masks, no per-row select)
+        if (u < min(blim, kcur)) {
 #pragma unroll
-            for (int l = 0; l < 32; l++) {
-                const bool keep = u < kcur;
-                xs[l * 64 + u] = make_float2(keep ? xr[l + 2] : 0.0f, keep ? xi[l + 2] : 0.0f);
-            }
+            for (int l = 0; l < 32; l++) xs[l * 64 + u] = make_float2(x[l + 2].x, x[l + 2].y);
+        } else if (u < blim) {
+#pragma unroll
+            for (int l = 0; l < 32; l++) xs[l * 64 + u] = make_float2(0.0f, 0.0f);
         }
         // Xsbr rows 32..39, every band (zero from kx + M up): the next frame's rows 0..7, the PS
         // look-ahead rows, the slot state
         float2* xc = reinterpret_cast<float2*>(A.xcarry + (size_t)cf * kSbrCarryFloats);
 #pragma unroll
-        for (int j = 0; j < 8; j++) xc[j * 64 + u] = make_float2(xr[32 + j], xi[32 + j]);
+        for (int j = 0; j < 8; j++) xc[j * 64 + u] = make_float2(x[32 + j].x, x[32 + j].y);
     }
+#if defined(JAAD_HF_STAMPS)
+    HF_STAMP(9);
+    if (kPhase == 0 && A.dbg && u < 12) reinterpret_cast<uint64_t*>(A.dbg)[(size_t)cf * 16 + u] = hf_t[u];
+#endif
     };
     if constexpr (kPhase == 4) {
         for (uint32_t it = 0; it < n_iter; it++) {
