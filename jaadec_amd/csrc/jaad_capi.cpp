@@ -80,6 +80,18 @@ struct PinnedBuf {
     }
 };
 
+// Host worker threads of a context: 16 (one GPU's CPU share on the target nodes) or fewer CPUs;
+// JAAD_HOST_THREADS overrides (1..64).
+static int host_threads()
+{
+    if (const char* e = std::getenv("JAAD_HOST_THREADS")) {
+        const int v = std::atoi(e);
+        if (v >= 1 && v <= 64) return v;
+    }
+    const unsigned hw = std::thread::hardware_concurrency();
+    return (int)std::min(16u, hw ? hw : 1u);
+}
+
 // Persistent host workers for the per-call record build (fn(t) for t < size(); the caller runs
 // t = 0), so a call does not pay thread start-up.
 class WorkerPool {
@@ -1561,9 +1573,7 @@ int jaad_ctx_create(const jaad_stream_cfg* cfg, uint32_t n_slots, int device, ja
         if ((e = hipStreamCreateWithFlags(&ctx->cstream, hipStreamNonBlocking)) != hipSuccess)
             return bail(e, "hipStreamCreate copy");
         {
-            const unsigned hw = std::thread::hardware_concurrency();
-            const int nw = (int)std::min(16u, hw ? hw : 1u);  // the box's CPU share per GPU
-            ctx->workers.reset(new (std::nothrow) WorkerPool(nw));
+            ctx->workers.reset(new (std::nothrow) WorkerPool(host_threads()));
         }
         for (RecSet& r : ctx->rsets) {
             if ((e = hipEventCreateWithFlags(&r.copied, hipEventDisableTiming)) != hipSuccess) return bail(e, "hipEventCreate");
@@ -1774,8 +1784,7 @@ static int io_setup(jaad_ctx* ctx)
         HIPCHK(hipEventCreateWithFlags(&ctx->ev_k[i], hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&ctx->ev_out[i], hipEventDisableTiming));
     }
-    const unsigned hw = std::thread::hardware_concurrency();
-    ctx->io.reset(new (std::nothrow) WorkerPool((int)std::min(16u, hw ? hw : 1u)));
+    ctx->io.reset(new (std::nothrow) WorkerPool(host_threads()));
     if (!ctx->io) return JAAD_ERR_NOMEM;
     return JAAD_OK;
 }
