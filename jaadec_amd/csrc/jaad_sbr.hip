@@ -36,6 +36,10 @@ struct HfLds {
     SbrTab tab;                             // copied once (see sbr_hf_kernel)
 };
 static_assert(sizeof(SbrRec) % 4 == 0 && sizeof(SbrTab) % 4 == 0, "record copies are dword-wise");
+// the fused analysis (sbr_hf_kernel<5>) stages its 1568-sample window in the gain-stage scratch and
+// reads SbrRec::first / ::slot from the record's dwords 2 (byte 3) and 16
+static_assert(offsetof(HfLds, rec) - offsetof(HfLds, ecurr) >= 1568 * sizeof(float), "analysis window in the gain scratch");
+static_assert(offsetof(SbrRec, first) == 11 && offsetof(SbrRec, slot) == 64, "SbrRec dwords read by readlane");
 
 // Math.round + short clamp (S/SampleBuffer.java:190-205)
 __device__ __forceinline__ int java_round16(float s)
@@ -395,6 +399,65 @@ __device__ __forceinline__ size_t batch_cf(const SbrArgs& A, size_t rcf)
 // ---------------------------------------------------------------------------------------------
 static_assert(sizeof(SbrChState) % 16 == 0 && offsetof(SbrChState, tail) % 16 == 0, "analysis reads tail as float4");
 
+// One pass of the analysis: slot 32-sample block l = 2p + half of the frame whose sample g is
+// smp(g) (g may be negative: the samples before the frame), band e of it in lane (half, e) as
+// (re, im), zero from band kx up.  Shared by sbr_analysis_kernel and the fused HF kernel.
+struct QmfCoefs {
+    float ca[5], cb[5];
+};
+__device__ __forceinline__ QmfCoefs load_qmf_coefs(const float* qmf_c, int e)
+{
+    QmfCoefs Q;
+#pragma unroll
+    for (int j = 0; j < 5; j++) {
+        Q.ca[j] = qmf_c[2 * (e + 64 * j)];
+        Q.cb[j] = qmf_c[2 * (e + 32 + 64 * j)];
+    }
+    return Q;
+}
+template <class Smp>
+__device__ __forceinline__ float2 qmf_analysis_pass(Smp smp, int l, int e, int hb, int E, const DctConst& K,
+                                                    const QmfCoefs& Q, int kx)
+{
+    // v[v_index + x] = sample (32 l + 31 - x); u[n] = sum_j v[n + 64 j] * c[2 (n + 64 j)]  (:19-30)
+    const int base = 32 * l + 31;
+    float ulo, uhi;
+    {
+        const float a0 = smp(base - e) * Q.ca[0], a1 = smp(base - e - 64) * Q.ca[1];
+        const float a2 = smp(base - e - 128) * Q.ca[2], a3 = smp(base - e - 192) * Q.ca[3];
+        const float a4 = smp(base - e - 256) * Q.ca[4];
+        ulo = (((a0 + a1) + a2) + a3) + a4;
+        const int n = e + 32;
+        const float b0 = smp(base - n) * Q.cb[0], b1 = smp(base - n - 64) * Q.cb[1];
+        const float b2 = smp(base - n - 128) * Q.cb[2], b3 = smp(base - n - 192) * Q.cb[3];
+        const float b4 = smp(base - n - 256) * Q.cb[4];
+        uhi = (((b0 + b1) + b2) + b3) + b4;
+    }
+    // in_real[0] = u[0], in_real[n] = -u[64-n]; in_imag[m] = u[32-m]  (:39-46)
+    const int src = hb + ((32 - e) & 31);
+    const float slo = shfl(ulo, src), shi = shfl(uhi, src);
+    const float in_r = e == 0 ? ulo : -shi;
+    const float in_i = e == 0 ? uhi : slo;
+    float orr, oi;
+    dct4(K, e, E, in_r, in_i, orr, oi);
+    // X[2n] = 2 out[n], X[2n+1] = -2 swap(out[31-n]) (:52-71): lane (half, k) holds band k of slot
+    // 2p + half (the DCT left output element m in lane bitrev5(m))
+    const int k = e;
+    const int srcl = hb + bitrev5((k & 1) ? 31 - (k >> 1) : (k >> 1));
+    const float vr = shfl(orr, srcl), vi = shfl(oi, srcl);
+    float re = 0.0f, im = 0.0f;
+    if (k < kx) {
+        if (k & 1) {
+            re = -2.0f * vi;
+            im = -2.0f * vr;
+        } else {
+            re = 2.0f * vr;
+            im = 2.0f * vi;
+        }
+    }
+    return make_float2(re, im);
+}
+
 __global__ __launch_bounds__(256) void sbr_analysis_kernel(SbrArgs A)
 {
     __shared__ __attribute__((aligned(16))) float win_s[kWavesPerBlock][288 + 1024];  // the 288 samples before the frame + the frame
@@ -411,12 +474,7 @@ __global__ __launch_bounds__(256) void sbr_analysis_kernel(SbrArgs A)
     const float* prev = R.first ? A.state[(size_t)R.slot * 2 + c].tail : A.time + batch_cf(A, cf - A.nch) * 1024 + 736;
     const int E = bitrev5(e);
     const DctConst K = load_dct_const(A.dct, e, E);
-    float ca[5], cb[5];
-#pragma unroll
-    for (int j = 0; j < 5; j++) {
-        ca[j] = A.qmf_c[2 * (e + 64 * j)];
-        cb[j] = A.qmf_c[2 * (e + 32 + 64 * j)];
-    }
+    const QmfCoefs Q = load_qmf_coefs(A.qmf_c, e);
     // the window's 1312 samples are staged in LDS with coalesced loads; the 160 taps per lane are
     // LDS reads (consecutive lanes, consecutive addresses)
     // (16-byte loads: tail and frame offsets are multiples of 4 floats, sizeof(SbrChState) of 16 B)
@@ -429,45 +487,8 @@ __global__ __launch_bounds__(256) void sbr_analysis_kernel(SbrArgs A)
     wave_sync();
     auto smp = [&](int g) { return win[288 + g]; };
     float* out = A.xlow + (size_t)cf * 32 * 32 * 2;
-    for (int p = 0; p < 16; p++) {
-        // v[v_index + x] = sample (32 l + 31 - x); u[n] = sum_j v[n + 64 j] * c[2 (n + 64 j)]  (:19-30)
-        const int base = 32 * (2 * p + half) + 31;
-        float ulo, uhi;
-        {
-            const float a0 = smp(base - e) * ca[0], a1 = smp(base - e - 64) * ca[1];
-            const float a2 = smp(base - e - 128) * ca[2], a3 = smp(base - e - 192) * ca[3];
-            const float a4 = smp(base - e - 256) * ca[4];
-            ulo = (((a0 + a1) + a2) + a3) + a4;
-            const int n = e + 32;
-            const float b0 = smp(base - n) * cb[0], b1 = smp(base - n - 64) * cb[1];
-            const float b2 = smp(base - n - 128) * cb[2], b3 = smp(base - n - 192) * cb[3];
-            const float b4 = smp(base - n - 256) * cb[4];
-            uhi = (((b0 + b1) + b2) + b3) + b4;
-        }
-        // in_real[0] = u[0], in_real[n] = -u[64-n]; in_imag[m] = u[32-m]  (:39-46)
-        const int src = hb + ((32 - e) & 31);
-        const float slo = shfl(ulo, src), shi = shfl(uhi, src);
-        const float in_r = e == 0 ? ulo : -shi;
-        const float in_i = e == 0 ? uhi : slo;
-        float orr, oi;
-        dct4(K, e, E, in_r, in_i, orr, oi);
-        // X[2n] = 2 out[n], X[2n+1] = -2 swap(out[31-n]) (:52-71): lane (half, k) stores band k of
-        // slot 2p + half (the DCT left output element m in lane bitrev5(m))
-        const int k = e;
-        const int srcl = hb + bitrev5((k & 1) ? 31 - (k >> 1) : (k >> 1));
-        const float vr = shfl(orr, srcl), vi = shfl(oi, srcl);
-        float re = 0.0f, im = 0.0f;
-        if (k < kx) {
-            if (k & 1) {
-                re = -2.0f * vi;
-                im = -2.0f * vr;
-            } else {
-                re = 2.0f * vr;
-                im = 2.0f * vi;
-            }
-        }
-        reinterpret_cast<float2*>(out)[(2 * p + half) * 32 + k] = make_float2(re, im);
-    }
+    for (int p = 0; p < 16; p++)
+        reinterpret_cast<float2*>(out)[(2 * p + half) * 32 + e] = qmf_analysis_pass(smp, 2 * p + half, e, hb, E, K, Q, kx);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -558,7 +579,11 @@ __device__ __forceinline__ f2 load_row_pair(__amdgpu_buffer_rsrc_t r, int off)
 template <int kPhase>
 __global__ __launch_bounds__(256, 3) void sbr_hf_kernel(SbrArgs A)
 {
-    constexpr int P = kPhase == 4 ? 3 : kPhase;  // the body's phase
+    // phase 5: phase 0 with the QMF analysis fused in (launches without smoothing and without fix
+    // passes, launch_sbr): the rows come from the core time samples in registers, not from X_low
+    // in HBM (no sbr_analysis_kernel, no X_low round trip)
+    constexpr bool kFused = kPhase == 5;
+    constexpr int P = kPhase == 4 ? 3 : kFused ? 0 : kPhase;  // the body's phase
 #if defined(JAAD_HF_STAMPS)
     uint64_t hf_t[16] = {};
 #endif
@@ -631,10 +656,23 @@ __global__ __launch_bounds__(256, 3) void sbr_hf_kernel(SbrArgs A)
     };
     int table0 = 0;
     uint32_t rv0 = 0;
+    // (fused) the analysis constants of lane (half, e) and the previous record's flags and table
+    // (its kx masks rows 0..7, as sbr_analysis_kernel masked that frame's X_low)
+    [[maybe_unused]] const int ea = u & 31, hba = u & 32, Ea = bitrev5(ea);
+    [[maybe_unused]] DctConst Ka;
+    [[maybe_unused]] QmfCoefs Qa;
+    [[maybe_unused]] uint32_t pflags = 0, ptable = 0;
     {
         const float2 n0 = reinterpret_cast<const float2*>(A.noise)[threadIdx.x];
         const float2 n1 = reinterpret_cast<const float2*>(A.noise)[threadIdx.x + 256];
         if (kPhase != 4) fetch_rec(live ? cf : 0, table0, rv0);
+        if constexpr (kFused) {
+            Ka = load_dct_const(A.dct, ea, Ea);
+            Qa = load_qmf_coefs(A.qmf_c, ea);
+            const uint32_t pcf = live && cf >= (uint32_t)A.nch ? cf - A.nch : 0;
+            pflags = A.recs[pcf].flags;
+            ptable = A.recs[pcf].table;
+        }
         noise_s[threadIdx.x] = n0;
         noise_s[threadIdx.x + 256] = n1;
     }
@@ -663,6 +701,27 @@ __global__ __launch_bounds__(256, 3) void sbr_hf_kernel(SbrArgs A)
         uint32_t tv[KT];
 #pragma unroll
         for (int j = 0; j < KT; j++) tv[j] = ts[u + 64 * j < NT ? u + 64 * j : NT - 1];
+        if constexpr (kFused) {
+            // the analysis window into the wave's gain scratch (free until the gain stage):
+            // win[0..543] = samples 480..1023 of the previous record's frame (a run's first record:
+            // win[256..543] = the slot state's 288-sample tail), win[544..1567] = this frame
+            const bool firstr = (__builtin_amdgcn_readlane(rv, 2) >> 24) != 0;  // SbrRec::first (byte 11)
+            const uint32_t slot = __builtin_amdgcn_readlane(rv, 16);             // SbrRec::slot
+            const float4* cur4 = reinterpret_cast<const float4*>(A.time + batch_cf(A, cf) * 1024);
+            const float4* prv4 = firstr ? reinterpret_cast<const float4*>(A.state[(size_t)slot * 2 + c].tail) - 64
+                                        : reinterpret_cast<const float4*>(A.time + batch_cf(A, cf - A.nch) * 1024 + 480);
+            float4* w4 = reinterpret_cast<float4*>(&L.ecurr[0][0]);
+            float4 wv[7];
+#pragma unroll
+            for (int j = 0; j < 7; j++) {  // 392 float4 = 136 (previous) + 256 (this frame)
+                const int i = u + 64 * j;
+                const bool pv = i < 136, skip = i >= 392 || (firstr && i < 64);
+                wv[j] = skip ? make_float4(0.f, 0.f, 0.f, 0.f) : pv ? prv4[i] : cur4[i - 136];
+            }
+#pragma unroll
+            for (int j = 0; j < 7; j++)
+                if (u + 64 * j < 392) w4[u + 64 * j] = wv[j];
+        }
         if (u < NR) rd[u] = rv;
 #pragma unroll
         for (int j = 0; j < KT; j++)
@@ -687,7 +746,32 @@ __global__ __launch_bounds__(256, 3) void sbr_hf_kernel(SbrArgs A)
     const float rel = __fdiv_rn(1.0f, 1.0f + 1e-6f);
 
     // rows 0..7 of a run's first record: the slot state's carry rows (issue_rows above)
-    issue_rows(cf, true);
+    if constexpr (kFused) {
+        // QMF analysis (A/sbr/AnalysisFilterbank.java:9-73, qmf_analysis_pass): pass p gives slots
+        // 2p (lanes 0..31) and 2p + 1 (lanes 32..63); one v_permlane32_swap brings both to lane =
+        // band.  Rows 8..39 = this frame's slots 0..31 (kx of this record); rows 0..7 = the previous
+        // frame's slots 24..31 (its kx), i.e. this frame's "slots -8..-1"; a run's first record
+        // takes them from the slot state below.
+        const float* win = &L.ecurr[0][0] + 544;
+        auto smp = [&](int g) { return win[g]; };
+        const int kxc = (R.flags & kSbrProcess) ? kx : 32;
+        const int kxp = (pflags & kSbrProcess) ? (int)A.tabs[ptable].kx : 32;
+        const bool firstr = ufl(R.first) != 0;
+#pragma unroll
+        for (int p = -4; p < 16; p++) {
+            if (p < 0 && firstr) continue;
+            const float2 v = qmf_analysis_pass(smp, 2 * p + (hba >> 5), ea, hba, Ea, Ka, Qa, p < 0 ? kxp : kxc);
+            const auto sr = __builtin_amdgcn_permlane32_swap(__float_as_int(v.x), __float_as_int(v.x), false, false);
+            const auto si = __builtin_amdgcn_permlane32_swap(__float_as_int(v.y), __float_as_int(v.y), false, false);
+            // lanes 0..31: own value = slot 2p, the swapped one = slot 2p + 1; bands >= 32 are zero
+            const int r0 = 8 + 2 * p;
+            x[r0] = u < 32 ? f2{v.x, v.y} : f2{0.0f, 0.0f};
+            x[r0 + 1] = u < 32 ? f2{__int_as_float(sr[1]), __int_as_float(si[1])} : f2{0.0f, 0.0f};
+        }
+        wave_sync();  // (the window's LDS is the gain stage's scratch)
+    } else {
+        issue_rows(cf, true);
+    }
     HF_STAMP(11);
     if (ufl(R.first)) load_rows(&A.state[(size_t)ufl(R.slot) * 2 + c].xcarry[0][0][0], 0, 8, 64, 512);
     // Parameter lookups issued now, while the Xlow rows are in flight: the generation's source band
@@ -1680,6 +1764,15 @@ hipError_t launch_sbr(const SbrArgs& a, hipStream_t stream, const uint32_t* fix_
     const dim3 blk(256);
     if (a.n_cf) {
         const dim3 g((a.n_cf + kWavesPerBlock - 1) / kWavesPerBlock);
+        // no smoothing and no fix pass: the analysis runs inside the HF kernel (phase 5), X_low never
+        // goes through HBM (JAAD_SBR_FUSED=0: the separate kernels, for A/B)
+        static const bool fuse_ok = [] {
+            const char* e = std::getenv("JAAD_SBR_FUSED");
+            return !(e && e[0] == '0');
+        }();
+        if (fuse_ok && !a.smoothing && n_fix_passes == 0 && !a.n_chains) {
+            hipLaunchKernelGGL(sbr_hf_kernel<5>, g, blk, 0, stream, a);
+        } else {
         hipLaunchKernelGGL(sbr_analysis_kernel, g, blk, 0, stream, a);
         if (a.smoothing) {
             hipLaunchKernelGGL(sbr_hf_kernel<1>, g, blk, 0, stream, a);
@@ -1701,6 +1794,7 @@ hipError_t launch_sbr(const SbrArgs& a, hipStream_t stream, const uint32_t* fix_
         if (a.n_chains)  // links past kSbrFixPasses: fa.fix now points at the walker's lists
             hipLaunchKernelGGL(sbr_hf_kernel<4>, dim3((a.n_chains + kWavesPerBlock - 1) / kWavesPerBlock), blk, 0,
                                stream, fa);
+        }
     }
     if (a.ps) {
         const hipError_t e = launch_ps(a, stream);
