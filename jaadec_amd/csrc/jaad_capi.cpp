@@ -909,6 +909,8 @@ int launch_sbr_stage(jaad_ctx* ctx, const jaad_batch* b, void* pcm, uint32_t fla
                 i++;
             }
             if (rcs[t]) break;
+            if (i > rbeg[r])
+                for (int c = 0; c < nch; c++) recs[(size_t)(i - 1) * nch + c].flags |= kSbrLast;
             // one band limit for the whole run: the highest of its records' and of the stream's
             // past (a band's PS all-pass state is zero only if no frame ever had input there);
             // rewritten only where a record's own limit is lower

@@ -45,6 +45,7 @@ enum : uint8_t {
     kSbrProcess = 8,     // a header has been seen (else analysis only, kx = 32)
     kSbrPsOn = 16,       // PS config: this frame carries PS data (SBR1.isPSUsed, A/sbr/SBR1.java:136)
     kSbrDep = 32,        // reads the high band of frame f-1's Xsbr rows 32..39: an HF fix pass
+    kSbrLast = 64,       // the last record of its run in this call (its G/Q ring goes to the slot state)
 };
 
 // One channel-frame.  232 bytes.  The SBR stages run on the call's SBR-processed frames only,

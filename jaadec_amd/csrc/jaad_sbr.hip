@@ -1083,8 +1083,10 @@ __global__ __launch_bounds__(256, 3) void sbr_hf_kernel(SbrArgs A)
     }
 
     HF_STAMP(6);
-    // G/Q ring after this frame: the last 5 assembled rows (rows >= 26 always, see the host check)
-    {
+    // G/Q ring after this frame: the last 5 assembled rows (rows >= 26 always, see the host check).
+    // Read by the next frame's smoothing (launches with smoothing) and, for a run's last record, by
+    // sbr_state_kernel: other records of a launch without smoothing skip the 2.5 KB.
+    if (A.smoothing || (ufl(R.flags) & kSbrLast)) {
         float* ring = A.gq + (size_t)cf * 640;
         const int rows = last - first;
         for (int j = 0; j < 5; j++) {
