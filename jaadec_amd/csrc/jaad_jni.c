@@ -28,11 +28,12 @@ static void* addr(JNIEnv* env, jobject bb, jlong need) {
 }
 
 /* static native long nativeCreate(int sfIndex, int channelConfig, int tnsMode, int sbr, int ps,
- *     int nSlots, int device); sfIndex is the core (AAC) rate, the SBR rate is twice it */
+ *     int precision, int nSlots, int device); sfIndex is the core (AAC) rate, the SBR rate is twice
+ *     it; precision = JAAD_PRECISION_EXACT (0) or JAAD_PRECISION_LSB1 (1) */
 JNIEXPORT jlong JNICALL Java_net_sourceforge_jaad_aac_gpu_GpuDSP_nativeCreate(JNIEnv* env, jclass cls, jint sf_index,
                                                                             jint channel_config, jint tns_mode,
-                                                                            jint sbr, jint ps, jint n_slots,
-                                                                            jint device) {
+                                                                            jint sbr, jint ps, jint precision,
+                                                                            jint n_slots, jint device) {
     (void)cls;
     jaad_stream_cfg cfg;
     memset(&cfg, 0, sizeof cfg);
@@ -44,6 +45,7 @@ JNIEXPORT jlong JNICALL Java_net_sourceforge_jaad_aac_gpu_GpuDSP_nativeCreate(JN
     cfg.sbr = (uint8_t)(sbr || ps);
     cfg.ps = (uint8_t)ps;
     cfg.ext_sf_index = (uint8_t)(cfg.sbr ? sf_index - 3 : 0);
+    cfg.precision = (uint8_t)precision;  /* jaad_ctx_create rejects values other than 0 / 1 */
     jaad_ctx* ctx = NULL;
     int rc = jaad_ctx_create(&cfg, (uint32_t)n_slots, device, &ctx);
     if (rc) {

@@ -26,7 +26,7 @@ def _lib():
     L.jni_mock_env.restype = C.c_void_p
     L.jni_mock_take_exception.argtypes = [C.c_char_p, C.c_int, C.c_char_p, C.c_int]
     create = getattr(L, PFX + "nativeCreate")
-    create.argtypes = [C.c_void_p, C.c_void_p] + [C.c_int32] * 7
+    create.argtypes = [C.c_void_p, C.c_void_p] + [C.c_int32] * 8
     create.restype = C.c_int64
     getattr(L, PFX + "nativeDestroy").argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
     decode = getattr(L, PFX + "nativeDecode")
@@ -105,7 +105,7 @@ def test_create_without_gpu_throws_no_device():
     if torch.cuda.device_count() > 0:
         pytest.skip("a GPU is present")
     L = _lib()
-    h = getattr(L, PFX + "nativeCreate")(L.jni_mock_env(), None, 3, 2, 0, 0, 0, 4, 0)
+    h = getattr(L, PFX + "nativeCreate")(L.jni_mock_env(), None, 3, 2, 0, 0, 0, 0, 4, 0)
     assert h == 0
     cls, msg = _exception(L)
     assert cls == AAC_EXC and N.strerror(N.ERR_NO_DEVICE) in msg
@@ -119,7 +119,7 @@ def test_decode_through_direct_buffers_and_capacity_checks():
     b = N.synth_batch(p)
     with N.Context(N.make_cfg(), 3) as ctx:
         want = ctx.decode(b, N.PCM_BIG_ENDIAN)
-    h = getattr(L, PFX + "nativeCreate")(env, None, 3, 2, 0, 0, 0, 3, 0)
+    h = getattr(L, PFX + "nativeCreate")(env, None, 3, 2, 0, 0, 0, 0, 3, 0)
     assert h and _exception(L) is None
     decode = getattr(L, PFX + "nativeDecode")
     try:
@@ -204,7 +204,7 @@ def test_coupled_decode_through_direct_buffers():
     b = coupled_batch(2, n_streams=2, fps=12, seed=4)
     with N.Context(N.make_cfg(), 2) as ctx:
         want = ctx.decode(b, N.PCM_BIG_ENDIAN)
-    h = getattr(L, PFX + "nativeCreate")(env, None, 3, 2, 0, 0, 0, 2, 0)
+    h = getattr(L, PFX + "nativeCreate")(env, None, 3, 2, 0, 0, 0, 0, 2, 0)
     assert h and _exception(L) is None
     try:
         out = np.zeros_like(want)
@@ -252,7 +252,7 @@ def test_coupled_he_aac_v2_decode_through_direct_buffers():
     b.cce_terms = np.array(terms, N.CCE_TERM_DTYPE)
     with N.Context(cfg, 3) as ctx:
         want = ctx.decode(b, N.PCM_BIG_ENDIAN)
-    h = getattr(L, PFX + "nativeCreate")(env, None, p.sf_index, p.channel_config, 0, 1, 1, 3, 0)
+    h = getattr(L, PFX + "nativeCreate")(env, None, p.sf_index, p.channel_config, 0, 1, 1, 0, 3, 0)
     assert h and _exception(L) is None
     try:
         out = np.zeros_like(want)
@@ -273,3 +273,35 @@ def test_coupled_he_aac_v2_decode_through_direct_buffers():
         assert cls == AAC_EXC and N.strerror(N.ERR_INVALID_ARG) in msg
     finally:
         getattr(L, PFX + "nativeDestroy")(env, None, h)
+
+
+@pytest.mark.gpu
+def test_lsb1_precision_through_the_jni_create():
+    """nativeCreate's precision argument reaches jaad_stream_cfg.precision: JAAD_PRECISION_LSB1 decodes
+    the stereo batch the same as the Python entry's LSB1 context (within 1 LSB of the exact PCM, and
+    not identical to it); a value other than 0 / 1 is refused at create."""
+    L = _lib()
+    env = L.jni_mock_env()
+    p = N.synth_params(2, n_streams=3, frames_per_stream=20)
+    b = N.synth_batch(p)
+    with N.Context(N.make_cfg(precision=N.PRECISION_LSB1), 3) as ctx:
+        want = ctx.decode(b, N.PCM_BIG_ENDIAN)
+    with N.Context(N.make_cfg(), 3) as ctx:
+        exact = ctx.decode(b, N.PCM_BIG_ENDIAN)
+    h = getattr(L, PFX + "nativeCreate")(env, None, 3, 2, 0, 0, 0, N.PRECISION_LSB1, 3, 0)
+    assert h and _exception(L) is None
+    try:
+        out = np.zeros_like(want)
+        keep = []
+        args = [_buf(x, keep) for x in (b.stream_slot, b.frame_begin, b.q, b.sf, b.cb, b.ics, b.ms_used, b.tns, None,
+                                         out)]
+        getattr(L, PFX + "nativeDecode")(env, None, h, b.n_frames, len(b.stream_slot), 2, *args, N.PCM_BIG_ENDIAN, None)
+        assert _exception(L) is None
+        assert (out == want).all()
+        d = np.abs(out.view(">i2").astype(np.int32) - exact.view(">i2").astype(np.int32))
+        assert d.max() == 1
+    finally:
+        getattr(L, PFX + "nativeDestroy")(env, None, h)
+    assert not getattr(L, PFX + "nativeCreate")(env, None, 3, 2, 0, 0, 0, 2, 3, 0)
+    cls, msg = _exception(L)
+    assert cls == AAC_EXC
