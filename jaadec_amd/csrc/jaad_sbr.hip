@@ -1768,10 +1768,8 @@ hipError_t launch_sbr(const SbrArgs& a, hipStream_t stream, const uint32_t* fix_
         const dim3 g((a.n_cf + kWavesPerBlock - 1) / kWavesPerBlock);
         // no smoothing and no fix pass: the analysis runs inside the HF kernel (phase 5), X_low never
         // goes through HBM (JAAD_SBR_FUSED=0: the separate kernels, for A/B)
-        static const bool fuse_ok = [] {
-            const char* e = std::getenv("JAAD_SBR_FUSED");
-            return !(e && e[0] == '0');
-        }();
+        const char* fz = std::getenv("JAAD_SBR_FUSED");  // (read per launch: tests switch it)
+        const bool fuse_ok = !(fz && fz[0] == '0');
         if (fuse_ok && !a.smoothing && n_fix_passes == 0 && !a.n_chains) {
             hipLaunchKernelGGL(sbr_hf_kernel<5>, g, blk, 0, stream, a);
         } else {

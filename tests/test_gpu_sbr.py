@@ -365,3 +365,28 @@ def test_upsample_only_call_and_state():
     # the upsampled frames repeat the core sample pairs (index 1 keeps core sample 1)
     L = g[1].view(">i2").reshape(-1, 2048, 2)[..., 0].astype(np.int32)
     assert np.array_equal(L[:, 2::2], L[:, 3::2])
+
+
+@pytest.mark.parametrize("cfgid", [4, 5])
+def test_fused_analysis_equals_the_separate_kernels(cfgid, monkeypatch):
+    """Round 6: a launch without smoothing or HF fix passes runs the QMF analysis inside the HF kernel
+    (sbr_hf_kernel<5>); JAAD_SBR_FUSED=0 keeps sbr_analysis_kernel + sbr_hf_kernel<0>.  Both give the
+    same PCM, and it is the restatement's, across a continuation call (rows 0..7 of a run's first
+    record from the slot state, of the others recomputed from the previous frame's samples)."""
+    p = N.synth_params(cfgid, n_streams=4, frames_per_stream=24)
+    b = N.synth_batch(p)
+    cfg = N.cfg_for(p)
+    n = int(b.stream_slot.max()) + 1
+    halves = b.split_frames(12)
+    outs = {}
+    for fz in ("1", "0"):
+        monkeypatch.setenv("JAAD_SBR_FUSED", fz)
+        with N.Context(cfg, n) as ctx:
+            outs[fz] = [ctx.decode(h, N.PCM_BIG_ENDIAN) for h in halves]
+    want = O.decode_batch(cfg, b, O.Streams(n), N.PCM_BIG_ENDIAN, threads=8)
+    fb = b.frame_begin
+    for k in range(2):
+        _assert_same(outs["1"][k], outs["0"][k], N.PCM_BIG_ENDIAN)
+    for r in range(len(fb) - 1):
+        assert np.array_equal(outs["1"][0][12 * r:12 * (r + 1)], want[fb[r]:fb[r] + 12])
+        assert np.array_equal(outs["1"][1][12 * r:12 * (r + 1)], want[fb[r] + 12:fb[r + 1]])
