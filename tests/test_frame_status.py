@@ -335,7 +335,7 @@ def test_jni_frame_status_and_state_export_import():
     b.frame_status = st
     cfg = N.cfg_for(p)
     want = oracle_pcm(cfg, b, N.PCM_BIG_ENDIAN)
-    h = getattr(L, PFX + "nativeCreate")(env, None, 3, 2, 0, 0, 0, 2, 0)
+    h = getattr(L, PFX + "nativeCreate")(env, None, 3, 2, 0, 0, 0, 0, 2, 0)
     assert h and _exception(L) is None
     decode = getattr(L, PFX + "nativeDecode")
     try:
