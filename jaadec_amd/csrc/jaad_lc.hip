@@ -1706,7 +1706,10 @@ __global__ __launch_bounds__(64 * waves_per_wg<kMode == 1 || kMode == 3>()) void
                 for (int m = 1; m < kW / 4; m++) mates_late[m - 1] = R[(wave + 4 * m) % kW];
             }
 #elif !defined(JAAD_ABL_NOPRIO)
-            {
+#ifndef JAAD_PRIO_EVERY  // (A/B builds: the priority recomputed every N frames)
+#define JAAD_PRIO_EVERY 1
+#endif
+            if ((it % JAAD_PRIO_EVERY) == 0) {
                 const uint32_t rem = (uint32_t)(my_n - it);
                 volatile uint32_t* R = S.rem;
                 R[wave] = rem;
@@ -1722,6 +1725,7 @@ __global__ __launch_bounds__(64 * waves_per_wg<kMode == 1 || kMode == 3>()) void
                 else __builtin_amdgcn_s_setprio(1);
             }
 #endif
+            STAMP(5);
 #ifdef JAAD_WAVETIME
             wt_frames++;
 #endif
@@ -1758,6 +1762,7 @@ __global__ __launch_bounds__(64 * waves_per_wg<kMode == 1 || kMode == 3>()) void
             }
             // ---------------- side info ----------------
             const Ics iL = ics_from_lanes(cur.side, 0, nswb_l, nswb_s);
+            STAMP(6);
             const Ics iR = stereo ? ics_from_lanes(cur.side, 4, nswb_l, nswb_s) : iL;
             const bool ms_on = stereo && (iL.flags & JAAD_ICS_COMMON_WINDOW) && (iL.flags & JAAD_ICS_MS_PRESENT);
             const bool is_on = stereo && (iR.flags & JAAD_ICS_HAS_IS);

@@ -37,8 +37,8 @@ ctx.decode_device(ptr, b, pcm.data_ptr(), pcm.numel(), 0, None)
 torch.cuda.synchronize()
 S = dbg.cpu().numpy().view(np.uint32).reshape(nw, 16).astype(np.int64)
 S = S[S.sum(1) > 0]
-names = ["top: loop head, side info", "band records", "prefetch issue (+PNS)", "M/S, I/S", "spectra to LDS",
-         "-", "-", "-", "IMDCT + OLA (both channels)", "drain next frame's loads",
+names = ["top: rest of side info (+ early IQ issue)", "band records", "prefetch issue (+PNS)", "M/S, I/S", "spectra to LDS",
+         "loop back + wave priority", "prefetched side info in (vmcnt)", "-", "IMDCT + OLA (both channels)", "drain next frame's loads",
          "PCM stage + stores", "chunk tail", "IQ R", "IQ L", "band record reads"]
 med = np.median(S, axis=0)
 tot = med[:15].sum()
