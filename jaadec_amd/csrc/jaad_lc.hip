@@ -950,6 +950,11 @@ __device__ __forceinline__ void imdct_short_pk(float* buf, const LdsTables& T, i
 // operations those of imdct_short_pk.  Only the mixed-window instantiations (kernel modes 5, 6,
 // chosen per launch when the batch holds EIGHT_SHORT frames) carry it: in one kernel body with
 // the long path it cost C2's long frames 1-3 % (round 5, profiles/round5_short_pair/).
+#if defined(JAAD_SHORT_R2)  // (A/B builds: the +-1 LSB short pair with the radix-2 stages)
+constexpr bool kShortR2 = true;
+#else
+constexpr bool kShortR2 = false;
+#endif
 template <bool F = false>
 __device__ __forceinline__ void imdct_short_pk2(float* bufL, float* bufR, const LdsTables& T, int u, float (&reL)[8],
                                                 float (&imL)[8], float (&reR)[8], float (&imR)[8])
@@ -989,11 +994,18 @@ __device__ __forceinline__ void imdct_short_pk2(float* bufL, float* bufR, const 
         c[1][s] = XR[xs(64 * w + b + 8 * s)];
     }
     wave_sync();
-    // stages i = 8, 16, 32 of the 64-point IFFT: roots[k*m], m = 4, 2, 1
-    fft_3stages_pk2<F>(c[0], c[1], [&](int j) {
-        const int idx = j == 0 ? 4 * b : (j < 3 ? 2 * (b + 8 * (j - 1)) : b + 8 * (j - 3));
-        return ld2(T.roots_s[idx]);
-    });
+    // stages i = 8, 16, 32 of the 64-point IFFT: roots[k*m], m = 4, 2, 1.  The +-1 LSB kernel runs
+    // them as the long transform's pass 2 (the same 64-point sub-transform structure, element
+    // b + 8 s in register s): radix-8 with the W64 twiddles of LdsTables::tw2f (FFT_TABLE_512
+    // entries, equal to FFT_TABLE_64's within the tables' rounding)
+    if constexpr (F && !kShortR2) {
+        fft_pass_r8<2>(c, [&](int j) { return ld2(T.tw2f[j][b]); });
+    } else {
+        fft_3stages_pk2<F>(c[0], c[1], [&](int j) {
+            const int idx = j == 0 ? 4 * b : (j < 3 ? 2 * (b + 8 * (j - 1)) : b + 8 * (j - 3));
+            return ld2(T.roots_s[idx]);
+        });
+    }
 #pragma unroll
     for (int s = 0; s < 8; s++) {
         const f2 tw = ld2(T.mdct_s[b + 8 * s]);
