@@ -320,7 +320,13 @@ void build_lds_tables(int sf_index, LdsTables* t, GlobalTables* gt)
         for (int u = 0; u < 64; u++) {
             t->mdct_post[s][u][0] = JAAD_MDCT_TABLE_2048[lane_pos_host(u) + 64 * s][0];
             t->mdct_post[s][u][1] = JAAD_MDCT_TABLE_2048[lane_pos_host(u) + 64 * s][1];
+            t->mdct_post_f[s][u][0] = t->mdct_post[s][u][0] * (1.0f / 32767.0f);
+            t->mdct_post_f[s][u][1] = t->mdct_post[s][u][1] * (1.0f / 32767.0f);
         }
+    for (int k = 0; k < 64; k++) {
+        t->mdct_s_f[k][0] = JAAD_MDCT_TABLE_128[k][0] * (1.0f / 32767.0f);
+        t->mdct_s_f[k][1] = JAAD_MDCT_TABLE_128[k][1] * (1.0f / 32767.0f);
+    }
     // 512-point IFFT twiddles roots[k*m] (FFT.java:116-120, inverse column 1) pre-arranged per
     // register pass: pass 1 (i = 4, m = 64); pass 2 by b = position mod 8: slot 0 -> stage 8
     // (m = 32, k = b), slots 1,2 -> stage 16 (m = 16, k = b + 8e), slots 3..6 -> stage 32 (m = 8,

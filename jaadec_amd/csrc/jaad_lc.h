@@ -48,6 +48,11 @@ struct alignas(16) LdsTables {
     // W64^(bitrev3(r) * (lane >> 3)), pass 3 W512^(bitrev3(r) * lane_pos(lane)) (FFT_TABLE_512 entries)
     float tw2f[7][8][2];
     float tw3f[7][64][2];
+    // +-1 LSB kernel: the post-twiddles (mdct_post, and mdct_s as the short transform's
+    // post-twiddle) times 1/32767, so that the IMDCT output, the overlap in registers and the OLA
+    // sum are in PCM full-scale units: v_cvt_pknorm_i16_f32 takes them without a multiply
+    float mdct_post_f[8][64][2];
+    float mdct_s_f[64][2];
 };
 
 // Tables only the slow paths (PNS, spec TNS) need; read from global memory.

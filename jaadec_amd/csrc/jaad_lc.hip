@@ -689,6 +689,16 @@ __device__ __forceinline__ void xch_bit(f2 (&c)[8], int u)
 // its bits 0,1,2).  The first exchange trades register bits 0,1,2 for lane bits 5,4,3 (e bits
 // 3,4,5 into registers; lane bits 3-5 then hold e bits 0-2), the second register bits 0,1,2 for
 // lane bits 2,1,0 (e bits 6,7,8 into registers), leaving lane u with positions lane_pos(u) + 64 s.
+// +-1 LSB kernel: IMDCT output in PCM full-scale units (post-twiddles x 1/32767, LdsTables::
+// mdct_post_f / mdct_s_f); the overlap state is converted where it enters and leaves the registers,
+// the float outputs where they are stored (JAAD_NO_SCALED: A/B builds with the unscaled tables)
+#if defined(JAAD_NO_SCALED)
+constexpr bool kScaledOut = false;
+#else
+constexpr bool kScaledOut = true;
+#endif
+constexpr float kPcmScale = 32767.0f, kPcmUnit = 1.0f / 32767.0f;
+
 template <int N, bool F = false>
 __device__ __forceinline__ void imdct_long_pk(float* const (&bufs)[N], const LdsTables& T, int u, f2 (&c)[N][8])
 {
@@ -777,14 +787,14 @@ __device__ __forceinline__ void imdct_long_pk(float* const (&bufs)[N], const Lds
     if constexpr (F && N == 2) {
 #pragma unroll
         for (int s = 0; s < 8; s++) {
-            const f2 w = ld2(T.mdct_post[s][u]);
+            const f2 w = ld2(kScaledOut ? T.mdct_post_f[s][u] : T.mdct_post[s][u]);
             cmul_fma2(c[0][s], w, c[1][s], w);
         }
     } else {
 #pragma unroll
     for (int s = 0; s < 8; s++)
 #pragma unroll
-        for (int n = 0; n < N; n++) c[n][s] = cmul_t<F>(c[n][s], ld2(T.mdct_post[s][u]));
+        for (int n = 0; n < N; n++) c[n][s] = cmul_t<F>(c[n][s], ld2(F && kScaledOut ? T.mdct_post_f[s][u] : T.mdct_post[s][u]));
     }
 }
 
@@ -938,7 +948,7 @@ __device__ __forceinline__ void imdct_short_pk(float* buf, const LdsTables& T, i
 #pragma unroll
     for (int s = 0; s < 8; s++) {
         // MDCT.java:48-53: re = t0*c - t1*sn, im = t1*c + t0*sn = cmul((t0, t1), (c, sn))
-        const f2 z = cmul_t<F>(c[s], ld2(T.mdct_s[b + 8 * s]));
+        const f2 z = cmul_t<F>(c[s], ld2(F && kScaledOut ? T.mdct_s_f[b + 8 * s] : T.mdct_s[b + 8 * s]));
         re[s] = z.x;
         im[s] = z.y;
     }
@@ -1008,7 +1018,7 @@ __device__ __forceinline__ void imdct_short_pk2(float* bufL, float* bufR, const 
     }
 #pragma unroll
     for (int s = 0; s < 8; s++) {
-        const f2 tw = ld2(T.mdct_s[b + 8 * s]);
+        const f2 tw = ld2(F && kScaledOut ? T.mdct_s_f[b + 8 * s] : T.mdct_s[b + 8 * s]);
         const f2 z = cmul_t<F>(c[0][s], tw), y = cmul_t<F>(c[1][s], tw);
         reL[s] = z.x;
         imL[s] = z.y;
@@ -1251,14 +1261,15 @@ __device__ __forceinline__ uint32_t round_pk16(float a, float b)
     return w;
 }
 
-// +-1 LSB kernel: two samples to int16 in one conversion after one packed multiply --
-// v_cvt_pknorm_i16_f32 rounds x * 32767 to nearest and saturates to [-32767, 32767], so the samples
-// are first scaled by 1/32767 (a product rounded once, then re-scaled inside the conversion: the
+// +-1 LSB kernel: two samples to int16 in one conversion -- v_cvt_pknorm_i16_f32 rounds x * 32767 to
+// nearest and saturates to [-32767, 32767], and the kernel's samples are already in those units
+// (kScaledOut: the post-twiddles carry the 1/32767; JAAD_NO_SCALED builds multiply here).  The
 // integer can differ from Math.round's by one at a tie, and -32768 comes out as -32767; both within
-// the mode's bar).  2 instructions per sample pair instead of 3.
+// the mode's bar.  1 instruction per sample pair instead of 3.
 __device__ __forceinline__ uint32_t round_pk16_lsb1(float a, float b)
 {
-    const f2 x = f2{a, b} * f2{1.0f / 32767.0f, 1.0f / 32767.0f};
+    f2 x = f2{a, b};
+    if constexpr (!kScaledOut) x = x * f2{kPcmUnit, kPcmUnit};
     uint32_t w;
     asm("v_cvt_pknorm_i16_f32 %0, %1, %2" : "=v"(w) : "v"(x.x), "v"(x.y));
     return w;
@@ -1686,6 +1697,10 @@ __global__ __launch_bounds__(64 * waves_per_wg<kMode == 1 || kMode == 3>()) void
                 for (int o = 0; o < 16; o++) {
                     ovL[o] = st[long_pos(u, o)];
                     ovR[o] = st[1024 + long_pos(u, o)];
+                    if constexpr (kFast && kScaledOut) {  // (the state is in reference units)
+                        ovL[o] *= kPcmUnit;
+                        ovR[o] *= kPcmUnit;
+                    }
                 }
             } else {
 #pragma unroll
@@ -2039,8 +2054,8 @@ __global__ __launch_bounds__(64 * waves_per_wg<kMode == 1 || kMode == 3>()) void
                 if constexpr (planar) {
 #pragma unroll
                     for (int o = 0; o < 16; o++) {
-                        W.buf[long_pos(u2, o)] = outL[o];
-                        if (stereo) W.rsp[long_pos(u2, o)] = outR[o];
+                        W.buf[long_pos(u2, o)] = kFast && kScaledOut ? outL[o] * kPcmScale : outL[o];
+                        if (stereo) W.rsp[long_pos(u2, o)] = kFast && kScaledOut ? outR[o] * kPcmScale : outR[o];
                     }
                     wave_sync();
 #pragma unroll
@@ -2062,7 +2077,9 @@ __global__ __launch_bounds__(64 * waves_per_wg<kMode == 1 || kMode == 3>()) void
                     const int drop8 = emit ? 0 : 8192;
 #pragma unroll
                     for (int o = 0; o < 16; o++) {
-                        const v2u w = {__float_as_uint(outL[o]), __float_as_uint(stereo ? outR[o] : outL[o])};
+                        const float sl = kFast && kScaledOut ? outL[o] * kPcmScale : outL[o];
+                        const float sr = stereo ? (kFast && kScaledOut ? outR[o] * kPcmScale : outR[o]) : sl;
+                        const v2u w = {__float_as_uint(sl), __float_as_uint(sr)};
                         __builtin_amdgcn_raw_buffer_store_b64(w, dst, 8 * long_pos(u2, o) + drop8, 0, 0);
                     }
                 } else {
@@ -2085,6 +2102,9 @@ __global__ __launch_bounds__(64 * waves_per_wg<kMode == 1 || kMode == 3>()) void
                         if constexpr (kPkNorm) {
                             pl = round_pk16_lsb1(outL[2 * m], outL[2 * m + 1]);
                             pr = stereo ? round_pk16_lsb1(outR[2 * m], outR[2 * m + 1]) : pl;
+                        } else if constexpr (kFast && kScaledOut) {
+                            pl = round_pk16(outL[2 * m] * kPcmScale, outL[2 * m + 1] * kPcmScale);
+                            pr = stereo ? round_pk16(outR[2 * m] * kPcmScale, outR[2 * m + 1] * kPcmScale) : pl;
                         } else {
                             pl = round_pk16(outL[2 * m], outL[2 * m + 1]);
                             pr = stereo ? round_pk16(outR[2 * m], outR[2 * m + 1]) : pl;
@@ -2107,10 +2127,11 @@ __global__ __launch_bounds__(64 * waves_per_wg<kMode == 1 || kMode == 3>()) void
         if (cd.info & kChunkStoreState) {
             const int u = lane_id();
             float* st = A.state_out + (size_t)cd.slot * 2048;
+            constexpr float sc = kFast && kScaledOut ? kPcmScale : 1.0f;
 #pragma unroll
             for (int o = 0; o < 16; o++) {
-                st[long_pos(u, o)] = ovL[o];
-                if (stereo) st[1024 + long_pos(u, o)] = ovR[o];
+                st[long_pos(u, o)] = kFast && kScaledOut ? ovL[o] * sc : ovL[o];
+                if (stereo) st[1024 + long_pos(u, o)] = kFast && kScaledOut ? ovR[o] * sc : ovR[o];
             }
         }
     }
