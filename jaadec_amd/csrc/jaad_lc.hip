@@ -989,6 +989,17 @@ __device__ __forceinline__ void imdct_short_pk2(float* bufL, float* bufR, const 
 #pragma unroll
         for (int k = 0; k < 4; k++) bfly_pk2(c[0][BR3[k]], c[0][BR3[k + 4]], c[1][BR3[k]], c[1][BR3[k + 4]], ld2(T.roots_s[8 * k]));
     }
+    // transpose within each window's 8 lanes: register p holds element e bits 0-2 = bitrev3(p), lane
+    // bits 0-2 hold e bits 5,4,3; afterwards register s holds e = b + 8 s.  Three register-bit /
+    // lane-bit exchanges (the long transform's second exchange: register bits 0,1,2 <-> lane bits
+    // 2,1,0) do it in registers, without the LDS round trip (JAAD_SHORT_LDS: A/B builds with it)
+#if !defined(JAAD_SHORT_LDS)
+    xch_bit_pair<0, 2>(c[0], c[1]);
+    xch_bit_pair<1, 1>(c[0], c[1]);
+    xch_bit_pair<2, 0>(c[0], c[1]);
+    (void)bufL;
+    (void)bufR;
+#else
     f2* XL = reinterpret_cast<f2*>(bufL);
     f2* XR = reinterpret_cast<f2*>(bufR);
     const int t = (int)(__builtin_bitreverse32((uint32_t)b) >> 29);
@@ -1004,6 +1015,7 @@ __device__ __forceinline__ void imdct_short_pk2(float* bufL, float* bufR, const 
         c[1][s] = XR[xs(64 * w + b + 8 * s)];
     }
     wave_sync();
+#endif
     // stages i = 8, 16, 32 of the 64-point IFFT: roots[k*m], m = 4, 2, 1.  The +-1 LSB kernel runs
     // them as the long transform's pass 2 (the same 64-point sub-transform structure, element
     // b + 8 s in register s): radix-8 with the W64 twiddles of LdsTables::tw2f (FFT_TABLE_512
