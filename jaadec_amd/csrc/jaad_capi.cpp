@@ -323,6 +323,12 @@ void build_lds_tables(int sf_index, LdsTables* t, GlobalTables* gt)
             t->mdct_post_f[s][u][0] = t->mdct_post[s][u][0] * (1.0f / 32767.0f);
             t->mdct_post_f[s][u][1] = t->mdct_post[s][u][1] * (1.0f / 32767.0f);
         }
+    for (int sh = 0; sh < 2; sh++)
+        for (int o = 0; o < 16; o++)
+            for (int u = 0; u < 64; u++) {
+                const int P = long_pos_host(u, o);
+                t->win_ss[sh][o >> 1][u][o & 1] = P < 448 ? 0.0f : P < 576 ? (sh ? JAAD_KBD_128 : JAAD_SINE_128)[P - 448] : 1.0f;
+            }
     for (int k = 0; k < 64; k++) {
         t->mdct_s_f[k][0] = JAAD_MDCT_TABLE_128[k][0] * (1.0f / 32767.0f);
         t->mdct_s_f[k][1] = JAAD_MDCT_TABLE_128[k][1] * (1.0f / 32767.0f);

@@ -53,6 +53,10 @@ struct alignas(16) LdsTables {
     // sum are in PCM full-scale units: v_cvt_pknorm_i16_f32 takes them without a multiply
     float mdct_post_f[8][64][2];
     float mdct_s_f[64][2];
+    // +-1 LSB kernel: LONG_STOP's rising window as a long window in win_pair's lane layout, W[P] = 0
+    // (P < 448), SW[P - 448] (P < 576), 1: LONG_START's falling one is W[1023 - P] (FilterBank.java:
+    // 61-70, 90-100), so both run the ONLY_LONG overlap-add with this table for one half
+    float win_ss[2][8][64][2];
 };
 
 // Tables only the slow paths (PNS, spec TNS) need; read from global memory.

@@ -854,13 +854,16 @@ __device__ __forceinline__ void ola_long_t(const LdsTables& T, const FrameCtx& f
 // ONLY_LONG window + overlap-add in packed form (slot pair (2s, 2s+1) of ola_long_t):
 //   out[o] = ov[o] + f_o * W[P_o],  new ov[o] = g * W[1023 - P_o]
 // with (f_0, f_1, g) = (-re, re, -im) for s < 4 and (im, -im, re) for s >= 4
+// (Wp / Wc: the rising and falling windows in win_pair's layout; the +-1 LSB kernel passes
+// LdsTables::win_ss for LONG_STOP's rising and LONG_START's falling half)
 template <bool F = false>
 __device__ __forceinline__ void ola_only_long_pk(const LdsTables& T, const FrameCtx& fc, const f2 (&c)[8],
-                                                 float (&ov)[16], float (&out)[16])
+                                                 float (&ov)[16], float (&out)[16], const f2* Wp = nullptr,
+                                                 const f2* Wc = nullptr)
 {
     const int u = lane_id();
-    const f2* Wp = reinterpret_cast<const f2*>(&T.win_pair[fc.shape_prev][0][0][0]);
-    const f2* Wc = reinterpret_cast<const f2*>(&T.win_pair[fc.shape][0][0][0]);
+    if (!Wp) Wp = reinterpret_cast<const f2*>(&T.win_pair[fc.shape_prev][0][0][0]);
+    if (!Wc) Wc = reinterpret_cast<const f2*>(&T.win_pair[fc.shape][0][0][0]);
 #pragma unroll
     for (int s = 0; s < 8; s++) {
         const f2 wp = Wp[64 * s + u], wc = Wc[64 * s + u];
@@ -898,6 +901,15 @@ __device__ __forceinline__ void ola_long_pk(const LdsTables& T, const FrameCtx& 
         ola_only_long_pk<F>(T, fc, c, ov, out);
         return;
     }
+#if !defined(JAAD_NO_WIN_SS)  // (A/B builds: the +-1 LSB kernel with ola_long_t for START / STOP)
+    if constexpr (F) {  // one half through win_ss (w * 1 and w * 0 instead of copies and zeros)
+        const f2* Wss = reinterpret_cast<const f2*>(
+            &T.win_ss[fc.seq == JAAD_LONG_START_SEQUENCE ? fc.shape : fc.shape_prev][0][0][0]);
+        if (fc.seq == JAAD_LONG_START_SEQUENCE) ola_only_long_pk<F>(T, fc, c, ov, out, nullptr, Wss);
+        else ola_only_long_pk<F>(T, fc, c, ov, out, Wss, nullptr);
+        return;
+    }
+#endif
     float re[8], im[8];
 #pragma unroll
     for (int s = 0; s < 8; s++) {
