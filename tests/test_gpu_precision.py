@@ -150,3 +150,27 @@ def test_mixed_window_instantiation_through_the_device_entry(precision):
         assert mx <= (0 if precision == N.PRECISION_EXACT else 1)
     if precision == N.PRECISION_EXACT:
         assert (outs[0] == outs[1]).all()
+
+
+def test_state_blob_crosses_precisions():
+    """The LSB1 kernel keeps its overlap in PCM full-scale units in registers (kScaledOut) and
+    converts it where the slot state is loaded and stored: a stream decoded by an exact context,
+    exported, and continued by an LSB1 context (and the reverse) stays within 1 LSB of the
+    restatement over the whole stream -- the blob is in reference units either way."""
+    p = N.synth_params(2, n_streams=2, frames_per_stream=40)
+    b = N.synth_batch(p)
+    first, second = b.split_frames(17)
+    want = O.decode_batch(N.make_cfg(), b, O.Streams(2), N.PCM_BIG_ENDIAN)
+    fb = b.frame_begin
+    for a, z in ((N.PRECISION_EXACT, N.PRECISION_LSB1), (N.PRECISION_LSB1, N.PRECISION_EXACT)):
+        with N.Context(N.make_cfg(precision=a), 2) as c1:
+            g1 = c1.decode(first)
+            blobs = [c1.state_export(s) for s in range(2)]
+        with N.Context(N.make_cfg(precision=z), 2) as c2:
+            for s in range(2):
+                c2.state_import(s, blobs[s])
+            g2 = c2.decode(second)
+        for r in range(2):
+            mx1, _ = _lsb_report(g1[17 * r:17 * (r + 1)], want[fb[r]:fb[r] + 17])
+            mx2, _ = _lsb_report(g2[23 * r:23 * (r + 1)], want[fb[r] + 17:fb[r + 1]])
+            assert mx1 <= 1 and mx2 <= 1, (a, z, r, mx1, mx2)
