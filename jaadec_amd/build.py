@@ -47,7 +47,10 @@ def _deps(*globs: str) -> list[Path]:
 
 
 # per-source extra flags (the LC kernel: see DESIGN.md §4a, scheduler strategy)
-GPU_FILE_FLAGS: dict[str, list[str]] = {}
+GPU_FILE_FLAGS: dict[str, list[str]] = {
+    # the +-1 LSB LC kernels (modes 4, 6): LLVM's iterative-ILP machine scheduler (-2.2 % on C2, round 6)
+    "jaad_lc_fast.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"],
+}
 # kernel sources whose device assembly goes through tools/vop3_rewrite.py (VCC-implicit VOP2 /
 # VOPC forms re-encoded as VOP3: DESIGN.md §4a, round 4) before it is assembled
 VOP3_REWRITE: dict[str, tuple[str, ...]] = {}
@@ -79,7 +82,7 @@ def build_gpu(force: bool = False, out: Path | None = None, defines: list[str] |
     the re-encoding pipeline), then linked."""
     out = out or LIB
     rewrite = VOP3_REWRITE if vop3 is None else vop3
-    srcs = [CSRC / "jaad_lc.hip", CSRC / "jaad_sbr.hip", CSRC / "jaad_ps.hip", CSRC / "jaad_capi.cpp", CSRC / "jaad_sbr_host.cpp",
+    srcs = [CSRC / "jaad_lc.hip", CSRC / "jaad_lc_fast.hip", CSRC / "jaad_sbr.hip", CSRC / "jaad_ps.hip", CSRC / "jaad_capi.cpp", CSRC / "jaad_sbr_host.cpp",
             CSRC / "jaad_parse.cpp", CSRC / "jaad_parse_sbr.cpp", CSRC / "jaad_mp4.cpp"]
     deps = srcs + _deps("jaadec_amd/csrc/*.h", "jaadec_amd/csrc/tables/*.inc", "include/*.h") + [ROOT / "tools" / "vop3_rewrite.py"]
     if force or defines or extra or vop3 is not None or _stale(out, deps):

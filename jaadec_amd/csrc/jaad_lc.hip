@@ -2193,20 +2193,21 @@ static void launch_lc_mode(const KernelArgs& a, hipStream_t stream)
 #undef JAAD_LAUNCH
 }
 
+// The +-1 LSB instantiations (modes 4, 6) live in their own translation unit, jaad_lc_fast.hip (this
+// file with JAAD_LC_FAST_TU), compiled with LLVM's iterative-ILP machine scheduler: -2.2 % on C2,
+// -1.5 % on C3 (profiles/round6_ab/sched_itilp_c*.txt), while on the exact modes it spills
+// (mode 0: 4 VGPRs, modes 1/3: 40+), so they keep the default scheduler.
+hipError_t launch_lc_fast(const KernelArgs& a, hipStream_t stream);
+
+#ifndef JAAD_LC_FAST_TU
 template <bool kStereo>
 static hipError_t launch_lc_ch(const KernelArgs& a, hipStream_t stream, bool tns_spec)
 {
     if (a.cce_off && tns_spec) launch_lc_mode<3, kStereo>(a, stream);  // coupling around the spec TNS filters
     else if (a.cce_off) launch_lc_mode<2, kStereo>(a, stream);
     else if (tns_spec) launch_lc_mode<1, kStereo>(a, stream);
-    else if (a.precision == JAAD_PRECISION_LSB1) {
-        if constexpr (kStereo)  // (the lockstep short path pairs a CPE's channels: stereo only)
-            if (a.short_pair) {
-                launch_lc_mode<6, kStereo>(a, stream);
-                return hipGetLastError();
-            }
-        launch_lc_mode<4, kStereo>(a, stream);
-    } else {
+    else if (a.precision == JAAD_PRECISION_LSB1) return launch_lc_fast(a, stream);
+    else {
         if constexpr (kStereo)
             if (a.short_pair) {
                 launch_lc_mode<5, kStereo>(a, stream);
@@ -2416,5 +2417,18 @@ int lc_resident_waves_per_cu(bool tns_spec)
     if (e != hipSuccess) return 0;
     return blocks * (tns_spec ? waves_per_wg<true>() : waves_per_wg<false>());
 }
+#else  // JAAD_LC_FAST_TU
+hipError_t launch_lc_fast(const KernelArgs& a, hipStream_t stream)
+{
+    // (the lockstep short path pairs a CPE's channels: stereo only)
+    if (a.nch == 2) {
+        if (a.short_pair) launch_lc_mode<6, true>(a, stream);
+        else launch_lc_mode<4, true>(a, stream);
+    } else {
+        launch_lc_mode<4, false>(a, stream);
+    }
+    return hipGetLastError();
+}
+#endif
 
 }  // namespace jaad
